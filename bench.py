@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Benchmark: scan-result dedup + new-record diff (BASELINE.json configs[1], "C2"):
+10M synthetic subdomain lines per GPU, sort -u + diff against the prior scan (90 % of the
+unique set), inputs resident in HBM before the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+       (records hash-partitioned over the GPUs with one RCCL all-to-all per step; weak
+       scaling: every rank brings its own 10M lines drawn from one global universe)
+
+Prints ONE JSON line (rank 0). `roofline` is the dominant kernel's algorithmic bytes ÷
+its average launch time (HIP events on the launch stream, live in the timed region);
+`cpu_baseline` is the oracle's Python restatement of the reference semantics
+(sorted(set()) + set difference) timed on this host, single thread, on rank 0 at N=1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0      # measured float4 copy (same guide)
+METRIC = "scan records/sec + GB/s (vs HBM roofline) for match+dedup+diff, 1 and 8 GPUs"
+
+
+def kernel_bytes(name, step_info):
+    """Algorithmic bytes moved by ALL launches of `name` in one step."""
+    R, n, Rp, npb = step_info["R"], step_info["n"], step_info["Rp"], step_info["n_prior"]
+    U, ub, F, fb = step_info["U"], step_info["ub"], step_info["F"], step_info["fb"]
+    if name == "rs_pass":
+        return 24.0 * R * step_info["passes"]          # 12 B read + 12 B written per pair
+    if name == "lines":
+        return float(n + 16 * R + npb + 16 * Rp)       # text read + (start,end,key) written
+    if name == "copy_records":
+        return float(2 * (ub + fb) + 12 * (U + F))     # bytes read+written + rec id/offset
+    if name == "diff_mark":
+        return float(12 * U + 8 * Rp + 8 * Rp)         # keys + ids read, prior keys/spans
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--lines", type=int, default=10_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=10_000_000)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    import swarm_amd
+    from swarm_amd import corpus
+
+    n_lines = args.lines
+    cur_np, ids = corpus.subdomains(n_lines, seed=1234 + rank, universe=n_lines * world)
+    cur = torch.from_numpy(cur_np).to(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ctx = swarm_amd.Context(local, stream)
+
+    if world == 1:
+        prior_np = corpus.prior_of(ids)
+        prior = torch.from_numpy(prior_np).to(dev)
+    else:
+        from swarm_amd import distributed as D
+        u = np.unique(ids)
+        cand = corpus._flatten(*corpus.render_names(u[(u % np.uint64(10)) != 0]))
+        prior = D.build_prior_partition(ctx, torch.from_numpy(cand).to(dev))
+        prior_np = None
+    torch.cuda.synchronize()
+
+    def step():
+        if world == 1:
+            return ctx.dedup_diff(cur.data_ptr(), cur.numel(), prior.data_ptr(), prior.numel()), cur.numel()
+        from swarm_amd import distributed as D
+        r, recv = D.dedup_diff_step(ctx, cur, prior)
+        return r, recv.numel()
+
+    for _ in range(args.warmup):
+        r, nrecv = step()
+    torch.cuda.synchronize()
+
+    ctx.reset_stats()
+    ctx.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r, nrecv = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.profile(False)
+    elapsed = t1 - t0
+    stats = ctx.kernel_stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_records = n_lines * world * args.steps
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = total_records / elapsed
+
+    # algorithmic bytes of the whole step (this rank): cur + prior + outputs
+    step_bytes = cur.numel() + prior.numel() + r.uniq_bytes + r.fresh_bytes
+    info = {"R": int(r.in_records), "n": int(nrecv), "Rp": int(r.prior_records), "n_prior": int(prior.numel()),
+            "U": int(r.uniq_records), "ub": int(r.uniq_bytes), "F": int(r.fresh_records), "fb": int(r.fresh_bytes)}
+    launches_rs = stats.get("rs_pass", (0, 0.0))[0]
+    info["passes"] = launches_rs / max(args.steps, 1)
+
+    # dominant kernel roofline
+    dom = max(stats.items(), key=lambda kv: kv[1][1]) if stats else None
+    roofline = None
+    if dom:
+        name, (launches, ms) = dom
+        per_step_bytes = kernel_bytes(name, info)
+        if per_step_bytes is not None and launches:
+            per_launch = per_step_bytes * args.steps / launches
+            avg_ms = ms / launches
+            ach = per_launch / (avg_ms * 1e-3) / 1e9
+            roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "bytes_per_launch": int(per_launch), "avg_launch_us": round(avg_ms * 1e3, 2)}
+    kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3)} for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])}
+    gpu_ms_sum = sum(v[1] for v in stats.values()) / args.steps
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import semantics as S  # CPU baseline leg only
+        m = min(args.cpu_sample, n_lines)
+        if m < n_lines:
+            cut = int(np.flatnonzero(cur_np == 10)[m - 1]) + 1
+            cbytes = cur_np[:cut].tobytes()
+        else:
+            cbytes = cur_np.tobytes()
+        pbytes = prior_np.tobytes()
+        tc = time.perf_counter()
+        eu, ef = S.dedup_diff(cbytes, pbytes)
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(m / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d C2 lines + full prior (%d B); oracle sorted(set())+set difference, 1 thread, %.2f s"
+                         % (m, len(pbytes), tc),
+               "host_cpus": os.cpu_count()}
+        if m == n_lines:
+            u_gpu = ctx.to_bytes(r.uniq, r.uniq_bytes)
+            f_gpu = ctx.to_bytes(r.fresh, r.fresh_bytes)
+            cpu["gpu_output_bit_exact"] = (u_gpu == eu and f_gpu == ef)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "records/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded subdomain corpus, SURVEY.md §8(d) C2)",
+            "config": {"workload": "C2: %dM-line subdomain merge + sort -u dedup + new-record diff per GPU"
+                                   % (n_lines // 1_000_000),
+                       "lines_per_gpu": n_lines, "bytes_per_gpu": int(cur.numel()),
+                       "prior_bytes": int(prior.numel()),
+                       "parallelism": "hash-partition all-to-all x%d" % world if world > 1 else "single GPU"},
+            "gbps": round(step_bytes * world * args.steps / elapsed / 1e9, 2),
+            "hbm_frac_step": round(step_bytes * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4),
+            "records": {"in": info["R"], "unique": info["U"], "new": info["F"], "prior": info["Rp"]},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "gpu_kernel_ms_per_step": round(gpu_ms_sum, 4),
+            "kernels": kernels,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+/*
+ * swarmgpu.h — C-ABI of libswarmgpu.so, the MI355X (gfx950) scan-result hot path.
+ *
+ * The reference (Jec00/swarm) has no native code and no FFI: its hot path is Python
+ * (server/server.py, worker/worker.py) around third-party scanners. Each entry point
+ * below replaces one reference step; the citation says which. Python binds these with
+ * ctypes (swarm_amd/_abi.py); INTEGRATION.md shows the binding a maintainer would add to
+ * the reference's worker.py / server.py.
+ *
+ * Conventions
+ *   - Every function returns an int status: SG_OK (0) or an SG_E_* code. No exception
+ *     crosses the ABI. sg_last_error() returns a thread-local message for the last error.
+ *   - Host-buffer entry points (no `_dev` suffix) take host pointers owned by the caller;
+ *     the library copies to HBM, computes, and copies back. If `cap` is too small they
+ *     return SG_E_CAP and store the required size in the *_n out-parameter.
+ *   - Device entry points (`sg_dev_*`) take device pointers on the context's device and
+ *     enqueue on the context's stream; their outputs are device buffers owned by the
+ *     context, valid until the next call on that context.
+ *   - Re-entrant: the host API draws a context from a mutex-guarded per-device pool, so
+ *     concurrent Flask request threads (flask/app.py threaded=True) may call it. A
+ *     single sg_ctx must not be used by two threads at once.
+ *   - Record = maximal run of non-'\n' bytes; empty records are dropped; '\r' is kept
+ *     (SURVEY.md §8(a) A3). Ordering is bytewise (memcmp, shorter-prefix first), i.e.
+ *     Python bytes order == LC_ALL=C sort.
+ *   - Buffers are < 4 GiB per call (32-bit record offsets); larger inputs are split by
+ *     the caller or sharded over GPUs (sg_dev_partition).
+ */
+#ifndef SWARMGPU_H
+#define SWARMGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_OK 0
+#define SG_E_INVAL 1        /* bad argument */
+#define SG_E_CAP 2          /* output capacity too small; required size returned */
+#define SG_E_HIP 3          /* HIP runtime error */
+#define SG_E_NOMEM 4        /* device or host allocation failed */
+#define SG_E_TOO_LARGE 5    /* buffer >= 4 GiB */
+#define SG_E_UNSUPPORTED 6  /* regex construct outside the supported subset */
+#define SG_E_STATES 7       /* automaton exceeds its state budget */
+#define SG_E_NODEV 8        /* no HIP device */
+
+/* matcher flags */
+#define SG_NOCASE 1u        /* ASCII case-insensitive (nuclei `case-insensitive: true`, grep -i) */
+
+const char *sg_last_error(void);
+int sg_version(void);
+int sg_device_count(int *n);
+
+/* ------------------------------------------------------------------ contexts */
+typedef struct sg_ctx sg_ctx;
+/* stream: a hipStream_t on `device` (e.g. torch.cuda.current_stream().cuda_stream), or
+ * NULL for a context-owned non-blocking stream. */
+int sg_ctx_create(int device, void *stream, sg_ctx **out);
+int sg_ctx_destroy(sg_ctx *ctx);
+int sg_ctx_sync(sg_ctx *ctx);
+/* Per-kernel HIP-event timing, recorded on the context's stream while enabled. */
+int sg_ctx_profile(sg_ctx *ctx, int enable);
+/* Kernel stats by index: name (static string), launches, total device ms. Returns
+ * SG_E_INVAL past the last index. */
+int sg_ctx_kernel_stat(sg_ctx *ctx, int idx, const char **name, uint64_t *launches, double *total_ms);
+int sg_ctx_reset_stats(sg_ctx *ctx);
+/* Synchronous copy on the context's stream (any direction: hipMemcpyDefault). */
+int sg_ctx_memcpy(sg_ctx *ctx, void *dst, const void *src, size_t n);
+
+/* ------------------------------------------------------------------ A3: parse
+ * Replaces: nothing in the reference parses module output; it is uploaded verbatim at
+ * worker/worker.py:96-98. Output: spans[2k] = start, spans[2k+1] = end (exclusive) of the
+ * k-th non-empty record. cap counts records. */
+int sg_lines(const uint8_t *buf, size_t n, uint64_t *spans, size_t cap, size_t *n_rec);
+
+/* ------------------------------------------------------------------ A5+A7: merge + dedup
+ * sort -u of the concatenation of `k` chunk bodies taken in the given order (the caller
+ * supplies server/server.py:403-404's key order; concatenation without separator is
+ * :407-410). Output is the unique records in byte order, each '\n'-terminated.
+ * Replaces the planned dedup of README.md:11 (semantics: BASELINE.json north_star). */
+int sg_dedup(const uint8_t *buf, size_t n, uint8_t *out, size_t cap, size_t *out_n);
+int sg_dedup_chunks(const uint8_t *const *chunks, const size_t *lens, size_t k,
+                    uint8_t *out, size_t cap, size_t *out_n);
+
+/* ------------------------------------------------------------------ A8: new-record diff
+ * sorted(set(cur) - set(prior)) == LC_ALL=C comm -13 (README.md:11 "alerting ... new
+ * subdomains"; prior scan resolved from asm.scans, server/server.py:277-294). `prior` is
+ * normally the previous scan's sort -u output; unsorted/duplicated priors are accepted
+ * (they are sorted on the GPU first). */
+int sg_diff(const uint8_t *cur, size_t n_cur, const uint8_t *prior, size_t n_prior,
+            uint8_t *out, size_t cap, size_t *out_n);
+/* Both at once (the scan-completion hook, server/server.py:274-294). */
+int sg_dedup_diff(const uint8_t *cur, size_t n_cur, const uint8_t *prior, size_t n_prior,
+                  uint8_t *uniq, size_t uniq_cap, size_t *uniq_n,
+                  uint8_t *fresh, size_t fresh_cap, size_t *fresh_n);
+
+/* ------------------------------------------------------------------ device-resident path */
+typedef struct sg_dev_result {
+    const uint8_t *uniq;      /* device: sort -u output */
+    uint64_t uniq_bytes;
+    uint64_t uniq_records;
+    const uint8_t *fresh;     /* device: new records (cur - prior), sorted */
+    uint64_t fresh_bytes;
+    uint64_t fresh_records;
+    uint64_t in_records;      /* non-empty records in cur */
+    uint64_t prior_records;   /* non-empty records in prior */
+} sg_dev_result;
+/* d_prior may be NULL with n_prior 0 (then fresh == uniq). */
+int sg_dev_dedup_diff(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur,
+                      const uint8_t *d_prior, size_t n_prior, sg_dev_result *res);
+
+/* Multi-GPU: route every record of d_buf to partition
+ * part(hash64(record), n_parts), n_parts <= 256. Writes '\n'-terminated records grouped by
+ * partition (input order kept inside a partition) into the caller's device buffer d_out
+ * (capacity out_cap >= n + 1) and the per-partition byte and record counts (host arrays
+ * of n_parts), ready for an all-to-all. */
+int sg_dev_partition(sg_ctx *ctx, const uint8_t *d_buf, size_t n, uint32_t n_parts,
+                     uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records);
+/* The record hash used by sg_dev_partition, on one host record (for tests/oracles). */
+uint64_t sg_hash64(const uint8_t *rec, size_t len);
+
+/* ------------------------------------------------------------------ A4: signature matching
+ * Patterns are concatenated in `pats`; pattern i is pats[pat_offs[i] .. pat_offs[i+1]).
+ * Match output: (record index, signature id) for every signature that occurs in a record,
+ * sorted by record then signature; record indices follow A3 order. Replaces the matcher
+ * arithmetic of the absent nuclei/httpx/nmap binaries (worker/modules/nuclei.json:2,
+ * httpx.json:2, nmap.json:2) with grep -F / re.search semantics. */
+typedef struct sg_matcher sg_matcher;
+int sg_ac_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats,
+                  uint32_t flags, sg_matcher **h);
+int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats,
+                   uint32_t flags, sg_matcher **h);
+/* Compiled-automaton facts: states and groups (DFA count; 1 for Aho-Corasick). */
+int sg_matcher_info(const sg_matcher *h, uint64_t *states, uint32_t *groups, uint32_t *n_pats);
+int sg_match(sg_matcher *h, const uint8_t *buf, size_t n, uint64_t *rec_idx, uint32_t *sig_id,
+             size_t cap, size_t *n_hit);
+/* Device form: hits stay in HBM (context-owned), plus the matched lines serialized in
+ * input order (grep output). */
+typedef struct sg_dev_hits {
+    const uint32_t *rec_idx;  /* device */
+    const uint32_t *sig_id;   /* device */
+    uint64_t n_hits;
+    const uint8_t *lines;     /* device: matched records, '\n'-terminated, input order */
+    uint64_t lines_bytes;
+    uint64_t matched_records;
+    uint64_t in_records;
+} sg_dev_hits;
+int sg_dev_match(sg_ctx *ctx, sg_matcher *h, const uint8_t *d_buf, size_t n, sg_dev_hits *res);
+void sg_free(void *h);  /* frees an sg_matcher */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWARMGPU_H */

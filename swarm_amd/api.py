@@ -1,0 +1,171 @@
+"""Host-side mirror of the scan-result hot path, over libswarmgpu.so (ctypes).
+
+These are the functions the reference-side worker.py / server.py call:
+  lines(buf)                 A3  module-output parsing             (worker/worker.py:83-98)
+  dedup(buf) / dedup_chunks  A5+A7 merge + sort -u                  (server/server.py:399-412)
+  diff(cur, prior)           A8  new records vs the prior scan      (README.md:11)
+  dedup_diff(cur, prior)     A9  scan-completion step               (server/server.py:274-294)
+  Matcher                    A4  literal (Aho-Corasick) / regex (DFA) signature matching
+  Context                    device-resident path (HBM inputs, per-kernel timing)
+
+Every call runs the HIP kernels; there is no CPU fallback. Inputs are bytes-like or numpy
+uint8 arrays; outputs are bytes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import _abi
+from ._abi import check, lib
+
+
+def _view(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        a = b.reshape(-1)
+        if a.dtype != np.uint8:
+            a = a.view(np.uint8)
+        return np.ascontiguousarray(a)
+    return np.frombuffer(memoryview(b), dtype=np.uint8)
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+def lines(buf) -> np.ndarray:
+    """A3: (start, end) spans of the non-empty records, shape (R, 2), uint64."""
+    a = _view(buf)
+    n_rec = C.c_size_t(0)
+    cap = a.size // 2 + 2
+    spans = np.empty(2 * cap, dtype=np.uint64)
+    check(lib.sg_lines(_ptr(a), a.size, spans.ctypes.data_as(C.POINTER(C.c_uint64)), cap,
+                       C.byref(n_rec)))
+    return spans[: 2 * n_rec.value].reshape(-1, 2)
+
+
+def records(buf) -> List[bytes]:
+    a = bytes(_view(buf))
+    return [a[s:e] for s, e in lines(a).tolist()]
+
+
+def dedup(buf) -> bytes:
+    """A7: sort -u of a line-delimited buffer (empty records dropped)."""
+    a = _view(buf)
+    out = np.empty(a.size + 1, dtype=np.uint8)
+    n = C.c_size_t(0)
+    check(lib.sg_dedup(_ptr(a), a.size, out.ctypes.data, out.size, C.byref(n)))
+    return out[: n.value].tobytes()
+
+
+def dedup_chunks(chunks: Sequence[bytes]) -> bytes:
+    """A5+A7: sort -u of the concatenation of chunk bodies, in the order given."""
+    views = [_view(c) for c in chunks]
+    k = len(views)
+    ptrs = (C.c_void_p * max(k, 1))(*[_ptr(v) for v in views])
+    lens = (C.c_size_t * max(k, 1))(*[v.size for v in views])
+    total = sum(v.size for v in views)
+    out = np.empty(total + 1, dtype=np.uint8)
+    n = C.c_size_t(0)
+    check(lib.sg_dedup_chunks(ptrs, lens, k, out.ctypes.data, out.size, C.byref(n)))
+    return out[: n.value].tobytes()
+
+
+def diff(cur, prior) -> bytes:
+    """A8: sorted(set(cur) - set(prior)), '\\n'-terminated."""
+    a, p = _view(cur), _view(prior)
+    out = np.empty(a.size + 1, dtype=np.uint8)
+    n = C.c_size_t(0)
+    check(lib.sg_diff(_ptr(a), a.size, _ptr(p), p.size, out.ctypes.data, out.size, C.byref(n)))
+    return out[: n.value].tobytes()
+
+
+def dedup_diff(cur, prior) -> Tuple[bytes, bytes]:
+    """A9: (sort -u of cur, new records of cur vs prior) in one pass."""
+    a, p = _view(cur), _view(prior)
+    u = np.empty(a.size + 1, dtype=np.uint8)
+    f = np.empty(a.size + 1, dtype=np.uint8)
+    un, fn = C.c_size_t(0), C.c_size_t(0)
+    check(lib.sg_dedup_diff(_ptr(a), a.size, _ptr(p), p.size, u.ctypes.data, u.size, C.byref(un),
+                            f.ctypes.data, f.size, C.byref(fn)))
+    return u[: un.value].tobytes(), f[: fn.value].tobytes()
+
+
+def hash64(rec: bytes) -> int:
+    a = _view(rec)
+    return int(lib.sg_hash64(_ptr(a), a.size))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib.sg_device_count(C.byref(n)))
+    return n.value
+
+
+class Context:
+    """A device context: one HIP device, one stream (torch's, if given), HBM workspaces,
+    optional HIP-event timing of every kernel launch."""
+
+    def __init__(self, device: int = 0, stream: int | None = None):
+        self._h = C.c_void_p()
+        check(lib.sg_ctx_create(device, C.c_void_p(stream) if stream else None, C.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib.sg_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(lib.sg_ctx_sync(self._h))
+
+    def profile(self, on: bool = True):
+        check(lib.sg_ctx_profile(self._h, 1 if on else 0))
+
+    def reset_stats(self):
+        check(lib.sg_ctx_reset_stats(self._h))
+
+    def kernel_stats(self) -> dict:
+        out = {}
+        i = 0
+        name = C.c_char_p()
+        launches = C.c_uint64()
+        ms = C.c_double()
+        while lib.sg_ctx_kernel_stat(self._h, i, C.byref(name), C.byref(launches), C.byref(ms)) == 0:
+            out[name.value.decode()] = (launches.value, ms.value)
+            i += 1
+        return out
+
+    def memcpy(self, dst: int, src: int, n: int):
+        check(lib.sg_ctx_memcpy(self._h, C.c_void_p(dst), C.c_void_p(src), n))
+
+    def to_bytes(self, dptr: int, n: int) -> bytes:
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            self.memcpy(out.ctypes.data, dptr, n)
+        return out.tobytes()
+
+    def dedup_diff(self, d_cur: int, n_cur: int, d_prior: int = 0, n_prior: int = 0) -> _abi.DevResult:
+        """Device pointers in, device result (context-owned) out."""
+        r = _abi.DevResult()
+        check(lib.sg_dev_dedup_diff(self._h, C.c_void_p(d_cur), n_cur,
+                                    C.c_void_p(d_prior) if d_prior else None, n_prior, C.byref(r)))
+        return r
+
+    def partition(self, d_buf: int, n: int, n_parts: int, d_out: int, out_cap: int):
+        """Route records to part(hash64(record), n_parts), writing them grouped by partition
+        into the caller's device buffer d_out (capacity >= n + 1). Returns (bytes per part,
+        records per part)."""
+        pb = (C.c_uint64 * n_parts)()
+        pr = (C.c_uint64 * n_parts)()
+        check(lib.sg_dev_partition(self._h, C.c_void_p(d_buf), n, n_parts, C.c_void_p(d_out),
+                                   out_cap, pb, pr))
+        return list(pb), list(pr)

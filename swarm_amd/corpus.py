@@ -1,0 +1,137 @@
+"""Deterministic synthetic corpora for the BASELINE.json configs.
+
+C1/C2 subdomains: label [a-z0-9]{3,14} + '.' + optional one of api./dev./www./mail. +
+target{0..63}.com, one per line. Records are draws from a universe of `n` names (seeded),
+so about 63 % of lines are unique (n draws from n items). The prior scan is the sorted
+unique set minus every name whose universe id is divisible by 10 (90 % of it).
+
+All generation is vectorized numpy: 10M lines take a few seconds.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ALPHA = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", dtype=np.uint8)
+OPTS = [b"", b"api.", b"dev.", b"www.", b"mail."]
+
+
+def _mix(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64, copy=True)
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+    return x
+
+
+def render_names(ids: np.ndarray, salt: int = 0) -> tuple:
+    """Render universe ids to subdomain bytes. Returns (matrix (m, W) uint8, lengths)."""
+    ids = ids.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        h = _mix(ids * np.uint64(0x9E3779B97F4A7C15) + np.uint64(salt))
+    m = ids.size
+    L = (3 + (h % np.uint64(12))).astype(np.int64)                 # label length 3..14
+    lab = np.empty((m, 14), dtype=np.uint8)
+    g = h
+    for j in range(14):
+        with np.errstate(over="ignore"):
+            g = _mix(g + np.uint64(j + 1))
+        lab[:, j] = ALPHA[(g % np.uint64(36)).astype(np.int64)]
+    opt = ((h >> np.uint64(40)) % np.uint64(5)).astype(np.int64)
+    tgt = ((h >> np.uint64(48)) % np.uint64(64)).astype(np.int64)
+    # middle: '.' + opt (padded to 6)
+    mid = np.zeros((m, 6), dtype=np.uint8)
+    mid[:, 0] = ord(".")
+    mid_len = np.ones(m, dtype=np.int64)
+    for k, o in enumerate(OPTS):
+        sel = opt == k
+        if o:
+            mid[sel, 1:1 + len(o)] = np.frombuffer(o, dtype=np.uint8)
+            mid_len[sel] = 1 + len(o)
+    # tail: target{i}.com
+    tail = np.zeros((m, 13), dtype=np.uint8)
+    tail[:, :6] = np.frombuffer(b"target", dtype=np.uint8)
+    two = tgt >= 10
+    d0 = np.where(two, tgt // 10, tgt)
+    tail[:, 6] = ord("0") + d0
+    tail[two, 7] = ord("0") + tgt[two] % 10
+    nd = np.where(two, 2, 1)
+    com = np.frombuffer(b".com", dtype=np.uint8)
+    for j in range(4):
+        col = 6 + nd + j
+        tail[np.arange(m), col] = com[j]
+    tail_len = 6 + nd + 4
+    W = 14 + 6 + 13
+    mat = np.zeros((m, W), dtype=np.uint8)
+    msk = np.zeros((m, W), dtype=bool)
+    mat[:, :14] = lab
+    msk[:, :14] = np.arange(14)[None, :] < L[:, None]
+    mat[:, 14:20] = mid
+    msk[:, 14:20] = np.arange(6)[None, :] < mid_len[:, None]
+    mat[:, 20:33] = tail
+    msk[:, 20:33] = np.arange(13)[None, :] < tail_len[:, None]
+    return mat, msk
+
+
+def _flatten(mat: np.ndarray, msk: np.ndarray, sep: int = 0x0A) -> np.ndarray:
+    m, W = mat.shape
+    full = np.empty((m, W + 1), dtype=np.uint8)
+    full[:, :W] = mat
+    full[:, W] = sep
+    fm = np.empty((m, W + 1), dtype=bool)
+    fm[:, :W] = msk
+    fm[:, W] = True
+    return full[fm]
+
+
+def subdomains(n: int, seed: int = 1234, universe: int | None = None, chunk: int = 1 << 20) -> np.ndarray:
+    """n subdomain lines (uint8 array, '\\n'-terminated) drawn from a universe of ids."""
+    U = universe or max(n, 1)
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(0, U, size=n, dtype=np.uint64)
+    parts = []
+    for i in range(0, n, chunk):
+        mat, msk = render_names(ids[i:i + chunk])
+        parts.append(_flatten(mat, msk))
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8), ids
+
+
+def prior_of(ids: np.ndarray) -> np.ndarray:
+    """The prior scan: sorted unique names of the drawn ids except ids % 10 == 0, serialized."""
+    u = np.unique(ids)
+    u = u[(u % np.uint64(10)) != 0]
+    mat, msk = render_names(u)
+    # sort rows bytewise: fixed-width rows padded with 0 sort like their byte strings
+    # because no name contains NUL and a shorter name is a prefix-padded-with-0.
+    W = mat.shape[1]
+    rows = np.where(msk, mat, 0)
+    # names are a concatenation of 3 segments; compact each row left first
+    comp = np.zeros_like(rows)
+    lens = msk.sum(axis=1)
+    flat = rows[msk]
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    idx = starts[:, None] + np.arange(W)[None, :]
+    valid = np.arange(W)[None, :] < lens[:, None]
+    comp[valid] = flat[idx[valid]]
+    v = comp.view(f"S{W}").reshape(-1)
+    order = np.argsort(v, kind="stable")
+    v_sorted = v[order]
+    keep = np.ones(v_sorted.size, dtype=bool)
+    keep[1:] = v_sorted[1:] != v_sorted[:-1]
+    sel = order[keep]
+    return _flatten(comp[sel], valid[sel])
+
+
+def chunk_layout(lines_arr: np.ndarray, n_chunks: int) -> list:
+    """Split a '\\n'-terminated buffer into n_chunks worker-output chunks at line boundaries
+    (the per-chunk outputs the server merges, server/server.py:399-412)."""
+    nl = np.flatnonzero(lines_arr == 0x0A)
+    R = nl.size
+    bounds = [0]
+    for k in range(1, n_chunks):
+        r = (R * k) // n_chunks
+        bounds.append(int(nl[r - 1]) + 1 if r > 0 else 0)
+    bounds.append(lines_arr.size)
+    return [lines_arr[bounds[i]:bounds[i + 1]] for i in range(n_chunks)]

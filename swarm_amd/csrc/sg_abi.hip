@@ -1,0 +1,249 @@
+// sg_abi.hip — the exported C entry points of libswarmgpu.so (include/swarmgpu.h) and the
+// multi-GPU record partition.
+#include "sg_internal.hpp"
+#include "sg_prims.hpp"
+
+#include <string.h>
+
+namespace sg {
+
+int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
+                   uint64_t n_prior, bool want_fresh, sg_dev_result *res);
+
+// ------------------------------------------------------------------ record hash
+// Shared host/device definition (oracle: tests restate it in Python).
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+template <class Load>
+__host__ __device__ __forceinline__ uint64_t hash_words(Load ld, uint32_t len) {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ ((uint64_t)len * 0xff51afd7ed558ccdull);
+    for (uint32_t o = 0; o < len; o += 8) {
+        uint64_t w = 0;
+        const uint32_t take = (len - o) < 8u ? (len - o) : 8u;
+        for (uint32_t j = 0; j < take; ++j) w |= (uint64_t)ld(o + j) << (8 * j);
+        h = (h ^ mix64(w)) * 0x9fb21c651e98df25ull;
+        h ^= h >> 29;
+    }
+    return mix64(h);
+}
+
+__host__ __device__ __forceinline__ uint32_t part_of(uint64_t h, uint32_t parts) {
+    return (uint32_t)(((h >> 32) * (uint64_t)parts) >> 32);
+}
+
+__global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ buf,
+                                                   const uint32_t *__restrict__ starts,
+                                                   const uint32_t *__restrict__ ends, uint32_t R,
+                                                   uint32_t parts, uint64_t *keys,
+                                                   unsigned long long *cnt /* [2*parts] */) {
+    __shared__ unsigned long long s_c[2 * 256];
+    for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) s_c[i] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < R) {
+        const uint32_t s = starts[i], e = ends[i];
+        const uint8_t *p = buf + s;
+        const uint64_t h = hash_words([&](uint32_t j) { return p[j]; }, e - s);
+        const uint32_t q = part_of(h, parts);
+        keys[i] = q;
+        atomicAdd(&s_c[q], 1ull);
+        atomicAdd(&s_c[256 + q], (unsigned long long)(e - s + 1));
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < parts; q += blockDim.x) {
+        if (s_c[q]) atomicAdd(&cnt[q], s_c[q]);
+        if (s_c[256 + q]) atomicAdd(&cnt[parts + q], s_c[256 + q]);
+    }
+}
+
+struct Acq {
+    sg_ctx *c = nullptr;
+    ~Acq() { if (c) pool_release(c); }
+};
+
+static int acquire(Acq *a) {
+    int dev = 0;
+    SG_TRY(pick_device(&dev));
+    SG_TRY(pool_acquire(dev, &a->c));
+    SG_HIP(hipSetDevice(dev));
+    return SG_OK;
+}
+
+static int upload(sg_ctx *c, int s, const uint8_t *host, size_t n, uint8_t **d) {
+    SG_TRY(slot(c, s, n + 16, d));
+    if (n) SG_HIP(hipMemcpyAsync(*d, host, n, hipMemcpyHostToDevice, c->stream));
+    return SG_OK;
+}
+
+static int aligned_in(sg_ctx *c, int s, const uint8_t *d, size_t n, const uint8_t **out) {
+    if (((uintptr_t)d & 15) == 0) { *out = d; return SG_OK; }
+    uint8_t *a;
+    SG_TRY(slot(c, s, n + 16, &a));
+    if (n) SG_HIP(hipMemcpyAsync(a, d, n, hipMemcpyDeviceToDevice, c->stream));
+    *out = a;
+    return SG_OK;
+}
+
+static int host_dedup_diff(const uint8_t *const *chunks, const size_t *lens, size_t k,
+                           const uint8_t *prior, size_t n_prior, bool want_uniq, bool want_fresh,
+                           uint8_t *uniq, size_t ucap, size_t *un, uint8_t *fresh, size_t fcap,
+                           size_t *fn) {
+    uint64_t n = 0;
+    for (size_t i = 0; i < k; ++i) {
+        if (!chunks[i] && lens[i]) { set_error("chunk %zu is NULL", i); return SG_E_INVAL; }
+        n += lens[i];
+    }
+    if (n > MAX_BYTES || n_prior > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    Acq a;
+    SG_TRY(acquire(&a));
+    sg_ctx *c = a.c;
+    uint8_t *d_cur;
+    SG_TRY(slot(c, S_IN, n + 16, &d_cur));
+    uint64_t o = 0;
+    for (size_t i = 0; i < k; ++i) {
+        if (lens[i]) SG_HIP(hipMemcpyAsync(d_cur + o, chunks[i], lens[i], hipMemcpyHostToDevice, c->stream));
+        o += lens[i];
+    }
+    uint8_t *d_prior = nullptr;
+    if (want_fresh && n_prior) SG_TRY(upload(c, S_IN2, prior, n_prior, &d_prior));
+    sg_dev_result r;
+    SG_TRY(dev_dedup_diff(c, d_cur, n, d_prior, want_fresh ? n_prior : 0, want_fresh, &r));
+    int rc = SG_OK;
+    if (want_uniq) {
+        *un = r.uniq_bytes;
+        if (r.uniq_bytes > ucap) rc = SG_E_CAP;
+    }
+    if (want_fresh) {
+        *fn = r.fresh_bytes;
+        if (r.fresh_bytes > fcap) rc = SG_E_CAP;
+    }
+    if (rc == SG_E_CAP) { set_error("output capacity too small"); SG_HIP(hipStreamSynchronize(c->stream)); return rc; }
+    if (want_uniq && r.uniq_bytes) SG_HIP(hipMemcpyAsync(uniq, r.uniq, r.uniq_bytes, hipMemcpyDeviceToHost, c->stream));
+    if (want_fresh && r.fresh_bytes) SG_HIP(hipMemcpyAsync(fresh, r.fresh, r.fresh_bytes, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
+    return SG_OK;
+}
+
+int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, uint8_t *d_out,
+                  size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
+    if (parts == 0 || parts > 256) { set_error("n_parts must be in 1..256"); return SG_E_INVAL; }
+    Lines L;
+    SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L));
+    const uint32_t R = L.n_rec;
+    unsigned long long *cnt;
+    SG_TRY(slot(c, S_M_CNT, 2 * 256, &cnt));
+    SG_HIP(hipMemsetAsync(cnt, 0, 2 * 256 * 8, c->stream));
+    uint64_t *keys, *keys2;
+    uint32_t *v1, *v2;
+    SG_TRY(slot(c, S_KEYS2, R, &keys));
+    SG_TRY(slot(c, S_R_KEY2, R, &keys2));
+    SG_TRY(slot(c, S_VALS, R, &v1));
+    SG_TRY(slot(c, S_VALS2, R, &v2));
+    if (R) {
+        SG_LAUNCH(c, "part_keys", k_part_keys, (R + 255) / 256, 256, 0, d_buf, L.starts, L.ends, R, parts, keys, cnt);
+    }
+    uint64_t *K;
+    uint32_t *V;
+    SG_TRY(radix_sort(c, keys, v1, keys2, v2, R, 0, 8, true, &K, &V, "rs_pass_part"));
+    uint8_t *out;
+    uint64_t bytes = 0;
+    SG_TRY(serialize(c, d_buf, L.starts, L.ends, V, nullptr, R, S_PART_OUT, &out, &bytes));
+    if (bytes > out_cap) { set_error("partition output capacity %zu < %llu", out_cap, (unsigned long long)bytes); return SG_E_CAP; }
+    if (bytes) SG_HIP(hipMemcpyAsync(d_out, out, bytes, hipMemcpyDeviceToDevice, c->stream));
+    uint64_t h[2 * 256];
+    SG_TRY(ctx_readback(c, h, cnt, 2 * parts * 8));
+    for (uint32_t q = 0; q < parts; ++q) {
+        if (part_records) part_records[q] = h[q];
+        if (part_bytes) part_bytes[q] = h[parts + q];
+    }
+    return SG_OK;
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+uint64_t sg_hash64(const uint8_t *rec, size_t len) {
+    return hash_words([&](uint32_t j) { return rec[j]; }, (uint32_t)len);
+}
+
+int sg_lines(const uint8_t *buf, size_t n, uint64_t *spans, size_t cap, size_t *n_rec) {
+    if ((!buf && n) || !n_rec) { set_error("sg_lines: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    Acq a;
+    SG_TRY(acquire(&a));
+    sg_ctx *c = a.c;
+    uint8_t *d;
+    SG_TRY(upload(c, S_IN, buf, n, &d));
+    Lines L;
+    SG_TRY(run_lines(c, d, n, CUR_SLOTS, &L));
+    *n_rec = L.n_rec;
+    if (L.n_rec > cap) { set_error("span capacity too small"); return SG_E_CAP; }
+    std::vector<uint32_t> s(L.n_rec), e(L.n_rec);
+    if (L.n_rec) {
+        SG_HIP(hipMemcpyAsync(s.data(), L.starts, L.n_rec * 4ull, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipMemcpyAsync(e.data(), L.ends, L.n_rec * 4ull, hipMemcpyDeviceToHost, c->stream));
+    }
+    SG_HIP(hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < L.n_rec; ++i) { spans[2 * i] = s[i]; spans[2 * i + 1] = e[i]; }
+    return SG_OK;
+}
+
+int sg_dedup(const uint8_t *buf, size_t n, uint8_t *out, size_t cap, size_t *out_n) {
+    if ((!buf && n) || !out_n) { set_error("sg_dedup: bad arguments"); return SG_E_INVAL; }
+    const uint8_t *ch[1] = {buf};
+    size_t ln[1] = {n};
+    return host_dedup_diff(ch, ln, 1, nullptr, 0, true, false, out, cap, out_n, nullptr, 0, nullptr);
+}
+
+int sg_dedup_chunks(const uint8_t *const *chunks, const size_t *lens, size_t k, uint8_t *out, size_t cap,
+                    size_t *out_n) {
+    if ((!chunks && k) || (!lens && k) || !out_n) { set_error("sg_dedup_chunks: bad arguments"); return SG_E_INVAL; }
+    return host_dedup_diff(chunks, lens, k, nullptr, 0, true, false, out, cap, out_n, nullptr, 0, nullptr);
+}
+
+int sg_diff(const uint8_t *cur, size_t n_cur, const uint8_t *prior, size_t n_prior, uint8_t *out, size_t cap,
+            size_t *out_n) {
+    if ((!cur && n_cur) || (!prior && n_prior) || !out_n) { set_error("sg_diff: bad arguments"); return SG_E_INVAL; }
+    const uint8_t *ch[1] = {cur};
+    size_t ln[1] = {n_cur};
+    return host_dedup_diff(ch, ln, 1, prior, n_prior, false, true, nullptr, 0, nullptr, out, cap, out_n);
+}
+
+int sg_dedup_diff(const uint8_t *cur, size_t n_cur, const uint8_t *prior, size_t n_prior, uint8_t *uniq,
+                  size_t uniq_cap, size_t *uniq_n, uint8_t *fresh, size_t fresh_cap, size_t *fresh_n) {
+    if ((!cur && n_cur) || (!prior && n_prior) || !uniq_n || !fresh_n) { set_error("sg_dedup_diff: bad arguments"); return SG_E_INVAL; }
+    const uint8_t *ch[1] = {cur};
+    size_t ln[1] = {n_cur};
+    return host_dedup_diff(ch, ln, 1, prior, n_prior, true, true, uniq, uniq_cap, uniq_n, fresh, fresh_cap, fresh_n);
+}
+
+int sg_dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, const uint8_t *d_prior, size_t n_prior,
+                      sg_dev_result *res) {
+    if (!c || !res || (!d_cur && n_cur) || (!d_prior && n_prior)) { set_error("sg_dev_dedup_diff: bad arguments"); return SG_E_INVAL; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *cur, *prior = nullptr;
+    SG_TRY(aligned_in(c, S_IN, d_cur, n_cur, &cur));
+    if (n_prior) SG_TRY(aligned_in(c, S_IN2, d_prior, n_prior, &prior));
+    return dev_dedup_diff(c, cur, n_cur, prior, n_prior, true, res);
+}
+
+int sg_dev_partition(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t n_parts, uint8_t *d_out,
+                     size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
+    if (!c || (!d_out && n) || (!d_buf && n)) { set_error("sg_dev_partition: bad arguments"); return SG_E_INVAL; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b;
+    SG_TRY(aligned_in(c, S_IN, d_buf, n, &b));
+    return dev_partition(c, b, n, n_parts, d_out, out_cap, part_bytes, part_records);
+}
+
+}  // extern "C"

@@ -1,0 +1,233 @@
+// sg_common.hpp — shared host/device infrastructure for libswarmgpu (gfx950 only).
+//
+// Host side: thread-local error text, the sg_ctx (device, stream, grow-only HBM buffer
+// slots, optional per-kernel HIP-event timing) and a launch wrapper.
+// Device side: wave64/block scans and the decoupled look-back used by every single-pass
+// kernel (line split, compaction, onesweep radix passes). Look-back status words are
+// 8-byte {flag:2 | value:62} granules written with one relaxed agent-scope (sc1) store
+// and polled with relaxed agent-scope loads: the data IS the flag, so no fences are
+// needed (MI355X_MICROARCH.md "Valid forms", R2 granule). Tiles take their id from an
+// atomic ticket so every tile a waiter depends on has already been dispatched.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/swarmgpu.h"
+
+namespace sg {
+
+// ------------------------------------------------------------------ errors
+void set_error(const char *fmt, ...);
+const char *get_error();
+
+#define SG_HIP(call)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            ::sg::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call,                 \
+                            hipGetErrorString(e_));                                    \
+            return SG_E_HIP;                                                           \
+        }                                                                              \
+    } while (0)
+
+#define SG_TRY(expr)                  \
+    do {                              \
+        int rc_ = (expr);             \
+        if (rc_ != SG_OK) return rc_; \
+    } while (0)
+
+// ------------------------------------------------------------------ context
+enum Slot : int {
+    // line split of the current buffer
+    S_STARTS, S_ENDS, S_KEYS, S_KEYS2, S_VALS, S_VALS2, S_LB, S_COUNT,
+    // dedup / refinement
+    S_UNIQ, S_GS, S_GE, S_SEL, S_OFFS, S_OUT_UNIQ, S_OUT_FRESH, S_FRESH_IDX,
+    S_R_POS, S_R_KEY, S_R_KEY2, S_R_VAL, S_R_VAL2, S_R_GID, S_R_OFF,
+    S_HIST, S_ALIGN,
+    // prior
+    S_P_STARTS, S_P_ENDS, S_P_KEYS, S_P_REC, S_P_FLAG, S_P_KEYS2, S_P_VALS, S_P_VALS2,
+    S_P_UNIQ, S_P_SORTED_KEYS,
+    // partition / match
+    S_PART, S_PART_OUT, S_M_HITS, S_M_SIG, S_M_LINES, S_M_TMP, S_M_TMP2, S_M_CNT,
+    S_IN, S_IN2, S_CUR_UR, S_CUR_UK, S_RS_STATUS,
+    S_NSLOTS
+};
+
+struct KStat {
+    const char *name;
+    uint64_t launches;
+    double ms;
+};
+
+struct sg_ctx_impl;
+}  // namespace sg
+
+struct sg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool owns_stream = false;
+    void *slot_ptr[sg::S_NSLOTS] = {};
+    size_t slot_cap[sg::S_NSLOTS] = {};
+    void *pinned = nullptr;   // host pinned staging for small readbacks
+    // profiling
+    bool profile = false;
+    std::vector<sg::KStat> stats;
+    struct Pending { int stat; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> free_events;
+};
+
+namespace sg {
+
+int ctx_slot(sg_ctx *c, int slot, size_t bytes, void **out);
+template <class T>
+inline int slot(sg_ctx *c, int s, size_t count, T **out) {
+    void *p = nullptr;
+    int rc = ctx_slot(c, s, count * sizeof(T) + 64, &p);
+    *out = (T *)p;
+    return rc;
+}
+int ctx_readback(sg_ctx *c, void *host, const void *dev, size_t bytes);  // sync on stream
+int ctx_harvest(sg_ctx *c);
+int prof_begin(sg_ctx *c, const char *name, int *stat, hipEvent_t *a);
+void prof_end(sg_ctx *c, int stat, hipEvent_t a);
+
+// Launch with optional HIP-event timing on the context stream.
+#define SG_LAUNCH(ctx, name, kernel, grid, block, lds, ...)                          \
+    do {                                                                              \
+        int st_ = -1;                                                                 \
+        hipEvent_t ea_ = nullptr;                                                     \
+        if ((ctx)->profile) ::sg::prof_begin((ctx), (name), &st_, &ea_);              \
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), (lds), (ctx)->stream,     \
+                           __VA_ARGS__);                                              \
+        hipError_t le_ = hipGetLastError();                                           \
+        if (le_ != hipSuccess) {                                                      \
+            ::sg::set_error("launch %s: %s", (name), hipGetErrorString(le_));         \
+            return SG_E_HIP;                                                          \
+        }                                                                             \
+        if (st_ >= 0) ::sg::prof_end((ctx), st_, ea_);                                \
+    } while (0)
+
+// ------------------------------------------------------------------ limits
+constexpr uint64_t MAX_BYTES = 0xFFFF0000ull;  // 32-bit record offsets with headroom
+
+// ------------------------------------------------------------------ device helpers
+#define LB_FLAG_AGG 1ull
+#define LB_FLAG_INC 2ull
+#define LB_VAL_MASK ((1ull << 62) - 1)
+
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t flag, uint64_t v) {
+    __hip_atomic_store(p, (flag << 62) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Exclusive block scan, BLOCK threads (multiple of 64). lds: >= BLOCK/64 elements.
+template <int BLOCK, class T>
+__device__ __forceinline__ T block_excl_scan(T v, T *total, T *lds) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    T inc = wave_incl_scan(v);
+    if (lane == 63) lds[wid] = inc;
+    __syncthreads();
+    T woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) {
+        T s = lds[w];
+        woff += (w < wid) ? s : T(0);
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return woff + inc - v;
+}
+
+// Decoupled look-back by ONE full wave: returns the exclusive prefix of tile `tile`
+// (values packed so that field sums never carry). Tile 0 must not call this.
+__device__ __forceinline__ uint64_t wave_lookback(const uint64_t *status, int64_t tile) {
+    const int lane = lane_id();
+    uint64_t excl = 0;
+    int64_t base = tile - 1;
+    uint32_t spins = 0;
+    while (true) {
+        const int64_t t = base - lane;
+        const uint64_t s = (t >= 0) ? lb_load(status + t) : (LB_FLAG_INC << 62);
+        const uint32_t flag = (uint32_t)(s >> 62);
+        const uint64_t inc_mask = __ballot(flag == LB_FLAG_INC);
+        const uint64_t empty_mask = __ballot(flag == 0);
+        const int first_inc = inc_mask ? (__ffsll((long long)inc_mask) - 1) : 64;
+        const uint64_t need = (first_inc >= 63) ? ~0ull : ((2ull << first_inc) - 1);
+        if (empty_mask & need) {
+            if (++spins > 64) __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t v = (lane <= first_inc) ? (s & LB_VAL_MASK) : 0ull;
+        excl += wave_sum(v);
+        if (first_inc < 64) break;
+        base -= 64;
+    }
+    return excl;
+}
+
+// Tile ticket: dynamic tile ids in dispatch order (forward progress for look-back).
+__device__ __forceinline__ uint32_t take_ticket(uint32_t *counter, uint32_t *lds_slot) {
+    if (threadIdx.x == 0) *lds_slot = atomicAdd(counter, 1u);
+    __syncthreads();
+    return *lds_slot;
+}
+
+// Bytewise compare of two records starting `off` bytes in (both have > off bytes or
+// not — lengths decide). Returns <0, 0, >0 like memcmp-then-length.
+__device__ __forceinline__ int rec_cmp(const uint8_t *buf_a, uint32_t sa, uint32_t ea,
+                                       const uint8_t *buf_b, uint32_t sb, uint32_t eb,
+                                       uint32_t off) {
+    uint32_t la = ea - sa, lb = eb - sb;
+    uint32_t m = la < lb ? la : lb;
+    for (uint32_t i = off; i < m; ++i) {
+        uint32_t x = buf_a[sa + i], y = buf_b[sb + i];
+        if (x != y) return (int)x - (int)y;
+    }
+    return (la < lb) ? -1 : (la > lb ? 1 : 0);
+}
+
+// Prefix key of a record at byte offset `off`: bytes [off, off+7) big-endian in bits
+// 63..8 (zero past the record end) and tag = min(remaining, 8) in bits 7..0. Ordering
+// of (key) == bytewise ordering of the suffixes when the tags differ or tag < 8;
+// equal keys with tag 8 need the next chunk.
+__device__ __forceinline__ uint64_t chunk_key(const uint8_t *buf, uint32_t s, uint32_t e, uint32_t off) {
+    uint32_t rem = (e - s > off) ? (e - s - off) : 0u;
+    uint32_t take = rem < 7u ? rem : 7u;
+    uint64_t k = 0;
+    const uint8_t *p = buf + s + off;
+    for (uint32_t j = 0; j < take; ++j) k |= (uint64_t)p[j] << (56 - 8 * j);
+    return k | (uint64_t)(rem < 8u ? rem : 8u);
+}
+
+}  // namespace sg

@@ -1,0 +1,53 @@
+// sg_internal.hpp — host-side internal API shared by the libswarmgpu translation units.
+#pragma once
+#include "sg_common.hpp"
+
+namespace sg {
+
+int pool_acquire(int device, sg_ctx **out);
+void pool_release(sg_ctx *c);
+int pick_device(int *dev);
+
+// Slot sets let the cur and prior buffers be parsed/sorted without sharing buffers.
+struct SlotSet {
+    int starts, ends, keys, keys2, vals, vals2, uniq, lb;
+};
+extern const SlotSet CUR_SLOTS;
+extern const SlotSet PRIOR_SLOTS;
+
+// A3 parse result (device arrays, n_rec records).
+struct Lines {
+    uint32_t *starts = nullptr;
+    uint32_t *ends = nullptr;
+    uint64_t *keys = nullptr;   // chunk_key(rec, 0)
+    uint32_t n_rec = 0;
+};
+// Split d_buf (16-byte aligned device pointer, n bytes) into non-empty records.
+int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out);
+
+// LSD radix sort of (u64 key, u32 val) pairs on bits [begin_bit, end_bit), stable.
+// Ping-pongs between (keys, vals) and (keys_alt, vals_alt); returns the final arrays.
+// iota_vals: vals[i] = i is implied on input (vals need not be initialised).
+int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
+               uint32_t n, int begin_bit, int end_bit, bool iota_vals,
+               uint64_t **keys_out, uint32_t **vals_out, const char *pass_name = "rs_pass");
+
+// Bytewise sort + uniqueness of the records of a parsed buffer.
+struct SortedSet {
+    uint64_t *keys = nullptr;  // chunk_key(rec, 0) in sorted order
+    uint32_t *recs = nullptr;  // record ids in sorted order
+    uint8_t *uniq = nullptr;   // 1 = first occurrence of its bytes
+    uint32_t n = 0;
+};
+int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet &ss, SortedSet *out);
+
+// Compaction: indices i < n with flag[i] != 0, in order. Returns count.
+int select_flags(sg_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out_idx, uint32_t *count);
+
+// Serialize records (ids into starts/ends, in list order) as '\n'-terminated bytes.
+// rec_of: list[i] is a position into `map` (if map != null) giving the record id.
+int serialize(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+              const uint32_t *list, const uint32_t *map, uint32_t count, int out_slot,
+              uint8_t **d_out, uint64_t *bytes);
+
+}  // namespace sg

@@ -1,0 +1,231 @@
+// sg_runtime.hip — context lifetime, HBM buffer slots, HIP-event kernel timing, errors,
+// and the per-device context pool behind the re-entrant host-buffer API.
+#include "sg_common.hpp"
+#include "sg_internal.hpp"
+
+#include <string.h>
+
+namespace sg {
+
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+const char *get_error() { return g_err.c_str(); }
+
+int ctx_slot(sg_ctx *c, int s, size_t bytes, void **out) {
+    if (bytes < 256) bytes = 256;
+    if (c->slot_cap[s] < bytes) {
+        if (c->slot_ptr[s]) {
+            SG_HIP(hipStreamSynchronize(c->stream));
+            SG_HIP(hipFree(c->slot_ptr[s]));
+            c->slot_ptr[s] = nullptr;
+            c->slot_cap[s] = 0;
+        }
+        size_t want = bytes + bytes / 8;  // headroom so small growth does not realloc
+        if (hipMalloc(&c->slot_ptr[s], want) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("hipMalloc(%zu) failed for slot %d", want, s);
+            return SG_E_NOMEM;
+        }
+        c->slot_cap[s] = want;
+    }
+    *out = c->slot_ptr[s];
+    return SG_OK;
+}
+
+int ctx_readback(sg_ctx *c, void *host, const void *dev, size_t bytes) {
+    if (bytes > 4096) {
+        SG_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipStreamSynchronize(c->stream));
+        return SG_OK;
+    }
+    SG_HIP(hipMemcpyAsync(c->pinned, dev, bytes, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
+    memcpy(host, c->pinned, bytes);
+    return SG_OK;
+}
+
+int prof_begin(sg_ctx *c, const char *name, int *stat, hipEvent_t *a) {
+    int idx = -1;
+    for (size_t i = 0; i < c->stats.size(); ++i)
+        if (c->stats[i].name == name || strcmp(c->stats[i].name, name) == 0) { idx = (int)i; break; }
+    if (idx < 0) {
+        c->stats.push_back(KStat{name, 0, 0.0});
+        idx = (int)c->stats.size() - 1;
+    }
+    hipEvent_t e;
+    if (!c->free_events.empty()) { e = c->free_events.back(); c->free_events.pop_back(); }
+    else if (hipEventCreate(&e) != hipSuccess) { (void)hipGetLastError(); return SG_E_HIP; }
+    (void)hipEventRecord(e, c->stream);
+    *stat = idx;
+    *a = e;
+    return SG_OK;
+}
+
+void prof_end(sg_ctx *c, int stat, hipEvent_t a) {
+    hipEvent_t e;
+    if (!c->free_events.empty()) { e = c->free_events.back(); c->free_events.pop_back(); }
+    else if (hipEventCreate(&e) != hipSuccess) { (void)hipGetLastError(); return; }
+    (void)hipEventRecord(e, c->stream);
+    c->pending.push_back(sg_ctx::Pending{stat, a, e});
+}
+
+int ctx_harvest(sg_ctx *c) {
+    if (c->pending.empty()) return SG_OK;
+    SG_HIP(hipStreamSynchronize(c->stream));
+    for (auto &p : c->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->stats[p.stat].ms += ms;
+            c->stats[p.stat].launches += 1;
+        } else {
+            (void)hipGetLastError();
+        }
+        c->free_events.push_back(p.a);
+        c->free_events.push_back(p.b);
+    }
+    c->pending.clear();
+    return SG_OK;
+}
+
+// ------------------------------------------------------------------ context pool
+struct Pool {
+    std::mutex mu;
+    std::vector<sg_ctx *> idle[64];
+};
+static Pool g_pool;
+
+int pool_acquire(int device, sg_ctx **out) {
+    {
+        std::lock_guard<std::mutex> g(g_pool.mu);
+        auto &v = g_pool.idle[device & 63];
+        if (!v.empty()) { *out = v.back(); v.pop_back(); return SG_OK; }
+    }
+    return sg_ctx_create(device, nullptr, out);
+}
+
+void pool_release(sg_ctx *c) {
+    std::lock_guard<std::mutex> g(g_pool.mu);
+    g_pool.idle[c->device & 63].push_back(c);
+}
+
+int pick_device(int *dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible");
+        return SG_E_NODEV;
+    }
+    SG_HIP(hipGetDevice(dev));
+    return SG_OK;
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+const char *sg_last_error(void) { return get_error(); }
+int sg_version(void) { return 10000; }
+
+int sg_device_count(int *n) {
+    if (!n) return SG_E_INVAL;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) { (void)hipGetLastError(); c = 0; }
+    *n = c;
+    return SG_OK;
+}
+
+int sg_ctx_create(int device, void *stream, sg_ctx **out) {
+    if (!out) return SG_E_INVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible");
+        return SG_E_NODEV;
+    }
+    if (device < 0 || device >= n) { set_error("device %d out of range", device); return SG_E_INVAL; }
+    SG_HIP(hipSetDevice(device));
+    sg_ctx *c = new sg_ctx();
+    c->device = device;
+    if (stream) {
+        c->stream = (hipStream_t)stream;
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete c;
+            set_error("hipStreamCreate failed");
+            return SG_E_HIP;
+        }
+        c->owns_stream = true;
+    }
+    if (hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        if (c->owns_stream) (void)hipStreamDestroy(c->stream);
+        delete c;
+        set_error("hipHostMalloc failed");
+        return SG_E_NOMEM;
+    }
+    *out = c;
+    return SG_OK;
+}
+
+int sg_ctx_destroy(sg_ctx *c) {
+    if (!c) return SG_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (int s = 0; s < S_NSLOTS; ++s)
+        if (c->slot_ptr[s]) (void)hipFree(c->slot_ptr[s]);
+    for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : c->free_events) (void)hipEventDestroy(e);
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->owns_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SG_OK;
+}
+
+int sg_ctx_sync(sg_ctx *c) {
+    if (!c) return SG_E_INVAL;
+    SG_HIP(hipStreamSynchronize(c->stream));
+    return SG_OK;
+}
+
+int sg_ctx_profile(sg_ctx *c, int enable) {
+    if (!c) return SG_E_INVAL;
+    c->profile = enable != 0;
+    return SG_OK;
+}
+
+int sg_ctx_kernel_stat(sg_ctx *c, int idx, const char **name, uint64_t *launches, double *total_ms) {
+    if (!c) return SG_E_INVAL;
+    SG_TRY(ctx_harvest(c));
+    if (idx < 0 || idx >= (int)c->stats.size()) return SG_E_INVAL;
+    if (name) *name = c->stats[idx].name;
+    if (launches) *launches = c->stats[idx].launches;
+    if (total_ms) *total_ms = c->stats[idx].ms;
+    return SG_OK;
+}
+
+int sg_ctx_memcpy(sg_ctx *c, void *dst, const void *src, size_t n) {
+    if (!c || (n && (!dst || !src))) return SG_E_INVAL;
+    if (!n) return SG_OK;
+    SG_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDefault, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
+    return SG_OK;
+}
+
+int sg_ctx_reset_stats(sg_ctx *c) {
+    if (!c) return SG_E_INVAL;
+    SG_TRY(ctx_harvest(c));
+    c->stats.clear();
+    return SG_OK;
+}
+
+}  // extern "C"

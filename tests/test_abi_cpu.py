@@ -1,0 +1,50 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the header
+declares, reports no device cleanly, and its host-side hash matches the restatement."""
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+from hash_oracle import hash64 as py_hash64
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "swarmgpu.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(sg_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from swarm_amd import _abi
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(_abi.lib, n), n
+    assert set(names) == set(_abi.EXPORTS)
+
+
+def test_version_and_device_count():
+    from swarm_amd import _abi
+    assert _abi.lib.sg_version() >= 10000
+    import ctypes
+    n = ctypes.c_int(-1)
+    assert _abi.lib.sg_device_count(ctypes.byref(n)) == 0
+    assert n.value >= 0
+
+
+@pytest.mark.parametrize("rec", [b"", b"a", b"abcdefg", b"abcdefgh", b"abcdefghi",
+                                 b"x.target12.com", bytes(range(256)), b"\x00" * 17])
+def test_hash64_host_matches_restatement(rec):
+    from swarm_amd import hash64
+    assert hash64(rec) == py_hash64(rec)
+
+
+def test_no_gpu_fails_loudly_not_silently():
+    """Without a device the product path raises instead of computing on the CPU."""
+    from swarm_amd import device_count, dedup
+    from swarm_amd._abi import SGError
+    if device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(SGError):
+        dedup(b"b\na\n")

@@ -1,0 +1,214 @@
+"""GPU parity: A3 parse, A5+A7 merge/dedup, A8 diff and the partition through the C-ABI,
+bit-exact against the CPU oracle and the GNU-tool golden vectors."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import b64d, load_golden
+from hash_oracle import hash64 as py_hash64, part_of
+from oracle import semantics as S
+
+pytestmark = pytest.mark.gpu
+
+CU = load_golden("coreutils_vectors.json")
+REF = load_golden("reference_vectors.json")
+
+
+@pytest.fixture(scope="module")
+def sg():
+    import swarm_amd
+    assert swarm_amd.device_count() > 0, "GPU tests need a HIP device"
+    return swarm_amd
+
+
+def rand_buf(rng, n_lines, alphabet=b"ab\x00\r\xff.", maxlen=20, p_empty=0.1, tail=True):
+    out = []
+    for _ in range(n_lines):
+        if rng.random() < p_empty:
+            out.append(b"")
+            continue
+        L = rng.randint(1, maxlen)
+        out.append(bytes(rng.choice(alphabet) for _ in range(L)))
+    b = b"\n".join(out)
+    return b + b"\n" if tail else b
+
+
+# ------------------------------------------------------------------ A3
+@pytest.mark.parametrize("size", [0, 1, 7, 8, 8191, 8192, 8193, 16384, 16385, 40000])
+@pytest.mark.parametrize("pattern", ["mixed", "nl_only", "no_nl", "tile_edges"])
+def test_lines_spans(sg, size, pattern):
+    rng = random.Random(size * 7 + len(pattern))
+    if pattern == "mixed":
+        b = bytes(rng.choice(b"xy\n\r") for _ in range(size))
+    elif pattern == "nl_only":
+        b = b"\n" * size
+    elif pattern == "no_nl":
+        b = bytes(rng.choice(b"pq") for _ in range(size))
+    else:
+        a = bytearray(b"z" * size)
+        for p in range(8191, size, 8192):
+            a[p] = 0x0A
+        b = bytes(a)
+    got = [tuple(x) for x in sg.lines(b).tolist()]
+    assert got == S.record_spans(b)
+
+
+# ------------------------------------------------------------------ A7
+@pytest.mark.parametrize("case", CU["dedup"], ids=lambda c: c["name"])
+def test_dedup_golden(sg, case):
+    assert sg.dedup(b64d(case["input"])) == b64d(case["sort_u"])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_dedup_random_bytes(sg, seed):
+    rng = random.Random(seed)
+    b = rand_buf(rng, 3000, maxlen=rng.choice([3, 9, 30]), tail=seed % 2 == 0)
+    assert sg.dedup(b) == S.dedup(b)
+
+
+def test_dedup_long_shared_prefixes(sg):
+    """Big groups of equal 7-byte prefixes force the radix refinement rounds."""
+    rng = random.Random(5)
+    pre = b"https://www.example.com/very/long/shared/prefix/"
+    recs = [pre + b"%d/%s" % (rng.randrange(300), rng.choice([b"a", b"b", b"ab", b""]))
+            for _ in range(20000)]
+    recs += [pre[:k] for k in range(0, len(pre), 3)]
+    rng.shuffle(recs)
+    b = b"\n".join(recs) + b"\n"
+    assert sg.dedup(b) == S.dedup(b)
+
+
+def test_dedup_identical_long_records(sg):
+    b = (b"q" * 100 + b"\n") * 5000 + (b"q" * 99 + b"\n") * 7 + (b"q" * 101 + b"\n") * 3
+    assert sg.dedup(b) == S.dedup(b)
+
+
+def test_dedup_subdomains_200k(sg):
+    from swarm_amd import corpus
+    buf, _ = corpus.subdomains(200_000, seed=99)
+    b = buf.tobytes()
+    assert sg.dedup(b) == S.dedup(b)
+
+
+@pytest.mark.parametrize("case", REF["a5_merge"], ids=lambda c: c["name"])
+def test_merge_dedup_reference_chunks(sg, case):
+    """A5 -> A7: the reference /raw merge order, then sort -u, from the chunk bodies."""
+    from swarm_amd import hooks
+    objs = {"%s/output/%s" % (case["scan_id"], k): b64d(v) for k, v in case["objects"].items()}
+    merged = S.merge_chunks(objs, case["scan_id"])
+    assert merged == b64d(case["raw"])
+    bodies = [objs[k] for k in hooks.merge_keys(objs.keys(), case["scan_id"])]
+    assert sg.dedup_chunks(bodies) == S.dedup(merged)
+
+
+# ------------------------------------------------------------------ A8
+@pytest.mark.parametrize("case", CU["diff"], ids=lambda c: c["name"])
+def test_diff_golden(sg, case):
+    assert sg.diff(b64d(case["cur"]), b64d(case["prior"])) == b64d(case["comm13"])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_dedup_diff_random(sg, seed):
+    rng = random.Random(100 + seed)
+    cur = rand_buf(rng, 4000, alphabet=b"abc\x00", maxlen=12)
+    prior_recs = sorted(set(S.parse_records(rand_buf(rng, 3000, alphabet=b"abc\x00", maxlen=12))))
+    prior = b"".join(r + b"\n" for r in prior_recs)
+    u, f = sg.dedup_diff(cur, prior)
+    eu, ef = S.dedup_diff(cur, prior)
+    assert u == eu and f == ef
+
+
+def test_diff_unsorted_prior(sg):
+    rng = random.Random(3)
+    cur = rand_buf(rng, 3000, alphabet=b"xyz", maxlen=9)
+    prior = rand_buf(rng, 3000, alphabet=b"xyz", maxlen=9)  # unsorted, duplicated
+    assert sg.diff(cur, prior) == S.diff(cur, prior)
+
+
+def test_dedup_diff_c1(sg):
+    """C1: 1M subdomains in 16 worker chunks merged in S3 key order, deduped, diffed."""
+    from swarm_amd import corpus, hooks
+    buf, ids = corpus.subdomains(1_000_000, seed=1234)
+    chunks = corpus.chunk_layout(buf, 16)
+    objs = {"c1_1/output/chunk_%d.txt" % i: ch.tobytes() for i, ch in enumerate(chunks)}
+    merged = S.merge_chunks(objs, "c1_1")
+    prior = corpus.prior_of(ids).tobytes()
+    u, f = hooks.completion_dedup_diff(objs, "c1_1", prior)
+    eu, ef = S.dedup_diff(merged, prior)
+    assert u == eu and f == ef
+
+
+# ------------------------------------------------------------------ device path + C2
+def test_device_path_torch_tensors(sg):
+    import torch
+    from swarm_amd import corpus
+    buf, ids = corpus.subdomains(300_000, seed=7)
+    prior = corpus.prior_of(ids)
+    d_cur = torch.from_numpy(buf).cuda()
+    d_pri = torch.from_numpy(prior).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    r = ctx.dedup_diff(d_cur.data_ptr(), d_cur.numel(), d_pri.data_ptr(), d_pri.numel())
+    u = ctx.to_bytes(r.uniq, r.uniq_bytes)
+    f = ctx.to_bytes(r.fresh, r.fresh_bytes)
+    eu, ef = S.dedup_diff(buf.tobytes(), prior.tobytes())
+    assert u == eu and f == ef
+    assert r.uniq_records == eu.count(b"\n") and r.fresh_records == ef.count(b"\n")
+    # misaligned device pointer (offset 3) still works
+    d_pad = torch.zeros(buf.size + 3, dtype=torch.uint8, device="cuda")
+    d_pad[3:] = d_cur
+    r2 = ctx.dedup_diff(d_pad.data_ptr() + 3, buf.size, d_pri.data_ptr(), d_pri.numel())
+    assert ctx.to_bytes(r2.fresh, r2.fresh_bytes) == ef
+    ctx.close()
+
+
+def _sorted_strict(recs_u8: np.ndarray) -> bool:
+    rows = recs_u8.tobytes().split(b"\n")[:-1]
+    return all(a < b for a, b in zip(rows, rows[1:]))
+
+
+def test_c2_full_size_properties(sg):
+    """C2 (10M lines): size-independent properties at the BASELINE size. Strictly sorted
+    output, unique count == numpy's, fresh == uniq minus prior (set identity), and the
+    output multiset is exactly the input's distinct records."""
+    import torch
+    from swarm_amd import corpus
+    buf, ids = corpus.subdomains(10_000_000, seed=1234)
+    prior = corpus.prior_of(ids)
+    d_cur = torch.from_numpy(buf).cuda()
+    d_pri = torch.from_numpy(prior).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    r = ctx.dedup_diff(d_cur.data_ptr(), d_cur.numel(), d_pri.data_ptr(), d_pri.numel())
+    u = ctx.to_bytes(r.uniq, r.uniq_bytes)
+    f = ctx.to_bytes(r.fresh, r.fresh_bytes)
+    n_unique_ids = np.unique(ids).size
+    assert r.in_records == 10_000_000
+    assert r.uniq_records == n_unique_ids  # every id renders to a distinct name
+    ur = u.split(b"\n")[:-1]
+    assert len(ur) == n_unique_ids and all(a < b for a, b in zip(ur, ur[1:]))
+    assert set(ur) == set(buf.tobytes().split(b"\n")[:-1])
+    pr = set(prior.tobytes().split(b"\n")[:-1])
+    fr = f.split(b"\n")[:-1]
+    assert fr == [x for x in ur if x not in pr]
+    ctx.close()
+
+
+# ------------------------------------------------------------------ partition (§8(e))
+@pytest.mark.parametrize("parts", [1, 2, 3, 8])
+def test_partition_matches_hash_oracle(sg, parts):
+    import torch
+    rng = random.Random(parts)
+    b = rand_buf(rng, 5000, alphabet=b"abcdef.", maxlen=25, tail=False)
+    recs = S.parse_records(b)
+    d = torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    dout = torch.empty(d.numel() + 1, dtype=torch.uint8, device="cuda")
+    pbytes, precs = ctx.partition(d.data_ptr(), d.numel(), parts, dout.data_ptr(), dout.numel())
+    out = ctx.to_bytes(dout.data_ptr(), sum(pbytes))
+    exp = [[] for _ in range(parts)]
+    for r in recs:
+        exp[part_of(py_hash64(r), parts)].append(r)
+    assert precs == [len(e) for e in exp]
+    assert pbytes == [sum(len(r) + 1 for r in e) for e in exp]
+    assert out == b"".join(r + b"\n" for e in exp for r in e)
+    ctx.close()
