@@ -98,30 +98,41 @@ def subdomains(n: int, seed: int = 1234, universe: int | None = None, chunk: int
     return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8), ids
 
 
-def prior_of(ids: np.ndarray) -> np.ndarray:
-    """The prior scan: sorted unique names of the drawn ids except ids % 10 == 0, serialized."""
-    u = np.unique(ids)
-    u = u[(u % np.uint64(10)) != 0]
-    mat, msk = render_names(u)
-    # sort rows bytewise: fixed-width rows padded with 0 sort like their byte strings
-    # because no name contains NUL and a shorter name is a prefix-padded-with-0.
+def name_rows(ids: np.ndarray) -> np.ndarray:
+    """Names of `ids` as left-compacted fixed-width rows (dtype S33). Rows compare like
+    their byte strings: no name contains NUL, and a shorter name is a 0-padded prefix."""
+    mat, msk = render_names(ids)
     W = mat.shape[1]
-    rows = np.where(msk, mat, 0)
-    # names are a concatenation of 3 segments; compact each row left first
-    comp = np.zeros_like(rows)
+    comp = np.zeros_like(mat)
     lens = msk.sum(axis=1)
-    flat = rows[msk]
-    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
-    idx = starts[:, None] + np.arange(W)[None, :]
+    flat = mat[msk]
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
     valid = np.arange(W)[None, :] < lens[:, None]
+    idx = starts[:, None] + np.arange(W)[None, :]
     comp[valid] = flat[idx[valid]]
-    v = comp.view(f"S{W}").reshape(-1)
-    order = np.argsort(v, kind="stable")
-    v_sorted = v[order]
-    keep = np.ones(v_sorted.size, dtype=bool)
-    keep[1:] = v_sorted[1:] != v_sorted[:-1]
-    sel = order[keep]
-    return _flatten(comp[sel], valid[sel])
+    return comp.view("S%d" % W).reshape(-1)
+
+
+def serialize_rows(rows: np.ndarray) -> np.ndarray:
+    """Fixed-width S rows -> '\n'-terminated byte buffer."""
+    W = rows.dtype.itemsize
+    mat = rows.view(np.uint8).reshape(-1, W)
+    return _flatten(mat, mat != 0)
+
+
+def sorted_unique_rows(ids: np.ndarray) -> np.ndarray:
+    return np.unique(name_rows(np.unique(ids)))
+
+
+def prior_rows(ids: np.ndarray) -> np.ndarray:
+    u = np.unique(ids)
+    return np.unique(name_rows(u[(u % np.uint64(10)) != 0]))
+
+
+def prior_of(ids: np.ndarray) -> np.ndarray:
+    """The prior scan: sort -u of the names of the drawn ids except ids % 10 == 0 (about
+    90 % of this scan's unique set), serialized."""
+    return serialize_rows(prior_rows(ids))
 
 
 def chunk_layout(lines_arr: np.ndarray, n_chunks: int) -> list:
