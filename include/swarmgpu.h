@@ -135,6 +135,9 @@ int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pat
 int sg_matcher_info(const sg_matcher *h, uint64_t *states, uint32_t *groups, uint32_t *n_pats);
 int sg_match(sg_matcher *h, const uint8_t *buf, size_t n, uint64_t *rec_idx, uint32_t *sig_id,
              size_t cap, size_t *n_hit);
+/* grep output: the matched records in input order, each '\n'-terminated. */
+int sg_match_lines(sg_matcher *h, const uint8_t *buf, size_t n, uint8_t *out, size_t cap,
+                   size_t *out_n);
 /* Device form: hits stay in HBM (context-owned), plus the matched lines serialized in
  * input order (grep output). */
 typedef struct sg_dev_hits {

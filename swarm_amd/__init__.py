@@ -4,8 +4,8 @@ diff), hand-written HIP for gfx950 behind a ctypes C-ABI (include/swarmgpu.h).
 Importing the package loads libswarmgpu.so and raises if it is missing: there is no CPU
 fallback on the product path.
 """
-from .api import (Context, dedup, dedup_chunks, dedup_diff, device_count, diff, hash64, lines,
-                  records)
+from .api import (Context, Matcher, dedup, dedup_chunks, dedup_diff, device_count, diff, hash64,
+                  lines, records)
 
-__all__ = ["Context", "dedup", "dedup_chunks", "dedup_diff", "device_count", "diff", "hash64",
-           "lines", "records"]
+__all__ = ["Context", "Matcher", "dedup", "dedup_chunks", "dedup_diff", "device_count", "diff",
+           "hash64", "lines", "records"]

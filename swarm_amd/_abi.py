@@ -28,7 +28,7 @@ EXPORTS = [
     "sg_lines",
     "sg_dedup", "sg_dedup_chunks", "sg_diff", "sg_dedup_diff", "sg_dev_dedup_diff",
     "sg_dev_partition", "sg_hash64", "sg_ac_compile", "sg_dfa_compile", "sg_matcher_info",
-    "sg_match", "sg_dev_match", "sg_free",
+    "sg_match", "sg_match_lines", "sg_dev_match", "sg_free",
 ]
 
 
@@ -88,6 +88,7 @@ def _load():
         "sg_dfa_compile": (C.c_int, [U8P, U32P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
         "sg_matcher_info": (C.c_int, [P, U64P, U32P, U32P]),
         "sg_match": (C.c_int, [P, U8P, SZ, U64P, U32P, SZ, SZP]),
+        "sg_match_lines": (C.c_int, [P, U8P, SZ, U8P, SZ, SZP]),
         "sg_dev_match": (C.c_int, [P, P, P, SZ, C.POINTER(DevHits)]),
         "sg_free": (None, [P]),
     }

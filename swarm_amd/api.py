@@ -93,6 +93,76 @@ def dedup_diff(cur, prior) -> Tuple[bytes, bytes]:
     return u[: un.value].tobytes(), f[: fn.value].tobytes()
 
 
+class Matcher:
+    """A4 signature matcher compiled to a GPU automaton.
+
+    kind="literal": Aho-Corasick, per record `sig in record` (LC_ALL=C grep -F [-i]).
+    kind="regex":   DFA set, per record `re.search(sig, record)` on bytes (subset in
+                    swarm_amd/csrc/sg_regex.hpp; unsupported constructs raise SGError).
+    """
+
+    def __init__(self, patterns: Sequence[bytes], kind: str = "literal", nocase: bool = False):
+        pats = [bytes(p) for p in patterns]
+        blob = b"".join(pats)
+        offs = np.zeros(len(pats) + 1, dtype=np.uint32)
+        np.cumsum([len(p) for p in pats], out=offs[1:])
+        a = np.frombuffer(blob, dtype=np.uint8) if blob else np.zeros(1, dtype=np.uint8)
+        self._h = C.c_void_p()
+        fn = lib.sg_ac_compile if kind == "literal" else lib.sg_dfa_compile
+        if kind not in ("literal", "regex"):
+            raise ValueError("kind must be 'literal' or 'regex'")
+        check(fn(a.ctypes.data, offs.ctypes.data_as(C.POINTER(C.c_uint32)), len(pats),
+                 _abi.SG_NOCASE if nocase else 0, C.byref(self._h)))
+        self.kind = kind
+        self.n = len(pats)
+
+    def close(self):
+        if self._h:
+            lib.sg_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        st, gr, n = C.c_uint64(), C.c_uint32(), C.c_uint32()
+        check(lib.sg_matcher_info(self._h, C.byref(st), C.byref(gr), C.byref(n)))
+        return {"states": st.value, "automata": gr.value, "patterns": n.value}
+
+    def match(self, buf) -> List[Tuple[int, int]]:
+        """(record index, signature index) for every signature occurring in a record,
+        sorted; record indices follow A3 (non-empty records in input order)."""
+        a = _view(buf)
+        cap = max(1024, a.size)
+        while True:
+            rec = np.empty(cap, dtype=np.uint64)
+            sig = np.empty(cap, dtype=np.uint32)
+            nh = C.c_size_t(0)
+            rc = lib.sg_match(self._h, _ptr(a), a.size, rec.ctypes.data_as(C.POINTER(C.c_uint64)),
+                              sig.ctypes.data_as(C.POINTER(C.c_uint32)), cap, C.byref(nh))
+            if rc == _abi.SG_E_CAP:
+                cap = nh.value
+                continue
+            check(rc)
+            return list(zip(rec[: nh.value].tolist(), sig[: nh.value].tolist()))
+
+    def match_lines(self, buf) -> bytes:
+        """grep output: matched records in input order, '\\n'-terminated."""
+        a = _view(buf)
+        out = np.empty(a.size + 1, dtype=np.uint8)
+        n = C.c_size_t(0)
+        check(lib.sg_match_lines(self._h, _ptr(a), a.size, out.ctypes.data, out.size, C.byref(n)))
+        return out[: n.value].tobytes()
+
+    def dev_match(self, ctx: "Context", d_buf: int, n: int) -> _abi.DevHits:
+        r = _abi.DevHits()
+        check(lib.sg_dev_match(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(r)))
+        return r
+
+
 def hash64(rec: bytes) -> int:
     a = _view(rec)
     return int(lib.sg_hash64(_ptr(a), a.size))

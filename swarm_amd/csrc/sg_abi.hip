@@ -152,11 +152,8 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
     uint64_t *K;
     uint32_t *V;
     SG_TRY(radix_sort(c, keys, v1, keys2, v2, R, 0, 8, true, &K, &V, "rs_pass_part"));
-    uint8_t *out;
     uint64_t bytes = 0;
-    SG_TRY(serialize(c, d_buf, L.starts, L.ends, V, nullptr, R, S_PART_OUT, &out, &bytes));
-    if (bytes > out_cap) { set_error("partition output capacity %zu < %llu", out_cap, (unsigned long long)bytes); return SG_E_CAP; }
-    if (bytes) SG_HIP(hipMemcpyAsync(d_out, out, bytes, hipMemcpyDeviceToDevice, c->stream));
+    SG_TRY(serialize_into(c, d_buf, L.starts, L.ends, V, R, d_out, out_cap, &bytes));
     uint64_t h[2 * 256];
     SG_TRY(ctx_readback(c, h, cnt, 2 * parts * 8));
     for (uint32_t q = 0; q < parts; ++q) {

@@ -221,13 +221,62 @@ __device__ __forceinline__ int rec_cmp(const uint8_t *buf_a, uint32_t sa, uint32
 // 63..8 (zero past the record end) and tag = min(remaining, 8) in bits 7..0. Ordering
 // of (key) == bytewise ordering of the suffixes when the tags differ or tag < 8;
 // equal keys with tag 8 need the next chunk.
+// Word-granular: at most two naturally aligned 8-byte loads (buf must be 8-byte aligned;
+// an aligned word that holds an in-bounds byte never crosses a page).
 __device__ __forceinline__ uint64_t chunk_key(const uint8_t *buf, uint32_t s, uint32_t e, uint32_t off) {
-    uint32_t rem = (e - s > off) ? (e - s - off) : 0u;
-    uint32_t take = rem < 7u ? rem : 7u;
-    uint64_t k = 0;
-    const uint8_t *p = buf + s + off;
-    for (uint32_t j = 0; j < take; ++j) k |= (uint64_t)p[j] << (56 - 8 * j);
-    return k | (uint64_t)(rem < 8u ? rem : 8u);
+    const uint32_t len = e - s;
+    const uint32_t rem = (len > off) ? (len - off) : 0u;
+    const uint64_t tag = rem < 8u ? rem : 8u;
+    if (rem == 0) return 0;
+    const uint32_t take = rem < 7u ? rem : 7u;
+    const uint32_t p = s + off;
+    const uint32_t a = p & ~7u;
+    const uint32_t sh = (p - a) * 8u;
+    uint64_t v = *reinterpret_cast<const uint64_t *>(buf + a) >> sh;
+    if (p + take > a + 8u) v |= *reinterpret_cast<const uint64_t *>(buf + a + 8) << (64u - sh);
+    v &= (1ull << (8u * take)) - 1ull;  // take <= 7
+    return (__builtin_bswap64(v) & ~0xffull) | tag;
+}
+
+// Bytes [p, p+t) (t <= 8) little-endian in a u64, zero above; buf 8-byte aligned.
+__device__ __forceinline__ uint64_t load_le(const uint8_t *buf, uint32_t p, uint32_t t) {
+    const uint32_t a = p & ~7u;
+    const uint32_t sh = (p - a) * 8u;
+    uint64_t v = *reinterpret_cast<const uint64_t *>(buf + a) >> sh;
+    if (p + t > a + 8u) v |= *reinterpret_cast<const uint64_t *>(buf + a + 8) << (64u - sh);
+    return t >= 8u ? v : (v & ((1ull << (8u * t)) - 1ull));
+}
+
+// Byte equality of two records from offset `off` (lengths must match). Loads of a
+// 32-byte block are issued together; one branch per block.
+__device__ __forceinline__ bool rec_equal(const uint8_t *ba, uint32_t sa, uint32_t ea, const uint8_t *bb,
+                                          uint32_t sb, uint32_t eb, uint32_t off) {
+    const uint32_t la = ea - sa;
+    if (la != eb - sb) return false;
+    for (uint32_t o = off; o < la; o += 32) {
+        uint64_t d = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t oo = o + 8 * q;
+            if (oo < la) {
+                const uint32_t t = (la - oo) < 8u ? (la - oo) : 8u;
+                d |= load_le(ba, sa + oo, t) ^ load_le(bb, sb + oo, t);
+            }
+        }
+        if (d) return false;
+    }
+    return true;
+}
+
+// Bytewise compare of the suffixes from `off` by 7-byte chunk keys (memcmp-then-length).
+__device__ __forceinline__ int rec_cmp_k(const uint8_t *ba, uint32_t sa, uint32_t ea, const uint8_t *bb,
+                                         uint32_t sb, uint32_t eb, uint32_t off) {
+    for (;;) {
+        const uint64_t x = chunk_key(ba, sa, ea, off), y = chunk_key(bb, sb, eb, off);
+        if (x != y) return x < y ? -1 : 1;
+        if ((x & 0xffu) < 8u) return 0;
+        off += 7;
+    }
 }
 
 }  // namespace sg

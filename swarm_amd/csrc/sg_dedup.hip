@@ -22,7 +22,8 @@ namespace sg {
 const SlotSet CUR_SLOTS = {S_STARTS, S_ENDS, S_KEYS, S_KEYS2, S_VALS, S_VALS2, S_UNIQ, S_LB};
 const SlotSet PRIOR_SLOTS = {S_P_STARTS, S_P_ENDS, S_P_KEYS, S_P_KEYS2, S_P_VALS, S_P_VALS2, S_P_UNIQ, S_P_FLAG};
 
-constexpr uint32_t SMALL_GROUP = 8;
+constexpr uint32_t EQ_GROUP = 4096;
+constexpr uint32_t WAVE_GROUP = 64;
 
 // ------------------------------------------------------------------ launch helpers
 template <class Pred>
@@ -60,7 +61,7 @@ static int run_scan64(sg_ctx *c, const char *name, Fn fn, uint32_t n, uint64_t *
     return SG_OK;
 }
 
-static inline uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap = 65535u * 4) {
+static inline uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap = 0x7fffffffu) {
     uint64_t g = (n + block - 1) / block;
     if (g == 0) g = 1;
     return (uint32_t)(g < cap ? g : cap);
@@ -108,15 +109,12 @@ struct RoundGroupPred {
 
 struct BigGroupPred {
     const uint32_t *GS, *GE;
-    __device__ uint32_t operator()(uint32_t i) const { return (GE[i] - GS[i] + 1u > SMALL_GROUP) ? 1u : 0u; }
+    __device__ uint32_t operator()(uint32_t i) const { return (GE[i] - GS[i] + 1u > WAVE_GROUP) ? 1u : 0u; }
 };
 
-struct RecLenFn {
-    const uint32_t *starts, *ends, *recs;
-    __device__ uint64_t operator()(uint32_t i) const {
-        const uint32_t r = recs[i];
-        return (uint64_t)(ends[r] - starts[r]) + 1ull;
-    }
+struct DenseLenFn {
+    const uint32_t *L;
+    __device__ uint64_t operator()(uint32_t i) const { return L[i]; }
 };
 
 struct GroupSizeFn {
@@ -127,49 +125,72 @@ struct GroupSizeFn {
     }
 };
 
-// ------------------------------------------------------------------ kernels
-// Groups of <= 8 records sharing `off` bytes: rank by full compare, stable; duplicates
-// (equal to an earlier member) lose uniq.
-__global__ __launch_bounds__(256) void k_refine_small(const uint8_t *__restrict__ buf,
-                                                      const uint32_t *__restrict__ starts,
-                                                      const uint32_t *__restrict__ ends,
-                                                      const uint32_t *__restrict__ GS,
-                                                      const uint32_t *__restrict__ GE, uint32_t G,
-                                                      uint32_t *V, uint8_t *uniq, uint32_t off) {
+__device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint32_t *starts, const uint32_t *ends,
+                                            uint64_t ka, uint32_t ra, uint64_t kb, uint32_t rb, uint32_t off) {
+    if (ka != kb) return ka < kb ? -1 : 1;
+    if ((ka & 0xffu) < 8u) return 0;
+    return rec_cmp_k(buf, starts[ra], ends[ra], buf, starts[rb], ends[rb], off + 7);
+}
+
+// ------------------------------------------------------------------ refinement kernels
+// Every group (records sharing `off` bytes, >= 2 members): one thread checks whether all
+// members are byte-identical to the first (the common case: duplicates). If so the first
+// stays unique and the rest are duplicates, order unchanged. Otherwise (or above
+// EQ_GROUP members) the group is flagged for ranking.
+__global__ __launch_bounds__(256) void k_refine_eq(const uint8_t *__restrict__ buf,
+                                                   const uint32_t *__restrict__ starts,
+                                                   const uint32_t *__restrict__ ends,
+                                                   const uint32_t *__restrict__ GS,
+                                                   const uint32_t *__restrict__ GE, uint32_t G,
+                                                   const uint32_t *__restrict__ V, uint8_t *uniq,
+                                                   uint32_t off, uint8_t *unresolved) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const uint32_t s = GS[g], k = GE[g] - s + 1u;
-    if (k > SMALL_GROUP) return;
-    uint32_t m[SMALL_GROUP], rs[SMALL_GROUP], re[SMALL_GROUP], rank[SMALL_GROUP];
-    bool dup[SMALL_GROUP];
-#pragma unroll
-    for (uint32_t a = 0; a < SMALL_GROUP; ++a) {
-        if (a < k) {
-            m[a] = V[s + a];
-            rs[a] = starts[m[a]];
-            re[a] = ends[m[a]];
-        }
-        rank[a] = 0;
-        dup[a] = false;
-    }
-#pragma unroll
-    for (uint32_t a = 0; a < SMALL_GROUP; ++a) {
-#pragma unroll
-        for (uint32_t b = a + 1; b < SMALL_GROUP; ++b) {
-            if (b < k) {
-                const int cmp = rec_cmp(buf, rs[a], re[a], buf, rs[b], re[b], off);
-                // stable: a precedes b when a <= b
-                if (cmp <= 0) rank[b]++; else rank[a]++;
-                if (cmp == 0) dup[b] = true;
-            }
+    bool same = k <= EQ_GROUP;
+    if (same) {
+        const uint32_t m0 = V[s];
+        const uint32_t s0 = starts[m0], e0 = ends[m0];
+        for (uint32_t a = 1; a < k; ++a) {
+            const uint32_t m = V[s + a];
+            if (!rec_equal(buf, s0, e0, buf, starts[m], ends[m], off)) { same = false; break; }
         }
     }
-#pragma unroll
-    for (uint32_t a = 0; a < SMALL_GROUP; ++a) {
-        if (a < k) {
-            V[s + rank[a]] = m[a];
-            uniq[s + rank[a]] = dup[a] ? 0 : 1;
+    if (same)
+        for (uint32_t a = 1; a < k; ++a) uniq[s + a] = 0;
+    unresolved[g] = same ? 0 : 1;
+}
+
+// Unresolved groups of <= 64 records: one wave per group, one member per lane; each lane counts the
+// members that precede it (stable), duplicates are members equal to an earlier one.
+__global__ __launch_bounds__(256) void k_refine_wave(const uint8_t *__restrict__ buf,
+                                                     const uint32_t *__restrict__ starts,
+                                                     const uint32_t *__restrict__ ends,
+                                                     const uint32_t *__restrict__ GS,
+                                                     const uint32_t *__restrict__ GE, uint32_t G,
+                                                     uint32_t *V, uint8_t *uniq, uint32_t off) {
+    const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = lane_id();
+    if (g >= G) return;
+    const uint32_t s = GS[g], k = GE[g] - s + 1u;
+    if (k > WAVE_GROUP) return;
+    const bool act = lane < k;
+    const uint32_t m = act ? V[s + lane] : 0u;
+    const uint64_t key = act ? chunk_key(buf, starts[m], ends[m], off) : ~0ull;
+    uint32_t rank = 0;
+    bool dup = false;
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint64_t kb = __shfl(key, (int)j, 64);
+        const uint32_t mb = __shfl(m, (int)j, 64);
+        if (act && j != lane) {
+            const int c = key_cmp_full(buf, starts, ends, key, m, kb, mb, off);
+            if (c > 0 || (c == 0 && j < lane)) rank++;
+            if (c == 0 && j < lane) dup = true;
         }
+    }
+    if (act) {
+        V[s + rank] = m;
+        uniq[s + rank] = dup ? 0 : 1;
     }
 }
 
@@ -196,6 +217,15 @@ __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
     RK[j] = chunk_key(buf, starts[r], ends[r], off);
     RG[j] = lo;
     RP[j] = pos;
+}
+
+__global__ void k_gather_pair(const uint32_t *__restrict__ idx, const uint32_t *__restrict__ A,
+                              const uint32_t *__restrict__ B, uint32_t n, uint32_t *A2, uint32_t *B2) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t q = idx[i];
+    A2[i] = A[q];
+    B2[i] = B[q];
 }
 
 __global__ void k_gid_keys(const uint32_t *__restrict__ RG, const uint32_t *__restrict__ perm,
@@ -228,32 +258,92 @@ __global__ void k_pos_of(const uint32_t *__restrict__ idx, const uint32_t *__res
     if (i < n) out[i] = RP[idx[i]];
 }
 
-__global__ void k_gather_u32(const uint32_t *__restrict__ src, const uint32_t *__restrict__ idx,
-                             uint32_t n, uint32_t *out) {
+// ------------------------------------------------------------------ gathers / output
+// Selected positions -> record id, key0 and serialized length (len + 1) per record.
+__global__ void k_gather_sel(const uint32_t *__restrict__ sel, const uint32_t *__restrict__ V,
+                             const uint64_t *__restrict__ K, const uint32_t *__restrict__ starts,
+                             const uint32_t *__restrict__ ends, uint32_t n, uint32_t *UR, uint64_t *UK,
+                             uint32_t *UL) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = src[idx[i]];
+    if (i >= n) return;
+    const uint32_t p = sel[i];
+    const uint32_t r = V ? V[p] : p;
+    UR[i] = r;
+    if (UK) UK[i] = K[p];
+    UL[i] = ends[r] - starts[r] + 1u;
 }
 
-__global__ void k_gather_u64(const uint64_t *__restrict__ src, const uint32_t *__restrict__ idx,
-                             uint32_t n, uint64_t *out) {
+__global__ void k_gather_rl(const uint32_t *__restrict__ idx, const uint32_t *__restrict__ R,
+                            const uint32_t *__restrict__ L, uint32_t n, uint32_t *R2, uint32_t *L2) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = src[idx[i]];
+    if (i >= n) return;
+    const uint32_t q = idx[i];
+    R2[i] = R[q];
+    L2[i] = L[q];
 }
 
-// Copy records (list order) to out at offs[i]; each followed by '\n'.
+constexpr uint32_t CP_WAVE_BYTES = 4096;
+
+// Records (list order) -> out at offs[i], each '\n'-terminated. Each wave stages its 64
+// records' bytes in LDS at their output positions (aligned word loads from the source),
+// then writes the wave's output span with 16-byte stores; spans wider than the wave's
+// LDS window fall back to per-lane byte copies.
 __global__ __launch_bounds__(256) void k_copy_records(const uint8_t *__restrict__ buf,
                                                       const uint32_t *__restrict__ starts,
                                                       const uint32_t *__restrict__ ends,
                                                       const uint32_t *__restrict__ recs,
                                                       const uint64_t *__restrict__ offs, uint32_t n,
                                                       uint8_t *__restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t r = recs[i];
-    const uint32_t s = starts[r], e = ends[r];
-    uint8_t *d = out + offs[i];
-    for (uint32_t p = s; p < e; ++p) *d++ = buf[p];
-    *d = 0x0a;
+    __shared__ __attribute__((aligned(16))) uint8_t s_buf[4][CP_WAVE_BYTES];
+    const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t wfirst = (blockIdx.x * 4 + wid) * 64u;
+    if (wfirst >= n) return;
+    const uint32_t i = wfirst + lane;
+    const bool act = i < n;
+    const uint32_t r = act ? recs[i] : 0u;
+    const uint32_t s = act ? starts[r] : 0u;
+    const uint32_t len = act ? ends[r] - s : 0u;
+    const uint64_t o = act ? offs[i] : 0ull;
+    const uint32_t last = (n - wfirst) < 64u ? (n - wfirst - 1u) : 63u;
+    const uint64_t o0 = __shfl(o, 0, 64);
+    const uint64_t oend = __shfl(o + len + 1u, (int)last, 64);
+    const uint64_t base = o0 & ~15ull;
+    const uint64_t span = oend - base;
+    if (span <= CP_WAVE_BYTES) {
+        uint8_t *L = s_buf[wid];
+        if (act) {
+            const uint32_t lo = (uint32_t)(o - base);
+            const uint32_t e = s + len;
+            for (uint32_t w = s & ~3u; w < e; w += 4) {
+                const uint32_t x = *reinterpret_cast<const uint32_t *>(buf + w);
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) {
+                    const uint32_t p = w + b;
+                    if (p >= s && p < e) L[lo + (p - s)] = (uint8_t)(x >> (8 * b));
+                }
+            }
+            L[lo + len] = 0x0a;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nch = (uint32_t)((span + 15) / 16);
+        for (uint32_t ch = lane; ch < nch; ch += 64) {
+            const uint64_t ga = base + 16ull * ch;
+            if (ga >= o0 && ga + 16 <= oend) {
+                *reinterpret_cast<uint4 *>(out + ga) = *reinterpret_cast<const uint4 *>(L + 16 * ch);
+            } else {
+#pragma unroll
+                for (uint32_t b = 0; b < 16; ++b) {
+                    const uint64_t a = ga + b;
+                    if (a >= o0 && a < oend) out[a] = L[16 * ch + b];
+                }
+            }
+        }
+    } else if (act) {
+        uint8_t *d = out + o;
+        for (uint32_t p = 0; p < len; ++p) d[p] = buf[s + p];
+        d[len] = 0x0a;
+    }
 }
 
 // Prior check: flag[0] = 1 if records are not strictly increasing.
@@ -262,57 +352,87 @@ __global__ void k_check_sorted(const uint8_t *__restrict__ buf, const uint32_t *
                                uint32_t n, uint32_t *flag) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x + 1;
     if (i >= n) return;
-    const uint64_t a = K[i - 1], b = K[i];
-    bool bad;
-    if (a != b) bad = a > b;
-    else if ((a & 0xffu) < 8u) bad = true;  // identical records
-    else bad = rec_cmp(buf, starts[i - 1], ends[i - 1], buf, starts[i], ends[i], 7) >= 0;
-    if (bad) atomicOr(flag, 1u);
+    if (key_cmp_full(buf, starts, ends, K[i - 1], i - 1, K[i], i, 0) >= 0) atomicOr(flag, 1u);
 }
 
-__device__ __forceinline__ int cmp_rec_key(const uint8_t *ub, uint32_t us, uint32_t ue, uint64_t uk,
-                                           const uint8_t *pb, uint32_t ps, uint32_t pe, uint64_t pk) {
-    if (uk != pk) return uk < pk ? -1 : 1;
-    if ((uk & 0xffu) < 8u) return 0;
-    return rec_cmp(ub, us, ue, pb, ps, pe, 7);
+// ------------------------------------------------------------------ diff (merge path)
+struct RecSet {
+    const uint8_t *buf;
+    const uint32_t *st, *en;
+    const uint32_t *ids;  // position -> record id (null = identity)
+    const uint64_t *K;    // key0 per position
+    uint32_t n;
+    __device__ uint32_t id(uint32_t i) const { return ids ? ids[i] : i; }
+};
+
+__device__ __forceinline__ int set_cmp(const RecSet &A, uint64_t ka, uint32_t ra, const RecSet &B, uint64_t kb,
+                                       uint32_t rb) {
+    if (ka != kb) return ka < kb ? -1 : 1;
+    if ((ka & 0xffu) < 8u) return 0;
+    return rec_cmp_k(A.buf, A.st[ra], A.en[ra], B.buf, B.st[rb], B.en[rb], 7);
 }
 
-// fresh[i] = unique cur record i (sorted) is absent from the prior (sorted unique).
-__global__ __launch_bounds__(256) void k_diff_mark(
-    const uint8_t *__restrict__ cbuf, const uint32_t *__restrict__ cst, const uint32_t *__restrict__ cen,
-    const uint32_t *__restrict__ UR, const uint64_t *__restrict__ UK, uint32_t U,
-    const uint8_t *__restrict__ pbuf, const uint32_t *__restrict__ pst, const uint32_t *__restrict__ pen,
-    const uint32_t *__restrict__ PR, const uint64_t *__restrict__ PK, uint32_t P, uint8_t *fresh) {
-    __shared__ uint32_t s_lo, s_hi;
-    const uint32_t i0 = blockIdx.x * blockDim.x;
-    const uint32_t i = i0 + threadIdx.x;
-    auto prec = [&](uint32_t j) { return PR ? PR[j] : j; };
-    auto lower = [&](uint32_t r, uint64_t k, uint32_t lo, uint32_t hi) {
-        const uint32_t us = cst[r], ue = cen[r];
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            const uint32_t q = prec(mid);
-            if (cmp_rec_key(cbuf, us, ue, k, pbuf, pst[q], pen[q], PK[mid]) > 0) lo = mid + 1;
-            else hi = mid;
-        }
-        return lo;
-    };
-    if (threadIdx.x == 0) {
-        const uint32_t last = (i0 + blockDim.x <= U) ? i0 + blockDim.x - 1 : U - 1;
-        s_lo = lower(UR[i0], UK[i0], 0, P);
-        s_hi = lower(UR[last], UK[last], s_lo, P);
+constexpr uint32_t MP_TILE = 2048;
+
+// Merge-path split of diagonal t*MP_TILE over (U, P), U first on ties: split[t] = i.
+__global__ void k_merge_split(RecSet U, RecSet P, uint32_t ntiles, uint32_t *split) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint64_t tot = (uint64_t)U.n + P.n;
+    const uint64_t d64 = (uint64_t)t * MP_TILE < tot ? (uint64_t)t * MP_TILE : tot;
+    const uint32_t d = (uint32_t)d64;
+    uint32_t lo = d > P.n ? d - P.n : 0u, hi = d < U.n ? d : U.n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint32_t j = d - mid - 1;
+        if (set_cmp(U, U.K[mid], U.id(mid), P, P.K[j], P.id(j)) <= 0) lo = mid + 1;
+        else hi = mid;
+    }
+    split[t] = lo;
+}
+
+// fresh[i] = 1 if U[i] is absent from P. Inside the tile's P range (keys staged in LDS)
+// find the run of P keys equal to U[i]'s key0: a tag < 8 key is the whole record, so the
+// run decides; a tag-8 run (usually one record) is checked with a wide byte compare. The
+// run may continue past the tile into P[j1...] (ties go to U first in the merge order).
+__global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uint32_t *__restrict__ split,
+                                                   uint8_t *fresh) {
+    __shared__ uint64_t s_k[MP_TILE];
+    __shared__ uint32_t s_r[MP_TILE];
+    const uint32_t t = blockIdx.x;
+    const uint64_t tot = (uint64_t)U.n + P.n;
+    const uint32_t d0 = (uint32_t)((uint64_t)t * MP_TILE);
+    const uint32_t d1 = (uint32_t)((uint64_t)(t + 1) * MP_TILE < tot ? (uint64_t)(t + 1) * MP_TILE : tot);
+    const uint32_t i0 = split[t], i1 = split[t + 1];
+    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
+    const uint32_t np = j1 - j0;
+    for (uint32_t q = threadIdx.x; q < np; q += blockDim.x) {
+        s_k[q] = P.K[j0 + q];
+        s_r[q] = P.id(j0 + q);
     }
     __syncthreads();
-    if (i >= U) return;
-    const uint32_t r = UR[i];
-    const uint64_t k = UK[i];
-    const uint32_t j = lower(r, k, s_lo, s_hi);
-    bool present = false;
-    if (j < P) {
-        const uint32_t q = prec(j);
-        present = cmp_rec_key(cbuf, cst[r], cen[r], k, pbuf, pst[q], pen[q], PK[j]) == 0;
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+        const uint64_t ku = U.K[i];
+        uint32_t lo = 0, hi = np;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_k[mid] < ku) lo = mid + 1;
+            else hi = mid;
+        }
+        bool present = false;
+        const bool whole = (ku & 0xffu) < 8u;
+        uint32_t ru = 0, us = 0, ue = 0;
+        if (!whole) { ru = U.id(i); us = U.st[ru]; ue = U.en[ru]; }
+        for (uint32_t q = j0 + lo; q < P.n; ++q) {
+            const uint32_t lq = q - j0;
+            const uint64_t kp = (lq < np) ? s_k[lq] : P.K[q];
+            if (kp != ku) break;
+            if (whole) { present = true; break; }
+            const uint32_t rp = (lq < np) ? s_r[lq] : P.id(q);
+            if (rec_equal(U.buf, us, ue, P.buf, P.st[rp], P.en[rp], 7)) { present = true; break; }
+        }
+        fresh[i] = present ? 0 : 1;
     }
-    fresh[i] = present ? 0 : 1;
 }
 
 // ------------------------------------------------------------------ host pipeline
@@ -320,18 +440,48 @@ int select_flags(sg_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out_idx,
     return run_select2(c, "select", FlagPred{flags}, n, out_idx, (uint32_t *)nullptr, count, nullptr);
 }
 
-int serialize(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
-              const uint32_t *recs, const uint32_t * /*map*/, uint32_t count, int out_slot,
-              uint8_t **d_out, uint64_t *bytes) {
+// recs/lens: record ids and serialized lengths (len + 1) in output order.
+static int serialize_dense(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+                           const uint32_t *recs, const uint32_t *lens, uint32_t count, int out_slot,
+                           uint8_t *dst, size_t dst_cap, uint8_t **d_out, uint64_t *bytes) {
     *bytes = 0;
     uint64_t *offs;
     SG_TRY(slot(c, S_OFFS, (size_t)count + 1, &offs));
     uint64_t total = 0;
-    SG_TRY(run_scan64(c, "scan_len", RecLenFn{starts, ends, recs}, count, offs, &total));
-    SG_TRY(slot(c, out_slot, (size_t)total + 16, d_out));
+    SG_TRY(run_scan64(c, "scan_len", DenseLenFn{lens}, count, offs, &total));
+    if (dst) {
+        if (total > dst_cap) { set_error("output capacity %zu < %llu", dst_cap, (unsigned long long)total); return SG_E_CAP; }
+        *d_out = dst;
+    } else {
+        SG_TRY(slot(c, out_slot, (size_t)total + 16, d_out));
+    }
     if (count) SG_LAUNCH(c, "copy_records", k_copy_records, grid_for(count, 256), 256, 0, d_buf, starts, ends, recs, offs, count, *d_out);
     *bytes = total;
     return SG_OK;
+}
+
+__global__ void k_lens_of(const uint32_t *__restrict__ recs, const uint32_t *__restrict__ starts,
+                          const uint32_t *__restrict__ ends, uint32_t n, uint32_t *L) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { const uint32_t r = recs[i]; L[i] = ends[r] - starts[r] + 1u; }
+}
+
+int serialize(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+              const uint32_t *recs, const uint32_t * /*map*/, uint32_t count, int out_slot,
+              uint8_t **d_out, uint64_t *bytes) {
+    uint32_t *L;
+    SG_TRY(slot(c, S_M_TMP2, (size_t)count + 1, &L));
+    if (count) SG_LAUNCH(c, "lens", k_lens_of, grid_for(count, 256), 256, 0, recs, starts, ends, count, L);
+    return serialize_dense(c, d_buf, starts, ends, recs, L, count, out_slot, nullptr, 0, d_out, bytes);
+}
+
+int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+                   const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes) {
+    uint32_t *L;
+    SG_TRY(slot(c, S_M_TMP2, (size_t)count + 1, &L));
+    if (count) SG_LAUNCH(c, "lens", k_lens_of, grid_for(count, 256), 256, 0, recs, starts, ends, count, L);
+    uint8_t *o;
+    return serialize_dense(c, d_buf, starts, ends, recs, L, count, 0, dst, dst_cap, &o, bytes);
 }
 
 int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet &ss, SortedSet *out) {
@@ -362,13 +512,27 @@ int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet 
 
     uint32_t off = 7;
     while (G > 0) {
-        SG_LAUNCH(c, "refine_small", k_refine_small, grid_for(G, 256), 256, 0, d_buf, L.starts, L.ends, GS, GE, G, V, uniq, off);
-        // big groups -> a radix round on the next chunk
+        uint8_t *unres;
+        SG_TRY(slot(c, S_M_TMP, (size_t)G + 16, &unres));
+        SG_LAUNCH(c, "refine_eq", k_refine_eq, grid_for(G, 256), 256, 0, d_buf, L.starts, L.ends, GS, GE, G, V, uniq, off, unres);
+        uint32_t *ulist;
+        SG_TRY(slot(c, S_SEL, (size_t)G + 16, &ulist));
+        uint32_t Ux = 0;
+        SG_TRY(select_flags(c, unres, G, ulist, &Ux));
+        if (Ux == 0) break;
+        uint32_t *GS2, *GE2;
+        SG_TRY(slot(c, S_R_GID, (size_t)Ux + 16, &GS2));
+        SG_TRY(slot(c, S_R_POS, (size_t)Ux + 16, &GE2));
+        SG_LAUNCH(c, "gather_groups", k_gather_pair, grid_for(Ux, 256), 256, 0, ulist, GS, GE, Ux, GS2, GE2);
+        SG_LAUNCH(c, "refine_wave", k_refine_wave, grid_for(Ux, 4), 256, 0, d_buf, L.starts, L.ends, GS2, GE2, Ux, V, uniq, off);
+        // unresolved groups above one wave -> a radix round on the next chunk
         uint32_t *big;
-        SG_TRY(slot(c, S_SEL, G + 16, &big));
+        SG_TRY(slot(c, S_SEL, Ux + 16, &big));
         uint32_t B = 0;
-        SG_TRY(run_select2(c, "select_big", BigGroupPred{GS, GE}, G, big, (uint32_t *)nullptr, &B, nullptr));
+        SG_TRY(run_select2(c, "select_big", BigGroupPred{GS2, GE2}, Ux, big, (uint32_t *)nullptr, &B, nullptr));
         if (B == 0) break;
+        SG_HIP(hipMemcpyAsync(GS, GS2, (size_t)Ux * 4, hipMemcpyDeviceToDevice, c->stream));
+        SG_HIP(hipMemcpyAsync(GE, GE2, (size_t)Ux * 4, hipMemcpyDeviceToDevice, c->stream));
         uint64_t *goff;
         SG_TRY(slot(c, S_R_OFF, (size_t)B + 1, &goff));
         uint64_t M64 = 0;
@@ -395,20 +559,17 @@ int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet 
         uint64_t *GK2 = (GK == RK) ? RK2 : RK;
         uint64_t *FKs;
         uint32_t *perm2;
-        // GK2 is the key currently holding sorted chunk keys (no longer needed).
         SG_TRY(radix_sort(c, GK, perm, GK2, pv_alt, M, 0, gbits, false, &FKs, &perm2, "rs_pass_refine"));
-        // T and FK into the arrays not holding perm2
         T = (perm2 == perm) ? pv_alt : perm;
         uint64_t *FK = (FKs == GK) ? GK2 : GK;
         SG_LAUNCH(c, "round_gather", k_round_gather, grid_for(M, 256), 256, 0, d_buf, L.starts, L.ends, V, RP, perm2, M, off, T, FK);
         SG_LAUNCH(c, "round_scatter", k_round_scatter, grid_for(M, 256), 256, 0, T, RP, M, V);
-        // sub-groups: RG is the group index of final row i as well (same row ranges)
-        uint32_t *NS = perm2, *NE = T;  // reuse (T consumed by scatter above; perm2 no longer needed)
-        // NOTE: NS/NE are written after the scatter kernel on the same stream.
+        // sub-groups: RG is the group index of final row i as well (same row ranges);
+        // perm2/T are free again after the scatter (same stream)
+        uint32_t *NS = perm2, *NE = T;
         uint32_t G3 = 0, G4 = 0;
         SG_TRY(run_select2(c, "round_mark", RoundGroupPred{FK, RG, RP, uniq, M}, M, NS, NE, &G3, &G4));
         if (G3 != G4) { set_error("round group mismatch"); return SG_E_HIP; }
-        // rows -> global positions into GS/GE
         if (G3) {
             SG_LAUNCH(c, "round_pos", k_pos_of, grid_for(G3, 256), 256, 0, NS, RP, G3, GS);
             SG_LAUNCH(c, "round_pos", k_pos_of, grid_for(G3, 256), 256, 0, NE, RP, G3, GE);
@@ -424,11 +585,12 @@ struct UniqView {
     Lines L;
     uint32_t *UR = nullptr;  // record ids, byte order (null = identity 0..U-1)
     uint64_t *UK = nullptr;  // key0 per unique record
+    uint32_t *UL = nullptr;  // serialized length per unique record (may be null)
     uint32_t U = 0;
 };
 
 static int unique_view(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, int ur_slot,
-                       int uk_slot, bool trust_sorted, UniqView *uv) {
+                       int uk_slot, int ul_slot, bool trust_sorted, UniqView *uv) {
     SG_TRY(run_lines(c, d_buf, n, ss, &uv->L));
     const uint32_t R = uv->L.n_rec;
     if (trust_sorted && R > 1) {
@@ -443,6 +605,7 @@ static int unique_view(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSe
     if (trust_sorted) {
         uv->UR = nullptr;
         uv->UK = uv->L.keys;
+        uv->UL = nullptr;
         uv->U = R;
         return SG_OK;
     }
@@ -454,10 +617,8 @@ static int unique_view(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSe
     SG_TRY(select_flags(c, S.uniq, R, sel, &U));
     SG_TRY(slot(c, ur_slot, (size_t)U + 1, &uv->UR));
     SG_TRY(slot(c, uk_slot, (size_t)U + 1, &uv->UK));
-    if (U) {
-        SG_LAUNCH(c, "gather", k_gather_u32, grid_for(U, 256), 256, 0, S.recs, sel, U, uv->UR);
-        SG_LAUNCH(c, "gather", k_gather_u64, grid_for(U, 256), 256, 0, S.keys, sel, U, uv->UK);
-    }
+    SG_TRY(slot(c, ul_slot, (size_t)U + 1, &uv->UL));
+    if (U) SG_LAUNCH(c, "gather_uniq", k_gather_sel, grid_for(U, 256), 256, 0, sel, S.recs, S.keys, uv->L.starts, uv->L.ends, U, uv->UR, uv->UK, uv->UL);
     uv->U = U;
     return SG_OK;
 }
@@ -466,13 +627,11 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
                    uint64_t n_prior, bool want_fresh, sg_dev_result *res) {
     *res = sg_dev_result{};
     UniqView cu;
-    SG_TRY(unique_view(c, d_cur, n_cur, CUR_SLOTS, S_CUR_UR, S_CUR_UK, false, &cu));
-    uint32_t *UR = cu.UR;
-    uint64_t *UK = cu.UK;
+    SG_TRY(unique_view(c, d_cur, n_cur, CUR_SLOTS, S_CUR_UR, S_CUR_UK, S_FRESH_IDX, false, &cu));
     res->in_records = cu.L.n_rec;
     uint8_t *uout;
     uint64_t ubytes = 0;
-    SG_TRY(serialize(c, d_cur, cu.L.starts, cu.L.ends, UR, nullptr, cu.U, S_OUT_UNIQ, &uout, &ubytes));
+    SG_TRY(serialize_dense(c, d_cur, cu.L.starts, cu.L.ends, cu.UR, cu.UL, cu.U, S_OUT_UNIQ, nullptr, 0, &uout, &ubytes));
     res->uniq = uout;
     res->uniq_bytes = ubytes;
     res->uniq_records = cu.U;
@@ -480,10 +639,10 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
 
     UniqView pv;
     if (d_prior && n_prior) {
-        SG_TRY(unique_view(c, d_prior, n_prior, PRIOR_SLOTS, S_P_REC, S_P_SORTED_KEYS, true, &pv));
+        SG_TRY(unique_view(c, d_prior, n_prior, PRIOR_SLOTS, S_P_REC, S_P_SORTED_KEYS, S_P_FLAG, true, &pv));
     }
     res->prior_records = pv.L.n_rec;
-    if (pv.U == 0) {
+    if (pv.U == 0 || cu.U == 0) {
         res->fresh = res->uniq;
         res->fresh_bytes = res->uniq_bytes;
         res->fresh_records = res->uniq_records;
@@ -491,20 +650,24 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     }
     uint8_t *fresh;
     SG_TRY(slot(c, S_M_TMP, (size_t)cu.U + 1, &fresh));
-    if (cu.U) {
-        SG_LAUNCH(c, "diff_mark", k_diff_mark, grid_for(cu.U, 256), 256, 0, d_cur, cu.L.starts, cu.L.ends, UR, UK, cu.U,
-                  d_prior, pv.L.starts, pv.L.ends, pv.UR, pv.UK, pv.U, fresh);
-    }
+    RecSet U{d_cur, cu.L.starts, cu.L.ends, cu.UR, cu.UK, cu.U};
+    RecSet P{d_prior, pv.L.starts, pv.L.ends, pv.UR, pv.UK, pv.U};
+    const uint32_t ntiles = (uint32_t)(((uint64_t)cu.U + pv.U + MP_TILE - 1) / MP_TILE);
+    uint32_t *split;
+    SG_TRY(slot(c, S_R_OFF, (size_t)ntiles + 2, &split));
+    SG_LAUNCH(c, "merge_split", k_merge_split, grid_for(ntiles + 1, 256), 256, 0, U, P, ntiles, split);
+    SG_LAUNCH(c, "diff_tile", k_diff_tile, ntiles, 256, 0, U, P, split, fresh);
     uint32_t *fidx;
     SG_TRY(slot(c, S_SEL, (size_t)cu.U + 16, &fidx));
     uint32_t F = 0;
     SG_TRY(select_flags(c, fresh, cu.U, fidx, &F));
-    uint32_t *FR;
-    SG_TRY(slot(c, S_M_TMP2, (size_t)F + 1, &FR));
-    if (F) SG_LAUNCH(c, "gather", k_gather_u32, grid_for(F, 256), 256, 0, UR, fidx, F, FR);
+    uint32_t *FR, *FL;
+    SG_TRY(slot(c, S_R_VAL, (size_t)F + 1, &FR));
+    SG_TRY(slot(c, S_R_GID, (size_t)F + 1, &FL));
+    if (F) SG_LAUNCH(c, "gather_fresh", k_gather_rl, grid_for(F, 256), 256, 0, fidx, cu.UR, cu.UL, F, FR, FL);
     uint8_t *fout;
     uint64_t fbytes = 0;
-    SG_TRY(serialize(c, d_cur, cu.L.starts, cu.L.ends, FR, nullptr, F, S_OUT_FRESH, &fout, &fbytes));
+    SG_TRY(serialize_dense(c, d_cur, cu.L.starts, cu.L.ends, FR, FL, F, S_OUT_FRESH, nullptr, 0, &fout, &fbytes));
     res->fresh = fout;
     res->fresh_bytes = fbytes;
     res->fresh_records = F;

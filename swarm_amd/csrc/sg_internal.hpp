@@ -49,5 +49,8 @@ int select_flags(sg_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out_idx,
 int serialize(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
               const uint32_t *list, const uint32_t *map, uint32_t count, int out_slot,
               uint8_t **d_out, uint64_t *bytes);
+// Same, into a caller buffer of dst_cap bytes (SG_E_CAP if too small).
+int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+                   const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes);
 
 }  // namespace sg

@@ -1,12 +1,552 @@
-// sg_match.hip — A4 signature matching (placeholder until the matcher lands).
+// sg_match.hip — A4 signature matching: Aho-Corasick for literal signatures (grep -F /
+// `sig in line`) and multi-DFA for regex signatures (re.search existence), on records of
+// an HBM-resident line buffer.
+//
+// Automata are built on the host (C++) into dense byte-class transition tables:
+//   * byte classes: every byte that occurs in some pattern gets its own class, all other
+//     bytes share class 0 (for Aho-Corasick class 0 always returns to the root); with
+//     SG_NOCASE 'A'-'Z' share the class of 'a'-'z' (C-locale grep -i);
+//   * states are numbered breadth-first, so the hot shallow states come first: the first
+//     H rows (u16 entries) are staged in LDS, the rest are read from HBM/L2;
+//   * a per-state "has output" bitmap (LDS when it fits) gates the output walk.
+// Device: one thread per record walks its bytes (aligned 4-byte loads) through the table;
+// every (record, signature) event is appended with an atomic slot; events are then
+// radix-sorted and de-duplicated, so hits come out sorted by (record, signature) and the
+// matched lines in input order (grep's output).
 #include "sg_internal.hpp"
+#include "sg_prims.hpp"
+
+#include <algorithm>
+#include <deque>
+#include <map>
+#include <string.h>
+
+#include "sg_regex.hpp"
+
 using namespace sg;
-struct sg_matcher { int dummy; };
-extern "C" {
-int sg_ac_compile(const uint8_t *, const uint32_t *, uint32_t, uint32_t, sg_matcher **) { set_error("not built yet"); return SG_E_UNSUPPORTED; }
-int sg_dfa_compile(const uint8_t *, const uint32_t *, uint32_t, uint32_t, sg_matcher **) { set_error("not built yet"); return SG_E_UNSUPPORTED; }
-int sg_matcher_info(const sg_matcher *, uint64_t *, uint32_t *, uint32_t *) { return SG_E_UNSUPPORTED; }
-int sg_match(sg_matcher *, const uint8_t *, size_t, uint64_t *, uint32_t *, size_t, size_t *) { return SG_E_UNSUPPORTED; }
-int sg_dev_match(sg_ctx *, sg_matcher *, const uint8_t *, size_t, sg_dev_hits *) { return SG_E_UNSUPPORTED; }
-void sg_free(void *) {}
+
+struct sg_matcher {
+    int kind = 0;                 // 0 = Aho-Corasick, 1 = regex DFA set
+    uint32_t n_pats = 0, flags = 0;
+    // one or more automata (AC: exactly one)
+    struct Table {
+        uint32_t n_states = 0, n_classes = 0;
+        uint8_t cls[256];
+        std::vector<uint32_t> delta;    // n_states * n_classes
+        std::vector<uint32_t> own_off;  // n_states + 1 (CSR of pattern ids accepted here)
+        std::vector<uint32_t> own_ids;
+        std::vector<uint32_t> dict;     // AC: next state on the suffix chain with output
+        std::vector<uint32_t> outbits;  // (n_states + 31) / 32
+        uint32_t anchored_eol = 0;      // DFA: class used for the end-of-record step (0 = none)
+    };
+    std::vector<Table> tables;
+    uint64_t total_states = 0;
+    // device copies (one device)
+    int dev = -1;
+    struct DevTable {
+        uint32_t *delta = nullptr, *own_off = nullptr, *own_ids = nullptr, *dict = nullptr, *outbits = nullptr;
+        uint16_t *hot = nullptr;  // first H rows as u16 (if n_states <= 65535)
+        uint8_t *cls = nullptr;
+        uint32_t H = 0;
+    };
+    std::vector<DevTable> dtabs;
+    std::mutex mu;
+};
+
+namespace sg {
+
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr uint32_t AC_HOT_BYTES = 64 * 1024;   // LDS budget for hot rows
+constexpr uint32_t AC_BITS_BYTES = 16 * 1024;  // LDS budget for the output bitmap
+
+static int build_ac(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags, sg_matcher::Table *T) {
+    const bool nocase = flags & SG_NOCASE;
+    auto fold = [&](uint8_t b) -> uint8_t { return (nocase && b >= 'A' && b <= 'Z') ? (uint8_t)(b + 32) : b; };
+    // byte classes
+    bool used[256] = {};
+    for (uint32_t i = 0; i < n; ++i) {
+        if (offs[i + 1] <= offs[i]) { set_error("signature %u is empty", i); return SG_E_INVAL; }
+        for (uint32_t p = offs[i]; p < offs[i + 1]; ++p) {
+            if (pats[p] == '\n') { set_error("signature %u contains a newline", i); return SG_E_INVAL; }
+            used[fold(pats[p])] = true;
+        }
+    }
+    uint32_t C = 1;
+    uint8_t cls_of[256] = {};
+    for (int b = 0; b < 256; ++b)
+        if (used[b]) cls_of[b] = (uint8_t)C++;
+    if (C > 256) { set_error("too many byte classes"); return SG_E_UNSUPPORTED; }
+    for (int b = 0; b < 256; ++b) T->cls[b] = cls_of[fold((uint8_t)b)];
+    // trie with map children, then BFS renumbering
+    std::vector<std::map<uint8_t, uint32_t>> kids(1);
+    std::vector<std::vector<uint32_t>> own(1);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t s = 0;
+        for (uint32_t p = offs[i]; p < offs[i + 1]; ++p) {
+            const uint8_t c = cls_of[fold(pats[p])];
+            auto it = kids[s].find(c);
+            if (it == kids[s].end()) {
+                kids.emplace_back();
+                own.emplace_back();
+                const uint32_t ns = (uint32_t)kids.size() - 1;
+                kids[s][c] = ns;
+                s = ns;
+            } else {
+                s = it->second;
+            }
+        }
+        own[s].push_back(i);
+    }
+    const uint32_t S = (uint32_t)kids.size();
+    std::vector<uint32_t> order, newid(S, NONE);
+    order.reserve(S);
+    order.push_back(0);
+    newid[0] = 0;
+    for (size_t q = 0; q < order.size(); ++q)
+        for (auto &kv : kids[order[q]]) {
+            newid[kv.second] = (uint32_t)order.size();
+            order.push_back(kv.second);
+        }
+    T->n_states = S;
+    T->n_classes = C;
+    T->delta.assign((size_t)S * C, 0);
+    std::vector<uint32_t> fail(S, 0);
+    T->dict.assign(S, NONE);
+    std::vector<bool> has_out(S, false);
+    // BFS over new ids (order[] is already BFS)
+    for (uint32_t q = 0; q < S; ++q) {
+        const uint32_t old = order[q];
+        const uint32_t s = q;
+        has_out[s] = !own[old].empty();
+        for (uint32_t c = 0; c < C; ++c) {
+            auto it = kids[old].find((uint8_t)c);
+            if (it != kids[old].end()) {
+                const uint32_t t = newid[it->second];
+                T->delta[(size_t)s * C + c] = t;
+                fail[t] = (s == 0) ? 0 : T->delta[(size_t)fail[s] * C + c];
+            } else {
+                T->delta[(size_t)s * C + c] = (s == 0) ? 0 : T->delta[(size_t)fail[s] * C + c];
+            }
+        }
+        if (s != 0) {
+            const uint32_t f = fail[s];
+            T->dict[s] = has_out[f] ? f : T->dict[f];
+        }
+    }
+    T->delta[0] = 0;
+    for (uint32_t s = 0; s < S; ++s) T->delta[(size_t)s * C + 0] = 0;  // class 0: no pattern byte
+    T->own_off.assign(S + 1, 0);
+    for (uint32_t q = 0; q < S; ++q) T->own_off[q + 1] = T->own_off[q] + (uint32_t)own[order[q]].size();
+    T->own_ids.resize(T->own_off[S]);
+    for (uint32_t q = 0; q < S; ++q)
+        std::copy(own[order[q]].begin(), own[order[q]].end(), T->own_ids.begin() + T->own_off[q]);
+    T->outbits.assign((S + 31) / 32, 0);
+    for (uint32_t s = 0; s < S; ++s)
+        if (has_out[s] || T->dict[s] != NONE) T->outbits[s / 32] |= 1u << (s % 32);
+    return SG_OK;
 }
+
+template <class T>
+static int upload_vec(const std::vector<T> &v, T **d) {
+    const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+    if (hipMalloc(d, bytes) != hipSuccess) { (void)hipGetLastError(); set_error("hipMalloc matcher table"); return SG_E_NOMEM; }
+    if (!v.empty()) SG_HIP(hipMemcpy(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SG_OK;
+}
+
+static void free_dev(sg_matcher *h) {
+    for (auto &d : h->dtabs) {
+        (void)hipFree(d.delta); (void)hipFree(d.own_off); (void)hipFree(d.own_ids); (void)hipFree(d.dict);
+        (void)hipFree(d.outbits); (void)hipFree(d.hot); (void)hipFree(d.cls);
+    }
+    h->dtabs.clear();
+    h->dev = -1;
+}
+
+static int ensure_device(sg_matcher *h, int dev) {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->dev == dev) return SG_OK;
+    if (h->dev >= 0) { (void)hipSetDevice(h->dev); free_dev(h); }
+    SG_HIP(hipSetDevice(dev));
+    for (auto &T : h->tables) {
+        sg_matcher::DevTable d;
+        SG_TRY(upload_vec(T.delta, &d.delta));
+        SG_TRY(upload_vec(T.own_off, &d.own_off));
+        SG_TRY(upload_vec(T.own_ids, &d.own_ids));
+        SG_TRY(upload_vec(T.dict, &d.dict));
+        SG_TRY(upload_vec(T.outbits, &d.outbits));
+        std::vector<uint8_t> cls(T.cls, T.cls + 256);
+        SG_TRY(upload_vec(cls, &d.cls));
+        uint32_t H = 0;
+        if (T.n_states <= 65535) {
+            H = std::min<uint32_t>(T.n_states, AC_HOT_BYTES / (2 * T.n_classes));
+            std::vector<uint16_t> hot((size_t)H * T.n_classes);
+            for (size_t q = 0; q < hot.size(); ++q) hot[q] = (uint16_t)T.delta[q];
+            SG_TRY(upload_vec(hot, &d.hot));
+        }
+        d.H = H;
+        h->dtabs.push_back(d);
+    }
+    h->dev = dev;
+    return SG_OK;
+}
+
+// ------------------------------------------------------------------ device: Aho-Corasick
+struct ACArgs {
+    const uint8_t *buf;
+    const uint32_t *starts, *ends;
+    uint32_t R;
+    const uint8_t *cls;
+    const uint32_t *delta;
+    const uint16_t *hot;
+    uint32_t C, H, S;
+    const uint32_t *outbits, *own_off, *own_ids, *dict;
+    unsigned long long *hits;
+    uint32_t *hit_count;
+    uint32_t cap;
+    uint32_t bits_in_lds;
+};
+
+__device__ __forceinline__ void emit_hit(const ACArgs &a, uint32_t rec, uint32_t sig, uint32_t *seen, uint32_t &nseen) {
+    const uint32_t key = sig;
+    for (uint32_t q = 0; q < nseen; ++q)
+        if (seen[q] == key) return;
+    if (nseen < 4) seen[nseen++] = key;
+    const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
+    if (slot_i < a.cap) a.hits[slot_i] = ((unsigned long long)rec << 32) | sig;
+}
+
+__global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *s_cls = lds;
+    uint16_t *s_hot = reinterpret_cast<uint16_t *>(lds + 256);
+    const uint32_t hot_n = a.H * a.C;
+    uint32_t *s_bits = reinterpret_cast<uint32_t *>(lds + 256 + ((hot_n * 2 + 15) & ~15u));
+    for (uint32_t q = threadIdx.x; q < 256; q += blockDim.x) s_cls[q] = a.cls[q];
+    for (uint32_t q = threadIdx.x; q < hot_n; q += blockDim.x) s_hot[q] = a.hot[q];
+    const uint32_t nbits = (a.S + 31) / 32;
+    if (a.bits_in_lds)
+        for (uint32_t q = threadIdx.x; q < nbits; q += blockDim.x) s_bits[q] = a.outbits[q];
+    __syncthreads();
+    const uint32_t *bits = a.bits_in_lds ? s_bits : a.outbits;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.R; r += gridDim.x * blockDim.x) {
+        const uint32_t s = a.starts[r], e = a.ends[r];
+        uint32_t st = 0;
+        uint32_t seen[4];
+        uint32_t nseen = 0;
+        for (uint32_t w = s & ~3u; w < e; w += 4) {
+            const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t p = w + b;
+                if (p < s || p >= e) continue;
+                const uint32_t c = s_cls[(x >> (8 * b)) & 0xffu];
+                st = (st < a.H) ? (uint32_t)s_hot[st * a.C + c] : a.delta[(size_t)st * a.C + c];
+                if ((bits[st >> 5] >> (st & 31)) & 1u) {
+                    for (uint32_t t = st; t != NONE; t = a.dict[t])
+                        for (uint32_t q = a.own_off[t]; q < a.own_off[t + 1]; ++q) emit_hit(a, r, a.own_ids[q], seen, nseen);
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ device: regex DFAs
+struct DFAArgs {
+    const uint8_t *buf;
+    const uint32_t *starts, *ends;
+    uint32_t R;
+    const uint8_t *cls;
+    const uint32_t *delta;
+    const uint16_t *hot;
+    uint32_t C, H, S, eol;
+    const uint32_t *outbits, *own_off, *own_ids;
+    unsigned long long *hits;
+    uint32_t *hit_count;
+    uint32_t cap;
+    uint32_t bits_in_lds;
+};
+
+// One DFA of a set. State 0 = dead (no pattern can still match), state 1 = start. A state
+// with output accepts the listed patterns; accepted patterns are removed from the
+// successor states at build time, so each pattern is reported once per record.
+__global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *s_cls = lds;
+    uint16_t *s_hot = reinterpret_cast<uint16_t *>(lds + 256);
+    const uint32_t hot_n = a.H * a.C;
+    uint32_t *s_bits = reinterpret_cast<uint32_t *>(lds + 256 + ((hot_n * 2 + 15) & ~15u));
+    for (uint32_t q = threadIdx.x; q < 256; q += blockDim.x) s_cls[q] = a.cls[q];
+    for (uint32_t q = threadIdx.x; q < hot_n; q += blockDim.x) s_hot[q] = a.hot[q];
+    const uint32_t nbits = (a.S + 31) / 32;
+    if (a.bits_in_lds)
+        for (uint32_t q = threadIdx.x; q < nbits; q += blockDim.x) s_bits[q] = a.outbits[q];
+    __syncthreads();
+    const uint32_t *bits = a.bits_in_lds ? s_bits : a.outbits;
+    auto step = [&](uint32_t st, uint32_t c) -> uint32_t {
+        return (st < a.H) ? (uint32_t)s_hot[st * a.C + c] : a.delta[(size_t)st * a.C + c];
+    };
+    auto accept = [&](uint32_t r, uint32_t st) {
+        if ((bits[st >> 5] >> (st & 31)) & 1u)
+            for (uint32_t q = a.own_off[st]; q < a.own_off[st + 1]; ++q) {
+                const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
+                if (slot_i < a.cap) a.hits[slot_i] = ((unsigned long long)r << 32) | a.own_ids[q];
+            }
+    };
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.R; r += gridDim.x * blockDim.x) {
+        const uint32_t s = a.starts[r], e = a.ends[r];
+        uint32_t st = 1;
+        accept(r, st);
+        for (uint32_t w = s & ~3u; w < e && st != 0; w += 4) {
+            const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t p = w + b;
+                if (p < s || p >= e || st == 0) continue;
+                st = step(st, s_cls[(x >> (8 * b)) & 0xffu]);
+                accept(r, st);
+            }
+        }
+        if (st != 0 && a.eol) accept(r, step(st, a.eol));
+    }
+}
+
+// ------------------------------------------------------------------ host driver
+struct HitKeyPred {
+    const unsigned long long *K;
+    uint32_t n;
+    __device__ uint32_t operator()(uint32_t i) const { return (i == 0 || K[i] != K[i - 1]) ? 1u : 0u; }
+};
+struct RecHeadPred {
+    const unsigned long long *K;
+    __device__ uint32_t operator()(uint32_t i) const { return (i == 0 || (K[i] >> 32) != (K[i - 1] >> 32)) ? 1u : 0u; }
+};
+
+__global__ void k_split_hits(const unsigned long long *K, const uint32_t *idx, uint32_t n, uint32_t *rec, uint32_t *sig) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = K[idx[i]];
+    rec[i] = (uint32_t)(k >> 32);
+    sig[i] = (uint32_t)k;
+}
+
+__global__ void k_rec_of(const unsigned long long *K, const uint32_t *idx, uint32_t n, uint32_t *rec) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) rec[i] = (uint32_t)(K[idx[i]] >> 32);
+}
+
+template <class Pred>
+static int select_one(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint32_t *out, uint32_t *count) {
+    *count = 0;
+    if (n == 0) return SG_OK;
+    const uint32_t ntiles = (n + SEL_TILE - 1) / SEL_TILE;
+    uint64_t *status;
+    SG_TRY(slot(c, S_COUNT, (size_t)ntiles + 4, &status));
+    uint32_t *counter = reinterpret_cast<uint32_t *>(status + ntiles);
+    SG_HIP(hipMemsetAsync(status, 0, ((size_t)ntiles + 4) * 8, c->stream));
+    SG_LAUNCH(c, name, k_select2<Pred>, ntiles, SEL_BLOCK, 0, pred, n, out, (uint32_t *)nullptr, status, counter, ntiles);
+    uint32_t cnt[2];
+    SG_TRY(ctx_readback(c, cnt, counter, 8));
+    *count = cnt[1];
+    return SG_OK;
+}
+
+static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res) {
+    *res = sg_dev_hits{};
+    SG_TRY(ensure_device(h, c->device));
+    Lines L;
+    SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L));
+    const uint32_t R = L.n_rec;
+    res->in_records = R;
+    uint32_t *cnt;
+    SG_TRY(slot(c, S_M_CNT, 4, &cnt));
+    uint64_t cap = std::max<uint64_t>(1u << 20, (uint64_t)R / 4);
+    uint32_t total = 0;
+    unsigned long long *hits = nullptr;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        SG_TRY(slot(c, S_M_HITS, cap, &hits));
+        SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
+        if (R) {
+            for (size_t ti = 0; ti < h->tables.size(); ++ti) {
+                const auto &T = h->tables[ti];
+                const auto &D = h->dtabs[ti];
+                const uint32_t nbits = (T.n_states + 31) / 32;
+                const uint32_t bits_in_lds = nbits * 4 <= AC_BITS_BYTES ? 1u : 0u;
+                const uint32_t lds = 256 + ((D.H * T.n_classes * 2 + 15) & ~15u) + (bits_in_lds ? nbits * 4 : 0);
+                const uint32_t grid = std::min<uint32_t>((R + 511) / 512, 256u * 8u);
+                if (h->kind == 0) {
+                    ACArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
+                             D.outbits, D.own_off, D.own_ids, D.dict, hits, cnt, (uint32_t)cap, bits_in_lds};
+                    SG_LAUNCH(c, "ac_match", k_ac_match, grid, 512, lds, a);
+                } else {
+                    DFAArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
+                              T.anchored_eol, D.outbits, D.own_off, D.own_ids, hits, cnt, (uint32_t)cap, bits_in_lds};
+                    SG_LAUNCH(c, "dfa_match", k_dfa_match, grid, 512, lds, a);
+                }
+            }
+        }
+        SG_TRY(ctx_readback(c, &total, cnt, 4));
+        if (total <= cap) break;
+        cap = (uint64_t)total + 1024;
+    }
+    // sort (rec << 32 | sig) and de-duplicate
+    uint64_t *k2;
+    uint32_t *v1, *v2;
+    SG_TRY(slot(c, S_R_KEY2, (size_t)total + 1, &k2));
+    SG_TRY(slot(c, S_R_VAL, (size_t)total + 1, &v1));
+    SG_TRY(slot(c, S_R_VAL2, (size_t)total + 1, &v2));
+    int rbits = 1;
+    while (rbits < 32 && (1u << rbits) < R) ++rbits;
+    uint64_t *K;
+    uint32_t *V;
+    SG_TRY(radix_sort(c, reinterpret_cast<uint64_t *>(hits), v1, k2, v2, total, 0, 32 + rbits, true, &K, &V, "rs_pass_hits"));
+    const unsigned long long *KK = reinterpret_cast<const unsigned long long *>(K);
+    uint32_t *sel;
+    SG_TRY(slot(c, S_SEL, (size_t)total + 16, &sel));
+    uint32_t H = 0;
+    SG_TRY(select_one(c, "hits_unique", HitKeyPred{KK, total}, total, sel, &H));
+    uint32_t *rec, *sig;
+    SG_TRY(slot(c, S_M_SIG, (size_t)H + 1, &sig));
+    SG_TRY(slot(c, S_R_GID, (size_t)H + 1, &rec));
+    if (H) SG_LAUNCH(c, "split_hits", k_split_hits, (H + 255) / 256, 256, 0, KK, sel, H, rec, sig);
+    res->rec_idx = rec;
+    res->sig_id = sig;
+    res->n_hits = H;
+    // matched records (input order) -> grep output
+    uint32_t M = 0;
+    SG_TRY(select_one(c, "hits_recs", RecHeadPred{KK}, total, sel, &M));
+    uint32_t *mrec;
+    SG_TRY(slot(c, S_R_POS, (size_t)M + 1, &mrec));
+    if (M) SG_LAUNCH(c, "rec_of", k_rec_of, (M + 255) / 256, 256, 0, KK, sel, M, mrec);
+    uint8_t *lines;
+    uint64_t lb = 0;
+    SG_TRY(serialize(c, d_buf, L.starts, L.ends, mrec, nullptr, M, S_M_LINES, &lines, &lb));
+    res->lines = lines;
+    res->lines_bytes = lb;
+    res->matched_records = M;
+    return SG_OK;
+}
+
+}  // namespace sg
+
+extern "C" {
+
+int sg_ac_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats, uint32_t flags, sg_matcher **h) {
+    if (!h || (n_pats && (!pats || !pat_offs))) { set_error("sg_ac_compile: bad arguments"); return SG_E_INVAL; }
+    sg_matcher *m = new sg_matcher();
+    m->kind = 0;
+    m->n_pats = n_pats;
+    m->flags = flags;
+    m->tables.emplace_back();
+    int rc = build_ac(pats, pat_offs, n_pats, flags, &m->tables[0]);
+    if (rc != SG_OK) { delete m; return rc; }
+    m->total_states = m->tables[0].n_states;
+    *h = m;
+    return SG_OK;
+}
+
+int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats, uint32_t flags, sg_matcher **h) {
+    if (!h || (n_pats && (!pats || !pat_offs))) { set_error("sg_dfa_compile: bad arguments"); return SG_E_INVAL; }
+    std::vector<RegexDFA> dfas;
+    int rc = regex_build_set(pats, pat_offs, n_pats, flags, &dfas);
+    if (rc != SG_OK) return rc;
+    sg_matcher *m = new sg_matcher();
+    m->kind = 1;
+    m->n_pats = n_pats;
+    m->flags = flags;
+    for (auto &d : dfas) {
+        sg_matcher::Table T;
+        T.n_states = d.n_states;
+        T.n_classes = d.n_classes;
+        memcpy(T.cls, d.cls, 256);
+        T.delta = std::move(d.delta);
+        T.own_off = std::move(d.acc_off);
+        T.own_ids = std::move(d.acc_ids);
+        T.anchored_eol = d.eol_class;
+        T.outbits.assign((T.n_states + 31) / 32, 0);
+        for (uint32_t s = 0; s < T.n_states; ++s)
+            if (T.own_off[s + 1] > T.own_off[s]) T.outbits[s / 32] |= 1u << (s % 32);
+        m->total_states += T.n_states;
+        m->tables.push_back(std::move(T));
+    }
+    *h = m;
+    return SG_OK;
+}
+
+int sg_matcher_info(const sg_matcher *h, uint64_t *states, uint32_t *groups, uint32_t *n_pats) {
+    if (!h) return SG_E_INVAL;
+    if (states) *states = h->total_states;
+    if (groups) *groups = (uint32_t)h->tables.size();
+    if (n_pats) *n_pats = h->n_pats;
+    return SG_OK;
+}
+
+int sg_dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, size_t n, sg_dev_hits *res) {
+    if (!c || !h || !res || (!d_buf && n)) { set_error("sg_dev_match: bad arguments"); return SG_E_INVAL; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b = d_buf;
+    if (((uintptr_t)d_buf & 15) != 0) {
+        uint8_t *a;
+        SG_TRY(slot(c, S_IN, n + 16, &a));
+        if (n) SG_HIP(hipMemcpyAsync(a, d_buf, n, hipMemcpyDeviceToDevice, c->stream));
+        b = a;
+    }
+    return dev_match(c, h, b, n, res);
+}
+
+int sg_match(sg_matcher *h, const uint8_t *buf, size_t n, uint64_t *rec_idx, uint32_t *sig_id, size_t cap,
+             size_t *n_hit) {
+    if (!h || !n_hit || (!buf && n)) { set_error("sg_match: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    int dev = 0;
+    SG_TRY(pick_device(&dev));
+    sg_ctx *c = nullptr;
+    SG_TRY(pool_acquire(dev, &c));
+    struct Rel { sg_ctx *c; ~Rel() { pool_release(c); } } rel{c};
+    SG_HIP(hipSetDevice(dev));
+    uint8_t *d;
+    SG_TRY(slot(c, S_IN, n + 16, &d));
+    if (n) SG_HIP(hipMemcpyAsync(d, buf, n, hipMemcpyHostToDevice, c->stream));
+    sg_dev_hits r;
+    SG_TRY(dev_match(c, h, d, n, &r));
+    *n_hit = r.n_hits;
+    if (r.n_hits > cap) { set_error("hit capacity too small"); SG_HIP(hipStreamSynchronize(c->stream)); return SG_E_CAP; }
+    std::vector<uint32_t> rr(r.n_hits);
+    if (r.n_hits) {
+        SG_HIP(hipMemcpyAsync(rr.data(), r.rec_idx, r.n_hits * 4, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipMemcpyAsync(sig_id, r.sig_id, r.n_hits * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    SG_HIP(hipStreamSynchronize(c->stream));
+    for (uint64_t i = 0; i < r.n_hits; ++i) rec_idx[i] = rr[i];
+    return SG_OK;
+}
+
+int sg_match_lines(sg_matcher *h, const uint8_t *buf, size_t n, uint8_t *out, size_t cap, size_t *out_n) {
+    if (!h || !out_n || (!buf && n)) { set_error("sg_match_lines: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    int dev = 0;
+    SG_TRY(pick_device(&dev));
+    sg_ctx *c = nullptr;
+    SG_TRY(pool_acquire(dev, &c));
+    struct Rel { sg_ctx *c; ~Rel() { pool_release(c); } } rel{c};
+    SG_HIP(hipSetDevice(dev));
+    uint8_t *d;
+    SG_TRY(slot(c, S_IN, n + 16, &d));
+    if (n) SG_HIP(hipMemcpyAsync(d, buf, n, hipMemcpyHostToDevice, c->stream));
+    sg_dev_hits r;
+    SG_TRY(dev_match(c, h, d, n, &r));
+    *out_n = r.lines_bytes;
+    if (r.lines_bytes > cap) { set_error("output capacity too small"); SG_HIP(hipStreamSynchronize(c->stream)); return SG_E_CAP; }
+    if (r.lines_bytes) SG_HIP(hipMemcpyAsync(out, r.lines, r.lines_bytes, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
+    return SG_OK;
+}
+
+void sg_free(void *p) {
+    sg_matcher *h = (sg_matcher *)p;
+    if (!h) return;
+    if (h->dev >= 0) { (void)hipSetDevice(h->dev); free_dev(h); }
+    delete h;
+}
+
+}  // extern "C"

@@ -1,0 +1,32 @@
+// sg_regex.hpp — regex signatures -> set of byte-class DFAs (host side).
+//
+// Dialect: Python `re` on bytes patterns (the oracle: re.search existence), subset:
+//   literals and escaped metacharacters, '.', classes [...] / [^...] with ranges and
+//   \d \w \s \D \W \S inside, escapes \t \n \r \f \v \xHH \0, anchors ^ $ \A \Z,
+//   groups ( ) (?: ) (?P<name> ), alternation |, quantifiers * + ? {n} {n,} {,m} {n,m}
+//   and their lazy forms (same existence semantics), global (?i) and scoped (?i:...).
+// Rejected with SG_E_UNSUPPORTED: backreferences, lookaround, \b \B, other inline flags.
+// Search semantics: a pattern matches a record if some substring matches; '^'/'\A' hold
+// at offset 0 only, '$'/'\Z' at the record end only (records hold no '\n').
+#pragma once
+#include <stdint.h>
+#include <vector>
+
+namespace sg {
+
+struct RegexDFA {
+    uint32_t n_states = 0, n_classes = 0;  // state 0 = dead, 1 = start; class n_classes-1 = EOL
+    uint8_t cls[256];
+    uint32_t eol_class = 0;
+    std::vector<uint32_t> delta;    // n_states * n_classes
+    std::vector<uint32_t> acc_off;  // n_states + 1
+    std::vector<uint32_t> acc_ids;  // pattern ids accepted on entering a state
+};
+
+// Builds DFAs for all patterns, splitting the set so that no DFA exceeds the state budget.
+int regex_build_set(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags,
+                    std::vector<RegexDFA> *out);
+// Parse-only check for one pattern (SG_OK or SG_E_UNSUPPORTED/SG_E_INVAL).
+int regex_check(const uint8_t *pat, uint32_t len, uint32_t flags);
+
+}  // namespace sg

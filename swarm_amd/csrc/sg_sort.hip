@@ -56,8 +56,8 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_pass(const uint64_t *__restrict
                                                       uint32_t *__restrict__ vout, uint32_t n,
                                                       int shift, const uint32_t *__restrict__ goffs,
                                                       uint64_t *status, uint32_t *counter) {
-    __shared__ uint64_t s_k[RS_TILE];
-    __shared__ uint32_t s_v[RS_TILE];
+    __shared__ uint64_t s_k[RS_TILE];  // keys, then (aliased) values
+    uint32_t *s_v = reinterpret_cast<uint32_t *>(s_k);
     __shared__ uint32_t s_wh[RS_WAVES][256];
     __shared__ uint32_t s_dstart[256];
     __shared__ uint32_t s_gbase[256];
@@ -135,29 +135,38 @@ __global__ __launch_bounds__(RS_BLOCK) void k_rs_pass(const uint64_t *__restrict
     s_gbase[tid] = goffs[tid] + (uint32_t)excl - dstart;
     __syncthreads();
 
+    // block-local destination of each item; keys then values go through LDS so the
+    // global writes of each digit run are contiguous
+    uint32_t dst[RS_ITEMS];
 #pragma unroll
     for (int i = 0; i < RS_ITEMS; ++i) {
         const bool valid = (wbase + i * 64 + lane) < n;
-        if (valid) {
-            const uint32_t d = (uint32_t)(k[i] >> shift) & 255u;
-            const uint32_t p = s_dstart[d] + s_wh[wid][d] + r[i];
-            s_k[p] = k[i];
-            s_v[p] = v[i];
-        }
+        const uint32_t d = (uint32_t)(k[i] >> shift) & 255u;
+        dst[i] = valid ? s_dstart[d] + s_wh[wid][d] + r[i] : 0xffffffffu;
+        if (valid) s_k[dst[i]] = k[i];
     }
     __syncthreads();
     const uint32_t tile_n = (n - tbase) < (uint32_t)RS_TILE ? (n - tbase) : (uint32_t)RS_TILE;
+    uint32_t g[RS_ITEMS];
 #pragma unroll
     for (int j = 0; j < RS_ITEMS; ++j) {
         const uint32_t p = j * RS_BLOCK + tid;
+        g[j] = 0xffffffffu;
         if (p < tile_n) {
             const uint64_t kk = s_k[p];
             const uint32_t d = (uint32_t)(kk >> shift) & 255u;
-            const uint32_t g = s_gbase[d] + p;
-            kout[g] = kk;
-            vout[g] = s_v[p];
+            g[j] = s_gbase[d] + p;
+            kout[g[j]] = kk;
         }
     }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RS_ITEMS; ++i)
+        if (dst[i] != 0xffffffffu) s_v[dst[i]] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; ++j)
+        if (g[j] != 0xffffffffu) vout[g[j]] = s_v[j * RS_BLOCK + tid];
 }
 
 int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,

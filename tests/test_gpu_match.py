@@ -1,0 +1,149 @@
+"""GPU parity for A4 signature matching: Aho-Corasick literals (== grep -F / `in`) and the
+regex DFA set (== Python re.search on bytes), against the grep golden vectors, the nuclei
+signature corpus and random fuzz cases."""
+import base64
+import random
+import re
+
+import pytest
+
+from conftest import b64d, load_golden
+from oracle import semantics as S
+
+pytestmark = pytest.mark.gpu
+
+GR = load_golden("grep_vectors.json")
+SIG = load_golden("signatures.json")
+WORDS = [base64.b64decode(w) for w in SIG["words"]]
+REGEXES = [base64.b64decode(r["p"]) for r in SIG["regexes"] if r["dfa_rc"] == 0]
+
+
+@pytest.fixture(scope="module")
+def sg():
+    import swarm_amd
+    assert swarm_amd.device_count() > 0
+    return swarm_amd
+
+
+@pytest.mark.parametrize("case", GR["literal"], ids=lambda c: c["name"])
+def test_literal_golden(sg, case):
+    data = b64d(case["input"])
+    sigs = [b64d(s) for s in case["sigs"]]
+    m = sg.Matcher(sigs, "literal", nocase=case["nocase"])
+    assert [list(h) for h in m.match(data)] == case["hits"]
+    hits = S.literal_hits(data, sigs, case["nocase"])
+    assert m.match_lines(data) == S.matched_lines(data, hits)
+
+
+@pytest.mark.parametrize("case", GR["regex"], ids=lambda c: c["name"])
+def test_regex_golden(sg, case):
+    data = b64d(case["input"])
+    pats = [b64d(s) for s in case["regexes"]]
+    m = sg.Matcher(pats, "regex")
+    assert [list(h) for h in m.match(data)] == case["hits"]
+
+
+def planted_corpus(rng, n, sigs, frac=0.05):
+    base = [b"https://h%d.target%d.com [%d] [%s] [%s]" % (
+        rng.randrange(99999), rng.randrange(64), rng.choice([200, 301, 403, 404]),
+        rng.choice([b"Login", b"Index of /", b"Dashboard", b"Welcome"]),
+        rng.choice([b"nginx/1.18.0", b"Apache/2.4.41 (Ubuntu)", b"cloudflare"])) for _ in range(n)]
+    for i in range(n):
+        if rng.random() < frac:
+            s = rng.choice(sigs)
+            k = rng.randrange(len(base[i]) + 1)
+            base[i] = base[i][:k] + s + base[i][k:]
+    return b"\n".join(x.replace(b"\n", b" ") for x in base) + b"\n"
+
+
+def test_literal_corpus_2k(sg):
+    """C3-style: 2,000 corpus words (len >= 4, seed 0) over planted httpx lines."""
+    rng = random.Random(0)
+    pool = [w for w in WORDS if len(w) >= 4]
+    sigs = rng.sample(pool, 2000)
+    data = planted_corpus(rng, 1500, sigs)
+    m = sg.Matcher(sigs, "literal")
+    assert m.match(data) == S.literal_hits(data, sigs)
+
+
+def test_literal_corpus_all_words_nocase(sg):
+    rng = random.Random(1)
+    data = planted_corpus(rng, 400, WORDS, 0.2)
+    m = sg.Matcher(WORDS, "literal", nocase=True)
+    assert m.match(data) == S.literal_hits(data, WORDS, nocase=True)
+
+
+def test_regex_corpus_subset(sg):
+    rng = random.Random(2)
+    pats = rng.sample(REGEXES, 60)
+    frags = [b"<title>Grafana</title>", b"Server: nginx", b"X-Powered-By: PHP/7.4.3", b"wp-content/plugins/",
+             b"ORA-01756", b"jenkins", b"SSH-2.0-OpenSSH_8.2p1", b"Apache Tomcat/9.0", b"phpMyAdmin",
+             b"Dell", b" asp.net ", b"APP_KEY=base64", b"DB_HOST=db", b"Location: https://interact.sh"]
+    data = planted_corpus(rng, 600, frags, 0.5)
+    m = sg.Matcher(pats, "regex")
+    assert m.match(data) == S.regex_hits(data, pats)
+
+
+def rand_regex(rng, depth=0):
+    atoms = [b"a", b"b", b"c", b".", b"[ab]", b"[^a]", b"\\d", b"\\w", b"\\s", b"x", b"(?:ab|c)", b"\\b", b"\\B"]
+    parts = []
+    for _ in range(rng.randint(1, 4)):
+        if depth < 2 and rng.random() < 0.2:
+            a = b"(" + rand_regex(rng, depth + 1) + b")"
+        else:
+            a = rng.choice(atoms)
+        q = rng.choice([b"", b"", b"", b"*", b"+", b"?", b"{1,2}", b"{2}", b"*?"])
+        if a in (b"\\b", b"\\B"):
+            q = b""
+        parts.append(a + q)
+    r = b"".join(parts)
+    if depth == 0:
+        if rng.random() < 0.2:
+            r = b"^" + r
+        if rng.random() < 0.2:
+            r = r + b"$"
+        if rng.random() < 0.15:
+            r = r + b"|" + rand_regex(rng, 1)
+    return r
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_regex_fuzz(sg, seed):
+    rng = random.Random(1000 + seed)
+    pats = []
+    while len(pats) < 25:
+        p = rand_regex(rng)
+        try:
+            re.compile(p)
+        except re.error:
+            continue
+        pats.append(p)
+    nocase = seed % 2 == 1
+    lines = [bytes(rng.choice(b"abcx 1_-A") for _ in range(rng.randint(1, 12))) for _ in range(300)]
+    data = b"\n".join(lines) + b"\n"
+    m = sg.Matcher(pats, "regex", nocase=nocase)
+    assert m.match(data) == S.regex_hits(data, pats, nocase=nocase)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_literal_fuzz_overlaps(sg, seed):
+    rng = random.Random(2000 + seed)
+    sigs = list({bytes(rng.choice(b"abc") for _ in range(rng.randint(1, 5))) for _ in range(40)})
+    data = b"\n".join(bytes(rng.choice(b"abcd") for _ in range(rng.randint(1, 30))) for _ in range(500)) + b"\n"
+    m = sg.Matcher(sigs, "literal")
+    assert m.match(data) == S.literal_hits(data, sigs)
+
+
+def test_device_match_lines(sg):
+    import torch
+    rng = random.Random(9)
+    sigs = rng.sample([w for w in WORDS if len(w) >= 4], 300)
+    data = planted_corpus(rng, 3000, sigs)
+    m = sg.Matcher(sigs, "literal")
+    d = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    r = m.dev_match(ctx, d.data_ptr(), d.numel())
+    hits = S.literal_hits(data, sigs)
+    assert r.n_hits == len(hits)
+    assert ctx.to_bytes(r.lines, r.lines_bytes) == S.matched_lines(data, hits)
+    ctx.close()
