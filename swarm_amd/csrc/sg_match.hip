@@ -41,6 +41,18 @@ struct sg_matcher {
     };
     std::vector<Table> tables;
     uint64_t total_states = 0;
+    // regex prefilter plan: factor Aho-Corasick + per-pattern verification DFAs
+    bool has_pre = false;
+    Table pre;
+    std::vector<uint32_t> fac_off, fac_pids;
+    std::vector<uint32_t> s_delta, s_off, s_C, s_eol, s_acc_off, single_of_pid;
+    std::vector<uint8_t> s_cls, s_acc;
+    uint32_t n_singles = 0;
+    struct DevPlan {
+        uint32_t *fac_off = nullptr, *fac_pids = nullptr, *s_delta = nullptr, *s_off = nullptr, *s_C = nullptr,
+                 *s_eol = nullptr, *s_acc_off = nullptr, *single_of_pid = nullptr;
+        uint8_t *s_cls = nullptr, *s_acc = nullptr;
+    } dplan;
     // device copies (one device)
     int dev = -1;
     struct DevTable {
@@ -160,6 +172,11 @@ static void free_dev(sg_matcher *h) {
         (void)hipFree(d.outbits); (void)hipFree(d.hot); (void)hipFree(d.cls);
     }
     h->dtabs.clear();
+    auto &p = h->dplan;
+    for (void *q : {(void *)p.fac_off, (void *)p.fac_pids, (void *)p.s_delta, (void *)p.s_off, (void *)p.s_C,
+                    (void *)p.s_eol, (void *)p.s_acc_off, (void *)p.single_of_pid, (void *)p.s_cls, (void *)p.s_acc})
+        if (q) (void)hipFree(q);
+    h->dplan = sg_matcher::DevPlan{};
     h->dev = -1;
 }
 
@@ -168,7 +185,25 @@ static int ensure_device(sg_matcher *h, int dev) {
     if (h->dev == dev) return SG_OK;
     if (h->dev >= 0) { (void)hipSetDevice(h->dev); free_dev(h); }
     SG_HIP(hipSetDevice(dev));
-    for (auto &T : h->tables) {
+    if (h->has_pre) {
+        auto &p = h->dplan;
+        SG_TRY(upload_vec(h->fac_off, &p.fac_off));
+        SG_TRY(upload_vec(h->fac_pids, &p.fac_pids));
+        SG_TRY(upload_vec(h->s_delta, &p.s_delta));
+        SG_TRY(upload_vec(h->s_off, &p.s_off));
+        SG_TRY(upload_vec(h->s_C, &p.s_C));
+        SG_TRY(upload_vec(h->s_eol, &p.s_eol));
+        SG_TRY(upload_vec(h->s_acc_off, &p.s_acc_off));
+        SG_TRY(upload_vec(h->single_of_pid, &p.single_of_pid));
+        SG_TRY(upload_vec(h->s_cls, &p.s_cls));
+        SG_TRY(upload_vec(h->s_acc, &p.s_acc));
+    }
+    // tables[]: the automata scanned over every record; the prefilter AC goes last
+    std::vector<sg_matcher::Table *> all;
+    for (auto &T : h->tables) all.push_back(&T);
+    if (h->has_pre) all.push_back(&h->pre);
+    for (auto *Tp : all) {
+        auto &T = *Tp;
         sg_matcher::DevTable d;
         SG_TRY(upload_vec(T.delta, &d.delta));
         SG_TRY(upload_vec(T.own_off, &d.own_off));
@@ -205,6 +240,7 @@ struct ACArgs {
     uint32_t *hit_count;
     uint32_t cap;
     uint32_t bits_in_lds;
+    const uint32_t *fac_off, *fac_pids;  // prefilter: factor -> candidate patterns (else null)
 };
 
 __device__ __forceinline__ void emit_hit(const ACArgs &a, uint32_t rec, uint32_t sig, uint32_t *seen, uint32_t &nseen) {
@@ -212,6 +248,13 @@ __device__ __forceinline__ void emit_hit(const ACArgs &a, uint32_t rec, uint32_t
     for (uint32_t q = 0; q < nseen; ++q)
         if (seen[q] == key) return;
     if (nseen < 4) seen[nseen++] = key;
+    if (a.fac_off) {  // prefilter: every pattern that needs this factor is a candidate
+        for (uint32_t q = a.fac_off[sig]; q < a.fac_off[sig + 1]; ++q) {
+            const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
+            if (slot_i < a.cap) a.hits[slot_i] = ((unsigned long long)rec << 32) | a.fac_pids[q];
+        }
+        return;
+    }
     const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
     if (slot_i < a.cap) a.hits[slot_i] = ((unsigned long long)rec << 32) | sig;
 }
@@ -311,6 +354,51 @@ __global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
     }
 }
 
+// Verify prefilter candidates: one thread per (record, pattern) runs that pattern's own
+// DFA over the record (state 0 dead, 1 start, EOL column last) and appends a hit on the
+// first accepting state.
+struct VerifyArgs {
+    const uint8_t *buf;
+    const uint32_t *starts, *ends;
+    const unsigned long long *cand;
+    uint32_t n_cand;
+    const uint32_t *s_delta, *s_off, *s_C, *s_eol, *s_acc_off, *single_of_pid;
+    const uint8_t *s_cls, *s_acc;
+    unsigned long long *hits;
+    uint32_t *hit_count;
+    uint32_t cap;
+};
+
+__global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_cand) return;
+    const unsigned long long cd = a.cand[i];
+    const uint32_t r = (uint32_t)(cd >> 32), pid = (uint32_t)cd;
+    const uint32_t k = a.single_of_pid[pid];
+    const uint32_t *D = a.s_delta + a.s_off[k];
+    const uint8_t *cls = a.s_cls + 256u * k;
+    const uint8_t *acc = a.s_acc + a.s_acc_off[k];
+    const uint32_t C = a.s_C[k];
+    const uint32_t s = a.starts[r], e = a.ends[r];
+    uint32_t st = 1;
+    bool hit = acc[st] != 0;
+    for (uint32_t w = s & ~3u; w < e && !hit && st != 0; w += 4) {
+        const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t p = w + b;
+            if (p < s || p >= e || hit || st == 0) continue;
+            st = D[st * C + cls[(x >> (8 * b)) & 0xffu]];
+            hit = acc[st] != 0;
+        }
+    }
+    if (!hit && st != 0) hit = acc[D[st * C + a.s_eol[k]]] != 0;
+    if (hit) {
+        const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
+        if (slot_i < a.cap) a.hits[slot_i] = cd;
+    }
+}
+
 // ------------------------------------------------------------------ host driver
 struct HitKeyPred {
     const unsigned long long *K;
@@ -359,10 +447,39 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
     const uint32_t R = L.n_rec;
     res->in_records = R;
     uint32_t *cnt;
-    SG_TRY(slot(c, S_M_CNT, 4, &cnt));
+    SG_TRY(slot(c, S_M_CNT, 8, &cnt));
     uint64_t cap = std::max<uint64_t>(1u << 20, (uint64_t)R / 4);
     uint32_t total = 0;
     unsigned long long *hits = nullptr;
+    auto geometry = [&](const sg_matcher::Table &T, const sg_matcher::DevTable &D, uint32_t *bits_in_lds,
+                        uint32_t *lds, uint32_t *grid) {
+        const uint32_t nbits = (T.n_states + 31) / 32;
+        *bits_in_lds = nbits * 4 <= AC_BITS_BYTES ? 1u : 0u;
+        *lds = 256 + ((D.H * T.n_classes * 2 + 15) & ~15u) + (*bits_in_lds ? nbits * 4 : 0);
+        *grid = std::min<uint32_t>((R + 511) / 512, 256u * 8u);
+    };
+    // prefilter candidates (regex plans): factor AC -> (record, pattern) pairs
+    unsigned long long *cand = nullptr;
+    uint32_t n_cand = 0;
+    if (h->has_pre && R) {
+        const auto &T = h->pre;
+        const auto &D = h->dtabs.back();
+        uint64_t ccap = std::max<uint64_t>(1u << 20, (uint64_t)R);
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            SG_TRY(slot(c, S_PART, ccap, &cand));
+            SG_HIP(hipMemsetAsync(cnt + 1, 0, 4, c->stream));
+            uint32_t bil, lds, grid;
+            geometry(T, D, &bil, &lds, &grid);
+            ACArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
+                     D.outbits, D.own_off, D.own_ids, D.dict, cand, cnt + 1, (uint32_t)ccap, bil,
+                     h->dplan.fac_off, h->dplan.fac_pids};
+            SG_LAUNCH(c, "re_prefilter", k_ac_match, grid, 512, lds, a);
+            SG_TRY(ctx_readback(c, &n_cand, cnt + 1, 4));
+            if (n_cand <= ccap) break;
+            ccap = (uint64_t)n_cand + 1024;
+        }
+        cap = std::max<uint64_t>(cap, (uint64_t)n_cand + 1024);
+    }
     for (int attempt = 0; attempt < 2; ++attempt) {
         SG_TRY(slot(c, S_M_HITS, cap, &hits));
         SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
@@ -370,19 +487,24 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
             for (size_t ti = 0; ti < h->tables.size(); ++ti) {
                 const auto &T = h->tables[ti];
                 const auto &D = h->dtabs[ti];
-                const uint32_t nbits = (T.n_states + 31) / 32;
-                const uint32_t bits_in_lds = nbits * 4 <= AC_BITS_BYTES ? 1u : 0u;
-                const uint32_t lds = 256 + ((D.H * T.n_classes * 2 + 15) & ~15u) + (bits_in_lds ? nbits * 4 : 0);
-                const uint32_t grid = std::min<uint32_t>((R + 511) / 512, 256u * 8u);
+                uint32_t bits_in_lds, lds, grid;
+                geometry(T, D, &bits_in_lds, &lds, &grid);
                 if (h->kind == 0) {
                     ACArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
-                             D.outbits, D.own_off, D.own_ids, D.dict, hits, cnt, (uint32_t)cap, bits_in_lds};
+                             D.outbits, D.own_off, D.own_ids, D.dict, hits, cnt, (uint32_t)cap, bits_in_lds,
+                             nullptr, nullptr};
                     SG_LAUNCH(c, "ac_match", k_ac_match, grid, 512, lds, a);
                 } else {
                     DFAArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                               T.anchored_eol, D.outbits, D.own_off, D.own_ids, hits, cnt, (uint32_t)cap, bits_in_lds};
                     SG_LAUNCH(c, "dfa_match", k_dfa_match, grid, 512, lds, a);
                 }
+            }
+            if (n_cand) {
+                const auto &p = h->dplan;
+                VerifyArgs v{d_buf, L.starts, L.ends, cand, n_cand, p.s_delta, p.s_off, p.s_C, p.s_eol,
+                             p.s_acc_off, p.single_of_pid, p.s_cls, p.s_acc, hits, cnt, (uint32_t)cap};
+                SG_LAUNCH(c, "re_verify", k_verify, (n_cand + 255) / 256, 256, 0, v);
             }
         }
         SG_TRY(ctx_readback(c, &total, cnt, 4));
@@ -447,14 +569,41 @@ int sg_ac_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats
 
 int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats, uint32_t flags, sg_matcher **h) {
     if (!h || (n_pats && (!pats || !pat_offs))) { set_error("sg_dfa_compile: bad arguments"); return SG_E_INVAL; }
-    std::vector<RegexDFA> dfas;
-    int rc = regex_build_set(pats, pat_offs, n_pats, flags, &dfas);
+    RegexPlan plan;
+    int rc = regex_build_plan(pats, pat_offs, n_pats, flags, &plan);
     if (rc != SG_OK) return rc;
     sg_matcher *m = new sg_matcher();
     m->kind = 1;
     m->n_pats = n_pats;
     m->flags = flags;
-    for (auto &d : dfas) {
+    if (!plan.singles.empty()) {
+        // factor Aho-Corasick (case-insensitive: a superset of the exact-case occurrences)
+        std::vector<uint8_t> blob;
+        std::vector<uint32_t> offs(1, 0);
+        for (auto &f : plan.factors) {
+            blob.insert(blob.end(), f.begin(), f.end());
+            offs.push_back((uint32_t)blob.size());
+        }
+        rc = build_ac(blob.data(), offs.data(), (uint32_t)plan.factors.size(), SG_NOCASE, &m->pre);
+        if (rc != SG_OK) { delete m; return rc; }
+        m->has_pre = true;
+        m->fac_off = plan.fac_off;
+        m->fac_pids = plan.fac_pids;
+        m->single_of_pid = plan.single_of_pid;
+        for (auto &d : plan.singles) {
+            m->s_off.push_back((uint32_t)m->s_delta.size());
+            m->s_C.push_back(d.n_classes);
+            m->s_eol.push_back(d.eol_class);
+            m->s_delta.insert(m->s_delta.end(), d.delta.begin(), d.delta.end());
+            m->s_cls.insert(m->s_cls.end(), d.cls, d.cls + 256);
+            m->s_acc_off.push_back((uint32_t)m->s_acc.size());
+            for (uint32_t s = 0; s < d.n_states; ++s) m->s_acc.push_back(d.acc_off[s + 1] > d.acc_off[s] ? 1 : 0);
+            m->total_states += d.n_states;
+        }
+        m->n_singles = (uint32_t)plan.singles.size();
+        m->total_states += m->pre.n_states;
+    }
+    for (auto &d : plan.groups) {
         sg_matcher::Table T;
         T.n_states = d.n_states;
         T.n_classes = d.n_classes;

@@ -8,6 +8,7 @@
 #include <bitset>
 #include <map>
 #include <memory>
+#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -728,6 +729,7 @@ static int build_split(std::vector<Pat *> ps, uint32_t budget, std::vector<Regex
         return SG_OK;
     }
     if (ps.size() == 1) {
+        if (budget < 65535) return build_split(ps, 65535, out);
         set_error("regex signature %u needs more than %u DFA states", ps[0]->id, budget);
         return SG_E_STATES;
     }
@@ -737,7 +739,183 @@ static int build_split(std::vector<Pat *> ps, uint32_t budget, std::vector<Regex
     return build_split(b, budget, out);
 }
 
+// ------------------------------------------------------------------ literal factors
+// For a node: `exact` = every string the node can match (lower-cased, when small), and
+// `fac` = a set such that every match of the node contains one of its strings.
+struct Sum {
+    bool exact_ok = false;
+    std::vector<std::string> exact;
+    bool fac_ok = false;
+    std::vector<std::string> fac;
+};
+constexpr size_t FAC_MAXSET = 64, FAC_MAXLEN = 48;
+
+static int fac_score(const std::vector<std::string> &f) {
+    if (f.empty()) return 0;
+    size_t m = f[0].size();
+    for (auto &s : f) m = std::min(m, s.size());
+    return (int)m;
+}
+static bool better(const std::vector<std::string> &a, const std::vector<std::string> &b) {
+    const int sa = fac_score(a), sb = fac_score(b);
+    if (sa != sb) return sa > sb;
+    return a.size() < b.size();
+}
+static void dedupe(std::vector<std::string> &v) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+}
+static std::vector<std::string> effective(const Sum &s) {
+    std::vector<std::string> best;
+    if (s.fac_ok) best = s.fac;
+    if (s.exact_ok) {
+        bool has_empty = false;
+        for (auto &x : s.exact) has_empty |= x.empty();
+        if (!has_empty && (best.empty() || better(s.exact, best))) best = s.exact;
+    }
+    return best;
+}
+
+static Sum summarize(const Node *n) {
+    Sum r;
+    switch (n->kind) {
+        case Node::LIT: {
+            std::vector<std::string> cs;
+            for (int c = 0; c < 256; ++c) {
+                if (!n->set[c]) continue;
+                int l = (c >= 'A' && c <= 'Z') ? c + 32 : c;
+                std::string s(1, (char)l);
+                if (std::find(cs.begin(), cs.end(), s) == cs.end()) cs.push_back(s);
+                if (cs.size() > 4) break;
+            }
+            if (cs.size() <= 4) { r.exact_ok = true; r.exact = cs; }
+            return r;
+        }
+        case Node::BOL: case Node::EOL: case Node::WB: case Node::NWB: case Node::EMPTY:
+            r.exact_ok = true;
+            r.exact = {std::string()};
+            return r;
+        case Node::CAT: {
+            std::vector<std::string> run{std::string()}, best;
+            bool all_exact = true;
+            auto consider = [&](const std::vector<std::string> &f) {
+                if (!f.empty() && fac_score(f) > 0 && (best.empty() || better(f, best))) best = f;
+            };
+            for (auto &k : n->kids) {
+                Sum cs = summarize(k.get());
+                consider(effective(cs));
+                if (cs.exact_ok && run.size() * cs.exact.size() <= FAC_MAXSET) {
+                    std::vector<std::string> nr;
+                    bool too_long = false;
+                    for (auto &a : run)
+                        for (auto &b : cs.exact) {
+                            nr.push_back(a + b);
+                            too_long |= nr.back().size() > FAC_MAXLEN;
+                        }
+                    if (!too_long) { dedupe(nr); run = nr; continue; }
+                }
+                all_exact = false;
+                consider(run);
+                run = cs.exact_ok ? cs.exact : std::vector<std::string>{std::string()};
+            }
+            consider(run);
+            if (all_exact) { r.exact_ok = true; r.exact = run; }
+            if (!best.empty()) { r.fac_ok = true; r.fac = best; }
+            return r;
+        }
+        case Node::ALT: {
+            bool all_exact = true, all_fac = true;
+            std::vector<std::string> ex, fa;
+            for (auto &k : n->kids) {
+                Sum cs = summarize(k.get());
+                if (cs.exact_ok) ex.insert(ex.end(), cs.exact.begin(), cs.exact.end()); else all_exact = false;
+                std::vector<std::string> e = effective(cs);
+                if (e.empty()) all_fac = false; else fa.insert(fa.end(), e.begin(), e.end());
+            }
+            dedupe(ex);
+            dedupe(fa);
+            if (all_exact && ex.size() <= FAC_MAXSET) { r.exact_ok = true; r.exact = ex; }
+            if (all_fac && fa.size() <= FAC_MAXSET) { r.fac_ok = true; r.fac = fa; }
+            return r;
+        }
+        case Node::REP: {
+            Sum cs = summarize(n->kids[0].get());
+            if (n->lo >= 1) {
+                std::vector<std::string> e = effective(cs);
+                if (!e.empty()) { r.fac_ok = true; r.fac = e; }
+                if (cs.exact_ok && n->lo == n->hi && n->lo <= 4) {
+                    std::vector<std::string> run{std::string()};
+                    bool ok = true;
+                    for (int k = 0; k < n->lo && ok; ++k) {
+                        std::vector<std::string> nr;
+                        for (auto &a : run)
+                            for (auto &b : cs.exact) nr.push_back(a + b);
+                        dedupe(nr);
+                        ok = nr.size() <= FAC_MAXSET;
+                        run = nr;
+                    }
+                    if (ok) { r.exact_ok = true; r.exact = run; }
+                }
+            }
+            return r;
+        }
+    }
+    return r;
+}
+
 }  // namespace
+
+int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags, RegexPlan *plan) {
+    std::vector<Pat> ps(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        ps[i].id = i;
+        try {
+            Parser pr(pats + offs[i], offs[i + 1] - offs[i], flags & SG_NOCASE);
+            ps[i].ast = pr.parse();
+        } catch (const ParseError &e) {
+            set_error("regex signature %u: %s", i, e.msg);
+            return e.code;
+        }
+    }
+    plan->single_of_pid.assign(n, 0xffffffffu);
+    std::map<std::string, std::vector<uint32_t>> fac_map;
+    std::vector<Pat *> unfiltered;
+    for (auto &p : ps) {
+        std::vector<std::string> f = effective(summarize(p.ast.get()));
+        const bool had = !f.empty();
+        // a factor holding '\n' can never occur inside a record: drop it
+        f.erase(std::remove_if(f.begin(), f.end(), [](const std::string &s) { return s.find('\n') != std::string::npos; }),
+                f.end());
+        bool filtered = fac_score(f) >= 3 || (had && f.empty());
+        if (filtered) {
+            RegexDFA d;
+            bool fits = false;
+            std::vector<Pat *> one{&p};
+            int rc = build_group(one, 65535, &d, &fits);
+            if (rc != SG_OK) return rc;
+            if (!fits) {
+                filtered = false;
+            } else {
+                plan->single_of_pid[p.id] = (uint32_t)plan->singles.size();
+                plan->singles.push_back(std::move(d));
+                plan->single_pid.push_back(p.id);
+                for (auto &s : f) fac_map[s].push_back(p.id);
+            }
+        }
+        if (!filtered) unfiltered.push_back(&p);
+    }
+    plan->fac_off.assign(1, 0);
+    for (auto &kv : fac_map) {
+        plan->factors.emplace_back(kv.first.begin(), kv.first.end());
+        std::vector<uint32_t> ids = kv.second;
+        std::sort(ids.begin(), ids.end());
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+        plan->fac_pids.insert(plan->fac_pids.end(), ids.begin(), ids.end());
+        plan->fac_off.push_back((uint32_t)plan->fac_pids.size());
+    }
+    if (!unfiltered.empty()) return build_split(unfiltered, 4096, &plan->groups);
+    return SG_OK;
+}
 
 int regex_check(const uint8_t *pat, uint32_t len, uint32_t flags) {
     NodeP n;

@@ -26,6 +26,22 @@ struct RegexDFA {
 // Builds DFAs for all patterns, splitting the set so that no DFA exceeds the state budget.
 int regex_build_set(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags,
                     std::vector<RegexDFA> *out);
+
+// Prefiltered plan (Hyperscan-style). Every pattern with a literal factor set F (any match
+// contains one string of F, compared case-insensitively, every string >= 3 bytes) is
+// "filtered": a case-insensitive Aho-Corasick pass over all factor strings proposes
+// (record, pattern) candidates, each verified by that pattern's own DFA. The remaining
+// patterns are scanned by the multi-pattern DFA groups.
+struct RegexPlan {
+    std::vector<RegexDFA> groups;              // unfiltered patterns
+    std::vector<std::vector<uint8_t>> factors; // distinct lowercase factor strings
+    std::vector<uint32_t> fac_off, fac_pids;   // factor -> patterns (CSR)
+    std::vector<RegexDFA> singles;             // one DFA per filtered pattern
+    std::vector<uint32_t> single_pid;          // pattern id of singles[k]
+    std::vector<uint32_t> single_of_pid;       // pattern id -> index into singles (or ~0)
+};
+int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags,
+                     RegexPlan *plan);
 // Parse-only check for one pattern (SG_OK or SG_E_UNSUPPORTED/SG_E_INVAL).
 int regex_check(const uint8_t *pat, uint32_t len, uint32_t flags);
 
