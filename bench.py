@@ -42,15 +42,88 @@ def kernel_bytes(name, step_info):
     return None
 
 
+def bench_c3(args):
+    """BASELINE.json configs[2] (C3): httpx-style response lines x 2,000 literal signatures
+    (sampled, seed 0, from the nuclei template words of length >= 4), Aho-Corasick, 1 GPU."""
+    import base64
+    import random
+
+    import numpy as np
+    import torch
+
+    import swarm_amd
+    from swarm_amd import corpus
+
+    torch.cuda.set_device(0)
+    sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
+    words = [base64.b64decode(w) for w in sig["words"]]
+    sigs = random.Random(0).sample([w for w in words if len(w) >= 4], 2000)
+    n_lines = args.lines if args.lines != 10_000_000 else 50_000_000
+    pool = corpus.httpx_pool(sigs, 1 << 16, 0.01, seed=0)
+    buf = corpus.lines_from_pool(pool, n_lines, seed=1)
+    d = torch.from_numpy(buf).cuda()
+    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    m = swarm_amd.Matcher(sigs, "literal")
+    for _ in range(args.warmup):
+        r = m.dev_match(ctx, d.data_ptr(), d.numel())
+    torch.cuda.synchronize()
+    ctx.reset_stats()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = m.dev_match(ctx, d.data_ptr(), d.numel())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ctx.profile(False)
+    stats = ctx.kernel_stats()
+    launches, ms = stats.get("ac_match", (0, 0.0))
+    R = int(r.in_records)
+    per_launch = d.numel() + 8.0 * R
+    ach = per_launch / (ms / launches * 1e-3) / 1e9 if launches else 0.0
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import semantics as S
+        m_s = 20_000
+        cut = int(np.flatnonzero(buf == 10)[m_s - 1]) + 1
+        sample = buf[:cut].tobytes()
+        tc = time.perf_counter()
+        hits = S.literal_hits(sample, sigs)
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(m_s / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d C3 lines x 2000 literals, oracle `sig in line`, 1 thread, %.2f s" % (m_s, tc),
+               "host_cpus": os.cpu_count()}
+        gh = m.match(sample)
+        cpu["gpu_hits_bit_exact_on_sample"] = (gh == hits)
+    print(json.dumps({
+        "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (httpx-style lines, 1 %% planted signatures, SURVEY.md §8(d) C3)",
+        "config": {"workload": "C3: %dM httpx lines x 2000 literal signatures (Aho-Corasick), 1 GPU" % (n_lines // 1_000_000),
+                   "bytes": int(d.numel()), "automaton_states": m.info()["states"]},
+        "gbps": round(d.numel() * args.steps / el / 1e9, 2),
+        "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records)},
+        "roofline": {"kernel": "ac_match", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_launch": int(per_launch), "avg_launch_us": round(ms / max(launches, 1) * 1e3, 2)},
+        "cpu_baseline": cpu,
+        "kernels": {k: {"launches": v[0], "ms_total": round(v[1], 3)} for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
+    }), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lines", type=int, default=10_000_000)
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     args = ap.parse_args()
+    if args.workload == "c3":
+        return bench_c3(args)
 
     import numpy as np
     import torch

@@ -135,6 +135,49 @@ def prior_of(ids: np.ndarray) -> np.ndarray:
     return serialize_rows(prior_rows(ids))
 
 
+TITLES = [b"Welcome to nginx!", b"Index of /", b"Grafana", b"Jenkins", b"phpMyAdmin", b"Login",
+          b"IIS Windows Server", b"Apache2 Ubuntu Default Page: It works", b"Dashboard", b"404 Not Found",
+          b"Sign in", b"Kibana", b"GitLab", b"RabbitMQ Management", b"Swagger UI", b"Home"]
+SERVERS = [b"nginx/1.18.0", b"Apache/2.4.41 (Ubuntu)", b"Microsoft-IIS/10.0", b"cloudflare", b"LiteSpeed",
+           b"openresty/1.19.3.1", b"Jetty(9.4.z-SNAPSHOT)", b"gunicorn/20.0.4", b"envoy", b"AmazonS3"]
+
+
+def httpx_pool(sigs, pool: int = 1 << 16, plant: float = 0.01, seed: int = 0):
+    """A pool of httpx-style result lines `url [status] [title] [server]` (~100 B); a
+    `plant` fraction carries a signature inside the title."""
+    import random
+    rng = random.Random(seed)
+    rows = []
+    for _ in range(pool):
+        title = rng.choice(TITLES)
+        if sigs and rng.random() < plant:
+            s = rng.choice(sigs)
+            k = rng.randrange(len(title) + 1)
+            title = title[:k] + s + title[k:]
+        rows.append(b"https://%s.target%d.com/%s [%d] [%s] [%s] [%d]" % (
+            b"".join(bytes([rng.choice(b"abcdefghijklmnopqrstuvwxyz0123456789")]) for _ in range(rng.randint(3, 12))),
+            rng.randrange(64), rng.choice([b"", b"login", b"admin/", b"index.php", b"api/v1/status"]),
+            rng.choice([200, 301, 302, 403, 404, 500]), title.replace(b"\n", b" "), rng.choice(SERVERS),
+            rng.randrange(100, 99999)))
+    return rows
+
+
+def lines_from_pool(rows, n: int, seed: int = 0, chunk: int = 1 << 20) -> np.ndarray:
+    """n lines drawn uniformly from `rows`, '\\n'-terminated (vectorized, chunked)."""
+    W = max(len(r) for r in rows)
+    mat = np.zeros((len(rows), W), dtype=np.uint8)
+    lens = np.array([len(r) for r in rows], dtype=np.int64)
+    for i, r in enumerate(rows):
+        mat[i, :len(r)] = np.frombuffer(r, dtype=np.uint8)
+    msk = np.arange(W)[None, :] < lens[:, None]
+    rng = np.random.default_rng(seed)
+    parts = []
+    for i in range(0, n, chunk):
+        idx = rng.integers(0, len(rows), size=min(chunk, n - i))
+        parts.append(_flatten(mat[idx], msk[idx]))
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8)
+
+
 def chunk_layout(lines_arr: np.ndarray, n_chunks: int) -> list:
     """Split a '\\n'-terminated buffer into n_chunks worker-output chunks at line boundaries
     (the per-chunk outputs the server merges, server/server.py:399-412)."""
