@@ -27,19 +27,31 @@ HBM_COPY_GBS = 6290.0      # measured float4 copy (same guide)
 METRIC = "scan records/sec + GB/s (vs HBM roofline) for match+dedup+diff, 1 and 8 GPUs"
 
 
-def kernel_bytes(name, step_info):
-    """Algorithmic bytes moved by ALL launches of `name` in one step."""
-    R, n, Rp, npb = step_info["R"], step_info["n"], step_info["Rp"], step_info["n_prior"]
-    U, ub, F, fb = step_info["U"], step_info["ub"], step_info["F"], step_info["fb"]
-    if name == "rs_pass":
-        return 24.0 * R * step_info["passes"]          # 12 B read + 12 B written per pair
-    if name == "lines":
-        return float(n + 16 * R + npb + 16 * Rp)       # text read + (start,end,key) written
-    if name == "copy_records":
-        return float(2 * (ub + fb) + 12 * (U + F))     # bytes read+written + rec id/offset
-    if name == "diff_mark":
-        return float(12 * U + 8 * Rp + 8 * Rp)         # keys + ids read, prior keys/spans
-    return None
+def roofline_of(stats, kernel=None):
+    """Dominant kernel (most device time) and its achieved GB/s: the algorithmic bytes the
+    library credited to its launches (SURVEY.md §8(d) model) over the
+    HIP-event time of the same launches, recorded on the launch stream."""
+    if not stats:
+        return None
+    if kernel is None:
+        kernel = max(stats.items(), key=lambda kv: kv[1][1])[0]
+    launches, ms, by = stats[kernel]
+    if not launches or ms <= 0:
+        return None
+    ach = by / (ms * 1e-3) / 1e9
+    return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_per_launch": int(by / launches), "avg_launch_us": round(ms / launches * 1e3, 2),
+            "frac_of_measured_copy_bw": round(ach / HBM_COPY_GBS, 4)}
+
+
+def kernel_table(stats):
+    out = {}
+    for k, (l, ms, by) in sorted(stats.items(), key=lambda kv: -kv[1][1]):
+        out[k] = {"launches": l, "ms_total": round(ms, 3)}
+        if by and ms:
+            out[k]["gbps"] = round(by / (ms * 1e-3) / 1e9, 1)
+    return out
 
 
 def bench_c3(args):
@@ -76,10 +88,7 @@ def bench_c3(args):
     el = time.perf_counter() - t0
     ctx.profile(False)
     stats = ctx.kernel_stats()
-    launches, ms = stats.get("ac_match", (0, 0.0))
     R = int(r.in_records)
-    per_launch = d.numel() + 8.0 * R
-    ach = per_launch / (ms / launches * 1e-3) / 1e9 if launches else 0.0
     cpu = None
     if not args.no_cpu_baseline:
         from oracle import semantics as S
@@ -98,16 +107,14 @@ def bench_c3(args):
         "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (httpx-style lines, 1 %% planted signatures, SURVEY.md §8(d) C3)",
+        "data": "synthetic (httpx-style lines, 1 % planted signatures, SURVEY.md §8(d) C3)",
         "config": {"workload": "C3: %dM httpx lines x 2000 literal signatures (Aho-Corasick), 1 GPU" % (n_lines // 1_000_000),
                    "bytes": int(d.numel()), "automaton_states": m.info()["states"]},
         "gbps": round(d.numel() * args.steps / el / 1e9, 2),
         "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records)},
-        "roofline": {"kernel": "ac_match", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                     "bytes_per_launch": int(per_launch), "avg_launch_us": round(ms / max(launches, 1) * 1e3, 2)},
+        "roofline": roofline_of(stats, "ac_match"),
         "cpu_baseline": cpu,
-        "kernels": {k: {"launches": v[0], "ms_total": round(v[1], 3)} for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
+        "kernels": kernel_table(stats),
     }), flush=True)
     ctx.close()
 
@@ -199,23 +206,9 @@ def main():
     step_bytes = cur.numel() + prior.numel() + r.uniq_bytes + r.fresh_bytes
     info = {"R": int(r.in_records), "n": int(nrecv), "Rp": int(r.prior_records), "n_prior": int(prior.numel()),
             "U": int(r.uniq_records), "ub": int(r.uniq_bytes), "F": int(r.fresh_records), "fb": int(r.fresh_bytes)}
-    launches_rs = stats.get("rs_pass", (0, 0.0))[0]
-    info["passes"] = launches_rs / max(args.steps, 1)
 
-    # dominant kernel roofline
-    dom = max(stats.items(), key=lambda kv: kv[1][1]) if stats else None
-    roofline = None
-    if dom:
-        name, (launches, ms) = dom
-        per_step_bytes = kernel_bytes(name, info)
-        if per_step_bytes is not None and launches:
-            per_launch = per_step_bytes * args.steps / launches
-            avg_ms = ms / launches
-            ach = per_launch / (avg_ms * 1e-3) / 1e9
-            roofline = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                        "bytes_per_launch": int(per_launch), "avg_launch_us": round(avg_ms * 1e3, 2)}
-    kernels = {k: {"launches": v[0], "ms_total": round(v[1], 3)} for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])}
+    roofline = roofline_of(stats)
+    kernels = kernel_table(stats)
     gpu_ms_sum = sum(v[1] for v in stats.values()) / args.steps
 
     cpu = None

@@ -61,9 +61,11 @@ int sg_ctx_destroy(sg_ctx *ctx);
 int sg_ctx_sync(sg_ctx *ctx);
 /* Per-kernel HIP-event timing, recorded on the context's stream while enabled. */
 int sg_ctx_profile(sg_ctx *ctx, int enable);
-/* Kernel stats by index: name (static string), launches, total device ms. Returns
- * SG_E_INVAL past the last index. */
-int sg_ctx_kernel_stat(sg_ctx *ctx, int idx, const char **name, uint64_t *launches, double *total_ms);
+/* Kernel stats by index: name (static string), launches, total device ms and the total
+ * algorithmic bytes those launches moved (0 where not modelled). Returns SG_E_INVAL past
+ * the last index. */
+int sg_ctx_kernel_stat(sg_ctx *ctx, int idx, const char **name, uint64_t *launches, double *total_ms,
+                       double *total_bytes);
 int sg_ctx_reset_stats(sg_ctx *ctx);
 /* Synchronous copy on the context's stream (any direction: hipMemcpyDefault). */
 int sg_ctx_memcpy(sg_ctx *ctx, void *dst, const void *src, size_t n);

@@ -73,7 +73,8 @@ def _load():
         "sg_ctx_destroy": (C.c_int, [P]),
         "sg_ctx_sync": (C.c_int, [P]),
         "sg_ctx_profile": (C.c_int, [P, C.c_int]),
-        "sg_ctx_kernel_stat": (C.c_int, [P, C.c_int, C.POINTER(C.c_char_p), U64P, C.POINTER(C.c_double)]),
+        "sg_ctx_kernel_stat": (C.c_int, [P, C.c_int, C.POINTER(C.c_char_p), U64P, C.POINTER(C.c_double),
+                                         C.POINTER(C.c_double)]),
         "sg_ctx_reset_stats": (C.c_int, [P]),
         "sg_ctx_memcpy": (C.c_int, [P, P, P, SZ]),
         "sg_lines": (C.c_int, [U8P, SZ, U64P, SZ, SZP]),

@@ -209,8 +209,9 @@ class Context:
         name = C.c_char_p()
         launches = C.c_uint64()
         ms = C.c_double()
-        while lib.sg_ctx_kernel_stat(self._h, i, C.byref(name), C.byref(launches), C.byref(ms)) == 0:
-            out[name.value.decode()] = (launches.value, ms.value)
+        by = C.c_double()
+        while lib.sg_ctx_kernel_stat(self._h, i, C.byref(name), C.byref(launches), C.byref(ms), C.byref(by)) == 0:
+            out[name.value.decode()] = (launches.value, ms.value, by.value)
             i += 1
         return out
 

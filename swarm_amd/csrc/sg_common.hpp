@@ -64,6 +64,7 @@ struct KStat {
     const char *name;
     uint64_t launches;
     double ms;
+    double bytes;  // algorithmic bytes (SURVEY.md §8(d) model) of the timed launches
 };
 
 struct sg_ctx_impl;
@@ -98,6 +99,8 @@ int ctx_readback(sg_ctx *c, void *host, const void *dev, size_t bytes);  // sync
 int ctx_harvest(sg_ctx *c);
 int prof_begin(sg_ctx *c, const char *name, int *stat, hipEvent_t *a);
 void prof_end(sg_ctx *c, int stat, hipEvent_t a);
+// Credit algorithmic bytes to the named kernel (no-op unless profiling).
+void prof_bytes(sg_ctx *c, const char *name, double bytes);
 
 // Launch with optional HIP-event timing on the context stream.
 #define SG_LAUNCH(ctx, name, kernel, grid, block, lds, ...)                          \
@@ -113,6 +116,13 @@ void prof_end(sg_ctx *c, int stat, hipEvent_t a);
             return SG_E_HIP;                                                          \
         }                                                                             \
         if (st_ >= 0) ::sg::prof_end((ctx), st_, ea_);                                \
+    } while (0)
+
+// Same, crediting `bytes` algorithmic bytes to the kernel's roofline accounting.
+#define SG_LAUNCH_B(ctx, name, bytes, kernel, grid, block, lds, ...)                 \
+    do {                                                                              \
+        SG_LAUNCH(ctx, name, kernel, grid, block, lds, __VA_ARGS__);                  \
+        if ((ctx)->profile) ::sg::prof_bytes((ctx), (name), (double)(bytes));         \
     } while (0)
 
 // ------------------------------------------------------------------ limits

@@ -42,6 +42,8 @@ static int run_select2(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint3
     SG_TRY(ctx_readback(c, cnt, counter, 12));
     *cntA = cnt[1];
     if (cntB) *cntB = cnt[2];
+    // model: the predicate reads ~8 B per item; 4 B written per selected index
+    prof_bytes(c, name, 8.0 * n + 4.0 * (cnt[1] + (cntB ? cnt[2] : 0)));
     return SG_OK;
 }
 
@@ -54,7 +56,7 @@ static int run_scan64(sg_ctx *c, const char *name, Fn fn, uint32_t n, uint64_t *
     SG_TRY(slot(c, S_COUNT, (size_t)ntiles + 4, &status));
     uint32_t *counter = reinterpret_cast<uint32_t *>(status + ntiles);
     SG_HIP(hipMemsetAsync(status, 0, ((size_t)ntiles + 4) * 8, c->stream));
-    SG_LAUNCH(c, name, k_scan64<Fn>, ntiles, SCAN_BLOCK, 0, fn, n, out, status, counter, ntiles);
+    SG_LAUNCH_B(c, name, 12.0 * n, k_scan64<Fn>, ntiles, SCAN_BLOCK, 0, fn, n, out, status, counter, ntiles);
     uint32_t cnt[3];
     SG_TRY(ctx_readback(c, cnt, counter, 12));
     *total = (uint64_t)cnt[1] | ((uint64_t)cnt[2] << 32);
@@ -455,7 +457,8 @@ static int serialize_dense(sg_ctx *c, const uint8_t *d_buf, const uint32_t *star
     } else {
         SG_TRY(slot(c, out_slot, (size_t)total + 16, d_out));
     }
-    if (count) SG_LAUNCH(c, "copy_records", k_copy_records, grid_for(count, 256), 256, 0, d_buf, starts, ends, recs, offs, count, *d_out);
+    // model: each output byte read once and written once, plus id/start/end/offset per record
+    if (count) SG_LAUNCH_B(c, "copy_records", 2.0 * total + 20.0 * count, k_copy_records, grid_for(count, 256), 256, 0, d_buf, starts, ends, recs, offs, count, *d_out);
     *bytes = total;
     return SG_OK;
 }
@@ -514,7 +517,8 @@ int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet 
     while (G > 0) {
         uint8_t *unres;
         SG_TRY(slot(c, S_M_TMP, (size_t)G + 16, &unres));
-        SG_LAUNCH(c, "refine_eq", k_refine_eq, grid_for(G, 256), 256, 0, d_buf, L.starts, L.ends, GS, GE, G, V, uniq, off, unres);
+        // model: per group GS/GE + flag; per member id, start, end and ~26 record bytes twice
+        SG_LAUNCH_B(c, "refine_eq", 9.0 * G + 64.0 * 2.0 * G, k_refine_eq, grid_for(G, 256), 256, 0, d_buf, L.starts, L.ends, GS, GE, G, V, uniq, off, unres);
         uint32_t *ulist;
         SG_TRY(slot(c, S_SEL, (size_t)G + 16, &ulist));
         uint32_t Ux = 0;
@@ -597,7 +601,7 @@ static int unique_view(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSe
         uint32_t *flag;
         SG_TRY(slot(c, S_M_CNT, 4, &flag));
         SG_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
-        SG_LAUNCH(c, "check_sorted", k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, uv->L.starts, uv->L.ends, uv->L.keys, R, flag);
+        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, uv->L.starts, uv->L.ends, uv->L.keys, R, flag);
         uint32_t f = 1;
         SG_TRY(ctx_readback(c, &f, flag, 4));
         trust_sorted = (f == 0);
@@ -618,7 +622,7 @@ static int unique_view(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSe
     SG_TRY(slot(c, ur_slot, (size_t)U + 1, &uv->UR));
     SG_TRY(slot(c, uk_slot, (size_t)U + 1, &uv->UK));
     SG_TRY(slot(c, ul_slot, (size_t)U + 1, &uv->UL));
-    if (U) SG_LAUNCH(c, "gather_uniq", k_gather_sel, grid_for(U, 256), 256, 0, sel, S.recs, S.keys, uv->L.starts, uv->L.ends, U, uv->UR, uv->UK, uv->UL);
+    if (U) SG_LAUNCH_B(c, "gather_uniq", 40.0 * U, k_gather_sel, grid_for(U, 256), 256, 0, sel, S.recs, S.keys, uv->L.starts, uv->L.ends, U, uv->UR, uv->UK, uv->UL);
     uv->U = U;
     return SG_OK;
 }
@@ -656,7 +660,8 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     uint32_t *split;
     SG_TRY(slot(c, S_R_OFF, (size_t)ntiles + 2, &split));
     SG_LAUNCH(c, "merge_split", k_merge_split, grid_for(ntiles + 1, 256), 256, 0, U, P, ntiles, split);
-    SG_LAUNCH(c, "diff_tile", k_diff_tile, ntiles, 256, 0, U, P, split, fresh);
+    // model: key+id of every unique cur and prior record, one flag per cur record
+    SG_LAUNCH_B(c, "diff_tile", 12.0 * (cu.U + (double)pv.U) + cu.U, k_diff_tile, ntiles, 256, 0, U, P, split, fresh);
     uint32_t *fidx;
     SG_TRY(slot(c, S_SEL, (size_t)cu.U + 16, &fidx));
     uint32_t F = 0;

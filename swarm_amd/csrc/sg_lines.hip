@@ -147,6 +147,7 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
         uint32_t R = 0;
         SG_TRY(ctx_readback(c, &R, counter + 1, 4));
         out->n_rec = R;
+        prof_bytes(c, "lines", (double)n + 16.0 * R);  // text read once + (start, end, key0)
         if (R <= cap) return SG_OK;
         want = (uint64_t)R + 4096;
     }

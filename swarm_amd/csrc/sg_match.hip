@@ -473,7 +473,7 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
             ACArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                      D.outbits, D.own_off, D.own_ids, D.dict, cand, cnt + 1, (uint32_t)ccap, bil,
                      h->dplan.fac_off, h->dplan.fac_pids};
-            SG_LAUNCH(c, "re_prefilter", k_ac_match, grid, 512, lds, a);
+            SG_LAUNCH_B(c, "re_prefilter", (double)n + 8.0 * R, k_ac_match, grid, 512, lds, a);
             SG_TRY(ctx_readback(c, &n_cand, cnt + 1, 4));
             if (n_cand <= ccap) break;
             ccap = (uint64_t)n_cand + 1024;
@@ -493,18 +493,18 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
                     ACArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                              D.outbits, D.own_off, D.own_ids, D.dict, hits, cnt, (uint32_t)cap, bits_in_lds,
                              nullptr, nullptr};
-                    SG_LAUNCH(c, "ac_match", k_ac_match, grid, 512, lds, a);
+                    SG_LAUNCH_B(c, "ac_match", (double)n + 8.0 * R, k_ac_match, grid, 512, lds, a);
                 } else {
                     DFAArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                               T.anchored_eol, D.outbits, D.own_off, D.own_ids, hits, cnt, (uint32_t)cap, bits_in_lds};
-                    SG_LAUNCH(c, "dfa_match", k_dfa_match, grid, 512, lds, a);
+                    SG_LAUNCH_B(c, "dfa_match", (double)n + 8.0 * R, k_dfa_match, grid, 512, lds, a);
                 }
             }
             if (n_cand) {
                 const auto &p = h->dplan;
                 VerifyArgs v{d_buf, L.starts, L.ends, cand, n_cand, p.s_delta, p.s_off, p.s_C, p.s_eol,
                              p.s_acc_off, p.single_of_pid, p.s_cls, p.s_acc, hits, cnt, (uint32_t)cap};
-                SG_LAUNCH(c, "re_verify", k_verify, (n_cand + 255) / 256, 256, 0, v);
+                SG_LAUNCH_B(c, "re_verify", n_cand * (16.0 + (double)n / R), k_verify, (n_cand + 255) / 256, 256, 0, v);
             }
         }
         SG_TRY(ctx_readback(c, &total, cnt, 4));

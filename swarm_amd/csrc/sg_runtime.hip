@@ -57,7 +57,7 @@ int prof_begin(sg_ctx *c, const char *name, int *stat, hipEvent_t *a) {
     for (size_t i = 0; i < c->stats.size(); ++i)
         if (c->stats[i].name == name || strcmp(c->stats[i].name, name) == 0) { idx = (int)i; break; }
     if (idx < 0) {
-        c->stats.push_back(KStat{name, 0, 0.0});
+        c->stats.push_back(KStat{name, 0, 0.0, 0.0});
         idx = (int)c->stats.size() - 1;
     }
     hipEvent_t e;
@@ -75,6 +75,13 @@ void prof_end(sg_ctx *c, int stat, hipEvent_t a) {
     else if (hipEventCreate(&e) != hipSuccess) { (void)hipGetLastError(); return; }
     (void)hipEventRecord(e, c->stream);
     c->pending.push_back(sg_ctx::Pending{stat, a, e});
+}
+
+void prof_bytes(sg_ctx *c, const char *name, double bytes) {
+    if (!c->profile) return;
+    for (auto &s : c->stats)
+        if (s.name == name || strcmp(s.name, name) == 0) { s.bytes += bytes; return; }
+    c->stats.push_back(KStat{name, 0, 0.0, bytes});
 }
 
 int ctx_harvest(sg_ctx *c) {
@@ -203,13 +210,15 @@ int sg_ctx_profile(sg_ctx *c, int enable) {
     return SG_OK;
 }
 
-int sg_ctx_kernel_stat(sg_ctx *c, int idx, const char **name, uint64_t *launches, double *total_ms) {
+int sg_ctx_kernel_stat(sg_ctx *c, int idx, const char **name, uint64_t *launches, double *total_ms,
+                       double *total_bytes) {
     if (!c) return SG_E_INVAL;
     SG_TRY(ctx_harvest(c));
     if (idx < 0 || idx >= (int)c->stats.size()) return SG_E_INVAL;
     if (name) *name = c->stats[idx].name;
     if (launches) *launches = c->stats[idx].launches;
     if (total_ms) *total_ms = c->stats[idx].ms;
+    if (total_bytes) *total_bytes = c->stats[idx].bytes;
     return SG_OK;
 }
 

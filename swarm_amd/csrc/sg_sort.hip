@@ -184,7 +184,7 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
     SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
     uint32_t hgrid = (n + 256 * 16 - 1) / (256 * 16);
     if (hgrid > 2048) hgrid = 2048;
-    SG_LAUNCH(c, "rs_hist", k_rs_hist, hgrid, 256, 0, keys, n, begin_bit, npasses, hist);
+    SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, 256, 0, keys, n, begin_bit, npasses, hist);
     SG_LAUNCH(c, "rs_scan", k_rs_scan, npasses, 256, 0, hist, offs, triv, n);
     uint32_t trivial[RS_MAXPASS];
     SG_TRY(ctx_readback(c, trivial, triv, npasses * 4));
@@ -208,6 +208,8 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
             SG_LAUNCH(c, pass_name, k_rs_pass<false>, ntiles, RS_BLOCK, 0, ck, cv, ak, av, n, shift,
                       offs + p * 256, status, counter);
         }
+        // 12 B read (8 B key + 4 B value; 8 B with implied iota values) + 12 B written per pair
+        prof_bytes(c, pass_name, (iota_pending ? 20.0 : 24.0) * n);
         iota_pending = false;
         uint64_t *tk = ck; ck = ak; ak = tk;
         uint32_t *tv = cv; cv = av; av = tv;
