@@ -39,8 +39,7 @@ __host__ __device__ __forceinline__ uint32_t part_of(uint64_t h, uint32_t parts)
 }
 
 __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ buf,
-                                                   const uint32_t *__restrict__ starts,
-                                                   const uint32_t *__restrict__ ends, uint32_t R,
+                                                   const uint2 *__restrict__ spans, uint32_t R,
                                                    uint32_t parts, uint64_t *keys,
                                                    unsigned long long *cnt /* [2*parts] */) {
     __shared__ unsigned long long s_c[2 * 256];
@@ -48,7 +47,7 @@ __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ b
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < R) {
-        const uint32_t s = starts[i], e = ends[i];
+        const uint32_t s = spans[i].x, e = spans[i].y;
         const uint8_t *p = buf + s;
         const uint64_t h = hash_words([&](uint32_t j) { return p[j]; }, e - s);
         const uint32_t q = part_of(h, parts);
@@ -147,13 +146,13 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
     SG_TRY(slot(c, S_VALS, R, &v1));
     SG_TRY(slot(c, S_VALS2, R, &v2));
     if (R) {
-        SG_LAUNCH(c, "part_keys", k_part_keys, (R + 255) / 256, 256, 0, d_buf, L.starts, L.ends, R, parts, keys, cnt);
+        SG_LAUNCH(c, "part_keys", k_part_keys, (R + 255) / 256, 256, 0, d_buf, L.spans, R, parts, keys, cnt);
     }
     uint64_t *K;
     uint32_t *V;
     SG_TRY(radix_sort(c, keys, v1, keys2, v2, R, 0, 8, true, &K, &V, "rs_pass_part"));
     uint64_t bytes = 0;
-    SG_TRY(serialize_into(c, d_buf, L.starts, L.ends, V, R, d_out, out_cap, &bytes));
+    SG_TRY(serialize_into(c, d_buf, L.spans, V, R, d_out, out_cap, &bytes));
     uint64_t h[2 * 256];
     SG_TRY(ctx_readback(c, h, cnt, 2 * parts * 8));
     for (uint32_t q = 0; q < parts; ++q) {
@@ -185,13 +184,10 @@ int sg_lines(const uint8_t *buf, size_t n, uint64_t *spans, size_t cap, size_t *
     SG_TRY(run_lines(c, d, n, CUR_SLOTS, &L));
     *n_rec = L.n_rec;
     if (L.n_rec > cap) { set_error("span capacity too small"); return SG_E_CAP; }
-    std::vector<uint32_t> s(L.n_rec), e(L.n_rec);
-    if (L.n_rec) {
-        SG_HIP(hipMemcpyAsync(s.data(), L.starts, L.n_rec * 4ull, hipMemcpyDeviceToHost, c->stream));
-        SG_HIP(hipMemcpyAsync(e.data(), L.ends, L.n_rec * 4ull, hipMemcpyDeviceToHost, c->stream));
-    }
+    std::vector<uint2> sp(L.n_rec);
+    if (L.n_rec) SG_HIP(hipMemcpyAsync(sp.data(), L.spans, L.n_rec * 8ull, hipMemcpyDeviceToHost, c->stream));
     SG_HIP(hipStreamSynchronize(c->stream));
-    for (uint32_t i = 0; i < L.n_rec; ++i) { spans[2 * i] = s[i]; spans[2 * i + 1] = e[i]; }
+    for (uint32_t i = 0; i < L.n_rec; ++i) { spans[2 * i] = sp[i].x; spans[2 * i + 1] = sp[i].y; }
     return SG_OK;
 }
 

@@ -127,11 +127,11 @@ struct GroupSizeFn {
     }
 };
 
-__device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint32_t *starts, const uint32_t *ends,
+__device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint2 *spans,
                                             uint64_t ka, uint32_t ra, uint64_t kb, uint32_t rb, uint32_t off) {
     if (ka != kb) return ka < kb ? -1 : 1;
     if ((ka & 0xffu) < 8u) return 0;
-    return rec_cmp_k(buf, starts[ra], ends[ra], buf, starts[rb], ends[rb], off + 7);
+    return rec_cmp_k(buf, spans[ra].x, spans[ra].y, buf, spans[rb].x, spans[rb].y, off + 7);
 }
 
 // ------------------------------------------------------------------ refinement kernels
@@ -140,8 +140,7 @@ __device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint32_t *
 // stays unique and the rest are duplicates, order unchanged. Otherwise (or above
 // EQ_GROUP members) the group is flagged for ranking.
 __global__ __launch_bounds__(256) void k_refine_eq(const uint8_t *__restrict__ buf,
-                                                   const uint32_t *__restrict__ starts,
-                                                   const uint32_t *__restrict__ ends,
+                                                   const uint2 *__restrict__ spans,
                                                    const uint32_t *__restrict__ GS,
                                                    const uint32_t *__restrict__ GE, uint32_t G,
                                                    const uint32_t *__restrict__ V, uint8_t *uniq,
@@ -152,10 +151,10 @@ __global__ __launch_bounds__(256) void k_refine_eq(const uint8_t *__restrict__ b
     bool same = k <= EQ_GROUP;
     if (same) {
         const uint32_t m0 = V[s];
-        const uint32_t s0 = starts[m0], e0 = ends[m0];
+        const uint32_t s0 = spans[m0].x, e0 = spans[m0].y;
         for (uint32_t a = 1; a < k; ++a) {
             const uint32_t m = V[s + a];
-            if (!rec_equal(buf, s0, e0, buf, starts[m], ends[m], off)) { same = false; break; }
+            if (!rec_equal(buf, s0, e0, buf, spans[m].x, spans[m].y, off)) { same = false; break; }
         }
     }
     if (same)
@@ -166,8 +165,7 @@ __global__ __launch_bounds__(256) void k_refine_eq(const uint8_t *__restrict__ b
 // Unresolved groups of <= 64 records: one wave per group, one member per lane; each lane counts the
 // members that precede it (stable), duplicates are members equal to an earlier one.
 __global__ __launch_bounds__(256) void k_refine_wave(const uint8_t *__restrict__ buf,
-                                                     const uint32_t *__restrict__ starts,
-                                                     const uint32_t *__restrict__ ends,
+                                                     const uint2 *__restrict__ spans,
                                                      const uint32_t *__restrict__ GS,
                                                      const uint32_t *__restrict__ GE, uint32_t G,
                                                      uint32_t *V, uint8_t *uniq, uint32_t off) {
@@ -178,14 +176,14 @@ __global__ __launch_bounds__(256) void k_refine_wave(const uint8_t *__restrict__
     if (k > WAVE_GROUP) return;
     const bool act = lane < k;
     const uint32_t m = act ? V[s + lane] : 0u;
-    const uint64_t key = act ? chunk_key(buf, starts[m], ends[m], off) : ~0ull;
+    const uint64_t key = act ? chunk_key(buf, spans[m].x, spans[m].y, off) : ~0ull;
     uint32_t rank = 0;
     bool dup = false;
     for (uint32_t j = 0; j < k; ++j) {
         const uint64_t kb = __shfl(key, (int)j, 64);
         const uint32_t mb = __shfl(m, (int)j, 64);
         if (act && j != lane) {
-            const int c = key_cmp_full(buf, starts, ends, key, m, kb, mb, off);
+            const int c = key_cmp_full(buf, spans, key, m, kb, mb, off);
             if (c > 0 || (c == 0 && j < lane)) rank++;
             if (c == 0 && j < lane) dup = true;
         }
@@ -199,8 +197,7 @@ __global__ __launch_bounds__(256) void k_refine_wave(const uint8_t *__restrict__
 // Expand big groups into member rows: row j -> group index (into big list), global
 // position, and the record's chunk key at `off`.
 __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
-                                                const uint32_t *__restrict__ starts,
-                                                const uint32_t *__restrict__ ends,
+                                                const uint2 *__restrict__ spans,
                                                 const uint32_t *__restrict__ GS,
                                                 const uint32_t *__restrict__ big,
                                                 const uint64_t *__restrict__ goff, uint32_t B,
@@ -216,7 +213,7 @@ __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
     }
     const uint32_t pos = GS[big[lo]] + (j - (uint32_t)goff[lo]);
     const uint32_t r = V[pos];
-    RK[j] = chunk_key(buf, starts[r], ends[r], off);
+    RK[j] = chunk_key(buf, spans[r].x, spans[r].y, off);
     RG[j] = lo;
     RP[j] = pos;
 }
@@ -237,15 +234,14 @@ __global__ void k_gid_keys(const uint32_t *__restrict__ RG, const uint32_t *__re
 }
 
 // Final order of a round: T[i] = record now at final index i; FK its chunk key.
-__global__ void k_round_gather(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ starts,
-                               const uint32_t *__restrict__ ends, const uint32_t *__restrict__ V,
+__global__ void k_round_gather(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, const uint32_t *__restrict__ V,
                                const uint32_t *__restrict__ RP, const uint32_t *__restrict__ perm,
                                uint32_t M, uint32_t off, uint32_t *T, uint64_t *FK) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= M) return;
     const uint32_t r = V[RP[perm[i]]];
     T[i] = r;
-    FK[i] = chunk_key(buf, starts[r], ends[r], off);
+    FK[i] = chunk_key(buf, spans[r].x, spans[r].y, off);
 }
 
 __global__ void k_round_scatter(const uint32_t *__restrict__ T, const uint32_t *__restrict__ RP,
@@ -263,8 +259,7 @@ __global__ void k_pos_of(const uint32_t *__restrict__ idx, const uint32_t *__res
 // ------------------------------------------------------------------ gathers / output
 // Selected positions -> record id, key0 and serialized length (len + 1) per record.
 __global__ void k_gather_sel(const uint32_t *__restrict__ sel, const uint32_t *__restrict__ V,
-                             const uint64_t *__restrict__ K, const uint32_t *__restrict__ starts,
-                             const uint32_t *__restrict__ ends, uint32_t n, uint32_t *UR, uint64_t *UK,
+                             const uint64_t *__restrict__ K, const uint2 *__restrict__ spans, uint32_t n, uint32_t *UR, uint64_t *UK,
                              uint32_t *UL) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -272,7 +267,7 @@ __global__ void k_gather_sel(const uint32_t *__restrict__ sel, const uint32_t *_
     const uint32_t r = V ? V[p] : p;
     UR[i] = r;
     if (UK) UK[i] = K[p];
-    UL[i] = ends[r] - starts[r] + 1u;
+    UL[i] = spans[r].y - spans[r].x + 1u;
 }
 
 __global__ void k_gather_rl(const uint32_t *__restrict__ idx, const uint32_t *__restrict__ R,
@@ -291,8 +286,7 @@ constexpr uint32_t CP_WAVE_BYTES = 4096;
 // then writes the wave's output span with 16-byte stores; spans wider than the wave's
 // LDS window fall back to per-lane byte copies.
 __global__ __launch_bounds__(256) void k_copy_records(const uint8_t *__restrict__ buf,
-                                                      const uint32_t *__restrict__ starts,
-                                                      const uint32_t *__restrict__ ends,
+                                                      const uint2 *__restrict__ spans,
                                                       const uint32_t *__restrict__ recs,
                                                       const uint64_t *__restrict__ offs, uint32_t n,
                                                       uint8_t *__restrict__ out) {
@@ -303,8 +297,8 @@ __global__ __launch_bounds__(256) void k_copy_records(const uint8_t *__restrict_
     const uint32_t i = wfirst + lane;
     const bool act = i < n;
     const uint32_t r = act ? recs[i] : 0u;
-    const uint32_t s = act ? starts[r] : 0u;
-    const uint32_t len = act ? ends[r] - s : 0u;
+    const uint32_t s = act ? spans[r].x : 0u;
+    const uint32_t len = act ? spans[r].y - s : 0u;
     const uint64_t o = act ? offs[i] : 0ull;
     const uint32_t last = (n - wfirst) < 64u ? (n - wfirst - 1u) : 63u;
     const uint64_t o0 = __shfl(o, 0, 64);
@@ -349,18 +343,17 @@ __global__ __launch_bounds__(256) void k_copy_records(const uint8_t *__restrict_
 }
 
 // Prior check: flag[0] = 1 if records are not strictly increasing.
-__global__ void k_check_sorted(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ starts,
-                               const uint32_t *__restrict__ ends, const uint64_t *__restrict__ K,
+__global__ void k_check_sorted(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, const uint64_t *__restrict__ K,
                                uint32_t n, uint32_t *flag) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x + 1;
     if (i >= n) return;
-    if (key_cmp_full(buf, starts, ends, K[i - 1], i - 1, K[i], i, 0) >= 0) atomicOr(flag, 1u);
+    if (key_cmp_full(buf, spans, K[i - 1], i - 1, K[i], i, 0) >= 0) atomicOr(flag, 1u);
 }
 
 // ------------------------------------------------------------------ diff (merge path)
 struct RecSet {
     const uint8_t *buf;
-    const uint32_t *st, *en;
+    const uint2 *sp;
     const uint32_t *ids;  // position -> record id (null = identity)
     const uint64_t *K;    // key0 per position
     uint32_t n;
@@ -371,7 +364,7 @@ __device__ __forceinline__ int set_cmp(const RecSet &A, uint64_t ka, uint32_t ra
                                        uint32_t rb) {
     if (ka != kb) return ka < kb ? -1 : 1;
     if ((ka & 0xffu) < 8u) return 0;
-    return rec_cmp_k(A.buf, A.st[ra], A.en[ra], B.buf, B.st[rb], B.en[rb], 7);
+    return rec_cmp_k(A.buf, A.sp[ra].x, A.sp[ra].y, B.buf, B.sp[rb].x, B.sp[rb].y, 7);
 }
 
 constexpr uint32_t MP_TILE = 2048;
@@ -424,14 +417,14 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
         bool present = false;
         const bool whole = (ku & 0xffu) < 8u;
         uint32_t ru = 0, us = 0, ue = 0;
-        if (!whole) { ru = U.id(i); us = U.st[ru]; ue = U.en[ru]; }
+        if (!whole) { ru = U.id(i); us = U.sp[ru].x; ue = U.sp[ru].y; }
         for (uint32_t q = j0 + lo; q < P.n; ++q) {
             const uint32_t lq = q - j0;
             const uint64_t kp = (lq < np) ? s_k[lq] : P.K[q];
             if (kp != ku) break;
             if (whole) { present = true; break; }
             const uint32_t rp = (lq < np) ? s_r[lq] : P.id(q);
-            if (rec_equal(U.buf, us, ue, P.buf, P.st[rp], P.en[rp], 7)) { present = true; break; }
+            if (rec_equal(U.buf, us, ue, P.buf, P.sp[rp].x, P.sp[rp].y, 7)) { present = true; break; }
         }
         fresh[i] = present ? 0 : 1;
     }
@@ -443,7 +436,7 @@ int select_flags(sg_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out_idx,
 }
 
 // recs/lens: record ids and serialized lengths (len + 1) in output order.
-static int serialize_dense(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+static int serialize_dense(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                            const uint32_t *recs, const uint32_t *lens, uint32_t count, int out_slot,
                            uint8_t *dst, size_t dst_cap, uint8_t **d_out, uint64_t *bytes) {
     *bytes = 0;
@@ -458,33 +451,32 @@ static int serialize_dense(sg_ctx *c, const uint8_t *d_buf, const uint32_t *star
         SG_TRY(slot(c, out_slot, (size_t)total + 16, d_out));
     }
     // model: each output byte read once and written once, plus id/start/end/offset per record
-    if (count) SG_LAUNCH_B(c, "copy_records", 2.0 * total + 20.0 * count, k_copy_records, grid_for(count, 256), 256, 0, d_buf, starts, ends, recs, offs, count, *d_out);
+    if (count) SG_LAUNCH_B(c, "copy_records", 2.0 * total + 20.0 * count, k_copy_records, grid_for(count, 256), 256, 0, d_buf, spans, recs, offs, count, *d_out);
     *bytes = total;
     return SG_OK;
 }
 
-__global__ void k_lens_of(const uint32_t *__restrict__ recs, const uint32_t *__restrict__ starts,
-                          const uint32_t *__restrict__ ends, uint32_t n, uint32_t *L) {
+__global__ void k_lens_of(const uint32_t *__restrict__ recs, const uint2 *__restrict__ spans, uint32_t n, uint32_t *L) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) { const uint32_t r = recs[i]; L[i] = ends[r] - starts[r] + 1u; }
+    if (i < n) { const uint32_t r = recs[i]; L[i] = spans[r].y - spans[r].x + 1u; }
 }
 
-int serialize(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+int serialize(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
               const uint32_t *recs, const uint32_t * /*map*/, uint32_t count, int out_slot,
               uint8_t **d_out, uint64_t *bytes) {
     uint32_t *L;
     SG_TRY(slot(c, S_M_TMP2, (size_t)count + 1, &L));
-    if (count) SG_LAUNCH(c, "lens", k_lens_of, grid_for(count, 256), 256, 0, recs, starts, ends, count, L);
-    return serialize_dense(c, d_buf, starts, ends, recs, L, count, out_slot, nullptr, 0, d_out, bytes);
+    if (count) SG_LAUNCH(c, "lens", k_lens_of, grid_for(count, 256), 256, 0, recs, spans, count, L);
+    return serialize_dense(c, d_buf, spans, recs, L, count, out_slot, nullptr, 0, d_out, bytes);
 }
 
-int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes) {
     uint32_t *L;
     SG_TRY(slot(c, S_M_TMP2, (size_t)count + 1, &L));
-    if (count) SG_LAUNCH(c, "lens", k_lens_of, grid_for(count, 256), 256, 0, recs, starts, ends, count, L);
+    if (count) SG_LAUNCH(c, "lens", k_lens_of, grid_for(count, 256), 256, 0, recs, spans, count, L);
     uint8_t *o;
-    return serialize_dense(c, d_buf, starts, ends, recs, L, count, 0, dst, dst_cap, &o, bytes);
+    return serialize_dense(c, d_buf, spans, recs, L, count, 0, dst, dst_cap, &o, bytes);
 }
 
 int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet &ss, SortedSet *out) {
@@ -518,7 +510,7 @@ int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet 
         uint8_t *unres;
         SG_TRY(slot(c, S_M_TMP, (size_t)G + 16, &unres));
         // model: per group GS/GE + flag; per member id, start, end and ~26 record bytes twice
-        SG_LAUNCH_B(c, "refine_eq", 9.0 * G + 64.0 * 2.0 * G, k_refine_eq, grid_for(G, 256), 256, 0, d_buf, L.starts, L.ends, GS, GE, G, V, uniq, off, unres);
+        SG_LAUNCH_B(c, "refine_eq", 9.0 * G + 64.0 * 2.0 * G, k_refine_eq, grid_for(G, 256), 256, 0, d_buf, L.spans, GS, GE, G, V, uniq, off, unres);
         uint32_t *ulist;
         SG_TRY(slot(c, S_SEL, (size_t)G + 16, &ulist));
         uint32_t Ux = 0;
@@ -528,7 +520,7 @@ int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet 
         SG_TRY(slot(c, S_R_GID, (size_t)Ux + 16, &GS2));
         SG_TRY(slot(c, S_R_POS, (size_t)Ux + 16, &GE2));
         SG_LAUNCH(c, "gather_groups", k_gather_pair, grid_for(Ux, 256), 256, 0, ulist, GS, GE, Ux, GS2, GE2);
-        SG_LAUNCH(c, "refine_wave", k_refine_wave, grid_for(Ux, 4), 256, 0, d_buf, L.starts, L.ends, GS2, GE2, Ux, V, uniq, off);
+        SG_LAUNCH(c, "refine_wave", k_refine_wave, grid_for(Ux, 4), 256, 0, d_buf, L.spans, GS2, GE2, Ux, V, uniq, off);
         // unresolved groups above one wave -> a radix round on the next chunk
         uint32_t *big;
         SG_TRY(slot(c, S_SEL, Ux + 16, &big));
@@ -550,7 +542,7 @@ int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet 
         SG_TRY(slot(c, S_R_POS, M, &RP));
         SG_TRY(slot(c, S_R_VAL, M, &RV));
         SG_TRY(slot(c, S_R_VAL2, M, &RV2));
-        SG_LAUNCH(c, "round_expand", k_expand, grid_for(M, 256), 256, 0, d_buf, L.starts, L.ends, GS, big, goff, B, V, M, off, RK, RG, RP);
+        SG_LAUNCH(c, "round_expand", k_expand, grid_for(M, 256), 256, 0, d_buf, L.spans, GS, big, goff, B, V, M, off, RK, RG, RP);
         uint64_t *SK;
         uint32_t *perm;
         SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, 64, true, &SK, &perm, "rs_pass_refine"));
@@ -566,7 +558,7 @@ int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet 
         SG_TRY(radix_sort(c, GK, perm, GK2, pv_alt, M, 0, gbits, false, &FKs, &perm2, "rs_pass_refine"));
         T = (perm2 == perm) ? pv_alt : perm;
         uint64_t *FK = (FKs == GK) ? GK2 : GK;
-        SG_LAUNCH(c, "round_gather", k_round_gather, grid_for(M, 256), 256, 0, d_buf, L.starts, L.ends, V, RP, perm2, M, off, T, FK);
+        SG_LAUNCH(c, "round_gather", k_round_gather, grid_for(M, 256), 256, 0, d_buf, L.spans, V, RP, perm2, M, off, T, FK);
         SG_LAUNCH(c, "round_scatter", k_round_scatter, grid_for(M, 256), 256, 0, T, RP, M, V);
         // sub-groups: RG is the group index of final row i as well (same row ranges);
         // perm2/T are free again after the scatter (same stream)
@@ -601,7 +593,7 @@ static int unique_view(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSe
         uint32_t *flag;
         SG_TRY(slot(c, S_M_CNT, 4, &flag));
         SG_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
-        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, uv->L.starts, uv->L.ends, uv->L.keys, R, flag);
+        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, uv->L.spans, uv->L.keys, R, flag);
         uint32_t f = 1;
         SG_TRY(ctx_readback(c, &f, flag, 4));
         trust_sorted = (f == 0);
@@ -622,7 +614,7 @@ static int unique_view(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSe
     SG_TRY(slot(c, ur_slot, (size_t)U + 1, &uv->UR));
     SG_TRY(slot(c, uk_slot, (size_t)U + 1, &uv->UK));
     SG_TRY(slot(c, ul_slot, (size_t)U + 1, &uv->UL));
-    if (U) SG_LAUNCH_B(c, "gather_uniq", 40.0 * U, k_gather_sel, grid_for(U, 256), 256, 0, sel, S.recs, S.keys, uv->L.starts, uv->L.ends, U, uv->UR, uv->UK, uv->UL);
+    if (U) SG_LAUNCH_B(c, "gather_uniq", 40.0 * U, k_gather_sel, grid_for(U, 256), 256, 0, sel, S.recs, S.keys, uv->L.spans, U, uv->UR, uv->UK, uv->UL);
     uv->U = U;
     return SG_OK;
 }
@@ -635,7 +627,7 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     res->in_records = cu.L.n_rec;
     uint8_t *uout;
     uint64_t ubytes = 0;
-    SG_TRY(serialize_dense(c, d_cur, cu.L.starts, cu.L.ends, cu.UR, cu.UL, cu.U, S_OUT_UNIQ, nullptr, 0, &uout, &ubytes));
+    SG_TRY(serialize_dense(c, d_cur, cu.L.spans, cu.UR, cu.UL, cu.U, S_OUT_UNIQ, nullptr, 0, &uout, &ubytes));
     res->uniq = uout;
     res->uniq_bytes = ubytes;
     res->uniq_records = cu.U;
@@ -654,8 +646,8 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     }
     uint8_t *fresh;
     SG_TRY(slot(c, S_M_TMP, (size_t)cu.U + 1, &fresh));
-    RecSet U{d_cur, cu.L.starts, cu.L.ends, cu.UR, cu.UK, cu.U};
-    RecSet P{d_prior, pv.L.starts, pv.L.ends, pv.UR, pv.UK, pv.U};
+    RecSet U{d_cur, cu.L.spans, cu.UR, cu.UK, cu.U};
+    RecSet P{d_prior, pv.L.spans, pv.UR, pv.UK, pv.U};
     const uint32_t ntiles = (uint32_t)(((uint64_t)cu.U + pv.U + MP_TILE - 1) / MP_TILE);
     uint32_t *split;
     SG_TRY(slot(c, S_R_OFF, (size_t)ntiles + 2, &split));
@@ -672,7 +664,7 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     if (F) SG_LAUNCH(c, "gather_fresh", k_gather_rl, grid_for(F, 256), 256, 0, fidx, cu.UR, cu.UL, F, FR, FL);
     uint8_t *fout;
     uint64_t fbytes = 0;
-    SG_TRY(serialize_dense(c, d_cur, cu.L.starts, cu.L.ends, FR, FL, F, S_OUT_FRESH, nullptr, 0, &fout, &fbytes));
+    SG_TRY(serialize_dense(c, d_cur, cu.L.spans, FR, FL, F, S_OUT_FRESH, nullptr, 0, &fout, &fbytes));
     res->fresh = fout;
     res->fresh_bytes = fbytes;
     res->fresh_records = F;

@@ -17,8 +17,7 @@ extern const SlotSet PRIOR_SLOTS;
 
 // A3 parse result (device arrays, n_rec records).
 struct Lines {
-    uint32_t *starts = nullptr;
-    uint32_t *ends = nullptr;
+    uint2 *spans = nullptr;     // (start, end) per record, interleaved: one 8-B load per record
     uint64_t *keys = nullptr;   // chunk_key(rec, 0)
     uint32_t n_rec = 0;
 };
@@ -46,11 +45,11 @@ int select_flags(sg_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out_idx,
 
 // Serialize records (ids into starts/ends, in list order) as '\n'-terminated bytes.
 // rec_of: list[i] is a position into `map` (if map != null) giving the record id.
-int serialize(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+int serialize(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
               const uint32_t *list, const uint32_t *map, uint32_t count, int out_slot,
               uint8_t **d_out, uint64_t *bytes);
 // Same, into a caller buffer of dst_cap bytes (SG_E_CAP if too small).
-int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint32_t *starts, const uint32_t *ends,
+int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes);
 
 }  // namespace sg

@@ -25,8 +25,7 @@ __device__ __forceinline__ uint32_t nl_mask4(uint32_t x) {
 }
 
 __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ buf, uint64_t n,
-                                                    uint32_t *__restrict__ starts,
-                                                    uint32_t *__restrict__ ends,
+                                                    uint2 *__restrict__ spans,
                                                     uint64_t *__restrict__ keys, uint32_t cap,
                                                     uint64_t *status, uint32_t *counter,
                                                     uint32_t ntiles) {
@@ -113,7 +112,7 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
                 if (c == 0x0a && rem == 8) rem = j;
                 if (j < 7 && (uint32_t)j < rem) k |= (uint64_t)c << (56 - 8 * j);
             }
-            starts[si] = (uint32_t)(my0 + b);
+            spans[si].x = (uint32_t)(my0 + b);
             keys[si] = k | rem;
         }
         ++si;
@@ -122,7 +121,7 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
     while (bits) {
         const int b = __ffs(bits) - 1;
         bits &= bits - 1;
-        if (ei < cap) ends[ei] = (uint32_t)(my0 + b);
+        if (ei < cap) spans[ei].y = (uint32_t)(my0 + b);
         ++ei;
     }
 }
@@ -135,14 +134,13 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
     SG_TRY(slot(c, ss.lb, (size_t)ntiles + 2, &status));
     uint32_t *counter = reinterpret_cast<uint32_t *>(status + ntiles);
     uint64_t want = n / 16 + 4096;
-    if (c->slot_cap[ss.starts] / 4 > want) want = c->slot_cap[ss.starts] / 4 - 64;
+    if (c->slot_cap[ss.starts] / 8 > want) want = c->slot_cap[ss.starts] / 8 - 64;
     for (int attempt = 0; attempt < 2; ++attempt) {
         uint32_t cap = (uint32_t)want;
-        SG_TRY(slot(c, ss.starts, cap, &out->starts));
-        SG_TRY(slot(c, ss.ends, cap, &out->ends));
+        SG_TRY(slot(c, ss.starts, cap, &out->spans));
         SG_TRY(slot(c, ss.keys, cap, &out->keys));
         SG_HIP(hipMemsetAsync(status, 0, ((size_t)ntiles + 2) * 8, c->stream));
-        SG_LAUNCH(c, "lines", k_lines, ntiles, LN_BLOCK, 0, d_buf, n, out->starts, out->ends,
+        SG_LAUNCH(c, "lines", k_lines, ntiles, LN_BLOCK, 0, d_buf, n, out->spans,
                   out->keys, cap, status, counter, ntiles);
         uint32_t R = 0;
         SG_TRY(ctx_readback(c, &R, counter + 1, 4));

@@ -229,7 +229,7 @@ static int ensure_device(sg_matcher *h, int dev) {
 // ------------------------------------------------------------------ device: Aho-Corasick
 struct ACArgs {
     const uint8_t *buf;
-    const uint32_t *starts, *ends;
+    const uint2 *spans;
     uint32_t R;
     const uint8_t *cls;
     const uint32_t *delta;
@@ -273,7 +273,8 @@ __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
     __syncthreads();
     const uint32_t *bits = a.bits_in_lds ? s_bits : a.outbits;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.R; r += gridDim.x * blockDim.x) {
-        const uint32_t s = a.starts[r], e = a.ends[r];
+        const uint2 sp_ = a.spans[r];
+        const uint32_t s = sp_.x, e = sp_.y;
         uint32_t st = 0;
         uint32_t seen[4];
         uint32_t nseen = 0;
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
 // ------------------------------------------------------------------ device: regex DFAs
 struct DFAArgs {
     const uint8_t *buf;
-    const uint32_t *starts, *ends;
+    const uint2 *spans;
     uint32_t R;
     const uint8_t *cls;
     const uint32_t *delta;
@@ -337,7 +338,8 @@ __global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
             }
     };
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.R; r += gridDim.x * blockDim.x) {
-        const uint32_t s = a.starts[r], e = a.ends[r];
+        const uint2 sp_ = a.spans[r];
+        const uint32_t s = sp_.x, e = sp_.y;
         uint32_t st = 1;
         accept(r, st);
         for (uint32_t w = s & ~3u; w < e && st != 0; w += 4) {
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
 // first accepting state.
 struct VerifyArgs {
     const uint8_t *buf;
-    const uint32_t *starts, *ends;
+    const uint2 *spans;
     const unsigned long long *cand;
     uint32_t n_cand;
     const uint32_t *s_delta, *s_off, *s_C, *s_eol, *s_acc_off, *single_of_pid;
@@ -379,7 +381,8 @@ __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
     const uint8_t *cls = a.s_cls + 256u * k;
     const uint8_t *acc = a.s_acc + a.s_acc_off[k];
     const uint32_t C = a.s_C[k];
-    const uint32_t s = a.starts[r], e = a.ends[r];
+    const uint2 sp_ = a.spans[r];
+        const uint32_t s = sp_.x, e = sp_.y;
     uint32_t st = 1;
     bool hit = acc[st] != 0;
     for (uint32_t w = s & ~3u; w < e && !hit && st != 0; w += 4) {
@@ -470,7 +473,7 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
             SG_HIP(hipMemsetAsync(cnt + 1, 0, 4, c->stream));
             uint32_t bil, lds, grid;
             geometry(T, D, &bil, &lds, &grid);
-            ACArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
+            ACArgs a{d_buf, L.spans, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                      D.outbits, D.own_off, D.own_ids, D.dict, cand, cnt + 1, (uint32_t)ccap, bil,
                      h->dplan.fac_off, h->dplan.fac_pids};
             SG_LAUNCH_B(c, "re_prefilter", (double)n + 8.0 * R, k_ac_match, grid, 512, lds, a);
@@ -490,19 +493,19 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
                 uint32_t bits_in_lds, lds, grid;
                 geometry(T, D, &bits_in_lds, &lds, &grid);
                 if (h->kind == 0) {
-                    ACArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
+                    ACArgs a{d_buf, L.spans, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                              D.outbits, D.own_off, D.own_ids, D.dict, hits, cnt, (uint32_t)cap, bits_in_lds,
                              nullptr, nullptr};
                     SG_LAUNCH_B(c, "ac_match", (double)n + 8.0 * R, k_ac_match, grid, 512, lds, a);
                 } else {
-                    DFAArgs a{d_buf, L.starts, L.ends, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
+                    DFAArgs a{d_buf, L.spans, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                               T.anchored_eol, D.outbits, D.own_off, D.own_ids, hits, cnt, (uint32_t)cap, bits_in_lds};
                     SG_LAUNCH_B(c, "dfa_match", (double)n + 8.0 * R, k_dfa_match, grid, 512, lds, a);
                 }
             }
             if (n_cand) {
                 const auto &p = h->dplan;
-                VerifyArgs v{d_buf, L.starts, L.ends, cand, n_cand, p.s_delta, p.s_off, p.s_C, p.s_eol,
+                VerifyArgs v{d_buf, L.spans, cand, n_cand, p.s_delta, p.s_off, p.s_C, p.s_eol,
                              p.s_acc_off, p.single_of_pid, p.s_cls, p.s_acc, hits, cnt, (uint32_t)cap};
                 SG_LAUNCH_B(c, "re_verify", n_cand * (16.0 + (double)n / R), k_verify, (n_cand + 255) / 256, 256, 0, v);
             }
@@ -542,7 +545,7 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
     if (M) SG_LAUNCH(c, "rec_of", k_rec_of, (M + 255) / 256, 256, 0, KK, sel, M, mrec);
     uint8_t *lines;
     uint64_t lb = 0;
-    SG_TRY(serialize(c, d_buf, L.starts, L.ends, mrec, nullptr, M, S_M_LINES, &lines, &lb));
+    SG_TRY(serialize(c, d_buf, L.spans, mrec, nullptr, M, S_M_LINES, &lines, &lb));
     res->lines = lines;
     res->lines_bytes = lb;
     res->matched_records = M;
