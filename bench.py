@@ -126,6 +126,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lines", type=int, default=10_000_000)
     ap.add_argument("--workload", choices=["c2", "c3"], default="c2")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL) for real runs; gloo rehearses N ranks on fewer GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     args = ap.parse_args()
@@ -141,8 +143,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)

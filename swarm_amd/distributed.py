@@ -27,6 +27,9 @@ def exchange_records(send: torch.Tensor, part_bytes: Sequence[int], group=None) 
     world = dist.get_world_size(group)
     if len(part_bytes) != world:
         raise ValueError("part_bytes has %d entries for world size %d" % (len(part_bytes), world))
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        # rehearsal mode (several ranks sharing one GPU): the collective runs on host copies
+        return exchange_records(send.cpu(), part_bytes, group).to(send.device)
     dev = send.device
     in_splits = torch.tensor(list(part_bytes), dtype=torch.int64, device=dev)
     out_splits = torch.empty_like(in_splits)

@@ -1,0 +1,83 @@
+"""Multi-rank rehearsal on one GPU: 2 ranks share cuda:0, exchange over gloo (host copies),
+and run the real GPU partition (sg_dev_partition), the exchange
+(swarm_amd.distributed.exchange_records) and the per-rank dedup+diff. The union of the
+ranks' outputs must equal the oracle on the concatenated input, and every rank may only
+hold records that hash to it."""
+import os
+import socket
+
+import pytest
+
+from hash_oracle import hash64, part_of
+from oracle import semantics as S
+
+pytestmark = pytest.mark.gpu
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def inputs(world):
+    from swarm_amd import corpus
+    shards = [corpus.subdomains(40_000, seed=500 + r, universe=40_000 * world) for r in range(world)]
+    return shards
+
+
+def worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import swarm_amd
+    from swarm_amd import corpus
+    from swarm_amd import distributed as D
+    shards = inputs(world)
+    buf, ids = shards[rank]
+    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    u = np.unique(ids)
+    cand = corpus._flatten(*corpus.render_names(u[(u % np.uint64(10)) != 0]))
+    prior = D.build_prior_partition(ctx, torch.from_numpy(cand).cuda())
+    cur = torch.from_numpy(buf).cuda()
+    r, recv = D.dedup_diff_step(ctx, cur, prior)
+    torch.cuda.synchronize()
+    q.put((rank, ctx.to_bytes(r.uniq, r.uniq_bytes), ctx.to_bytes(r.fresh, r.fresh_bytes),
+           bytes(prior.cpu().numpy().tobytes())))
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_on_one_gpu():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    import numpy as np
+    from swarm_amd import corpus
+    shards = inputs(world)
+    full = b"".join(b.tobytes() for b, _ in shards)
+    all_ids = np.concatenate([i for _, i in shards])
+    prior_full = corpus.prior_of(all_ids).tobytes()
+    eu, ef = S.dedup_diff(full, prior_full)
+    for rank, u, f, p in res:
+        for rec in S.parse_records(u) + S.parse_records(p):
+            assert part_of(hash64(rec), world) == rank
+    u_all = sorted(rec for _, u, _, _ in res for rec in S.parse_records(u))
+    f_all = sorted(rec for _, _, f, _ in res for rec in S.parse_records(f))
+    assert S.serialize(u_all) == eu
+    assert S.serialize(f_all) == ef
