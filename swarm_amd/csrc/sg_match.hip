@@ -62,6 +62,20 @@ struct sg_matcher {
         uint32_t H = 0;
     };
     std::vector<DevTable> dtabs;
+    // hashed q-gram literal filter (used instead of the automaton when it does not fit LDS)
+    struct Lit {
+        bool on = false;
+        bool nocase = false;
+        uint32_t cls_mask = 0;           // bit L-1: some pattern has prefix class L (1..4)
+        uint32_t bits[4] = {0, 0, 0, 0}; // log2 bitmap size per class
+        uint32_t bm_off[4] = {0, 0, 0, 0}, bk_base[4] = {0, 0, 0, 0};
+        std::vector<uint32_t> bitmap, bk_off, bk_ids, pat_off;
+        std::vector<uint8_t> pat;
+        uint32_t *d_bitmap = nullptr, *d_bk_off = nullptr, *d_bk_ids = nullptr, *d_pat_off = nullptr;
+        uint8_t *d_pat = nullptr;
+    };
+    Lit lit;      // literal signatures
+    Lit prelit;   // regex prefilter factors
     std::mutex mu;
 };
 
@@ -158,6 +172,72 @@ static int build_ac(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint3
     return SG_OK;
 }
 
+// ------------------------------------------------------------------ hashed q-gram literal filter
+// Prefix class L = min(len, 4). Classes 1 and 2 index exactly (256 / 65,536 buckets);
+// classes 3 and 4 hash the prefix (multiplicative) into 2^bits buckets. A bitmap per
+// class (LDS-resident) says which buckets hold patterns; a CSR per class lists them.
+__host__ __device__ __forceinline__ uint32_t lit_h(uint32_t key, uint32_t L, uint32_t bits) {
+    return (L <= 2) ? key : (uint32_t)((key * 0x9E3779B1u) >> (32u - bits));
+}
+
+static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags, sg_matcher::Lit *T) {
+    const bool nocase = flags & SG_NOCASE;
+    auto fold = [&](uint8_t b) -> uint8_t { return (nocase && b >= 'A' && b <= 'Z') ? (uint8_t)(b + 32) : b; };
+    T->on = true;
+    T->nocase = nocase;
+    T->pat.clear();
+    T->pat_off.assign(1, 0);
+    uint32_t cnt[5] = {0, 0, 0, 0, 0};
+    for (uint32_t i = 0; i < n; ++i) {
+        if (offs[i + 1] <= offs[i]) { set_error("signature %u is empty", i); return SG_E_INVAL; }
+        for (uint32_t p = offs[i]; p < offs[i + 1]; ++p) {
+            if (pats[p] == '\n') { set_error("signature %u contains a newline", i); return SG_E_INVAL; }
+            T->pat.push_back(fold(pats[p]));
+        }
+        T->pat_off.push_back((uint32_t)T->pat.size());
+        cnt[std::min<uint32_t>(offs[i + 1] - offs[i], 4)]++;
+    }
+    uint32_t words = 0, buckets = 0;
+    T->cls_mask = 0;
+    for (uint32_t L = 1; L <= 4; ++L) {
+        uint32_t b = 0;
+        if (cnt[L]) {
+            T->cls_mask |= 1u << (L - 1);
+            if (L <= 2) {
+                b = 8 * L;
+            } else {
+                b = 10;
+                while (b < (L == 4 ? 18u : 16u) && (1ull << b) < 64ull * cnt[L]) ++b;
+            }
+        }
+        T->bits[L - 1] = b;
+        T->bm_off[L - 1] = words;
+        T->bk_base[L - 1] = buckets;
+        if (cnt[L]) {
+            words += std::max<uint32_t>((1u << b) / 32, 1);
+            buckets += (1u << b) + 1;
+        }
+    }
+    T->bitmap.assign(words, 0);
+    std::vector<uint32_t> count(buckets + 1, 0), hid(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t len = T->pat_off[i + 1] - T->pat_off[i];
+        const uint32_t L = std::min<uint32_t>(len, 4);
+        uint32_t key = 0;
+        for (uint32_t j = 0; j < L; ++j) key |= (uint32_t)T->pat[T->pat_off[i] + j] << (8 * j);
+        const uint32_t h = lit_h(key, L, T->bits[L - 1]);
+        T->bitmap[T->bm_off[L - 1] + (h >> 5)] |= 1u << (h & 31);
+        hid[i] = T->bk_base[L - 1] + h;
+        count[hid[i]]++;
+    }
+    T->bk_off.assign(buckets + 1, 0);
+    for (uint32_t b = 0; b < buckets; ++b) T->bk_off[b + 1] = T->bk_off[b] + count[b];
+    T->bk_ids.assign(n, 0);
+    std::vector<uint32_t> fillp(T->bk_off.begin(), T->bk_off.end() - 1);
+    for (uint32_t i = 0; i < n; ++i) T->bk_ids[fillp[hid[i]]++] = i;
+    return SG_OK;
+}
+
 template <class T>
 static int upload_vec(const std::vector<T> &v, T **d) {
     const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
@@ -177,6 +257,13 @@ static void free_dev(sg_matcher *h) {
                     (void *)p.s_eol, (void *)p.s_acc_off, (void *)p.single_of_pid, (void *)p.s_cls, (void *)p.s_acc})
         if (q) (void)hipFree(q);
     h->dplan = sg_matcher::DevPlan{};
+    for (sg_matcher::Lit *L : {&h->lit, &h->prelit}) {
+        for (void *q : {(void *)L->d_bitmap, (void *)L->d_bk_off, (void *)L->d_bk_ids, (void *)L->d_pat_off,
+                        (void *)L->d_pat})
+            if (q) (void)hipFree(q);
+        L->d_bitmap = L->d_bk_off = L->d_bk_ids = L->d_pat_off = nullptr;
+        L->d_pat = nullptr;
+    }
     h->dev = -1;
 }
 
@@ -198,10 +285,17 @@ static int ensure_device(sg_matcher *h, int dev) {
         SG_TRY(upload_vec(h->s_cls, &p.s_cls));
         SG_TRY(upload_vec(h->s_acc, &p.s_acc));
     }
+    for (sg_matcher::Lit *L : {&h->lit, &h->prelit}) {
+        if (!L->on) continue;
+        SG_TRY(upload_vec(L->bitmap, &L->d_bitmap));
+        SG_TRY(upload_vec(L->bk_off, &L->d_bk_off));
+        SG_TRY(upload_vec(L->bk_ids, &L->d_bk_ids));
+        SG_TRY(upload_vec(L->pat_off, &L->d_pat_off));
+        SG_TRY(upload_vec(L->pat, &L->d_pat));
+    }
     // tables[]: the automata scanned over every record; the prefilter AC goes last
     std::vector<sg_matcher::Table *> all;
     for (auto &T : h->tables) all.push_back(&T);
-    if (h->has_pre) all.push_back(&h->pre);
     for (auto *Tp : all) {
         auto &T = *Tp;
         sg_matcher::DevTable d;
@@ -291,6 +385,100 @@ __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
                         for (uint32_t q = a.own_off[t]; q < a.own_off[t + 1]; ++q) emit_hit(a, r, a.own_ids[q], seen, nseen);
                 }
             }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ device: literal filter
+struct LitArgs {
+    const uint8_t *buf;
+    const uint2 *spans;
+    uint32_t R;
+    const uint32_t *bitmap;
+    uint32_t bm_words, cls_mask, nocase;
+    uint32_t bits[4], bm_off[4], bk_base[4];
+    const uint32_t *bk_off, *bk_ids, *pat_off;
+    const uint8_t *pat;
+    unsigned long long *hits;
+    uint32_t *hit_count;
+    uint32_t cap;
+    const uint32_t *fac_off, *fac_pids;  // regex prefilter expansion (else null)
+};
+
+__device__ __forceinline__ uint32_t fold4(uint32_t w) {
+    // ASCII 'A'..'Z' -> 'a'..'z' in each byte (SWAR)
+    const uint32_t h7 = w & 0x7f7f7f7fu;
+    const uint32_t ge_a = h7 + 0x3f3f3f3fu;  // high bit: byte >= 'A'
+    const uint32_t gt_z = h7 + 0x25252525u;  // high bit: byte > 'Z'
+    const uint32_t up = ge_a & ~gt_z & ~w & 0x80808080u;
+    return w | (up >> 2);
+}
+
+__device__ __forceinline__ void emit_pair(unsigned long long *hits, uint32_t *hit_count, uint32_t cap,
+                                          const uint32_t *fac_off, const uint32_t *fac_pids, uint32_t rec,
+                                          uint32_t sig, uint32_t *seen, uint32_t &nseen) {
+    for (uint32_t q = 0; q < nseen; ++q)
+        if (seen[q] == sig) return;
+    if (nseen < 4) seen[nseen++] = sig;
+    if (fac_off) {
+        for (uint32_t q = fac_off[sig]; q < fac_off[sig + 1]; ++q) {
+            const uint32_t slot_i = atomicAdd(hit_count, 1u);
+            if (slot_i < cap) hits[slot_i] = ((unsigned long long)rec << 32) | fac_pids[q];
+        }
+        return;
+    }
+    const uint32_t slot_i = atomicAdd(hit_count, 1u);
+    if (slot_i < cap) hits[slot_i] = ((unsigned long long)rec << 32) | sig;
+}
+
+// One thread per record. At every byte position p the next min(r, 4) bytes (r = bytes
+// left in the record) form the prefix key of each present class; a set bit in that
+// class's LDS bitmap triggers the byte compare of the patterns in the bucket.
+__global__ __launch_bounds__(512) void k_lit_match(LitArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_bm[];
+    for (uint32_t q = threadIdx.x; q < a.bm_words; q += blockDim.x) s_bm[q] = a.bitmap[q];
+    __syncthreads();
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.R; r += gridDim.x * blockDim.x) {
+        const uint2 sp = a.spans[r];
+        const uint32_t s = sp.x, e = sp.y;
+        uint32_t seen[4];
+        uint32_t nseen = 0;
+        const uint32_t a0 = s & ~3u;
+        uint32_t w0 = *reinterpret_cast<const uint32_t *>(a.buf + a0);
+        uint32_t w1 = (a0 + 4 < e) ? *reinterpret_cast<const uint32_t *>(a.buf + a0 + 4) : 0u;
+        if (a.nocase) { w0 = fold4(w0); w1 = fold4(w1); }
+        for (uint32_t q = a0; q < e; q += 4) {
+            const uint64_t win = (uint64_t)w0 | ((uint64_t)w1 << 32);
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t p = q + b;
+                if (p < s || p >= e) continue;
+                const uint32_t rem = e - p;
+                const uint32_t key4 = (uint32_t)(win >> (8 * b));
+#pragma unroll
+                for (uint32_t L = 1; L <= 4; ++L) {
+                    if (!((a.cls_mask >> (L - 1)) & 1u) || rem < L) continue;
+                    const uint32_t key = (L == 4) ? key4 : (key4 & ((1u << (8 * L)) - 1u));
+                    const uint32_t h = lit_h(key, L, a.bits[L - 1]);
+                    if (!((s_bm[a.bm_off[L - 1] + (h >> 5)] >> (h & 31)) & 1u)) continue;
+                    const uint32_t bk = a.bk_base[L - 1] + h;
+                    for (uint32_t i = a.bk_off[bk]; i < a.bk_off[bk + 1]; ++i) {
+                        const uint32_t pid = a.bk_ids[i];
+                        const uint32_t ps = a.pat_off[pid], pl = a.pat_off[pid + 1] - ps;
+                        if (pl > rem || (pl < 4) != (L < 4)) continue;
+                        bool eq = true;
+                        for (uint32_t j = 0; j < pl && eq; ++j) {
+                            uint32_t c = a.buf[p + j];
+                            if (a.nocase && c >= 'A' && c <= 'Z') c += 32;
+                            eq = c == a.pat[ps + j];
+                        }
+                        if (eq) emit_pair(a.hits, a.hit_count, a.cap, a.fac_off, a.fac_pids, r, pid, seen, nseen);
+                    }
+                }
+            }
+            w0 = w1;
+            w1 = (q + 8 < e) ? *reinterpret_cast<const uint32_t *>(a.buf + q + 8) : 0u;
+            if (a.nocase) w1 = fold4(w1);
         }
     }
 }
@@ -464,19 +652,25 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
     // prefilter candidates (regex plans): factor AC -> (record, pattern) pairs
     unsigned long long *cand = nullptr;
     uint32_t n_cand = 0;
+    auto lit_args = [&](const sg_matcher::Lit &Lt, unsigned long long *out, uint32_t *counter, uint32_t ocap,
+                        const uint32_t *fo, const uint32_t *fp) {
+        LitArgs a{};
+        a.buf = d_buf; a.spans = L.spans; a.R = R;
+        a.bitmap = Lt.d_bitmap; a.bm_words = (uint32_t)Lt.bitmap.size(); a.cls_mask = Lt.cls_mask;
+        a.nocase = Lt.nocase ? 1u : 0u;
+        for (int k = 0; k < 4; ++k) { a.bits[k] = Lt.bits[k]; a.bm_off[k] = Lt.bm_off[k]; a.bk_base[k] = Lt.bk_base[k]; }
+        a.bk_off = Lt.d_bk_off; a.bk_ids = Lt.d_bk_ids; a.pat_off = Lt.d_pat_off; a.pat = Lt.d_pat;
+        a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
+        return a;
+    };
+    const uint32_t lgrid = std::min<uint32_t>((R + 511) / 512, 256u * 8u);
     if (h->has_pre && R) {
-        const auto &T = h->pre;
-        const auto &D = h->dtabs.back();
         uint64_t ccap = std::max<uint64_t>(1u << 20, (uint64_t)R);
         for (int attempt = 0; attempt < 2; ++attempt) {
             SG_TRY(slot(c, S_PART, ccap, &cand));
             SG_HIP(hipMemsetAsync(cnt + 1, 0, 4, c->stream));
-            uint32_t bil, lds, grid;
-            geometry(T, D, &bil, &lds, &grid);
-            ACArgs a{d_buf, L.spans, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
-                     D.outbits, D.own_off, D.own_ids, D.dict, cand, cnt + 1, (uint32_t)ccap, bil,
-                     h->dplan.fac_off, h->dplan.fac_pids};
-            SG_LAUNCH_B(c, "re_prefilter", (double)n + 8.0 * R, k_ac_match, grid, 512, lds, a);
+            LitArgs a = lit_args(h->prelit, cand, cnt + 1, (uint32_t)ccap, h->dplan.fac_off, h->dplan.fac_pids);
+            SG_LAUNCH_B(c, "re_prefilter", (double)n + 8.0 * R, k_lit_match, lgrid, 512, a.bm_words * 4, a);
             SG_TRY(ctx_readback(c, &n_cand, cnt + 1, 4));
             if (n_cand <= ccap) break;
             ccap = (uint64_t)n_cand + 1024;
@@ -486,6 +680,10 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
     for (int attempt = 0; attempt < 2; ++attempt) {
         SG_TRY(slot(c, S_M_HITS, cap, &hits));
         SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
+        if (R && h->lit.on) {
+            LitArgs a = lit_args(h->lit, hits, cnt, (uint32_t)cap, nullptr, nullptr);
+            SG_LAUNCH_B(c, "lit_match", (double)n + 8.0 * R, k_lit_match, lgrid, 512, a.bm_words * 4, a);
+        }
         if (R) {
             for (size_t ti = 0; ti < h->tables.size(); ++ti) {
                 const auto &T = h->tables[ti];
@@ -566,6 +764,15 @@ int sg_ac_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats
     int rc = build_ac(pats, pat_offs, n_pats, flags, &m->tables[0]);
     if (rc != SG_OK) { delete m; return rc; }
     m->total_states = m->tables[0].n_states;
+    // An automaton whose rows all fit the LDS hot table walks at LDS speed; a larger one
+    // would chase dependent HBM/L2 rows on every byte, so it is replaced by the hashed
+    // q-gram filter (independent per-position probes, byte compares on bitmap hits).
+    const auto &T = m->tables[0];
+    if ((uint64_t)T.n_states * T.n_classes * 2 > AC_HOT_BYTES || getenv("SG_FORCE_LITFILTER")) {
+        rc = build_lit(pats, pat_offs, n_pats, flags, &m->lit);
+        if (rc != SG_OK) { delete m; return rc; }
+        m->tables.clear();
+    }
     *h = m;
     return SG_OK;
 }
@@ -587,7 +794,7 @@ int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pat
             blob.insert(blob.end(), f.begin(), f.end());
             offs.push_back((uint32_t)blob.size());
         }
-        rc = build_ac(blob.data(), offs.data(), (uint32_t)plan.factors.size(), SG_NOCASE, &m->pre);
+        rc = build_lit(blob.data(), offs.data(), (uint32_t)plan.factors.size(), SG_NOCASE, &m->prelit);
         if (rc != SG_OK) { delete m; return rc; }
         m->has_pre = true;
         m->fac_off = plan.fac_off;
@@ -604,7 +811,6 @@ int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pat
             m->total_states += d.n_states;
         }
         m->n_singles = (uint32_t)plan.singles.size();
-        m->total_states += m->pre.n_states;
     }
     for (auto &d : plan.groups) {
         sg_matcher::Table T;

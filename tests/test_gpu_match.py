@@ -18,11 +18,17 @@ WORDS = [base64.b64decode(w) for w in SIG["words"]]
 REGEXES = [base64.b64decode(r["p"]) for r in SIG["regexes"] if r["dfa_rc"] == 0]
 
 
-@pytest.fixture(scope="module")
-def sg():
+@pytest.fixture(scope="module", params=["auto", "litfilter"])
+def sg(request):
+    """Run every literal test with the engine the compiler picks and with the hashed
+    q-gram filter forced (SG_FORCE_LITFILTER is read at compile time)."""
+    import os
     import swarm_amd
     assert swarm_amd.device_count() > 0
-    return swarm_amd
+    if request.param == "litfilter":
+        os.environ["SG_FORCE_LITFILTER"] = "1"
+    yield swarm_amd
+    os.environ.pop("SG_FORCE_LITFILTER", None)
 
 
 @pytest.mark.parametrize("case", GR["literal"], ids=lambda c: c["name"])
