@@ -108,11 +108,12 @@ def bench_c3(args):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (httpx-style lines, 1 % planted signatures, SURVEY.md §8(d) C3)",
-        "config": {"workload": "C3: %dM httpx lines x 2000 literal signatures (Aho-Corasick), 1 GPU" % (n_lines // 1_000_000),
+        "config": {"workload": "C3: %dM httpx lines x 2000 literal signatures, 1 GPU" % (n_lines // 1_000_000),
+                   "engine": "lit_match" if "lit_match" in stats else "ac_match",
                    "bytes": int(d.numel()), "automaton_states": m.info()["states"]},
         "gbps": round(d.numel() * args.steps / el / 1e9, 2),
         "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records)},
-        "roofline": roofline_of(stats, "ac_match"),
+        "roofline": roofline_of(stats, "lit_match" if "lit_match" in stats else "ac_match"),
         "cpu_baseline": cpu,
         "kernels": kernel_table(stats),
     }), flush=True)

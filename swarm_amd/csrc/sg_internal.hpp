@@ -18,11 +18,15 @@ extern const SlotSet PRIOR_SLOTS;
 // A3 parse result (device arrays, n_rec records).
 struct Lines {
     uint2 *spans = nullptr;     // (start, end) per record, interleaved: one 8-B load per record
-    uint64_t *keys = nullptr;   // chunk_key(rec, 0)
+    uint64_t *keys = nullptr;   // chunk_key(rec, 0) (null when not requested)
     uint32_t n_rec = 0;
+    // Look-back status of the parse: tile_prefix[t] & LB_VAL_MASK is the inclusive packed
+    // (starts << 31 | ends) count through tile t of tile_bytes bytes each.
+    const uint64_t *tile_prefix = nullptr;
+    uint32_t tile_bytes = 0, n_tiles = 0;
 };
 // Split d_buf (16-byte aligned device pointer, n bytes) into non-empty records.
-int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out);
+int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys = true);
 
 // LSD radix sort of (u64 key, u32 val) pairs on bits [begin_bit, end_bit), stable.
 // Ping-pongs between (keys, vals) and (keys_alt, vals_alt); returns the final arrays.

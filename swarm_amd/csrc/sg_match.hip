@@ -66,13 +66,23 @@ struct sg_matcher {
     struct Lit {
         bool on = false;
         bool nocase = false;
-        uint32_t cls_mask = 0;           // bit L-1: some pattern has prefix class L (1..4)
-        uint32_t bits[4] = {0, 0, 0, 0}; // log2 bitmap size per class
-        uint32_t bm_off[4] = {0, 0, 0, 0}, bk_base[4] = {0, 0, 0, 0};
-        std::vector<uint32_t> bitmap, bk_off, bk_ids, pat_off;
-        std::vector<uint8_t> pat;
-        uint32_t *d_bitmap = nullptr, *d_bk_off = nullptr, *d_bk_ids = nullptr, *d_pat_off = nullptr;
-        uint8_t *d_pat = nullptr;
+        uint32_t cls_mask = 0;               // bit c: some pattern is filed in class c (LIT_CLASSES)
+        uint32_t tmpl = 0;                   // class set the scan kernel is compiled for
+        uint32_t bits[5] = {0, 0, 0, 0, 0};  // log2 bitmap size per class
+        uint32_t bm_off[5] = {0, 0, 0, 0, 0};
+        std::vector<uint32_t> bitmap;        // all classes, word-concatenated
+        std::vector<uint16_t> rank;          // per bitmap word: set bits in earlier words of its class
+        uint32_t rank_base[5] = {0, 0, 0, 0, 0};  // entries (buckets) of all earlier classes
+        std::vector<uint32_t> eoff;          // per non-empty bucket: entry range (CSR)
+        std::vector<uint32_t> efp;           // per entry: gram fingerprint (the gram itself for L <= 4)
+        std::vector<uint32_t> einfo;         // per entry: {pid, anchor, len, 16-B pattern row}
+        std::vector<uint32_t> brec;          // per bucket: {fp, pid, len | anchor << 24, row | more << 31}
+        std::vector<uint32_t> pat_off;       // per pattern (n + 1), into pat
+        std::vector<uint8_t> pat;            // folded pattern bytes
+        std::vector<uint8_t> pat16;          // folded pattern bytes, each padded to 16 B rows
+        uint32_t *d_bitmap = nullptr, *d_eoff = nullptr, *d_efp = nullptr, *d_einfo = nullptr, *d_brec = nullptr;
+        uint16_t *d_rank = nullptr;
+        uint8_t *d_pat16 = nullptr;
     };
     Lit lit;      // literal signatures
     Lit prelit;   // regex prefilter factors
@@ -173,11 +183,40 @@ static int build_ac(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint3
 }
 
 // ------------------------------------------------------------------ hashed q-gram literal filter
-// Prefix class L = min(len, 4). Classes 1 and 2 index exactly (256 / 65,536 buckets);
-// classes 3 and 4 hash the prefix (multiplicative) into 2^bits buckets. A bitmap per
-// class (LDS-resident) says which buckets hold patterns; a CSR per class lists them.
-__host__ __device__ __forceinline__ uint32_t lit_h(uint32_t key, uint32_t L, uint32_t bits) {
-    return (L <= 2) ? key : (uint32_t)((key * 0x9E3779B1u) >> (32u - bits));
+// Every pattern is filed under ONE gram, in one of five classes (LIT_CLASSES):
+//   len 1, 2, 3   -> the whole pattern (classes 1 and 2 index exactly, 3 hashes);
+//   len 4..7      -> one of its 4-byte grams (hashed);
+//   len >= 8      -> one of its 8-byte grams (hashed).
+// The anchor offset is chosen per pattern to balance the buckets and to avoid bytes that
+// are frequent in banners (shared prefixes such as "https://" would otherwise pile up and
+// be confirmed at every line). Device side: one LDS bitmap bit per (class, bucket); a set
+// bit is confirmed against the bucket's entry fingerprints (rank + CSR, in LDS), then the
+// whole pattern is byte-compared.
+constexpr uint32_t LIT_CLASSES = 5;
+__host__ __device__ constexpr uint32_t lit_len(uint32_t c) { return c < 4 ? c + 1 : 8; }
+// class-set templates of k_lit_scan: {4-7, 8+}, {3, 4-7, 8+}, all
+static uint32_t lit_template(uint32_t cls_mask) {
+    if ((cls_mask & ~0x18u) == 0) return 0x18u;
+    if ((cls_mask & ~0x1Cu) == 0) return 0x1Cu;
+    return 0x1Fu;
+}
+
+__host__ __device__ __forceinline__ uint32_t lit_h(uint32_t lo, uint32_t hi, uint32_t c, uint32_t bits) {
+    if (c <= 1) return lo;
+    const uint32_t k = (c == 4) ? (lo ^ ((hi << 13) | (hi >> 19))) : lo;
+    return (k * 0x9E3779B1u) >> (32u - bits);
+}
+__host__ __device__ __forceinline__ uint32_t lit_fp(uint32_t lo, uint32_t hi, uint32_t c) {
+    return (c == 4) ? (lo ^ ((hi << 13) | (hi >> 19)) ^ (hi * 0xC2B2AE35u)) : lo;
+}
+
+static uint32_t gram_commonness(const uint8_t *g, uint32_t L) {
+    // bytes that are frequent in banners / HTTP lines make poor anchors
+    static const char *freq = " etaoinsrhldcu/.:-_=<>\"'0123456789";
+    uint32_t s = 0;
+    for (uint32_t j = 0; j < L; ++j)
+        if (g[j] && strchr(freq, g[j])) ++s;
+    return s;
 }
 
 static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags, sg_matcher::Lit *T) {
@@ -187,7 +226,8 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
     T->nocase = nocase;
     T->pat.clear();
     T->pat_off.assign(1, 0);
-    uint32_t cnt[5] = {0, 0, 0, 0, 0};
+    auto cls_of_len = [](uint32_t len) -> uint32_t { return len < 4 ? len - 1 : (len < 8 ? 3u : 4u); };
+    uint32_t cnt[LIT_CLASSES] = {};
     for (uint32_t i = 0; i < n; ++i) {
         if (offs[i + 1] <= offs[i]) { set_error("signature %u is empty", i); return SG_E_INVAL; }
         for (uint32_t p = offs[i]; p < offs[i + 1]; ++p) {
@@ -195,46 +235,119 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
             T->pat.push_back(fold(pats[p]));
         }
         T->pat_off.push_back((uint32_t)T->pat.size());
-        cnt[std::min<uint32_t>(offs[i + 1] - offs[i], 4)]++;
+        cnt[cls_of_len(offs[i + 1] - offs[i])]++;
     }
-    uint32_t words = 0, buckets = 0;
+    uint32_t words = 0;
     T->cls_mask = 0;
-    for (uint32_t L = 1; L <= 4; ++L) {
+    for (uint32_t c = 0; c < LIT_CLASSES; ++c) {
         uint32_t b = 0;
-        if (cnt[L]) {
-            T->cls_mask |= 1u << (L - 1);
-            if (L <= 2) {
-                b = 8 * L;
+        if (cnt[c]) {
+            T->cls_mask |= 1u << c;
+            if (c <= 1) {
+                b = 8 * (c + 1);
             } else {
                 b = 10;
-                while (b < (L == 4 ? 18u : 16u) && (1ull << b) < 64ull * cnt[L]) ++b;
+                static const uint32_t cap4 = getenv("SG_LIT_BITS4") ? (uint32_t)atoi(getenv("SG_LIT_BITS4")) : 16u;
+                while (b < (c == 2 ? 15u : cap4) && (1ull << b) < 64ull * cnt[c]) ++b;
             }
         }
-        T->bits[L - 1] = b;
-        T->bm_off[L - 1] = words;
-        T->bk_base[L - 1] = buckets;
-        if (cnt[L]) {
-            words += std::max<uint32_t>((1u << b) / 32, 1);
-            buckets += (1u << b) + 1;
-        }
+        T->bits[c] = b;
+        T->bm_off[c] = words;
+        if (cnt[c]) words += std::max<uint32_t>((1u << b) / 32, 1);
+    }
+    // The scan kernel is compiled for a superset of the present classes (lit_template);
+    // a class of the superset with no pattern probes an all-zero region of its size.
+    T->tmpl = lit_template(T->cls_mask);
+    for (uint32_t c = 0; c < LIT_CLASSES; ++c) {
+        if (cnt[c] || !((T->tmpl >> c) & 1u)) continue;
+        T->bits[c] = (c <= 1) ? 8 * (c + 1) : 5;
+        T->bm_off[c] = words;
+        words += std::max<uint32_t>((1u << T->bits[c]) / 32, 1);
     }
     T->bitmap.assign(words, 0);
-    std::vector<uint32_t> count(buckets + 1, 0), hid(n);
+    auto word_at = [&](uint32_t i, uint32_t o, uint32_t L) {
+        uint32_t key = 0;
+        for (uint32_t j = 0; j < L && j < 4; ++j) key |= (uint32_t)T->pat[T->pat_off[i] + o + j] << (8 * j);
+        return key;
+    };
+    // anchors: shortest patterns (fewest choices) first, each on its least-loaded gram
+    std::vector<uint32_t> anc(n, 0), cls(n), hb(n), fp(n);
+    std::vector<uint32_t> order;
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t len = T->pat_off[i + 1] - T->pat_off[i];
-        const uint32_t L = std::min<uint32_t>(len, 4);
-        uint32_t key = 0;
-        for (uint32_t j = 0; j < L; ++j) key |= (uint32_t)T->pat[T->pat_off[i] + j] << (8 * j);
-        const uint32_t h = lit_h(key, L, T->bits[L - 1]);
-        T->bitmap[T->bm_off[L - 1] + (h >> 5)] |= 1u << (h & 31);
-        hid[i] = T->bk_base[L - 1] + h;
-        count[hid[i]]++;
+        cls[i] = cls_of_len(len);
+        order.push_back(i);
     }
-    T->bk_off.assign(buckets + 1, 0);
-    for (uint32_t b = 0; b < buckets; ++b) T->bk_off[b + 1] = T->bk_off[b] + count[b];
-    T->bk_ids.assign(n, 0);
-    std::vector<uint32_t> fillp(T->bk_off.begin(), T->bk_off.end() - 1);
-    for (uint32_t i = 0; i < n; ++i) T->bk_ids[fillp[hid[i]]++] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+        return T->pat_off[x + 1] - T->pat_off[x] < T->pat_off[y + 1] - T->pat_off[y];
+    });
+    std::vector<std::vector<uint32_t>> load(LIT_CLASSES);
+    for (uint32_t c = 0; c < LIT_CLASSES; ++c) load[c].assign(cnt[c] ? (1u << T->bits[c]) : 1, 0);
+    for (uint32_t i : order) {
+        const uint32_t len = T->pat_off[i + 1] - T->pat_off[i];
+        const uint32_t c = cls[i], L = lit_len(c);
+        const uint32_t last = (c < 3) ? 0 : len - L;
+        uint64_t best = ~0ull;
+        for (uint32_t o = 0; o <= last && o < 256; ++o) {  // anchor fits the bucket record's 8 bits
+            const uint32_t lo = word_at(i, o, L), hi = (L == 8) ? word_at(i, o + 4, 4) : 0u;
+            const uint32_t h = lit_h(lo, hi, c, T->bits[c]);
+            const uint64_t cost = (uint64_t)load[c][h] * 16 + gram_commonness(&T->pat[T->pat_off[i] + o], L);
+            if (cost < best) { best = cost; anc[i] = o; hb[i] = h; fp[i] = lit_fp(lo, hi, c); }
+        }
+        load[c][hb[i]]++;
+    }
+    // entries sorted by (class, bucket); the bitmap word order is the same
+    std::vector<uint32_t> ids(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        ids[i] = i;
+        T->bitmap[T->bm_off[cls[i]] + (hb[i] >> 5)] |= 1u << (hb[i] & 31);
+    }
+    std::stable_sort(ids.begin(), ids.end(), [&](uint32_t x, uint32_t y) {
+        return cls[x] != cls[y] ? cls[x] < cls[y] : hb[x] < hb[y];
+    });
+    T->rank.assign(words, 0);
+    uint32_t acc = 0;
+    for (uint32_t c = 0; c < LIT_CLASSES; ++c) {
+        T->rank_base[c] = acc;
+        if (!((T->tmpl >> c) & 1u) && !cnt[c]) continue;
+        const uint32_t w0 = T->bm_off[c], w1 = w0 + std::max<uint32_t>((1u << T->bits[c]) / 32, 1);
+        uint32_t in_cls = 0;
+        for (uint32_t w = w0; w < w1; ++w) {
+            T->rank[w] = (uint16_t)in_cls;
+            in_cls += (uint32_t)__builtin_popcount(T->bitmap[w]);
+        }
+        if (in_cls > 65535) { set_error("build_lit: more than 65,535 buckets in one length class"); return SG_E_UNSUPPORTED; }
+        acc += in_cls;
+    }
+    T->eoff.assign(1, 0);
+    T->efp.clear();
+    T->einfo.clear();
+    T->pat16.clear();
+    std::vector<uint32_t> row(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        row[i] = (uint32_t)(T->pat16.size() / 16);
+        T->pat16.insert(T->pat16.end(), T->pat.begin() + T->pat_off[i], T->pat.begin() + T->pat_off[i + 1]);
+        T->pat16.resize((T->pat16.size() + 15) & ~(size_t)15, 0);
+    }
+    for (uint32_t q = 0; q < n; ++q) {
+        const uint32_t i = ids[q];
+        if (q > 0 && (cls[ids[q - 1]] != cls[i] || hb[ids[q - 1]] != hb[i])) T->eoff.push_back(q);
+        T->efp.push_back(fp[i]);
+        T->einfo.insert(T->einfo.end(), {i, anc[i], T->pat_off[i + 1] - T->pat_off[i], row[i]});
+    }
+    if (n) T->eoff.push_back(n);
+    if (T->eoff.size() != (size_t)acc + 1) { set_error("build_lit: bucket bookkeeping mismatch"); return SG_E_INVAL; }
+    // one 16-B record per bucket: its first entry, plus a flag when more entries follow
+    T->brec.assign((size_t)acc * 4, 0);
+    for (uint32_t k = 0; k < acc; ++k) {
+        const uint32_t e = T->eoff[k];
+        const uint32_t *inf = &T->einfo[(size_t)e * 4];
+        if (inf[2] >= (1u << 24)) { set_error("signature %u longer than 16 MiB", inf[0]); return SG_E_INVAL; }
+        T->brec[4 * k + 0] = T->efp[e];
+        T->brec[4 * k + 1] = inf[0];
+        T->brec[4 * k + 2] = inf[2] | (inf[1] << 24);
+        T->brec[4 * k + 3] = inf[3] | ((T->eoff[k + 1] - e > 1) ? 0x80000000u : 0u);
+    }
     return SG_OK;
 }
 
@@ -258,11 +371,12 @@ static void free_dev(sg_matcher *h) {
         if (q) (void)hipFree(q);
     h->dplan = sg_matcher::DevPlan{};
     for (sg_matcher::Lit *L : {&h->lit, &h->prelit}) {
-        for (void *q : {(void *)L->d_bitmap, (void *)L->d_bk_off, (void *)L->d_bk_ids, (void *)L->d_pat_off,
-                        (void *)L->d_pat})
+        for (void *q : {(void *)L->d_bitmap, (void *)L->d_rank, (void *)L->d_eoff, (void *)L->d_efp,
+                        (void *)L->d_einfo, (void *)L->d_pat16, (void *)L->d_brec})
             if (q) (void)hipFree(q);
-        L->d_bitmap = L->d_bk_off = L->d_bk_ids = L->d_pat_off = nullptr;
-        L->d_pat = nullptr;
+        L->d_bitmap = L->d_eoff = L->d_efp = L->d_einfo = L->d_brec = nullptr;
+        L->d_rank = nullptr;
+        L->d_pat16 = nullptr;
     }
     h->dev = -1;
 }
@@ -288,10 +402,12 @@ static int ensure_device(sg_matcher *h, int dev) {
     for (sg_matcher::Lit *L : {&h->lit, &h->prelit}) {
         if (!L->on) continue;
         SG_TRY(upload_vec(L->bitmap, &L->d_bitmap));
-        SG_TRY(upload_vec(L->bk_off, &L->d_bk_off));
-        SG_TRY(upload_vec(L->bk_ids, &L->d_bk_ids));
-        SG_TRY(upload_vec(L->pat_off, &L->d_pat_off));
-        SG_TRY(upload_vec(L->pat, &L->d_pat));
+        SG_TRY(upload_vec(L->rank, &L->d_rank));
+        SG_TRY(upload_vec(L->eoff, &L->d_eoff));
+        SG_TRY(upload_vec(L->efp, &L->d_efp));
+        SG_TRY(upload_vec(L->einfo, &L->d_einfo));
+        SG_TRY(upload_vec(L->pat16, &L->d_pat16));
+        SG_TRY(upload_vec(L->brec, &L->d_brec));
     }
     // tables[]: the automata scanned over every record; the prefilter AC goes last
     std::vector<sg_matcher::Table *> all;
@@ -392,18 +508,29 @@ __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
 // ------------------------------------------------------------------ device: literal filter
 struct LitArgs {
     const uint8_t *buf;
-    const uint2 *spans;
-    uint32_t R;
-    const uint32_t *bitmap;
-    uint32_t bm_words, cls_mask, nocase;
-    uint32_t bits[4], bm_off[4], bk_base[4];
-    const uint32_t *bk_off, *bk_ids, *pat_off;
-    const uint8_t *pat;
+    uint64_t n;
+    const uint64_t *tile_prefix;  // the parse's look-back status (inclusive packed counts per tile)
+    uint32_t n_tiles;
+    const uint32_t *bitmap, *eoff, *efp;
+    const uint16_t *rank;
+    const uint4 *einfo;           // {pid, anchor, len, 16-B row}
+    const uint4 *brec;            // per bucket {fp, pid, len | anchor << 24, row | more << 31}
+    const uint4 *pat16;
+    uint32_t bm_words, n_bk, n_ent, cls_mask, nocase;
+    uint32_t bits[LIT_CLASSES], bm_off[LIT_CLASSES], rank_base[LIT_CLASSES];
     unsigned long long *hits;
     uint32_t *hit_count;
     uint32_t cap;
     const uint32_t *fac_off, *fac_pids;  // regex prefilter expansion (else null)
+    unsigned long long *dbg;             // SG_LIT_DEBUG: {candidates, fingerprint matches, hits}
+    uint32_t dbg_mode;                   // bit 0: skip pass 2, bit 1: skip pass 1 probes
 };
+
+constexpr int LS_BLOCK = 256;
+constexpr uint32_t LS_HB = 256;    // per-block LDS hit buffer (entries)
+constexpr uint32_t LS_HALO = 64;   // text bytes staged on each side of the tile
+constexpr uint32_t LS_Q = 512;     // per-block candidate queue (entries: pos:14 | class:3 | record:14)
+constexpr int LS_BATCH = 4;        // candidates per lane whose global loads are issued together
 
 __device__ __forceinline__ uint32_t fold4(uint32_t w) {
     // ASCII 'A'..'Z' -> 'a'..'z' in each byte (SWAR)
@@ -414,73 +541,333 @@ __device__ __forceinline__ uint32_t fold4(uint32_t w) {
     return w | (up >> 2);
 }
 
-__device__ __forceinline__ void emit_pair(unsigned long long *hits, uint32_t *hit_count, uint32_t cap,
-                                          const uint32_t *fac_off, const uint32_t *fac_pids, uint32_t rec,
-                                          uint32_t sig, uint32_t *seen, uint32_t &nseen) {
-    for (uint32_t q = 0; q < nseen; ++q)
-        if (seen[q] == sig) return;
-    if (nseen < 4) seen[nseen++] = sig;
-    if (fac_off) {
-        for (uint32_t q = fac_off[sig]; q < fac_off[sig + 1]; ++q) {
-            const uint32_t slot_i = atomicAdd(hit_count, 1u);
-            if (slot_i < cap) hits[slot_i] = ((unsigned long long)rec << 32) | fac_pids[q];
+
+// Byte-compare pattern `row` (len bytes, first 32 preloaded in w0/w1) with the text at
+// p - anchor; text from the LDS tile (with halos) when it lies there, else from HBM.
+// Grams of classes 1..3 are the whole pattern and already compared exactly.
+template <class Args>
+__device__ __forceinline__ bool lit_verify(const Args &a, const uint8_t *s_tile, uint64_t base, uint32_t tile,
+                                           uint64_t p, uint32_t an, uint32_t len, uint32_t row, uint32_t c,
+                                           uint4 w0, uint4 w1) {
+    if (p < an) return false;
+    const uint64_t ps = p - an;
+    if (ps + len > a.n) return false;
+    if (c <= 2) return true;
+    const bool in_lds = ps + LS_HALO >= base && ps + len + 8 <= base + tile + LS_HALO;
+    bool eq = true;
+    if (in_lds) {
+        // word compares: aligned LDS reads + alignbyte
+        const int64_t off = (int64_t)(ps - base);          // >= -LS_HALO
+        const uint8_t *tb = s_tile + (off & ~(int64_t)3);
+        const uint32_t sh = (uint32_t)(off & 3);
+        uint32_t prev = *reinterpret_cast<const uint32_t *>(tb);
+        for (uint32_t j = 0; j < len && eq; j += 4) {
+            const uint32_t nxt = *reinterpret_cast<const uint32_t *>(tb + j + 4);
+            uint32_t tw = sh ? __builtin_amdgcn_alignbyte(nxt, prev, sh) : prev;
+            prev = nxt;
+            if (a.nocase) tw = fold4(tw);
+            uint32_t pw;
+            if (j < 32) {
+                const uint32_t q = j >> 2;
+                const uint32_t x0 = (q & 2) ? ((q & 1) ? w0.w : w0.z) : ((q & 1) ? w0.y : w0.x);
+                const uint32_t x1 = (q & 2) ? ((q & 1) ? w1.w : w1.z) : ((q & 1) ? w1.y : w1.x);
+                pw = (q & 4) ? x1 : x0;
+            } else {
+                pw = reinterpret_cast<const uint32_t *>(a.pat16 + row)[j >> 2];
+            }
+            const uint32_t rem = len - j;
+            const uint32_t mask = rem >= 4 ? 0xffffffffu : ((1u << (8 * rem)) - 1u);
+            eq = ((tw ^ pw) & mask) == 0;
         }
-        return;
+    } else {
+        const uint8_t *pb = reinterpret_cast<const uint8_t *>(a.pat16 + row);
+        for (uint32_t j = 0; j < len && eq; ++j) {
+            uint32_t ch = a.buf[ps + j];
+            if (a.nocase && ch >= 'A' && ch <= 'Z') ch += 32;
+            eq = ch == pb[j];
+        }
     }
-    const uint32_t slot_i = atomicAdd(hit_count, 1u);
-    if (slot_i < cap) hits[slot_i] = ((unsigned long long)rec << 32) | sig;
+    return eq;
 }
 
-// One thread per record. At every byte position p the next min(r, 4) bytes (r = bytes
-// left in the record) form the prefix key of each present class; a set bit in that
-// class's LDS bitmap triggers the byte compare of the patterns in the bucket.
-__global__ __launch_bounds__(512) void k_lit_match(LitArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_bm[];
-    for (uint32_t q = threadIdx.x; q < a.bm_words; q += blockDim.x) s_bm[q] = a.bitmap[q];
+template <class Args, class Push>
+__device__ __forceinline__ void lit_emit(const Args &a, Push &push, uint32_t rec, uint32_t pid) {
+    if (a.dbg) atomicAdd(&a.dbg[2], 1ull);
+    if (a.fac_off) {
+        for (uint32_t z = a.fac_off[pid]; z < a.fac_off[pid + 1]; ++z) push(rec, a.fac_pids[z]);
+    } else {
+        push(rec, pid);
+    }
+}
+
+// One block per tile of the parse (same tile size as k_lines, so the record index of any
+// position is the tile's inclusive start count from the parse plus a block scan of the
+// tile's own starts). Each thread owns BPT consecutive positions. Pass 1 tests the LDS
+// bitmap of every class of the template CM at every position (unconditional ds_reads the
+// compiler can keep in flight together) into candidate masks. The tile's candidates are
+// then compacted into an LDS queue and pass 2 spreads them over all lanes: confirm against
+// the bucket's entry fingerprints, then byte-compare the pattern (16-B rows from L2, text
+// from the LDS tile). Hits go through a per-block LDS buffer flushed with one atomic.
+template <int BPT, uint32_t CM>
+__global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
+    constexpr int TILE = LS_BLOCK * BPT;
+    constexpr int NW = BPT / 4;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    __shared__ __attribute__((aligned(16))) uint8_t s_t[LS_HALO + TILE + LS_HALO];
+    __shared__ unsigned long long s_hits[LS_HB];
+    __shared__ uint32_t s_q[LS_Q];
+    __shared__ uint2 s_kf[LS_Q];  // per queued candidate: (bucket, fingerprint)
+    __shared__ uint32_t s_red[LS_BLOCK / 64];
+    __shared__ uint32_t s_hn, s_g, s_base;
+    uint32_t *s_bm = s_dyn;
+    uint16_t *s_rank = reinterpret_cast<uint16_t *>(s_dyn + a.bm_words);
+    for (uint32_t q = threadIdx.x; q < a.bm_words; q += LS_BLOCK) { s_bm[q] = a.bitmap[q]; s_rank[q] = a.rank[q]; }
+    if (threadIdx.x == 0) s_hn = 0;
     __syncthreads();
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.R; r += gridDim.x * blockDim.x) {
-        const uint2 sp = a.spans[r];
-        const uint32_t s = sp.x, e = sp.y;
-        uint32_t seen[4];
-        uint32_t nseen = 0;
-        const uint32_t a0 = s & ~3u;
-        uint32_t w0 = *reinterpret_cast<const uint32_t *>(a.buf + a0);
-        uint32_t w1 = (a0 + 4 < e) ? *reinterpret_cast<const uint32_t *>(a.buf + a0 + 4) : 0u;
-        if (a.nocase) { w0 = fold4(w0); w1 = fold4(w1); }
-        for (uint32_t q = a0; q < e; q += 4) {
-            const uint64_t win = (uint64_t)w0 | ((uint64_t)w1 << 32);
+    const uint32_t t = threadIdx.x;
+    const uint64_t n = a.n;
+    uint8_t *s_tile = s_t + LS_HALO;
+
+    auto push = [&](uint32_t rec, uint32_t sig) {
+        const unsigned long long v = ((unsigned long long)rec << 32) | sig;
+        const uint32_t i = atomicAdd(&s_hn, 1u);
+        if (i < LS_HB) {
+            s_hits[i] = v;
+        } else {
+            const uint32_t g = atomicAdd(a.hit_count, 1u);
+            if (g < a.cap) a.hits[g] = v;
+        }
+    };
+
+    for (uint32_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+        const uint64_t base = (uint64_t)tile * TILE;
+        const uint64_t my0 = base + (uint64_t)t * BPT;
+        uint32_t w[NW];
+        if (base + TILE + LS_HALO <= n) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(a.buf + my0);
 #pragma unroll
-            for (uint32_t b = 0; b < 4; ++b) {
-                const uint32_t p = q + b;
-                if (p < s || p >= e) continue;
-                const uint32_t rem = e - p;
-                const uint32_t key4 = (uint32_t)(win >> (8 * b));
+            for (int j = 0; j < NW / 4; ++j) {
+                const uint4 v = p[j];
+                w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+            }
+        } else {
 #pragma unroll
-                for (uint32_t L = 1; L <= 4; ++L) {
-                    if (!((a.cls_mask >> (L - 1)) & 1u) || rem < L) continue;
-                    const uint32_t key = (L == 4) ? key4 : (key4 & ((1u << (8 * L)) - 1u));
-                    const uint32_t h = lit_h(key, L, a.bits[L - 1]);
-                    if (!((s_bm[a.bm_off[L - 1] + (h >> 5)] >> (h & 31)) & 1u)) continue;
-                    const uint32_t bk = a.bk_base[L - 1] + h;
-                    for (uint32_t i = a.bk_off[bk]; i < a.bk_off[bk + 1]; ++i) {
-                        const uint32_t pid = a.bk_ids[i];
-                        const uint32_t ps = a.pat_off[pid], pl = a.pat_off[pid + 1] - ps;
-                        if (pl > rem || (pl < 4) != (L < 4)) continue;
-                        bool eq = true;
-                        for (uint32_t j = 0; j < pl && eq; ++j) {
-                            uint32_t c = a.buf[p + j];
-                            if (a.nocase && c >= 'A' && c <= 'Z') c += 32;
-                            eq = c == a.pat[ps + j];
+            for (int j = 0; j < NW; ++j) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint64_t pos = my0 + 4 * j + k;
+                    x |= (uint32_t)((pos < n) ? a.buf[pos] : 0x0au) << (8 * k);
+                }
+                w[j] = x;
+            }
+        }
+        // halos: 16 lanes x 4 B on each side ('\n' outside the buffer)
+        if (t < 2 * LS_HALO / 4) {
+            const bool right = t >= LS_HALO / 4;
+            const int64_t pos0 = right ? (int64_t)(base + TILE) + 4 * (t - LS_HALO / 4) : (int64_t)base - LS_HALO + 4 * t;
+            uint32_t x = 0;
+            if (pos0 >= 0 && (uint64_t)pos0 + 4 <= n) {
+                x = *reinterpret_cast<const uint32_t *>(a.buf + pos0);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int64_t pos = pos0 + k;
+                    x |= (uint32_t)((pos >= 0 && (uint64_t)pos < n) ? a.buf[pos] : 0x0au) << (8 * k);
+                }
+            }
+            *reinterpret_cast<uint32_t *>(right ? s_tile + TILE + 4 * (t - LS_HALO / 4) : s_t + 4 * t) = x;
+        }
+#pragma unroll
+        for (int j = 0; j < NW / 4; ++j)
+            reinterpret_cast<uint4 *>(s_tile)[(NW / 4) * t + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+        if (t == 0) s_base = tile ? (uint32_t)((a.tile_prefix[tile - 1] & LB_VAL_MASK) >> 31) : 0u;
+        uint64_t m = 0;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+            const uint32_t y = w[j] ^ 0x0a0a0a0au;
+            const uint32_t r = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
+            m |= (uint64_t)(((r >> 7) & 1u) | ((r >> 14) & 2u) | ((r >> 21) & 4u) | ((r >> 28) & 8u)) << (4 * j);
+        }
+        __syncthreads();
+        const uint64_t cin = (s_tile[(int)(t * BPT) - 1] == 0x0a) || (base == 0 && t == 0);
+        const uint64_t full = (BPT == 64) ? ~0ull : ((1ull << (BPT & 63)) - 1);
+        const uint64_t sm = ~m & ((m << 1) | cin) & full;
+        uint32_t tot;
+        const uint32_t excl = block_excl_scan<LS_BLOCK>((uint32_t)__popcll(sm), &tot, s_red);
+        uint32_t wn0 = *reinterpret_cast<const uint32_t *>(s_tile + (t + 1) * BPT);
+        uint32_t wn1 = *reinterpret_cast<const uint32_t *>(s_tile + (t + 1) * BPT + 4);
+        if (a.nocase) {
+#pragma unroll
+            for (int j = 0; j < NW; ++j) w[j] = fold4(w[j]);
+            wn0 = fold4(wn0);
+            wn1 = fold4(wn1);
+        }
+        // pass 1: bitmap probes
+        uint64_t cand[LIT_CLASSES] = {};
+        if (!(a.dbg_mode & 2u))
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+            const int i0 = b >> 2;
+            const uint32_t x0 = w[i0];
+            const uint32_t x1 = (i0 + 1 < NW) ? w[i0 + 1] : wn0;
+            const uint32_t x2 = (i0 + 2 < NW) ? w[i0 + 2] : (i0 + 2 == NW ? wn0 : wn1);
+            const uint32_t lo = (b & 3) ? __builtin_amdgcn_alignbyte(x1, x0, b & 3) : x0;
+#pragma unroll
+            for (uint32_t c = 0; c < LIT_CLASSES; ++c) {
+                if (!((CM >> c) & 1u)) continue;
+                uint32_t h;
+                if (c == 4) {
+                    const uint32_t hi = (b & 3) ? __builtin_amdgcn_alignbyte(x2, x1, b & 3) : x1;
+                    h = lit_h(lo, hi, c, a.bits[c]);
+                } else {
+                    const uint32_t key = (c == 3) ? lo : (lo & ((1u << (8 * (c + 1))) - 1u));
+                    h = lit_h(key, 0u, c, a.bits[c]);
+                }
+                cand[c] |= (uint64_t)((s_bm[a.bm_off[c] + (h >> 5)] >> (h & 31)) & 1u) << b;
+            }
+        }
+        if (my0 + BPT > n) {
+            const uint64_t valid = (my0 >= n) ? 0ull : ((1ull << (n - my0)) - 1);
+#pragma unroll
+            for (uint32_t c = 0; c < LIT_CLASSES; ++c) cand[c] &= valid;
+        }
+        if (a.dbg_mode & 1u) {
+            uint32_t cc = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < LIT_CLASSES; ++c) cc += (uint32_t)__popcll(cand[c]);
+            if (cc == 0xffffffffu) a.hits[0] = 0;  // keep pass 1 live
+#pragma unroll
+            for (uint32_t c = 0; c < LIT_CLASSES; ++c) cand[c] = 0;
+        }
+        if (a.dbg) {
+            uint32_t cc = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < LIT_CLASSES; ++c) cc += (uint32_t)__popcll(cand[c]);
+            cc = wave_sum(cc);
+            if (lane_id() == 0 && cc) atomicAdd(&a.dbg[0], (unsigned long long)cc);
+        }
+        // pass 2: queue the tile's candidates, then confirm/verify them across all lanes
+        uint32_t ncand = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < LIT_CLASSES; ++c) ncand += (uint32_t)__popcll(cand[c]);
+        uint32_t qtot;
+        const uint32_t qex = block_excl_scan<LS_BLOCK>(ncand, &qtot, s_red);
+        const uint32_t lrec0 = excl;  // tile-local index of this thread's first record start
+        for (uint32_t r0 = 0; r0 < qtot; r0 += LS_Q) {
+            uint32_t qi = qex;
+            if (qi < r0 + LS_Q && qi + ncand > r0) {
+#pragma unroll
+                for (uint32_t c = 0; c < LIT_CLASSES; ++c) {
+                    uint64_t cm = cand[c];
+                    while (cm) {
+                        const int b = __ffsll((long long)cm) - 1;
+                        cm &= cm - 1;
+                        if (qi >= r0 && qi < r0 + LS_Q) {
+                            // record containing p: starts at or before p, minus one (may be -1
+                            // relative to the tile: the record began in an earlier tile)
+                            const uint32_t lrec = lrec0 + (uint32_t)__popcll(sm & ((2ull << b) - 1));
+                            s_q[qi - r0] = ((t * BPT + b) << 17) | (c << 14) | lrec;
                         }
-                        if (eq) emit_pair(a.hits, a.hit_count, a.cap, a.fac_off, a.fac_pids, r, pid, seen, nseen);
+                        ++qi;
                     }
                 }
             }
-            w0 = w1;
-            w1 = (q + 8 < e) ? *reinterpret_cast<const uint32_t *>(a.buf + q + 8) : 0u;
-            if (a.nocase) w1 = fold4(w1);
+            __syncthreads();
+            const uint32_t qn = min(LS_Q, qtot - r0);
+            // stage 1 (LDS only): gram -> bucket and fingerprint
+            for (uint32_t i = t; i < qn; i += LS_BLOCK) {
+                const uint32_t ent = s_q[i];
+                const int q = (int)(ent >> 17);
+                const uint32_t c = (ent >> 14) & 7u;
+                uint32_t lo = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3));
+                uint32_t l1 = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3) + 4);
+                uint32_t l2 = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3) + 8);
+                if (a.nocase) { lo = fold4(lo); l1 = fold4(l1); l2 = fold4(l2); }
+                const uint32_t sh = q & 3;
+                const uint32_t k0 = sh ? __builtin_amdgcn_alignbyte(l1, lo, sh) : lo;
+                const uint32_t k1 = sh ? __builtin_amdgcn_alignbyte(l2, l1, sh) : l1;
+                const uint32_t key = (c >= 3) ? k0 : (k0 & ((1u << (8 * (c + 1))) - 1u));
+                const uint32_t h = lit_h(key, k1, c, a.bits[c]);
+                const uint32_t wi = a.bm_off[c] + (h >> 5);
+                const uint32_t k = a.rank_base[c] + s_rank[wi] + (uint32_t)__popc(s_bm[wi] & ((1u << (h & 31)) - 1u));
+                s_kf[i] = make_uint2(k, lit_fp(key, k1, c));
+            }
+            // stage 2: LS_BATCH candidates per lane, their bucket records and first pattern
+            // rows loaded together, then verified against the LDS text
+            for (uint32_t i0 = t; i0 < qn; i0 += LS_BATCH * LS_BLOCK) {
+                uint4 br[LS_BATCH];
+                uint32_t fpv[LS_BATCH];
+#pragma unroll
+                for (int u = 0; u < LS_BATCH; ++u) {
+                    const uint32_t i = i0 + u * LS_BLOCK;
+                    br[u] = make_uint4(0, 0, 0, 0);
+                    fpv[u] = 1;
+                    if (i < qn) {
+                        const uint2 kf = s_kf[i];
+                        br[u] = a.brec[kf.x];
+                        fpv[u] = kf.y;
+                    }
+                }
+                uint4 r0w[LS_BATCH], r1w[LS_BATCH];
+#pragma unroll
+                for (int u = 0; u < LS_BATCH; ++u) {
+                    const bool m = (i0 + u * LS_BLOCK < qn) && br[u].x == fpv[u];
+                    const uint32_t row = br[u].w & 0x7fffffffu;
+                    const uint32_t len = br[u].z & 0xffffffu;
+                    r0w[u] = m ? a.pat16[row] : make_uint4(0, 0, 0, 0);
+                    r1w[u] = (m && len > 16) ? a.pat16[row + 1] : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < LS_BATCH; ++u) {
+                    const uint32_t i = i0 + u * LS_BLOCK;
+                    if (i >= qn) continue;
+                    const uint32_t ent = s_q[i];
+                    const uint32_t q = ent >> 17;
+                    const uint32_t c = (ent >> 14) & 7u;
+                    const uint32_t rec = s_base + (ent & 0x3fffu) - 1;
+                    const uint64_t p = base + q;
+                    if (br[u].x == fpv[u]) {
+                        if (a.dbg) atomicAdd(&a.dbg[1], 1ull);
+                        if (lit_verify(a, s_tile, base, TILE, p, br[u].z >> 24, br[u].z & 0xffffffu, br[u].w & 0x7fffffffu,
+                                       c, r0w[u], r1w[u]))
+                            lit_emit(a, push, rec, br[u].y);
+                    }
+                    if (br[u].w >> 31) {
+                        // rare: more patterns share this bucket
+                        const uint32_t k = s_kf[i].x;
+                        for (uint32_t e = a.eoff[k] + 1; e < a.eoff[k + 1]; ++e) {
+                            if (a.efp[e] != fpv[u]) continue;
+                            const uint4 inf = a.einfo[e];
+                            const uint4 w0 = a.pat16[inf.w];
+                            const uint4 w1 = inf.z > 16 ? a.pat16[inf.w + 1] : make_uint4(0, 0, 0, 0);
+                            if (lit_verify(a, s_tile, base, TILE, p, inf.y, inf.z, inf.w, c, w0, w1))
+                                lit_emit(a, push, rec, inf.x);
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        __syncthreads();
+        const uint32_t hn = min(s_hn, LS_HB);
+        if (hn >= LS_HB / 2 || tile + gridDim.x >= a.n_tiles) {
+            if (t == 0) s_g = hn ? atomicAdd(a.hit_count, hn) : 0u;
+            __syncthreads();
+            for (uint32_t i = t; i < hn; i += LS_BLOCK) {
+                const uint32_t g = s_g + i;
+                if (g < a.cap) a.hits[g] = s_hits[i];
+            }
+            __syncthreads();
+            if (t == 0) s_hn = 0;
         }
     }
+}
+
+// LDS bytes of k_lit_scan's dynamic tables for a filter (entries in LDS when they fit).
+static uint32_t lit_lds_bytes(const sg_matcher::Lit &T) {
+    const uint32_t bmw = (uint32_t)T.bitmap.size();
+    return 4u * (bmw + (bmw + 1) / 2);  // bitmaps (u32) + ranks (u16)
 }
 
 // ------------------------------------------------------------------ device: regex DFAs
@@ -634,12 +1021,15 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
     *res = sg_dev_hits{};
     SG_TRY(ensure_device(h, c->device));
     Lines L;
-    SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L));
+    SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L, false));
     const uint32_t R = L.n_rec;
     res->in_records = R;
     uint32_t *cnt;
     SG_TRY(slot(c, S_M_CNT, 8, &cnt));
+    // hit capacity: remembered from earlier calls through the slot size (no relaunch in
+    // steady state), at least R / 4
     uint64_t cap = std::max<uint64_t>(1u << 20, (uint64_t)R / 4);
+    cap = std::max<uint64_t>(cap, c->slot_cap[S_M_HITS] / 8);
     uint32_t total = 0;
     unsigned long long *hits = nullptr;
     auto geometry = [&](const sg_matcher::Table &T, const sg_matcher::DevTable &D, uint32_t *bits_in_lds,
@@ -649,41 +1039,75 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
         *lds = 256 + ((D.H * T.n_classes * 2 + 15) & ~15u) + (*bits_in_lds ? nbits * 4 : 0);
         *grid = std::min<uint32_t>((R + 511) / 512, 256u * 8u);
     };
-    // prefilter candidates (regex plans): factor AC -> (record, pattern) pairs
+    // prefilter candidates (regex plans): factor filter -> (record, pattern) pairs
     unsigned long long *cand = nullptr;
     uint32_t n_cand = 0;
-    auto lit_args = [&](const sg_matcher::Lit &Lt, unsigned long long *out, uint32_t *counter, uint32_t ocap,
-                        const uint32_t *fo, const uint32_t *fp) {
+    const int bpt = (int)(L.tile_bytes / LS_BLOCK);
+    auto run_lit = [&](const char *name, const sg_matcher::Lit &Lt, unsigned long long *out, uint32_t *counter,
+                       uint32_t ocap, const uint32_t *fo, const uint32_t *fp) -> int {
         LitArgs a{};
-        a.buf = d_buf; a.spans = L.spans; a.R = R;
-        a.bitmap = Lt.d_bitmap; a.bm_words = (uint32_t)Lt.bitmap.size(); a.cls_mask = Lt.cls_mask;
-        a.nocase = Lt.nocase ? 1u : 0u;
-        for (int k = 0; k < 4; ++k) { a.bits[k] = Lt.bits[k]; a.bm_off[k] = Lt.bm_off[k]; a.bk_base[k] = Lt.bk_base[k]; }
-        a.bk_off = Lt.d_bk_off; a.bk_ids = Lt.d_bk_ids; a.pat_off = Lt.d_pat_off; a.pat = Lt.d_pat;
+        a.buf = d_buf; a.n = n; a.tile_prefix = L.tile_prefix; a.n_tiles = L.n_tiles;
+        a.bitmap = Lt.d_bitmap; a.rank = Lt.d_rank; a.eoff = Lt.d_eoff; a.efp = Lt.d_efp;
+        a.brec = reinterpret_cast<const uint4 *>(Lt.d_brec);
+        a.einfo = reinterpret_cast<const uint4 *>(Lt.d_einfo); a.pat16 = reinterpret_cast<const uint4 *>(Lt.d_pat16);
+        a.bm_words = (uint32_t)Lt.bitmap.size(); a.n_bk = (uint32_t)Lt.eoff.size() - 1;
+        a.n_ent = (uint32_t)Lt.efp.size(); a.cls_mask = Lt.cls_mask; a.nocase = Lt.nocase ? 1u : 0u;
+        for (uint32_t k = 0; k < LIT_CLASSES; ++k) {
+            a.bits[k] = Lt.bits[k]; a.bm_off[k] = Lt.bm_off[k]; a.rank_base[k] = Lt.rank_base[k];
+        }
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
-        return a;
+        static const int dbg_mode = getenv("SG_LIT_DEBUG") ? atoi(getenv("SG_LIT_DEBUG")) : -1;
+        unsigned long long *dbg = nullptr;
+        if (dbg_mode >= 0) a.dbg_mode = (uint32_t)dbg_mode;  // bit 0 skip pass 2, bit 1 skip pass 1, bit 3 count
+        if (dbg_mode >= 0 && (dbg_mode & 8)) {
+            SG_TRY(slot(c, S_M_TMP2, 4, &dbg));
+            SG_HIP(hipMemsetAsync(dbg, 0, 32, c->stream));
+            a.dbg = dbg;
+        }
+        const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + 64;
+        const uint32_t dyn = lit_lds_bytes(Lt);
+        const uint32_t bpc = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
+        const uint32_t grid = std::min<uint32_t>(L.n_tiles, 256u * bpc);
+        const double bytes = (double)n + 8.0 * R;
+        auto launch = [&](auto kern) -> int {
+            SG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
+            SG_LAUNCH_B(c, name, bytes, kern, grid, LS_BLOCK, dyn, a);
+            return SG_OK;
+        };
+        if (bpt == 32) {
+            if (Lt.tmpl == 0x18u) SG_TRY(launch(k_lit_scan<32, 0x18u>));
+            else if (Lt.tmpl == 0x1Cu) SG_TRY(launch(k_lit_scan<32, 0x1Cu>));
+            else SG_TRY(launch(k_lit_scan<32, 0x1Fu>));
+        } else {
+            if (Lt.tmpl == 0x18u) SG_TRY(launch(k_lit_scan<64, 0x18u>));
+            else if (Lt.tmpl == 0x1Cu) SG_TRY(launch(k_lit_scan<64, 0x1Cu>));
+            else SG_TRY(launch(k_lit_scan<64, 0x1Fu>));
+        }
+        if (dbg) {
+            unsigned long long d[3];
+            SG_TRY(ctx_readback(c, d, dbg, 24));
+            fprintf(stderr, "[%s] grid=%u lds=%u+%u cand=%llu fp=%llu hits=%llu bm_words=%u classes=%x bits=%u,%u,%u,%u,%u\n",
+                    name, grid, dyn, stat, d[0], d[1], d[2], a.bm_words, a.cls_mask, a.bits[0], a.bits[1], a.bits[2],
+                    a.bits[3], a.bits[4]);
+        }
+        return SG_OK;
     };
-    const uint32_t lgrid = std::min<uint32_t>((R + 511) / 512, 256u * 8u);
     if (h->has_pre && R) {
-        uint64_t ccap = std::max<uint64_t>(1u << 20, (uint64_t)R);
+        uint64_t ccap = std::max<uint64_t>(std::max<uint64_t>(1u << 20, (uint64_t)R), c->slot_cap[S_PART] / 8);
         for (int attempt = 0; attempt < 2; ++attempt) {
             SG_TRY(slot(c, S_PART, ccap, &cand));
             SG_HIP(hipMemsetAsync(cnt + 1, 0, 4, c->stream));
-            LitArgs a = lit_args(h->prelit, cand, cnt + 1, (uint32_t)ccap, h->dplan.fac_off, h->dplan.fac_pids);
-            SG_LAUNCH_B(c, "re_prefilter", (double)n + 8.0 * R, k_lit_match, lgrid, 512, a.bm_words * 4, a);
+            SG_TRY(run_lit("re_prefilter", h->prelit, cand, cnt + 1, (uint32_t)ccap, h->dplan.fac_off, h->dplan.fac_pids));
             SG_TRY(ctx_readback(c, &n_cand, cnt + 1, 4));
             if (n_cand <= ccap) break;
-            ccap = (uint64_t)n_cand + 1024;
+            ccap = (uint64_t)n_cand + (n_cand >> 3) + 1024;
         }
         cap = std::max<uint64_t>(cap, (uint64_t)n_cand + 1024);
     }
     for (int attempt = 0; attempt < 2; ++attempt) {
         SG_TRY(slot(c, S_M_HITS, cap, &hits));
         SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
-        if (R && h->lit.on) {
-            LitArgs a = lit_args(h->lit, hits, cnt, (uint32_t)cap, nullptr, nullptr);
-            SG_LAUNCH_B(c, "lit_match", (double)n + 8.0 * R, k_lit_match, lgrid, 512, a.bm_words * 4, a);
-        }
+        if (R && h->lit.on) SG_TRY(run_lit("lit_match", h->lit, hits, cnt, (uint32_t)cap, nullptr, nullptr));
         if (R) {
             for (size_t ti = 0; ti < h->tables.size(); ++ti) {
                 const auto &T = h->tables[ti];
@@ -710,7 +1134,7 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
         }
         SG_TRY(ctx_readback(c, &total, cnt, 4));
         if (total <= cap) break;
-        cap = (uint64_t)total + 1024;
+        cap = (uint64_t)total + (total >> 3) + 1024;
     }
     // sort (rec << 32 | sig) and de-duplicate
     uint64_t *k2;
@@ -770,8 +1194,14 @@ int sg_ac_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats
     const auto &T = m->tables[0];
     if ((uint64_t)T.n_states * T.n_classes * 2 > AC_HOT_BYTES || getenv("SG_FORCE_LITFILTER")) {
         rc = build_lit(pats, pat_offs, n_pats, flags, &m->lit);
-        if (rc != SG_OK) { delete m; return rc; }
-        m->tables.clear();
+        if (rc == SG_E_UNSUPPORTED) {
+            m->lit = sg_matcher::Lit{};  // too many patterns of one length class: keep the automaton
+        } else if (rc != SG_OK) {
+            delete m;
+            return rc;
+        } else {
+            m->tables.clear();
+        }
     }
     *h = m;
     return SG_OK;

@@ -153,3 +153,35 @@ def test_device_match_lines(sg):
     assert r.n_hits == len(hits)
     assert ctx.to_bytes(r.lines, r.lines_bytes) == S.matched_lines(data, hits)
     ctx.close()
+
+
+@pytest.mark.parametrize("nocase", [False, True])
+def test_literal_tile_edges(sg, nocase):
+    """Every pattern-length class (1..3 whole, 4..7 and >= 8 anchored), records longer than a
+    parse tile (16 KiB) and patterns planted across tile boundaries and at buffer ends."""
+    rng = random.Random(77 + nocase)
+    alpha = b"abcdefgh/:.-ABCD"
+    sigs = list({bytes(rng.choice(alpha) for _ in range(L)) for L in list(range(1, 12)) * 6 + [16, 23, 31, 40] * 4})
+    sigs = [s for s in sigs if s]
+    parts = []
+    for i in range(60):
+        L = rng.choice([0, 1, 5, 40, 300, 5000, 20000])
+        line = bytearray(rng.choice(b"xyzXYZ0123 ") for _ in range(L))
+        for _ in range(rng.randint(0, 6)):
+            s = rng.choice(sigs)
+            if nocase:
+                s = bytes(c ^ 0x20 if 97 <= c <= 122 and rng.random() < 0.5 else c for c in s)
+            k = rng.randrange(len(line) + 1)
+            line[k:k] = s
+        parts.append(bytes(line))
+    data = b"\n".join(parts)
+    # plant patterns straddling the 16 KiB tile edges
+    data = bytearray(data)
+    for edge in range(16384, len(data) - 64, 16384):
+        s = rng.choice(sigs)
+        off = edge - rng.randrange(len(s) + 1)
+        data[off:off + len(s)] = s
+    data = bytes(data)
+    m = sg.Matcher(sigs, "literal", nocase=nocase)
+    assert m.match(data) == S.literal_hits(data, sigs, nocase=nocase)
+    assert m.match(data + b"\n") == S.literal_hits(data + b"\n", sigs, nocase=nocase)
