@@ -279,66 +279,73 @@ __global__ void k_gather_rl(const uint32_t *__restrict__ idx, const uint32_t *__
     L2[i] = L[q];
 }
 
-constexpr uint32_t CP_WAVE_BYTES = 4096;
+constexpr uint32_t CP_WAVE_BYTES = 8192;
 
-// Records (list order) -> out at offs[i], each '\n'-terminated. Each wave stages its 64
-// records' bytes in LDS at their output positions (aligned word loads from the source),
-// then writes the wave's output span with 16-byte stores; spans wider than the wave's
-// LDS window fall back to per-lane byte copies.
+// Records (list order) -> out at offs[i], each '\n'-terminated. Each wave owns 64
+// consecutive list entries, whose output is one contiguous span. The wave assembles that
+// span in an LDS window: groups of 16 lanes copy one record at a time with coalesced
+// aligned word loads (the record's bytes are contiguous in the source), then the whole
+// wave writes the window with 16-byte stores. Spans wider than the window (records longer
+// than CP_WAVE_BYTES / 64 on average) are copied the same way straight to HBM.
 __global__ __launch_bounds__(256) void k_copy_records(const uint8_t *__restrict__ buf,
                                                       const uint2 *__restrict__ spans,
                                                       const uint32_t *__restrict__ recs,
                                                       const uint64_t *__restrict__ offs, uint32_t n,
                                                       uint8_t *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint8_t s_buf[4][CP_WAVE_BYTES];
+    __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
     const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
     const uint32_t wfirst = (blockIdx.x * 4 + wid) * 64u;
     if (wfirst >= n) return;
     const uint32_t i = wfirst + lane;
     const bool act = i < n;
     const uint32_t r = act ? recs[i] : 0u;
-    const uint32_t s = act ? spans[r].x : 0u;
-    const uint32_t len = act ? spans[r].y - s : 0u;
+    const uint2 sp = act ? spans[r] : make_uint2(0, 0);
+    const uint32_t s = sp.x, len = sp.y - sp.x;
     const uint64_t o = act ? offs[i] : 0ull;
     const uint32_t last = (n - wfirst) < 64u ? (n - wfirst - 1u) : 63u;
     const uint64_t o0 = __shfl(o, 0, 64);
     const uint64_t oend = __shfl(o + len + 1u, (int)last, 64);
     const uint64_t base = o0 & ~15ull;
     const uint64_t span = oend - base;
-    if (span <= CP_WAVE_BYTES) {
-        uint8_t *L = s_buf[wid];
-        if (act) {
-            const uint32_t lo = (uint32_t)(o - base);
-            const uint32_t e = s + len;
-            for (uint32_t w = s & ~3u; w < e; w += 4) {
-                const uint32_t x = *reinterpret_cast<const uint32_t *>(buf + w);
+    const bool in_lds = span <= CP_WAVE_BYTES;
+    s_src[wid][lane] = s;
+    s_len[wid][lane] = len;
+    s_dst[wid][lane] = (uint32_t)(o - base);  // < 4 GiB: one call's output
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t g = lane >> 4, gl = lane & 15;
+    uint8_t *L = s_buf[wid];
+    for (uint32_t j = g; j <= last; j += 4) {
+        const uint32_t sj = s_src[wid][j], lj = s_len[wid][j];
+        const uint32_t ej = sj + lj;
+        const uint32_t a0 = sj & ~3u;
+        uint8_t *dst = (in_lds ? L : out + base) + s_dst[wid][j];
+        for (uint32_t a = a0 + 4 * gl; a < ej; a += 64) {
+            const uint32_t x = *reinterpret_cast<const uint32_t *>(buf + a);
 #pragma unroll
-                for (uint32_t b = 0; b < 4; ++b) {
-                    const uint32_t p = w + b;
-                    if (p >= s && p < e) L[lo + (p - s)] = (uint8_t)(x >> (8 * b));
-                }
-            }
-            L[lo + len] = 0x0a;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t nch = (uint32_t)((span + 15) / 16);
-        for (uint32_t ch = lane; ch < nch; ch += 64) {
-            const uint64_t ga = base + 16ull * ch;
-            if (ga >= o0 && ga + 16 <= oend) {
-                *reinterpret_cast<uint4 *>(out + ga) = *reinterpret_cast<const uint4 *>(L + 16 * ch);
-            } else {
-#pragma unroll
-                for (uint32_t b = 0; b < 16; ++b) {
-                    const uint64_t a = ga + b;
-                    if (a >= o0 && a < oend) out[a] = L[16 * ch + b];
-                }
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t p = a + b;
+                if (p >= sj && p < ej) dst[p - sj] = (uint8_t)(x >> (8 * b));
             }
         }
-    } else if (act) {
-        uint8_t *d = out + o;
-        for (uint32_t p = 0; p < len; ++p) d[p] = buf[s + p];
-        d[len] = 0x0a;
+        if (gl == 0) dst[lj] = 0x0a;
+    }
+    if (!in_lds) return;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t nch = (uint32_t)((span + 15) / 16);
+    for (uint32_t ch = lane; ch < nch; ch += 64) {
+        const uint64_t ga = base + 16ull * ch;
+        if (ga >= o0 && ga + 16 <= oend) {
+            *reinterpret_cast<uint4 *>(out + ga) = *reinterpret_cast<const uint4 *>(L + 16 * ch);
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 16; ++b) {
+                const uint64_t ad = ga + b;
+                if (ad >= o0 && ad < oend) out[ad] = L[16 * ch + b];
+            }
+        }
     }
 }
 
