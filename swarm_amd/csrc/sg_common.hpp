@@ -57,6 +57,9 @@ enum Slot : int {
     // partition / match
     S_PART, S_PART_OUT, S_M_HITS, S_M_SIG, S_M_LINES, S_M_TMP, S_M_TMP2, S_M_CNT,
     S_IN, S_IN2, S_CUR_UR, S_CUR_UK, S_RS_STATUS,
+    // sorted materialisation (shared temporaries) and per-view outputs
+    S_SBUF, S_SSPANS, S_DUP, S_BAD, S_BRK, S_MIRROR, S_EMIT, S_EMIT2, S_EMIT3, S_ERR,
+    S_U_SPANS, S_U_KEYS, S_P_UBUF, S_P_USPANS, S_P_UKEYS, S_FRESHF, S_ECACHE, S_TILES,
     S_NSLOTS
 };
 
@@ -205,6 +208,15 @@ __device__ __forceinline__ uint64_t wave_lookback(const uint64_t *status, int64_
     }
     return excl;
 }
+
+// Exclusive scan of per-tile aggregates (u64 whose packed fields never carry), ONE block:
+// the middle step of every reduce-then-scan kernel pair (count pass -> this -> apply pass).
+// On MI355X a single-pass decoupled look-back over small tiles waits a cross-XCD round trip
+// per tile; reading the per-item input twice is cheaper (tools/c2_probe.py measurements).
+constexpr int TS_BLOCK = 1024;
+constexpr int TS_ITEMS = 4;
+__global__ __launch_bounds__(TS_BLOCK) void k_tile_scan(const uint64_t *__restrict__ tot, uint32_t nt,
+                                                        uint64_t *__restrict__ pre, uint64_t *__restrict__ total);
 
 // Tile ticket: dynamic tile ids in dispatch order (forward progress for look-back).
 __device__ __forceinline__ uint32_t take_ticket(uint32_t *counter, uint32_t *lds_slot) {

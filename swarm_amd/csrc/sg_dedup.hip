@@ -1,65 +1,61 @@
 // sg_dedup.hip — A7 sort -u dedup and A8 new-record diff on HBM-resident text.
 //
-// Pipeline (one stream):
-//   lines   -> (start, end, key0) per record, key0 = chunk_key(rec, 0)
-//   sort    -> LSD radix sort of (key0, rec id)
-//   mark    -> equal-key groups; a group with tag < 8 is a run of identical records
-//              (keep the first); a tag-8 group of >= 2 records shares 7 bytes and
-//              continues, so it is refined:
-//   refine  -> groups of <= 8 records: one thread ranks members by full byte compare
-//              (stable; later equal members are duplicates). Larger groups: a radix
-//              round on the next 7-byte chunk (stable sort by chunk, then by group),
-//              repeated until every group is resolved. Exact for any input, including
-//              64-bit-hash collisions, NULs and long shared prefixes.
-//   select  -> unique positions in byte order -> serialize '\n'-terminated output.
-//   diff    -> each unique record binary-searches the prior's sorted keys inside the
-//              key range its 256-record block spans (full compare on 8-byte ties).
+// Pipeline (one stream), per buffer:
+//   lines    -> (start, end, key0) per record; key0 = bytes [0,7) + tag min(len, 8)
+//   sort     -> LSD radix sort of (key0, rec id)
+//   big      -> equal-key0 groups of > 64 records sharing 7 bytes are split further by
+//               radix rounds on the next 7-byte chunk (stable by chunk, then by group),
+//               until every unresolved segment has <= 64 records; segment heads -> brk
+//   emit     -> the records in that order, materialised ONCE into a contiguous sorted
+//               buffer S (fused length scan + gather + copy, sg_emit.hpp); every later
+//               step reads S sequentially instead of gathering records from the input
+//   adjacent -> dup[i] = record i equals record i-1 (same segment, bytes from S);
+//               bad[i] = same segment but different bytes (segment not yet ordered)
+//   run sort -> each segment holding a bad position (<= 64 records) is sorted by one wave
+//               in LDS by full byte compare, rewritten in place in S, dup recomputed
+//   emit     -> the records with dup == 0: the sort -u output, contiguous, + spans/key0
+//   diff     -> merge-path tiles over the unique output and the prior's sorted unique
+//               view (both contiguous), equality from LDS-staged keys + wide compares
+//   emit     -> the records absent from the prior: the new-record output
+// The result is exact for any input (NULs, CR, 0xff, long shared prefixes, duplicates of
+// any multiplicity): ordering is decided by bytes, never by a hash.
 #include "sg_internal.hpp"
-#include "sg_prims.hpp"
+#include "sg_prims_host.hpp"
+#include "sg_emit.hpp"
+
+#include <stdlib.h>
 
 namespace sg {
 
 const SlotSet CUR_SLOTS = {S_STARTS, S_ENDS, S_KEYS, S_KEYS2, S_VALS, S_VALS2, S_UNIQ, S_LB};
 const SlotSet PRIOR_SLOTS = {S_P_STARTS, S_P_ENDS, S_P_KEYS, S_P_KEYS2, S_P_VALS, S_P_VALS2, S_P_UNIQ, S_P_FLAG};
 
-constexpr uint32_t EQ_GROUP = 4096;
 constexpr uint32_t WAVE_GROUP = 64;
 
 // ------------------------------------------------------------------ launch helpers
-template <class Pred>
-static int run_select2(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint32_t *outA,
-                       uint32_t *outB, uint32_t *cntA, uint32_t *cntB) {
-    *cntA = 0;
-    if (cntB) *cntB = 0;
-    if (n == 0) return SG_OK;
-    const uint32_t ntiles = (n + SEL_TILE - 1) / SEL_TILE;
-    uint64_t *status;
-    SG_TRY(slot(c, S_COUNT, (size_t)ntiles + 4, &status));
-    uint32_t *counter = reinterpret_cast<uint32_t *>(status + ntiles);
-    SG_HIP(hipMemsetAsync(status, 0, ((size_t)ntiles + 4) * 8, c->stream));
-    SG_LAUNCH(c, name, k_select2<Pred>, ntiles, SEL_BLOCK, 0, pred, n, outA, outB, status, counter, ntiles);
-    uint32_t cnt[3];
-    SG_TRY(ctx_readback(c, cnt, counter, 12));
-    *cntA = cnt[1];
-    if (cntB) *cntB = cnt[2];
-    // model: the predicate reads ~8 B per item; 4 B written per selected index
-    prof_bytes(c, name, 8.0 * n + 4.0 * (cnt[1] + (cntB ? cnt[2] : 0)));
-    return SG_OK;
-}
-
-template <class Fn>
-static int run_scan64(sg_ctx *c, const char *name, Fn fn, uint32_t n, uint64_t *out, uint64_t *total) {
-    *total = 0;
-    if (n == 0) return SG_OK;
-    const uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-    uint64_t *status;
-    SG_TRY(slot(c, S_COUNT, (size_t)ntiles + 4, &status));
-    uint32_t *counter = reinterpret_cast<uint32_t *>(status + ntiles);
-    SG_HIP(hipMemsetAsync(status, 0, ((size_t)ntiles + 4) * 8, c->stream));
-    SG_LAUNCH_B(c, name, 12.0 * n, k_scan64<Fn>, ntiles, SCAN_BLOCK, 0, fn, n, out, status, counter, ntiles);
-    uint32_t cnt[3];
-    SG_TRY(ctx_readback(c, cnt, counter, 12));
-    *total = (uint64_t)cnt[1] | ((uint64_t)cnt[2] << 32);
+// Queue one emit (no host sync): count pass, tile scan, apply pass. *total_out: device u64,
+// (records << 32 | bytes). `bytes_model`: algorithmic bytes credited to the apply launch
+// (DESIGN.md §4).
+template <class Item>
+static int run_emit(sg_ctx *c, const char *name, const char *cname, int status_slot, Item item, uint32_t n,
+                    const uint8_t *src, uint8_t *dst, uint2 *out_spans, const uint64_t *kin, uint64_t *kout,
+                    uint64_t **total_out, double bytes_model) {
+    const uint32_t ntiles = (n + EM_TILE - 1) / EM_TILE;
+    uint64_t *tp;  // tot[ntiles] | pre[ntiles] | total
+    SG_TRY(slot(c, status_slot, 2 * (size_t)ntiles + 4, &tp));
+    uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
+    *total_out = total;
+    if (ntiles == 0) {
+        SG_HIP(hipMemsetAsync(total, 0, 8, c->stream));
+        return SG_OK;
+    }
+    uint2 *cache;
+    SG_TRY(slot(c, S_ECACHE, (size_t)n + 1, &cache));
+    static const int dbg = getenv("SG_EMIT_DEBUG") ? atoi(getenv("SG_EMIT_DEBUG")) : 0;
+    SG_LAUNCH(c, cname, k_emit_count<Item>, ntiles, EM_BLOCK, 0, item, n, cache, tot);
+    SG_TRY(tile_scan(c, tot, ntiles, pre, total));
+    SG_LAUNCH_B(c, name, bytes_model, k_emit_apply, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin,
+                kout, dbg & 1);
     return SG_OK;
 }
 
@@ -75,43 +71,43 @@ struct FlagPred {
     __device__ uint32_t operator()(uint32_t i) const { return f[i] ? 1u : 0u; }
 };
 
-// Over sorted keys: uniq[i] = head(i); A = start of a multi-record tag-8 group,
-// B = its last record.
-struct GroupPred {
+// Over the key0-sorted order: brk[i] = i starts a new key0 group; A/B = first/last
+// position of a tag-8 group of more than WAVE_GROUP records (they share 7 bytes).
+struct BigGroupPred {
     const uint64_t *K;
-    uint8_t *uniq;
+    uint8_t *brk;
     uint32_t n;
     __device__ uint32_t operator()(uint32_t i) const {
         const uint64_t k = K[i];
         const bool head = (i == 0) || K[i - 1] != k;
+        brk[i] = head ? 1 : 0;
+        if ((k & 0xffu) != 8u) return 0u;
         const bool tail = (i + 1 == n) || K[i + 1] != k;
-        uniq[i] = head ? 1 : 0;
-        const bool t8 = (k & 0xffu) == 8u;
-        return (t8 && head && !tail ? 1u : 0u) | (t8 && tail && !head ? 2u : 0u);
+        const bool bh = head && (i + WAVE_GROUP < n) && K[i + WAVE_GROUP] == k;
+        const bool bt = tail && (i >= WAVE_GROUP) && K[i - WAVE_GROUP] == k;
+        return (bh ? 1u : 0u) | (bt ? 2u : 0u);
     }
 };
 
-// Over the final order of a refinement round: sub-groups by (gid, chunk key).
+// Over the final order of a refinement round: sub-segments by (group, chunk key). brk at
+// every sub-segment head; A/B = bounds of tag-8 sub-segments of more than WAVE_GROUP rows.
 struct RoundGroupPred {
     const uint64_t *FK;     // chunk key, final order
     const uint32_t *G;      // group index, final order
     const uint32_t *P;      // global position, final order
-    uint8_t *uniq;
+    uint8_t *brk;
     uint32_t n;
     __device__ uint32_t operator()(uint32_t i) const {
         const uint64_t k = FK[i];
         const uint32_t g = G[i];
         const bool head = (i == 0) || FK[i - 1] != k || G[i - 1] != g;
+        brk[P[i]] = head ? 1 : 0;
+        if ((k & 0xffu) != 8u) return 0u;
         const bool tail = (i + 1 == n) || FK[i + 1] != k || G[i + 1] != g;
-        uniq[P[i]] = head ? 1 : 0;
-        const bool t8 = (k & 0xffu) == 8u;
-        return (t8 && head && !tail ? 1u : 0u) | (t8 && tail && !head ? 2u : 0u);
+        const bool bh = head && (i + WAVE_GROUP < n) && FK[i + WAVE_GROUP] == k && G[i + WAVE_GROUP] == g;
+        const bool bt = tail && (i >= WAVE_GROUP) && FK[i - WAVE_GROUP] == k && G[i - WAVE_GROUP] == g;
+        return (bh ? 1u : 0u) | (bt ? 2u : 0u);
     }
-};
-
-struct BigGroupPred {
-    const uint32_t *GS, *GE;
-    __device__ uint32_t operator()(uint32_t i) const { return (GE[i] - GS[i] + 1u > WAVE_GROUP) ? 1u : 0u; }
 };
 
 struct DenseLenFn {
@@ -120,11 +116,8 @@ struct DenseLenFn {
 };
 
 struct GroupSizeFn {
-    const uint32_t *GS, *GE, *big;
-    __device__ uint64_t operator()(uint32_t i) const {
-        const uint32_t g = big[i];
-        return (uint64_t)(GE[g] - GS[g] + 1u);
-    }
+    const uint32_t *GS, *GE;
+    __device__ uint64_t operator()(uint32_t g) const { return (uint64_t)(GE[g] - GS[g] + 1u); }
 };
 
 __device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint2 *spans,
@@ -134,72 +127,12 @@ __device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint2 *spa
     return rec_cmp_k(buf, spans[ra].x, spans[ra].y, buf, spans[rb].x, spans[rb].y, off + 7);
 }
 
-// ------------------------------------------------------------------ refinement kernels
-// Every group (records sharing `off` bytes, >= 2 members): one thread checks whether all
-// members are byte-identical to the first (the common case: duplicates). If so the first
-// stays unique and the rest are duplicates, order unchanged. Otherwise (or above
-// EQ_GROUP members) the group is flagged for ranking.
-__global__ __launch_bounds__(256) void k_refine_eq(const uint8_t *__restrict__ buf,
-                                                   const uint2 *__restrict__ spans,
-                                                   const uint32_t *__restrict__ GS,
-                                                   const uint32_t *__restrict__ GE, uint32_t G,
-                                                   const uint32_t *__restrict__ V, uint8_t *uniq,
-                                                   uint32_t off, uint8_t *unresolved) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= G) return;
-    const uint32_t s = GS[g], k = GE[g] - s + 1u;
-    bool same = k <= EQ_GROUP;
-    if (same) {
-        const uint32_t m0 = V[s];
-        const uint32_t s0 = spans[m0].x, e0 = spans[m0].y;
-        for (uint32_t a = 1; a < k; ++a) {
-            const uint32_t m = V[s + a];
-            if (!rec_equal(buf, s0, e0, buf, spans[m].x, spans[m].y, off)) { same = false; break; }
-        }
-    }
-    if (same)
-        for (uint32_t a = 1; a < k; ++a) uniq[s + a] = 0;
-    unresolved[g] = same ? 0 : 1;
-}
-
-// Unresolved groups of <= 64 records: one wave per group, one member per lane; each lane counts the
-// members that precede it (stable), duplicates are members equal to an earlier one.
-__global__ __launch_bounds__(256) void k_refine_wave(const uint8_t *__restrict__ buf,
-                                                     const uint2 *__restrict__ spans,
-                                                     const uint32_t *__restrict__ GS,
-                                                     const uint32_t *__restrict__ GE, uint32_t G,
-                                                     uint32_t *V, uint8_t *uniq, uint32_t off) {
-    const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const uint32_t lane = lane_id();
-    if (g >= G) return;
-    const uint32_t s = GS[g], k = GE[g] - s + 1u;
-    if (k > WAVE_GROUP) return;
-    const bool act = lane < k;
-    const uint32_t m = act ? V[s + lane] : 0u;
-    const uint64_t key = act ? chunk_key(buf, spans[m].x, spans[m].y, off) : ~0ull;
-    uint32_t rank = 0;
-    bool dup = false;
-    for (uint32_t j = 0; j < k; ++j) {
-        const uint64_t kb = __shfl(key, (int)j, 64);
-        const uint32_t mb = __shfl(m, (int)j, 64);
-        if (act && j != lane) {
-            const int c = key_cmp_full(buf, spans, key, m, kb, mb, off);
-            if (c > 0 || (c == 0 && j < lane)) rank++;
-            if (c == 0 && j < lane) dup = true;
-        }
-    }
-    if (act) {
-        V[s + rank] = m;
-        uniq[s + rank] = dup ? 0 : 1;
-    }
-}
-
-// Expand big groups into member rows: row j -> group index (into big list), global
-// position, and the record's chunk key at `off`.
+// ------------------------------------------------------------------ refinement rounds
+// Expand big groups into member rows: row j -> group index, global position, and the
+// record's chunk key at `off`.
 __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
                                                 const uint2 *__restrict__ spans,
                                                 const uint32_t *__restrict__ GS,
-                                                const uint32_t *__restrict__ big,
                                                 const uint64_t *__restrict__ goff, uint32_t B,
                                                 const uint32_t *__restrict__ V, uint32_t M,
                                                 uint32_t off, uint64_t *RK, uint32_t *RG,
@@ -211,20 +144,11 @@ __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
         const uint32_t mid = (lo + hi) >> 1;
         if (goff[mid] <= j) lo = mid; else hi = mid;
     }
-    const uint32_t pos = GS[big[lo]] + (j - (uint32_t)goff[lo]);
+    const uint32_t pos = GS[lo] + (j - (uint32_t)goff[lo]);
     const uint32_t r = V[pos];
     RK[j] = chunk_key(buf, spans[r].x, spans[r].y, off);
     RG[j] = lo;
     RP[j] = pos;
-}
-
-__global__ void k_gather_pair(const uint32_t *__restrict__ idx, const uint32_t *__restrict__ A,
-                              const uint32_t *__restrict__ B, uint32_t n, uint32_t *A2, uint32_t *B2) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t q = idx[i];
-    A2[i] = A[q];
-    B2[i] = B[q];
 }
 
 __global__ void k_gid_keys(const uint32_t *__restrict__ RG, const uint32_t *__restrict__ perm,
@@ -256,20 +180,159 @@ __global__ void k_pos_of(const uint32_t *__restrict__ idx, const uint32_t *__res
     if (i < n) out[i] = RP[idx[i]];
 }
 
-// ------------------------------------------------------------------ gathers / output
-// Selected positions -> record id, key0 and serialized length (len + 1) per record.
-__global__ void k_gather_sel(const uint32_t *__restrict__ sel, const uint32_t *__restrict__ V,
-                             const uint64_t *__restrict__ K, const uint2 *__restrict__ spans, uint32_t n, uint32_t *UR, uint64_t *UK,
-                             uint32_t *UL) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t p = sel[i];
-    const uint32_t r = V ? V[p] : p;
-    UR[i] = r;
-    if (UK) UK[i] = K[p];
-    UL[i] = spans[r].y - spans[r].x + 1u;
+// ------------------------------------------------------------------ segment sort (spans in S)
+// A segment is a maximal run [a, b] with brk[a] = 1 and brk[a+1..b] = 0: its records share
+// their first 7 bytes (equal key0; inside big groups, the refined chunks too) but are not
+// yet in byte order. A segment holding two different records ("bad") has <= 64 members:
+// bigger groups went through the refinement rounds. Sorting permutes the segment's spans
+// into S (and recomputes dup); the bytes in S stay where they are, and the unique emit
+// gathers through the permuted spans (still inside the same few cache lines).
+constexpr uint32_t SEG_SMALL = 16;
+
+// Memcmp-then-length of two records of `buf` from byte `off`, 8 bytes per step.
+__device__ __forceinline__ int rec_cmp8(const uint8_t *buf, uint32_t sa, uint32_t la, uint32_t sb, uint32_t lb,
+                                        uint32_t off) {
+    const uint32_t m = la < lb ? la : lb;
+    for (uint32_t o = off; o < m; o += 8) {
+        const uint32_t t = (m - o) < 8u ? (m - o) : 8u;
+        const uint64_t x = load_le(buf, sa + o, t), y = load_le(buf, sb + o, t);
+        if (x != y) return __builtin_bswap64(x) < __builtin_bswap64(y) ? -1 : 1;
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
 }
 
+// dup[i] = record i equals record i-1 inside its segment (tag < 8 key0: whole record).
+__global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S, const uint2 *__restrict__ SS,
+                                                  const uint64_t *__restrict__ K, const uint8_t *__restrict__ brk,
+                                                  uint32_t n, uint8_t *__restrict__ dup, uint8_t *__restrict__ bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    bool d = false, b = false;
+    if (i > 0 && !brk[i]) {
+        if ((K[i] & 0xffu) < 8u) {
+            d = true;
+        } else {
+            const uint2 x = SS[i - 1], y = SS[i];
+            d = rec_equal(S, x.x, x.y, S, y.x, y.y, 7);
+        }
+        b = !d;
+    }
+    dup[i] = d ? 1 : 0;
+    bad[i] = b ? 1 : 0;
+}
+
+// Segment heads whose segment holds a bad position: A = up to SEG_SMALL members, B = more.
+struct SegPred {
+    const uint8_t *brk, *bad;
+    uint32_t n;
+    __device__ uint32_t operator()(uint32_t i) const {
+        if (!brk[i] || i + 1 >= n || brk[i + 1]) return 0u;
+        bool anyb = false;
+        uint32_t j = i + 1;
+        for (; j < n && j <= i + 64u && !brk[j]; ++j) anyb |= bad[j] != 0;
+        if (!anyb) return 0u;
+        return (j - i <= SEG_SMALL) ? 1u : 2u;
+    }
+};
+
+__device__ __forceinline__ uint32_t seg_len(const uint8_t *brk, uint32_t a, uint32_t n, uint32_t cap) {
+    uint32_t j = a + 1;
+    while (j < n && j < a + cap && !brk[j]) ++j;
+    return j - a;
+}
+
+// 16 lanes per small segment (<= SEG_SMALL members), lane per member. The segment's
+// bytes are contiguous in S: staged into the group's LDS window with 16-byte loads, then
+// every lane ranks its record against the others from LDS (stable; dup = an equal member
+// precedes it). Segments wider than the window compare from S directly.
+constexpr uint32_t SEG_WIN = 1024;
+
+__device__ __forceinline__ int win_cmp(const uint8_t *w, uint32_t sa, uint32_t la, uint32_t sb, uint32_t lb,
+                                       uint32_t off) {
+    const uint32_t m = la < lb ? la : lb;
+    for (uint32_t i = off; i < m; ++i) {
+        const uint32_t x = w[sa + i], y = w[sb + i];
+        if (x != y) return (int)x - (int)y;
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+__global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
+                                                   const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
+                                                   const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_w[16][SEG_WIN];
+    const uint32_t lane = lane_id(), gl = lane & 15u, gbase = lane & ~15u;
+    const uint32_t grp = threadIdx.x >> 4;
+    const uint32_t q = blockIdx.x * 16u + grp;
+    const bool live = q < nh;
+    const uint32_t a = live ? heads[q] : 0u;
+    const uint32_t pe = a + 1u + gl;
+    const bool eb = !live || pe >= n || gl == 15u || brk[pe];
+    const uint32_t me = (uint32_t)(__ballot(eb) >> gbase) & 0xffffu;
+    const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);  // members: a .. a+k-1
+    const bool act = live && gl < k;
+    const uint2 x = act ? SS[a + gl] : make_uint2(0u, 0u);
+    const uint32_t len = x.y - x.x;
+    const uint32_t r0 = (uint32_t)__shfl(x.x, (int)gbase, 64);
+    const uint32_t r1 = (uint32_t)__shfl(x.y, (int)(gbase + k - 1u), 64) + 1u;
+    const uint32_t base = r0 & ~15u;
+    const bool in_lds = live && (r1 - base <= SEG_WIN);
+    uint8_t *w = s_w[grp];
+    if (in_lds)
+        for (uint32_t o = base + 16u * gl; o < r1; o += 256u)
+            *reinterpret_cast<uint4 *>(w + (o - base)) = *reinterpret_cast<const uint4 *>(S + o);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint32_t rank = 0;
+    bool d = false;
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint32_t ys = (uint32_t)__shfl(x.x, (int)(gbase + j), 64);
+        const uint32_t ye = (uint32_t)__shfl(x.y, (int)(gbase + j), 64);
+        if (act && j != gl) {
+            const int c = in_lds ? win_cmp(w, x.x - base, len, ys - base, ye - ys, 7)
+                                 : rec_cmp8(S, x.x, len, ys, ye - ys, 7);
+            if (c > 0 || (c == 0 && j < gl)) ++rank;
+            if (c == 0 && j < gl) d = true;
+        }
+    }
+    if (act) {
+        SS[a + rank] = x;
+        dup[a + rank] = d ? 1 : 0;
+    }
+}
+
+// One wave per larger segment (<= 64 members): lane per member.
+__global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
+                                                  const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
+                                                  const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n,
+                                                  uint32_t *err) {
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = lane_id();
+    if (q >= nh) return;
+    const uint32_t a = heads[q];
+    const uint32_t pe = a + 1u + lane;
+    const uint64_t me = __ballot(pe >= n || brk[pe]);
+    if (!me) { if (lane == 0) atomicOr(err, 1u); return; }
+    const uint32_t k = 1u + (uint32_t)(__ffsll((long long)me) - 1);
+    const bool act = lane < k;
+    const uint2 x = act ? SS[a + lane] : make_uint2(0u, 0u);
+    uint32_t rank = 0;
+    bool d = false;
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint32_t ys = (uint32_t)__shfl(x.x, (int)j, 64), ye = (uint32_t)__shfl(x.y, (int)j, 64);
+        if (act && j != lane) {
+            const int c = rec_cmp8(S, x.x, x.y - x.x, ys, ye - ys, 7);
+            if (c > 0 || (c == 0 && j < lane)) ++rank;
+            if (c == 0 && j < lane) d = true;
+        }
+    }
+    if (act) {
+        SS[a + rank] = x;
+        dup[a + rank] = d ? 1 : 0;
+    }
+}
+
+// ------------------------------------------------------------------ gathers / output
 __global__ void k_gather_rl(const uint32_t *__restrict__ idx, const uint32_t *__restrict__ R,
                             const uint32_t *__restrict__ L, uint32_t n, uint32_t *R2, uint32_t *L2) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -277,6 +340,11 @@ __global__ void k_gather_rl(const uint32_t *__restrict__ idx, const uint32_t *__
     const uint32_t q = idx[i];
     R2[i] = R[q];
     L2[i] = L[q];
+}
+
+__global__ void k_mark(const uint32_t *__restrict__ idx, uint32_t n, uint8_t *flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[idx[i]] = 1;
 }
 
 constexpr uint32_t CP_WAVE_BYTES = 8192;
@@ -486,75 +554,34 @@ int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
     return serialize_dense(c, d_buf, spans, recs, L, count, 0, dst, dst_cap, &o, bytes);
 }
 
-int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet &ss, SortedSet *out) {
-    const uint32_t R = L.n_rec;
-    out->n = R;
-    uint64_t *k2;
-    uint32_t *v1, *v2;
-    SG_TRY(slot(c, ss.keys2, R, &k2));
-    SG_TRY(slot(c, ss.vals, R, &v1));
-    SG_TRY(slot(c, ss.vals2, R, &v2));
-    uint8_t *uniq;
-    SG_TRY(slot(c, ss.uniq, R, &uniq));
-    out->uniq = uniq;
-    if (R == 0) { out->keys = L.keys; out->recs = v1; return SG_OK; }
-    uint64_t *K;
-    uint32_t *V;
-    SG_TRY(radix_sort(c, L.keys, v1, k2, v2, R, 0, 64, true, &K, &V));
-    out->keys = K;
-    out->recs = V;
 
-    // groups of the first chunk
-    uint32_t *GS, *GE;
-    SG_TRY(slot(c, S_GS, R / 2 + 16, &GS));
-    SG_TRY(slot(c, S_GE, R / 2 + 16, &GE));
-    uint32_t G = 0, G2 = 0;
-    SG_TRY(run_select2(c, "mark_groups", GroupPred{K, uniq, R}, R, GS, GE, &G, &G2));
-    if (G != G2) { set_error("group start/end mismatch %u/%u", G, G2); return SG_E_HIP; }
-
+// ------------------------------------------------------------------ big-group rounds
+// Positions GS[g]..GE[g] (g < B) are groups of > 64 records sharing their first `off`
+// bytes. Each round sorts every group's members by the next 7-byte chunk (stable), marks
+// sub-segment heads in brk, and keeps the sub-segments that are still > 64 records.
+static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, uint32_t *V, uint8_t *brk,
+                             uint32_t *GS, uint32_t *GE, uint32_t B) {
     uint32_t off = 7;
-    while (G > 0) {
-        uint8_t *unres;
-        SG_TRY(slot(c, S_M_TMP, (size_t)G + 16, &unres));
-        // model: per group GS/GE + flag; per member id, start, end and ~26 record bytes twice
-        SG_LAUNCH_B(c, "refine_eq", 9.0 * G + 64.0 * 2.0 * G, k_refine_eq, grid_for(G, 256), 256, 0, d_buf, L.spans, GS, GE, G, V, uniq, off, unres);
-        uint32_t *ulist;
-        SG_TRY(slot(c, S_SEL, (size_t)G + 16, &ulist));
-        uint32_t Ux = 0;
-        SG_TRY(select_flags(c, unres, G, ulist, &Ux));
-        if (Ux == 0) break;
-        uint32_t *GS2, *GE2;
-        SG_TRY(slot(c, S_R_GID, (size_t)Ux + 16, &GS2));
-        SG_TRY(slot(c, S_R_POS, (size_t)Ux + 16, &GE2));
-        SG_LAUNCH(c, "gather_groups", k_gather_pair, grid_for(Ux, 256), 256, 0, ulist, GS, GE, Ux, GS2, GE2);
-        SG_LAUNCH(c, "refine_wave", k_refine_wave, grid_for(Ux, 4), 256, 0, d_buf, L.spans, GS2, GE2, Ux, V, uniq, off);
-        // unresolved groups above one wave -> a radix round on the next chunk
-        uint32_t *big;
-        SG_TRY(slot(c, S_SEL, Ux + 16, &big));
-        uint32_t B = 0;
-        SG_TRY(run_select2(c, "select_big", BigGroupPred{GS2, GE2}, Ux, big, (uint32_t *)nullptr, &B, nullptr));
-        if (B == 0) break;
-        SG_HIP(hipMemcpyAsync(GS, GS2, (size_t)Ux * 4, hipMemcpyDeviceToDevice, c->stream));
-        SG_HIP(hipMemcpyAsync(GE, GE2, (size_t)Ux * 4, hipMemcpyDeviceToDevice, c->stream));
+    while (B > 0) {
         uint64_t *goff;
         SG_TRY(slot(c, S_R_OFF, (size_t)B + 1, &goff));
         uint64_t M64 = 0;
-        SG_TRY(run_scan64(c, "scan_groups", GroupSizeFn{GS, GE, big}, B, goff, &M64));
+        SG_TRY(run_scan64(c, "scan_groups", GroupSizeFn{GS, GE}, B, goff, &M64));
         const uint32_t M = (uint32_t)M64;
-        uint64_t *RK, *RK2, *GK;
-        uint32_t *RG, *RP, *RV, *RV2, *T;
+        uint64_t *RK, *RK2;
+        uint32_t *RG, *RP, *RV, *RV2;
         SG_TRY(slot(c, S_R_KEY, M, &RK));
         SG_TRY(slot(c, S_R_KEY2, M, &RK2));
         SG_TRY(slot(c, S_R_GID, M, &RG));
         SG_TRY(slot(c, S_R_POS, M, &RP));
         SG_TRY(slot(c, S_R_VAL, M, &RV));
         SG_TRY(slot(c, S_R_VAL2, M, &RV2));
-        SG_LAUNCH(c, "round_expand", k_expand, grid_for(M, 256), 256, 0, d_buf, L.spans, GS, big, goff, B, V, M, off, RK, RG, RP);
+        SG_LAUNCH(c, "round_expand", k_expand, grid_for(M, 256), 256, 0, d_buf, spans, GS, goff, B, V, M, off, RK, RG, RP);
         uint64_t *SK;
         uint32_t *perm;
         SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, 64, true, &SK, &perm, "rs_pass_refine"));
         // stable by group index on top: keys = gid of each row in current order
-        GK = (SK == RK) ? RK2 : RK;
+        uint64_t *GK = (SK == RK) ? RK2 : RK;
         uint32_t *pv_alt = (perm == RV) ? RV2 : RV;
         SG_LAUNCH(c, "round_gid", k_gid_keys, grid_for(M, 256), 256, 0, RG, perm, GK, M);
         int gbits = 1;
@@ -563,118 +590,206 @@ int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet 
         uint64_t *FKs;
         uint32_t *perm2;
         SG_TRY(radix_sort(c, GK, perm, GK2, pv_alt, M, 0, gbits, false, &FKs, &perm2, "rs_pass_refine"));
-        T = (perm2 == perm) ? pv_alt : perm;
+        uint32_t *T = (perm2 == perm) ? pv_alt : perm;
         uint64_t *FK = (FKs == GK) ? GK2 : GK;
-        SG_LAUNCH(c, "round_gather", k_round_gather, grid_for(M, 256), 256, 0, d_buf, L.spans, V, RP, perm2, M, off, T, FK);
+        SG_LAUNCH(c, "round_gather", k_round_gather, grid_for(M, 256), 256, 0, d_buf, spans, V, RP, perm2, M, off, T, FK);
         SG_LAUNCH(c, "round_scatter", k_round_scatter, grid_for(M, 256), 256, 0, T, RP, M, V);
-        // sub-groups: RG is the group index of final row i as well (same row ranges);
         // perm2/T are free again after the scatter (same stream)
         uint32_t *NS = perm2, *NE = T;
-        uint32_t G3 = 0, G4 = 0;
-        SG_TRY(run_select2(c, "round_mark", RoundGroupPred{FK, RG, RP, uniq, M}, M, NS, NE, &G3, &G4));
-        if (G3 != G4) { set_error("round group mismatch"); return SG_E_HIP; }
-        if (G3) {
-            SG_LAUNCH(c, "round_pos", k_pos_of, grid_for(G3, 256), 256, 0, NS, RP, G3, GS);
-            SG_LAUNCH(c, "round_pos", k_pos_of, grid_for(G3, 256), 256, 0, NE, RP, G3, GE);
+        uint32_t B3 = 0, B4 = 0;
+        SG_TRY(run_select2(c, "round_mark", RoundGroupPred{FK, RG, RP, brk, M}, M, NS, NE, &B3, &B4));
+        if (B3 != B4) { set_error("round group mismatch %u/%u", B3, B4); return SG_E_HIP; }
+        if (B3) {
+            SG_LAUNCH(c, "round_pos", k_pos_of, grid_for(B3, 256), 256, 0, NS, RP, B3, GS);
+            SG_LAUNCH(c, "round_pos", k_pos_of, grid_for(B3, 256), 256, 0, NE, RP, B3, GE);
         }
-        G = G3;
+        B = B3;
         off += 7;
     }
     return SG_OK;
 }
 
-// Parsed + sorted-unique view of one buffer.
-struct UniqView {
-    Lines L;
-    uint32_t *UR = nullptr;  // record ids, byte order (null = identity 0..U-1)
-    uint64_t *UK = nullptr;  // key0 per unique record
-    uint32_t *UL = nullptr;  // serialized length per unique record (may be null)
-    uint32_t U = 0;
+// ------------------------------------------------------------------ unique view
+// The sorted unique records of one buffer: serialized ('\n'-terminated, byte order) with
+// per-record spans into `buf` and key0. For a prior that is already strictly increasing
+// the view is the input itself.
+struct UView {
+    const uint8_t *buf = nullptr;
+    const uint2 *spans = nullptr;
+    const uint64_t *keys = nullptr;
+    uint32_t n = 0;
+    uint64_t bytes = 0;
+    uint32_t in_records = 0;
 };
 
-static int unique_view(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, int ur_slot,
-                       int uk_slot, int ul_slot, bool trust_sorted, UniqView *uv) {
-    SG_TRY(run_lines(c, d_buf, n, ss, &uv->L));
-    const uint32_t R = uv->L.n_rec;
+struct ViewSlots {
+    SlotSet lines;
+    int ubuf, uspans, ukeys;
+};
+
+static const ViewSlots CUR_VIEW = {CUR_SLOTS, S_OUT_UNIQ, S_U_SPANS, S_U_KEYS};
+static const ViewSlots PRIOR_VIEW = {PRIOR_SLOTS, S_P_UBUF, S_P_USPANS, S_P_UKEYS};
+
+static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
+                        UView *uv) {
+    *uv = UView{};
+    Lines L;
+    SG_TRY(run_lines(c, d_buf, n, vs.lines, &L));
+    const uint32_t R = L.n_rec;
+    uv->in_records = R;
+    if (R >= (1u << 30)) { set_error("%u records exceed the 2^30 per-call limit", R); return SG_E_TOO_LARGE; }
     if (trust_sorted && R > 1) {
         uint32_t *flag;
         SG_TRY(slot(c, S_M_CNT, 4, &flag));
         SG_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
-        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, uv->L.spans, uv->L.keys, R, flag);
+        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, L.spans, L.keys, R, flag);
         uint32_t f = 1;
         SG_TRY(ctx_readback(c, &f, flag, 4));
         trust_sorted = (f == 0);
     }
-    if (trust_sorted) {
-        uv->UR = nullptr;
-        uv->UK = uv->L.keys;
-        uv->UL = nullptr;
-        uv->U = R;
-        return SG_OK;
+    if (trust_sorted || R <= 1) {
+        if (R == 1 || trust_sorted) {
+            uv->buf = d_buf;
+            uv->spans = L.spans;
+            uv->keys = L.keys;
+            uv->n = R;
+            uv->bytes = R ? (uint64_t)0 : 0;  // not used for an input view
+            if (!trust_sorted) {
+                // a single record: serialize it (the caller may return this view)
+                uint8_t *ub;
+                uint2 *us;
+                uint64_t *uk;
+                SG_TRY(slot(c, vs.ubuf, (size_t)n + 64, &ub));
+                SG_TRY(slot(c, vs.uspans, 1, &us));
+                SG_TRY(slot(c, vs.ukeys, 1, &uk));
+                uint64_t *cnt;
+                SG_TRY(run_emit(c, "emit_uniq", "emit_uniq.count", S_EMIT2, PermItem{nullptr, L.spans}, R, d_buf, ub,
+                                us, L.keys, uk, &cnt, 0.0));
+                uint64_t t = 0;
+                SG_TRY(ctx_readback(c, &t, cnt, 8));
+                *uv = UView{ub, us, uk, (uint32_t)(t >> 32), (uint32_t)t, R};
+            }
+            return SG_OK;
+        }
+        uint8_t *ub;
+        SG_TRY(slot(c, vs.ubuf, 64, &ub));
+        uv->buf = ub;
+        return SG_OK;  // R == 0
     }
-    SortedSet S;
-    SG_TRY(sort_records(c, d_buf, uv->L, ss, &S));
-    uint32_t *sel;
-    SG_TRY(slot(c, S_SEL, R + 16, &sel));
-    uint32_t U = 0;
-    SG_TRY(select_flags(c, S.uniq, R, sel, &U));
-    SG_TRY(slot(c, ur_slot, (size_t)U + 1, &uv->UR));
-    SG_TRY(slot(c, uk_slot, (size_t)U + 1, &uv->UK));
-    SG_TRY(slot(c, ul_slot, (size_t)U + 1, &uv->UL));
-    if (U) SG_LAUNCH_B(c, "gather_uniq", 40.0 * U, k_gather_sel, grid_for(U, 256), 256, 0, sel, S.recs, S.keys, uv->L.spans, U, uv->UR, uv->UK, uv->UL);
-    uv->U = U;
+
+    // sort by key0
+    uint64_t *k2;
+    uint32_t *v1, *v2;
+    SG_TRY(slot(c, vs.lines.keys2, R, &k2));
+    SG_TRY(slot(c, vs.lines.vals, R, &v1));
+    SG_TRY(slot(c, vs.lines.vals2, R, &v2));
+    uint64_t *K;
+    uint32_t *V;
+    SG_TRY(radix_sort(c, L.keys, v1, k2, v2, R, 0, 64, true, &K, &V));
+
+    // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
+    uint8_t *brk;
+    SG_TRY(slot(c, S_BRK, R, &brk));
+    uint32_t *GS, *GE;
+    SG_TRY(slot(c, S_GS, R / 64 + 16, &GS));
+    SG_TRY(slot(c, S_GE, R / 64 + 16, &GE));
+    uint32_t B = 0, B2 = 0;
+    SG_TRY(run_select2(c, "mark_groups", BigGroupPred{K, brk, R}, R, GS, GE, &B, &B2, 9.0));
+    if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
+    if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B));
+
+    // materialise the records in this order: S (contiguous), SS spans into S
+    uint8_t *Sb;
+    uint2 *SS;
+    SG_TRY(slot(c, S_SBUF, (size_t)n + 64, &Sb));
+    SG_TRY(slot(c, S_SSPANS, R, &SS));
+    uint64_t *pc;
+    // model: input bytes read + S written once; cached span per record in, span per record out
+    SG_TRY(run_emit(c, "emit_sorted", "emit_sorted.count", S_EMIT, PermItem{V, L.spans}, R, d_buf, Sb, SS, nullptr,
+                    nullptr, &pc, 2.0 * (double)n + 16.0 * R));
+
+    // adjacent equality inside segments; segments holding two different records -> sort
+    uint8_t *dup, *bad;
+    SG_TRY(slot(c, S_DUP, R, &dup));
+    SG_TRY(slot(c, S_BAD, R, &bad));
+    // model: key0 + brk + span per record, both records' bytes where compared, dup + bad out
+    SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, k_adjacent, grid_for(R, 256), 256, 0, Sb, SS, K, brk, R, dup, bad);
+    uint32_t *hs, *hb;
+    SG_TRY(slot(c, S_SEL, (size_t)R / 2 + 16, &hs));
+    SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
+    uint32_t ns = 0, nb = 0;
+    SG_TRY(run_select2(c, "seg_heads", SegPred{brk, bad, R}, R, hs, hb, &ns, &nb, 2.0));
+    uint32_t *err;
+    SG_TRY(slot(c, S_ERR, 4, &err));
+    if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
+    if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R);
+    if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for(nb, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err);
+
+    // compact the unique records
+    uint8_t *ub;
+    uint2 *us;
+    uint64_t *uk;
+    SG_TRY(slot(c, vs.ubuf, (size_t)n + 64, &ub));
+    SG_TRY(slot(c, vs.uspans, R, &us));
+    SG_TRY(slot(c, vs.ukeys, R, &uk));
+    uint64_t *uc;
+    SG_TRY(run_emit(c, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
+                    0.0));
+    uint64_t tt = 0;
+    SG_TRY(ctx_readback(c, &tt, uc, 8));
+    const uint32_t t1 = (uint32_t)(tt >> 32), t2 = (uint32_t)tt;
+    // model: cached span per record; kept bytes read + written; span + key0 per kept record
+    if (c->profile) prof_bytes(c, "emit_uniq", 8.0 * R + 2.0 * t2 + 24.0 * t1);
+    if (nb) {
+        uint32_t e = 0;
+        SG_TRY(ctx_readback(c, &e, err, 4));
+        if (e) { set_error("run sort: segment bound violated (0x%x)", e); return SG_E_HIP; }
+    }
+    *uv = UView{ub, us, uk, t1, t2, R};
     return SG_OK;
 }
 
 int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
                    uint64_t n_prior, bool want_fresh, sg_dev_result *res) {
     *res = sg_dev_result{};
-    UniqView cu;
-    SG_TRY(unique_view(c, d_cur, n_cur, CUR_SLOTS, S_CUR_UR, S_CUR_UK, S_FRESH_IDX, false, &cu));
-    res->in_records = cu.L.n_rec;
-    uint8_t *uout;
-    uint64_t ubytes = 0;
-    SG_TRY(serialize_dense(c, d_cur, cu.L.spans, cu.UR, cu.UL, cu.U, S_OUT_UNIQ, nullptr, 0, &uout, &ubytes));
-    res->uniq = uout;
-    res->uniq_bytes = ubytes;
-    res->uniq_records = cu.U;
+    UView pv;
+    const bool have_prior = want_fresh && d_prior && n_prior;
+    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, true, &pv));
+    UView cu;
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu));
+    res->in_records = cu.in_records;
+    res->uniq = const_cast<uint8_t *>(cu.buf);
+    res->uniq_bytes = cu.bytes;
+    res->uniq_records = cu.n;
     if (!want_fresh) return SG_OK;
-
-    UniqView pv;
-    if (d_prior && n_prior) {
-        SG_TRY(unique_view(c, d_prior, n_prior, PRIOR_SLOTS, S_P_REC, S_P_SORTED_KEYS, S_P_FLAG, true, &pv));
-    }
-    res->prior_records = pv.L.n_rec;
-    if (pv.U == 0 || cu.U == 0) {
+    res->prior_records = pv.in_records;
+    if (pv.n == 0 || cu.n == 0) {
         res->fresh = res->uniq;
         res->fresh_bytes = res->uniq_bytes;
         res->fresh_records = res->uniq_records;
         return SG_OK;
     }
     uint8_t *fresh;
-    SG_TRY(slot(c, S_M_TMP, (size_t)cu.U + 1, &fresh));
-    RecSet U{d_cur, cu.L.spans, cu.UR, cu.UK, cu.U};
-    RecSet P{d_prior, pv.L.spans, pv.UR, pv.UK, pv.U};
-    const uint32_t ntiles = (uint32_t)(((uint64_t)cu.U + pv.U + MP_TILE - 1) / MP_TILE);
+    SG_TRY(slot(c, S_FRESHF, (size_t)cu.n + 1, &fresh));
+    RecSet U{cu.buf, cu.spans, nullptr, cu.keys, cu.n};
+    RecSet P{pv.buf, pv.spans, nullptr, pv.keys, pv.n};
+    const uint32_t ntiles = (uint32_t)(((uint64_t)cu.n + pv.n + MP_TILE - 1) / MP_TILE);
     uint32_t *split;
     SG_TRY(slot(c, S_R_OFF, (size_t)ntiles + 2, &split));
     SG_LAUNCH(c, "merge_split", k_merge_split, grid_for(ntiles + 1, 256), 256, 0, U, P, ntiles, split);
-    // model: key+id of every unique cur and prior record, one flag per cur record
-    SG_LAUNCH_B(c, "diff_tile", 12.0 * (cu.U + (double)pv.U) + cu.U, k_diff_tile, ntiles, 256, 0, U, P, split, fresh);
-    uint32_t *fidx;
-    SG_TRY(slot(c, S_SEL, (size_t)cu.U + 16, &fidx));
-    uint32_t F = 0;
-    SG_TRY(select_flags(c, fresh, cu.U, fidx, &F));
-    uint32_t *FR, *FL;
-    SG_TRY(slot(c, S_R_VAL, (size_t)F + 1, &FR));
-    SG_TRY(slot(c, S_R_GID, (size_t)F + 1, &FL));
-    if (F) SG_LAUNCH(c, "gather_fresh", k_gather_rl, grid_for(F, 256), 256, 0, fidx, cu.UR, cu.UL, F, FR, FL);
+    // model: key + span of every unique cur and prior record, one flag per cur record
+    SG_LAUNCH_B(c, "diff_tile", 16.0 * (cu.n + (double)pv.n) + cu.n, k_diff_tile, ntiles, 256, 0, U, P, split, fresh);
     uint8_t *fout;
-    uint64_t fbytes = 0;
-    SG_TRY(serialize_dense(c, d_cur, cu.L.spans, FR, FL, F, S_OUT_FRESH, nullptr, 0, &fout, &fbytes));
+    SG_TRY(slot(c, S_OUT_FRESH, (size_t)cu.bytes + 64, &fout));
+    uint64_t *fc;
+    SG_TRY(run_emit(c, "emit_fresh", "emit_fresh.count", S_EMIT3, FlagItem{cu.spans, fresh, 1}, cu.n, cu.buf, fout,
+                    nullptr, nullptr, nullptr, &fc, 0.0));
+    uint64_t tt = 0;
+    SG_TRY(ctx_readback(c, &tt, fc, 8));
+    if (c->profile) prof_bytes(c, "emit_fresh", 8.0 * cu.n + 2.0 * (double)(uint32_t)tt);
     res->fresh = fout;
-    res->fresh_bytes = fbytes;
-    res->fresh_records = F;
+    res->fresh_bytes = (uint32_t)tt;
+    res->fresh_records = (uint32_t)(tt >> 32);
     return SG_OK;
 }
 

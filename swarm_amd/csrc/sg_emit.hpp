@@ -1,0 +1,282 @@
+// sg_emit.hpp — "emit": order-preserving select + byte-offset scan + record copy, fused
+// into ONE single-pass kernel (decoupled look-back).
+//
+// Item i (0 <= i < n) names a record of `src` by (start, len) and whether it is kept. Kept
+// records are written to `dst` in item order, each '\n'-terminated; optionally the j-th
+// kept record's output span (o, o + len) and a per-item u64 payload (the sort key) are
+// written at j. Used for: materialising the sorted records (gather through a permutation),
+// compacting the unique records out of the sorted buffer, the new-record output, and
+// serialising partitions / match output.
+//
+// Tile = 4 waves x 4 rounds x 64 items. The apply pass scans each wave's 256 items' packed
+// (count:32 | bytes:32) values and adds the tile prefix. The copy then goes round by round:
+// the kept records of one round are one contiguous output span, assembled in a per-wave LDS
+// window and written with 16-byte stores. A record whose aligned source span is <= 64 B is
+// loaded by its own lane (four 16-B loads, the wave's loads all in flight together) and
+// placed with dword stores built by funnel shifts; longer records are copied by 16-lane
+// groups with coalesced word loads. Spans wider than the window go straight to HBM.
+//
+// Limits: fewer than 2^32 kept records and 2^32 output bytes per launch (checked by callers).
+#pragma once
+#include "sg_common.hpp"
+
+namespace sg {
+
+constexpr int EM_BLOCK = 256;
+constexpr int EM_ROUNDS = 4;
+constexpr uint32_t EM_TILE = EM_BLOCK * EM_ROUNDS;
+constexpr uint32_t EM_WIN = 6144;
+constexpr uint64_t EM_ONE = 1ull << 32;
+
+// Per-lane copy of a short record (aligned source span <= 64 B) whose 16-byte source
+// chunks are already in registers: bytes [sh, sh+len) of c[] go to d[0..len), then '\n'.
+template <class Ptr>
+__device__ __forceinline__ void put_short(Ptr d, const uint4 (&c)[4], uint32_t sh, uint32_t len) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t w4[4] = {c[k].x, c[k].y, c[k].z, c[k].w};
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t p = 16 * k + 4 * q + b;
+                if (p >= sh && p < sh + len) d[p - sh] = (uint8_t)(w4[q] >> (8 * b));
+            }
+        }
+    }
+    d[len] = 0x0a;
+}
+
+// LDS-window form of put_short: whole dwords of the destination are built with a funnel
+// shift of two source dwords (one ds_write_b32 each); only the <= 3 head and <= 3 tail
+// bytes of the record are byte stores, from byte loads issued with the chunk loads.
+__device__ __forceinline__ void put_short_win(uint8_t *win, uint32_t d, const uint4 (&c)[4], uint32_t sh,
+                                              uint32_t len, const uint32_t (&hb)[3], uint32_t h,
+                                              const uint32_t (&tb)[3], uint32_t ts, uint32_t tn) {
+    const uint32_t dw[17] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w,
+                             c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w, 0u};
+    const uint32_t e = (sh - d) & 3u;
+#pragma unroll
+    for (uint32_t w = 0; w < 16; ++w) {
+        const uint32_t P = 4 * w + e;
+        if (P >= sh + h && P + 4 <= sh + len) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(dw[w + 1], dw[w], e);
+            *reinterpret_cast<uint32_t *>(win + d + (P - sh)) = v;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+        if (j < h) win[d + j] = (uint8_t)hb[j];
+        if (j < tn) win[d + ts + j] = (uint8_t)tb[j];
+    }
+    win[d + len] = 0x0a;
+}
+
+// Copy the records of one round into out[o0..oend) (base = o0 & ~15): lane-owned record
+// (f, s, len, dst offset d from base). Short records: the lane loads its aligned 16-byte
+// chunks (all loads of the wave in flight together) and places the bytes. Longer records:
+// compacted into s_src/s_len/s_dst and copied by 16-lane groups with coalesced word loads.
+// Assembled in the wave's LDS window when the span fits, then written with 16-byte stores.
+__device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src, uint8_t *__restrict__ out,
+                                                uint8_t *win, uint32_t *s_src, uint32_t *s_len, uint32_t *s_dst,
+                                                bool f, uint32_t s, uint32_t len, uint32_t d, uint64_t o0,
+                                                uint64_t oend, uint64_t base) {
+    const uint32_t lane = lane_id();
+    const uint64_t span = oend - base;
+    const bool in_lds = span <= EM_WIN;
+    const uint32_t q0 = s & ~15u, sh = s - q0;
+    const bool shortr = f && (sh + len <= 64u);
+    uint4 c[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        c[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (shortr && 16u * k < sh + len) c[k] = *reinterpret_cast<const uint4 *>(src + q0 + 16u * k);
+    }
+    // destination dword bounds inside the window: head bytes [d, d+h), whole dwords, tail
+    // bytes [d+ts, d+ts+tn)
+    const uint32_t D0 = (d + 3u) & ~3u, D1 = (d + len) & ~3u;
+    const uint32_t h = (D0 - d) < len ? (D0 - d) : len;
+    const uint32_t ts = (D1 > d + h ? D1 : d + h) - d;
+    const uint32_t tn = len - ts;
+    uint32_t hb[3], tb[3];
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+        hb[j] = (shortr && in_lds && j < h) ? src[s + j] : 0u;
+        tb[j] = (shortr && in_lds && j < tn) ? src[s + ts + j] : 0u;
+    }
+    const bool longr = f && !shortr;
+    const uint64_t ml = __ballot(longr);
+    if (longr) {
+        const uint32_t cidx = (uint32_t)__popcll(ml & ((1ull << lane) - 1ull));
+        s_src[cidx] = s;
+        s_len[cidx] = len;
+        s_dst[cidx] = d;
+    }
+    if (shortr) {
+        if (in_lds) put_short_win(win, d, c, sh, len, hb, h, tb, ts, tn);
+        else put_short(out + base + d, c, sh, len);
+    }
+    if (ml) {
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t cnt = (uint32_t)__popcll(ml);
+        const uint32_t g = lane >> 4, gl = lane & 15;
+        for (uint32_t j = g; j < cnt; j += 4) {
+            const uint32_t sj = s_src[j], lj = s_len[j];
+            const uint32_t ej = sj + lj;
+            const uint32_t a0 = sj & ~3u;
+            uint8_t *dd = (in_lds ? win : out + base) + s_dst[j];
+            for (uint32_t a = a0 + 4 * gl; a < ej; a += 64) {
+                const uint32_t x = *reinterpret_cast<const uint32_t *>(src + a);
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) {
+                    const uint32_t p = a + b;
+                    if (p >= sj && p < ej) dd[p - sj] = (uint8_t)(x >> (8 * b));
+                }
+            }
+            if (gl == 0) dd[lj] = 0x0a;
+        }
+    }
+    if (!in_lds) return;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t nch = (uint32_t)((span + 15) / 16);
+    for (uint32_t ch = lane; ch < nch; ch += 64) {
+        const uint64_t ga = base + 16ull * ch;
+        if (ga >= o0 && ga + 16 <= oend) {
+            *reinterpret_cast<uint4 *>(out + ga) = *reinterpret_cast<const uint4 *>(win + 16 * ch);
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 16; ++b) {
+                const uint64_t ad = ga + b;
+                if (ad >= o0 && ad < oend) out[ad] = win[16 * ch + b];
+            }
+        }
+    }
+}
+
+// Reduce-then-scan form (3 launches, no inter-block waits):
+//   k_emit_count<Item>: item i -> cache[i] = (start, len) or (0, EM_DROP); per-tile packed
+//                       (count << 32 | bytes) aggregate -> tot[tile]
+//   k_tile_scan:        exclusive tile prefixes + grand total
+//   k_emit_apply:       per tile: re-scan the cached items, add the tile prefix, write
+//                       out_spans / kout and copy the records
+// The cache makes the apply pass a sequential read even when the item is a gather
+// (PermItem: spans[V[i]]).
+constexpr uint32_t EM_DROP = 0xffffffffu;
+
+template <class Item>
+__global__ __launch_bounds__(EM_BLOCK) void k_emit_count(Item item, uint32_t n, uint2 *__restrict__ cache,
+                                                         uint64_t *__restrict__ tot) {
+    __shared__ uint64_t s_red[EM_BLOCK / 64];
+    const uint32_t base = blockIdx.x * EM_TILE;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        const uint32_t i = base + r * EM_BLOCK + threadIdx.x;
+        if (i < n) {
+            uint32_t s = 0, l = 0;
+            const bool f = item(i, &s, &l);
+            cache[i] = make_uint2(s, f ? l : EM_DROP);
+            sum += f ? (EM_ONE | (uint64_t)(l + 1u)) : 0ull;
+        }
+    }
+    sum = wave_sum(sum);
+    if (lane_id() == 0) s_red[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < EM_BLOCK / 64; ++w) t += s_red[w];
+        tot[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(EM_BLOCK) void k_emit_apply(const uint2 *__restrict__ cache, uint32_t n,
+                                                         const uint64_t *__restrict__ pre,
+                                                         const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                         uint2 *__restrict__ out_spans,
+                                                         const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
+                                                         int dbg) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][EM_WIN];
+    __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
+    __shared__ uint64_t s_wt[4];
+    const uint32_t tile = blockIdx.x;
+    const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t wbase = tile * EM_TILE + wid * 256u;
+    uint32_t st[EM_ROUNDS], ln[EM_ROUNDS];
+    uint64_t loc[EM_ROUNDS];
+    uint64_t run = 0;
+    uint32_t fmask = 0;
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        const uint32_t i = wbase + r * 64u + lane;
+        const uint2 cv = (i < n) ? cache[i] : make_uint2(0u, EM_DROP);
+        const bool f = cv.y != EM_DROP;
+        st[r] = cv.x;
+        ln[r] = f ? cv.y : 0u;
+        const uint64_t v = f ? (EM_ONE | (uint64_t)(cv.y + 1u)) : 0ull;
+        const uint64_t inc = wave_incl_scan(v);
+        loc[r] = run + inc - v;
+        run += __shfl(inc, 63, 64);
+        fmask |= (f ? 1u : 0u) << r;
+    }
+    if (lane == 0) s_wt[wid] = run;
+    __syncthreads();
+    uint64_t woff = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) woff += (w < wid) ? s_wt[w] : 0ull;
+    const uint64_t wpre = pre[tile] + woff;
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        const bool f = (fmask >> r) & 1u;
+        const uint64_t m = __ballot(f);
+        if (!m) continue;
+        const uint64_t gp = wpre + loc[r];
+        const uint32_t j = (uint32_t)(gp >> 32);
+        const uint64_t o = (uint32_t)gp;
+        if (f) {
+            if (out_spans) out_spans[j] = make_uint2((uint32_t)o, (uint32_t)o + ln[r]);
+            if (kout) kout[j] = kin[wbase + r * 64u + lane];
+        }
+        if (dbg & 1) continue;  // probe mode: no copy (timing only)
+        const uint32_t first = (uint32_t)(__ffsll((long long)m) - 1);
+        const uint32_t last = 63u - (uint32_t)__clzll((long long)m);
+        const uint64_t o0 = __shfl(o, (int)first, 64);
+        const uint64_t oend = __shfl(o + ln[r] + 1u, (int)last, 64);
+        const uint64_t base = o0 & ~15ull;
+        wave_copy_round(src, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, st[r], ln[r],
+                        (uint32_t)(o - base), o0, oend, base);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+}
+
+// ------------------------------------------------------------------ common items
+// Sorted position i -> input record V[i] (V null: record i).
+struct PermItem {
+    const uint32_t *V;
+    const uint2 *spans;
+    __device__ bool operator()(uint32_t i, uint32_t *s, uint32_t *l) const {
+        const uint2 sp = spans[V ? V[i] : i];
+        *s = sp.x;
+        *l = sp.y - sp.x;
+        return true;
+    }
+};
+
+// Record i by its span, kept where flag[i] == want.
+struct FlagItem {
+    const uint2 *spans;
+    const uint8_t *flag;
+    uint8_t want;
+    __device__ bool operator()(uint32_t i, uint32_t *s, uint32_t *l) const {
+        if (flag[i] != want) return false;
+        const uint2 sp = spans[i];
+        *s = sp.x;
+        *l = sp.y - sp.x;
+        return true;
+    }
+};
+
+}  // namespace sg

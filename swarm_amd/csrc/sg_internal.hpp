@@ -8,6 +8,9 @@ int pool_acquire(int device, sg_ctx **out);
 void pool_release(sg_ctx *c);
 int pick_device(int *dev);
 
+// Exclusive scan of nt per-tile u64 aggregates into pre; the sum into *total (device).
+int tile_scan(sg_ctx *c, const uint64_t *tot, uint32_t nt, uint64_t *pre, uint64_t *total);
+
 // Slot sets let the cur and prior buffers be parsed/sorted without sharing buffers.
 struct SlotSet {
     int starts, ends, keys, keys2, vals, vals2, uniq, lb;
@@ -20,9 +23,9 @@ struct Lines {
     uint2 *spans = nullptr;     // (start, end) per record, interleaved: one 8-B load per record
     uint64_t *keys = nullptr;   // chunk_key(rec, 0) (null when not requested)
     uint32_t n_rec = 0;
-    // Look-back status of the parse: tile_prefix[t] & LB_VAL_MASK is the inclusive packed
-    // (starts << 31 | ends) count through tile t of tile_bytes bytes each.
-    const uint64_t *tile_prefix = nullptr;
+    // Exclusive packed (starts << 31 | ends) record-boundary counts before tile t (tiles of
+    // tile_bytes bytes): the tile prefixes of the parse's reduce-then-scan.
+    const uint64_t *tile_excl = nullptr;
     uint32_t tile_bytes = 0, n_tiles = 0;
 };
 // Split d_buf (16-byte aligned device pointer, n bytes) into non-empty records.
@@ -34,15 +37,6 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
 int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
                uint32_t n, int begin_bit, int end_bit, bool iota_vals,
                uint64_t **keys_out, uint32_t **vals_out, const char *pass_name = "rs_pass");
-
-// Bytewise sort + uniqueness of the records of a parsed buffer.
-struct SortedSet {
-    uint64_t *keys = nullptr;  // chunk_key(rec, 0) in sorted order
-    uint32_t *recs = nullptr;  // record ids in sorted order
-    uint8_t *uniq = nullptr;   // 1 = first occurrence of its bytes
-    uint32_t n = 0;
-};
-int sort_records(sg_ctx *c, const uint8_t *d_buf, const Lines &L, const SlotSet &ss, SortedSet *out);
 
 // Compaction: indices i < n with flag[i] != 0, in order. Returns count.
 int select_flags(sg_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out_idx, uint32_t *count);

@@ -1,6 +1,6 @@
 // sg_lines.hip — A3 module-output parsing: split a line-delimited buffer in HBM into its
-// non-empty records in ONE pass (decoupled look-back), emitting per record its start,
-// its end and its 8-byte prefix key for the sort.
+// non-empty records, emitting per record its (start, end) span and its 8-byte prefix key
+// for the sort.
 //
 // Record starts and ends are purely local predicates with one byte of look-behind:
 //   start at p : byte[p] != '\n' && (p == 0 || byte[p-1] == '\n')
@@ -8,8 +8,10 @@
 //                unterminated last record: bytes >= n read as '\n')
 // so the k-th start pairs with the k-th end and empty records vanish without any
 // carried state. Each thread owns 64 contiguous bytes (four 16-B loads, coalesced per
-// wave), builds a 64-bit newline mask with SWAR, and the block scans the packed
-// (starts:31 | ends:31) counts. Algorithmic bytes: n read + 16 B written per record.
+// wave) and builds a 64-bit newline mask with SWAR. Reduce-then-scan: k_lines_count
+// reduces the packed (starts:31 | ends:31) counts per 16 KiB tile, k_tile_scan turns them
+// into tile prefixes, k_lines re-reads the tile and writes the records. Algorithmic bytes:
+// 2 n read + 16 B written per record.
 #include "sg_internal.hpp"
 
 #include <stdlib.h>
@@ -17,6 +19,9 @@
 namespace sg {
 
 constexpr int LN_BLOCK = 256;
+constexpr int LN_BPT = 64;
+constexpr int LN_TILE = LN_BLOCK * LN_BPT;
+constexpr int LN_NW = LN_BPT / 4;
 
 __device__ __forceinline__ uint32_t nl_mask4(uint32_t x) {
     uint32_t y = x ^ 0x0a0a0a0au;
@@ -24,37 +29,19 @@ __device__ __forceinline__ uint32_t nl_mask4(uint32_t x) {
     return ((r >> 7) & 1u) | ((r >> 14) & 2u) | ((r >> 21) & 4u) | ((r >> 28) & 8u);
 }
 
-// BPT bytes per thread (32 or 64): the tile is LN_BLOCK * BPT bytes. Larger tiles halve
-// the look-back chain and put more loads in flight per thread.
-template <int BPT>
-__global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ buf, uint64_t n,
-                                                    uint2 *__restrict__ spans,
-                                                    uint64_t *__restrict__ keys, uint32_t cap,
-                                                    uint64_t *status, uint32_t *counter,
-                                                    uint32_t ntiles) {
-    constexpr int TILE = LN_BLOCK * BPT;
-    constexpr int NW = BPT / 4;
-    __shared__ __attribute__((aligned(16))) uint8_t s_b[TILE + 16];
-    __shared__ uint64_t s_red[LN_BLOCK / 64];
-    __shared__ uint64_t s_prefix;
-    __shared__ uint32_t s_tile;
-    const uint32_t tile = take_ticket(counter, &s_tile);
-    const uint32_t t = threadIdx.x;
-    const uint64_t base = (uint64_t)tile * TILE;
-    const uint64_t my0 = base + (uint64_t)t * BPT;
-
-    uint32_t w[NW];
-    if (base + TILE + 8 <= n) {
+// This thread's 64 bytes (bytes >= n read as '\n') and the byte before them.
+__device__ __forceinline__ void load64(const uint8_t *__restrict__ buf, uint64_t n, uint64_t base, uint64_t my0,
+                                       uint32_t (&w)[LN_NW], uint32_t *prev) {
+    if (base + LN_TILE + 8 <= n) {
         const uint4 *p = reinterpret_cast<const uint4 *>(buf + my0);
 #pragma unroll
-        for (int j = 0; j < NW / 4; ++j) {
+        for (int j = 0; j < LN_NW / 4; ++j) {
             const uint4 a = p[j];
             w[4 * j] = a.x; w[4 * j + 1] = a.y; w[4 * j + 2] = a.z; w[4 * j + 3] = a.w;
         }
-        if (t < 8) s_b[TILE + t] = buf[base + TILE + t];
     } else {
 #pragma unroll
-        for (int j = 0; j < NW; ++j) {
+        for (int j = 0; j < LN_NW; ++j) {
             uint32_t x = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -64,66 +51,79 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
             }
             w[j] = x;
         }
-        if (t < 8) {
-            const uint64_t pos = base + TILE + t;
-            s_b[TILE + t] = (pos < n) ? buf[pos] : (uint8_t)0x0a;
-        }
     }
-#pragma unroll
-    for (int j = 0; j < NW / 4; ++j)
-        reinterpret_cast<uint4 *>(s_b)[(NW / 4) * t + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+    *prev = (my0 == 0) ? 0x0au : ((my0 - 1 < n) ? buf[my0 - 1] : 0x0au);
+}
 
+__device__ __forceinline__ void masks(const uint32_t (&w)[LN_NW], uint32_t prev, uint64_t *sm, uint64_t *em) {
     uint64_t m = 0;
 #pragma unroll
-    for (int j = 0; j < NW; ++j) m |= (uint64_t)nl_mask4(w[j]) << (4 * j);
-    __syncthreads();
-    uint64_t cin;
-    if (t > 0) cin = (s_b[t * BPT - 1] == 0x0a);
-    else cin = (base == 0) ? 1u : (buf[base - 1] == 0x0a);
-    const uint64_t prevnl = (m << 1) | cin;
-    const uint64_t sm = ~m & prevnl & (BPT == 64 ? ~0ull : 0xffffffffull);
-    const uint64_t em = m & ~prevnl;
-    const uint64_t packed = ((uint64_t)__popcll(sm) << 31) | (uint64_t)__popcll(em);
+    for (int j = 0; j < LN_NW; ++j) m |= (uint64_t)nl_mask4(w[j]) << (4 * j);
+    const uint64_t prevnl = (m << 1) | (prev == 0x0au ? 1ull : 0ull);
+    *sm = ~m & prevnl;
+    *em = m & ~prevnl;
+}
 
-    uint64_t total;
-    const uint64_t excl = block_excl_scan<LN_BLOCK>(packed, &total, s_red);
-    if (t < 64) {
-        uint64_t prefix = 0;
-        if (tile == 0) {
-            if (t == 0) lb_store(status, LB_FLAG_INC, total);
-        } else {
-            if (t == 0) lb_store(status + tile, LB_FLAG_AGG, total);
-            prefix = wave_lookback(status, tile);
-            if (t == 0) lb_store(status + tile, LB_FLAG_INC, prefix + total);
-        }
-        if (t == 0) {
-            s_prefix = prefix;
-            if (tile == ntiles - 1) counter[1] = (uint32_t)((prefix + total) >> 31);
+__global__ __launch_bounds__(LN_BLOCK) void k_lines_count(const uint8_t *__restrict__ buf, uint64_t n,
+                                                          uint64_t *__restrict__ tot) {
+    __shared__ uint64_t s_red[LN_BLOCK / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * LN_TILE;
+    const uint64_t my0 = base + (uint64_t)threadIdx.x * LN_BPT;
+    uint32_t w[LN_NW], prev;
+    load64(buf, n, base, my0, w, &prev);
+    uint64_t sm, em;
+    masks(w, prev, &sm, &em);
+    uint64_t v = ((uint64_t)__popcll(sm) << 31) | (uint64_t)__popcll(em);
+    v = wave_sum(v);
+    if (lane_id() == 0) s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) tot[blockIdx.x] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+}
+
+__global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ buf, uint64_t n,
+                                                    const uint64_t *__restrict__ pre, uint2 *__restrict__ spans,
+                                                    uint64_t *__restrict__ keys) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_b[LN_TILE + 16];
+    __shared__ uint64_t s_red[LN_BLOCK / 64];
+    const uint32_t t = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * LN_TILE;
+    const uint64_t my0 = base + (uint64_t)t * LN_BPT;
+    uint32_t w[LN_NW], prev;
+    load64(buf, n, base, my0, w, &prev);
+    if (keys) {
+#pragma unroll
+        for (int j = 0; j < LN_NW / 4; ++j)
+            reinterpret_cast<uint4 *>(s_b)[(LN_NW / 4) * t + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+        if (t < 8) {
+            const uint64_t pos = base + LN_TILE + t;
+            s_b[LN_TILE + t] = (pos < n) ? buf[pos] : (uint8_t)0x0a;
         }
     }
-    __syncthreads();
-    const uint64_t pre = s_prefix + excl;
-    uint32_t si = (uint32_t)(pre >> 31);
-    uint32_t ei = (uint32_t)(pre & 0x7fffffffu);
+    uint64_t sm, em;
+    masks(w, prev, &sm, &em);
+    const uint64_t packed = ((uint64_t)__popcll(sm) << 31) | (uint64_t)__popcll(em);
+    uint64_t total;
+    const uint64_t excl = block_excl_scan<LN_BLOCK>(packed, &total, s_red);  // includes barriers
+    const uint64_t p0 = pre[blockIdx.x] + excl;
+    uint32_t si = (uint32_t)(p0 >> 31);
+    uint32_t ei = (uint32_t)(p0 & 0x7fffffffu);
 
     uint64_t bits = sm;
     while (bits) {
         const int b = __ffsll((long long)bits) - 1;
         bits &= bits - 1;
-        if (si < cap) {
-            spans[si].x = (uint32_t)(my0 + b);
-            if (keys) {
-                const int q = t * BPT + b;
-                uint32_t rem = 8;
-                uint64_t k = 0;
+        spans[si].x = (uint32_t)(my0 + b);
+        if (keys) {
+            const int q = t * LN_BPT + b;
+            uint32_t rem = 8;
+            uint64_t k = 0;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint32_t c = s_b[q + j];
-                    if (c == 0x0a && rem == 8) rem = j;
-                    if (j < 7 && (uint32_t)j < rem) k |= (uint64_t)c << (56 - 8 * j);
-                }
-                keys[si] = k | rem;
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t c = s_b[q + j];
+                if (c == 0x0a && rem == 8) rem = j;
+                if (j < 7 && (uint32_t)j < rem) k |= (uint64_t)c << (56 - 8 * j);
             }
+            keys[si] = k | rem;
         }
         ++si;
     }
@@ -131,54 +131,36 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
     while (bits) {
         const int b = __ffsll((long long)bits) - 1;
         bits &= bits - 1;
-        if (ei < cap) spans[ei].y = (uint32_t)(my0 + b);
+        spans[ei].y = (uint32_t)(my0 + b);
         ++ei;
     }
-}
-
-static int lines_bpt() {
-    static int v = [] {
-        const char *e = getenv("SG_LINES_BPT");
-        return (e && atoi(e) == 32) ? 32 : 64;
-    }();
-    return v;
 }
 
 int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys) {
     if (n > MAX_BYTES) { set_error("buffer of %llu bytes exceeds the 4 GiB per-call limit", (unsigned long long)n); return SG_E_TOO_LARGE; }
     if (((uintptr_t)d_buf & 15) != 0) { set_error("run_lines: device buffer not 16-byte aligned"); return SG_E_INVAL; }
-    const int bpt = lines_bpt();
-    const uint32_t tile_bytes = LN_BLOCK * bpt;
-    const uint32_t ntiles = (uint32_t)(n / tile_bytes + 1);
-    uint64_t *status;
-    SG_TRY(slot(c, ss.lb, (size_t)ntiles + 2, &status));
-    uint32_t *counter = reinterpret_cast<uint32_t *>(status + ntiles);
-    uint64_t want = n / 16 + 4096;
-    if (c->slot_cap[ss.starts] / 8 > want) want = c->slot_cap[ss.starts] / 8 - 64;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        uint32_t cap = (uint32_t)want;
-        SG_TRY(slot(c, ss.starts, cap, &out->spans));
-        out->keys = nullptr;
-        if (want_keys) SG_TRY(slot(c, ss.keys, cap, &out->keys));
-        SG_HIP(hipMemsetAsync(status, 0, ((size_t)ntiles + 2) * 8, c->stream));
-        if (bpt == 32)
-            SG_LAUNCH(c, "lines", k_lines<32>, ntiles, LN_BLOCK, 0, d_buf, n, out->spans, out->keys, cap, status,
-                      counter, ntiles);
-        else
-            SG_LAUNCH(c, "lines", k_lines<64>, ntiles, LN_BLOCK, 0, d_buf, n, out->spans, out->keys, cap, status,
-                      counter, ntiles);
-        uint32_t R = 0;
-        SG_TRY(ctx_readback(c, &R, counter + 1, 4));
-        out->n_rec = R;
-        out->tile_prefix = status;
-        out->tile_bytes = tile_bytes;
-        out->n_tiles = ntiles;
-        prof_bytes(c, "lines", (double)n + (want_keys ? 16.0 : 8.0) * R);  // text read once + (start, end[, key0])
-        if (R <= cap) return SG_OK;
-        want = (uint64_t)R + 4096;
-    }
-    set_error("run_lines: capacity retry failed");
-    return SG_E_NOMEM;
+    const uint32_t ntiles = (uint32_t)(n / LN_TILE + 1);
+    uint64_t *tp;  // tot[ntiles] | pre[ntiles] | total
+    SG_TRY(slot(c, ss.lb, 2 * (size_t)ntiles + 4, &tp));
+    uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
+    SG_LAUNCH(c, "lines.count", k_lines_count, ntiles, LN_BLOCK, 0, d_buf, n, tot);
+    SG_TRY(tile_scan(c, tot, ntiles, pre, total));
+    uint64_t tv = 0;
+    SG_TRY(ctx_readback(c, &tv, total, 8));
+    const uint32_t R = (uint32_t)(tv >> 31);
+    if (R != (uint32_t)(tv & 0x7fffffffu)) { set_error("run_lines: start/end count mismatch"); return SG_E_HIP; }
+    SG_TRY(slot(c, ss.starts, (size_t)R + 1, &out->spans));
+    out->keys = nullptr;
+    if (want_keys) SG_TRY(slot(c, ss.keys, (size_t)R + 1, &out->keys));
+    SG_LAUNCH(c, "lines", k_lines, ntiles, LN_BLOCK, 0, d_buf, n, pre, out->spans, out->keys);
+    out->n_rec = R;
+    out->tile_excl = pre;
+    out->tile_bytes = LN_TILE;
+    out->n_tiles = ntiles;
+    // text read twice (count + apply) + (start, end[, key0]) per record
+    prof_bytes(c, "lines", (double)n + (want_keys ? 16.0 : 8.0) * R);
+    prof_bytes(c, "lines.count", (double)n);
+    return SG_OK;
 }
 
 }  // namespace sg

@@ -14,7 +14,7 @@
 // radix-sorted and de-duplicated, so hits come out sorted by (record, signature) and the
 // matched lines in input order (grep's output).
 #include "sg_internal.hpp"
-#include "sg_prims.hpp"
+#include "sg_prims_host.hpp"
 
 #include <algorithm>
 #include <deque>
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
 struct LitArgs {
     const uint8_t *buf;
     uint64_t n;
-    const uint64_t *tile_prefix;  // the parse's look-back status (inclusive packed counts per tile)
+    const uint64_t *tile_excl;    // the parse's exclusive packed (starts << 31 | ends) prefix per tile
     uint32_t n_tiles;
     const uint32_t *bitmap, *eoff, *efp;
     const uint16_t *rank;
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
 #pragma unroll
         for (int j = 0; j < NW / 4; ++j)
             reinterpret_cast<uint4 *>(s_tile)[(NW / 4) * t + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
-        if (t == 0) s_base = tile ? (uint32_t)((a.tile_prefix[tile - 1] & LB_VAL_MASK) >> 31) : 0u;
+        if (t == 0) s_base = (uint32_t)(a.tile_excl[tile] >> 31);
         uint64_t m = 0;
 #pragma unroll
         for (int j = 0; j < NW; ++j) {
@@ -1003,18 +1003,7 @@ __global__ void k_rec_of(const unsigned long long *K, const uint32_t *idx, uint3
 
 template <class Pred>
 static int select_one(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint32_t *out, uint32_t *count) {
-    *count = 0;
-    if (n == 0) return SG_OK;
-    const uint32_t ntiles = (n + SEL_TILE - 1) / SEL_TILE;
-    uint64_t *status;
-    SG_TRY(slot(c, S_COUNT, (size_t)ntiles + 4, &status));
-    uint32_t *counter = reinterpret_cast<uint32_t *>(status + ntiles);
-    SG_HIP(hipMemsetAsync(status, 0, ((size_t)ntiles + 4) * 8, c->stream));
-    SG_LAUNCH(c, name, k_select2<Pred>, ntiles, SEL_BLOCK, 0, pred, n, out, (uint32_t *)nullptr, status, counter, ntiles);
-    uint32_t cnt[2];
-    SG_TRY(ctx_readback(c, cnt, counter, 8));
-    *count = cnt[1];
-    return SG_OK;
+    return run_select2(c, name, pred, n, out, (uint32_t *)nullptr, count, nullptr);
 }
 
 static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res) {
@@ -1046,7 +1035,7 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
     auto run_lit = [&](const char *name, const sg_matcher::Lit &Lt, unsigned long long *out, uint32_t *counter,
                        uint32_t ocap, const uint32_t *fo, const uint32_t *fp) -> int {
         LitArgs a{};
-        a.buf = d_buf; a.n = n; a.tile_prefix = L.tile_prefix; a.n_tiles = L.n_tiles;
+        a.buf = d_buf; a.n = n; a.tile_excl = L.tile_excl; a.n_tiles = L.n_tiles;
         a.bitmap = Lt.d_bitmap; a.rank = Lt.d_rank; a.eoff = Lt.d_eoff; a.efp = Lt.d_efp;
         a.brec = reinterpret_cast<const uint4 *>(Lt.d_brec);
         a.einfo = reinterpret_cast<const uint4 *>(Lt.d_einfo); a.pat16 = reinterpret_cast<const uint4 *>(Lt.d_pat16);

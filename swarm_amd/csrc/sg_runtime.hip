@@ -2,6 +2,7 @@
 // and the per-device context pool behind the re-entrant host-buffer API.
 #include "sg_common.hpp"
 #include "sg_internal.hpp"
+#include "sg_prims.hpp"
 
 #include <string.h>
 
@@ -238,3 +239,69 @@ int sg_ctx_reset_stats(sg_ctx *c) {
 }
 
 }  // extern "C"
+
+namespace sg {
+
+__global__ __launch_bounds__(TS_BLOCK) void k_tile_scan(const uint64_t *__restrict__ tot, uint32_t nt,
+                                                        uint64_t *__restrict__ pre, uint64_t *__restrict__ total) {
+    __shared__ uint64_t s_red[TS_BLOCK / 64];
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < nt; base += TS_BLOCK * TS_ITEMS) {
+        const uint32_t i0 = base + threadIdx.x * TS_ITEMS;
+        uint64_t v[TS_ITEMS];
+        uint64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < TS_ITEMS; ++j) {
+            v[j] = (i0 + j < nt) ? tot[i0 + j] : 0ull;
+            sum += v[j];
+        }
+        uint64_t btot;
+        const uint64_t ex = block_excl_scan<TS_BLOCK>(sum, &btot, s_red);
+        uint64_t run = carry + ex;
+#pragma unroll
+        for (int j = 0; j < TS_ITEMS; ++j) {
+            if (i0 + j < nt) pre[i0 + j] = run;
+            run += v[j];
+        }
+        carry += btot;
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+int tile_scan(sg_ctx *c, const uint64_t *tot, uint32_t nt, uint64_t *pre, uint64_t *total) {
+    SG_LAUNCH(c, "tile_scan", k_tile_scan, 1, TS_BLOCK, 0, tot, nt, pre, total);
+    return SG_OK;
+}
+
+__global__ __launch_bounds__(SEL_BLOCK) void k_sel_apply(uint32_t n, const uint64_t *__restrict__ mA,
+                                                         const uint64_t *__restrict__ mB,
+                                                         const uint64_t *__restrict__ pre, uint32_t *__restrict__ outA,
+                                                         uint32_t *__restrict__ outB) {
+    __shared__ uint32_t s_ca[SEL_MASKS], s_cb[SEL_MASKS];
+    const int t = threadIdx.x, lane = lane_id(), wid = t >> 6;
+    const uint32_t base = blockIdx.x * SEL_TILE;
+    const uint64_t *ma = mA + (uint64_t)blockIdx.x * SEL_MASKS;
+    const uint64_t *mb = mB + (uint64_t)blockIdx.x * SEL_MASKS;
+    if (t < 64) {
+        const uint32_t a = (uint32_t)__popcll(ma[t]), b = (uint32_t)__popcll(mb[t]);
+        const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+        s_ca[t] = ia - a;
+        s_cb[t] = ib - b;
+    }
+    __syncthreads();
+    const uint64_t p0 = pre[blockIdx.x];
+    const uint32_t preA = (uint32_t)(p0 >> 31), preB = (uint32_t)(p0 & 0x7fffffffu);
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < SEL_ROWS; ++j) {
+        const uint32_t i = base + j * SEL_BLOCK + t;
+        const uint64_t xa = ma[j * 4 + wid];
+        if ((xa >> lane) & 1ull) outA[preA + s_ca[j * 4 + wid] + (uint32_t)__popcll(xa & lt)] = i;
+        if (outB) {
+            const uint64_t xb = mb[j * 4 + wid];
+            if ((xb >> lane) & 1ull) outB[preB + s_cb[j * 4 + wid] + (uint32_t)__popcll(xb & lt)] = i;
+        }
+    }
+}
+
+}  // namespace sg

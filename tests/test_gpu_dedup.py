@@ -205,3 +205,37 @@ def test_partition_matches_hash_oracle(sg, parts):
     assert pbytes == [sum(len(r) + 1 for r in e) for e in exp]
     assert out == b"".join(r + b"\n" for e in exp for r in e)
     ctx.close()
+
+
+@pytest.mark.parametrize("k", [2, 3, 63, 64, 65, 66, 129, 200])
+def test_dedup_segment_sizes(sg, k):
+    """Segments of k distinct records sharing their first 7+ bytes: <= 64 are sorted by one
+    wave in LDS (run sort), > 64 go through the radix refinement rounds first."""
+    rng = random.Random(k)
+    recs = [b"shared_" + bytes(rng.choice(b"xyz\x00\xff") for _ in range(rng.randint(0, 6))) for _ in range(k)]
+    recs += rng.sample(recs, min(len(recs), 10))  # duplicates inside the segment
+    recs += [b"other%d" % i for i in range(50)]
+    rng.shuffle(recs)
+    b = b"\n".join(recs) + b"\n"
+    assert sg.dedup(b) == S.dedup(b)
+
+
+def test_dedup_long_records_segment_mirror(sg):
+    """A segment whose bytes exceed the per-wave LDS window (global mirror path)."""
+    rng = random.Random(77)
+    recs = [b"samepre" + bytes(rng.choice(b"ab") for _ in range(rng.randint(200, 700))) for _ in range(40)]
+    recs += recs[:5]
+    rng.shuffle(recs)
+    b = b"\n".join(recs) + b"\n"
+    assert sg.dedup(b) == S.dedup(b)
+
+
+def test_dedup_unsorted_prior_long(sg):
+    """An unsorted prior goes through the full sort/unique pipeline before the diff."""
+    rng = random.Random(8)
+    pool = [b"host%05d.example.com" % i for i in range(3000)]
+    cur = b"\n".join(rng.choice(pool) for _ in range(5000)) + b"\n"
+    prior = b"\n".join(rng.choice(pool) for _ in range(4000)) + b"\n"
+    u, f = sg.dedup_diff(cur, prior)
+    eu, ef = S.dedup_diff(cur, prior)
+    assert u == eu and f == ef
