@@ -27,22 +27,47 @@ HBM_COPY_GBS = 6290.0      # measured float4 copy (same guide)
 METRIC = "scan records/sec + GB/s (vs HBM roofline) for match+dedup+diff, 1 and 8 GPUs"
 
 
-def roofline_of(stats, kernel=None):
-    """Dominant kernel (most device time) and its achieved GB/s: the algorithmic bytes the
-    library credited to its launches (SURVEY.md §8(d) model) over the
-    HIP-event time of the same launches, recorded on the launch stream."""
+# library stat name -> HIP kernel symbol (rocprofv3 -T names) for the PMC traffic lookup
+KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_uniq": "k_emit_uniq",
+                 "emit_fresh": "k_emit_fresh", "diff_tile": "k_diff_tile", "adjacent": "k_adjacent",
+                 "lines": "k_lines", "lit_match": "k_lit_scan", "dfa_match": "k_dfa_match", "ac_match": "k_ac_match"}
+
+
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE
+    passes (profiles/pmc_traffic.json, written by tools/pmc_summary.py; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md). None when no pass covers this kernel."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        t = json.load(open(path))[workload][KERNEL_SYMBOL.get(kernel, kernel)]
+    except (OSError, KeyError, ValueError):
+        return None
+    return t
+
+
+def roofline_of(stats, kernel=None, workload=None):
+    """The dominant kernel and its achieved GB/s: the algorithmic bytes the library credited
+    to its launches (SURVEY.md §8(d) model) over the HIP-event time of the
+    same launches, recorded on the launch stream inside the timed region."""
     if not stats:
         return None
     if kernel is None:
         kernel = max(stats.items(), key=lambda kv: kv[1][1])[0]
+    if kernel not in stats:
+        return None
     launches, ms, by = stats[kernel]
     if not launches or ms <= 0:
         return None
     ach = by / (ms * 1e-3) / 1e9
-    return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-            "bytes_per_launch": int(by / launches), "avg_launch_us": round(ms / launches * 1e3, 2),
-            "frac_of_measured_copy_bw": round(ach / HBM_COPY_GBS, 4)}
+    out = {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+           "bytes_per_launch": int(by / launches), "avg_launch_us": round(ms / launches * 1e3, 2),
+           "frac_of_measured_copy_bw": round(ach / HBM_COPY_GBS, 4)}
+    t = pmc_traffic(workload, kernel) if workload else None
+    if t:
+        out["traffic"] = t["bytes"]
+        out["traffic_source"] = "profiles/" + t["source"] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+    return out
 
 
 def kernel_table(stats):
@@ -52,6 +77,38 @@ def kernel_table(stats):
         if by and ms:
             out[k]["gbps"] = round(by / (ms * 1e-3) / 1e9, 1)
     return out
+
+
+def timed_steps(ctx, run, args, barrier=None):
+    """W warmup steps; one fully profiled untimed step (per-kernel table, dominant kernel);
+    then K timed steps with HIP events only around the dominant kernel's launches.
+    Returns (elapsed_s, full_stats, timed_stats, dominant, last_result)."""
+    import torch
+    r = None
+    for _ in range(args.warmup):
+        r = run()
+    torch.cuda.synchronize()
+    ctx.reset_stats()
+    ctx.profile(True)
+    r = run()
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    full = ctx.kernel_stats()
+    dominant = max(full.items(), key=lambda kv: kv[1][1])[0] if full else None
+    ctx.reset_stats()
+    ctx.profile(True, only=dominant)
+    if barrier:
+        barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = run()
+    torch.cuda.synchronize()
+    if barrier:
+        barrier()
+    el = time.perf_counter() - t0
+    ctx.profile(False)
+    return el, full, ctx.kernel_stats(), dominant, r
 
 
 def bench_c3(args):
@@ -76,18 +133,8 @@ def bench_c3(args):
     d = torch.from_numpy(buf).cuda()
     ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
     m = swarm_amd.Matcher(sigs, "literal")
-    for _ in range(args.warmup):
-        r = m.dev_match(ctx, d.data_ptr(), d.numel())
-    torch.cuda.synchronize()
-    ctx.reset_stats()
-    ctx.profile(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        r = m.dev_match(ctx, d.data_ptr(), d.numel())
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    ctx.profile(False)
-    stats = ctx.kernel_stats()
+    run = lambda: m.dev_match(ctx, d.data_ptr(), d.numel())  # noqa: E731
+    el, full, stats, dominant, r = timed_steps(ctx, run, args)
     R = int(r.in_records)
     cpu = None
     if not args.no_cpu_baseline:
@@ -109,13 +156,15 @@ def bench_c3(args):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (httpx-style lines, 1 % planted signatures, SURVEY.md §8(d) C3)",
         "config": {"workload": "C3: %dM httpx lines x 2000 literal signatures, 1 GPU" % (n_lines // 1_000_000),
-                   "engine": "lit_match" if "lit_match" in stats else "ac_match",
+                   "engine": "lit_match" if "lit_match" in full else "ac_match",
                    "bytes": int(d.numel()), "automaton_states": m.info()["states"]},
         "gbps": round(d.numel() * args.steps / el / 1e9, 2),
         "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records)},
-        "roofline": roofline_of(stats, "lit_match" if "lit_match" in stats else "ac_match"),
+        "roofline": roofline_of(stats, dominant, "c3"),
         "cpu_baseline": cpu,
-        "kernels": kernel_table(stats),
+        "kernels": kernel_table(full),
+        "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
+                        "HIP events only around the dominant kernel",
     }), flush=True)
     ctx.close()
 
@@ -182,8 +231,22 @@ def main():
         r, nrecv = step()
     torch.cuda.synchronize()
 
+    # one fully profiled step (untimed): per-kernel breakdown, and the dominant kernel
     ctx.reset_stats()
     ctx.profile(True)
+    step()
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    full = ctx.kernel_stats()
+    dominant = max(full.items(), key=lambda kv: kv[1][1])[0] if full else None
+    if world > 1:
+        names = [None] * world
+        dist.all_gather_object(names, dominant)
+        dominant = names[0]
+
+    # timed region: HIP events only around the dominant kernel's launches (on its stream)
+    ctx.reset_stats()
+    ctx.profile(True, only=dominant)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -211,9 +274,9 @@ def main():
     info = {"R": int(r.in_records), "n": int(nrecv), "Rp": int(r.prior_records), "n_prior": int(prior.numel()),
             "U": int(r.uniq_records), "ub": int(r.uniq_bytes), "F": int(r.fresh_records), "fb": int(r.fresh_bytes)}
 
-    roofline = roofline_of(stats)
-    kernels = kernel_table(stats)
-    gpu_ms_sum = sum(v[1] for v in stats.values()) / args.steps
+    roofline = roofline_of(stats, dominant, "c2")
+    kernels = kernel_table(full)
+    gpu_ms_sum = sum(v[1] for v in full.values())
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -255,6 +318,8 @@ def main():
             "cpu_baseline": cpu,
             "gpu_kernel_ms_per_step": round(gpu_ms_sum, 4),
             "kernels": kernels,
+            "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
+                            "HIP events only around the dominant kernel",
         }
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -61,6 +61,8 @@ int sg_ctx_destroy(sg_ctx *ctx);
 int sg_ctx_sync(sg_ctx *ctx);
 /* Per-kernel HIP-event timing, recorded on the context's stream while enabled. */
 int sg_ctx_profile(sg_ctx *ctx, int enable);
+/* Restrict event timing to launches named `name` (NULL or "": all launches). */
+int sg_ctx_profile_only(sg_ctx *ctx, const char *name);
 /* Kernel stats by index: name (static string), launches, total device ms and the total
  * algorithmic bytes those launches moved (0 where not modelled). Returns SG_E_INVAL past
  * the last index. */

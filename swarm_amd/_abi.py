@@ -24,7 +24,7 @@ ERRNAMES = {1: "SG_E_INVAL", 2: "SG_E_CAP", 3: "SG_E_HIP", 4: "SG_E_NOMEM", 5: "
 
 EXPORTS = [
     "sg_last_error", "sg_version", "sg_device_count", "sg_ctx_create", "sg_ctx_destroy",
-    "sg_ctx_sync", "sg_ctx_profile", "sg_ctx_kernel_stat", "sg_ctx_reset_stats", "sg_ctx_memcpy",
+    "sg_ctx_sync", "sg_ctx_profile", "sg_ctx_profile_only", "sg_ctx_kernel_stat", "sg_ctx_reset_stats", "sg_ctx_memcpy",
     "sg_lines",
     "sg_dedup", "sg_dedup_chunks", "sg_diff", "sg_dedup_diff", "sg_dev_dedup_diff",
     "sg_dev_partition", "sg_hash64", "sg_ac_compile", "sg_dfa_compile", "sg_matcher_info",
@@ -73,6 +73,7 @@ def _load():
         "sg_ctx_destroy": (C.c_int, [P]),
         "sg_ctx_sync": (C.c_int, [P]),
         "sg_ctx_profile": (C.c_int, [P, C.c_int]),
+        "sg_ctx_profile_only": (C.c_int, [P, C.c_char_p]),
         "sg_ctx_kernel_stat": (C.c_int, [P, C.c_int, C.POINTER(C.c_char_p), U64P, C.POINTER(C.c_double),
                                          C.POINTER(C.c_double)]),
         "sg_ctx_reset_stats": (C.c_int, [P]),

@@ -197,7 +197,9 @@ class Context:
     def sync(self):
         check(lib.sg_ctx_sync(self._h))
 
-    def profile(self, on: bool = True):
+    def profile(self, on: bool = True, only: str = None):
+        """HIP-event timing of every launch on the context stream (only: one kernel name)."""
+        check(lib.sg_ctx_profile_only(self._h, (only or "").encode()))
         check(lib.sg_ctx_profile(self._h, 1 if on else 0))
 
     def reset_stats(self):

@@ -59,7 +59,7 @@ enum Slot : int {
     S_IN, S_IN2, S_CUR_UR, S_CUR_UK, S_RS_STATUS,
     // sorted materialisation (shared temporaries) and per-view outputs
     S_SBUF, S_SSPANS, S_DUP, S_BAD, S_BRK, S_MIRROR, S_EMIT, S_EMIT2, S_EMIT3, S_ERR,
-    S_U_SPANS, S_U_KEYS, S_P_UBUF, S_P_USPANS, S_P_UKEYS, S_FRESHF, S_ECACHE, S_TILES,
+    S_U_SPANS, S_U_KEYS, S_P_UBUF, S_P_USPANS, S_P_UKEYS, S_FRESHF, S_ECACHE, S_TILES, S_RS_TCNT, S_RS_DIGITS,
     S_NSLOTS
 };
 
@@ -82,6 +82,7 @@ struct sg_ctx {
     void *pinned = nullptr;   // host pinned staging for small readbacks
     // profiling
     bool profile = false;
+    std::string prof_only;  // non-empty: time only launches with this name
     std::vector<sg::KStat> stats;
     struct Pending { int stat; hipEvent_t a, b; };
     std::vector<Pending> pending;
@@ -102,6 +103,7 @@ int ctx_readback(sg_ctx *c, void *host, const void *dev, size_t bytes);  // sync
 int ctx_harvest(sg_ctx *c);
 int prof_begin(sg_ctx *c, const char *name, int *stat, hipEvent_t *a);
 void prof_end(sg_ctx *c, int stat, hipEvent_t a);
+inline bool prof_wanted(sg_ctx *c, const char *name) { return c->prof_only.empty() || c->prof_only == name; }
 // Credit algorithmic bytes to the named kernel (no-op unless profiling).
 void prof_bytes(sg_ctx *c, const char *name, double bytes);
 
@@ -110,7 +112,8 @@ void prof_bytes(sg_ctx *c, const char *name, double bytes);
     do {                                                                              \
         int st_ = -1;                                                                 \
         hipEvent_t ea_ = nullptr;                                                     \
-        if ((ctx)->profile) ::sg::prof_begin((ctx), (name), &st_, &ea_);              \
+        if ((ctx)->profile && ::sg::prof_wanted((ctx), (name)))                        \
+            ::sg::prof_begin((ctx), (name), &st_, &ea_);                              \
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), (lds), (ctx)->stream,     \
                            __VA_ARGS__);                                              \
         hipError_t le_ = hipGetLastError();                                           \

@@ -36,8 +36,11 @@ constexpr uint32_t WAVE_GROUP = 64;
 // Queue one emit (no host sync): count pass, tile scan, apply pass. *total_out: device u64,
 // (records << 32 | bytes). `bytes_model`: algorithmic bytes credited to the apply launch
 // (DESIGN.md §4).
+typedef void (*EmitApplyFn)(const uint2 *, uint32_t, const uint64_t *, const uint8_t *, uint8_t *, uint2 *,
+                            const uint64_t *, uint64_t *, int);
+
 template <class Item>
-static int run_emit(sg_ctx *c, const char *name, const char *cname, int status_slot, Item item, uint32_t n,
+static int run_emit(sg_ctx *c, EmitApplyFn kern, const char *name, const char *cname, int status_slot, Item item, uint32_t n,
                     const uint8_t *src, uint8_t *dst, uint2 *out_spans, const uint64_t *kin, uint64_t *kout,
                     uint64_t **total_out, double bytes_model) {
     const uint32_t ntiles = (n + EM_TILE - 1) / EM_TILE;
@@ -54,7 +57,7 @@ static int run_emit(sg_ctx *c, const char *name, const char *cname, int status_s
     static const int dbg = getenv("SG_EMIT_DEBUG") ? atoi(getenv("SG_EMIT_DEBUG")) : 0;
     SG_LAUNCH(c, cname, k_emit_count<Item>, ntiles, EM_BLOCK, 0, item, n, cache, tot);
     SG_TRY(tile_scan(c, tot, ntiles, pre, total));
-    SG_LAUNCH_B(c, name, bytes_model, k_emit_apply, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin,
+    SG_LAUNCH_B(c, name, bytes_model, kern, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin,
                 kout, dbg & 1);
     return SG_OK;
 }
@@ -202,12 +205,14 @@ __device__ __forceinline__ int rec_cmp8(const uint8_t *buf, uint32_t sa, uint32_
 }
 
 // dup[i] = record i equals record i-1 inside its segment (tag < 8 key0: whole record).
+// A position whose bytes differ from its predecessor's inside a segment marks the segment
+// bad at its head (walk back to the brk, <= 64 positions): segbad[head] = 1.
 __global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S, const uint2 *__restrict__ SS,
                                                   const uint64_t *__restrict__ K, const uint8_t *__restrict__ brk,
-                                                  uint32_t n, uint8_t *__restrict__ dup, uint8_t *__restrict__ bad) {
+                                                  uint32_t n, uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    bool d = false, b = false;
+    bool d = false;
     if (i > 0 && !brk[i]) {
         if ((K[i] & 0xffu) < 8u) {
             d = true;
@@ -215,55 +220,60 @@ __global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S,
             const uint2 x = SS[i - 1], y = SS[i];
             d = rec_equal(S, x.x, x.y, S, y.x, y.y, 7);
         }
-        b = !d;
+        if (!d) {
+            uint32_t h = i - 1;
+            while (h > 0 && !brk[h]) --h;
+            segbad[h] = 1;
+        }
     }
     dup[i] = d ? 1 : 0;
-    bad[i] = b ? 1 : 0;
 }
 
-// Segment heads whose segment holds a bad position: A = up to SEG_SMALL members, B = more.
+// Heads of bad segments: A = up to SEG_SMALL members, B = more (<= 64).
 struct SegPred {
-    const uint8_t *brk, *bad;
+    const uint8_t *brk, *segbad;
     uint32_t n;
     __device__ uint32_t operator()(uint32_t i) const {
-        if (!brk[i] || i + 1 >= n || brk[i + 1]) return 0u;
-        bool anyb = false;
+        if (!segbad[i]) return 0u;
         uint32_t j = i + 1;
-        for (; j < n && j <= i + 64u && !brk[j]; ++j) anyb |= bad[j] != 0;
-        if (!anyb) return 0u;
+        while (j < n && j <= i + SEG_SMALL && !brk[j]) ++j;
         return (j - i <= SEG_SMALL) ? 1u : 2u;
     }
 };
 
-__device__ __forceinline__ uint32_t seg_len(const uint8_t *brk, uint32_t a, uint32_t n, uint32_t cap) {
-    uint32_t j = a + 1;
-    while (j < n && j < a + cap && !brk[j]) ++j;
-    return j - a;
+// Ranking inside a segment. Members share their first 7 bytes, so they are ordered by the
+// 7-byte chunk keys at offsets 7, 14, 21, 28 (chunk_key: big-endian bytes + tag, tag < 8
+// ends the record) held in registers, and by a byte compare from offset 35 only when all
+// four chunks tie with tag 8. dup = an equal member with a smaller index exists.
+constexpr int SEG_CH = 4;
+
+struct SegKeys {
+    uint64_t c[SEG_CH];
+};
+
+__device__ __forceinline__ SegKeys seg_keys(const uint8_t *S, uint2 x) {
+    SegKeys k;
+#pragma unroll
+    for (int q = 0; q < SEG_CH; ++q) k.c[q] = chunk_key(S, x.x, x.y, 7u + 7u * q);
+    return k;
 }
 
-// 16 lanes per small segment (<= SEG_SMALL members), lane per member. The segment's
-// bytes are contiguous in S: staged into the group's LDS window with 16-byte loads, then
-// every lane ranks its record against the others from LDS (stable; dup = an equal member
-// precedes it). Segments wider than the window compare from S directly.
-constexpr uint32_t SEG_WIN = 1024;
-
-__device__ __forceinline__ int win_cmp(const uint8_t *w, uint32_t sa, uint32_t la, uint32_t sb, uint32_t lb,
-                                       uint32_t off) {
-    const uint32_t m = la < lb ? la : lb;
-    for (uint32_t i = off; i < m; ++i) {
-        const uint32_t x = w[sa + i], y = w[sb + i];
-        if (x != y) return (int)x - (int)y;
+// <0, 0, >0 for record a vs record b (spans xa, xb) given their chunk keys.
+__device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2 xa, const SegKeys &b, uint2 xb) {
+#pragma unroll
+    for (int q = 0; q < SEG_CH; ++q) {
+        if (a.c[q] != b.c[q]) return a.c[q] < b.c[q] ? -1 : 1;
+        if ((a.c[q] & 0xffu) < 8u) return 0;
     }
-    return la < lb ? -1 : (la > lb ? 1 : 0);
+    return rec_cmp8(S, xa.x, xa.y - xa.x, xb.x, xb.y - xb.x, 7u + 7u * SEG_CH);
 }
 
+// 16 lanes per small segment (<= SEG_SMALL members), lane per member.
 __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                    const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
                                                    const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_w[16][SEG_WIN];
     const uint32_t lane = lane_id(), gl = lane & 15u, gbase = lane & ~15u;
-    const uint32_t grp = threadIdx.x >> 4;
-    const uint32_t q = blockIdx.x * 16u + grp;
+    const uint32_t q = blockIdx.x * 16u + (threadIdx.x >> 4);
     const bool live = q < nh;
     const uint32_t a = live ? heads[q] : 0u;
     const uint32_t pe = a + 1u + gl;
@@ -272,25 +282,17 @@ __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S
     const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);  // members: a .. a+k-1
     const bool act = live && gl < k;
     const uint2 x = act ? SS[a + gl] : make_uint2(0u, 0u);
-    const uint32_t len = x.y - x.x;
-    const uint32_t r0 = (uint32_t)__shfl(x.x, (int)gbase, 64);
-    const uint32_t r1 = (uint32_t)__shfl(x.y, (int)(gbase + k - 1u), 64) + 1u;
-    const uint32_t base = r0 & ~15u;
-    const bool in_lds = live && (r1 - base <= SEG_WIN);
-    uint8_t *w = s_w[grp];
-    if (in_lds)
-        for (uint32_t o = base + 16u * gl; o < r1; o += 256u)
-            *reinterpret_cast<uint4 *>(w + (o - base)) = *reinterpret_cast<const uint4 *>(S + o);
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const SegKeys mk = act ? seg_keys(S, x) : SegKeys{{0, 0, 0, 0}};
     uint32_t rank = 0;
     bool d = false;
     for (uint32_t j = 0; j < k; ++j) {
-        const uint32_t ys = (uint32_t)__shfl(x.x, (int)(gbase + j), 64);
-        const uint32_t ye = (uint32_t)__shfl(x.y, (int)(gbase + j), 64);
+        const int src = (int)(gbase + j);
+        SegKeys ok;
+#pragma unroll
+        for (int c = 0; c < SEG_CH; ++c) ok.c[c] = __shfl(mk.c[c], src, 64);
+        const uint2 y = make_uint2((uint32_t)__shfl(x.x, src, 64), (uint32_t)__shfl(x.y, src, 64));
         if (act && j != gl) {
-            const int c = in_lds ? win_cmp(w, x.x - base, len, ys - base, ye - ys, 7)
-                                 : rec_cmp8(S, x.x, len, ys, ye - ys, 7);
+            const int c = seg_cmp(S, mk, x, ok, y);
             if (c > 0 || (c == 0 && j < gl)) ++rank;
             if (c == 0 && j < gl) d = true;
         }
@@ -316,12 +318,16 @@ __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S,
     const uint32_t k = 1u + (uint32_t)(__ffsll((long long)me) - 1);
     const bool act = lane < k;
     const uint2 x = act ? SS[a + lane] : make_uint2(0u, 0u);
+    const SegKeys mk = act ? seg_keys(S, x) : SegKeys{{0, 0, 0, 0}};
     uint32_t rank = 0;
     bool d = false;
     for (uint32_t j = 0; j < k; ++j) {
-        const uint32_t ys = (uint32_t)__shfl(x.x, (int)j, 64), ye = (uint32_t)__shfl(x.y, (int)j, 64);
+        SegKeys ok;
+#pragma unroll
+        for (int c = 0; c < SEG_CH; ++c) ok.c[c] = __shfl(mk.c[c], (int)j, 64);
+        const uint2 y = make_uint2((uint32_t)__shfl(x.x, (int)j, 64), (uint32_t)__shfl(x.y, (int)j, 64));
         if (act && j != lane) {
-            const int c = rec_cmp8(S, x.x, x.y - x.x, ys, ye - ys, 7);
+            const int c = seg_cmp(S, mk, x, ok, y);
             if (c > 0 || (c == 0 && j < lane)) ++rank;
             if (c == 0 && j < lane) d = true;
         }
@@ -663,7 +669,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
                 SG_TRY(slot(c, vs.uspans, 1, &us));
                 SG_TRY(slot(c, vs.ukeys, 1, &uk));
                 uint64_t *cnt;
-                SG_TRY(run_emit(c, "emit_uniq", "emit_uniq.count", S_EMIT2, PermItem{nullptr, L.spans}, R, d_buf, ub,
+                SG_TRY(run_emit(c, k_emit_uniq, "emit_uniq", "emit_uniq.count", S_EMIT2, PermItem{nullptr, L.spans}, R, d_buf, ub,
                                 us, L.keys, uk, &cnt, 0.0));
                 uint64_t t = 0;
                 SG_TRY(ctx_readback(c, &t, cnt, 8));
@@ -705,20 +711,21 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, S_SSPANS, R, &SS));
     uint64_t *pc;
     // model: input bytes read + S written once; cached span per record in, span per record out
-    SG_TRY(run_emit(c, "emit_sorted", "emit_sorted.count", S_EMIT, PermItem{V, L.spans}, R, d_buf, Sb, SS, nullptr,
+    SG_TRY(run_emit(c, k_emit_sorted, "emit_sorted", "emit_sorted.count", S_EMIT, PermItem{V, L.spans}, R, d_buf, Sb, SS, nullptr,
                     nullptr, &pc, 2.0 * (double)n + 16.0 * R));
 
     // adjacent equality inside segments; segments holding two different records -> sort
-    uint8_t *dup, *bad;
+    uint8_t *dup, *segbad;
     SG_TRY(slot(c, S_DUP, R, &dup));
-    SG_TRY(slot(c, S_BAD, R, &bad));
-    // model: key0 + brk + span per record, both records' bytes where compared, dup + bad out
-    SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, k_adjacent, grid_for(R, 256), 256, 0, Sb, SS, K, brk, R, dup, bad);
+    SG_TRY(slot(c, S_BAD, R, &segbad));
+    SG_HIP(hipMemsetAsync(segbad, 0, R, c->stream));
+    // model: key0 + brk + span per record, both records' bytes where compared, dup out
+    SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, k_adjacent, grid_for(R, 256), 256, 0, Sb, SS, K, brk, R, dup, segbad);
     uint32_t *hs, *hb;
     SG_TRY(slot(c, S_SEL, (size_t)R / 2 + 16, &hs));
     SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
     uint32_t ns = 0, nb = 0;
-    SG_TRY(run_select2(c, "seg_heads", SegPred{brk, bad, R}, R, hs, hb, &ns, &nb, 2.0));
+    SG_TRY(run_select2(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, &ns, &nb, 1.0));
     uint32_t *err;
     SG_TRY(slot(c, S_ERR, 4, &err));
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
@@ -733,7 +740,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, vs.uspans, R, &us));
     SG_TRY(slot(c, vs.ukeys, R, &uk));
     uint64_t *uc;
-    SG_TRY(run_emit(c, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
+    SG_TRY(run_emit(c, k_emit_uniq, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
                     0.0));
     uint64_t tt = 0;
     SG_TRY(ctx_readback(c, &tt, uc, 8));
@@ -782,7 +789,7 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     uint8_t *fout;
     SG_TRY(slot(c, S_OUT_FRESH, (size_t)cu.bytes + 64, &fout));
     uint64_t *fc;
-    SG_TRY(run_emit(c, "emit_fresh", "emit_fresh.count", S_EMIT3, FlagItem{cu.spans, fresh, 1}, cu.n, cu.buf, fout,
+    SG_TRY(run_emit(c, k_emit_fresh, "emit_fresh", "emit_fresh.count", S_EMIT3, FlagItem{cu.spans, fresh, 1}, cu.n, cu.buf, fout,
                     nullptr, nullptr, nullptr, &fc, 0.0));
     uint64_t tt = 0;
     SG_TRY(ctx_readback(c, &tt, fc, 8));

@@ -47,29 +47,57 @@ __device__ __forceinline__ void put_short(Ptr d, const uint4 (&c)[4], uint32_t s
     d[len] = 0x0a;
 }
 
-// LDS-window form of put_short: whole dwords of the destination are built with a funnel
-// shift of two source dwords (one ds_write_b32 each); only the <= 3 head and <= 3 tail
-// bytes of the record are byte stores, from byte loads issued with the chunk loads.
+// LDS-window form of put_short. The 64-byte source window c[] is first normalised so the
+// record starts at byte 0 (a dword barrel shift by sh>>2 done with mask blends, then a
+// byte funnel shift by sh&3), masked (bytes >= len zero, '\n' at len), then re-aligned to
+// the destination dword grid (funnel shift by 4 - (d&3)). Whole destination dwords are
+// ds_write_b32; only the first and last partial dwords (shared with the neighbouring
+// records) are written bytewise. No extra memory traffic beyond the chunk loads.
 __device__ __forceinline__ void put_short_win(uint8_t *win, uint32_t d, const uint4 (&c)[4], uint32_t sh,
-                                              uint32_t len, const uint32_t (&hb)[3], uint32_t h,
-                                              const uint32_t (&tb)[3], uint32_t ts, uint32_t tn) {
-    const uint32_t dw[17] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w,
-                             c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w, 0u};
-    const uint32_t e = (sh - d) & 3u;
+                                              uint32_t len) {
+    const uint32_t dw[18] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w,
+                             c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w, 0u, 0u};
+    const uint32_t t = sh >> 2, e = sh & 3u;
+    const uint32_t m2 = (t & 2u) ? ~0u : 0u, m1 = (t & 1u) ? ~0u : 0u;
+    uint32_t s1[16], s2[15], rec[14];
 #pragma unroll
-    for (uint32_t w = 0; w < 16; ++w) {
-        const uint32_t P = 4 * w + e;
-        if (P >= sh + h && P + 4 <= sh + len) {
-            const uint32_t v = __builtin_amdgcn_alignbyte(dw[w + 1], dw[w], e);
-            *reinterpret_cast<uint32_t *>(win + d + (P - sh)) = v;
+    for (int o = 0; o < 16; ++o) s1[o] = dw[o] ^ ((dw[o] ^ dw[o + 2]) & m2);
+#pragma unroll
+    for (int o = 0; o < 15; ++o) s2[o] = s1[o] ^ ((s1[o] ^ s1[o + 1]) & m1);
+    // record bytes [4o, 4o+4) for o < 13 (len + 1 <= 50 bytes), masked
+#pragma unroll
+    for (int o = 0; o < 14; ++o) {
+        uint32_t x = (o < 13) ? __builtin_amdgcn_alignbyte(s2[o + 1], s2[o], e) : 0u;
+        const uint32_t b0 = 4u * o;
+        if (b0 + 4u > len) {
+            if (b0 <= len) {
+                const uint32_t k = len - b0;
+                x = (x & ((1u << (8u * k)) - 1u)) | (0x0au << (8u * k));
+            } else {
+                x = 0u;
+            }
+        }
+        rec[o] = x;
+    }
+    // destination: bytes [d, d + len + 1); dword j of the grid starting at D = d - f
+    const uint32_t f = d & 3u, D = d - f, end = f + len + 1u;  // end: bytes used from D
+    const uint32_t mf = f ? ~0u : 0u;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+        const uint32_t lo = (j > 0) ? rec[j - 1] : 0u;
+        // f == 0: rec[j]; else bytes (4-f..3) of rec[j-1] then (0..f-1) of rec[j]
+        const uint32_t sh_v = __builtin_amdgcn_alignbyte(rec[j], lo, (4u - f) & 3u);
+        const uint32_t v = (rec[j] & ~mf) | (sh_v & mf);
+        const uint32_t b0 = 4u * j;
+        if (b0 >= end) continue;
+        if (b0 >= f && b0 + 4u <= end) {
+            *reinterpret_cast<uint32_t *>(win + D + b0) = v;
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b)
+                if (b0 + b >= f && b0 + b < end) win[D + b0 + b] = (uint8_t)(v >> (8 * b));
         }
     }
-#pragma unroll
-    for (uint32_t j = 0; j < 3; ++j) {
-        if (j < h) win[d + j] = (uint8_t)hb[j];
-        if (j < tn) win[d + ts + j] = (uint8_t)tb[j];
-    }
-    win[d + len] = 0x0a;
 }
 
 // Copy the records of one round into out[o0..oend) (base = o0 & ~15): lane-owned record
@@ -85,24 +113,12 @@ __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src,
     const uint64_t span = oend - base;
     const bool in_lds = span <= EM_WIN;
     const uint32_t q0 = s & ~15u, sh = s - q0;
-    const bool shortr = f && (sh + len <= 64u);
+    const bool shortr = f && (sh + len <= 64u) && (len < 50u);
     uint4 c[4];
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
         c[k] = make_uint4(0u, 0u, 0u, 0u);
         if (shortr && 16u * k < sh + len) c[k] = *reinterpret_cast<const uint4 *>(src + q0 + 16u * k);
-    }
-    // destination dword bounds inside the window: head bytes [d, d+h), whole dwords, tail
-    // bytes [d+ts, d+ts+tn)
-    const uint32_t D0 = (d + 3u) & ~3u, D1 = (d + len) & ~3u;
-    const uint32_t h = (D0 - d) < len ? (D0 - d) : len;
-    const uint32_t ts = (D1 > d + h ? D1 : d + h) - d;
-    const uint32_t tn = len - ts;
-    uint32_t hb[3], tb[3];
-#pragma unroll
-    for (uint32_t j = 0; j < 3; ++j) {
-        hb[j] = (shortr && in_lds && j < h) ? src[s + j] : 0u;
-        tb[j] = (shortr && in_lds && j < tn) ? src[s + ts + j] : 0u;
     }
     const bool longr = f && !shortr;
     const uint64_t ml = __ballot(longr);
@@ -113,7 +129,7 @@ __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src,
         s_dst[cidx] = d;
     }
     if (shortr) {
-        if (in_lds) put_short_win(win, d, c, sh, len, hb, h, tb, ts, tn);
+        if (in_lds) put_short_win(win, d, c, sh, len);
         else put_short(out + base + d, c, sh, len);
     }
     if (ml) {
@@ -192,12 +208,12 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_count(Item item, uint32_t n, 
     }
 }
 
-__global__ __launch_bounds__(EM_BLOCK) void k_emit_apply(const uint2 *__restrict__ cache, uint32_t n,
-                                                         const uint64_t *__restrict__ pre,
-                                                         const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
-                                                         uint2 *__restrict__ out_spans,
-                                                         const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
-                                                         int dbg) {
+__device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache, uint32_t n,
+                                                const uint64_t *__restrict__ pre,
+                                                const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                uint2 *__restrict__ out_spans,
+                                                const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
+                                                int dbg) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4][EM_WIN];
     __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
     __shared__ uint64_t s_wt[4];
@@ -251,6 +267,20 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_apply(const uint2 *__restrict
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 }
+
+// One symbol per use, so rocprofv3 kernel stats and PMC passes attribute each separately.
+#define SG_EMIT_APPLY(NAME)                                                                         \
+    __global__ __launch_bounds__(EM_BLOCK) void NAME(                                               \
+        const uint2 *__restrict__ cache, uint32_t n, const uint64_t *__restrict__ pre,              \
+        const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, uint2 *__restrict__ out_spans,  \
+        const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout, int dbg) {                   \
+        emit_apply_body(cache, n, pre, src, dst, out_spans, kin, kout, dbg);                        \
+    }
+SG_EMIT_APPLY(k_emit_sorted)
+SG_EMIT_APPLY(k_emit_uniq)
+SG_EMIT_APPLY(k_emit_fresh)
+SG_EMIT_APPLY(k_emit_apply)
+#undef SG_EMIT_APPLY
 
 // ------------------------------------------------------------------ common items
 // Sorted position i -> input record V[i] (V null: record i).

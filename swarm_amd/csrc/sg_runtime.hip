@@ -79,7 +79,7 @@ void prof_end(sg_ctx *c, int stat, hipEvent_t a) {
 }
 
 void prof_bytes(sg_ctx *c, const char *name, double bytes) {
-    if (!c->profile) return;
+    if (!c->profile || !prof_wanted(c, name)) return;
     for (auto &s : c->stats)
         if (s.name == name || strcmp(s.name, name) == 0) { s.bytes += bytes; return; }
     c->stats.push_back(KStat{name, 0, 0.0, bytes});
@@ -208,6 +208,12 @@ int sg_ctx_sync(sg_ctx *c) {
 int sg_ctx_profile(sg_ctx *c, int enable) {
     if (!c) return SG_E_INVAL;
     c->profile = enable != 0;
+    return SG_OK;
+}
+
+int sg_ctx_profile_only(sg_ctx *c, const char *name) {
+    if (!c) return SG_E_INVAL;
+    c->prof_only = name ? name : "";
     return SG_OK;
 }
 

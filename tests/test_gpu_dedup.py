@@ -239,3 +239,20 @@ def test_dedup_unsorted_prior_long(sg):
     u, f = sg.dedup_diff(cur, prior)
     eu, ef = S.dedup_diff(cur, prior)
     assert u == eu and f == ef
+
+
+@pytest.mark.parametrize("maxlen", [1, 15, 16, 31, 32, 33, 63, 64, 65, 200])
+def test_dedup_slot_width_boundaries(sg, maxlen):
+    """Longest record just below / at / above the fixed-slot widths (32, 64 bytes) and the
+    packed fallback; records start at every source alignment."""
+    rng = random.Random(maxlen)
+    recs = [bytes(rng.choice(b"ab\x00\xff") for _ in range(rng.randint(1, maxlen))) for _ in range(3000)]
+    recs.append(b"z" * maxlen)
+    recs += rng.sample(recs, 500)
+    rng.shuffle(recs)
+    b = b"\n".join(recs) + b"\n"
+    assert sg.dedup(b) == S.dedup(b)
+    prior = b"".join(r + b"\n" for r in sorted(set(recs[:1500])))
+    u, f = sg.dedup_diff(b, prior)
+    eu, ef = S.dedup_diff(b, prior)
+    assert u == eu and f == ef

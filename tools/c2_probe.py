@@ -21,6 +21,11 @@ ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
 for _ in range(2):
     r = ctx.dedup_diff(d_cur.data_ptr(), d_cur.numel(), d_pri.data_ptr(), d_pri.numel())
 torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(5):
+    r = ctx.dedup_diff(d_cur.data_ptr(), d_cur.numel(), d_pri.data_ptr(), d_pri.numel())
+torch.cuda.synchronize()
+el_noprof = (time.perf_counter() - t0) / 5
 ctx.reset_stats()
 ctx.profile(True)
 t0 = time.perf_counter()
@@ -30,7 +35,8 @@ torch.cuda.synchronize()
 el = (time.perf_counter() - t0) / 5
 ctx.profile(False)
 st = ctx.kernel_stats()
-out = {"mode": {k: v for k, v in os.environ.items() if k.startswith("SG_")}, "ms_step": round(el * 1e3, 3),
+out = {"mode": {k: v for k, v in os.environ.items() if k.startswith("SG_")}, "ms_step": round(el * 1e3, 3), "ms_step_noprof": round(el_noprof * 1e3, 3),
+       "kernel_sum_ms": round(sum(v[1] for v in st.values()) / 5, 3),
        "kernels_us": {k: round(v[1] / v[0] * 1e3, 1) for k, v in sorted(st.items(), key=lambda kv: -kv[1][1])}}
 print(json.dumps(out), flush=True)
 ctx.close()
