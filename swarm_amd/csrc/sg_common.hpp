@@ -293,6 +293,61 @@ __device__ __forceinline__ bool rec_equal(const uint8_t *ba, uint32_t sa, uint32
     return true;
 }
 
+// The 52 bytes starting at window byte sh (0..15) of four 16-B chunks, as dwords r[0..12]:
+// a dword barrel shift by sh>>2 (mask blends: a select between elements of one array would
+// be folded into a dynamically indexed load and spill the array to scratch) and a byte
+// funnel shift by sh&3.
+__device__ __forceinline__ void normalize52(const uint4 (&c)[4], uint32_t sh, uint32_t (&r)[13]) {
+    const uint32_t dw[18] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w,
+                             c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w, 0u, 0u};
+    const uint32_t t = sh >> 2, e = sh & 3u;
+    const uint32_t m2 = (t & 2u) ? ~0u : 0u, m1 = (t & 1u) ? ~0u : 0u;
+    uint32_t s1[16], s2[15];
+#pragma unroll
+    for (int o = 0; o < 16; ++o) s1[o] = dw[o] ^ ((dw[o] ^ dw[o + 2]) & m2);
+#pragma unroll
+    for (int o = 0; o < 15; ++o) s2[o] = s1[o] ^ ((s1[o] ^ s1[o + 1]) & m1);
+#pragma unroll
+    for (int o = 0; o < 13; ++o) r[o] = __builtin_amdgcn_alignbyte(s2[o + 1], s2[o], e);
+}
+
+// Aligned 16-B chunks covering bytes [p, p + cl) of buf (cl <= 48): chunk k loaded only when
+// it holds some of them.
+__device__ __forceinline__ void load_chunks(const uint8_t *buf, uint32_t p, uint32_t cl, uint4 (&c)[4]) {
+    const uint32_t q0 = p & ~15u, sh = p - q0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        c[k] = (16u * k < sh + cl) ? *reinterpret_cast<const uint4 *>(buf + q0 + 16u * k) : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// rec_equal with wide loads: when the compared span (len - off) is <= 48 bytes each side
+// takes at most four 16-B loads and the comparison is a masked XOR of normalised dwords;
+// longer spans use rec_equal. Buffers must be 16-byte aligned.
+__device__ __forceinline__ bool rec_equal_w(const uint8_t *ba, uint32_t sa, uint32_t ea, const uint8_t *bb,
+                                            uint32_t sb, uint32_t eb, uint32_t off) {
+    const uint32_t la = ea - sa;
+    if (la != eb - sb) return false;
+    if (la <= off) return true;
+    const uint32_t cl = la - off;
+    if (cl > 48u) return rec_equal(ba, sa, ea, bb, sb, eb, off);
+    uint4 ca[4], cb[4];
+    load_chunks(ba, sa + off, cl, ca);
+    load_chunks(bb, sb + off, cl, cb);
+    uint32_t ra[13], rb[13];
+    normalize52(ca, (sa + off) & 15u, ra);
+    normalize52(cb, (sb + off) & 15u, rb);
+    uint32_t d = 0;
+#pragma unroll
+    for (uint32_t o = 0; o < 12; ++o) {
+        if (4u * o < cl) {
+            const uint32_t k = cl - 4u * o;
+            const uint32_t m = k >= 4u ? ~0u : ((1u << (8u * k)) - 1u);
+            d |= (ra[o] ^ rb[o]) & m;
+        }
+    }
+    return d == 0;
+}
+
 // Bytewise compare of the suffixes from `off` by 7-byte chunk keys (memcmp-then-length).
 __device__ __forceinline__ int rec_cmp_k(const uint8_t *ba, uint32_t sa, uint32_t ea, const uint8_t *bb,
                                          uint32_t sb, uint32_t eb, uint32_t off) {

@@ -192,16 +192,23 @@ __global__ void k_pos_of(const uint32_t *__restrict__ idx, const uint32_t *__res
 // gathers through the permuted spans (still inside the same few cache lines).
 constexpr uint32_t SEG_SMALL = 16;
 
-// Memcmp-then-length of two records of `buf` from byte `off`, 8 bytes per step.
-__device__ __forceinline__ int rec_cmp8(const uint8_t *buf, uint32_t sa, uint32_t la, uint32_t sb, uint32_t lb,
-                                        uint32_t off) {
+// Memcmp-then-length of record a of `ba` and record b of `bb` from byte `off`, 8 bytes per
+// step.
+__device__ __forceinline__ int rec_cmp8_2(const uint8_t *ba, uint32_t sa, uint32_t la, const uint8_t *bb,
+                                          uint32_t sb, uint32_t lb, uint32_t off) {
     const uint32_t m = la < lb ? la : lb;
     for (uint32_t o = off; o < m; o += 8) {
         const uint32_t t = (m - o) < 8u ? (m - o) : 8u;
-        const uint64_t x = load_le(buf, sa + o, t), y = load_le(buf, sb + o, t);
+        const uint64_t x = load_le(ba, sa + o, t), y = load_le(bb, sb + o, t);
         if (x != y) return __builtin_bswap64(x) < __builtin_bswap64(y) ? -1 : 1;
     }
     return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// The same for two records of one buffer.
+__device__ __forceinline__ int rec_cmp8(const uint8_t *buf, uint32_t sa, uint32_t la, uint32_t sb, uint32_t lb,
+                                        uint32_t off) {
+    return rec_cmp8_2(buf, sa, la, buf, sb, lb, off);
 }
 
 // dup[i] = record i equals record i-1 inside its segment (tag < 8 key0: whole record).
@@ -212,14 +219,14 @@ __global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S,
                                                   uint32_t n, uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    // all first-level loads issued together (one round trip before the byte compare)
+    const uint32_t ip = i > 0 ? i - 1 : 0;
+    const uint8_t b = brk[i];
+    const uint64_t ki = K[i];
+    const uint2 x = SS[ip], y = SS[i];
     bool d = false;
-    if (i > 0 && !brk[i]) {
-        if ((K[i] & 0xffu) < 8u) {
-            d = true;
-        } else {
-            const uint2 x = SS[i - 1], y = SS[i];
-            d = rec_equal(S, x.x, x.y, S, y.x, y.y, 7);
-        }
+    if (i > 0 && !b) {
+        d = ((ki & 0xffu) < 8u) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, 7);
         if (!d) {
             uint32_t h = i - 1;
             while (h > 0 && !brk[h]) --h;
@@ -431,84 +438,133 @@ __global__ void k_check_sorted(const uint8_t *__restrict__ buf, const uint2 *__r
     if (key_cmp_full(buf, spans, K[i - 1], i - 1, K[i], i, 0) >= 0) atomicOr(flag, 1u);
 }
 
-// ------------------------------------------------------------------ diff (merge path)
+// ------------------------------------------------------------------ diff
+// U (this scan's unique records) and P (the prior's) are both sorted and duplicate-free,
+// and equal records have equal key0. So the work splits on key0 alone: tile t owns
+// U[t*DF_TILE, (t+1)*DF_TILE) and the P records with keys in [U.K[i0], U.K[i1]), found by
+// a wave-cooperative 64-ary lower_bound over P.K (4 dependent probes at 10M, no byte
+// compares). A U record is present in P iff some P record with its key0 has its bytes: a
+// tag < 8 key0 is the whole record; a tag-8 one is compared bytewise (from byte 7) with
+// the equal-key P records (almost always exactly one).
 struct RecSet {
     const uint8_t *buf;
     const uint2 *sp;
-    const uint32_t *ids;  // position -> record id (null = identity)
     const uint64_t *K;    // key0 per position
     uint32_t n;
-    __device__ uint32_t id(uint32_t i) const { return ids ? ids[i] : i; }
 };
 
-__device__ __forceinline__ int set_cmp(const RecSet &A, uint64_t ka, uint32_t ra, const RecSet &B, uint64_t kb,
-                                       uint32_t rb) {
-    if (ka != kb) return ka < kb ? -1 : 1;
-    if ((ka & 0xffu) < 8u) return 0;
-    return rec_cmp_k(A.buf, A.sp[ra].x, A.sp[ra].y, B.buf, B.sp[rb].x, B.sp[rb].y, 7);
-}
+constexpr uint32_t DF_TILE = 1024;  // U records per block
+constexpr uint32_t DF_PCAP = 4096;  // P keys staged in LDS per block
+constexpr uint32_t DF_PER = DF_TILE / 256;
 
-constexpr uint32_t MP_TILE = 2048;
-
-// Merge-path split of diagonal t*MP_TILE over (U, P), U first on ties: split[t] = i.
-__global__ void k_merge_split(RecSet U, RecSet P, uint32_t ntiles, uint32_t *split) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    const uint64_t tot = (uint64_t)U.n + P.n;
-    const uint64_t d64 = (uint64_t)t * MP_TILE < tot ? (uint64_t)t * MP_TILE : tot;
-    const uint32_t d = (uint32_t)d64;
-    uint32_t lo = d > P.n ? d - P.n : 0u, hi = d < U.n ? d : U.n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const uint32_t j = d - mid - 1;
-        if (set_cmp(U, U.K[mid], U.id(mid), P, P.K[j], P.id(j)) <= 0) lo = mid + 1;
-        else hi = mid;
+// One wave per boundary t: jb[t] = lower_bound(P.K, U.K[t * DF_TILE]) (P.n past the end).
+__global__ __launch_bounds__(256) void k_diff_split(const uint64_t *__restrict__ UK, uint32_t nu,
+                                                    const uint64_t *__restrict__ PK, uint32_t np, uint32_t nb,
+                                                    uint32_t *__restrict__ jb) {
+    const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = lane_id();
+    if (t >= nb) return;
+    const uint64_t i = (uint64_t)t * DF_TILE;
+    if (i >= nu) { if (lane == 0) jb[t] = np; return; }
+    const uint64_t key = UK[i];
+    uint32_t lo = 0, hi = np;  // answer in [lo, hi]
+    while (hi > lo) {
+        const uint32_t span = hi - lo;
+        if (span <= 64) {
+            const uint32_t p = lo + lane;
+            const bool ge = (p >= hi) || PK[p] >= key;
+            const uint64_t m = __ballot(ge);
+            lo = lo + (uint32_t)(__ffsll((long long)m) - 1);
+            break;
+        }
+        const uint32_t p = lo + (uint32_t)(((uint64_t)span * (lane + 1)) / 65);
+        const bool ge = PK[p] >= key;
+        const uint64_t m = __ballot(ge);
+        if (!m) {
+            lo = (uint32_t)__shfl((int)p, 63, 64) + 1;
+        } else {
+            const int f = __ffsll((long long)m) - 1;
+            const uint32_t pf = (uint32_t)__shfl((int)p, f, 64);
+            const uint32_t pp = (uint32_t)__shfl((int)p, f > 0 ? f - 1 : 0, 64);
+            hi = pf;
+            if (f > 0) lo = pp + 1;
+        }
     }
-    split[t] = lo;
+    if (lane == 0) jb[t] = lo;
 }
 
-// fresh[i] = 1 if U[i] is absent from P. Inside the tile's P range (keys staged in LDS)
-// find the run of P keys equal to U[i]'s key0: a tag < 8 key is the whole record, so the
-// run decides; a tag-8 run (usually one record) is checked with a wide byte compare. The
-// run may continue past the tile into P[j1...] (ties go to U first in the merge order).
-__global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uint32_t *__restrict__ split,
-                                                   uint8_t *fresh) {
-    __shared__ uint64_t s_k[MP_TILE];
-    __shared__ uint32_t s_r[MP_TILE];
+__global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uint32_t *__restrict__ jb,
+                                                   uint8_t *__restrict__ fresh) {
+    __shared__ uint64_t s_k[DF_PCAP];
     const uint32_t t = blockIdx.x;
-    const uint64_t tot = (uint64_t)U.n + P.n;
-    const uint32_t d0 = (uint32_t)((uint64_t)t * MP_TILE);
-    const uint32_t d1 = (uint32_t)((uint64_t)(t + 1) * MP_TILE < tot ? (uint64_t)(t + 1) * MP_TILE : tot);
-    const uint32_t i0 = split[t], i1 = split[t + 1];
-    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
+    const uint32_t i0 = t * DF_TILE;
+    const uint32_t j0 = jb[t], j1 = jb[t + 1];
     const uint32_t np = j1 - j0;
-    for (uint32_t q = threadIdx.x; q < np; q += blockDim.x) {
-        s_k[q] = P.K[j0 + q];
-        s_r[q] = P.id(j0 + q);
-    }
+    const bool staged = np <= DF_PCAP;
+    if (staged)
+        for (uint32_t q = threadIdx.x; q < np; q += 256) s_k[q] = P.K[j0 + q];
     __syncthreads();
-    for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-        const uint64_t ku = U.K[i];
+    uint32_t idx[DF_PER], cand[DF_PER];
+    uint64_t ku[DF_PER];
+    bool need[DF_PER], pres[DF_PER];
+#pragma unroll
+    for (int k = 0; k < DF_PER; ++k) {
+        idx[k] = i0 + threadIdx.x + 256u * k;
+        ku[k] = idx[k] < U.n ? U.K[idx[k]] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < DF_PER; ++k) {
+        // lower_bound of ku in P[j0, j1) (LDS when staged)
         uint32_t lo = 0, hi = np;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (s_k[mid] < ku) lo = mid + 1;
-            else hi = mid;
+            const uint64_t v = staged ? s_k[mid] : P.K[j0 + mid];
+            if (v < ku[k]) lo = mid + 1; else hi = mid;
         }
-        bool present = false;
-        const bool whole = (ku & 0xffu) < 8u;
-        uint32_t ru = 0, us = 0, ue = 0;
-        if (!whole) { ru = U.id(i); us = U.sp[ru].x; ue = U.sp[ru].y; }
-        for (uint32_t q = j0 + lo; q < P.n; ++q) {
-            const uint32_t lq = q - j0;
-            const uint64_t kp = (lq < np) ? s_k[lq] : P.K[q];
-            if (kp != ku) break;
-            if (whole) { present = true; break; }
-            const uint32_t rp = (lq < np) ? s_r[lq] : P.id(q);
-            if (rec_equal(U.buf, us, ue, P.buf, P.sp[rp].x, P.sp[rp].y, 7)) { present = true; break; }
-        }
-        fresh[i] = present ? 0 : 1;
+        cand[k] = j0 + lo;
+        const uint64_t kp = (lo < np) ? (staged ? s_k[lo] : P.K[j0 + lo]) : (j0 + lo < P.n ? P.K[j0 + lo] : ~ku[k]);
+        const bool eq = idx[k] < U.n && j0 + lo < P.n && kp == ku[k];
+        pres[k] = eq && (ku[k] & 0xffu) < 8u;
+        need[k] = eq && !pres[k];
     }
+    // tag-8 candidates: spans of both records, then a wide compare (loads of all items together)
+    uint2 us[DF_PER], ps[DF_PER];
+#pragma unroll
+    for (int k = 0; k < DF_PER; ++k) {
+        us[k] = need[k] ? U.sp[idx[k]] : make_uint2(0u, 0u);
+        ps[k] = need[k] ? P.sp[cand[k]] : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < DF_PER; ++k) {
+        if (!need[k]) continue;
+        if (rec_equal_w(U.buf, us[k].x, us[k].y, P.buf, ps[k].x, ps[k].y, 7)) { pres[k] = true; continue; }
+        // other P records sharing this key0 (distinct records with the same first 7 bytes):
+        // they are sorted by their remaining bytes, so binary-search the run [c+1, c_end)
+        // by full compare instead of scanning it
+        const uint32_t c0 = cand[k] + 1;
+        uint32_t ce = c0;
+        if (staged && c0 - j0 <= np) {
+            uint32_t lo = c0 - j0, hi = np;  // upper bound of ku in the staged keys
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_k[mid] <= ku[k]) lo = mid + 1; else hi = mid;
+            }
+            ce = j0 + lo;
+        }
+        if (!staged || ce >= j1)
+            while (ce < P.n && P.K[ce] == ku[k]) ++ce;  // run reaches past the staged keys
+        uint32_t lo = c0, hi = ce;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint2 x = P.sp[mid];
+            const int cmp = rec_cmp8_2(P.buf, x.x, x.y - x.x, U.buf, us[k].x, us[k].y - us[k].x, 7);
+            if (cmp == 0) { pres[k] = true; break; }
+            if (cmp < 0) lo = mid + 1; else hi = mid;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < DF_PER; ++k)
+        if (idx[k] < U.n) fresh[idx[k]] = pres[k] ? 0 : 1;
 }
 
 // ------------------------------------------------------------------ host pipeline
@@ -778,14 +834,16 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     }
     uint8_t *fresh;
     SG_TRY(slot(c, S_FRESHF, (size_t)cu.n + 1, &fresh));
-    RecSet U{cu.buf, cu.spans, nullptr, cu.keys, cu.n};
-    RecSet P{pv.buf, pv.spans, nullptr, pv.keys, pv.n};
-    const uint32_t ntiles = (uint32_t)(((uint64_t)cu.n + pv.n + MP_TILE - 1) / MP_TILE);
-    uint32_t *split;
-    SG_TRY(slot(c, S_R_OFF, (size_t)ntiles + 2, &split));
-    SG_LAUNCH(c, "merge_split", k_merge_split, grid_for(ntiles + 1, 256), 256, 0, U, P, ntiles, split);
-    // model: key + span of every unique cur and prior record, one flag per cur record
-    SG_LAUNCH_B(c, "diff_tile", 16.0 * (cu.n + (double)pv.n) + cu.n, k_diff_tile, ntiles, 256, 0, U, P, split, fresh);
+    RecSet U{cu.buf, cu.spans, cu.keys, cu.n};
+    RecSet P{pv.buf, pv.spans, pv.keys, pv.n};
+    const uint32_t ntiles = (cu.n + DF_TILE - 1) / DF_TILE;
+    uint32_t *jb;
+    SG_TRY(slot(c, S_R_OFF, (size_t)ntiles + 2, &jb));
+    SG_LAUNCH(c, "diff_split", k_diff_split, grid_for(ntiles + 1, 4), 256, 0, cu.keys, cu.n, pv.keys, pv.n, ntiles + 1, jb);
+    // model: key + span of every unique cur record, key of every prior record, the compared
+    // bytes of both sides (~ the unique output + the prior), one flag per cur record
+    SG_LAUNCH_B(c, "diff_tile", 16.0 * cu.n + 8.0 * pv.n + (double)cu.bytes + cu.n, k_diff_tile, ntiles, 256, 0,
+                U, P, jb, fresh);
     uint8_t *fout;
     SG_TRY(slot(c, S_OUT_FRESH, (size_t)cu.bytes + 64, &fout));
     uint64_t *fc;

@@ -114,16 +114,19 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
         bits &= bits - 1;
         spans[si].x = (uint32_t)(my0 + b);
         if (keys) {
-            const int q = t * LN_BPT + b;
-            uint32_t rem = 8;
-            uint64_t k = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t c = s_b[q + j];
-                if (c == 0x0a && rem == 8) rem = j;
-                if (j < 7 && (uint32_t)j < rem) k |= (uint64_t)c << (56 - 8 * j);
-            }
-            keys[si] = k | rem;
+            // bytes [q, q+8) from three aligned dwords; tag = first '\n' in them (SWAR: the
+            // lowest flagged byte is exact), key = the bytes before it (<= 7), big-endian
+            const uint32_t q = t * LN_BPT + b;
+            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_b) + (q >> 2);
+            const uint32_t w0 = w32[0], w1 = w32[1], w2 = w32[2];
+            const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, q & 3u) |
+                               ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, q & 3u) << 32);
+            const uint64_t y = v ^ 0x0a0a0a0a0a0a0a0aull;
+            const uint64_t z = (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
+            const uint32_t rem = z ? (uint32_t)(__builtin_ctzll(z) >> 3) : 8u;
+            const uint32_t take = rem < 7u ? rem : 7u;
+            const uint64_t m = (1ull << (8u * take)) - 1ull;
+            keys[si] = (__builtin_bswap64(v & m) & ~0xffull) | rem;
         }
         ++si;
     }
