@@ -169,13 +169,73 @@ def bench_c3(args):
     ctx.close()
 
 
+def bench_c4(args):
+    """BASELINE.json configs[3] (C4): nmap-service-probes-style port banners x ~10k regex
+    signatures (the 1,176 DFA-compilable nuclei template regexes + 8,800 synthetic
+    nmap-style `match` families), regex-DFA with literal-factor prefilter. Per GPU: the
+    8-GPU config's share, 12.5M banners; weak scaling with --gpus."""
+    import base64
+
+    import numpy as np
+    import torch
+
+    import swarm_amd
+    from swarm_amd import corpus
+
+    torch.cuda.set_device(0)
+    sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
+    pats = [base64.b64decode(r["p"]) for r in sig["regexes"] if r["dfa_rc"] == 0] + corpus.nmap_signatures()
+    n_lines = args.lines if args.lines != 10_000_000 else 12_500_000
+    pool = corpus.banner_pool()
+    buf = corpus.lines_from_pool(pool, n_lines, seed=3)
+    d = torch.from_numpy(buf).cuda()
+    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    tc0 = time.perf_counter()
+    m = swarm_amd.Matcher(pats, "regex")
+    compile_s = time.perf_counter() - tc0
+    run = lambda: m.dev_match(ctx, d.data_ptr(), d.numel())  # noqa: E731
+    el, full, stats, dominant, r = timed_steps(ctx, run, args)
+    R = int(r.in_records)
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import semantics as S
+        m_s = 1000
+        cut = int(np.flatnonzero(buf == 10)[m_s - 1]) + 1
+        sample = buf[:cut].tobytes()
+        tc = time.perf_counter()
+        hits = S.regex_hits(sample, pats)
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(m_s / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d C4 banners x %d regexes, oracle re.search, 1 thread, %.2f s" % (m_s, len(pats), tc),
+               "host_cpus": os.cpu_count()}
+        cpu["gpu_hits_bit_exact_on_sample"] = (m.match(sample) == hits)
+    print(json.dumps({
+        "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (nmap-style port banners, ~30 % from known products, SURVEY.md §8(d) C4)",
+        "config": {"workload": "C4: %.1fM banners x %d regex signatures per GPU (8-GPU config share)"
+                               % (n_lines / 1e6, len(pats)),
+                   "bytes": int(d.numel()), "automaton_states": m.info()["states"],
+                   "compile_s": round(compile_s, 2)},
+        "gbps": round(d.numel() * args.steps / el / 1e9, 2),
+        "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records)},
+        "roofline": roofline_of(stats, dominant, "c4"),
+        "cpu_baseline": cpu,
+        "kernels": kernel_table(full),
+        "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
+                        "HIP events only around the dominant kernel",
+    }), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lines", type=int, default=10_000_000)
-    ap.add_argument("--workload", choices=["c2", "c3"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real runs; gloo rehearses N ranks on fewer GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -183,6 +243,8 @@ def main():
     args = ap.parse_args()
     if args.workload == "c3":
         return bench_c3(args)
+    if args.workload == "c4":
+        return bench_c4(args)
 
     import numpy as np
     import torch

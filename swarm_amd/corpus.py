@@ -189,3 +189,60 @@ def chunk_layout(lines_arr: np.ndarray, n_chunks: int) -> list:
         bounds.append(int(nl[r - 1]) + 1 if r > 0 else 0)
     bounds.append(lines_arr.size)
     return [lines_arr[bounds[i]:bounds[i + 1]] for i in range(n_chunks)]
+
+
+# ------------------------------------------------------------------ C4: nmap-style banners
+_SYL = [b"Open", b"Pure", b"Pro", b"Free", b"Net", b"Cyber", b"Micro", b"Mega", b"Secure", b"Fast", b"Quick",
+        b"Blue", b"Red", b"Iron", b"Cloud", b"Data", b"Web", b"Mail", b"File", b"Core", b"Edge", b"Star",
+        b"Nova", b"Zen", b"Arc", b"Hyper", b"Ultra", b"Smart", b"Tiny", b"Big"]
+_SUF = [b"SSH", b"FTPd", b"Mail", b"Web", b"Srv", b"Box", b"Gate", b"Hub", b"Link", b"Wall", b"Stack", b"Store",
+        b"Proxy", b"DB", b"Cache", b"Queue", b"Vault", b"Shell", b"Port", b"Node"]
+
+# nmap-service-probes-style `match` templates ({p} = product). Each yields one signature
+# per product; the banner generator renders matching lines with concrete versions.
+_FAMILIES = [
+    (rb"^SSH-2\.0-{p}[_-]([\d.]+)(?:p\d+)?", b"SSH-2.0-{p}_{v}p1 Debian-{b}"),
+    (rb"^220 [\w.-]+ ESMTP {p}(?: \(([\w ]+)\))?", b"220 mx{b}.mail.example.net ESMTP {p} (Ubuntu) ready at {v}"),
+    (rb"^220[- ]{p} FTP [Ss]erver \(Version ([\w.]+)\)", b"220 {p} FTP server (Version {v}) ready."),
+    (rb"^HTTP/1\.[01] \d{3} .*Server: {p}/([\d.]+)",
+     b"HTTP/1.1 200 OK Date: Mon, 12 Oct 2026 10:{b} GMT Content-Type: text/html Server: {p}/{v}"),
+    (rb"^\+OK {p} POP3 (?:server )?ready", b"+OK {p} POP3 server ready <{b}@host>"),
+    (rb"^\* OK \[CAPABILITY IMAP4rev1[^\]]*\] {p} ready", b"* OK [CAPABILITY IMAP4rev1 IDLE] {p} ready"),
+    (rb"^{p} ([\d.]+) \(build (\d+)\)", b"{p} {v} (build {b})"),
+    (rb"^-ERR unknown command '{p}[^']*'", b"-ERR unknown command '{p}-{b}'"),
+]
+
+
+def nmap_products(n: int, seed: int = 7) -> list:
+    rng = np.random.default_rng(seed)
+    out, seen = [], set()
+    while len(out) < n:
+        a, b = _SYL[rng.integers(len(_SYL))], _SUF[rng.integers(len(_SUF))]
+        p = a + b + (b"%d" % rng.integers(100) if rng.random() < 0.7 else b"")
+        if p not in seen:
+            seen.add(p)
+            out.append(p)
+    return out
+
+
+def nmap_signatures(n_products: int = 1100, seed: int = 7) -> list:
+    """len(_FAMILIES) * n_products regexes (C4's synthetic nmap-style families)."""
+    prods = nmap_products(n_products, seed)
+    return [t.replace(b"{p}", p) for t, _ in _FAMILIES for p in prods]
+
+
+def banner_pool(n_products: int = 1100, pool: int = 1 << 16, match_frac: float = 0.3, seed: int = 9) -> list:
+    """Port-banner lines (~60 B): match_frac render a signature family with a known product,
+    the rest the same shapes with unknown products."""
+    rng = np.random.default_rng(seed)
+    prods = nmap_products(n_products, 7)
+    rows = []
+    for _ in range(pool):
+        fam = _FAMILIES[rng.integers(len(_FAMILIES))][1]
+        if rng.random() < match_frac:
+            p = prods[rng.integers(len(prods))]
+        else:
+            p = b"Unk" + _SUF[rng.integers(len(_SUF))] + b"%d" % rng.integers(1000)
+        v = b"%d.%d.%d" % (rng.integers(10), rng.integers(20), rng.integers(30))
+        rows.append(fam.replace(b"{p}", p).replace(b"{v}", v).replace(b"{b}", b"%d" % rng.integers(100000)))
+    return rows

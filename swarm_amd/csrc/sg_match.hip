@@ -453,20 +453,54 @@ struct ACArgs {
     const uint32_t *fac_off, *fac_pids;  // prefilter: factor -> candidate patterns (else null)
 };
 
-__device__ __forceinline__ void emit_hit(const ACArgs &a, uint32_t rec, uint32_t sig, uint32_t *seen, uint32_t &nseen) {
+// Per-block LDS staging of (record << 32 | signature) events: an append is one LDS atomic;
+// the block drains the buffer with ONE global atomic per flush. (One global atomic per
+// event serialises every block on a single counter, which bounded the regex kernels at a
+// few GB/s on hit-dense inputs.) A full buffer falls back to a direct global append.
+constexpr uint32_t HS_CAP = 1024;
+struct HitSink {
+    unsigned long long *lds;  // HS_CAP entries
+    uint32_t *n, *g;          // LDS counter, LDS broadcast slot
+    unsigned long long *hits;
+    uint32_t *count;
+    uint32_t cap;
+    __device__ __forceinline__ void push(unsigned long long v) const {
+        const uint32_t i = atomicAdd(n, 1u);
+        if (i < HS_CAP) {
+            lds[i] = v;
+        } else {
+            const uint32_t q = atomicAdd(count, 1u);
+            if (q < cap) hits[q] = v;
+        }
+    }
+    // Whole block, uniform control flow. Drains when at least half full (or `force`).
+    __device__ __forceinline__ void flush(bool force) const {
+        __syncthreads();
+        const uint32_t hn = min(*n, HS_CAP);
+        if (!force && hn < HS_CAP / 2) return;
+        if (threadIdx.x == 0) *g = hn ? atomicAdd(count, hn) : 0u;
+        __syncthreads();
+        const uint32_t base = *g;
+        for (uint32_t i = threadIdx.x; i < hn; i += blockDim.x)
+            if (base + i < cap) hits[base + i] = lds[i];
+        __syncthreads();
+        if (threadIdx.x == 0) *n = 0;
+        __syncthreads();
+    }
+};
+
+__device__ __forceinline__ void emit_hit(const ACArgs &a, const HitSink &sink, uint32_t rec, uint32_t sig,
+                                         uint32_t *seen, uint32_t &nseen) {
     const uint32_t key = sig;
     for (uint32_t q = 0; q < nseen; ++q)
         if (seen[q] == key) return;
     if (nseen < 4) seen[nseen++] = key;
     if (a.fac_off) {  // prefilter: every pattern that needs this factor is a candidate
-        for (uint32_t q = a.fac_off[sig]; q < a.fac_off[sig + 1]; ++q) {
-            const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
-            if (slot_i < a.cap) a.hits[slot_i] = ((unsigned long long)rec << 32) | a.fac_pids[q];
-        }
+        for (uint32_t q = a.fac_off[sig]; q < a.fac_off[sig + 1]; ++q)
+            sink.push(((unsigned long long)rec << 32) | a.fac_pids[q]);
         return;
     }
-    const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
-    if (slot_i < a.cap) a.hits[slot_i] = ((unsigned long long)rec << 32) | sig;
+    sink.push(((unsigned long long)rec << 32) | sig);
 }
 
 __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
@@ -480,9 +514,15 @@ __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
     const uint32_t nbits = (a.S + 31) / 32;
     if (a.bits_in_lds)
         for (uint32_t q = threadIdx.x; q < nbits; q += blockDim.x) s_bits[q] = a.outbits[q];
+    __shared__ unsigned long long s_hb[HS_CAP];
+    __shared__ uint32_t s_hn, s_hg;
+    if (threadIdx.x == 0) s_hn = 0;
     __syncthreads();
+    const HitSink sink{s_hb, &s_hn, &s_hg, a.hits, a.hit_count, a.cap};
     const uint32_t *bits = a.bits_in_lds ? s_bits : a.outbits;
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.R; r += gridDim.x * blockDim.x) {
+    for (uint32_t r0 = blockIdx.x * blockDim.x; r0 < a.R; r0 += gridDim.x * blockDim.x, sink.flush(false)) {
+        const uint32_t r = r0 + threadIdx.x;
+        if (r >= a.R) continue;
         const uint2 sp_ = a.spans[r];
         const uint32_t s = sp_.x, e = sp_.y;
         uint32_t st = 0;
@@ -498,11 +538,13 @@ __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
                 st = (st < a.H) ? (uint32_t)s_hot[st * a.C + c] : a.delta[(size_t)st * a.C + c];
                 if ((bits[st >> 5] >> (st & 31)) & 1u) {
                     for (uint32_t t = st; t != NONE; t = a.dict[t])
-                        for (uint32_t q = a.own_off[t]; q < a.own_off[t + 1]; ++q) emit_hit(a, r, a.own_ids[q], seen, nseen);
+                        for (uint32_t q = a.own_off[t]; q < a.own_off[t + 1]; ++q)
+                            emit_hit(a, sink, r, a.own_ids[q], seen, nseen);
                 }
             }
         }
     }
+    sink.flush(true);
 }
 
 // ------------------------------------------------------------------ device: literal filter
@@ -900,19 +942,23 @@ __global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
     const uint32_t nbits = (a.S + 31) / 32;
     if (a.bits_in_lds)
         for (uint32_t q = threadIdx.x; q < nbits; q += blockDim.x) s_bits[q] = a.outbits[q];
+    __shared__ unsigned long long s_hb[HS_CAP];
+    __shared__ uint32_t s_hn, s_hg;
+    if (threadIdx.x == 0) s_hn = 0;
     __syncthreads();
+    const HitSink sink{s_hb, &s_hn, &s_hg, a.hits, a.hit_count, a.cap};
     const uint32_t *bits = a.bits_in_lds ? s_bits : a.outbits;
     auto step = [&](uint32_t st, uint32_t c) -> uint32_t {
         return (st < a.H) ? (uint32_t)s_hot[st * a.C + c] : a.delta[(size_t)st * a.C + c];
     };
     auto accept = [&](uint32_t r, uint32_t st) {
         if ((bits[st >> 5] >> (st & 31)) & 1u)
-            for (uint32_t q = a.own_off[st]; q < a.own_off[st + 1]; ++q) {
-                const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
-                if (slot_i < a.cap) a.hits[slot_i] = ((unsigned long long)r << 32) | a.own_ids[q];
-            }
+            for (uint32_t q = a.own_off[st]; q < a.own_off[st + 1]; ++q)
+                sink.push(((unsigned long long)r << 32) | a.own_ids[q]);
     };
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < a.R; r += gridDim.x * blockDim.x) {
+    for (uint32_t r0 = blockIdx.x * blockDim.x; r0 < a.R; r0 += gridDim.x * blockDim.x, sink.flush(false)) {
+        const uint32_t r = r0 + threadIdx.x;
+        if (r >= a.R) continue;
         const uint2 sp_ = a.spans[r];
         const uint32_t s = sp_.x, e = sp_.y;
         uint32_t st = 1;
@@ -929,6 +975,7 @@ __global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
         }
         if (st != 0 && a.eol) accept(r, step(st, a.eol));
     }
+    sink.flush(true);
 }
 
 // Verify prefilter candidates: one thread per (record, pattern) runs that pattern's own
@@ -946,10 +993,7 @@ struct VerifyArgs {
     uint32_t cap;
 };
 
-__global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n_cand) return;
-    const unsigned long long cd = a.cand[i];
+__device__ __forceinline__ bool verify_one(const VerifyArgs &a, unsigned long long cd) {
     const uint32_t r = (uint32_t)(cd >> 32), pid = (uint32_t)cd;
     const uint32_t k = a.single_of_pid[pid];
     const uint32_t *D = a.s_delta + a.s_off[k];
@@ -971,8 +1015,25 @@ __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
         }
     }
     if (!hit && st != 0) hit = acc[D[st * C + a.s_eol[k]]] != 0;
+    return hit;
+}
+
+__global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool hit = false;
+    unsigned long long cd = 0;
+    if (i < a.n_cand) {
+        cd = a.cand[i];
+        hit = verify_one(a, cd);
+    }
+    // one global append per wave: ballot, lane 0 reserves, each hitting lane its slot
+    const uint64_t m = __ballot(hit);
+    if (!m) return;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(a.hit_count, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, 0, 64);
     if (hit) {
-        const uint32_t slot_i = atomicAdd(a.hit_count, 1u);
+        const uint32_t slot_i = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
         if (slot_i < a.cap) a.hits[slot_i] = cd;
     }
 }

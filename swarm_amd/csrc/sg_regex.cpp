@@ -747,7 +747,11 @@ struct Sum {
     std::vector<std::string> exact;
     bool fac_ok = false;
     std::vector<std::string> fac;
+    // every factor set of a concatenation's parts (score >= 3), so the plan can prefer
+    // a set that few other signatures share over the merely longest one
+    std::vector<std::vector<std::string>> alts;
 };
+constexpr size_t FAC_MAXALTS = 24;
 constexpr size_t FAC_MAXSET = 64, FAC_MAXLEN = 48;
 
 static int fac_score(const std::vector<std::string> &f) {
@@ -800,6 +804,7 @@ static Sum summarize(const Node *n) {
             bool all_exact = true;
             auto consider = [&](const std::vector<std::string> &f) {
                 if (!f.empty() && fac_score(f) > 0 && (best.empty() || better(f, best))) best = f;
+                if (fac_score(f) >= 3 && r.alts.size() < FAC_MAXALTS) r.alts.push_back(f);
             };
             for (auto &k : n->kids) {
                 Sum cs = summarize(k.get());
@@ -880,8 +885,36 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
     plan->single_of_pid.assign(n, 0xffffffffu);
     std::map<std::string, std::vector<uint32_t>> fac_map;
     std::vector<Pat *> unfiltered;
+    // candidate factor sets per pattern; how many patterns could use each string
+    std::vector<std::vector<std::vector<std::string>>> cands(n);
+    std::vector<std::vector<std::string>> eff(n);
+    std::map<std::string, uint32_t> share;
     for (auto &p : ps) {
-        std::vector<std::string> f = effective(summarize(p.ast.get()));
+        Sum sm = summarize(p.ast.get());
+        auto &cs = cands[p.id];
+        cs = sm.alts;
+        eff[p.id] = effective(sm);
+        if (!eff[p.id].empty()) cs.push_back(eff[p.id]);
+        for (auto &f : cs) dedupe(f);
+        std::sort(cs.begin(), cs.end());
+        cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+        std::vector<std::string> mine;
+        for (auto &f : cs) mine.insert(mine.end(), f.begin(), f.end());
+        dedupe(mine);
+        for (auto &x : mine) share[x]++;
+    }
+    for (auto &p : ps) {
+        // the least shared set (max over its strings of the number of patterns that could
+        // use them), then the longest; the effective set when nothing scores >= 3
+        std::vector<std::string> f = eff[p.id];
+        uint64_t best_cost = ~0ull;
+        for (auto &c : cands[p.id]) {
+            if (fac_score(c) < 3) continue;
+            uint32_t worst = 0;
+            for (auto &x : c) worst = std::max(worst, share[x]);
+            const uint64_t cost = ((uint64_t)worst << 32) | (uint32_t)(0x7fffffff - fac_score(c));
+            if (cost < best_cost) { best_cost = cost; f = c; }
+        }
         const bool had = !f.empty();
         // a factor holding '\n' can never occur inside a record: drop it
         f.erase(std::remove_if(f.begin(), f.end(), [](const std::string &s) { return s.find('\n') != std::string::npos; }),

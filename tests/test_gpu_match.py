@@ -185,3 +185,17 @@ def test_literal_tile_edges(sg, nocase):
     m = sg.Matcher(sigs, "literal", nocase=nocase)
     assert m.match(data) == S.literal_hits(data, sigs, nocase=nocase)
     assert m.match(data + b"\n") == S.literal_hits(data + b"\n", sigs, nocase=nocase)
+
+
+def test_regex_c4_banners_full_signature_set(sg):
+    """C4 shape: nmap-style banners against the full ~10k regex set (corpus regexes +
+    synthetic nmap `match` families), bit-exact vs re.search on a sample."""
+    from swarm_amd import corpus
+    pats = REGEXES + corpus.nmap_signatures()
+    pool = corpus.banner_pool(pool=400, seed=21)
+    data = b"\n".join(pool) + b"\n"
+    m = sg.Matcher(pats, "regex")
+    got = m.match(data)
+    exp = S.regex_hits(data, pats)
+    assert got == exp
+    assert len(exp) > 50
