@@ -38,6 +38,8 @@ struct sg_matcher {
         std::vector<uint32_t> dict;     // AC: next state on the suffix chain with output
         std::vector<uint32_t> outbits;  // (n_states + 31) / 32
         uint32_t anchored_eol = 0;      // DFA: class used for the end-of-record step (0 = none)
+        std::vector<uint32_t> gpids;    // DFA: group-local pattern -> signature id (<= 64)
+        std::vector<uint64_t> omask;    // DFA: per state, group-local patterns accepted on entry
     };
     std::vector<Table> tables;
     uint64_t total_states = 0;
@@ -59,6 +61,8 @@ struct sg_matcher {
         uint32_t *delta = nullptr, *own_off = nullptr, *own_ids = nullptr, *dict = nullptr, *outbits = nullptr;
         uint16_t *hot = nullptr;  // first H rows as u16 (if n_states <= 65535)
         uint8_t *cls = nullptr;
+        uint64_t *omask = nullptr;
+        uint32_t *gpids = nullptr;
         uint32_t H = 0;
     };
     std::vector<DevTable> dtabs;
@@ -247,7 +251,7 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
                 b = 8 * (c + 1);
             } else {
                 b = 10;
-                static const uint32_t cap4 = getenv("SG_LIT_BITS4") ? (uint32_t)atoi(getenv("SG_LIT_BITS4")) : 16u;
+                static const uint32_t cap4 = getenv("SG_LIT_BITS4") ? (uint32_t)atoi(getenv("SG_LIT_BITS4")) : 18u;
                 while (b < (c == 2 ? 15u : cap4) && (1ull << b) < 64ull * cnt[c]) ++b;
             }
         }
@@ -363,6 +367,7 @@ static void free_dev(sg_matcher *h) {
     for (auto &d : h->dtabs) {
         (void)hipFree(d.delta); (void)hipFree(d.own_off); (void)hipFree(d.own_ids); (void)hipFree(d.dict);
         (void)hipFree(d.outbits); (void)hipFree(d.hot); (void)hipFree(d.cls);
+        (void)hipFree(d.omask); (void)hipFree(d.gpids);
     }
     h->dtabs.clear();
     auto &p = h->dplan;
@@ -420,6 +425,12 @@ static int ensure_device(sg_matcher *h, int dev) {
         SG_TRY(upload_vec(T.own_ids, &d.own_ids));
         SG_TRY(upload_vec(T.dict, &d.dict));
         SG_TRY(upload_vec(T.outbits, &d.outbits));
+        if (!T.omask.empty()) {
+            std::vector<uint32_t> gp(64, 0);
+            std::copy(T.gpids.begin(), T.gpids.end(), gp.begin());
+            SG_TRY(upload_vec(T.omask, &d.omask));
+            SG_TRY(upload_vec(gp, &d.gpids));
+        }
         std::vector<uint8_t> cls(T.cls, T.cls + 256);
         SG_TRY(upload_vec(cls, &d.cls));
         uint32_t H = 0;
@@ -921,17 +932,25 @@ struct DFAArgs {
     const uint32_t *delta;
     const uint16_t *hot;
     uint32_t C, H, S, eol;
-    const uint32_t *outbits, *own_off, *own_ids;
+    const uint32_t *outbits;
+    const unsigned long long *omask;  // per state: group-local patterns accepted on entry
+    const uint32_t *gpids;            // group-local pattern -> signature id (<= 64)
     unsigned long long *hits;
     uint32_t *hit_count;
     uint32_t cap;
     uint32_t bits_in_lds;
 };
 
-// One DFA of a set. State 0 = dead (no pattern can still match), state 1 = start. A state
-// with output accepts the listed patterns; accepted patterns are removed from the
-// successor states at build time, so each pattern is reported once per record.
-__global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
+constexpr int DFA_BLOCK = 512;
+
+// One DFA of a set (<= 64 patterns). State 0 = dead (no pattern can still match), state
+// 1 = start. A state with output accepts a mask of group-local patterns; accepted
+// patterns are removed from the successor states at build time. One thread walks one
+// record, OR-ing the accept masks into a register; the block then appends all of its
+// records' hits at once (block scan of the popcounts -> LDS staging buffer, one global
+// atomic per drain), so generic signatures that fire on every banner cost no contended
+// atomics at all.
+__global__ __launch_bounds__(DFA_BLOCK) void k_dfa_match(DFAArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint8_t *s_cls = lds;
     uint16_t *s_hot = reinterpret_cast<uint16_t *>(lds + 256);
@@ -943,7 +962,10 @@ __global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
     if (a.bits_in_lds)
         for (uint32_t q = threadIdx.x; q < nbits; q += blockDim.x) s_bits[q] = a.outbits[q];
     __shared__ unsigned long long s_hb[HS_CAP];
+    __shared__ uint32_t s_gp[64];
+    __shared__ uint32_t s_red[DFA_BLOCK / 64];
     __shared__ uint32_t s_hn, s_hg;
+    if (threadIdx.x < 64) s_gp[threadIdx.x] = a.gpids[threadIdx.x];
     if (threadIdx.x == 0) s_hn = 0;
     __syncthreads();
     const HitSink sink{s_hb, &s_hn, &s_hg, a.hits, a.hit_count, a.cap};
@@ -951,29 +973,53 @@ __global__ __launch_bounds__(512) void k_dfa_match(DFAArgs a) {
     auto step = [&](uint32_t st, uint32_t c) -> uint32_t {
         return (st < a.H) ? (uint32_t)s_hot[st * a.C + c] : a.delta[(size_t)st * a.C + c];
     };
-    auto accept = [&](uint32_t r, uint32_t st) {
-        if ((bits[st >> 5] >> (st & 31)) & 1u)
-            for (uint32_t q = a.own_off[st]; q < a.own_off[st + 1]; ++q)
-                sink.push(((unsigned long long)r << 32) | a.own_ids[q]);
+    unsigned long long acc = 0;
+    auto accept = [&](uint32_t st) {
+        if ((bits[st >> 5] >> (st & 31)) & 1u) acc |= a.omask[st];
     };
-    for (uint32_t r0 = blockIdx.x * blockDim.x; r0 < a.R; r0 += gridDim.x * blockDim.x, sink.flush(false)) {
+    for (uint32_t r0 = blockIdx.x * DFA_BLOCK; r0 < a.R; r0 += gridDim.x * DFA_BLOCK) {
         const uint32_t r = r0 + threadIdx.x;
-        if (r >= a.R) continue;
-        const uint2 sp_ = a.spans[r];
-        const uint32_t s = sp_.x, e = sp_.y;
-        uint32_t st = 1;
-        accept(r, st);
-        for (uint32_t w = s & ~3u; w < e && st != 0; w += 4) {
-            const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
+        acc = 0;
+        if (r < a.R) {
+            const uint2 sp_ = a.spans[r];
+            const uint32_t s = sp_.x, e = sp_.y;
+            uint32_t st = 1;
+            accept(st);
+            for (uint32_t w = s & ~3u; w < e && st != 0; w += 4) {
+                const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
 #pragma unroll
-            for (uint32_t b = 0; b < 4; ++b) {
-                const uint32_t p = w + b;
-                if (p < s || p >= e || st == 0) continue;
-                st = step(st, s_cls[(x >> (8 * b)) & 0xffu]);
-                accept(r, st);
+                for (uint32_t b = 0; b < 4; ++b) {
+                    const uint32_t p = w + b;
+                    if (p < s || p >= e || st == 0) continue;
+                    st = step(st, s_cls[(x >> (8 * b)) & 0xffu]);
+                    accept(st);
+                }
             }
+            if (st != 0 && a.eol) accept(step(st, a.eol));
         }
-        if (st != 0 && a.eol) accept(r, step(st, a.eol));
+        // block-uniform append of this round's hits
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<DFA_BLOCK>((uint32_t)__popcll(acc), &tot, s_red);
+        if (tot == 0) continue;
+        if (s_hn + tot > HS_CAP) sink.flush(true);
+        unsigned long long *dst;
+        if (tot > HS_CAP) {
+            if (threadIdx.x == 0) s_hg = atomicAdd(a.hit_count, tot);
+            __syncthreads();
+            const uint32_t g = s_hg;
+            for (unsigned long long m = acc, k = 0; m; m &= m - 1, ++k) {
+                const uint32_t q = g + ex + (uint32_t)k;
+                if (q < a.cap) a.hits[q] = ((unsigned long long)r << 32) | s_gp[__ffsll((long long)m) - 1];
+            }
+            __syncthreads();
+            continue;
+        }
+        dst = s_hb + s_hn + ex;
+        for (unsigned long long m = acc; m; m &= m - 1)
+            *dst++ = ((unsigned long long)r << 32) | s_gp[__ffsll((long long)m) - 1];
+        __syncthreads();
+        if (threadIdx.x == 0) s_hn += tot;
+        __syncthreads();
     }
     sink.flush(true);
 }
@@ -1171,8 +1217,9 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
                     SG_LAUNCH_B(c, "ac_match", (double)n + 8.0 * R, k_ac_match, grid, 512, lds, a);
                 } else {
                     DFAArgs a{d_buf, L.spans, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
-                              T.anchored_eol, D.outbits, D.own_off, D.own_ids, hits, cnt, (uint32_t)cap, bits_in_lds};
-                    SG_LAUNCH_B(c, "dfa_match", (double)n + 8.0 * R, k_dfa_match, grid, 512, lds, a);
+                              T.anchored_eol, D.outbits, reinterpret_cast<const unsigned long long *>(D.omask), D.gpids,
+                              hits, cnt, (uint32_t)cap, bits_in_lds};
+                    SG_LAUNCH_B(c, "dfa_match", (double)n + 8.0 * R, k_dfa_match, grid, DFA_BLOCK, lds, a);
                 }
             }
             if (n_cand) {
@@ -1304,6 +1351,14 @@ int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pat
         T.outbits.assign((T.n_states + 31) / 32, 0);
         for (uint32_t s = 0; s < T.n_states; ++s)
             if (T.own_off[s + 1] > T.own_off[s]) T.outbits[s / 32] |= 1u << (s % 32);
+        // group-local pattern numbering for the per-thread accept mask
+        std::map<uint32_t, uint32_t> local;
+        for (uint32_t id : T.own_ids) local.emplace(id, 0u);
+        if (local.size() > 64) { delete m; set_error("regex group holds more than 64 patterns"); return SG_E_STATES; }
+        for (auto &kv : local) { kv.second = (uint32_t)T.gpids.size(); T.gpids.push_back(kv.first); }
+        T.omask.assign(T.n_states, 0);
+        for (uint32_t s = 0; s < T.n_states; ++s)
+            for (uint32_t q = T.own_off[s]; q < T.own_off[s + 1]; ++q) T.omask[s] |= 1ull << local[T.own_ids[q]];
         m->total_states += T.n_states;
         m->tables.push_back(std::move(T));
     }

@@ -2,6 +2,8 @@
 #include "sg_regex.hpp"
 
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -719,10 +721,12 @@ static int build_group(const std::vector<Pat *> &ps, uint32_t budget, RegexDFA *
     }
 }
 
+// Groups hold at most 64 patterns (the matcher keeps a per-record accept mask in one
+// 64-bit register) and at most `budget` states.
 static int build_split(std::vector<Pat *> ps, uint32_t budget, std::vector<RegexDFA> *out) {
     RegexDFA d;
     bool fits = false;
-    int rc = build_group(ps, budget, &d, &fits);
+    int rc = ps.size() <= 64 ? build_group(ps, budget, &d, &fits) : SG_OK;
     if (rc != SG_OK) return rc;
     if (fits) {
         out->push_back(std::move(d));
@@ -946,7 +950,18 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         plan->fac_pids.insert(plan->fac_pids.end(), ids.begin(), ids.end());
         plan->fac_off.push_back((uint32_t)plan->fac_pids.size());
     }
-    if (!unfiltered.empty()) return build_split(unfiltered, 4096, &plan->groups);
+    if (getenv("SG_REGEX_DEBUG")) {
+        fprintf(stderr, "[regex plan] %zu filtered, %zu factors, %zu unfiltered:", plan->singles.size(),
+                plan->factors.size(), unfiltered.size());
+        for (Pat *p : unfiltered) fprintf(stderr, " %u", p->id);
+        fprintf(stderr, "\n");
+    }
+    if (!unfiltered.empty()) {
+        int rc = build_split(unfiltered, 4096, &plan->groups);
+        if (rc == SG_OK && getenv("SG_REGEX_DEBUG"))
+            for (auto &g : plan->groups) fprintf(stderr, "[regex plan] group states=%u classes=%u\n", g.n_states, g.n_classes);
+        return rc;
+    }
     return SG_OK;
 }
 
