@@ -156,6 +156,46 @@ typedef struct sg_dev_hits {
 int sg_dev_match(sg_ctx *ctx, sg_matcher *h, const uint8_t *d_buf, size_t n, sg_dev_hits *res);
 void sg_free(void *h);  /* frees an sg_matcher */
 
+/* ------------------------------------------------------------------ module-output formats
+ * the worker's module outputs (worker/modules/<name>.json:2) turned
+ * into records on the GPU before matching (A4) and dedup (A7). */
+typedef struct sg_dev_text {
+    const uint8_t *data;      /* device: '\n'-terminated records (context-owned) */
+    uint64_t bytes;
+    uint64_t records;
+    uint64_t in_records;      /* non-empty input lines */
+} sg_dev_text;
+/* nmap -oN (worker/modules/nmap.json:2) -> "host:port" records, one per open port, in
+ * input order. Host = the text after "Nmap scan report for " up to the first space (the
+ * name when nmap prints "NAME (IP)", else the address); an open-port line matches
+ * [0-9]{1,5}/(tcp|udp|sctp)[ \t]+open([ \t]|$) at the start of a line; port lines before
+ * any report line are dropped. */
+int sg_nmap_ports(const uint8_t *buf, size_t n, uint8_t *out, size_t cap, size_t *out_n);
+int sg_dev_nmap_ports(sg_ctx *ctx, const uint8_t *d_buf, size_t n, sg_dev_text *res);
+
+typedef struct sg_dev_rows {
+    const uint8_t *data;      /* device: rows, each '\n'-terminated (a line buffer) */
+    uint64_t bytes;
+    uint64_t rows;
+    const uint32_t *row_rec;  /* device: input record of each row */
+    const uint32_t *row_key;  /* device: requested-key index of each row */
+    uint64_t in_records;
+} sg_dev_rows;
+/* httpx -json (worker/modules/http2.json:2, web.json:2) -> field rows. For every input
+ * line that is one JSON object, and for each requested top-level key present (last
+ * duplicate wins, as json.loads): a string value is one row of its decoded bytes (UTF-8;
+ * a decoded newline is written as the two bytes '\' 'n'); an array value is one row per
+ * element (strings decoded, other elements as their raw text); any other value is its raw
+ * text. Empty rows are dropped. Rows are ordered by record, then key index, then element.
+ * Lines that are not a single JSON object produce no rows. keys: n_keys (<= 64) names,
+ * key i = keys[key_offs[i] .. key_offs[i+1]), total <= 4096 bytes, no characters that
+ * need JSON escaping. */
+int sg_json_fields(const uint8_t *buf, size_t n, const uint8_t *keys, const uint32_t *key_offs,
+                   uint32_t n_keys, uint8_t *out, size_t cap, size_t *out_n,
+                   uint32_t *row_rec, uint32_t *row_key, size_t rows_cap, size_t *n_rows);
+int sg_dev_json_fields(sg_ctx *ctx, const uint8_t *d_buf, size_t n, const uint8_t *keys,
+                       const uint32_t *key_offs, uint32_t n_keys, sg_dev_rows *res);
+
 #ifdef __cplusplus
 }
 #endif

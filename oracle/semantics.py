@@ -162,3 +162,217 @@ def hash_partition(records: Iterable[bytes], n_parts: int, hash_fn) -> List[List
     for r in records:
         parts[hash_fn(r) % n_parts].append(r)
     return parts
+
+
+# ----------------------------------------------------------------------------- §8(f)2 nmap -oN
+# worker/modules/nmap.json:2 runs `nmap ... -oN {output}`; the reference uploads the text
+# verbatim (worker/worker.py:96-98). The build turns it into C5-style host:port records.
+_NMAP_REPORT = b"Nmap scan report for "
+_NMAP_PORT = re.compile(rb"([0-9]{1,5})/(?:tcp|udp|sctp)[ \t]+open(?:[ \t]|$)")
+
+
+def nmap_host_ports(buf: bytes) -> bytes:
+    """One 'host:port' record per open-port line, in input order ('\\n'-terminated). host =
+    the report line's text after 'Nmap scan report for ' up to the first space; port lines
+    before any report line, or under a report with an empty host, are dropped."""
+    host = None
+    out = []
+    for rec in parse_records(buf):
+        if rec.startswith(_NMAP_REPORT):
+            host = rec[len(_NMAP_REPORT):].split(b" ", 1)[0]
+            continue
+        m = _NMAP_PORT.match(rec)
+        if m and host:
+            out.append(host + b":" + m.group(1))
+    return serialize(out)
+
+
+# ----------------------------------------------------------------------------- §8(f)1 httpx -json
+# worker/modules/http2.json:2 / web.json:2 run `httpx ... -json`: one JSON object per line.
+# Byte-level restatement of json.loads for top-level member lookup (last duplicate wins)
+# and string decoding; tests pin it against json.loads on valid lines.
+_JWS = b" \t\r\n"
+
+
+def _json_members(rec: bytes):
+    """[(raw key, value start, value end)] of a line holding exactly one JSON object, or
+    None (structural check: one top-level object, balanced strings/brackets, only
+    whitespace around it)."""
+    depth = 0
+    in_str = esc = False
+    done = False
+    str_s = str_e = val_s = 0
+    cur = None
+    first = last = open_pos = close_pos = None
+    members = []
+    for i, ch in enumerate(rec):
+        if ch not in _JWS:
+            if first is None:
+                first = i
+            last = i
+        if in_str:
+            if esc:
+                esc = False
+            elif ch == 0x5C:
+                esc = True
+            elif ch == 0x22:
+                in_str = False
+                str_e = i
+            continue
+        if ch == 0x22:
+            if depth == 0:
+                return None
+            in_str = True
+            str_s = i + 1
+        elif ch in b"{[:,}]" and done:
+            return None
+        elif ch in b"{[":
+            if depth == 0:
+                if ch != 0x7B:
+                    return None
+                open_pos = i
+            depth += 1
+        elif ch in b"}]":
+            if depth == 0:
+                return None
+            if depth == 1:
+                if ch != 0x7D:
+                    return None
+                if cur is not None:
+                    members.append((cur, val_s, i))
+                cur = None
+                done = True
+                close_pos = i
+            depth -= 1
+        elif ch == 0x3A and depth == 1:
+            cur = rec[str_s:str_e]
+            val_s = i + 1
+        elif ch == 0x2C and depth == 1:
+            if cur is not None:
+                members.append((cur, val_s, i))
+            cur = None
+    if in_str or depth or not done or first != open_pos or last != close_pos:
+        return None
+    return members
+
+
+def _json_put_cp(out: bytearray, cp: int) -> None:
+    if cp == 0x0A:
+        out += b"\\n"  # a row stays one line
+    else:
+        out += chr(cp).encode("utf-8", "surrogatepass")
+
+
+def json_decode_string(s: bytes) -> bytes:
+    """JSON string body (between the quotes) -> bytes, as json.loads + UTF-8 encoding
+    ('surrogatepass' for lone surrogates), newline written as backslash-n."""
+    out = bytearray()
+    p, n = 0, len(s)
+    hexd = b"0123456789abcdefABCDEF"
+
+    def u4(q):
+        if q + 4 > n or any(c not in hexd for c in s[q:q + 4]):
+            return None
+        return int(s[q:q + 4], 16)
+
+    simple = {0x22: b'"', 0x5C: b"\\", 0x2F: b"/", 0x62: b"\x08", 0x66: b"\x0c", 0x6E: b"\\n", 0x72: b"\r",
+              0x74: b"\t"}
+    while p < n:
+        ch = s[p]
+        if ch != 0x5C or p + 1 >= n:
+            out.append(ch)
+            p += 1
+            continue
+        e = s[p + 1]
+        if e in simple:
+            out += simple[e]
+            p += 2
+        elif e == 0x75:
+            v = u4(p + 2)
+            if v is None:
+                out.append(ch)
+                p += 1
+                continue
+            p += 6
+            if 0xD800 <= v < 0xDC00 and p + 1 < n and s[p] == 0x5C and s[p + 1] == 0x75:
+                lo = u4(p + 2)
+                if lo is not None and 0xDC00 <= lo < 0xE000:
+                    v = 0x10000 + ((v - 0xD800) << 10) + (lo - 0xDC00)
+                    p += 6
+            _json_put_cp(out, v)
+        else:
+            out.append(ch)
+            p += 1
+    return bytes(out)
+
+
+def _json_trim(v: bytes) -> bytes:
+    return v.strip(_JWS)
+
+
+def _json_item(v: bytes) -> List[bytes]:
+    v = _json_trim(v)
+    if not v:
+        return []
+    if len(v) >= 2 and v[0] == 0x22 and v[-1] == 0x22:
+        return [json_decode_string(v[1:-1])] if len(v) > 2 else []
+    return [v]
+
+
+def json_value_rows(v: bytes) -> List[bytes]:
+    """Rows of one member value: a string -> its decoded bytes; an array -> one row per
+    element (strings decoded, others raw); anything else -> its raw text. Empty rows are
+    dropped."""
+    v = _json_trim(v)
+    if not v:
+        return []
+    if v[0] != 0x5B:
+        return _json_item(v)
+    rows: List[bytes] = []
+    depth = 0
+    start = 1
+    in_str = esc = False
+    for p, ch in enumerate(v):
+        if in_str:
+            if esc:
+                esc = False
+            elif ch == 0x5C:
+                esc = True
+            elif ch == 0x22:
+                in_str = False
+            continue
+        if ch == 0x22:
+            in_str = True
+        elif ch in b"[{":
+            depth += 1
+        elif ch in b"]}":
+            if depth == 1:
+                rows += _json_item(v[start:p])
+                start = p + 1
+            depth -= 1
+        elif ch == 0x2C and depth == 1:
+            rows += _json_item(v[start:p])
+            start = p + 1
+    return rows
+
+
+def json_field_rows(buf: bytes, keys: Sequence[bytes]) -> Tuple[bytes, List[int], List[int]]:
+    """(rows '\\n'-terminated, record index per row, key index per row): for each record
+    (A3 order) holding one JSON object, each requested key in request order, the rows of
+    its last occurrence."""
+    rows, rrec, rkey = [], [], []
+    for ri, rec in enumerate(parse_records(buf)):
+        mem = _json_members(rec)
+        if mem is None:
+            continue
+        last = {}
+        for k, s, e in mem:
+            last[k] = (s, e)
+        for ki, k in enumerate(keys):
+            if k in last:
+                s, e = last[k]
+                for row in json_value_rows(rec[s:e]):
+                    rows.append(row)
+                    rrec.append(ri)
+                    rkey.append(ki)
+    return serialize(rows), rrec, rkey

@@ -29,6 +29,7 @@ EXPORTS = [
     "sg_dedup", "sg_dedup_chunks", "sg_diff", "sg_dedup_diff", "sg_dev_dedup_diff",
     "sg_dev_partition", "sg_hash64", "sg_ac_compile", "sg_dfa_compile", "sg_matcher_info",
     "sg_match", "sg_match_lines", "sg_dev_match", "sg_free",
+    "sg_nmap_ports", "sg_dev_nmap_ports", "sg_json_fields", "sg_dev_json_fields",
 ]
 
 
@@ -48,6 +49,15 @@ class DevHits(C.Structure):
     _fields_ = [("rec_idx", C.c_void_p), ("sig_id", C.c_void_p), ("n_hits", C.c_uint64),
                 ("lines", C.c_void_p), ("lines_bytes", C.c_uint64), ("matched_records", C.c_uint64),
                 ("in_records", C.c_uint64)]
+
+
+class DevText(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("bytes", C.c_uint64), ("records", C.c_uint64), ("in_records", C.c_uint64)]
+
+
+class DevRows(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("bytes", C.c_uint64), ("rows", C.c_uint64), ("row_rec", C.c_void_p),
+                ("row_key", C.c_void_p), ("in_records", C.c_uint64)]
 
 
 def _load():
@@ -93,6 +103,10 @@ def _load():
         "sg_match_lines": (C.c_int, [P, U8P, SZ, U8P, SZ, SZP]),
         "sg_dev_match": (C.c_int, [P, P, P, SZ, C.POINTER(DevHits)]),
         "sg_free": (None, [P]),
+        "sg_nmap_ports": (C.c_int, [U8P, SZ, U8P, SZ, SZP]),
+        "sg_dev_nmap_ports": (C.c_int, [P, P, SZ, C.POINTER(DevText)]),
+        "sg_json_fields": (C.c_int, [U8P, SZ, U8P, U32P, C.c_uint32, U8P, SZ, SZP, U32P, U32P, SZ, SZP]),
+        "sg_dev_json_fields": (C.c_int, [P, P, SZ, U8P, U32P, C.c_uint32, C.POINTER(DevRows)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

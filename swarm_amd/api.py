@@ -6,6 +6,8 @@ These are the functions the reference-side worker.py / server.py call (INTEGRATI
   diff(cur, prior)           A8  new records vs the prior scan      (README.md:11)
   dedup_diff(cur, prior)     A9  scan-completion step               (server/server.py:274-294)
   Matcher                    A4  literal (Aho-Corasick) / regex (DFA) signature matching
+  nmap_ports(buf)            §8(f)2 nmap -oN -> host:port records  (worker/modules/nmap.json:2)
+  json_fields(buf, keys)     §8(f)1 httpx -json -> field rows      (worker/modules/http2.json:2)
   Context                    device-resident path (HBM inputs, per-kernel timing)
 
 Every call runs the HIP kernels; there is no CPU fallback. Inputs are bytes-like or numpy
@@ -163,6 +165,48 @@ class Matcher:
         return r
 
 
+def nmap_ports(buf) -> bytes:
+    """nmap -oN text -> 'host:port' records (one per open port, input order), each
+    '\n'-terminated (include/swarmgpu.h sg_nmap_ports)."""
+    a = _view(buf)
+    cap = 2 * a.size + 64
+    while True:
+        out = np.empty(cap, dtype=np.uint8)
+        n = C.c_size_t(0)
+        rc = lib.sg_nmap_ports(_ptr(a), a.size, out.ctypes.data, out.size, C.byref(n))
+        if rc == _abi.SG_E_CAP:
+            cap = n.value
+            continue
+        check(rc)
+        return out[: n.value].tobytes()
+
+
+def _keys_blob(keys: Sequence[bytes]):
+    ks = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+    blob = np.frombuffer(b"".join(ks) or b"\0", dtype=np.uint8)
+    offs = np.zeros(len(ks) + 1, dtype=np.uint32)
+    np.cumsum([len(k) for k in ks], out=offs[1:])
+    return blob, offs
+
+
+def json_fields(buf, keys: Sequence[bytes]) -> Tuple[bytes, np.ndarray, np.ndarray]:
+    """httpx -json lines -> (rows, row_rec, row_key): '\n'-terminated decoded values of the
+    requested top-level keys (include/swarmgpu.h sg_json_fields), the input record and
+    key index of each row."""
+    a = _view(buf)
+    blob, offs = _keys_blob(keys)
+    cap, rcap = a.size + 64, a.size // 2 + 64
+    out = np.empty(cap, dtype=np.uint8)
+    rrec = np.empty(rcap, dtype=np.uint32)
+    rkey = np.empty(rcap, dtype=np.uint32)
+    n, nr = C.c_size_t(0), C.c_size_t(0)
+    U32P = C.POINTER(C.c_uint32)
+    check(lib.sg_json_fields(_ptr(a), a.size, blob.ctypes.data, offs.ctypes.data_as(U32P), len(offs) - 1,
+                             out.ctypes.data, cap, C.byref(n), rrec.ctypes.data_as(U32P), rkey.ctypes.data_as(U32P),
+                             rcap, C.byref(nr)))
+    return out[: n.value].tobytes(), rrec[: nr.value].copy(), rkey[: nr.value].copy()
+
+
 def hash64(rec: bytes) -> int:
     a = _view(rec)
     return int(lib.sg_hash64(_ptr(a), a.size))
@@ -231,6 +275,18 @@ class Context:
         r = _abi.DevResult()
         check(lib.sg_dev_dedup_diff(self._h, C.c_void_p(d_cur), n_cur,
                                     C.c_void_p(d_prior) if d_prior else None, n_prior, C.byref(r)))
+        return r
+
+    def nmap_ports(self, d_buf: int, n: int) -> _abi.DevText:
+        r = _abi.DevText()
+        check(lib.sg_dev_nmap_ports(self._h, C.c_void_p(d_buf), n, C.byref(r)))
+        return r
+
+    def json_fields(self, d_buf: int, n: int, keys: Sequence[bytes]) -> _abi.DevRows:
+        blob, offs = _keys_blob(keys)
+        r = _abi.DevRows()
+        check(lib.sg_dev_json_fields(self._h, C.c_void_p(d_buf), n, blob.ctypes.data,
+                                     offs.ctypes.data_as(C.POINTER(C.c_uint32)), len(offs) - 1, C.byref(r)))
         return r
 
     def partition(self, d_buf: int, n: int, n_parts: int, d_out: int, out_cap: int):

@@ -246,3 +246,94 @@ def banner_pool(n_products: int = 1100, pool: int = 1 << 16, match_frac: float =
         v = b"%d.%d.%d" % (rng.integers(10), rng.integers(20), rng.integers(30))
         rows.append(fam.replace(b"{p}", p).replace(b"{v}", v).replace(b"{b}", b"%d" % rng.integers(100000)))
     return rows
+
+
+# ------------------------------------------------------------------ §8(f): module-output formats
+_TECH = [b"Nginx:1.18.0", b"PHP:7.4.3", b"jQuery", b"Bootstrap:4.5.2", b"WordPress:5.8", b"Cloudflare", b"React",
+         b"Amazon S3", b"Apache HTTP Server:2.4.41", b"Ubuntu", b"Google Font API", b"Font Awesome", b"HSTS",
+         b"Varnish", b"Express", b"Node.js", b"Jenkins:2.303", b"Grafana:8.1.2", b"Kibana", b"GitLab"]
+_UNI = ["\u00e9t\u00e9", "\u65e5\u672c\u8a9e", "\U0001F600 smile", "caf\u00e9 \u2014 menu", "\u0414\u043e\u043c"]
+
+
+def httpx_json_pool(pool: int = 1 << 12, seed: int = 5) -> list:
+    """httpx -json result lines (the keys and value shapes httpx v1 prints), serialized the
+    way Go's encoding/json does (HTML characters escaped as \\u003c etc., non-ASCII kept)."""
+    import json
+    import random
+    rng = random.Random(seed)
+    rows = []
+    for _ in range(pool):
+        host = "%s.target%d.com" % ("".join(rng.choice("abcdefghijklmnopqrstuvwxyz0123456789")
+                                           for _ in range(rng.randint(3, 12))), rng.randrange(64))
+        scheme = rng.choice(["http", "https"])
+        port = {"http": "80", "https": "443"}[scheme]
+        title = rng.choice(TITLES).decode()
+        r = rng.random()
+        if r < 0.1:
+            title = rng.choice(_UNI)
+        elif r < 0.15:
+            title = title + ' <b>"quoted"</b> & \\ back'
+        elif r < 0.17:
+            title = "line1\nline2\ttab"
+        elif r < 0.19:
+            title = ""
+        obj = {
+            "timestamp": "2026-10-12T10:%02d:%02d.%06d+00:00" % (rng.randrange(60), rng.randrange(60),
+                                                                 rng.randrange(10 ** 6)),
+            "hash": {"body_md5": "%032x" % rng.getrandbits(128), "header_md5": "%032x" % rng.getrandbits(128)},
+            "port": port,
+            "url": "%s://%s" % (scheme, host),
+            "input": host,
+            "title": title,
+            "scheme": scheme,
+            "webserver": rng.choice(SERVERS).decode(),
+            "content_type": rng.choice(["text/html", "application/json", "text/plain"]),
+            "method": "GET",
+            "host": "%d.%d.%d.%d" % tuple(rng.randrange(256) for _ in range(4)),
+            "path": "/",
+            "time": "%.6fms" % (rng.random() * 900),
+            "a": ["%d.%d.%d.%d" % tuple(rng.randrange(256) for _ in range(4)) for _ in range(rng.randint(1, 3))],
+            "tech": [t.decode() for t in rng.sample(_TECH, rng.randint(0, 4))],
+            "words": rng.randrange(5000),
+            "lines": rng.randrange(500),
+            "status_code": rng.choice([200, 301, 302, 403, 404, 500]),
+            "content_length": rng.randrange(100000),
+            "failed": False,
+            "knowledgebase": {"PageType": "nonerror", "pHash": 0},
+        }
+        if rng.random() < 0.3:
+            del obj["tech"]
+        s = json.dumps(obj, ensure_ascii=False, separators=(",", ":"))
+        s = s.replace("<", "\\u003c").replace(">", "\\u003e").replace("&", "\\u0026")
+        rows.append(s.encode("utf-8"))
+    return rows
+
+
+def nmap_report(n_hosts: int, seed: int = 11, max_ports: int = 6) -> bytes:
+    """nmap -sV -oN text for n_hosts hosts (header, per-host report, port table, footer)."""
+    import random
+    rng = random.Random(seed)
+    svc = [(22, b"ssh", b"OpenSSH 8.2p1 Ubuntu 4ubuntu0.5 (Ubuntu Linux; protocol 2.0)"),
+           (25, b"smtp", b"Postfix smtpd"), (53, b"domain", b"ISC BIND 9.16.1"), (80, b"http", b"nginx 1.18.0"),
+           (443, b"ssl/http", b"nginx 1.18.0"), (3306, b"mysql", b"MySQL 5.7.33"),
+           (8080, b"http-proxy", b""), (8443, b"ssl/https-alt", b"")]
+    out = [b"# Nmap 7.80 scan initiated Mon Oct 12 10:00:00 2026 as: nmap -sV -iL input -oN output"]
+    for h in range(n_hosts):
+        name = b"h%d.target%d.com" % (rng.randrange(10 ** 6), rng.randrange(64))
+        ip = b"%d.%d.%d.%d" % tuple(rng.randrange(256) for _ in range(4))
+        out.append(b"Nmap scan report for %s (%s)" % (name, ip) if rng.random() < 0.8
+                   else b"Nmap scan report for %s" % ip)
+        out.append(b"Host is up (0.0%dms latency)." % rng.randrange(100))
+        out.append(b"Not shown: 996 filtered ports")
+        out.append(b"PORT     STATE  SERVICE  VERSION")
+        for port, name_, ver in rng.sample(svc, rng.randint(0, max_ports)):
+            state = rng.choice([b"open", b"open", b"open", b"closed", b"filtered"])
+            proto = b"tcp" if port != 53 or rng.random() < 0.5 else b"udp"
+            out.append(b"%s/%s %s %s %s" % (b"%d" % port, proto, state, name_, ver))
+        if rng.random() < 0.3:
+            out.append(b"Service Info: OS: Linux; CPE: cpe:/o:linux:linux_kernel")
+        out.append(b"")
+    out.append(b"Service detection performed. Please report any incorrect results at https://nmap.org/submit/ .")
+    out.append(b"# Nmap done at Mon Oct 12 10:05:00 2026 -- %d IP addresses (%d hosts up) scanned in 300.00 seconds"
+               % (n_hosts, n_hosts))
+    return b"\n".join(out) + b"\n"

@@ -1,0 +1,599 @@
+// sg_formats.hip — module-output formats on the GPU:
+//
+//   * nmap -oN  -> host:port records (worker/modules/nmap.json:2). Each record is one
+//     line; a "Nmap scan report for HOST ..." line sets the host for the open-port lines
+//     ("PORT/tcp open ...") that follow it. Classification is a two-predicate compaction
+//     (report lines, open-port lines), each port finds its report by a binary search over
+//     the report list (the last report before it), and the records are written with an
+//     exclusive scan of their lengths. Output feeds A7 dedup unchanged (C5-style records).
+//
+//   * httpx -json -> field rows (worker/modules/http2.json:2, web.json:2). One wave per
+//     JSON line walks the structural characters of 64-byte chunks: the chunk's quote,
+//     backslash, bracket, colon and comma bytes become wave ballots (u64 masks), and the
+//     wave iterates over those events with scalar (wave-uniform) state, so the escaped-
+//     quote test, string state and depth cost a few SALU ops per event, not per byte.
+//     Colons at depth 1 name a top-level key; lane k of the wave owns requested key k and
+//     keeps the span of its last occurrence (json.loads keeps the last duplicate). Each
+//     lane then measures its value (string decode length, array elements) and the rows
+//     are written after one exclusive scan, one thread per (record, key). Rows are
+//     '\n'-terminated decoded values — the buffer is itself a line buffer, so the A4
+//     matchers run on it unchanged (part-scoped matching, §8(f) row 3).
+#include "sg_internal.hpp"
+#include "sg_prims_host.hpp"
+
+namespace sg {
+
+static const SlotSet FMT_SLOTS = {S_F_SPANS, S_F_SPANS, S_F_A, S_F_A, S_F_B, S_F_B, S_F_B, S_F_LB};
+
+// ------------------------------------------------------------------ nmap -oN
+constexpr uint32_t NM_PREFIX_LEN = 21;  // "Nmap scan report for "
+
+__device__ __forceinline__ bool nm_is_digit(uint8_t b) { return b >= '0' && b <= '9'; }
+__device__ __forceinline__ bool nm_is_blank(uint8_t b) { return b == ' ' || b == '\t'; }
+
+// bit 0: report line; bit 1: open-port line. Port line grammar (re.match):
+//   [0-9]{1,5} / (tcp|udp|sctp) [ \t]+ open ([ \t] | end)
+struct NmapPred {
+    const uint8_t *buf;
+    const uint2 *spans;
+    __device__ uint32_t operator()(uint32_t i) const {
+        const uint2 sp = spans[i];
+        const uint8_t *p = buf + sp.x;
+        const uint32_t len = sp.y - sp.x;
+        if (len >= NM_PREFIX_LEN && p[0] == 'N') {
+            const char *pre = "Nmap scan report for ";
+            bool ok = true;
+            for (uint32_t j = 1; j < NM_PREFIX_LEN && ok; ++j) ok = p[j] == (uint8_t)pre[j];
+            return ok ? 1u : 0u;
+        }
+        uint32_t j = 0;
+        while (j < len && j < 5 && nm_is_digit(p[j])) ++j;
+        if (j == 0 || j >= len || p[j] != '/') return 0u;
+        ++j;
+        auto word = [&](const char *w, uint32_t wl) {
+            if (j + wl > len) return false;
+            for (uint32_t q = 0; q < wl; ++q)
+                if (p[j + q] != (uint8_t)w[q]) return false;
+            return true;
+        };
+        if (word("tcp", 3) || word("udp", 3)) j += 3;
+        else if (word("sctp", 4)) j += 4;
+        else return 0u;
+        const uint32_t b0 = j;
+        while (j < len && nm_is_blank(p[j])) ++j;
+        if (j == b0 || !word("open", 4)) return 0u;
+        j += 4;
+        return (j == len || nm_is_blank(p[j])) ? 2u : 0u;
+    }
+};
+
+// Per open-port line: {host start, host end, port start, port end} (host empty -> dropped).
+__global__ __launch_bounds__(256) void k_nmap_prep(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
+                                                   const uint32_t *__restrict__ reps, uint32_t nrep,
+                                                   const uint32_t *__restrict__ ports, uint32_t nport,
+                                                   uint4 *__restrict__ desc) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nport) return;
+    const uint32_t r = ports[k];
+    // last report record before r
+    uint32_t lo = 0, hi = nrep;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (reps[mid] < r) lo = mid + 1; else hi = mid;
+    }
+    uint4 d = make_uint4(0, 0, 0, 0);
+    if (lo > 0) {
+        const uint2 rs = spans[reps[lo - 1]];
+        uint32_t he = rs.x + NM_PREFIX_LEN;
+        while (he < rs.y && buf[he] != ' ') ++he;
+        const uint2 ps = spans[r];
+        uint32_t pe = ps.x;
+        while (nm_is_digit(buf[pe])) ++pe;
+        if (he > rs.x + NM_PREFIX_LEN) d = make_uint4(rs.x + NM_PREFIX_LEN, he, ps.x, pe);
+    }
+    desc[k] = d;
+}
+
+struct NmapLen {
+    const uint4 *desc;
+    __device__ uint64_t operator()(uint32_t k) const {
+        const uint4 d = desc[k];
+        return d.y > d.x ? (uint64_t)(d.y - d.x) + 1 + (d.w - d.z) + 1 : 0ull;
+    }
+};
+
+__global__ __launch_bounds__(256) void k_nmap_emit(const uint8_t *__restrict__ buf, const uint4 *__restrict__ desc,
+                                                   const uint64_t *__restrict__ offs, uint32_t nport,
+                                                   uint8_t *__restrict__ out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nport) return;
+    const uint4 d = desc[k];
+    if (d.y <= d.x) return;
+    uint8_t *o = out + offs[k];
+    for (uint32_t q = d.x; q < d.y; ++q) *o++ = buf[q];
+    *o++ = ':';
+    for (uint32_t q = d.z; q < d.w; ++q) *o++ = buf[q];
+    *o = '\n';
+}
+
+static int dev_nmap_ports(sg_ctx *c, const uint8_t *d_buf, uint64_t n, sg_dev_text *res) {
+    *res = sg_dev_text{};
+    Lines L;
+    SG_TRY(run_lines(c, d_buf, n, FMT_SLOTS, &L, false));
+    const uint32_t R = L.n_rec;
+    res->in_records = R;
+    if (R == 0) return SG_OK;
+    uint32_t *reps, *ports;
+    SG_TRY(slot(c, S_F_REC, (size_t)R + 16, &reps));
+    SG_TRY(slot(c, S_F_KEY, (size_t)R + 16, &ports));
+    uint32_t nrep = 0, nport = 0;
+    SG_TRY(run_select2(c, "nmap_classify", NmapPred{d_buf, L.spans}, R, reps, ports, &nrep, &nport, 40.0));
+    if (nport == 0) return SG_OK;
+    uint4 *desc;
+    uint64_t *offs;
+    SG_TRY(slot(c, S_F_DESC, (size_t)nport + 1, &desc));
+    SG_TRY(slot(c, S_F_OFFS, (size_t)nport + 1, &offs));
+    SG_LAUNCH(c, "nmap_prep", k_nmap_prep, (nport + 255) / 256, 256, 0, d_buf, L.spans, reps, nrep, ports, nport, desc);
+    uint64_t total = 0;
+    SG_TRY(run_scan64(c, "nmap_scan", NmapLen{desc}, nport, offs, &total));
+    uint8_t *out;
+    SG_TRY(slot(c, S_F_OUT, total + 16, &out));
+    SG_LAUNCH_B(c, "nmap_emit", 2.0 * total, k_nmap_emit, (nport + 255) / 256, 256, 0, d_buf, desc, offs, nport, out);
+    res->data = out;
+    res->bytes = total;
+    // records = ports with a host (count from the descriptors: rows of nonzero length)
+    uint64_t recs = 0;
+    {
+        // lengths are > 0 exactly for kept rows; count them on the host from a compaction
+        uint32_t *tmp;
+        SG_TRY(slot(c, S_F_A, (size_t)nport + 16, &tmp));
+        uint32_t kept = 0;
+        struct KeptPred {
+            const uint4 *d;
+            __device__ uint32_t operator()(uint32_t i) const { return d[i].y > d[i].x ? 1u : 0u; }
+        };
+        SG_TRY(run_select2(c, "nmap_kept", KeptPred{desc}, nport, tmp, (uint32_t *)nullptr, &kept, nullptr, 16.0));
+        recs = kept;
+    }
+    res->records = recs;
+    return SG_OK;
+}
+
+// ------------------------------------------------------------------ httpx -json
+constexpr int JS_BLOCK = 256;
+constexpr uint32_t JS_MAXKEYS = 64;
+constexpr uint32_t JS_KEYBYTES = 4096;
+constexpr uint32_t JS_NONE = 0xffffffffu;
+
+struct JsonArgs {
+    const uint8_t *buf;
+    const uint2 *spans;
+    uint32_t R;
+    const uint8_t *keys;       // concatenated key bytes
+    const uint32_t *key_offs;  // nkeys + 1
+    uint32_t nkeys;
+    uint4 *desc;               // R * nkeys: {value start, value end, rows, bytes}
+};
+
+__device__ __forceinline__ bool js_ws(uint8_t b) { return b == ' ' || b == '\t' || b == '\r' || b == '\n'; }
+
+__device__ __forceinline__ int js_hex(uint8_t b) {
+    if (b >= '0' && b <= '9') return b - '0';
+    if (b >= 'a' && b <= 'f') return b - 'a' + 10;
+    if (b >= 'A' && b <= 'F') return b - 'A' + 10;
+    return -1;
+}
+
+// Decode the JSON string body [a, b) (between the quotes) into `put`. Escapes follow
+// json.loads: \" \\ \/ \b \f \n \r \t and \uXXXX (a high+low surrogate pair combines into
+// one code point; a lone surrogate is encoded as its 3-byte form, like Python's
+// 'surrogatepass'). A decoded U+000A is written as the two bytes '\' 'n' so a row stays
+// one line. Malformed escapes are copied verbatim.
+template <class Put>
+__device__ __forceinline__ void js_decode(const uint8_t *buf, uint32_t a, uint32_t b, Put &put) {
+    auto put_cp = [&](uint32_t cp) {
+        if (cp == 0x0a) { put('\\'); put('n'); }
+        else if (cp < 0x80) put((uint8_t)cp);
+        else if (cp < 0x800) { put((uint8_t)(0xc0 | (cp >> 6))); put((uint8_t)(0x80 | (cp & 0x3f))); }
+        else if (cp < 0x10000) {
+            put((uint8_t)(0xe0 | (cp >> 12))); put((uint8_t)(0x80 | ((cp >> 6) & 0x3f))); put((uint8_t)(0x80 | (cp & 0x3f)));
+        } else {
+            put((uint8_t)(0xf0 | (cp >> 18))); put((uint8_t)(0x80 | ((cp >> 12) & 0x3f)));
+            put((uint8_t)(0x80 | ((cp >> 6) & 0x3f))); put((uint8_t)(0x80 | (cp & 0x3f)));
+        }
+    };
+    auto u4 = [&](uint32_t p, uint32_t *v) -> bool {
+        if (p + 4 > b) return false;
+        uint32_t x = 0;
+        for (uint32_t q = 0; q < 4; ++q) {
+            const int h = js_hex(buf[p + q]);
+            if (h < 0) return false;
+            x = (x << 4) | (uint32_t)h;
+        }
+        *v = x;
+        return true;
+    };
+    uint32_t p = a;
+    while (p < b) {
+        const uint8_t ch = buf[p];
+        if (ch != '\\' || p + 1 >= b) { put(ch); ++p; continue; }
+        const uint8_t e = buf[p + 1];
+        uint32_t v;
+        switch (e) {
+            case '"': case '\\': case '/': put(e); p += 2; break;
+            case 'b': put(0x08); p += 2; break;
+            case 'f': put(0x0c); p += 2; break;
+            case 'n': put('\\'); put('n'); p += 2; break;
+            case 'r': put(0x0d); p += 2; break;
+            case 't': put(0x09); p += 2; break;
+            case 'u':
+                if (!u4(p + 2, &v)) { put(ch); ++p; break; }
+                p += 6;
+                if (v >= 0xd800 && v < 0xdc00 && p + 1 < b && buf[p] == '\\' && buf[p + 1] == 'u') {
+                    uint32_t lo;
+                    if (u4(p + 2, &lo) && lo >= 0xdc00 && lo < 0xe000) {
+                        v = 0x10000 + ((v - 0xd800) << 10) + (lo - 0xdc00);
+                        p += 6;
+                    }
+                }
+                put_cp(v);
+                break;
+            default: put(ch); ++p; break;
+        }
+    }
+}
+
+// Walk one value [vs, ve) (already trimmed): a string -> one decoded row; an array ->
+// one row per element (strings decoded, anything else its trimmed raw text); anything
+// else -> its raw text. Empty rows are dropped. `row(begin)` / `put(byte)` / `end()`
+// receive the output.
+template <class Sink>
+__device__ __forceinline__ void js_value(const uint8_t *buf, uint32_t vs, uint32_t ve, Sink &sk) {
+    auto emit_item = [&](uint32_t a, uint32_t b) {
+        while (a < b && js_ws(buf[a])) ++a;
+        while (b > a && js_ws(buf[b - 1])) --b;
+        if (a >= b) return;
+        if (buf[a] == '"' && b - a >= 2 && buf[b - 1] == '"') {
+            if (b - a == 2) return;  // ""
+            sk.begin();
+            js_decode(buf, a + 1, b - 1, sk);
+            sk.end();
+        } else {
+            sk.begin();
+            for (uint32_t q = a; q < b; ++q) sk(buf[q]);
+            sk.end();
+        }
+    };
+    if (vs >= ve) return;
+    if (buf[vs] != '[') { emit_item(vs, ve); return; }
+    // array: split at depth-1 commas outside strings
+    uint32_t depth = 0, start = vs + 1;
+    bool in_str = false, esc = false;
+    for (uint32_t p = vs; p < ve; ++p) {
+        const uint8_t ch = buf[p];
+        if (in_str) {
+            if (esc) esc = false;
+            else if (ch == '\\') esc = true;
+            else if (ch == '"') in_str = false;
+            continue;
+        }
+        if (ch == '"') { in_str = true; continue; }
+        if (ch == '[' || ch == '{') { ++depth; continue; }
+        if (ch == ']' || ch == '}') {
+            if (depth == 1) { emit_item(start, p); start = p + 1; }
+            --depth;
+            continue;
+        }
+        if (ch == ',' && depth == 1) { emit_item(start, p); start = p + 1; }
+    }
+}
+
+struct JsCount {
+    uint32_t rows = 0, bytes = 0, cur = 0;
+    __device__ void begin() { cur = 0; }
+    __device__ void operator()(uint8_t) { ++cur; }
+    __device__ void end() { if (cur) { ++rows; bytes += cur + 1; } }
+};
+
+// One wave per record.
+__global__ __launch_bounds__(JS_BLOCK) void k_json_scan(JsonArgs a) {
+    __shared__ uint8_t s_keys[JS_KEYBYTES];
+    __shared__ uint32_t s_koff[JS_MAXKEYS + 1];
+    for (uint32_t q = threadIdx.x; q <= a.nkeys; q += JS_BLOCK) s_koff[q] = a.key_offs[q];
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < s_koff[a.nkeys]; q += JS_BLOCK) s_keys[q] = a.keys[q];
+    __syncthreads();
+    const int lane = lane_id();
+    const uint32_t nw = gridDim.x * (JS_BLOCK / 64);
+    const uint32_t my_klen = (lane < (int)a.nkeys) ? s_koff[lane + 1] - s_koff[lane] : 0xffffffffu;
+    for (uint32_t r = blockIdx.x * (JS_BLOCK / 64) + (threadIdx.x >> 6); r < a.R; r += nw) {
+        const uint2 sp = a.spans[r];
+        uint32_t my_vs = JS_NONE, my_ve = 0;
+        // wave-uniform walk state
+        uint32_t depth = 0, str_s = 0, str_e = 0, val_s = 0, open_pos = JS_NONE, close_pos = JS_NONE;
+        uint32_t first_nws = JS_NONE, last_nws = 0;
+        int cur_key = -1;
+        bool in_str = false, bad = false, done = false;
+        uint32_t bs_run = 0;  // trailing backslash run length of the previous chunk
+        for (uint32_t base = sp.x; base < sp.y && !bad; base += 64) {
+            const uint32_t pos = base + lane;
+            const bool valid = pos < sp.y;
+            const uint8_t b = valid ? a.buf[pos] : 0;
+            const uint64_t Q = __ballot(valid && b == '"');
+            const uint64_t BS = __ballot(valid && b == '\\');
+            const uint64_t ST = __ballot(valid && (b == '{' || b == '[' || b == '}' || b == ']' || b == ':' || b == ','));
+            const uint64_t NWS = __ballot(valid && !js_ws(b));
+            if (NWS) {
+                if (first_nws == JS_NONE) first_nws = base + (uint32_t)(__ffsll((long long)NWS) - 1);
+                last_nws = base + 63u - (uint32_t)__clzll(NWS);
+            }
+            uint64_t E = Q | ST;
+            while (E) {
+                const uint32_t p = (uint32_t)(__ffsll((long long)E) - 1);
+                E &= E - 1;
+                const uint64_t bit = 1ull << p;
+                if (Q & bit) {
+                    if (!in_str) {
+                        if (depth == 0) { bad = true; break; }
+                        in_str = true;
+                        str_s = base + p + 1;
+                    } else {
+                        // escaped iff preceded by an odd run of backslashes
+                        const uint64_t below = bit - 1;
+                        const uint64_t zeros = ~BS & below;
+                        const uint32_t run = zeros ? p - 1 - (63u - (uint32_t)__clzll(zeros)) : p + bs_run;
+                        if (run & 1u) continue;
+                        in_str = false;
+                        str_e = base + p;
+                    }
+                    continue;
+                }
+                if (in_str) continue;
+                const uint8_t ch = (uint8_t)__shfl((int)b, (int)p, 64);
+                const uint32_t at = base + p;
+                if (done) { bad = true; break; }
+                if (ch == '{' || ch == '[') {
+                    if (depth == 0) {
+                        if (ch != '{') { bad = true; break; }
+                        open_pos = at;
+                    }
+                    ++depth;
+                } else if (ch == '}' || ch == ']') {
+                    if (depth == 0) { bad = true; break; }
+                    if (depth == 1) {
+                        if (ch != '}') { bad = true; break; }
+                        if (cur_key >= 0 && lane == cur_key) { my_vs = val_s; my_ve = at; }
+                        cur_key = -1;
+                        done = true;
+                        close_pos = at;
+                    }
+                    --depth;
+                } else if (ch == ':') {
+                    if (depth == 1) {
+                        // the key is the last string; lane k tests requested key k
+                        const uint32_t kl = str_e - str_s;
+                        bool eq = my_klen == kl;
+                        for (uint32_t q = 0; q < kl && eq; ++q) eq = a.buf[str_s + q] == s_keys[s_koff[lane] + q];
+                        const uint64_t m = __ballot(eq);
+                        cur_key = m ? __ffsll((long long)m) - 1 : -1;
+                        val_s = at + 1;
+                    }
+                } else {  // ','
+                    if (depth == 1) {
+                        if (cur_key >= 0 && lane == cur_key) { my_vs = val_s; my_ve = at; }
+                        cur_key = -1;
+                    }
+                }
+            }
+            // trailing backslash run carried into the next chunk
+            if (BS == ~0ull) bs_run += 64;
+            else bs_run = (uint32_t)__clzll(~BS);
+        }
+        bad = bad || in_str || depth != 0 || !done || first_nws != open_pos || last_nws != close_pos;
+        if (lane < (int)a.nkeys) {
+            uint4 d = make_uint4(0, 0, 0, 0);
+            if (!bad && my_vs != JS_NONE) {
+                uint32_t vs = my_vs, ve = my_ve;
+                while (vs < ve && js_ws(a.buf[vs])) ++vs;
+                while (ve > vs && js_ws(a.buf[ve - 1])) --ve;
+                JsCount cnt;
+                js_value(a.buf, vs, ve, cnt);
+                d = make_uint4(vs, ve, cnt.rows, cnt.bytes);
+            }
+            a.desc[(size_t)r * a.nkeys + lane] = d;
+        }
+    }
+}
+
+// packed (bytes << 32 | rows) per (record, key). Rows never outgrow the input: each
+// value's rows are no longer than its raw text plus the delimiter that follows it, so
+// the output total stays below the 4 GiB input limit and the fields never carry.
+struct JsonLen {
+    const uint4 *desc;
+    __device__ uint64_t operator()(uint32_t i) const {
+        const uint4 d = desc[i];
+        return ((uint64_t)d.w << 32) | d.z;
+    }
+};
+
+struct JsWrite {
+    uint8_t *out;
+    uint32_t *row_rec, *row_key;
+    uint64_t o;
+    uint32_t row, rec, key;
+    __device__ void begin() {}
+    __device__ void operator()(uint8_t ch) { out[o++] = ch; }
+    __device__ void end() {
+        out[o++] = '\n';
+        row_rec[row] = rec;
+        row_key[row] = key;
+        ++row;
+    }
+};
+
+__global__ __launch_bounds__(256) void k_json_emit(const uint8_t *__restrict__ buf, const uint4 *__restrict__ desc,
+                                                   const uint64_t *__restrict__ offs, uint32_t nitems, uint32_t nkeys,
+                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ row_rec,
+                                                   uint32_t *__restrict__ row_key) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nitems) return;
+    const uint4 d = desc[i];
+    if (d.z == 0) return;
+    const uint64_t off = offs[i];
+    JsWrite w{out, row_rec, row_key, off >> 32, (uint32_t)off, i / nkeys, i % nkeys};
+    js_value(buf, d.x, d.y, w);
+}
+
+static int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *keys, const uint32_t *key_offs,
+                           uint32_t nkeys, sg_dev_rows *res) {
+    *res = sg_dev_rows{};
+    if (nkeys == 0 || nkeys > JS_MAXKEYS) { set_error("json fields: 1..%u keys", JS_MAXKEYS); return SG_E_INVAL; }
+    if (key_offs[0] != 0 || key_offs[nkeys] > JS_KEYBYTES) { set_error("json fields: keys exceed %u bytes", JS_KEYBYTES); return SG_E_INVAL; }
+    for (uint32_t k = 0; k < nkeys; ++k) {
+        if (key_offs[k + 1] < key_offs[k]) { set_error("json fields: bad key offsets"); return SG_E_INVAL; }
+        for (uint32_t q = key_offs[k]; q < key_offs[k + 1]; ++q)
+            if (keys[q] == '"' || keys[q] == '\\' || keys[q] < 0x20) {
+                set_error("json fields: key %u needs JSON escaping (unsupported)", k);
+                return SG_E_INVAL;
+            }
+    }
+    Lines L;
+    SG_TRY(run_lines(c, d_buf, n, FMT_SLOTS, &L, false));
+    const uint32_t R = L.n_rec;
+    res->in_records = R;
+    if (R == 0) return SG_OK;
+    const uint64_t items = (uint64_t)R * nkeys;
+    if (items >= (1ull << 32)) { set_error("json fields: records x keys exceeds 2^32"); return SG_E_TOO_LARGE; }
+    uint32_t *d_koff;
+    uint8_t *d_keys;
+    SG_TRY(slot(c, S_F_KEYS, JS_KEYBYTES + 4 * (JS_MAXKEYS + 1), &d_keys));
+    d_koff = reinterpret_cast<uint32_t *>(d_keys + JS_KEYBYTES);
+    SG_HIP(hipMemcpyAsync(d_keys, keys, key_offs[nkeys] ? key_offs[nkeys] : 1, hipMemcpyHostToDevice, c->stream));
+    SG_HIP(hipMemcpyAsync(d_koff, key_offs, 4 * (nkeys + 1), hipMemcpyHostToDevice, c->stream));
+    uint4 *desc;
+    uint64_t *offs;
+    SG_TRY(slot(c, S_F_DESC, items + 1, &desc));
+    SG_TRY(slot(c, S_F_OFFS, items + 1, &offs));
+    JsonArgs ja{d_buf, L.spans, R, d_keys, d_koff, nkeys, desc};
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((R + 3) / 4, 256u * 16u);
+    SG_LAUNCH_B(c, "json_scan", (double)n + 16.0 * items, k_json_scan, grid, JS_BLOCK, 0, ja);
+    uint64_t total = 0;
+    SG_TRY(run_scan64(c, "json_scan_len", JsonLen{desc}, (uint32_t)items, offs, &total));
+    const uint64_t rows = total & 0xffffffffu, bytes = total >> 32;
+    uint8_t *out;
+    uint32_t *rrec, *rkey;
+    SG_TRY(slot(c, S_F_OUT, bytes + 16, &out));
+    SG_TRY(slot(c, S_F_REC, rows + 1, &rrec));
+    SG_TRY(slot(c, S_F_KEY, rows + 1, &rkey));
+    SG_LAUNCH_B(c, "json_emit", 2.0 * bytes + 8.0 * rows, k_json_emit, (uint32_t)((items + 255) / 256), 256, 0, d_buf,
+                desc, offs, (uint32_t)items, nkeys, out, rrec, rkey);
+    res->data = out;
+    res->bytes = bytes;
+    res->rows = rows;
+    res->row_rec = rrec;
+    res->row_key = rkey;
+    return SG_OK;
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+namespace {
+struct Acq {
+    sg_ctx *c = nullptr;
+    ~Acq() { if (c) pool_release(c); }
+};
+int acquire_ctx(Acq *a) {
+    int dev = 0;
+    SG_TRY(pick_device(&dev));
+    SG_TRY(pool_acquire(dev, &a->c));
+    SG_HIP(hipSetDevice(dev));
+    return SG_OK;
+}
+int upload_aligned(sg_ctx *c, const uint8_t *host, size_t n, uint8_t **d) {
+    SG_TRY(slot(c, S_IN, n + 16, d));
+    if (n) SG_HIP(hipMemcpyAsync(*d, host, n, hipMemcpyHostToDevice, c->stream));
+    return SG_OK;
+}
+int dev_aligned(sg_ctx *c, const uint8_t *d, size_t n, const uint8_t **out) {
+    if (((uintptr_t)d & 15) == 0) { *out = d; return SG_OK; }
+    uint8_t *a;
+    SG_TRY(slot(c, S_IN, n + 16, &a));
+    if (n) SG_HIP(hipMemcpyAsync(a, d, n, hipMemcpyDeviceToDevice, c->stream));
+    *out = a;
+    return SG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int sg_dev_nmap_ports(sg_ctx *c, const uint8_t *d_buf, size_t n, sg_dev_text *res) {
+    if (!c || !res || (!d_buf && n)) { set_error("sg_dev_nmap_ports: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b;
+    SG_TRY(dev_aligned(c, d_buf, n, &b));
+    return dev_nmap_ports(c, b, n, res);
+}
+
+int sg_nmap_ports(const uint8_t *buf, size_t n, uint8_t *out, size_t cap, size_t *out_n) {
+    if (!out_n || (!buf && n)) { set_error("sg_nmap_ports: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    Acq a;
+    SG_TRY(acquire_ctx(&a));
+    sg_ctx *c = a.c;
+    uint8_t *d;
+    SG_TRY(upload_aligned(c, buf, n, &d));
+    sg_dev_text r;
+    SG_TRY(dev_nmap_ports(c, d, n, &r));
+    *out_n = r.bytes;
+    if (r.bytes > cap) { SG_HIP(hipStreamSynchronize(c->stream)); set_error("output capacity too small"); return SG_E_CAP; }
+    if (r.bytes) SG_HIP(hipMemcpyAsync(out, r.data, r.bytes, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
+    return SG_OK;
+}
+
+int sg_dev_json_fields(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint8_t *keys, const uint32_t *key_offs,
+                       uint32_t n_keys, sg_dev_rows *res) {
+    if (!c || !res || !key_offs || (!d_buf && n) || (!keys && n_keys)) {
+        set_error("sg_dev_json_fields: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b;
+    SG_TRY(dev_aligned(c, d_buf, n, &b));
+    return dev_json_fields(c, b, n, keys, key_offs, n_keys, res);
+}
+
+int sg_json_fields(const uint8_t *buf, size_t n, const uint8_t *keys, const uint32_t *key_offs, uint32_t n_keys,
+                   uint8_t *out, size_t cap, size_t *out_n, uint32_t *row_rec, uint32_t *row_key, size_t rows_cap,
+                   size_t *n_rows) {
+    if (!out_n || !n_rows || !key_offs || (!buf && n) || (!keys && n_keys)) {
+        set_error("sg_json_fields: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    Acq a;
+    SG_TRY(acquire_ctx(&a));
+    sg_ctx *c = a.c;
+    uint8_t *d;
+    SG_TRY(upload_aligned(c, buf, n, &d));
+    sg_dev_rows r;
+    SG_TRY(dev_json_fields(c, d, n, keys, key_offs, n_keys, &r));
+    *out_n = r.bytes;
+    *n_rows = r.rows;
+    if (r.bytes > cap || r.rows > rows_cap) {
+        SG_HIP(hipStreamSynchronize(c->stream));
+        set_error("output capacity too small");
+        return SG_E_CAP;
+    }
+    if (r.bytes) SG_HIP(hipMemcpyAsync(out, r.data, r.bytes, hipMemcpyDeviceToHost, c->stream));
+    if (r.rows && row_rec) SG_HIP(hipMemcpyAsync(row_rec, r.row_rec, 4 * r.rows, hipMemcpyDeviceToHost, c->stream));
+    if (r.rows && row_key) SG_HIP(hipMemcpyAsync(row_key, r.row_key, 4 * r.rows, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
+    return SG_OK;
+}
+
+}  // extern "C"
