@@ -196,6 +196,49 @@ int sg_json_fields(const uint8_t *buf, size_t n, const uint8_t *keys, const uint
 int sg_dev_json_fields(sg_ctx *ctx, const uint8_t *d_buf, size_t n, const uint8_t *keys,
                        const uint32_t *key_offs, uint32_t n_keys, sg_dev_rows *res);
 
+/* ------------------------------------------------------------------ nuclei matcher logic
+ * SURVEY.md §8(f) row 3. A template = matchers joined by `matchers-condition`
+ * (technologies/tech-detect.yaml:16); a matcher = words or regexes joined by its
+ * `condition`, optionally `negative` (file/audit/cisco/disable-ip-source-route.yaml:19-22)
+ * and `case-insensitive` (technologies/typo3-detect.yaml:23), reading one part: 0 = the
+ * record, k+1 = field key k of an httpx -json line (sg_json_fields rows; a pattern hits a
+ * field when it occurs in any of its rows). `encoding: hex` words are passed decoded.
+ * Semantics per part text: word = substring (case-insensitive: ASCII-folded), regex =
+ * re.search; condition or = any, and = all; negative inverts the matcher; the template
+ * joins its matchers with and/or. `dsl`, `status`, `size` matchers are out of scope. */
+#define SG_TM_WORD 0u
+#define SG_TM_REGEX 1u
+#define SG_TM_AND 1u        /* condition: and (default: or); also the template flag */
+#define SG_TM_NEGATIVE 2u
+#define SG_TM_NOCASE 4u     /* case-insensitive words (regexes use (?i)) */
+typedef struct sg_tm_matcher {
+    uint32_t kind;          /* SG_TM_WORD | SG_TM_REGEX */
+    uint32_t part;          /* 0 = record, k + 1 = field key k */
+    uint32_t flags;         /* SG_TM_AND | SG_TM_NEGATIVE | SG_TM_NOCASE */
+    uint32_t tmpl;          /* owning template (non-decreasing over the matcher array) */
+    uint32_t first, count;  /* its patterns: pats[pat_offs[first] ..], count >= 1 */
+} sg_tm_matcher;
+typedef struct sg_templates sg_templates;
+/* tmpl_flags[t]: SG_TM_AND for matchers-condition and. keys: field names for parts >= 1
+ * (as sg_json_fields). */
+int sg_tmpl_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats,
+                    const sg_tm_matcher *matchers, uint32_t n_matchers,
+                    const uint32_t *tmpl_flags, uint32_t n_templates,
+                    const uint8_t *keys, const uint32_t *key_offs, uint32_t n_keys,
+                    sg_templates **h);
+/* distinct atoms (part, kind, case, pattern), engines, templates true on empty evidence */
+int sg_tmpl_info(const sg_templates *h, uint32_t *n_atoms, uint32_t *n_engines, uint32_t *n_vacuous);
+typedef struct sg_dev_tmatches {
+    const uint32_t *rec_idx;  /* device: record (A3 order) */
+    const uint32_t *tmpl_id;  /* device: template */
+    uint64_t n;               /* (record, template) pairs, sorted */
+    uint64_t in_records;
+} sg_dev_tmatches;
+int sg_dev_tmpl_eval(sg_ctx *ctx, sg_templates *h, const uint8_t *d_buf, size_t n, sg_dev_tmatches *res);
+int sg_tmpl_eval(sg_templates *h, const uint8_t *buf, size_t n, uint32_t *rec_idx, uint32_t *tmpl_id,
+                 size_t cap, size_t *n_out);
+void sg_tmpl_free(sg_templates *h);
+
 #ifdef __cplusplus
 }
 #endif

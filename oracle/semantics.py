@@ -376,3 +376,62 @@ def json_field_rows(buf: bytes, keys: Sequence[bytes]) -> Tuple[bytes, List[int]
                     rrec.append(ri)
                     rkey.append(ki)
     return serialize(rows), rrec, rkey
+
+
+# ----------------------------------------------------------------------------- §8(f)3 nuclei matchers
+# Matcher logic of nuclei templates (worker/modules/nuclei.json:2; the corpus is
+# worker/artifacts/templates/**): matchers-condition and/or over matchers
+# (technologies/tech-detect.yaml:16), each matcher words/regexes joined by its condition,
+# `negative` (file/audit/cisco/disable-ip-source-route.yaml:19-22), `case-insensitive`
+# (technologies/typo3-detect.yaml:23), `part` = the record, or an httpx -json field when the
+# part names one of the requested keys (a pattern hits a field when it occurs in any of the
+# field's rows). nuclei is an absent Go binary: this restates its documented semantics.
+def _tm_part(part, keys: Sequence[bytes]) -> int:
+    p = part.encode() if isinstance(part, str) else bytes(part)
+    return keys.index(p) + 1 if p in keys else 0
+
+
+def template_matches(buf: bytes, templates, keys: Sequence[bytes] = ()) -> List[Tuple[int, int]]:
+    """Sorted (record index, template index) pairs for which the template holds."""
+    keys = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+    norm = []
+    for t in templates:
+        ms = []
+        for m in t["matchers"]:
+            nc = bool(m.get("case-insensitive"))
+            pats = [bytes(p) for p in m["patterns"]]
+            if m["type"] == "regex":
+                comp = [re.compile(p) for p in pats]  # case-insensitive is a word option; regexes use (?i)
+                test = (lambda comp: lambda text: [c.search(text) is not None for c in comp])(comp)
+            else:
+                ws = [_fold(p) if nc else p for p in pats]
+                test = (lambda ws, nc: lambda text: [w in (_fold(text) if nc else text) for w in ws])(ws, nc)
+            ms.append((_tm_part(m.get("part", "body"), keys), test, m.get("condition", "or") == "and",
+                       bool(m.get("negative"))))
+        norm.append((t.get("condition", "or") == "and", ms))
+    recs = parse_records(buf)
+    rows_of = [dict() for _ in recs]
+    if keys:
+        rows, rrec, rkey = json_field_rows(buf, keys)
+        for row, r, k in zip(rows.split(b"\n")[:-1], rrec, rkey):
+            rows_of[r].setdefault(k + 1, []).append(row)
+    out = []
+    for ri, rec in enumerate(recs):
+        for ti, (and_t, ms) in enumerate(norm):
+            acc = and_t
+            for part, test, and_m, neg in ms:
+                texts = [rec] if part == 0 else rows_of[ri].get(part, [])
+                hits = [False] * 0
+                for text in texts:
+                    h = test(text)
+                    hits = h if not hits else [a or b for a, b in zip(hits, h)]
+                if not hits:
+                    ok = False
+                else:
+                    ok = all(hits) if and_m else any(hits)
+                if neg:
+                    ok = not ok
+                acc = (acc and ok) if and_t else (acc or ok)
+            if acc:
+                out.append((ri, ti))
+    return out

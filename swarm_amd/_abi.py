@@ -121,3 +121,30 @@ lib = _load()
 def check(rc: int) -> None:
     if rc != SG_OK:
         raise SGError(rc, lib.sg_last_error().decode(errors="replace"))
+
+
+class TmMatcher(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("part", C.c_uint32), ("flags", C.c_uint32), ("tmpl", C.c_uint32),
+                ("first", C.c_uint32), ("count", C.c_uint32)]
+
+
+class DevTMatches(C.Structure):
+    _fields_ = [("rec_idx", C.c_void_p), ("tmpl_id", C.c_void_p), ("n", C.c_uint64), ("in_records", C.c_uint64)]
+
+
+SG_TM_WORD, SG_TM_REGEX = 0, 1
+SG_TM_AND, SG_TM_NEGATIVE, SG_TM_NOCASE = 1, 2, 4
+EXPORTS += ["sg_tmpl_compile", "sg_tmpl_info", "sg_dev_tmpl_eval", "sg_tmpl_eval", "sg_tmpl_free"]
+for _name, (_res, _args) in {
+    "sg_tmpl_compile": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(TmMatcher), C.c_uint32,
+                                  C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32,
+                                  C.POINTER(C.c_void_p)]),
+    "sg_tmpl_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "sg_dev_tmpl_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(DevTMatches)]),
+    "sg_tmpl_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                               C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sg_tmpl_free": (None, [C.c_void_p]),
+}.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args

@@ -298,3 +298,84 @@ class Context:
         check(lib.sg_dev_partition(self._h, C.c_void_p(d_buf), n, n_parts, C.c_void_p(d_out),
                                    out_cap, pb, pr))
         return list(pb), list(pr)
+
+
+class Templates:
+    """nuclei matcher logic compiled for the GPU.
+
+    templates: [{"condition": "and"|"or", "matchers": [{"type": "word"|"regex",
+    "part": str, "condition": "and"|"or", "negative": bool, "case-insensitive": bool,
+    "patterns": [bytes]}]}] — the matcher block of a nuclei template with `encoding: hex`
+    words already decoded (tests/golden/gen_template_fixtures.py shows the conversion).
+    A matcher whose part names one of `keys` reads that httpx -json field; any other part
+    reads the whole record."""
+
+    def __init__(self, templates, keys: Sequence[bytes] = ()):
+        self.keys = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+        pats, ms, tflags = [], [], []
+        for ti, t in enumerate(templates):
+            tflags.append(_abi.SG_TM_AND if t.get("condition", "or") == "and" else 0)
+            for m in t["matchers"]:
+                part = m.get("part", "body")
+                part = part.encode() if isinstance(part, str) else bytes(part)
+                f = 0
+                if m.get("condition", "or") == "and":
+                    f |= _abi.SG_TM_AND
+                if m.get("negative"):
+                    f |= _abi.SG_TM_NEGATIVE
+                if m.get("case-insensitive"):
+                    f |= _abi.SG_TM_NOCASE
+                kind = _abi.SG_TM_REGEX if m["type"] == "regex" else _abi.SG_TM_WORD
+                ms.append(_abi.TmMatcher(kind, self.keys.index(part) + 1 if part in self.keys else 0, f, ti,
+                                         len(pats), len(m["patterns"])))
+                pats += [bytes(p) for p in m["patterns"]]
+        blob = np.frombuffer(b"".join(pats) or b"\0", dtype=np.uint8)
+        offs = np.zeros(len(pats) + 1, dtype=np.uint32)
+        np.cumsum([len(p) for p in pats], out=offs[1:])
+        marr = (_abi.TmMatcher * max(1, len(ms)))(*ms)
+        tf = np.array(tflags or [0], dtype=np.uint32)
+        kb, ko = _keys_blob(self.keys)
+        U32P = C.POINTER(C.c_uint32)
+        self._h = C.c_void_p()
+        check(lib.sg_tmpl_compile(blob.ctypes.data, offs.ctypes.data_as(U32P), len(pats), marr, len(ms),
+                                  tf.ctypes.data_as(U32P), len(tflags), kb.ctypes.data, ko.ctypes.data_as(U32P),
+                                  len(self.keys), C.byref(self._h)))
+        self.n = len(tflags)
+
+    def close(self):
+        if self._h:
+            lib.sg_tmpl_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        a, e, v = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib.sg_tmpl_info(self._h, C.byref(a), C.byref(e), C.byref(v)))
+        return {"atoms": a.value, "engines": e.value, "vacuous": v.value, "templates": self.n}
+
+    def match(self, buf) -> List[Tuple[int, int]]:
+        """Sorted (record index, template index) pairs for which the template holds."""
+        a = _view(buf)
+        cap = max(1024, a.size // 8)
+        while True:
+            rec = np.empty(cap, dtype=np.uint32)
+            tid = np.empty(cap, dtype=np.uint32)
+            n = C.c_size_t(0)
+            U32P = C.POINTER(C.c_uint32)
+            rc = lib.sg_tmpl_eval(self._h, _ptr(a), a.size, rec.ctypes.data_as(U32P), tid.ctypes.data_as(U32P), cap,
+                                  C.byref(n))
+            if rc == _abi.SG_E_CAP:
+                cap = n.value
+                continue
+            check(rc)
+            return list(zip(rec[: n.value].tolist(), tid[: n.value].tolist()))
+
+    def dev_match(self, ctx: "Context", d_buf: int, n: int) -> _abi.DevTMatches:
+        r = _abi.DevTMatches()
+        check(lib.sg_dev_tmpl_eval(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(r)))
+        return r

@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256) void k_json_emit(const uint8_t *__restrict__ b
     js_value(buf, d.x, d.y, w);
 }
 
-static int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *keys, const uint32_t *key_offs,
+int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *keys, const uint32_t *key_offs,
                            uint32_t nkeys, sg_dev_rows *res) {
     *res = sg_dev_rows{};
     if (nkeys == 0 || nkeys > JS_MAXKEYS) { set_error("json fields: 1..%u keys", JS_MAXKEYS); return SG_E_INVAL; }

@@ -50,4 +50,11 @@ int serialize(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
 int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes);
 
+// A4 matching of a device line buffer (sg_match.hip); want_lines = false skips the grep
+// output (hits only).
+int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res, bool want_lines);
+// httpx -json field rows (sg_formats.hip).
+int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *keys, const uint32_t *key_offs,
+                    uint32_t nkeys, sg_dev_rows *res);
+
 }  // namespace sg

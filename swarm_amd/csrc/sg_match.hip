@@ -1113,7 +1113,7 @@ static int select_one(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint32
     return run_select2(c, name, pred, n, out, (uint32_t *)nullptr, count, nullptr);
 }
 
-static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res) {
+int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res, bool want_lines) {
     *res = sg_dev_hits{};
     SG_TRY(ensure_device(h, c->device));
     Lines L;
@@ -1256,6 +1256,7 @@ static int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n,
     res->rec_idx = rec;
     res->sig_id = sig;
     res->n_hits = H;
+    if (!want_lines) return SG_OK;
     // matched records (input order) -> grep output
     uint32_t M = 0;
     SG_TRY(select_one(c, "hits_recs", RecHeadPred{KK}, total, sel, &M));
@@ -1384,7 +1385,7 @@ int sg_dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, size_t n, sg_de
         if (n) SG_HIP(hipMemcpyAsync(a, d_buf, n, hipMemcpyDeviceToDevice, c->stream));
         b = a;
     }
-    return dev_match(c, h, b, n, res);
+    return dev_match(c, h, b, n, res, true);
 }
 
 int sg_match(sg_matcher *h, const uint8_t *buf, size_t n, uint64_t *rec_idx, uint32_t *sig_id, size_t cap,
@@ -1401,7 +1402,7 @@ int sg_match(sg_matcher *h, const uint8_t *buf, size_t n, uint64_t *rec_idx, uin
     SG_TRY(slot(c, S_IN, n + 16, &d));
     if (n) SG_HIP(hipMemcpyAsync(d, buf, n, hipMemcpyHostToDevice, c->stream));
     sg_dev_hits r;
-    SG_TRY(dev_match(c, h, d, n, &r));
+    SG_TRY(dev_match(c, h, d, n, &r, true));
     *n_hit = r.n_hits;
     if (r.n_hits > cap) { set_error("hit capacity too small"); SG_HIP(hipStreamSynchronize(c->stream)); return SG_E_CAP; }
     std::vector<uint32_t> rr(r.n_hits);
@@ -1427,7 +1428,7 @@ int sg_match_lines(sg_matcher *h, const uint8_t *buf, size_t n, uint8_t *out, si
     SG_TRY(slot(c, S_IN, n + 16, &d));
     if (n) SG_HIP(hipMemcpyAsync(d, buf, n, hipMemcpyHostToDevice, c->stream));
     sg_dev_hits r;
-    SG_TRY(dev_match(c, h, d, n, &r));
+    SG_TRY(dev_match(c, h, d, n, &r, true));
     *out_n = r.lines_bytes;
     if (r.lines_bytes > cap) { set_error("output capacity too small"); SG_HIP(hipStreamSynchronize(c->stream)); return SG_E_CAP; }
     if (r.lines_bytes) SG_HIP(hipMemcpyAsync(out, r.lines, r.lines_bytes, hipMemcpyDeviceToHost, c->stream));

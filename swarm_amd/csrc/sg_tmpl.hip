@@ -1,0 +1,574 @@
+// sg_tmpl.hip — nuclei matcher semantics on the GPU.
+//
+// A template is a list of matchers joined by `matchers-condition` and/or
+// (technologies/tech-detect.yaml:16); a matcher is a list of words or regexes joined by
+// its `condition` and/or, optionally `negative` (file/audit/cisco/disable-ip-source-
+// route.yaml:19-22) and `case-insensitive` (technologies/typo3-detect.yaml:23), and reads
+// one `part`: the record itself (part 0) or a field of an httpx -json line (part k+1 =
+// requested key k, e.g. title / webserver / tech; a word matches a field when it occurs in
+// any of the field's rows). `encoding: hex` words arrive already decoded.
+//
+// Compile: every distinct (part, kind, case, pattern) is an "atom"; atoms are matched by
+// the A4 engines (literal filter / Aho-Corasick, regex DFA plan), one engine per (stream,
+// kind, case) where stream 0 is the record buffer and stream 1 the field rows of
+// sg_json_fields. Evaluation is a sparse join done entirely with sort/select primitives:
+//   hits (record, atom)  --sort, unique-->  expand over atom -> matchers
+//   (record, matcher)    --sort-->          segments per (record, template)
+//   one thread per segment walks the template's matchers (counts distinct words per
+//   matcher for `and`), applies `negative`, joins with the template condition;
+//   templates that hold on an empty record ("vacuous": e.g. a lone negative matcher)
+//   are added for every record without a segment for them (binary search).
+// Output: (record, template) pairs, sorted.
+#include "sg_internal.hpp"
+#include "sg_prims_host.hpp"
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+
+namespace sg {
+
+struct TmRun {
+    sg_matcher *m = nullptr;
+    int stream = 0;
+    std::vector<uint32_t> soff, satoms;  // signature -> atoms (CSR)
+    uint32_t *d_soff = nullptr, *d_satoms = nullptr;
+};
+
+}  // namespace sg
+
+struct sg_templates {
+    uint32_t n_tmpl = 0, n_match = 0, n_atoms = 0;
+    std::vector<uint8_t> key_blob;
+    std::vector<uint32_t> key_offs;
+    std::vector<sg::TmRun> runs;
+    std::vector<uint32_t> atom_part, occ_off, occ_m, m_tmpl, m_need, m_flags, t_first, t_count, t_flags, vac;
+    struct Dev {
+        uint32_t *atom_part = nullptr, *occ_off = nullptr, *occ_m = nullptr, *m_tmpl = nullptr, *m_need = nullptr,
+                 *m_flags = nullptr, *t_first = nullptr, *t_count = nullptr, *t_flags = nullptr, *vac = nullptr;
+    } d;
+    int dev = -1;
+    std::mutex mu;
+};
+
+namespace sg {
+
+template <class T>
+static int tm_upload(const std::vector<T> &v, T **d) {
+    const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+    if (hipMalloc(d, bytes) != hipSuccess) { (void)hipGetLastError(); set_error("hipMalloc template table"); return SG_E_NOMEM; }
+    if (!v.empty()) SG_HIP(hipMemcpy(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return SG_OK;
+}
+
+static void tm_free_dev(sg_templates *h) {
+    auto &d = h->d;
+    for (void *p : {(void *)d.atom_part, (void *)d.occ_off, (void *)d.occ_m, (void *)d.m_tmpl, (void *)d.m_need,
+                    (void *)d.m_flags, (void *)d.t_first, (void *)d.t_count, (void *)d.t_flags, (void *)d.vac})
+        if (p) (void)hipFree(p);
+    d = sg_templates::Dev{};
+    for (auto &r : h->runs) {
+        if (r.d_soff) (void)hipFree(r.d_soff);
+        if (r.d_satoms) (void)hipFree(r.d_satoms);
+        r.d_soff = r.d_satoms = nullptr;
+    }
+    h->dev = -1;
+}
+
+static int tm_ensure_device(sg_templates *h, int dev) {
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->dev == dev) return SG_OK;
+    if (h->dev >= 0) { (void)hipSetDevice(h->dev); tm_free_dev(h); }
+    SG_HIP(hipSetDevice(dev));
+    auto &d = h->d;
+    SG_TRY(tm_upload(h->atom_part, &d.atom_part));
+    SG_TRY(tm_upload(h->occ_off, &d.occ_off));
+    SG_TRY(tm_upload(h->occ_m, &d.occ_m));
+    SG_TRY(tm_upload(h->m_tmpl, &d.m_tmpl));
+    SG_TRY(tm_upload(h->m_need, &d.m_need));
+    SG_TRY(tm_upload(h->m_flags, &d.m_flags));
+    SG_TRY(tm_upload(h->t_first, &d.t_first));
+    SG_TRY(tm_upload(h->t_count, &d.t_count));
+    SG_TRY(tm_upload(h->t_flags, &d.t_flags));
+    SG_TRY(tm_upload(h->vac, &d.vac));
+    for (auto &r : h->runs) {
+        SG_TRY(tm_upload(r.soff, &r.d_soff));
+        SG_TRY(tm_upload(r.satoms, &r.d_satoms));
+    }
+    h->dev = dev;
+    return SG_OK;
+}
+
+// ------------------------------------------------------------------ device
+constexpr uint64_t TM_NONE = ~0ull;
+
+// hits (record or row, signature) -> (record << 32 | atom); a field-row hit keeps the atom
+// whose part is the row's field (none: sentinel, dropped by the unique pass).
+__global__ __launch_bounds__(256) void k_tm_collect(const uint32_t *__restrict__ rec_idx, const uint32_t *__restrict__ sig,
+                                                    uint32_t nh, const uint32_t *__restrict__ soff,
+                                                    const uint32_t *__restrict__ satoms,
+                                                    const uint32_t *__restrict__ apart,
+                                                    const uint32_t *__restrict__ row_rec,
+                                                    const uint32_t *__restrict__ row_key, uint64_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nh) return;
+    const uint32_t r = rec_idx[i], s = sig[i];
+    uint64_t key = TM_NONE;
+    if (!row_rec) {
+        key = ((uint64_t)r << 32) | satoms[soff[s]];
+    } else {
+        const uint32_t want = row_key[r] + 1;
+        for (uint32_t q = soff[s]; q < soff[s + 1]; ++q)
+            if (apart[satoms[q]] == want) { key = ((uint64_t)row_rec[r] << 32) | satoms[q]; break; }
+    }
+    out[i] = key;
+}
+
+struct TmUniqPred {
+    const uint64_t *K;
+    __device__ uint32_t operator()(uint32_t i) const {
+        const uint64_t k = K[i];
+        return (k != TM_NONE && (i == 0 || k != K[i - 1])) ? 1u : 0u;
+    }
+};
+
+struct TmOccLen {
+    const uint64_t *K;
+    const uint32_t *U, *occ_off;
+    __device__ uint64_t operator()(uint32_t i) const {
+        const uint32_t a = (uint32_t)K[U[i]];
+        return occ_off[a + 1] - occ_off[a];
+    }
+};
+
+__global__ __launch_bounds__(256) void k_tm_expand(const uint64_t *__restrict__ K, const uint32_t *__restrict__ U,
+                                                   uint32_t nu, const uint64_t *__restrict__ offs,
+                                                   const uint32_t *__restrict__ occ_off,
+                                                   const uint32_t *__restrict__ occ_m, uint64_t *__restrict__ E) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nu) return;
+    const uint64_t k = K[U[i]];
+    const uint32_t a = (uint32_t)k;
+    const uint64_t rec = k & 0xffffffff00000000ull;
+    uint64_t o = offs[i];
+    for (uint32_t q = occ_off[a]; q < occ_off[a + 1]; ++q) E[o++] = rec | occ_m[q];
+}
+
+struct TmSegPred {
+    const uint64_t *E;
+    const uint32_t *m_tmpl;
+    __device__ uint32_t operator()(uint32_t i) const {
+        if (i == 0) return 1u;
+        const uint64_t a = E[i - 1], b = E[i];
+        return ((a >> 32) != (b >> 32) || m_tmpl[(uint32_t)a] != m_tmpl[(uint32_t)b]) ? 1u : 0u;
+    }
+};
+
+__global__ __launch_bounds__(256) void k_tm_eval(const uint64_t *__restrict__ E, uint32_t n2,
+                                                 const uint32_t *__restrict__ seg, uint32_t ns,
+                                                 const uint32_t *__restrict__ m_tmpl, const uint32_t *__restrict__ m_need,
+                                                 const uint32_t *__restrict__ m_flags,
+                                                 const uint32_t *__restrict__ t_first,
+                                                 const uint32_t *__restrict__ t_count,
+                                                 const uint32_t *__restrict__ t_flags, uint32_t *__restrict__ flag,
+                                                 uint64_t *__restrict__ segkey) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const uint32_t e1 = (s + 1 < ns) ? seg[s + 1] : n2;
+    uint32_t e = seg[s];
+    const uint64_t k0 = E[e];
+    const uint32_t t = m_tmpl[(uint32_t)k0];
+    const bool and_t = t_flags[t] & SG_TM_AND;
+    bool acc = and_t;
+    const uint32_t m0 = t_first[t], m1 = m0 + t_count[t];
+    for (uint32_t m = m0; m < m1; ++m) {
+        uint32_t cnt = 0;
+        while (e < e1 && (uint32_t)E[e] == m) { ++cnt; ++e; }
+        const uint32_t f = m_flags[m];
+        bool hit = (f & SG_TM_AND) ? cnt >= m_need[m] : cnt > 0;
+        if (f & SG_TM_NEGATIVE) hit = !hit;
+        acc = and_t ? (acc && hit) : (acc || hit);
+    }
+    flag[s] = acc ? 1u : 0u;
+    segkey[s] = (k0 & 0xffffffff00000000ull) | t;
+}
+
+struct TmFlagPred {
+    const uint32_t *flag;
+    __device__ uint32_t operator()(uint32_t i) const { return flag[i]; }
+};
+
+// (record, vacuous template) pairs with no segment: the template holds there.
+struct TmVacPred {
+    const uint64_t *segkey;
+    uint32_t ns;
+    const uint32_t *vac;
+    uint32_t nv;
+    __device__ uint32_t operator()(uint32_t i) const {
+        const uint32_t r = i / nv, t = vac[i % nv];
+        const uint64_t key = ((uint64_t)r << 32) | t;
+        uint32_t lo = 0, hi = ns;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (segkey[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        return (lo < ns && segkey[lo] == key) ? 0u : 1u;
+    }
+};
+
+__global__ __launch_bounds__(256) void k_tm_gather(const uint64_t *__restrict__ segkey, const uint32_t *__restrict__ sel,
+                                                   uint32_t nt, const uint32_t *__restrict__ vsel, uint32_t nvac,
+                                                   const uint32_t *__restrict__ vac, uint32_t nv,
+                                                   uint64_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nt) {
+        out[i] = segkey[sel[i]];
+    } else if (i < nt + nvac) {
+        const uint32_t x = vsel[i - nt];
+        out[i] = ((uint64_t)(x / nv) << 32) | vac[x % nv];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tm_split(const uint64_t *__restrict__ K, uint32_t n, uint32_t *__restrict__ rec,
+                                                  uint32_t *__restrict__ tid) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = K[i];
+    rec[i] = (uint32_t)(k >> 32);
+    tid[i] = (uint32_t)k;
+}
+
+struct TmAccum {
+    int slot_id = S_T_HITS;
+    uint64_t *p = nullptr;
+    uint64_t n = 0, cap = 0;
+};
+
+static int tm_grow(sg_ctx *c, TmAccum *a, uint64_t need) {
+    if (need <= a->cap) return SG_OK;
+    const int other = a->slot_id == S_T_HITS ? S_T_EXP : S_T_HITS;
+    const uint64_t cap = std::max<uint64_t>(std::max<uint64_t>(need, 2 * a->cap), 1u << 16);
+    uint64_t *np;
+    SG_TRY(slot(c, other, cap, &np));
+    if (a->n) SG_HIP(hipMemcpyAsync(np, a->p, a->n * 8, hipMemcpyDeviceToDevice, c->stream));
+    a->slot_id = other;
+    a->p = np;
+    a->cap = cap;
+    return SG_OK;
+}
+
+static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint64_t n, sg_dev_tmatches *res) {
+    *res = sg_dev_tmatches{};
+    SG_TRY(tm_ensure_device(h, c->device));
+    const auto &D = h->d;
+    TmAccum acc;
+    uint64_t R = 0;
+    bool have_R = false;
+    // stream 0: the records themselves
+    for (auto &run : h->runs) {
+        if (run.stream != 0) continue;
+        sg_dev_hits r;
+        SG_TRY(dev_match(c, run.m, d_buf, n, &r, false));
+        R = r.in_records;
+        have_R = true;
+        if (!r.n_hits) continue;
+        SG_TRY(tm_grow(c, &acc, acc.n + r.n_hits));
+        SG_LAUNCH(c, "tm_collect", k_tm_collect, (uint32_t)((r.n_hits + 255) / 256), 256, 0, r.rec_idx, r.sig_id,
+                  (uint32_t)r.n_hits, run.d_soff, run.d_satoms, D.atom_part, (const uint32_t *)nullptr,
+                  (const uint32_t *)nullptr, acc.p + acc.n);
+        acc.n += r.n_hits;
+    }
+    // stream 1: httpx -json field rows
+    bool any1 = false;
+    for (auto &run : h->runs) any1 |= run.stream == 1;
+    if (any1) {
+        sg_dev_rows rows;
+        SG_TRY(dev_json_fields(c, d_buf, n, h->key_blob.data(), h->key_offs.data(), (uint32_t)h->key_offs.size() - 1,
+                               &rows));
+        R = rows.in_records;
+        have_R = true;
+        for (auto &run : h->runs) {
+            if (run.stream != 1 || rows.bytes == 0) continue;
+            sg_dev_hits r;
+            SG_TRY(dev_match(c, run.m, rows.data, rows.bytes, &r, false));
+            if (!r.n_hits) continue;
+            SG_TRY(tm_grow(c, &acc, acc.n + r.n_hits));
+            SG_LAUNCH(c, "tm_collect", k_tm_collect, (uint32_t)((r.n_hits + 255) / 256), 256, 0, r.rec_idx, r.sig_id,
+                      (uint32_t)r.n_hits, run.d_soff, run.d_satoms, D.atom_part, rows.row_rec, rows.row_key,
+                      acc.p + acc.n);
+            acc.n += r.n_hits;
+        }
+    }
+    if (!have_R) {
+        Lines L;
+        SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L, false));
+        R = L.n_rec;
+    }
+    res->in_records = R;
+    if (acc.n >= (1ull << 32)) { set_error("template eval: more than 2^32 atom hits"); return SG_E_TOO_LARGE; }
+    int rbits = 1;
+    while (rbits < 32 && (1ull << rbits) < R) ++rbits;
+    const int kbits = 32 + rbits;
+    // (record, atom): sort + unique
+    uint32_t nu = 0, ns = 0, nt = 0;
+    uint64_t *E = nullptr;
+    uint64_t n2 = 0;
+    uint32_t *seg = nullptr, *flag = nullptr, *sel = nullptr;
+    uint64_t *segkey = nullptr;
+    if (acc.n) {
+        const uint32_t n1 = (uint32_t)acc.n;
+        uint64_t *k2, *K;
+        uint32_t *v1, *v2, *V;
+        SG_TRY(slot(c, S_T_K2, (size_t)n1 + 1, &k2));
+        SG_TRY(slot(c, S_T_V1, (size_t)n1 + 1, &v1));
+        SG_TRY(slot(c, S_T_V2, (size_t)n1 + 1, &v2));
+        SG_TRY(radix_sort(c, acc.p, v1, k2, v2, n1, 0, kbits, true, &K, &V, "tm_rs_atoms"));
+        SG_TRY(slot(c, S_T_SEL, (size_t)n1 + 16, &sel));
+        SG_TRY(run_select2(c, "tm_unique", TmUniqPred{K}, n1, sel, (uint32_t *)nullptr, &nu, nullptr, 16.0));
+        if (nu) {
+            uint64_t *offs;
+            SG_TRY(slot(c, S_T_OUT, (size_t)nu + 1, &offs));
+            SG_TRY(run_scan64(c, "tm_occ_scan", TmOccLen{K, sel, D.occ_off}, nu, offs, &n2));
+            if (n2 >= (1ull << 32)) { set_error("template eval: more than 2^32 matcher hits"); return SG_E_TOO_LARGE; }
+            if (n2) {
+                uint64_t *e1, *e2;
+                SG_TRY(slot(c, S_T_E, n2 + 1, &e1));
+                SG_TRY(slot(c, S_T_E2, n2 + 1, &e2));
+                SG_LAUNCH(c, "tm_expand", k_tm_expand, (nu + 255) / 256, 256, 0, K, sel, nu, offs, D.occ_off, D.occ_m, e1);
+                uint32_t *w1, *w2, *WV;
+                SG_TRY(slot(c, S_T_V1, n2 + 1, &w1));
+                SG_TRY(slot(c, S_T_V2, n2 + 1, &w2));
+                SG_TRY(radix_sort(c, e1, w1, e2, w2, (uint32_t)n2, 0, kbits, true, &E, &WV, "tm_rs_matchers"));
+                SG_TRY(slot(c, S_T_SEG, n2 + 16, &seg));
+                SG_TRY(run_select2(c, "tm_segments", TmSegPred{E, D.m_tmpl}, (uint32_t)n2, seg, (uint32_t *)nullptr, &ns,
+                                   nullptr, 24.0));
+                SG_TRY(slot(c, S_T_FLAG, (size_t)ns + 16, &flag));
+                SG_TRY(slot(c, S_T_O, (size_t)ns + 16, &segkey));
+                SG_LAUNCH(c, "tm_eval", k_tm_eval, (ns + 255) / 256, 256, 0, E, (uint32_t)n2, seg, ns, D.m_tmpl, D.m_need,
+                          D.m_flags, D.t_first, D.t_count, D.t_flags, flag, segkey);
+                SG_TRY(slot(c, S_T_SEL, (size_t)ns + 16, &sel));  // segments may outnumber the atom hits
+                SG_TRY(run_select2(c, "tm_true", TmFlagPred{flag}, ns, sel, (uint32_t *)nullptr, &nt, nullptr, 4.0));
+            }
+        }
+    }
+    // vacuous templates on records without a segment for them
+    const uint32_t nv = (uint32_t)h->vac.size();
+    uint32_t nvac = 0;
+    uint32_t *vsel = nullptr;
+    if (nv && R) {
+        const uint64_t items = R * nv;
+        if (items >= (1ull << 32)) { set_error("template eval: records x vacuous templates exceeds 2^32"); return SG_E_TOO_LARGE; }
+        SG_TRY(slot(c, S_T_HITS, items + 16, &vsel));
+        uint64_t *sk = segkey;
+        if (!sk) SG_TRY(slot(c, S_T_O, 16, &sk));
+        SG_TRY(run_select2(c, "tm_vacuous", TmVacPred{sk, ns, D.vac, nv}, (uint32_t)items, vsel, (uint32_t *)nullptr, &nvac,
+                           nullptr, 8.0));
+    }
+    const uint64_t nout = (uint64_t)nt + nvac;
+    res->n = nout;
+    if (nout == 0) return SG_OK;
+    uint64_t *o1, *o2, *OK;
+    uint32_t *u1, *u2, *UV;
+    SG_TRY(slot(c, S_T_OUT, nout + 1, &o1));
+    SG_TRY(slot(c, S_T_K2, nout + 1, &o2));
+    SG_TRY(slot(c, S_T_V1, nout + 1, &u1));
+    SG_TRY(slot(c, S_T_V2, nout + 1, &u2));
+    SG_LAUNCH(c, "tm_gather", k_tm_gather, (uint32_t)((nout + 255) / 256), 256, 0, segkey, sel, nt, vsel, nvac, D.vac,
+              nv ? nv : 1u, o1);
+    if (nvac && nt) SG_TRY(radix_sort(c, o1, u1, o2, u2, (uint32_t)nout, 0, kbits, true, &OK, &UV, "tm_rs_out"));
+    else OK = o1;  // one sorted source: segment keys or the (record, vacuous) grid order
+    uint32_t *rec, *tid;
+    SG_TRY(slot(c, S_T_REC, nout + 1, &rec));
+    SG_TRY(slot(c, S_T_TID, nout + 1, &tid));
+    SG_LAUNCH(c, "tm_split", k_tm_split, (uint32_t)((nout + 255) / 256), 256, 0, OK, (uint32_t)nout, rec, tid);
+    res->rec_idx = rec;
+    res->tmpl_id = tid;
+    return SG_OK;
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" {
+
+int sg_tmpl_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats, const sg_tm_matcher *ms,
+                    uint32_t n_matchers, const uint32_t *tmpl_flags, uint32_t n_templates, const uint8_t *keys,
+                    const uint32_t *key_offs, uint32_t n_keys, sg_templates **out) {
+    if (!out || (n_pats && (!pats || !pat_offs)) || (n_matchers && !ms) || (n_templates && !tmpl_flags) ||
+        (n_keys && (!keys || !key_offs))) {
+        set_error("sg_tmpl_compile: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (n_keys > 64) { set_error("sg_tmpl_compile: at most 64 field keys"); return SG_E_INVAL; }
+    std::unique_ptr<sg_templates> h(new sg_templates());
+    h->n_tmpl = n_templates;
+    h->n_match = n_matchers;
+    h->key_offs.assign(1, 0);
+    for (uint32_t k = 0; k < n_keys; ++k) {
+        h->key_blob.insert(h->key_blob.end(), keys + key_offs[k], keys + key_offs[k + 1]);
+        h->key_offs.push_back((uint32_t)h->key_blob.size());
+    }
+    if (h->key_blob.empty()) h->key_blob.push_back(0);
+    h->t_first.assign(n_templates, 0);
+    h->t_count.assign(n_templates, 0);
+    h->t_flags.assign(tmpl_flags, tmpl_flags + n_templates);
+    // atoms: (part, kind, nocase, bytes)
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t, std::string>, uint32_t> atoms;
+    std::vector<std::vector<uint32_t>> m_atoms(n_matchers);
+    std::vector<std::tuple<uint32_t, uint32_t, uint32_t, std::string>> atom_key;
+    for (uint32_t i = 0; i < n_matchers; ++i) {
+        const sg_tm_matcher &m = ms[i];
+        if (m.tmpl >= n_templates || (i && m.tmpl < ms[i - 1].tmpl)) {
+            set_error("matcher %u: template ids must be < n_templates and non-decreasing", i);
+            return SG_E_INVAL;
+        }
+        if (m.kind > SG_TM_REGEX || m.part > n_keys || m.count == 0 || (uint64_t)m.first + m.count > n_pats) {
+            set_error("matcher %u: bad kind/part/pattern range", i);
+            return SG_E_INVAL;
+        }
+        if (h->t_count[m.tmpl] == 0) h->t_first[m.tmpl] = i;
+        h->t_count[m.tmpl]++;
+        // case-insensitive applies to words (nuclei lowercases words and part); regexes use (?i)
+        const uint32_t nc = ((m.flags & SG_TM_NOCASE) && m.kind == SG_TM_WORD) ? 1u : 0u;
+        for (uint32_t q = m.first; q < m.first + m.count; ++q) {
+            std::string s((const char *)pats + pat_offs[q], pat_offs[q + 1] - pat_offs[q]);
+            if (s.empty()) { set_error("matcher %u: empty pattern", i); return SG_E_INVAL; }
+            if (nc && m.kind == SG_TM_WORD)
+                for (auto &ch : s) if (ch >= 'A' && ch <= 'Z') ch = (char)(ch + 32);
+            auto key = std::make_tuple(m.part, m.kind, nc, s);
+            auto it = atoms.find(key);
+            uint32_t a;
+            if (it == atoms.end()) {
+                a = (uint32_t)atom_key.size();
+                atoms.emplace(key, a);
+                atom_key.push_back(key);
+            } else {
+                a = it->second;
+            }
+            m_atoms[i].push_back(a);
+        }
+        std::sort(m_atoms[i].begin(), m_atoms[i].end());
+        m_atoms[i].erase(std::unique(m_atoms[i].begin(), m_atoms[i].end()), m_atoms[i].end());
+        h->m_tmpl.push_back(m.tmpl);
+        h->m_need.push_back((uint32_t)m_atoms[i].size());
+        h->m_flags.push_back(m.flags);
+    }
+    for (uint32_t t = 0; t < n_templates; ++t)
+        if (h->t_count[t] == 0) { set_error("template %u has no matchers", t); return SG_E_INVAL; }
+    h->n_atoms = (uint32_t)atom_key.size();
+    // atom -> matchers (CSR)
+    std::vector<std::vector<uint32_t>> occ(h->n_atoms);
+    for (uint32_t i = 0; i < n_matchers; ++i)
+        for (uint32_t a : m_atoms[i]) occ[a].push_back(i);
+    h->occ_off.assign(1, 0);
+    for (auto &v : occ) {
+        h->occ_m.insert(h->occ_m.end(), v.begin(), v.end());
+        h->occ_off.push_back((uint32_t)h->occ_m.size());
+    }
+    h->atom_part.resize(h->n_atoms);
+    // engines: (stream, kind, nocase) over the distinct pattern bytes of that group
+    std::map<std::tuple<int, uint32_t, uint32_t>, std::map<std::string, std::vector<uint32_t>>> groups;
+    for (uint32_t a = 0; a < h->n_atoms; ++a) {
+        const auto &k = atom_key[a];
+        h->atom_part[a] = std::get<0>(k);
+        const std::string &s = std::get<3>(k);
+        // a word holding '\n' can never occur inside a record or a row: it never hits
+        if (std::get<1>(k) == SG_TM_WORD && s.find('\n') != std::string::npos) continue;
+        const int stream = std::get<0>(k) == 0 ? 0 : 1;
+        groups[std::make_tuple(stream, std::get<1>(k), std::get<2>(k))][s].push_back(a);
+    }
+    for (auto &g : groups) {
+        TmRun run;
+        run.stream = std::get<0>(g.first);
+        const uint32_t kind = std::get<1>(g.first), nc = std::get<2>(g.first);
+        std::vector<uint8_t> blob;
+        std::vector<uint32_t> offs(1, 0);
+        run.soff.assign(1, 0);
+        for (auto &kv : g.second) {
+            blob.insert(blob.end(), kv.first.begin(), kv.first.end());
+            offs.push_back((uint32_t)blob.size());
+            run.satoms.insert(run.satoms.end(), kv.second.begin(), kv.second.end());
+            run.soff.push_back((uint32_t)run.satoms.size());
+        }
+        const uint32_t flags = nc ? SG_NOCASE : 0u;
+        int rc = kind == SG_TM_WORD
+                     ? sg_ac_compile(blob.data(), offs.data(), (uint32_t)(offs.size() - 1), flags, &run.m)
+                     : sg_dfa_compile(blob.data(), offs.data(), (uint32_t)(offs.size() - 1), flags, &run.m);
+        if (rc != SG_OK) {
+            for (auto &r : h->runs) sg_free(r.m);
+            return rc;
+        }
+        h->runs.push_back(std::move(run));
+    }
+    // vacuous templates: true with no evidence at all (every matcher count 0)
+    for (uint32_t t = 0; t < n_templates; ++t) {
+        const bool and_t = h->t_flags[t] & SG_TM_AND;
+        bool acc = and_t;
+        for (uint32_t m = h->t_first[t]; m < h->t_first[t] + h->t_count[t]; ++m) {
+            const bool hit = (h->m_flags[m] & SG_TM_NEGATIVE) != 0;
+            acc = and_t ? (acc && hit) : (acc || hit);
+        }
+        if (acc) h->vac.push_back(t);
+    }
+    *out = h.release();
+    return SG_OK;
+}
+
+int sg_tmpl_info(const sg_templates *h, uint32_t *n_atoms, uint32_t *n_engines, uint32_t *n_vacuous) {
+    if (!h) return SG_E_INVAL;
+    if (n_atoms) *n_atoms = h->n_atoms;
+    if (n_engines) *n_engines = (uint32_t)h->runs.size();
+    if (n_vacuous) *n_vacuous = (uint32_t)h->vac.size();
+    return SG_OK;
+}
+
+int sg_dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, size_t n, sg_dev_tmatches *res) {
+    if (!c || !h || !res || (!d_buf && n)) { set_error("sg_dev_tmpl_eval: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b = d_buf;
+    if (((uintptr_t)d_buf & 15) != 0) {
+        uint8_t *a;
+        SG_TRY(slot(c, S_IN, n + 16, &a));
+        if (n) SG_HIP(hipMemcpyAsync(a, d_buf, n, hipMemcpyDeviceToDevice, c->stream));
+        b = a;
+    }
+    return dev_tmpl_eval(c, h, b, n, res);
+}
+
+int sg_tmpl_eval(sg_templates *h, const uint8_t *buf, size_t n, uint32_t *rec_idx, uint32_t *tmpl_id, size_t cap,
+                 size_t *n_out) {
+    if (!h || !n_out || (!buf && n)) { set_error("sg_tmpl_eval: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    int dev = 0;
+    SG_TRY(pick_device(&dev));
+    sg_ctx *c = nullptr;
+    SG_TRY(pool_acquire(dev, &c));
+    struct Rel { sg_ctx *c; ~Rel() { pool_release(c); } } rel{c};
+    SG_HIP(hipSetDevice(dev));
+    uint8_t *d;
+    SG_TRY(slot(c, S_IN, n + 16, &d));
+    if (n) SG_HIP(hipMemcpyAsync(d, buf, n, hipMemcpyHostToDevice, c->stream));
+    sg_dev_tmatches r;
+    SG_TRY(dev_tmpl_eval(c, h, d, n, &r));
+    *n_out = r.n;
+    if (r.n > cap) { SG_HIP(hipStreamSynchronize(c->stream)); set_error("output capacity too small"); return SG_E_CAP; }
+    if (r.n) {
+        SG_HIP(hipMemcpyAsync(rec_idx, r.rec_idx, 4 * r.n, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipMemcpyAsync(tmpl_id, r.tmpl_id, 4 * r.n, hipMemcpyDeviceToHost, c->stream));
+    }
+    SG_HIP(hipStreamSynchronize(c->stream));
+    return SG_OK;
+}
+
+void sg_tmpl_free(sg_templates *h) {
+    if (!h) return;
+    if (h->dev >= 0) { (void)hipSetDevice(h->dev); tm_free_dev(h); }
+    for (auto &r : h->runs) sg_free(r.m);
+    delete h;
+}
+
+}  // extern "C"
