@@ -239,6 +239,20 @@ int sg_tmpl_eval(sg_templates *h, const uint8_t *buf, size_t n, uint32_t *rec_id
                  size_t cap, size_t *n_out);
 void sg_tmpl_free(sg_templates *h);
 
+/* ------------------------------------------------------------------ streamed merge ingestion
+ * instead of building the /raw body with `str +=`
+ * (server/server.py:407-410), the server appends every chunk body — or each piece of one
+ * as it streams from S3 — in the A5 key order (server/server.py:403-404). Pieces go
+ * through two pinned staging buffers with async H2D copies on the context's stream, so
+ * the merged body (concatenation, no separator, byte-identical to A5) is resident in HBM
+ * when the last body ends. sg_ingest_finish returns the device buffer (owned by the
+ * ingest handle, valid until sg_ingest_close) for sg_dev_dedup_diff / sg_dev_match. */
+typedef struct sg_ingest sg_ingest;
+int sg_ingest_open(sg_ctx *ctx, size_t size_hint, sg_ingest **out);
+int sg_ingest_append(sg_ingest *s, const uint8_t *data, size_t n);
+int sg_ingest_finish(sg_ingest *s, const uint8_t **d_buf, uint64_t *n);
+int sg_ingest_close(sg_ingest *s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,7 +5,7 @@ Importing the package loads libswarmgpu.so and raises if it is missing: there is
 fallback on the product path.
 """
 from .api import (Context, Matcher, dedup, dedup_chunks, dedup_diff, device_count, diff, hash64,
-                  Templates, json_fields, lines, nmap_ports, records)
+                  Ingest, Templates, json_fields, lines, nmap_ports, records)
 
 __all__ = ["Context", "Matcher", "dedup", "dedup_chunks", "dedup_diff", "device_count", "diff",
-           "hash64", "json_fields", "lines", "nmap_ports", "records", "Templates"]
+           "hash64", "json_fields", "lines", "nmap_ports", "records", "Templates", "Ingest"]

@@ -148,3 +148,14 @@ for _name, (_res, _args) in {
     _f = getattr(lib, _name)
     _f.restype = _res
     _f.argtypes = _args
+
+EXPORTS += ["sg_ingest_open", "sg_ingest_append", "sg_ingest_finish", "sg_ingest_close"]
+for _name, (_res, _args) in {
+    "sg_ingest_open": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "sg_ingest_append": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "sg_ingest_finish": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    "sg_ingest_close": (C.c_int, [C.c_void_p]),
+}.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args

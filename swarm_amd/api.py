@@ -379,3 +379,52 @@ class Templates:
         r = _abi.DevTMatches()
         check(lib.sg_dev_tmpl_eval(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(r)))
         return r
+
+
+class Ingest:
+    """Streamed /raw merge (§8(f) row 4): append chunk bodies (or pieces of them, as they
+    stream from S3) in the A5 key order; finish() returns the merged body resident in HBM
+    (device pointer, length), byte-identical to server/server.py:407-410's concatenation."""
+
+    def __init__(self, ctx: "Context", size_hint: int = 0):
+        self.ctx = ctx
+        self._h = C.c_void_p()
+        check(lib.sg_ingest_open(ctx._h, size_hint, C.byref(self._h)))
+
+    def append(self, piece) -> None:
+        a = _view(piece)
+        if a.size:
+            check(lib.sg_ingest_append(self._h, a.ctypes.data, a.size))
+
+    def finish(self) -> Tuple[int, int]:
+        d, n = C.c_void_p(), C.c_uint64()
+        check(lib.sg_ingest_finish(self._h, C.byref(d), C.byref(n)))
+        return d.value or 0, n.value
+
+    def dedup_diff(self, prior=None) -> Tuple[bytes, bytes]:
+        """(sort -u of the merged body, new records vs `prior`) as bytes."""
+        d, n = self.finish()
+        pd, pn, keep = 0, 0, None
+        if prior:
+            import torch
+            keep = torch.from_numpy(np.array(_view(prior))).cuda(self.ctx.device)
+            pd, pn = keep.data_ptr(), keep.numel()
+        r = self.ctx.dedup_diff(d, n, pd, pn)
+        return self.ctx.to_bytes(r.uniq, r.uniq_bytes), self.ctx.to_bytes(r.fresh, r.fresh_bytes)
+
+    def close(self):
+        if self._h:
+            lib.sg_ingest_close(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

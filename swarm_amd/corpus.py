@@ -86,8 +86,8 @@ def _flatten(mat: np.ndarray, msk: np.ndarray, sep: int = 0x0A) -> np.ndarray:
     return full[fm]
 
 
-def subdomains(n: int, seed: int = 1234, universe: int | None = None, chunk: int = 1 << 20) -> np.ndarray:
-    """n subdomain lines (uint8 array, '\\n'-terminated) drawn from a universe of ids."""
+def subdomains(n: int, seed: int = 1234, universe: int | None = None, chunk: int = 1 << 20) -> tuple:
+    """(n subdomain lines as a '\\n'-terminated uint8 array, their universe ids)."""
     U = universe or max(n, 1)
     rng = np.random.default_rng(seed)
     ids = rng.integers(0, U, size=n, dtype=np.uint64)

@@ -69,7 +69,23 @@ def postprocess_output(output_file: str, matcher=None, matches_file: Optional[st
         data = f.read()
     n = len(api.lines(data))
     if matcher is not None and matches_file:
-        lines_out, _hits = matcher.match_lines(data)
+        lines_out = matcher.match_lines(data)
         with open(matches_file, "wb") as f:
             f.write(lines_out)
     return n
+
+
+def raw_stream_dedup_diff(ctx, keys: Iterable[str], scan_id: str, read_body, prior_unique: Optional[bytes] = None,
+                          sizes: Optional[Dict[str, int]] = None) -> Tuple[bytes, bytes]:
+    """/raw + completion without the `str +=` merge (server/server.py:399-412, §8(f) row 4):
+    `read_body(key)` yields the pieces of one S3 object body (e.g. botocore's
+    StreamingBody.iter_chunks()); they are appended straight into pinned staging buffers
+    and copied to HBM in A5 key order while the next piece is read. `sizes` (key ->
+    ContentLength from the listing) pre-sizes the device buffer."""
+    order = merge_keys(keys, scan_id)
+    hint = sum(sizes.get(k, 0) for k in order) if sizes else 0
+    with api.Ingest(ctx, hint) as ing:
+        for k in order:
+            for piece in read_body(k):
+                ing.append(piece)
+        return ing.dedup_diff(prior_unique)
