@@ -30,7 +30,9 @@ METRIC = "scan records/sec + GB/s (vs HBM roofline) for match+dedup+diff, 1 and 
 # library stat name -> HIP kernel symbol (rocprofv3 -T names) for the PMC traffic lookup
 KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_uniq": "k_emit_uniq",
                  "emit_fresh": "k_emit_fresh", "diff_tile": "k_diff_tile", "adjacent": "k_adjacent",
-                 "lines": "k_lines", "lit_match": "k_lit_scan", "dfa_match": "k_dfa_match", "ac_match": "k_ac_match"}
+                 "lines": "k_lines", "lit_match": "k_lit_scan", "dfa_match": "k_dfa_match", "ac_match": "k_ac_match",
+                 "re_prefilter": "k_lit_scan", "re_verify": "k_verify", "json_scan": "k_json_scan",
+                 "json_emit": "k_json_emit", "tm_eval": "k_tm_eval", "tm_collect": "k_tm_collect"}
 
 
 def pmc_traffic(workload, kernel):
@@ -229,13 +231,91 @@ def bench_c4(args):
     ctx.close()
 
 
+def field_templates():
+    """The template corpus (tests/golden/templates.json, record part) plus tech-detect-style
+    templates on httpx -json fields (title / webserver / tech)."""
+    import base64
+    from swarm_amd import corpus
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "templates.json")))
+    T = [dict(t, matchers=[dict(m, patterns=[base64.b64decode(p) for p in m["patterns"]]) for m in t["matchers"]])
+         for t in d["templates"]]
+    for tech in corpus._TECH:
+        T.append({"condition": "or", "matchers": [{"type": "word", "part": "tech", "condition": "or",
+                                                   "patterns": [tech.split(b":")[0]]}]})
+    for srv in corpus.SERVERS:
+        T.append({"condition": "and", "matchers": [
+            {"type": "word", "part": "webserver", "patterns": [srv.split(b"/")[0]]},
+            {"type": "word", "part": "title", "patterns": [b"Login", b"Admin"], "negative": True}]})
+    T.append({"condition": "or", "matchers": [{"type": "regex", "part": "title", "patterns": [rb"(?i)index of /"]}]})
+    return T
+
+
+def bench_fields(args):
+    """SURVEY.md §8(f) rows 1+3: httpx -json result lines -> field rows (url, title,
+    webserver, tech) and nuclei matcher logic (the 1,006 word/regex templates of the
+    reference corpus on the record + 31 field templates) per GPU. One step = field
+    extraction + template evaluation over the whole batch."""
+    import numpy as np
+    import torch
+
+    import swarm_amd
+    from swarm_amd import corpus
+
+    torch.cuda.set_device(0)
+    n_lines = args.lines if args.lines != 10_000_000 else 4_000_000
+    buf = corpus.lines_from_pool(corpus.httpx_json_pool(1 << 14, seed=5), n_lines, seed=6)
+    d = torch.from_numpy(buf).cuda()
+    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    keys = [b"url", b"title", b"webserver", b"tech"]
+    T = field_templates()
+    tm = swarm_amd.Templates(T, keys)
+    holder = {}
+
+    def run():
+        holder["rows"] = ctx.json_fields(d.data_ptr(), d.numel(), keys)
+        return tm.dev_match(ctx, d.data_ptr(), d.numel())
+    el, full, stats, dominant, r = timed_steps(ctx, run, args)
+    R = int(r.in_records)
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import semantics as S
+        m_s = 300
+        cut = int(np.flatnonzero(buf == 10)[m_s - 1]) + 1
+        sample = buf[:cut].tobytes()
+        tc = time.perf_counter()
+        want = S.template_matches(sample, T, keys)
+        rows = S.json_field_rows(sample, keys)
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(m_s / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d httpx -json lines: oracle field rows + %d templates, 1 thread, %.2f s" % (m_s, len(T), tc),
+               "host_cpus": os.cpu_count()}
+        cpu["gpu_bit_exact_on_sample"] = (tm.match(sample) == want and
+                                          swarm_amd.json_fields(sample, keys)[0] == rows[0])
+    print(json.dumps({
+        "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (httpx -json lines, Go-style escaping; template corpus from the reference)",
+        "config": {"workload": "F: %.1fM httpx -json lines -> 4 field keys + %d nuclei templates per GPU"
+                               % (n_lines / 1e6, len(T)), "bytes": int(d.numel()), "templates": tm.info()},
+        "gbps": round(d.numel() * args.steps / el / 1e9, 2),
+        "records": {"in": R, "field_rows": int(holder["rows"].rows), "template_matches": int(r.n)},
+        "roofline": roofline_of(stats, dominant, "fields"),
+        "cpu_baseline": cpu,
+        "kernels": kernel_table(full),
+        "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
+                        "HIP events only around the dominant kernel",
+    }), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lines", type=int, default=10_000_000)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "fields"], default="c2")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real runs; gloo rehearses N ranks on fewer GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -245,6 +325,8 @@ def main():
         return bench_c3(args)
     if args.workload == "c4":
         return bench_c4(args)
+    if args.workload == "fields":
+        return bench_fields(args)
 
     import numpy as np
     import torch

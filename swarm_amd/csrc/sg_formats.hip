@@ -19,6 +19,8 @@
 //     '\n'-terminated decoded values — the buffer is itself a line buffer, so the A4
 //     matchers run on it unchanged (part-scoped matching, §8(f) row 3).
 #include "sg_internal.hpp"
+
+#include <stdlib.h>
 #include "sg_prims_host.hpp"
 
 namespace sg {
@@ -405,6 +407,114 @@ __global__ __launch_bounds__(JS_BLOCK) void k_json_scan(JsonArgs a) {
     }
 }
 
+// One thread per record: the record is read with aligned 16-byte loads and walked byte by
+// byte with the same state machine as the wave walker (string/escape state, depth, key at a
+// depth-1 colon, value end at a depth-1 comma or the closing brace, whitespace-only
+// framing). Per-thread key spans live in LDS. Requested keys are pre-filtered by length
+// and first byte before a byte compare.
+constexpr int JT_BLOCK = 128;
+__global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
+    extern __shared__ uint2 s_span[];  // JT_BLOCK * nkeys
+    __shared__ uint8_t s_keys[JS_KEYBYTES];
+    __shared__ uint32_t s_koff[JS_MAXKEYS + 1];
+    __shared__ uint32_t s_kid[JS_MAXKEYS];  // klen | first byte << 16
+    for (uint32_t q = threadIdx.x; q <= a.nkeys; q += JT_BLOCK) s_koff[q] = a.key_offs[q];
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < s_koff[a.nkeys]; q += JT_BLOCK) s_keys[q] = a.keys[q];
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < a.nkeys; q += JT_BLOCK) {
+        const uint32_t kl = s_koff[q + 1] - s_koff[q];
+        s_kid[q] = kl | ((kl ? (uint32_t)s_keys[s_koff[q]] : 0x100u) << 16);
+    }
+    __syncthreads();
+    const uint32_t nk = a.nkeys;
+    uint2 *my = s_span + threadIdx.x * nk;
+    for (uint32_t r = blockIdx.x * JT_BLOCK + threadIdx.x; r < a.R; r += gridDim.x * JT_BLOCK) {
+        const uint2 sp = a.spans[r];
+        for (uint32_t k = 0; k < nk; ++k) my[k] = make_uint2(JS_NONE, 0);
+        uint32_t depth = 0, str_s = 0, str_e = 0, val_s = 0, open_pos = JS_NONE, close_pos = JS_NONE;
+        uint32_t first_nws = JS_NONE, last_nws = 0, c0 = 0;
+        int cur_key = -1;
+        bool in_str = false, esc = false, bad = false, done = false;
+        for (uint32_t w = sp.x & ~15u; w < sp.y && !bad; w += 16) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
+            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t q = w + j;
+                if (q < sp.x || q >= sp.y || bad) continue;
+                const uint32_t b = (wd[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                if (!js_ws((uint8_t)b)) {
+                    if (first_nws == JS_NONE) first_nws = q;
+                    last_nws = q;
+                }
+                if (in_str) {
+                    if (q == str_s) c0 = b;
+                    if (esc) esc = false;
+                    else if (b == '\\') esc = true;
+                    else if (b == '"') { in_str = false; str_e = q; }
+                    continue;
+                }
+                if (b == '"') {
+                    if (depth == 0) bad = true;
+                    in_str = true;
+                    str_s = q + 1;
+                    c0 = 0x100u;
+                } else if (b == '{' || b == '[' || b == '}' || b == ']' || b == ':' || b == ',') {
+                    if (done) { bad = true; continue; }
+                    if (b == '{' || b == '[') {
+                        if (depth == 0) {
+                            if (b != '{') bad = true;
+                            open_pos = q;
+                        }
+                        ++depth;
+                    } else if (b == '}' || b == ']') {
+                        if (depth == 0) { bad = true; continue; }
+                        if (depth == 1) {
+                            if (b != '}') bad = true;
+                            if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
+                            cur_key = -1;
+                            done = true;
+                            close_pos = q;
+                        }
+                        --depth;
+                    } else if (depth == 1) {
+                        if (b == ':') {
+                            const uint32_t kl = str_e - str_s;
+                            const uint32_t id = kl | ((kl ? c0 : 0x100u) << 16);
+                            cur_key = -1;
+                            for (uint32_t k = 0; k < nk; ++k) {
+                                if (s_kid[k] != id) continue;
+                                bool eq = true;
+                                for (uint32_t x = 1; x < kl && eq; ++x) eq = a.buf[str_s + x] == s_keys[s_koff[k] + x];
+                                if (eq) { cur_key = (int)k; break; }
+                            }
+                            val_s = q + 1;
+                        } else {  // ','
+                            if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
+                            cur_key = -1;
+                        }
+                    }
+                }
+            }
+        }
+        const bool ok = !bad && !in_str && depth == 0 && done && first_nws == open_pos && last_nws == close_pos;
+        for (uint32_t k = 0; k < nk; ++k) {
+            uint4 d = make_uint4(0, 0, 0, 0);
+            const uint2 vsp = my[k];
+            if (ok && vsp.x != JS_NONE) {
+                uint32_t vs = vsp.x, ve = vsp.y;
+                while (vs < ve && js_ws(a.buf[vs])) ++vs;
+                while (ve > vs && js_ws(a.buf[ve - 1])) --ve;
+                JsCount cnt;
+                js_value(a.buf, vs, ve, cnt);
+                d = make_uint4(vs, ve, cnt.rows, cnt.bytes);
+            }
+            a.desc[(size_t)r * nk + k] = d;
+        }
+    }
+}
+
 // packed (bytes << 32 | rows) per (record, key). Rows never outgrow the input: each
 // value's rows are no longer than its raw text plus the delimiter that follows it, so
 // the output total stays below the 4 GiB input limit and the fields never carry.
@@ -475,8 +585,15 @@ int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *
     SG_TRY(slot(c, S_F_DESC, items + 1, &desc));
     SG_TRY(slot(c, S_F_OFFS, items + 1, &offs));
     JsonArgs ja{d_buf, L.spans, R, d_keys, d_koff, nkeys, desc};
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((R + 3) / 4, 256u * 16u);
-    SG_LAUNCH_B(c, "json_scan", (double)n + 16.0 * items, k_json_scan, grid, JS_BLOCK, 0, ja);
+    static const bool wave_walk = getenv("SG_JSON_WAVE") != nullptr;
+    if (wave_walk) {
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((R + 3) / 4, 256u * 16u);
+        SG_LAUNCH_B(c, "json_scan", (double)n + 16.0 * items, k_json_scan, grid, JS_BLOCK, 0, ja);
+    } else {
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((R + JT_BLOCK - 1) / JT_BLOCK, 256u * 16u);
+        SG_LAUNCH_B(c, "json_scan", (double)n + 16.0 * items, k_json_scan_t, grid, JT_BLOCK,
+                    JT_BLOCK * nkeys * sizeof(uint2), ja);
+    }
     uint64_t total = 0;
     SG_TRY(run_scan64(c, "json_scan_len", JsonLen{desc}, (uint32_t)items, offs, &total));
     const uint64_t rows = total & 0xffffffffu, bytes = total >> 32;

@@ -28,6 +28,10 @@ step "bench c4"
 timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 > "$OUT/bench_c4.json" 2> "$OUT/bench_c4.err" || { tail -20 "$OUT/bench_c4.err"; exit 1; }
 cat "$OUT/bench_c4.json"
 
+step "bench fields"
+timeout -k 10 300 python -u bench.py --workload fields --steps 3 --warmup 1 > "$OUT/bench_fields.json" 2> "$OUT/bench_fields.err" || { tail -20 "$OUT/bench_fields.err"; exit 1; }
+cat "$OUT/bench_fields.json"
+
 step "rocprofv3 stats c2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_c2" -o c2 --output-format csv -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof_c2.json" 2> "$OUT/prof_c2.err" || { tail -20 "$OUT/prof_c2.err"; exit 1; }
@@ -39,6 +43,10 @@ step "rocprofv3 stats c4"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_c4" -o c4 --output-format csv -- \
     python3 bench.py --workload c4 --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_c4.json" 2> "$OUT/prof_c4.err" || { tail -20 "$OUT/prof_c4.err"; exit 1; }
 
+step "rocprofv3 stats fields"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_fields" -o fields --output-format csv -- \
+    python3 bench.py --workload fields --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_fields.json" 2> "$OUT/prof_fields.err" || { tail -20 "$OUT/prof_fields.err"; exit 1; }
+
 for ctr in FETCH_SIZE WRITE_SIZE; do
   step "pmc $ctr c2"
   timeout -s KILL 240 rocprofv3 --pmc $ctr -T -d "$OUT/pmc_c2_$ctr" -o p --output-format csv -- \
@@ -49,5 +57,8 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   step "pmc $ctr c4"
   timeout -s KILL 240 rocprofv3 --pmc $ctr -T -d "$OUT/pmc_c4_$ctr" -o p --output-format csv -- \
       python3 bench.py --workload c4 --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/pmc_c4_$ctr.json" 2> "$OUT/pmc_c4_$ctr.err" || { tail -20 "$OUT/pmc_c4_$ctr.err"; exit 1; }
+  step "pmc $ctr fields"
+  timeout -s KILL 240 rocprofv3 --pmc $ctr -T -d "$OUT/pmc_fields_$ctr" -o p --output-format csv -- \
+      python3 bench.py --workload fields --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fields_$ctr.json" 2> "$OUT/pmc_fields_$ctr.err" || { tail -20 "$OUT/pmc_fields_$ctr.err"; exit 1; }
 done
 step "done"
