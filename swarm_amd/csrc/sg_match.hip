@@ -252,7 +252,8 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
             } else {
                 b = 10;
                 static const uint32_t cap4 = getenv("SG_LIT_BITS4") ? (uint32_t)atoi(getenv("SG_LIT_BITS4")) : 18u;
-                while (b < (c == 2 ? 15u : cap4) && (1ull << b) < 64ull * cnt[c]) ++b;
+                static const uint32_t extra = getenv("SG_LIT_EXTRA") ? (uint32_t)atoi(getenv("SG_LIT_EXTRA")) : 0u;
+                while (b < (c == 2 ? 15u : cap4) && (1ull << b) < (64ull << extra) * cnt[c]) ++b;
             }
         }
         T->bits[c] = b;
