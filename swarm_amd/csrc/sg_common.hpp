@@ -103,6 +103,13 @@ inline int slot(sg_ctx *c, int s, size_t count, T **out) {
     *out = (T *)p;
     return rc;
 }
+// Element capacity a slot already holds for T (0 if unallocated): callers that size an
+// output by an upper bound reuse a larger existing slot without growing it (slot() adds
+// its own headroom, so feeding slot_cap back into a request would compound).
+template <class T>
+inline uint64_t slot_elems(const sg_ctx *c, int s) {
+    return c->slot_cap[s] > 64 ? (c->slot_cap[s] - 64) / sizeof(T) : 0;
+}
 int ctx_readback(sg_ctx *c, void *host, const void *dev, size_t bytes);  // sync on stream
 int ctx_harvest(sg_ctx *c);
 int prof_begin(sg_ctx *c, const char *name, int *stat, hipEvent_t *a);

@@ -47,11 +47,13 @@ struct sg_matcher {
     bool has_pre = false;
     Table pre;
     std::vector<uint32_t> fac_off, fac_pids;
-    std::vector<uint32_t> s_delta, s_off, s_C, s_eol, s_acc_off, single_of_pid;
+    std::vector<uint16_t> s_delta;  // single-pattern DFAs have <= 65535 states
+    std::vector<uint32_t> s_off, s_C, s_eol, s_acc_off, single_of_pid;
     std::vector<uint8_t> s_cls, s_acc;
     uint32_t n_singles = 0;
     struct DevPlan {
-        uint32_t *fac_off = nullptr, *fac_pids = nullptr, *s_delta = nullptr, *s_off = nullptr, *s_C = nullptr,
+        uint16_t *s_delta = nullptr;
+        uint32_t *fac_off = nullptr, *fac_pids = nullptr, *s_off = nullptr, *s_C = nullptr,
                  *s_eol = nullptr, *s_acc_off = nullptr, *single_of_pid = nullptr;
         uint8_t *s_cls = nullptr, *s_acc = nullptr;
     } dplan;
@@ -1033,7 +1035,8 @@ struct VerifyArgs {
     const uint2 *spans;
     const unsigned long long *cand;
     uint32_t n_cand;
-    const uint32_t *s_delta, *s_off, *s_C, *s_eol, *s_acc_off, *single_of_pid;
+    const uint16_t *s_delta;
+    const uint32_t *s_off, *s_C, *s_eol, *s_acc_off, *single_of_pid;
     const uint8_t *s_cls, *s_acc;
     unsigned long long *hits;
     uint32_t *hit_count;
@@ -1043,7 +1046,7 @@ struct VerifyArgs {
 __device__ __forceinline__ bool verify_one(const VerifyArgs &a, unsigned long long cd) {
     const uint32_t r = (uint32_t)(cd >> 32), pid = (uint32_t)cd;
     const uint32_t k = a.single_of_pid[pid];
-    const uint32_t *D = a.s_delta + a.s_off[k];
+    const uint16_t *D = a.s_delta + a.s_off[k];
     const uint8_t *cls = a.s_cls + 256u * k;
     const uint8_t *acc = a.s_acc + a.s_acc_off[k];
     const uint32_t C = a.s_C[k];
@@ -1126,7 +1129,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     // hit capacity: remembered from earlier calls through the slot size (no relaunch in
     // steady state), at least R / 4
     uint64_t cap = std::max<uint64_t>(1u << 20, (uint64_t)R / 4);
-    cap = std::max<uint64_t>(cap, c->slot_cap[S_M_HITS] / 8);
+    cap = std::min<uint64_t>(std::max<uint64_t>(cap, slot_elems<uint64_t>(c, S_M_HITS)), 0xfffff000ull);
     uint32_t total = 0;
     unsigned long long *hits = nullptr;
     auto geometry = [&](const sg_matcher::Table &T, const sg_matcher::DevTable &D, uint32_t *bits_in_lds,
@@ -1190,16 +1193,33 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         return SG_OK;
     };
     if (h->has_pre && R) {
-        uint64_t ccap = std::max<uint64_t>(std::max<uint64_t>(1u << 20, (uint64_t)R), c->slot_cap[S_PART] / 8);
+        uint64_t ccap = std::min<uint64_t>(std::max<uint64_t>(std::max<uint64_t>(1u << 20, (uint64_t)R), slot_elems<uint64_t>(c, S_PART)),
+                                           0xfffff000ull);
         for (int attempt = 0; attempt < 2; ++attempt) {
             SG_TRY(slot(c, S_PART, ccap, &cand));
             SG_HIP(hipMemsetAsync(cnt + 1, 0, 4, c->stream));
             SG_TRY(run_lit("re_prefilter", h->prelit, cand, cnt + 1, (uint32_t)ccap, h->dplan.fac_off, h->dplan.fac_pids));
             SG_TRY(ctx_readback(c, &n_cand, cnt + 1, 4));
             if (n_cand <= ccap) break;
-            ccap = (uint64_t)n_cand + (n_cand >> 3) + 1024;
+            ccap = std::min<uint64_t>((uint64_t)n_cand + (n_cand >> 3) + 1024, 0xfffff000ull);
         }
         cap = std::max<uint64_t>(cap, (uint64_t)n_cand + 1024);
+    }
+    // Verify candidates grouped by pattern (stable sort on the pattern bits): the lanes of
+    // a wave then walk the same DFA, so its rows are shared in L1/L2 instead of every lane
+    // pulling a different automaton's rows from HBM.
+    const unsigned long long *vcand = cand;
+    static const bool vsort = !getenv("SG_VERIFY_SORT") || atoi(getenv("SG_VERIFY_SORT")) != 0;
+    if (vsort && n_cand > 4096) {
+        int pbits = 1;
+        while (pbits < 32 && (1u << pbits) < h->n_pats) ++pbits;
+        uint64_t *alt, *KC;
+        uint32_t *w1, *w2, *WV;
+        SG_TRY(slot(c, S_M_TMP, (size_t)n_cand + 1, &alt));
+        SG_TRY(slot(c, S_R_VAL, (size_t)n_cand + 1, &w1));
+        SG_TRY(slot(c, S_R_VAL2, (size_t)n_cand + 1, &w2));
+        SG_TRY(radix_sort(c, reinterpret_cast<uint64_t *>(cand), w1, alt, w2, n_cand, 0, pbits, true, &KC, &WV, "rs_cand"));
+        vcand = reinterpret_cast<const unsigned long long *>(KC);
     }
     for (int attempt = 0; attempt < 2; ++attempt) {
         SG_TRY(slot(c, S_M_HITS, cap, &hits));
@@ -1225,14 +1245,14 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
             }
             if (n_cand) {
                 const auto &p = h->dplan;
-                VerifyArgs v{d_buf, L.spans, cand, n_cand, p.s_delta, p.s_off, p.s_C, p.s_eol,
+                VerifyArgs v{d_buf, L.spans, vcand, n_cand, p.s_delta, p.s_off, p.s_C, p.s_eol,
                              p.s_acc_off, p.single_of_pid, p.s_cls, p.s_acc, hits, cnt, (uint32_t)cap};
                 SG_LAUNCH_B(c, "re_verify", n_cand * (16.0 + (double)n / R), k_verify, (n_cand + 255) / 256, 256, 0, v);
             }
         }
         SG_TRY(ctx_readback(c, &total, cnt, 4));
         if (total <= cap) break;
-        cap = (uint64_t)total + (total >> 3) + 1024;
+        cap = std::min<uint64_t>((uint64_t)total + (total >> 3) + 1024, 0xfffff000ull);
     }
     // sort (rec << 32 | sig) and de-duplicate
     uint64_t *k2;
@@ -1333,7 +1353,8 @@ int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pat
             m->s_off.push_back((uint32_t)m->s_delta.size());
             m->s_C.push_back(d.n_classes);
             m->s_eol.push_back(d.eol_class);
-            m->s_delta.insert(m->s_delta.end(), d.delta.begin(), d.delta.end());
+            if (d.n_states > 65536) { delete m; set_error("regex signature DFA exceeds 65536 states"); return SG_E_STATES; }
+            for (uint32_t x : d.delta) m->s_delta.push_back((uint16_t)x);
             m->s_cls.insert(m->s_cls.end(), d.cls, d.cls + 256);
             m->s_acc_off.push_back((uint32_t)m->s_acc.size());
             for (uint32_t s = 0; s < d.n_states; ++s) m->s_acc.push_back(d.acc_off[s + 1] > d.acc_off[s] ? 1 : 0);

@@ -199,3 +199,21 @@ def test_regex_c4_banners_full_signature_set(sg):
     exp = S.regex_hits(data, pats)
     assert got == exp
     assert len(exp) > 50
+
+
+def test_repeated_calls_keep_workspace_bounded():
+    """Hundreds of matches on one context reuse the hit workspace instead of growing it
+    (a capacity fed back from the slot size used to compound by the slot headroom)."""
+    import torch
+    import numpy as np
+    import swarm_amd
+    data = b"".join(b"host%d nginx login\n" % i for i in range(2000))
+    d = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    lit = swarm_amd.Matcher([b"nginx", b"login"], "literal")
+    rx = swarm_amd.Matcher([rb"host[0-9]+ ", rb"login$"], "regex")
+    for _ in range(400):
+        r1 = lit.dev_match(ctx, d.data_ptr(), d.numel())
+        r2 = rx.dev_match(ctx, d.data_ptr(), d.numel())
+    assert r1.n_hits == 4000 and r2.n_hits == 4000
+    ctx.close()
