@@ -113,11 +113,6 @@ struct RoundGroupPred {
     }
 };
 
-struct DenseLenFn {
-    const uint32_t *L;
-    __device__ uint64_t operator()(uint32_t i) const { return L[i]; }
-};
-
 struct GroupSizeFn {
     const uint32_t *GS, *GE;
     __device__ uint64_t operator()(uint32_t g) const { return (uint64_t)(GE[g] - GS[g] + 1u); }
@@ -360,76 +355,6 @@ __global__ void k_mark(const uint32_t *__restrict__ idx, uint32_t n, uint8_t *fl
     if (i < n) flag[idx[i]] = 1;
 }
 
-constexpr uint32_t CP_WAVE_BYTES = 8192;
-
-// Records (list order) -> out at offs[i], each '\n'-terminated. Each wave owns 64
-// consecutive list entries, whose output is one contiguous span. The wave assembles that
-// span in an LDS window: groups of 16 lanes copy one record at a time with coalesced
-// aligned word loads (the record's bytes are contiguous in the source), then the whole
-// wave writes the window with 16-byte stores. Spans wider than the window (records longer
-// than CP_WAVE_BYTES / 64 on average) are copied the same way straight to HBM.
-__global__ __launch_bounds__(256) void k_copy_records(const uint8_t *__restrict__ buf,
-                                                      const uint2 *__restrict__ spans,
-                                                      const uint32_t *__restrict__ recs,
-                                                      const uint64_t *__restrict__ offs, uint32_t n,
-                                                      uint8_t *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_buf[4][CP_WAVE_BYTES];
-    __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
-    const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t wfirst = (blockIdx.x * 4 + wid) * 64u;
-    if (wfirst >= n) return;
-    const uint32_t i = wfirst + lane;
-    const bool act = i < n;
-    const uint32_t r = act ? recs[i] : 0u;
-    const uint2 sp = act ? spans[r] : make_uint2(0, 0);
-    const uint32_t s = sp.x, len = sp.y - sp.x;
-    const uint64_t o = act ? offs[i] : 0ull;
-    const uint32_t last = (n - wfirst) < 64u ? (n - wfirst - 1u) : 63u;
-    const uint64_t o0 = __shfl(o, 0, 64);
-    const uint64_t oend = __shfl(o + len + 1u, (int)last, 64);
-    const uint64_t base = o0 & ~15ull;
-    const uint64_t span = oend - base;
-    const bool in_lds = span <= CP_WAVE_BYTES;
-    s_src[wid][lane] = s;
-    s_len[wid][lane] = len;
-    s_dst[wid][lane] = (uint32_t)(o - base);  // < 4 GiB: one call's output
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const uint32_t g = lane >> 4, gl = lane & 15;
-    uint8_t *L = s_buf[wid];
-    for (uint32_t j = g; j <= last; j += 4) {
-        const uint32_t sj = s_src[wid][j], lj = s_len[wid][j];
-        const uint32_t ej = sj + lj;
-        const uint32_t a0 = sj & ~3u;
-        uint8_t *dst = (in_lds ? L : out + base) + s_dst[wid][j];
-        for (uint32_t a = a0 + 4 * gl; a < ej; a += 64) {
-            const uint32_t x = *reinterpret_cast<const uint32_t *>(buf + a);
-#pragma unroll
-            for (uint32_t b = 0; b < 4; ++b) {
-                const uint32_t p = a + b;
-                if (p >= sj && p < ej) dst[p - sj] = (uint8_t)(x >> (8 * b));
-            }
-        }
-        if (gl == 0) dst[lj] = 0x0a;
-    }
-    if (!in_lds) return;
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const uint32_t nch = (uint32_t)((span + 15) / 16);
-    for (uint32_t ch = lane; ch < nch; ch += 64) {
-        const uint64_t ga = base + 16ull * ch;
-        if (ga >= o0 && ga + 16 <= oend) {
-            *reinterpret_cast<uint4 *>(out + ga) = *reinterpret_cast<const uint4 *>(L + 16 * ch);
-        } else {
-#pragma unroll
-            for (uint32_t b = 0; b < 16; ++b) {
-                const uint64_t ad = ga + b;
-                if (ad >= o0 && ad < oend) out[ad] = L[16 * ch + b];
-            }
-        }
-    }
-}
-
 // Prior check: flag[0] = 1 if records are not strictly increasing.
 __global__ void k_check_sorted(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, const uint64_t *__restrict__ K,
                                uint32_t n, uint32_t *flag) {
@@ -572,48 +497,51 @@ int select_flags(sg_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out_idx,
     return run_select2(c, "select", FlagPred{flags}, n, out_idx, (uint32_t *)nullptr, count, nullptr);
 }
 
-// recs/lens: record ids and serialized lengths (len + 1) in output order.
-static int serialize_dense(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
-                           const uint32_t *recs, const uint32_t *lens, uint32_t count, int out_slot,
-                           uint8_t *dst, size_t dst_cap, uint8_t **d_out, uint64_t *bytes) {
+// Records recs[0..count) (ids into spans), in list order, '\n'-terminated: the emit
+// machinery (count -> tile scan -> LDS-window copy), with one host sync for the size.
+static int emit_records(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, const uint32_t *recs, uint32_t count,
+                        int out_slot, uint8_t *dst, size_t dst_cap, uint8_t **d_out, uint64_t *bytes) {
     *bytes = 0;
-    uint64_t *offs;
-    SG_TRY(slot(c, S_OFFS, (size_t)count + 1, &offs));
-    uint64_t total = 0;
-    SG_TRY(run_scan64(c, "scan_len", DenseLenFn{lens}, count, offs, &total));
+    const uint32_t ntiles = (count + EM_TILE - 1) / EM_TILE;
+    if (ntiles == 0) {
+        if (!dst) SG_TRY(slot(c, out_slot, 16, d_out));
+        else *d_out = dst;
+        return SG_OK;
+    }
+    uint64_t *tp;  // tot[ntiles] | pre[ntiles] | total
+    SG_TRY(slot(c, S_EMIT, 2 * (size_t)ntiles + 4, &tp));
+    uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
+    uint2 *cache;
+    SG_TRY(slot(c, S_ECACHE, (size_t)count + 1, &cache));
+    const PermItem item{recs, spans};
+    SG_LAUNCH(c, "emit_lines.count", k_emit_count<PermItem>, ntiles, EM_BLOCK, 0, item, count, cache, tot);
+    SG_TRY(tile_scan(c, tot, ntiles, pre, total));
+    uint64_t tv = 0;
+    SG_TRY(ctx_readback(c, &tv, total, 8));
+    const uint64_t nb = (uint32_t)tv;
     if (dst) {
-        if (total > dst_cap) { set_error("output capacity %zu < %llu", dst_cap, (unsigned long long)total); return SG_E_CAP; }
+        if (nb > dst_cap) { set_error("output capacity %zu < %llu", dst_cap, (unsigned long long)nb); return SG_E_CAP; }
         *d_out = dst;
     } else {
-        SG_TRY(slot(c, out_slot, (size_t)total + 16, d_out));
+        SG_TRY(slot(c, out_slot, nb + 16, d_out));
     }
-    // model: each output byte read once and written once, plus id/start/end/offset per record
-    if (count) SG_LAUNCH_B(c, "copy_records", 2.0 * total + 20.0 * count, k_copy_records, grid_for(count, 256), 256, 0, d_buf, spans, recs, offs, count, *d_out);
-    *bytes = total;
+    // model: each output byte read once and written once, plus the cached (start, len)
+    SG_LAUNCH_B(c, "emit_lines", 2.0 * nb + 8.0 * count, k_emit_apply, ntiles, EM_BLOCK, 0, cache, count, pre, d_buf,
+                *d_out, (uint2 *)nullptr, (const uint64_t *)nullptr, (uint64_t *)nullptr, 0);
+    *bytes = nb;
     return SG_OK;
-}
-
-__global__ void k_lens_of(const uint32_t *__restrict__ recs, const uint2 *__restrict__ spans, uint32_t n, uint32_t *L) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) { const uint32_t r = recs[i]; L[i] = spans[r].y - spans[r].x + 1u; }
 }
 
 int serialize(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
               const uint32_t *recs, const uint32_t * /*map*/, uint32_t count, int out_slot,
               uint8_t **d_out, uint64_t *bytes) {
-    uint32_t *L;
-    SG_TRY(slot(c, S_M_TMP2, (size_t)count + 1, &L));
-    if (count) SG_LAUNCH(c, "lens", k_lens_of, grid_for(count, 256), 256, 0, recs, spans, count, L);
-    return serialize_dense(c, d_buf, spans, recs, L, count, out_slot, nullptr, 0, d_out, bytes);
+    return emit_records(c, d_buf, spans, recs, count, out_slot, nullptr, 0, d_out, bytes);
 }
 
 int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes) {
-    uint32_t *L;
-    SG_TRY(slot(c, S_M_TMP2, (size_t)count + 1, &L));
-    if (count) SG_LAUNCH(c, "lens", k_lens_of, grid_for(count, 256), 256, 0, recs, spans, count, L);
     uint8_t *o;
-    return serialize_dense(c, d_buf, spans, recs, L, count, 0, dst, dst_cap, &o, bytes);
+    return emit_records(c, d_buf, spans, recs, count, 0, dst, dst_cap, &o, bytes);
 }
 
 
