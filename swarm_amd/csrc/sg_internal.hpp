@@ -29,7 +29,10 @@ struct Lines {
     uint32_t tile_bytes = 0, n_tiles = 0;
 };
 // Split d_buf (16-byte aligned device pointer, n bytes) into non-empty records.
-int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys = true);
+// apply = false: count and allocate only; the spans are then written by a consumer that
+// re-reads the same tiles anyway (k_lit_scan with LitArgs::spans_out).
+int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys = true,
+              bool apply = true);
 
 // LSD radix sort of (u64 key, u32 val) pairs on bits [begin_bit, end_bit), stable.
 // Ping-pongs between (keys, vals) and (keys_alt, vals_alt); returns the final arrays.

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
     }
 }
 
-int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys) {
+int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys, bool apply) {
     if (n > MAX_BYTES) { set_error("buffer of %llu bytes exceeds the 4 GiB per-call limit", (unsigned long long)n); return SG_E_TOO_LARGE; }
     if (((uintptr_t)d_buf & 15) != 0) { set_error("run_lines: device buffer not 16-byte aligned"); return SG_E_INVAL; }
     const uint32_t ntiles = (uint32_t)(n / LN_TILE + 1);
@@ -155,13 +155,13 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
     SG_TRY(slot(c, ss.starts, (size_t)R + 1, &out->spans));
     out->keys = nullptr;
     if (want_keys) SG_TRY(slot(c, ss.keys, (size_t)R + 1, &out->keys));
-    SG_LAUNCH(c, "lines", k_lines, ntiles, LN_BLOCK, 0, d_buf, n, pre, out->spans, out->keys);
+    if (apply) SG_LAUNCH(c, "lines", k_lines, ntiles, LN_BLOCK, 0, d_buf, n, pre, out->spans, out->keys);
     out->n_rec = R;
     out->tile_excl = pre;
     out->tile_bytes = LN_TILE;
     out->n_tiles = ntiles;
     // text read twice (count + apply) + (start, end[, key0]) per record
-    prof_bytes(c, "lines", (double)n + (want_keys ? 16.0 : 8.0) * R);
+    if (apply) prof_bytes(c, "lines", (double)n + (want_keys ? 16.0 : 8.0) * R);
     prof_bytes(c, "lines.count", (double)n);
     return SG_OK;
 }

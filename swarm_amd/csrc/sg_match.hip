@@ -578,6 +578,7 @@ struct LitArgs {
     uint32_t *hit_count;
     uint32_t cap;
     const uint32_t *fac_off, *fac_pids;  // regex prefilter expansion (else null)
+    uint2 *spans_out;                    // non-null: also write the parse's record spans (fused A3)
     unsigned long long *dbg;             // SG_LIT_DEBUG: {candidates, fingerprint matches, hits}
     uint32_t dbg_mode;                   // bit 0: skip pass 2, bit 1: skip pass 1 probes
 };
@@ -674,7 +675,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
     __shared__ uint32_t s_q[LS_Q];
     __shared__ uint2 s_kf[LS_Q];  // per queued candidate: (bucket, fingerprint)
     __shared__ uint32_t s_red[LS_BLOCK / 64];
-    __shared__ uint32_t s_hn, s_g, s_base;
+    __shared__ uint32_t s_hn, s_g, s_base, s_ebase;
     uint32_t *s_bm = s_dyn;
     uint16_t *s_rank = reinterpret_cast<uint16_t *>(s_dyn + a.bm_words);
     for (uint32_t q = threadIdx.x; q < a.bm_words; q += LS_BLOCK) { s_bm[q] = a.bitmap[q]; s_rank[q] = a.rank[q]; }
@@ -737,7 +738,11 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
 #pragma unroll
         for (int j = 0; j < NW / 4; ++j)
             reinterpret_cast<uint4 *>(s_tile)[(NW / 4) * t + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
-        if (t == 0) s_base = (uint32_t)(a.tile_excl[tile] >> 31);
+        if (t == 0) {
+            const uint64_t te = a.tile_excl[tile];
+            s_base = (uint32_t)(te >> 31);
+            s_ebase = (uint32_t)(te & 0x7fffffffu);
+        }
         uint64_t m = 0;
 #pragma unroll
         for (int j = 0; j < NW; ++j) {
@@ -751,6 +756,15 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
         const uint64_t sm = ~m & ((m << 1) | cin) & full;
         uint32_t tot;
         const uint32_t excl = block_excl_scan<LS_BLOCK>((uint32_t)__popcll(sm), &tot, s_red);
+        if (a.spans_out) {
+            // the record spans of this tile, as k_lines writes them (k-th start / k-th end)
+            const uint64_t em = m & ~((m << 1) | cin) & full;
+            uint32_t etot;
+            const uint32_t eexcl = block_excl_scan<LS_BLOCK>((uint32_t)__popcll(em), &etot, s_red);
+            uint32_t si = s_base + excl, ei = s_ebase + eexcl;
+            for (uint64_t bits = sm; bits; bits &= bits - 1) a.spans_out[si++].x = (uint32_t)(my0 + __ffsll((long long)bits) - 1);
+            for (uint64_t bits = em; bits; bits &= bits - 1) a.spans_out[ei++].y = (uint32_t)(my0 + __ffsll((long long)bits) - 1);
+        }
         uint32_t wn0 = *reinterpret_cast<const uint32_t *>(s_tile + (t + 1) * BPT);
         uint32_t wn1 = *reinterpret_cast<const uint32_t *>(s_tile + (t + 1) * BPT + 4);
         if (a.nocase) {
@@ -1121,7 +1135,11 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     *res = sg_dev_hits{};
     SG_TRY(ensure_device(h, c->device));
     Lines L;
-    SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L, false));
+    // When a literal scan runs first (literal filter or regex prefilter), it writes the
+    // record spans itself from the same tiles, so the parse's second pass is skipped.
+    const bool fuse_spans = h->has_pre || h->lit.on;
+    const char *span_writer = h->has_pre ? "re_prefilter" : "lit_match";
+    SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L, false, !fuse_spans));
     const uint32_t R = L.n_rec;
     res->in_records = R;
     uint32_t *cnt;
@@ -1156,6 +1174,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
             a.bits[k] = Lt.bits[k]; a.bm_off[k] = Lt.bm_off[k]; a.rank_base[k] = Lt.rank_base[k];
         }
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
+        a.spans_out = (fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
         static const int dbg_mode = getenv("SG_LIT_DEBUG") ? atoi(getenv("SG_LIT_DEBUG")) : -1;
         unsigned long long *dbg = nullptr;
         if (dbg_mode >= 0) a.dbg_mode = (uint32_t)dbg_mode;  // bit 0 skip pass 2, bit 1 skip pass 1, bit 3 count
