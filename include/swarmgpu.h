@@ -121,6 +121,19 @@ int sg_dev_dedup_diff(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur,
  * of n_parts), ready for an all-to-all. */
 int sg_dev_partition(sg_ctx *ctx, const uint8_t *d_buf, size_t n, uint32_t n_parts,
                      uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records);
+/* Range routing: part(record) = number of splitters <= key0(record), where key0 = the
+ * record's first 7 bytes big-endian << 8 | min(len, 8) (a key0 order is a
+ * byte order). splitters: n_parts - 1 non-decreasing host values. Part p's records all sort
+ * below part p+1's, so per-part sort -u outputs concatenated in part order are the global
+ * sort -u output: the way a shard larger than one 4 GiB call, or a global byte order
+ * across GPUs, is processed. Same output layout as sg_dev_partition. */
+int sg_dev_partition_range(sg_ctx *ctx, const uint8_t *d_buf, size_t n, const uint64_t *splitters,
+                           uint32_t n_parts, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
+                           uint64_t *part_records);
+/* m evenly spaced records' key0 values (host array; ~0 when the buffer has no records), for
+ * choosing splitters; *n_rec = the buffer's record count. */
+int sg_dev_key_sample(sg_ctx *ctx, const uint8_t *d_buf, size_t n, uint32_t m, uint64_t *keys,
+                      uint64_t *n_rec);
 /* The record hash used by sg_dev_partition, on one host record (for tests/oracles). */
 uint64_t sg_hash64(const uint8_t *rec, size_t len);
 

@@ -289,6 +289,26 @@ class Context:
                                      offs.ctypes.data_as(C.POINTER(C.c_uint32)), len(offs) - 1, C.byref(r)))
         return r
 
+    def partition_range(self, d_buf: int, n: int, splitters, d_out: int, out_cap: int):
+        """Order-preserving routing by key0 splitters (len(splitters) + 1 parts); same output
+        layout as partition(). Returns (bytes per part, records per part)."""
+        sp = np.ascontiguousarray(np.asarray(splitters, dtype=np.uint64))
+        parts = sp.size + 1
+        pb = (C.c_uint64 * parts)()
+        pr = (C.c_uint64 * parts)()
+        arr = (C.c_uint64 * max(1, sp.size))(*sp.tolist())
+        check(lib.sg_dev_partition_range(self._h, C.c_void_p(d_buf), n, arr, parts, C.c_void_p(d_out), out_cap,
+                                         pb, pr))
+        return list(pb), list(pr)
+
+    def key_sample(self, d_buf: int, n: int, m: int):
+        """(m evenly spaced records' key0 values as uint64 (all ~0 if empty), record count)."""
+        out = np.empty(max(1, m), dtype=np.uint64)
+        nr = C.c_uint64()
+        check(lib.sg_dev_key_sample(self._h, C.c_void_p(d_buf), n, m, out.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                    C.byref(nr)))
+        return out[:m], nr.value
+
     def partition(self, d_buf: int, n: int, n_parts: int, d_out: int, out_cap: int):
         """Route records to part(hash64(record), n_parts), writing them grouped by partition
         into the caller's device buffer d_out (capacity >= n + 1). Returns (bytes per part,

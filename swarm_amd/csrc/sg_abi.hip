@@ -62,6 +62,43 @@ __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ b
     }
 }
 
+// Range routing (order-preserving shards): part = number of splitters <= key0(record).
+// key0 order is consistent with byte order, and equal key0 values share a
+// part, so part p holds only records below every record of part p+1: the per-part sort -u
+// outputs concatenated in part order are the global sort -u output.
+__global__ __launch_bounds__(256) void k_range_keys(const uint64_t *__restrict__ key0, const uint2 *__restrict__ spans,
+                                                    uint32_t R, const uint64_t *__restrict__ split, uint32_t ns,
+                                                    uint64_t *keys, unsigned long long *cnt /* [2*parts] */) {
+    __shared__ unsigned long long s_c[2 * 256];
+    __shared__ uint64_t s_split[256];
+    for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) s_c[i] = 0;
+    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) s_split[i] = split[i];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < R) {
+        const uint64_t k = key0[i];
+        uint32_t lo = 0, hi = ns;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_split[mid] <= k) lo = mid + 1; else hi = mid;
+        }
+        keys[i] = lo;
+        atomicAdd(&s_c[lo], 1ull);
+        atomicAdd(&s_c[256 + lo], (unsigned long long)(spans[i].y - spans[i].x + 1));
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q <= ns; q += blockDim.x) {
+        if (s_c[q]) atomicAdd(&cnt[q], s_c[q]);
+        if (s_c[256 + q]) atomicAdd(&cnt[ns + 1 + q], s_c[256 + q]);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_key_sample(const uint64_t *__restrict__ key0, uint32_t R, uint32_t m,
+                                                    uint64_t *__restrict__ out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) out[k] = key0[(uint32_t)(((uint64_t)k * R) / m)];
+}
+
 struct Acq {
     sg_ctx *c = nullptr;
     ~Acq() { if (c) pool_release(c); }
@@ -130,9 +167,13 @@ static int host_dedup_diff(const uint8_t *const *chunks, const size_t *lens, siz
     return SG_OK;
 }
 
+// Hash routing (split == null) or range routing by key0 splitters (parts - 1 of them).
 int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, uint8_t *d_out,
-                  size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
+                  size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, const uint64_t *split = nullptr) {
     if (parts == 0 || parts > 256) { set_error("n_parts must be in 1..256"); return SG_E_INVAL; }
+    if (split)
+        for (uint32_t q = 1; q + 1 < parts; ++q)
+            if (split[q] < split[q - 1]) { set_error("splitters must be non-decreasing"); return SG_E_INVAL; }
     Lines L;
     SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L));
     const uint32_t R = L.n_rec;
@@ -145,8 +186,14 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
     SG_TRY(slot(c, S_R_KEY2, R, &keys2));
     SG_TRY(slot(c, S_VALS, R, &v1));
     SG_TRY(slot(c, S_VALS2, R, &v2));
-    if (R) {
+    if (R && !split) {
         SG_LAUNCH(c, "part_keys", k_part_keys, (R + 255) / 256, 256, 0, d_buf, L.spans, R, parts, keys, cnt);
+    } else if (R) {
+        uint64_t *d_split;
+        SG_TRY(slot(c, S_M_TMP2, 256, &d_split));
+        if (parts > 1) SG_HIP(hipMemcpyAsync(d_split, split, 8 * (parts - 1), hipMemcpyHostToDevice, c->stream));
+        SG_LAUNCH(c, "range_keys", k_range_keys, (R + 255) / 256, 256, 0, L.keys, L.spans, R, d_split, parts - 1, keys,
+                  cnt);
     }
     uint64_t *K;
     uint32_t *V;
@@ -228,6 +275,40 @@ int sg_dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, const uint8
     SG_TRY(aligned_in(c, S_IN, d_cur, n_cur, &cur));
     if (n_prior) SG_TRY(aligned_in(c, S_IN2, d_prior, n_prior, &prior));
     return dev_dedup_diff(c, cur, n_cur, prior, n_prior, true, res);
+}
+
+int sg_dev_partition_range(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint64_t *splitters, uint32_t n_parts,
+                           uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
+    if (!c || (!d_out && n) || (!d_buf && n) || (!splitters && n_parts > 1)) {
+        set_error("sg_dev_partition_range: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b;
+    SG_TRY(aligned_in(c, S_IN, d_buf, n, &b));
+    static const uint64_t none = 0;
+    return dev_partition(c, b, n, n_parts, d_out, out_cap, part_bytes, part_records, n_parts > 1 ? splitters : &none);
+}
+
+int sg_dev_key_sample(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t m, uint64_t *keys, uint64_t *n_rec) {
+    if (!c || !keys || (!d_buf && n)) { set_error("sg_dev_key_sample: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b;
+    SG_TRY(aligned_in(c, S_IN, d_buf, n, &b));
+    Lines L;
+    SG_TRY(run_lines(c, b, n, CUR_SLOTS, &L));
+    if (n_rec) *n_rec = L.n_rec;
+    const uint32_t take = L.n_rec ? m : 0u;
+    if (take) {
+        uint64_t *d;
+        SG_TRY(slot(c, S_M_TMP2, take, &d));
+        SG_LAUNCH(c, "key_sample", k_key_sample, (take + 255) / 256, 256, 0, L.keys, L.n_rec, take, d);
+        SG_TRY(ctx_readback(c, keys, d, 8ull * take));
+    }
+    for (uint32_t k = take; k < m; ++k) keys[k] = ~0ull;
+    return SG_OK;
 }
 
 int sg_dev_partition(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t n_parts, uint8_t *d_out,

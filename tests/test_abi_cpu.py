@@ -48,3 +48,13 @@ def test_no_gpu_fails_loudly_not_silently():
         pytest.skip("a GPU is present")
     with pytest.raises(SGError):
         dedup(b"b\na\n")
+
+
+def test_choose_splitters_quantiles():
+    import numpy as np
+    from swarm_amd import sharded
+    s = np.array([5, 1, 9, 3, 7, 0xFFFFFFFFFFFFFFFF], dtype=np.uint64)
+    sp = sharded.choose_splitters(s, 3)
+    assert sp.tolist() == [3, 7]
+    assert sharded.choose_splitters(s, 1).size == 0
+    assert np.all(np.diff(sharded.choose_splitters(np.arange(1000, dtype=np.uint64), 17).astype(np.int64)) >= 0)
