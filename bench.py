@@ -309,13 +309,152 @@ def bench_fields(args):
     ctx.close()
 
 
+def bench_c5(args):
+    """BASELINE.json configs[4] (C5): 1B host:port records (~31 GB) deduped and diffed against
+    a prior scan at 90 % overlap, strong scaling over N ranks. Records are rendered on the
+    GPU: 64M hosts x 4 open-port slots (ports from 32 common ones) = 256M distinct combos,
+    1B draws (~4 copies each). Each rank routes
+    its draw by key0 ranges agreed across ranks (RCCL all-to-all when N > 1), then processes
+    its range in local range parts of < 4 GiB (swarm_amd.sharded); rank outputs concatenated
+    in rank order are the global sort -u / comm -13 output. Setup (untimed): the prior scan
+    = sort -u of another 1B draw over combos shifted by 10 %, routed to its owner ranks, and
+    the splitters (from the prior's key0 samples, known before the scan)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import swarm_amd
+    from swarm_amd import corpus, sharded
+    from swarm_amd import distributed as D
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        local = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        dist.init_process_group(args.dist_backend)
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+    total = args.lines if args.lines != 10_000_000 else 1_000_000_000
+    per = total // world
+    n_hosts = args.c5_hosts
+    K = 4  # open-port slots per host (ports drawn from 32 common ports)
+    U = n_hosts * K
+    pool = corpus.host_pool_torch(n_hosts + n_hosts // 10 + 1, seed=5, device=dev)
+    ctx = swarm_amd.Context(local, torch.cuda.current_stream(dev).cuda_stream)
+    t_setup = time.perf_counter()
+    prior_raw = corpus.hostport_pieces(pool, per, U // 10, U + U // 10, seed=900 + rank, ports_per_host=K)
+    gsplit = D.agree_splitters(ctx, prior_raw, world) if world > 1 else np.zeros(0, dtype=np.uint64)
+    mine = D.range_exchange(ctx, prior_raw, gsplit) if world > 1 else prior_raw
+    parts = sharded.plan_parts(mine, [], 2 << 30)
+    lsplit = sharded.choose_splitters(np.concatenate(
+        [ctx.key_sample(p.data_ptr(), p.numel(), 1 << 14)[0] for p in mine]), parts)
+    pu, _, _ = sharded.dedup_diff_large(ctx, mine, (), splitters=lsplit)
+    del prior_raw, mine
+    prior_local = sharded.split_at_newlines(pu, 3 << 30)
+    cur = corpus.hostport_pieces(pool, per, 0, U, seed=100 + rank, ports_per_host=K)
+    del pool
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t_setup
+
+    def step():
+        return D.dedup_diff_range_step(ctx, cur, prior_local, gsplit, lsplit)
+
+    for _ in range(args.warmup):
+        u, f, st = step()
+        del u, f
+    torch.cuda.synchronize()
+    ctx.reset_stats()
+    ctx.profile(True)
+    u, f, st = step()
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    full = ctx.kernel_stats()
+    ub, fb = int(u.numel()), int(f.numel())
+    del u, f
+    dominant = max(full.items(), key=lambda kv: kv[1][1])[0] if full else None
+    if world > 1:
+        names = [None] * world
+        dist.all_gather_object(names, dominant)
+        dominant = names[0]
+    ctx.reset_stats()
+    ctx.profile(True, only=dominant)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        u, f, st = step()
+        del u, f
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ctx.profile(False)
+    stats = ctx.kernel_stats()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    cur_bytes = sum(p.numel() for p in cur)
+    prior_bytes = sum(p.numel() for p in prior_local)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import semantics as S
+        m = 2_000_000
+        c0 = cur[0][: int(torch.nonzero(cur[0][: 40 * m] == 10)[m - 1].item()) + 1].cpu().numpy().tobytes()
+        p0 = prior_local[0][:40 * m].cpu().numpy().tobytes()
+        p0 = p0[: p0.rfind(b"\n") + 1]
+        tc = time.perf_counter()
+        eu, ef = S.dedup_diff(c0, p0)
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(m / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "2M C5 records + a 2M-record slice of the prior; oracle sorted(set())+set difference, "
+                         "1 thread, %.2f s" % tc, "host_cpus": os.cpu_count()}
+        gu, gf, _ = sharded.dedup_diff_large(ctx, [dev_bytes(c0, dev)], [dev_bytes(p0, dev)], part_bytes=16 << 20)
+        cpu["gpu_bit_exact_on_sample"] = (gu.cpu().numpy().tobytes() == eu and gf.cpu().numpy().tobytes() == ef)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(total * args.steps / el, 1), "unit": "records/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (host:port records rendered on the GPU, SURVEY.md §8(d) C5)",
+            "config": {"workload": "C5: %dM host:port records (%.1f GB on rank 0) + prior at 90%% overlap, "
+                                   "key0-range sharded over %d GPU(s)" % (total // 1_000_000, cur_bytes / 1e9, world),
+                       "records_total": total, "prior_bytes_rank0": int(prior_bytes), "local_parts": int(lsplit.size + 1),
+                       "setup_s": round(t_setup, 1),
+                       "parallelism": "key0-range all-to-all x%d" % world if world > 1 else "single GPU"},
+            "gbps": round((cur_bytes + prior_bytes + ub + fb) * world * args.steps / el / 1e9, 2),
+            "records": {"in_rank0": st["in_records"], "unique_rank0": st["uniq_records"],
+                        "new_rank0": st["fresh_records"], "max_part_bytes": st["max_part_bytes"]},
+            "roofline": roofline_of(stats, dominant, "c5"),
+            "cpu_baseline": cpu,
+            "kernels": kernel_table(full),
+            "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
+                            "HIP events only around the dominant kernel",
+        }), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dev_bytes(b, dev):
+    import numpy as np
+    import torch
+    return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).to(dev)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lines", type=int, default=10_000_000)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "fields"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "fields"], default="c2")
+    ap.add_argument("--c5-hosts", type=int, default=64_000_000, help="C5 hosts (x 4 open-port slots = combos)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real runs; gloo rehearses N ranks on fewer GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -327,6 +466,8 @@ def main():
         return bench_c4(args)
     if args.workload == "fields":
         return bench_fields(args)
+    if args.workload == "c5":
+        return bench_c5(args)
 
     import numpy as np
     import torch

@@ -54,8 +54,11 @@ int sg_device_count(int *n);
 
 /* ------------------------------------------------------------------ contexts */
 typedef struct sg_ctx sg_ctx;
-/* stream: a hipStream_t on `device` (e.g. torch.cuda.current_stream().cuda_stream), or
- * NULL for a context-owned non-blocking stream. */
+/* stream: a hipStream_t on `device` (e.g. torch.cuda.current_stream().cuda_stream),
+ * SG_NULL_STREAM for the device's null (legacy default) stream — the one torch uses unless
+ * told otherwise, whose handle reads as 0 — or NULL for a context-owned non-blocking
+ * stream (which does not order against the null stream: the caller synchronises). */
+#define SG_NULL_STREAM ((void *)-1)
 int sg_ctx_create(int device, void *stream, sg_ctx **out);
 int sg_ctx_destroy(sg_ctx *ctx);
 int sg_ctx_sync(sg_ctx *ctx);

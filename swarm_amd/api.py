@@ -224,7 +224,10 @@ class Context:
 
     def __init__(self, device: int = 0, stream: int | None = None):
         self._h = C.c_void_p()
-        check(lib.sg_ctx_create(device, C.c_void_p(stream) if stream else None, C.byref(self._h)))
+        # stream None: a context-owned stream; 0 (torch's default stream handle): the null
+        # stream, so kernels order against torch work without explicit synchronisation
+        s = None if stream is None else (C.c_void_p(stream) if stream else C.c_void_p(-1))
+        check(lib.sg_ctx_create(device, s, C.byref(self._h)))
         self.device = device
 
     def close(self):

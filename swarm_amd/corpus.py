@@ -337,3 +337,125 @@ def nmap_report(n_hosts: int, seed: int = 11, max_ports: int = 6) -> bytes:
     out.append(b"# Nmap done at Mon Oct 12 10:05:00 2026 -- %d IP addresses (%d hosts up) scanned in 300.00 seconds"
                % (n_hosts, n_hosts))
     return b"\n".join(out) + b"\n"
+
+
+# ------------------------------------------------------------------ C5: host:port records
+PORTS = [b"21", b"22", b"23", b"25", b"53", b"80", b"81", b"110", b"111", b"135", b"139", b"143", b"443", b"445",
+         b"465", b"587", b"993", b"995", b"1433", b"1723", b"2049", b"3000", b"3306", b"3389", b"5432", b"5900",
+         b"6379", b"8000", b"8080", b"8443", b"9200", b"27017"]
+
+
+def host_pool_gpu(n_hosts: int, seed: int = 5, device="cuda", chunk: int = 1 << 21):
+    """n_hosts subdomain names rendered on the host (render_names), left-aligned on the GPU:
+    (matrix (n_hosts, 33) uint8, lengths int32)."""
+    import torch
+    mats, lens = [], []
+    for i in range(0, n_hosts, chunk):
+        ids = np.arange(i, min(n_hosts, i + chunk), dtype=np.uint64)
+        mat, msk = render_names(ids, salt=seed)
+        m = torch.from_numpy(mat).to(device)
+        k = torch.from_numpy(msk).to(device)
+        order = torch.sort((~k).to(torch.uint8), dim=1, stable=True).indices
+        mats.append(torch.gather(m, 1, order))
+        lens.append(k.sum(1).to(torch.int32))
+    return torch.cat(mats), torch.cat(lens)
+
+
+_ALPHA_T = b"abcdefghijklmnopqrstuvwxyz0123456789"
+
+
+def _tmix(x):
+    """splitmix64 finalizer on int64 tensors (wrapping multiplies, logical shifts)."""
+    def shr(v, k):
+        return (v >> k) & ((1 << (64 - k)) - 1)
+    c1 = 0xBF58476D1CE4E5B9 - (1 << 64)
+    c2 = 0x94D049BB133111EB - (1 << 64)
+    x = x ^ shr(x, 30)
+    x = x * c1
+    x = x ^ shr(x, 27)
+    x = x * c2
+    return x ^ shr(x, 31)
+
+
+def host_pool_torch(n_hosts: int, seed: int = 5, device="cuda", chunk: int = 1 << 23):
+    """n_hosts host names rendered on the GPU (label of 6..14 [a-z0-9], optional
+    api./dev./www./mail., target{0..63}.com), left-aligned: (matrix (n, 33) uint8, lengths)."""
+    import torch
+    alpha = torch.frombuffer(bytearray(_ALPHA_T), dtype=torch.uint8).to(device)
+    opts = [b"", b"api", b"dev", b"www", b"mail"]
+    optm = torch.zeros((5, 6), dtype=torch.uint8)
+    optl = torch.zeros(5, dtype=torch.int64)
+    for k, o in enumerate(opts):
+        b = (b"." + o) if o else b""
+        optm[k, :len(b)] = torch.frombuffer(bytearray(b or b"\0"), dtype=torch.uint8)[:len(b)]
+        optl[k] = len(b)
+    optm, optl = optm.to(device), optl.to(device)
+    tails = torch.zeros((64, 13), dtype=torch.uint8)
+    taill = torch.zeros(64, dtype=torch.int64)
+    for t in range(64):
+        b = b".target%d.com" % t
+        tails[t, :len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        taill[t] = len(b)
+    tails, taill = tails.to(device), taill.to(device)
+    mats, lens = [], []
+    for i in range(0, n_hosts, chunk):
+        ids = torch.arange(i, min(n_hosts, i + chunk), dtype=torch.int64, device=device)
+        h = _tmix(ids * 0x1E3779B97F4A7C15 + seed)
+        m = ids.numel()
+        L = 6 + (h & 0x7FFFFFFF) % 9
+        row = torch.zeros((m, 33), dtype=torch.uint8, device=device)
+        msk = torch.zeros((m, 33), dtype=torch.bool, device=device)
+        g = h
+        for j in range(14):
+            g = _tmix(g + (j + 1))
+            row[:, j] = alpha[(g & 0x7FFFFFFF) % 36]
+        col = torch.arange(33, device=device)
+        msk[:, :14] = col[None, :14] < L[:, None]
+        o = ((h >> 40) & 0xFFFFFF) % 5
+        row[:, 14:20] = optm[o]
+        msk[:, 14:20] = col[None, :6] < optl[o][:, None]
+        t = ((h >> 48) & 0xFFFF) % 64
+        row[:, 20:33] = tails[t]
+        msk[:, 20:33] = col[None, :13] < taill[t][:, None]
+        order = torch.sort((~msk).to(torch.uint8), dim=1, stable=True).indices
+        mats.append(torch.gather(row, 1, order))
+        lens.append(msk.sum(1).to(torch.int32))
+    return torch.cat(mats), torch.cat(lens)
+
+
+def hostport_pieces(pool, n: int, lo: int, hi: int, seed: int, per_piece: int = 50_000_000,
+                    ports_per_host: int | None = None):
+    """n 'host:port' records ('\\n'-terminated) for combo ids drawn uniformly from [lo, hi),
+    rendered on the GPU, as a list of device byte tensors of <= per_piece records each (each
+    ends at a record boundary). Combo c: host c // k and, with ports_per_host = k, the k-slot
+    port PORTS[hash(c) % 32] (a host keeps a few open ports, as in a port scan); without it,
+    k = len(PORTS) and port c % k."""
+    import torch
+    mat, lens = pool
+    dev = mat.device
+    P = len(PORTS)
+    K = ports_per_host or P
+    pm = torch.zeros((P, 8), dtype=torch.uint8)
+    pl = torch.zeros(P, dtype=torch.int64)
+    for i, p in enumerate(PORTS):
+        b = b":" + p + b"\n"
+        pm[i, :len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        pl[i] = len(b)
+    pm, pl = pm.to(dev), pl.to(dev)
+    W = mat.shape[1]
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    out = []
+    cols = torch.arange(W + 8, device=dev)
+    for s in range(0, n, per_piece):
+        m = min(per_piece, n - s)
+        c = torch.randint(lo, hi, (m,), generator=g, device=dev, dtype=torch.int64)
+        h = c // K
+        p = (c % P) if ports_per_host is None else ((_tmix(c * 0x2545F4914F6CDD1D) & 0x7FFFFFFF) % P)
+        rows = torch.zeros((m, W + 8), dtype=torch.uint8, device=dev)
+        rows[:, :W] = mat[h]
+        hl = lens[h].to(torch.int64)
+        rows.scatter_(1, hl[:, None] + torch.arange(8, device=dev)[None, :], pm[p])
+        out.append(rows[cols[None, :] < (hl + pl[p])[:, None]])
+        del rows, c, h, p, hl
+    return out

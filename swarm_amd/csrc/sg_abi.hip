@@ -38,6 +38,26 @@ __host__ __device__ __forceinline__ uint32_t part_of(uint64_t h, uint32_t parts)
     return (uint32_t)(((h >> 32) * (uint64_t)parts) >> 32);
 }
 
+// Add (1 record, `bytes`) to counter slot `q` of the block's LDS histogram with one LDS
+// atomic per distinct q in the wave (few parts: most waves hold one or two values), not
+// one per lane on a handful of hot addresses.
+__device__ __forceinline__ void wave_count(unsigned long long *s_c, uint32_t stride, bool act, uint32_t q,
+                                           uint32_t bytes) {
+    uint64_t pending = __ballot(act);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint32_t lq = (uint32_t)__shfl((int)q, leader, 64);
+        const bool mine = act && q == lq;
+        const uint64_t m = __ballot(mine);
+        const uint64_t b = wave_sum<uint64_t>(mine ? (uint64_t)bytes : 0ull);
+        if (lane_id() == leader) {
+            atomicAdd(&s_c[lq], (unsigned long long)__popcll(m));
+            atomicAdd(&s_c[stride + lq], (unsigned long long)b);
+        }
+        pending &= ~m;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ buf,
                                                    const uint2 *__restrict__ spans, uint32_t R,
                                                    uint32_t parts, uint64_t *keys,
@@ -45,15 +65,20 @@ __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ b
     __shared__ unsigned long long s_c[2 * 256];
     for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) s_c[i] = 0;
     __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < R) {
-        const uint32_t s = spans[i].x, e = spans[i].y;
-        const uint8_t *p = buf + s;
-        const uint64_t h = hash_words([&](uint32_t j) { return p[j]; }, e - s);
-        const uint32_t q = part_of(h, parts);
-        keys[i] = q;
-        atomicAdd(&s_c[q], 1ull);
-        atomicAdd(&s_c[256 + q], (unsigned long long)(e - s + 1));
+    // grid-stride (a bounded grid): each block flushes its histogram once, so the global
+    // counters see ~grid x parts atomics instead of one burst per 256 records
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < R; i0 += gridDim.x * blockDim.x) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint32_t q = 0, bytes = 0;
+        if (i < R) {
+            const uint32_t s = spans[i].x, e = spans[i].y;
+            const uint8_t *p = buf + s;
+            const uint64_t h = hash_words([&](uint32_t j) { return p[j]; }, e - s);
+            q = part_of(h, parts);
+            keys[i] = q;
+            bytes = e - s + 1;
+        }
+        wave_count(s_c, 256, i < R, q, bytes);
     }
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < parts; q += blockDim.x) {
@@ -74,17 +99,20 @@ __global__ __launch_bounds__(256) void k_range_keys(const uint64_t *__restrict__
     for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) s_c[i] = 0;
     for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) s_split[i] = split[i];
     __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < R) {
-        const uint64_t k = key0[i];
-        uint32_t lo = 0, hi = ns;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_split[mid] <= k) lo = mid + 1; else hi = mid;
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < R; i0 += gridDim.x * blockDim.x) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint32_t lo = 0, bytes = 0;
+        if (i < R) {
+            const uint64_t k = key0[i];
+            uint32_t hi = ns;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_split[mid] <= k) lo = mid + 1; else hi = mid;
+            }
+            keys[i] = lo;
+            bytes = spans[i].y - spans[i].x + 1;
         }
-        keys[i] = lo;
-        atomicAdd(&s_c[lo], 1ull);
-        atomicAdd(&s_c[256 + lo], (unsigned long long)(spans[i].y - spans[i].x + 1));
+        wave_count(s_c, 256, i < R, lo, bytes);
     }
     __syncthreads();
     for (uint32_t q = threadIdx.x; q <= ns; q += blockDim.x) {
@@ -187,13 +215,14 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
     SG_TRY(slot(c, S_VALS, R, &v1));
     SG_TRY(slot(c, S_VALS2, R, &v2));
     if (R && !split) {
-        SG_LAUNCH(c, "part_keys", k_part_keys, (R + 255) / 256, 256, 0, d_buf, L.spans, R, parts, keys, cnt);
+        SG_LAUNCH(c, "part_keys", k_part_keys, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, d_buf, L.spans, R,
+                  parts, keys, cnt);
     } else if (R) {
         uint64_t *d_split;
         SG_TRY(slot(c, S_M_TMP2, 256, &d_split));
         if (parts > 1) SG_HIP(hipMemcpyAsync(d_split, split, 8 * (parts - 1), hipMemcpyHostToDevice, c->stream));
-        SG_LAUNCH(c, "range_keys", k_range_keys, (R + 255) / 256, 256, 0, L.keys, L.spans, R, d_split, parts - 1, keys,
-                  cnt);
+        SG_LAUNCH_B(c, "range_keys", 24.0 * R, k_range_keys, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, L.keys, L.spans, R,
+                  d_split, parts - 1, keys, cnt);
     }
     uint64_t *K;
     uint32_t *V;

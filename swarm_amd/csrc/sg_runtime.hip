@@ -165,7 +165,7 @@ int sg_ctx_create(int device, void *stream, sg_ctx **out) {
     sg_ctx *c = new sg_ctx();
     c->device = device;
     if (stream) {
-        c->stream = (hipStream_t)stream;
+        c->stream = stream == SG_NULL_STREAM ? (hipStream_t)0 : (hipStream_t)stream;
     } else {
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
             delete c;

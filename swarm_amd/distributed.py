@@ -12,6 +12,11 @@ Per step and rank:
 The union of the ranks' outputs is the global result; rank r owns the records that hash
 to r. (A byte-ordered global file is a k-way merge of the G sorted outputs, done where the
 file is written, outside this path.)
+
+The C5 path (1B host:port records, shards larger than one 4 GiB call) routes by key0 RANGE
+instead (sg_dev_partition_range with splitters agreed across ranks): rank r owns key range
+r, so the ranks' outputs concatenated in rank order are the global sort -u output, and each
+rank processes its range with swarm_amd.sharded (local range parts of < 4 GiB).
 """
 from __future__ import annotations
 
@@ -67,3 +72,41 @@ def build_prior_partition(ctx, candidates: torch.Tensor, group=None) -> torch.Te
     if r.uniq_bytes:
         ctx.memcpy(out.data_ptr(), r.uniq, int(r.uniq_bytes))
     return out[: int(r.uniq_bytes)]
+
+
+# ------------------------------------------------------------------ C5: range-partitioned shards
+def agree_splitters(ctx, pieces: Sequence[torch.Tensor], parts: int, samples_per_piece: int = 1 << 14,
+                    group=None):
+    """Splitters (parts - 1 key0 quantiles) from key0 samples of every rank's pieces."""
+    import numpy as np
+    from . import sharded
+    local = [ctx.key_sample(p.data_ptr(), p.numel(), samples_per_piece)[0] for p in pieces if p.numel()]
+    local = np.concatenate(local) if local else np.zeros(0, dtype=np.uint64)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        allv = [None] * dist.get_world_size(group)
+        dist.all_gather_object(allv, local, group=group)
+        local = np.concatenate(allv)
+    return sharded.choose_splitters(local, parts)
+
+
+def range_exchange(ctx, pieces: Sequence[torch.Tensor], gsplit, group=None, piece_bytes: int = 3 << 30):
+    """Route every piece into world key ranges, exchange, return this rank's range as
+    pieces of < piece_bytes ending at record boundaries."""
+    from . import sharded
+    parts = sharded.route(ctx, pieces, gsplit)
+    dev = pieces[0].device if len(pieces) else torch.device("cuda", ctx.device)
+    pb = [int(p.numel()) if p is not None else 0 for p in parts]
+    send = torch.cat([p for p in parts if p is not None]) if any(pb) else torch.empty(0, dtype=torch.uint8, device=dev)
+    del parts
+    recv = exchange_records(send, pb, group)
+    del send
+    return sharded.split_at_newlines(recv, piece_bytes) if recv.numel() else []
+
+
+def dedup_diff_range_step(ctx, cur_pieces, prior_local, gsplit, lsplit, group=None):
+    """One C5 step on this rank: range exchange (world > 1), then local range parts
+    (sharded.dedup_diff_large with the rank's fixed local splitters)."""
+    from . import sharded
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    mine = range_exchange(ctx, cur_pieces, gsplit, group) if world > 1 else list(cur_pieces)
+    return sharded.dedup_diff_large(ctx, mine, prior_local, splitters=lsplit)

@@ -121,8 +121,12 @@ def dedup_diff_large(ctx, cur_pieces: Sequence, prior_pieces: Sequence = (), par
         if c.numel() > PART_LIMIT or (p is not None and p.numel() > PART_LIMIT):
             raise ValueError("a key0 range holds more than 4 GiB: use more parts (smaller part_bytes)")
         st["max_part_bytes"] = max(st["max_part_bytes"], c.numel())
-        r = ctx.dedup_diff(c.data_ptr(), c.numel(), p.data_ptr() if p is not None else 0,
-                           p.numel() if p is not None else 0)
+        try:
+            r = ctx.dedup_diff(c.data_ptr(), c.numel(), p.data_ptr() if p is not None else 0,
+                               p.numel() if p is not None else 0)
+        except Exception as e:
+            raise type(e)(e.rc, "%s (part of %d bytes at %#x, prior %s)" % (
+                e, c.numel(), c.data_ptr(), None if p is None else p.numel())) if hasattr(e, "rc") else e
         uniq.append(_take(ctx, r.uniq, r.uniq_bytes, dev))
         fresh.append(_take(ctx, r.fresh, r.fresh_bytes, dev) if p is not None else uniq[-1])
         st["in_records"] += int(r.in_records)

@@ -81,3 +81,53 @@ def test_two_ranks_on_one_gpu():
     f_all = sorted(rec for _, _, f, _ in res for rec in S.parse_records(f))
     assert S.serialize(u_all) == eu
     assert S.serialize(f_all) == ef
+
+
+def range_worker(rank, world, port, q):
+    """C5 path: key0-range exchange + local range parts; rank outputs in rank order must be
+    the global sort -u / comm -13 output."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import swarm_amd
+    from swarm_amd import corpus, sharded
+    from swarm_amd import distributed as D
+    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    pool = corpus.host_pool_gpu(20_000, seed=5)
+    U = 20_000 * len(corpus.PORTS)
+    prior_raw = corpus.hostport_pieces(pool, 150_000, U // 10, U, seed=900 + rank, per_piece=40_000)
+    cur = corpus.hostport_pieces(pool, 200_000, 0, U, seed=100 + rank, per_piece=60_000)
+    gsplit = D.agree_splitters(ctx, prior_raw, world)
+    mine = D.range_exchange(ctx, prior_raw, gsplit, piece_bytes=1 << 20)
+    import numpy as np
+    lsplit = sharded.choose_splitters(np.concatenate([ctx.key_sample(p.data_ptr(), p.numel(), 512)[0] for p in mine]), 3)
+    pu, _, _ = sharded.dedup_diff_large(ctx, mine, (), splitters=lsplit)
+    u, f, st = D.dedup_diff_range_step(ctx, cur, sharded.split_at_newlines(pu, 1 << 20), gsplit, lsplit)
+    torch.cuda.synchronize()
+    q.put((rank, u.cpu().numpy().tobytes(), f.cpu().numpy().tobytes(),
+           b"".join(p.cpu().numpy().tobytes() for p in cur), b"".join(p.cpu().numpy().tobytes() for p in prior_raw)))
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_range_sharded_global_order():
+    import torch.multiprocessing as mp
+    world = 2
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    port = free_port()
+    procs = [mctx.Process(target=range_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    cur_all = b"".join(r[3] for r in res)
+    prior_all = S.dedup(b"".join(r[4] for r in res))
+    eu, ef = S.dedup_diff(cur_all, prior_all)
+    assert b"".join(r[1] for r in res) == eu
+    assert b"".join(r[2] for r in res) == ef
