@@ -47,10 +47,12 @@ def pmc_traffic(workload, kernel):
     return t
 
 
-def roofline_of(stats, kernel=None, workload=None):
+def roofline_of(stats, kernel=None, workload=None, full=None):
     """The dominant kernel and its achieved GB/s: the algorithmic bytes the library credited
     to its launches (SURVEY.md §8(d) model) over the HIP-event time of the
-    same launches, recorded on the launch stream inside the timed region."""
+    same launches, recorded on the launch stream inside the timed region. A kernel whose
+    byte model needs a profiling-only count (the segment sorts) takes its bytes per launch
+    from the fully profiled step `full`."""
     if not stats:
         return None
     if kernel is None:
@@ -60,6 +62,8 @@ def roofline_of(stats, kernel=None, workload=None):
     launches, ms, by = stats[kernel]
     if not launches or ms <= 0:
         return None
+    if not by and full and kernel in full and full[kernel][0]:
+        by = full[kernel][2] / full[kernel][0] * launches
     ach = by / (ms * 1e-3) / 1e9
     out = {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
@@ -162,7 +166,7 @@ def bench_c3(args):
                    "bytes": int(d.numel()), "automaton_states": m.info()["states"]},
         "gbps": round(d.numel() * args.steps / el / 1e9, 2),
         "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records)},
-        "roofline": roofline_of(stats, dominant, "c3"),
+        "roofline": roofline_of(stats, dominant, "c3", full),
         "cpu_baseline": cpu,
         "kernels": kernel_table(full),
         "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
@@ -222,7 +226,7 @@ def bench_c4(args):
                    "compile_s": round(compile_s, 2)},
         "gbps": round(d.numel() * args.steps / el / 1e9, 2),
         "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records)},
-        "roofline": roofline_of(stats, dominant, "c4"),
+        "roofline": roofline_of(stats, dominant, "c4", full),
         "cpu_baseline": cpu,
         "kernels": kernel_table(full),
         "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
@@ -300,7 +304,7 @@ def bench_fields(args):
                                % (n_lines / 1e6, len(T)), "bytes": int(d.numel()), "templates": tm.info()},
         "gbps": round(d.numel() * args.steps / el / 1e9, 2),
         "records": {"in": R, "field_rows": int(holder["rows"].rows), "template_matches": int(r.n)},
-        "roofline": roofline_of(stats, dominant, "fields"),
+        "roofline": roofline_of(stats, dominant, "fields", full),
         "cpu_baseline": cpu,
         "kernels": kernel_table(full),
         "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
@@ -430,7 +434,7 @@ def bench_c5(args):
             "gbps": round((cur_bytes + prior_bytes + ub + fb) * world * args.steps / el / 1e9, 2),
             "records": {"in_rank0": st["in_records"], "unique_rank0": st["uniq_records"],
                         "new_rank0": st["fresh_records"], "max_part_bytes": st["max_part_bytes"]},
-            "roofline": roofline_of(stats, dominant, "c5"),
+            "roofline": roofline_of(stats, dominant, "c5", full),
             "cpu_baseline": cpu,
             "kernels": kernel_table(full),
             "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
@@ -559,7 +563,7 @@ def main():
     info = {"R": int(r.in_records), "n": int(nrecv), "Rp": int(r.prior_records), "n_prior": int(prior.numel()),
             "U": int(r.uniq_records), "ub": int(r.uniq_bytes), "F": int(r.fresh_records), "fb": int(r.fresh_bytes)}
 
-    roofline = roofline_of(stats, dominant, "c2")
+    roofline = roofline_of(stats, dominant, "c2", full)
     kernels = kernel_table(full)
     gpu_ms_sum = sum(v[1] for v in full.values())
 

@@ -38,23 +38,24 @@ __host__ __device__ __forceinline__ uint32_t part_of(uint64_t h, uint32_t parts)
     return (uint32_t)(((h >> 32) * (uint64_t)parts) >> 32);
 }
 
-// Add (1 record, `bytes`) to counter slot `q` of the block's LDS histogram with one LDS
-// atomic per distinct q in the wave (few parts: most waves hold one or two values), not
-// one per lane on a handful of hot addresses.
+// Add (1 record, `bytes`) to counter slot `q` of the block's LDS histogram: one LDS
+// atomic pair per wave when the whole wave routes to one part (sorted inputs, few
+// parts), else one per lane (LDS atomics spread over the parts' addresses).
 __device__ __forceinline__ void wave_count(unsigned long long *s_c, uint32_t stride, bool act, uint32_t q,
                                            uint32_t bytes) {
-    uint64_t pending = __ballot(act);
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const uint32_t lq = (uint32_t)__shfl((int)q, leader, 64);
-        const bool mine = act && q == lq;
-        const uint64_t m = __ballot(mine);
-        const uint64_t b = wave_sum<uint64_t>(mine ? (uint64_t)bytes : 0ull);
+    const uint64_t am = __ballot(act);
+    if (!am) return;
+    const int leader = __ffsll((long long)am) - 1;
+    const uint32_t lq = (uint32_t)__shfl((int)q, leader, 64);
+    if (__ballot(act && q != lq) == 0) {
+        const uint64_t b = wave_sum<uint64_t>(act ? (uint64_t)bytes : 0ull);
         if (lane_id() == leader) {
-            atomicAdd(&s_c[lq], (unsigned long long)__popcll(m));
+            atomicAdd(&s_c[lq], (unsigned long long)__popcll(am));
             atomicAdd(&s_c[stride + lq], (unsigned long long)b);
         }
-        pending &= ~m;
+    } else if (act) {
+        atomicAdd(&s_c[q], 1ull);
+        atomicAdd(&s_c[stride + q], (unsigned long long)bytes);
     }
 }
 

@@ -270,30 +270,30 @@ __device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2
     return rec_cmp8(S, xa.x, xa.y - xa.x, xb.x, xb.y - xb.x, 7u + 7u * SEG_CH);
 }
 
-// 16 lanes per small segment (<= SEG_SMALL members), lane per member.
-__global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
-                                                   const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
-                                                   const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n) {
-    const uint32_t lane = lane_id(), gl = lane & 15u, gbase = lane & ~15u;
-    const uint32_t q = blockIdx.x * 16u + (threadIdx.x >> 4);
-    const bool live = q < nh;
-    const uint32_t a = live ? heads[q] : 0u;
-    const uint32_t pe = a + 1u + gl;
-    const bool eb = !live || pe >= n || gl == 15u || brk[pe];
-    const uint32_t me = (uint32_t)(__ballot(eb) >> gbase) & 0xffffu;
-    const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);  // members: a .. a+k-1
+// Rank the k members a.. of one segment with the G lanes gbase.. of the wave (lane gl of
+// the group = member gl): rank = members ordered before it (ties by index), dup = an
+// equal member with a smaller index exists. Writes the member's span at its rank.
+template <int G>
+__device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
+                                               uint8_t *__restrict__ dup, uint32_t a, uint32_t k, uint32_t gl,
+                                               uint32_t gbase, bool live) {
     const bool act = live && gl < k;
     const uint2 x = act ? SS[a + gl] : make_uint2(0u, 0u);
     const SegKeys mk = act ? seg_keys(S, x) : SegKeys{{0, 0, 0, 0}};
     uint32_t rank = 0;
     bool d = false;
-    for (uint32_t j = 0; j < k; ++j) {
-        const int src = (int)(gbase + j);
+    const uint32_t kk = live ? k : 0u;
+    // loop bound uniform across the wave (max over its groups)
+    uint32_t kmax = kk;
+#pragma unroll
+    for (int o = G; o < 64; o <<= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    for (uint32_t j = 0; j < kmax; ++j) {
+        const int src = (int)(gbase + (j < kk ? j : 0u));
         SegKeys ok;
 #pragma unroll
         for (int c = 0; c < SEG_CH; ++c) ok.c[c] = __shfl(mk.c[c], src, 64);
         const uint2 y = make_uint2((uint32_t)__shfl(x.x, src, 64), (uint32_t)__shfl(x.y, src, 64));
-        if (act && j != gl) {
+        if (act && j < kk && j != gl) {
             const int c = seg_cmp(S, mk, x, ok, y);
             if (c > 0 || (c == 0 && j < gl)) ++rank;
             if (c == 0 && j < gl) d = true;
@@ -305,39 +305,62 @@ __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S
     }
 }
 
-// One wave per larger segment (<= 64 members): lane per member.
+// 16 lanes per small segment (<= SEG_SMALL members).
+__global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
+                                                   const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
+                                                   const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n) {
+    const uint32_t lane = lane_id(), gl = lane & 15u, gbase = lane & ~15u;
+    const uint32_t q = blockIdx.x * 16u + (threadIdx.x >> 4);
+    const bool live = q < nh;
+    const uint32_t a = live ? heads[q] : 0u;
+    const uint32_t pe = a + 1u + gl;
+    const bool eb = !live || pe >= n || gl == 15u || brk[pe];
+    const uint32_t me = (uint32_t)(__ballot(eb) >> gbase) & 0xffffu;
+    const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);  // members: a .. a+k-1
+    seg_rank_group<16>(S, SS, dup, a, k, gl, gbase, live);
+}
+
+// Larger segments (17..64 members), two heads per wave: two half-waves when both segments
+// hold <= 32 members (the common case: a host's few ports x a few copies), else one
+// segment after the other on the whole wave.
 __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                   const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
                                                   const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n,
                                                   uint32_t *err) {
-    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t q0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2u;
     const uint32_t lane = lane_id();
-    if (q >= nh) return;
-    const uint32_t a = heads[q];
-    const uint32_t pe = a + 1u + lane;
-    const uint64_t me = __ballot(pe >= n || brk[pe]);
-    if (!me) { if (lane == 0) atomicOr(err, 1u); return; }
-    const uint32_t k = 1u + (uint32_t)(__ffsll((long long)me) - 1);
-    const bool act = lane < k;
-    const uint2 x = act ? SS[a + lane] : make_uint2(0u, 0u);
-    const SegKeys mk = act ? seg_keys(S, x) : SegKeys{{0, 0, 0, 0}};
-    uint32_t rank = 0;
-    bool d = false;
-    for (uint32_t j = 0; j < k; ++j) {
-        SegKeys ok;
+    if (q0 >= nh) return;
+    uint32_t a[2], k[2];
 #pragma unroll
-        for (int c = 0; c < SEG_CH; ++c) ok.c[c] = __shfl(mk.c[c], (int)j, 64);
-        const uint2 y = make_uint2((uint32_t)__shfl(x.x, (int)j, 64), (uint32_t)__shfl(x.y, (int)j, 64));
-        if (act && j != lane) {
-            const int c = seg_cmp(S, mk, x, ok, y);
-            if (c > 0 || (c == 0 && j < lane)) ++rank;
-            if (c == 0 && j < lane) d = true;
-        }
+    for (int t = 0; t < 2; ++t) {
+        const bool live = q0 + t < nh;
+        a[t] = live ? heads[q0 + t] : 0u;
+        const uint32_t pe = a[t] + 1u + lane;
+        const uint64_t me = __ballot(!live || pe >= n || brk[pe]);
+        if (!me) { if (lane == 0) atomicOr(err, 1u); return; }
+        k[t] = live ? 1u + (uint32_t)(__ffsll((long long)me) - 1) : 0u;
     }
-    if (act) {
-        SS[a + rank] = x;
-        dup[a + rank] = d ? 1 : 0;
+    if (k[0] <= 32u && k[1] <= 32u) {
+        const uint32_t t = lane >> 5;
+        seg_rank_group<32>(S, SS, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u, (t ? k[1] : k[0]) > 0);
+    } else {
+        seg_rank_group<64>(S, SS, dup, a[0], k[0], lane, 0u, true);
+        if (k[1]) seg_rank_group<64>(S, SS, dup, a[1], k[1], lane, 0u, true);
     }
+}
+
+// Profiling only: members of the listed bad segments (their heads), for the byte model of
+// the segment sorts (span in/out, the record bytes behind the chunk keys, dup flag).
+__global__ __launch_bounds__(256) void k_seg_members(const uint8_t *__restrict__ brk, const uint32_t *__restrict__ heads,
+                                                     uint32_t nh, uint32_t n, unsigned long long *__restrict__ out) {
+    uint32_t sum = 0;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nh; q += gridDim.x * blockDim.x) {
+        uint32_t j = heads[q] + 1;
+        while (j < n && !brk[j] && j - heads[q] < 64u) ++j;
+        sum += j - heads[q];
+    }
+    sum = wave_sum(sum);
+    if (lane_id() == 0 && sum) atomicAdd(out, (unsigned long long)sum);
 }
 
 // ------------------------------------------------------------------ gathers / output
@@ -714,7 +737,21 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, S_ERR, 4, &err));
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
     if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R);
-    if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for(nb, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err);
+    if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err);
+    if (c->profile && c->prof_only.empty() && (ns || nb)) {  // full-profile steps only
+        // byte model: per member its span read + written, ~4 chunk keys of record bytes, flag
+        unsigned long long *mc;
+        SG_TRY(slot(c, S_M_CNT, 4, &mc));
+        SG_HIP(hipMemsetAsync(mc, 0, 16, c->stream));
+        if (ns) SG_LAUNCH(c, "seg_members", k_seg_members, std::min<uint32_t>(grid_for(ns, 256), 1024u), 256, 0, brk, hs,
+                          ns, R, mc);
+        if (nb) SG_LAUNCH(c, "seg_members", k_seg_members, std::min<uint32_t>(grid_for(nb, 256), 1024u), 256, 0, brk, hb,
+                          nb, R, mc + 1);
+        unsigned long long m[2];
+        SG_TRY(ctx_readback(c, m, mc, 16));
+        prof_bytes(c, "seg_small", 45.0 * (double)m[0]);
+        prof_bytes(c, "seg_wave", 45.0 * (double)m[1]);
+    }
 
     // compact the unique records
     uint8_t *ub;
