@@ -32,6 +32,10 @@ step "bench fields"
 timeout -k 10 300 python -u bench.py --workload fields --steps 3 --warmup 1 > "$OUT/bench_fields.json" 2> "$OUT/bench_fields.err" || { tail -20 "$OUT/bench_fields.err"; exit 1; }
 cat "$OUT/bench_fields.json"
 
+step "bench c5"
+timeout -k 10 600 python -u bench.py --workload c5 --steps 3 --warmup 1 > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err" || { tail -20 "$OUT/bench_c5.err"; exit 1; }
+cat "$OUT/bench_c5.json"
+
 step "rocprofv3 stats c2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_c2" -o c2 --output-format csv -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/prof_c2.json" 2> "$OUT/prof_c2.err" || { tail -20 "$OUT/prof_c2.err"; exit 1; }
@@ -46,6 +50,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_c4" -o c4 --
 step "rocprofv3 stats fields"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_fields" -o fields --output-format csv -- \
     python3 bench.py --workload fields --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/prof_fields.json" 2> "$OUT/prof_fields.err" || { tail -20 "$OUT/prof_fields.err"; exit 1; }
+
+step "rocprofv3 stats c5"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_c5" -o c5 --output-format csv -- \
+    python3 bench.py --workload c5 --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/prof_c5.json" 2> "$OUT/prof_c5.err" || { tail -20 "$OUT/prof_c5.err"; exit 1; }
 
 for ctr in FETCH_SIZE WRITE_SIZE; do
   step "pmc $ctr c2"
