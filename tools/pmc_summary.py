@@ -21,6 +21,8 @@ from collections import defaultdict
 
 def per_kernel_counter(path, counter):
     acc = defaultdict(lambda: [0, 0.0])
+    if not os.path.exists(path):  # no PMC pass for this workload: stats only
+        return {}
     with open(path) as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] != counter:
