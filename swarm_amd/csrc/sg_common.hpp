@@ -2,12 +2,10 @@
 //
 // Host side: thread-local error text, the sg_ctx (device, stream, grow-only HBM buffer
 // slots, optional per-kernel HIP-event timing) and a launch wrapper.
-// Device side: wave64/block scans and the decoupled look-back used by every single-pass
-// kernel (line split, compaction, onesweep radix passes). Look-back status words are
-// 8-byte {flag:2 | value:62} granules written with one relaxed agent-scope (sc1) store
-// and polled with relaxed agent-scope loads: the data IS the flag, so no fences are
-// needed (MI355X_MICROARCH.md "Valid forms", R2 granule). Tiles take their id from an
-// atomic ticket so every tile a waiter depends on has already been dispatched.
+// Device side: wave64/block scans, the one-block tile scan declaration shared by every
+// reduce-then-scan kernel pair (count pass -> tile scan -> apply pass), and record
+// compare/key helpers. No kernel waits on another block: single-pass decoupled look-back
+// was measured slower on MI355X (a cross-XCD round trip per tile).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -56,7 +54,7 @@ enum Slot : int {
     S_P_UNIQ, S_P_SORTED_KEYS,
     // partition / match
     S_PART, S_PART_OUT, S_M_HITS, S_M_SIG, S_M_LINES, S_M_TMP, S_M_TMP2, S_M_CNT,
-    S_IN, S_IN2, S_CUR_UR, S_CUR_UK, S_RS_STATUS,
+    S_IN, S_IN2, S_CUR_UR, S_CUR_UK,
     // sorted materialisation (shared temporaries) and per-view outputs
     S_SBUF, S_SSPANS, S_DUP, S_BAD, S_BRK, S_MIRROR, S_EMIT, S_EMIT2, S_EMIT3, S_ERR,
     S_U_SPANS, S_U_KEYS, S_P_UBUF, S_P_USPANS, S_P_UKEYS, S_FRESHF, S_ECACHE, S_TILES, S_RS_TCNT, S_RS_DIGITS,
@@ -146,17 +144,6 @@ void prof_bytes(sg_ctx *c, const char *name, double bytes);
 constexpr uint64_t MAX_BYTES = 0xFFFF0000ull;  // 32-bit record offsets with headroom
 
 // ------------------------------------------------------------------ device helpers
-#define LB_FLAG_AGG 1ull
-#define LB_FLAG_INC 2ull
-#define LB_VAL_MASK ((1ull << 62) - 1)
-
-__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t flag, uint64_t v) {
-    __hip_atomic_store(p, (flag << 62) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
-    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 template <class T>
@@ -196,33 +183,6 @@ __device__ __forceinline__ T block_excl_scan(T v, T *total, T *lds) {
     return woff + inc - v;
 }
 
-// Decoupled look-back by ONE full wave: returns the exclusive prefix of tile `tile`
-// (values packed so that field sums never carry). Tile 0 must not call this.
-__device__ __forceinline__ uint64_t wave_lookback(const uint64_t *status, int64_t tile) {
-    const int lane = lane_id();
-    uint64_t excl = 0;
-    int64_t base = tile - 1;
-    uint32_t spins = 0;
-    while (true) {
-        const int64_t t = base - lane;
-        const uint64_t s = (t >= 0) ? lb_load(status + t) : (LB_FLAG_INC << 62);
-        const uint32_t flag = (uint32_t)(s >> 62);
-        const uint64_t inc_mask = __ballot(flag == LB_FLAG_INC);
-        const uint64_t empty_mask = __ballot(flag == 0);
-        const int first_inc = inc_mask ? (__ffsll((long long)inc_mask) - 1) : 64;
-        const uint64_t need = (first_inc >= 63) ? ~0ull : ((2ull << first_inc) - 1);
-        if (empty_mask & need) {
-            if (++spins > 64) __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        uint64_t v = (lane <= first_inc) ? (s & LB_VAL_MASK) : 0ull;
-        excl += wave_sum(v);
-        if (first_inc < 64) break;
-        base -= 64;
-    }
-    return excl;
-}
-
 // Exclusive scan of per-tile aggregates (u64 whose packed fields never carry), ONE block:
 // the middle step of every reduce-then-scan kernel pair (count pass -> this -> apply pass).
 // On MI355X a single-pass decoupled look-back over small tiles waits a cross-XCD round trip
@@ -231,13 +191,6 @@ constexpr int TS_BLOCK = 1024;
 constexpr int TS_ITEMS = 4;
 __global__ __launch_bounds__(TS_BLOCK) void k_tile_scan(const uint64_t *__restrict__ tot, uint32_t nt,
                                                         uint64_t *__restrict__ pre, uint64_t *__restrict__ total);
-
-// Tile ticket: dynamic tile ids in dispatch order (forward progress for look-back).
-__device__ __forceinline__ uint32_t take_ticket(uint32_t *counter, uint32_t *lds_slot) {
-    if (threadIdx.x == 0) *lds_slot = atomicAdd(counter, 1u);
-    __syncthreads();
-    return *lds_slot;
-}
 
 // Bytewise compare of two records starting `off` bytes in (both have > off bytes or
 // not — lengths decide). Returns <0, 0, >0 like memcmp-then-length.

@@ -11,11 +11,13 @@
 //               step reads S sequentially instead of gathering records from the input
 //   adjacent -> dup[i] = record i equals record i-1 (same segment, bytes from S);
 //               bad[i] = same segment but different bytes (segment not yet ordered)
-//   run sort -> each segment holding a bad position (<= 64 records) is sorted by one wave
-//               in LDS by full byte compare, rewritten in place in S, dup recomputed
+//   run sort -> each segment holding a bad position is ranked in registers (16-lane
+//               groups up to 16 records, half or whole waves up to 64) by its 7-byte chunk
+//               keys at offsets 7..34 and a byte compare beyond; spans permuted in place
 //   emit     -> the records with dup == 0: the sort -u output, contiguous, + spans/key0
-//   diff     -> merge-path tiles over the unique output and the prior's sorted unique
-//               view (both contiguous), equality from LDS-staged keys + wide compares
+//   diff     -> per 1024 unique records, the prior's key range found by a 64-ary wave
+//               search, its keys staged in LDS; membership by binary search over key0,
+//               then wide compares (binary search over runs of equal key0)
 //   emit     -> the records absent from the prior: the new-record output
 // The result is exact for any input (NULs, CR, 0xff, long shared prefixes, duplicates of
 // any multiplicity): ordering is decided by bytes, never by a hash.

@@ -1,5 +1,5 @@
-// sg_emit.hpp — "emit": order-preserving select + byte-offset scan + record copy, fused
-// into ONE single-pass kernel (decoupled look-back).
+// sg_emit.hpp — "emit": order-preserving select + byte-offset scan + record copy, as a
+// reduce-then-scan pair (k_emit_count -> k_tile_scan -> k_emit_<use>).
 //
 // Item i (0 <= i < n) names a record of `src` by (start, len) and whether it is kept. Kept
 // records are written to `dst` in item order, each '\n'-terminated; optionally the j-th
