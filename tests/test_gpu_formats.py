@@ -137,3 +137,16 @@ def test_json_device_rows_match_and_feed_matcher(sg):
     m = sg.Matcher([b"nginx", b"Login", b"\xe6\x97\xa5"], "literal")
     assert m.match(rows) == S.literal_hits(o_rows, [b"nginx", b"Login", b"\xe6\x97\xa5"])
     ctx.close()
+
+
+def test_json_long_lines_and_many_rows(sg):
+    """Lines of 100 KB+ (a long title, a 5,000-element tech array) and rows past 2^16."""
+    big = json.dumps({"title": "t" * 120_000 + "é", "tech": ["x%d" % i for i in range(5000)],
+                      "url": "u"}).encode()
+    lines = [big] + corpus.httpx_json_pool(20_000, seed=17)
+    check(sg, b"\n".join(lines) + b"\n", [b"title", b"tech", b"url"])
+
+
+def test_nmap_many_hosts_crlf(sg):
+    txt = corpus.nmap_report(100_000, seed=9).replace(b"\n", b"\r\n")
+    assert sg.nmap_ports(txt) == S.nmap_host_ports(txt)

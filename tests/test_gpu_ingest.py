@@ -76,3 +76,14 @@ def test_empty_ingest(ctx):
     with swarm_amd.Ingest(ctx) as ing:
         assert ing.finish()[1] == 0
         assert ing.dedup_diff(None) == (b"", b"")
+
+
+def test_byte_by_byte_pieces(ctx):
+    import swarm_amd
+    body = b"".join(b"r%d.example.com\n" % (i % 977) for i in range(5000))
+    with swarm_amd.Ingest(ctx) as ing:
+        for i in range(len(body)):
+            ing.append(body[i:i + 1])
+        u, f = ing.dedup_diff(b"r1.example.com\n")
+    eu, ef = S.dedup_diff(body, b"r1.example.com\n")
+    assert u == eu and f == ef

@@ -73,3 +73,18 @@ def test_dedup_large_unsorted_prior_and_no_prior(ctx):
     assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
     u2, f2, _ = sharded.dedup_diff_large(ctx, [dev(cur)], (), part_bytes=1 << 20)
     assert u2.cpu().numpy().tobytes() == eu and f2.cpu().numpy().tobytes() == eu
+
+
+def test_many_tiny_parts_and_skewed_keys(ctx):
+    """Up to 256 parts (the routing maximum), many empty ones, and a key0 value shared by a
+    large run of records (it cannot be split: it stays in one part)."""
+    from swarm_amd import sharded
+    buf, ids = corpus.subdomains(100_000, seed=35)
+    same = b"".join(b"samekey-%d.example\n" % (i % 5000) for i in range(60_000))
+    cur = buf.tobytes() + same
+    prior = S.dedup(same[: len(same) // 3])
+    u, f, st = sharded.dedup_diff_large(ctx, sharded.split_at_newlines(dev(cur), 512 << 10), [dev(prior)],
+                                        part_bytes=16 << 10)
+    assert st["parts"] == 256
+    eu, ef = S.dedup_diff(cur, prior)
+    assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
