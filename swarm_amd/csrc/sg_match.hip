@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <deque>
 #include <map>
+#include <unordered_map>
 #include <string.h>
 
 #include "sg_regex.hpp"
@@ -288,6 +289,33 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
     std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
         return T->pat_off[x + 1] - T->pat_off[x] < T->pat_off[y + 1] - T->pat_off[y];
     });
+    // How many patterns contain each 4-/8-byte gram: a gram that many signatures share is
+    // a common substring of the domain ("openssh_", "server: "), so text holds it far more
+    // often than a gram unique to one signature (C4 factors: 8.7 confirmed grams per banner
+    // for 1 factor hit when anchors ignored this).
+    std::unordered_map<uint64_t, uint32_t> share;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t len = T->pat_off[i + 1] - T->pat_off[i];
+        const uint32_t c = cls_of_len(len);
+        if (c < 3) continue;
+        const uint32_t L = lit_len(c);
+        std::vector<uint64_t> mine;
+        for (uint32_t o = 0; o + L <= len; ++o) {
+            uint64_t g = 0;
+            memcpy(&g, &T->pat[T->pat_off[i] + o], L);
+            mine.push_back(g | ((uint64_t)L << 60));
+        }
+        std::sort(mine.begin(), mine.end());
+        mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
+        for (uint64_t g : mine) share[g]++;
+    }
+    auto shared_by = [&](uint32_t i, uint32_t o, uint32_t L) -> uint32_t {
+        if (L < 4) return 0;
+        uint64_t g = 0;
+        memcpy(&g, &T->pat[T->pat_off[i] + o], L);
+        auto it = share.find(g | ((uint64_t)L << 60));
+        return it == share.end() ? 0u : it->second;
+    };
     std::vector<std::vector<uint32_t>> load(LIT_CLASSES);
     for (uint32_t c = 0; c < LIT_CLASSES; ++c) load[c].assign(cnt[c] ? (1u << T->bits[c]) : 1, 0);
     for (uint32_t i : order) {
@@ -298,7 +326,9 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         for (uint32_t o = 0; o <= last && o < 256; ++o) {  // anchor fits the bucket record's 8 bits
             const uint32_t lo = word_at(i, o, L), hi = (L == 8) ? word_at(i, o + 4, 4) : 0u;
             const uint32_t h = lit_h(lo, hi, c, T->bits[c]);
-            const uint64_t cost = (uint64_t)load[c][h] * 16 + gram_commonness(&T->pat[T->pat_off[i] + o], L);
+            static const uint32_t w_share = getenv("SG_LIT_SHARE_W") ? (uint32_t)atoi(getenv("SG_LIT_SHARE_W")) : 64u;
+            const uint64_t cost = (uint64_t)(std::max(shared_by(i, o, L), 1u) - 1) * w_share + (uint64_t)load[c][h] * 16 +
+                                  gram_commonness(&T->pat[T->pat_off[i] + o], L);
             if (cost < best) { best = cost; anc[i] = o; hb[i] = h; fp[i] = lit_fp(lo, hi, c); }
         }
         load[c][hb[i]]++;
@@ -583,7 +613,6 @@ struct LitArgs {
     uint32_t dbg_mode;                   // bit 0: skip pass 2, bit 1: skip pass 1 probes
 };
 
-constexpr int LS_BLOCK = 256;
 constexpr uint32_t LS_HB = 256;    // per-block LDS hit buffer (entries)
 constexpr uint32_t LS_HALO = 64;   // text bytes staged on each side of the tile
 constexpr uint32_t LS_Q = 512;     // per-block candidate queue (entries: pos:14 | class:3 | record:14)
@@ -665,20 +694,20 @@ __device__ __forceinline__ void lit_emit(const Args &a, Push &push, uint32_t rec
 // then compacted into an LDS queue and pass 2 spreads them over all lanes: confirm against
 // the bucket's entry fingerprints, then byte-compare the pattern (16-B rows from L2, text
 // from the LDS tile). Hits go through a per-block LDS buffer flushed with one atomic.
-template <int BPT, uint32_t CM>
-__global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
-    constexpr int TILE = LS_BLOCK * BPT;
+template <int BLK, int BPT, uint32_t CM>
+__global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
+    constexpr int TILE = BLK * BPT;
     constexpr int NW = BPT / 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     __shared__ __attribute__((aligned(16))) uint8_t s_t[LS_HALO + TILE + LS_HALO];
     __shared__ unsigned long long s_hits[LS_HB];
     __shared__ uint32_t s_q[LS_Q];
     __shared__ uint2 s_kf[LS_Q];  // per queued candidate: (bucket, fingerprint)
-    __shared__ uint32_t s_red[LS_BLOCK / 64];
+    __shared__ uint32_t s_red[BLK / 64];
     __shared__ uint32_t s_hn, s_g, s_base, s_ebase;
     uint32_t *s_bm = s_dyn;
     uint16_t *s_rank = reinterpret_cast<uint16_t *>(s_dyn + a.bm_words);
-    for (uint32_t q = threadIdx.x; q < a.bm_words; q += LS_BLOCK) { s_bm[q] = a.bitmap[q]; s_rank[q] = a.rank[q]; }
+    for (uint32_t q = threadIdx.x; q < a.bm_words; q += BLK) { s_bm[q] = a.bitmap[q]; s_rank[q] = a.rank[q]; }
     if (threadIdx.x == 0) s_hn = 0;
     __syncthreads();
     const uint32_t t = threadIdx.x;
@@ -691,8 +720,29 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
         if (i < LS_HB) {
             s_hits[i] = v;
         } else {
-            const uint32_t g = atomicAdd(a.hit_count, 1u);
+            // overflow: one global atomic per wave (the lanes pushing now), not per event
+            const uint64_t act = __ballot(1);
+            const int lead = __ffsll((long long)act) - 1;
+            uint32_t g0 = 0;
+            if (lane_id() == lead) g0 = atomicAdd(a.hit_count, (uint32_t)__popcll(act));
+            const uint32_t g = (uint32_t)__shfl((int)g0, lead) + (uint32_t)__popcll(act & ((1ull << lane_id()) - 1));
             if (g < a.cap) a.hits[g] = v;
+        }
+    };
+    // drain the LDS hit buffer with one global atomic (block-uniform call sites only)
+    auto flush = [&](bool force) {
+        const uint32_t hn = min(s_hn, LS_HB);
+        if (hn >= LS_HB / 2 || (force && hn)) {
+            __syncthreads();
+            if (t == 0) s_g = atomicAdd(a.hit_count, hn);
+            __syncthreads();
+            for (uint32_t i = t; i < hn; i += BLK) {
+                const uint32_t g = s_g + i;
+                if (g < a.cap) a.hits[g] = s_hits[i];
+            }
+            __syncthreads();
+            if (t == 0) s_hn = 0;
+            __syncthreads();
         }
     };
 
@@ -755,12 +805,12 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
         const uint64_t full = (BPT == 64) ? ~0ull : ((1ull << (BPT & 63)) - 1);
         const uint64_t sm = ~m & ((m << 1) | cin) & full;
         uint32_t tot;
-        const uint32_t excl = block_excl_scan<LS_BLOCK>((uint32_t)__popcll(sm), &tot, s_red);
+        const uint32_t excl = block_excl_scan<BLK>((uint32_t)__popcll(sm), &tot, s_red);
         if (a.spans_out) {
             // the record spans of this tile, as k_lines writes them (k-th start / k-th end)
             const uint64_t em = m & ~((m << 1) | cin) & full;
             uint32_t etot;
-            const uint32_t eexcl = block_excl_scan<LS_BLOCK>((uint32_t)__popcll(em), &etot, s_red);
+            const uint32_t eexcl = block_excl_scan<BLK>((uint32_t)__popcll(em), &etot, s_red);
             uint32_t si = s_base + excl, ei = s_ebase + eexcl;
             for (uint64_t bits = sm; bits; bits &= bits - 1) a.spans_out[si++].x = (uint32_t)(my0 + __ffsll((long long)bits) - 1);
             for (uint64_t bits = em; bits; bits &= bits - 1) a.spans_out[ei++].y = (uint32_t)(my0 + __ffsll((long long)bits) - 1);
@@ -822,7 +872,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
 #pragma unroll
         for (uint32_t c = 0; c < LIT_CLASSES; ++c) ncand += (uint32_t)__popcll(cand[c]);
         uint32_t qtot;
-        const uint32_t qex = block_excl_scan<LS_BLOCK>(ncand, &qtot, s_red);
+        const uint32_t qex = block_excl_scan<BLK>(ncand, &qtot, s_red);
         const uint32_t lrec0 = excl;  // tile-local index of this thread's first record start
         for (uint32_t r0 = 0; r0 < qtot; r0 += LS_Q) {
             uint32_t qi = qex;
@@ -846,7 +896,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
             __syncthreads();
             const uint32_t qn = min(LS_Q, qtot - r0);
             // stage 1 (LDS only): gram -> bucket and fingerprint
-            for (uint32_t i = t; i < qn; i += LS_BLOCK) {
+            for (uint32_t i = t; i < qn; i += BLK) {
                 const uint32_t ent = s_q[i];
                 const int q = (int)(ent >> 17);
                 const uint32_t c = (ent >> 14) & 7u;
@@ -865,12 +915,12 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
             }
             // stage 2: LS_BATCH candidates per lane, their bucket records and first pattern
             // rows loaded together, then verified against the LDS text
-            for (uint32_t i0 = t; i0 < qn; i0 += LS_BATCH * LS_BLOCK) {
+            for (uint32_t i0 = t; i0 < qn; i0 += LS_BATCH * BLK) {
                 uint4 br[LS_BATCH];
                 uint32_t fpv[LS_BATCH];
 #pragma unroll
                 for (int u = 0; u < LS_BATCH; ++u) {
-                    const uint32_t i = i0 + u * LS_BLOCK;
+                    const uint32_t i = i0 + u * BLK;
                     br[u] = make_uint4(0, 0, 0, 0);
                     fpv[u] = 1;
                     if (i < qn) {
@@ -882,7 +932,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
                 uint4 r0w[LS_BATCH], r1w[LS_BATCH];
 #pragma unroll
                 for (int u = 0; u < LS_BATCH; ++u) {
-                    const bool m = (i0 + u * LS_BLOCK < qn) && br[u].x == fpv[u];
+                    const bool m = (i0 + u * BLK < qn) && br[u].x == fpv[u];
                     const uint32_t row = br[u].w & 0x7fffffffu;
                     const uint32_t len = br[u].z & 0xffffffu;
                     r0w[u] = m ? a.pat16[row] : make_uint4(0, 0, 0, 0);
@@ -890,7 +940,7 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
                 }
 #pragma unroll
                 for (int u = 0; u < LS_BATCH; ++u) {
-                    const uint32_t i = i0 + u * LS_BLOCK;
+                    const uint32_t i = i0 + u * BLK;
                     if (i >= qn) continue;
                     const uint32_t ent = s_q[i];
                     const uint32_t q = ent >> 17;
@@ -918,19 +968,12 @@ __global__ __launch_bounds__(LS_BLOCK) void k_lit_scan(LitArgs a) {
                 }
             }
             __syncthreads();
+            // hit-dense inputs (regex prefilter fan-out): drain between queue batches, so the
+            // buffer rarely overflows into per-wave global atomics
+            flush(false);
         }
         __syncthreads();
-        const uint32_t hn = min(s_hn, LS_HB);
-        if (hn >= LS_HB / 2 || tile + gridDim.x >= a.n_tiles) {
-            if (t == 0) s_g = hn ? atomicAdd(a.hit_count, hn) : 0u;
-            __syncthreads();
-            for (uint32_t i = t; i < hn; i += LS_BLOCK) {
-                const uint32_t g = s_g + i;
-                if (g < a.cap) a.hits[g] = s_hits[i];
-            }
-            __syncthreads();
-            if (t == 0) s_hn = 0;
-        }
+        flush(tile + gridDim.x >= a.n_tiles);
     }
 }
 
@@ -1002,13 +1045,16 @@ __global__ __launch_bounds__(DFA_BLOCK) void k_dfa_match(DFAArgs a) {
             const uint32_t s = sp_.x, e = sp_.y;
             uint32_t st = 1;
             accept(st);
-            for (uint32_t w = s & ~3u; w < e && st != 0; w += 4) {
-                const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
+            // 16-B loads: lanes walk different records, so every load instruction touches
+            // up to 64 cache lines; a quarter of the 4-B loads' instructions
+            for (uint32_t w = s & ~15u; w < e && st != 0; w += 16) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
+                const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                for (uint32_t b = 0; b < 4; ++b) {
+                for (uint32_t b = 0; b < 16; ++b) {
                     const uint32_t p = w + b;
                     if (p < s || p >= e || st == 0) continue;
-                    st = step(st, s_cls[(x >> (8 * b)) & 0xffu]);
+                    st = step(st, s_cls[(xs[b >> 2] >> (8 * (b & 3))) & 0xffu]);
                     accept(st);
                 }
             }
@@ -1068,13 +1114,14 @@ __device__ __forceinline__ bool verify_one(const VerifyArgs &a, unsigned long lo
         const uint32_t s = sp_.x, e = sp_.y;
     uint32_t st = 1;
     bool hit = acc[st] != 0;
-    for (uint32_t w = s & ~3u; w < e && !hit && st != 0; w += 4) {
-        const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
+    for (uint32_t w = s & ~15u; w < e && !hit && st != 0; w += 16) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
+        const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (uint32_t b = 0; b < 4; ++b) {
+        for (uint32_t b = 0; b < 16; ++b) {
             const uint32_t p = w + b;
             if (p < s || p >= e || hit || st == 0) continue;
-            st = D[st * C + cls[(x >> (8 * b)) & 0xffu]];
+            st = D[st * C + cls[(xs[b >> 2] >> (8 * (b & 3))) & 0xffu]];
             hit = acc[st] != 0;
         }
     }
@@ -1160,7 +1207,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     // prefilter candidates (regex plans): factor filter -> (record, pattern) pairs
     unsigned long long *cand = nullptr;
     uint32_t n_cand = 0;
-    const int bpt = (int)(L.tile_bytes / LS_BLOCK);
+    static const int ls_block_env = getenv("SG_LS_BLOCK") ? atoi(getenv("SG_LS_BLOCK")) : 0;
     auto run_lit = [&](const char *name, const sg_matcher::Lit &Lt, unsigned long long *out, uint32_t *counter,
                        uint32_t ocap, const uint32_t *fo, const uint32_t *fp) -> int {
         LitArgs a{};
@@ -1187,21 +1234,30 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         const uint32_t dyn = lit_lds_bytes(Lt);
         const uint32_t bpc = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
         const uint32_t grid = std::min<uint32_t>(L.n_tiles, 256u * bpc);
+        // Block size: when the tables leave room for only <= 2 blocks per CU (large factor
+        // sets: the regex prefilter), 512-thread blocks double the waves that hide the
+        // candidate stage's L2 latency (C4 prefilter 2.71 -> 1.84 ms per 4M banners); with
+        // room for 3+ blocks, 256 threads x 64 positions probe faster (C3 1.35 vs 1.54 ms).
+        const int ls_block = ls_block_env ? ls_block_env : (bpc <= 2 ? 512 : 256);
+        const int bpt = (int)(L.tile_bytes / ls_block);
         const double bytes = (double)n + 8.0 * R;
-        auto launch = [&](auto kern) -> int {
+        auto launch = [&](auto kern, int blk) -> int {
             SG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-            SG_LAUNCH_B(c, name, bytes, kern, grid, LS_BLOCK, dyn, a);
+            SG_LAUNCH_B(c, name, bytes, kern, grid, blk, dyn, a);
             return SG_OK;
         };
-        if (bpt == 32) {
-            if (Lt.tmpl == 0x18u) SG_TRY(launch(k_lit_scan<32, 0x18u>));
-            else if (Lt.tmpl == 0x1Cu) SG_TRY(launch(k_lit_scan<32, 0x1Cu>));
-            else SG_TRY(launch(k_lit_scan<32, 0x1Fu>));
-        } else {
-            if (Lt.tmpl == 0x18u) SG_TRY(launch(k_lit_scan<64, 0x18u>));
-            else if (Lt.tmpl == 0x1Cu) SG_TRY(launch(k_lit_scan<64, 0x1Cu>));
-            else SG_TRY(launch(k_lit_scan<64, 0x1Fu>));
-        }
+        // (block, positions per thread) pairs of one parse tile; the template picks the
+        // length classes probed per position
+        auto by_tmpl = [&](auto k18, auto k1c, auto k1f, int blk) -> int {
+            if (Lt.tmpl == 0x18u) return launch(k18, blk);
+            if (Lt.tmpl == 0x1Cu) return launch(k1c, blk);
+            return launch(k1f, blk);
+        };
+        if (ls_block == 512 && bpt == 16) SG_TRY(by_tmpl(k_lit_scan<512, 16, 0x18u>, k_lit_scan<512, 16, 0x1Cu>, k_lit_scan<512, 16, 0x1Fu>, 512));
+        else if (ls_block == 512 && bpt == 32) SG_TRY(by_tmpl(k_lit_scan<512, 32, 0x18u>, k_lit_scan<512, 32, 0x1Cu>, k_lit_scan<512, 32, 0x1Fu>, 512));
+        else if (ls_block == 256 && bpt == 32) SG_TRY(by_tmpl(k_lit_scan<256, 32, 0x18u>, k_lit_scan<256, 32, 0x1Cu>, k_lit_scan<256, 32, 0x1Fu>, 256));
+        else if (ls_block == 256 && bpt == 64) SG_TRY(by_tmpl(k_lit_scan<256, 64, 0x18u>, k_lit_scan<256, 64, 0x1Cu>, k_lit_scan<256, 64, 0x1Fu>, 256));
+        else { set_error("k_lit_scan: unsupported tile geometry"); return SG_E_INVAL; }
         if (dbg) {
             unsigned long long d[3];
             SG_TRY(ctx_readback(c, d, dbg, 24));

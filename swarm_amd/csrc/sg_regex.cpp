@@ -743,6 +743,55 @@ static int build_split(std::vector<Pat *> ps, uint32_t budget, std::vector<Regex
     return build_split(b, budget, out);
 }
 
+// Small unfiltered sets are packed first-fit (largest single DFA first) into groups whose
+// whole transition table fits the matcher's LDS hot-row budget (states x classes x 2 B
+// <= 64 KiB) and the state budget: every group costs one pass over the text, and a table
+// that spills rows to L2 costs a dependent L2 load on the cold steps. (The C4 set's 20
+// factor-less signatures: 5 halving-split groups, 2 of them over the LDS budget -> packed.)
+constexpr uint64_t PACK_TABLE_BYTES = 64 * 1024;
+static uint64_t table_bytes(const RegexDFA &d) { return (uint64_t)d.n_states * d.n_classes * 2; }
+
+static int build_pack(std::vector<Pat *> ps, uint32_t budget, std::vector<RegexDFA> *out) {
+    if (ps.size() > 128) return build_split(ps, budget, out);
+    std::vector<std::pair<uint64_t, Pat *>> order;
+    for (Pat *p : ps) {
+        RegexDFA d;
+        bool fits = false;
+        int rc = build_group({p}, budget, &d, &fits);
+        if (rc != SG_OK) return rc;
+        order.push_back({fits ? table_bytes(d) : ~0ull, p});
+    }
+    std::stable_sort(order.begin(), order.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+    std::vector<std::vector<Pat *>> groups;
+    std::vector<RegexDFA> dfas;
+    for (auto &op : order) {
+        bool placed = false;
+        for (size_t g = 0; g < groups.size() && !placed && op.first <= PACK_TABLE_BYTES; ++g) {
+            if (groups[g].size() >= 64 || table_bytes(dfas[g]) > PACK_TABLE_BYTES) continue;
+            std::vector<Pat *> trial = groups[g];
+            trial.push_back(op.second);
+            RegexDFA d;
+            bool fits = false;
+            int rc = build_group(trial, budget, &d, &fits);
+            if (rc != SG_OK) return rc;
+            if (fits && table_bytes(d) <= PACK_TABLE_BYTES) {
+                groups[g] = std::move(trial);
+                dfas[g] = std::move(d);
+                placed = true;
+            }
+        }
+        if (!placed) {
+            std::vector<RegexDFA> one;
+            int rc = build_split({op.second}, budget, &one);
+            if (rc != SG_OK) return rc;
+            groups.push_back({op.second});
+            dfas.push_back(std::move(one[0]));
+        }
+    }
+    for (auto &d : dfas) out->push_back(std::move(d));
+    return SG_OK;
+}
+
 // ------------------------------------------------------------------ literal factors
 // For a node: `exact` = every string the node can match (lower-cased, when small), and
 // `fac` = a set such that every match of the node contains one of its strings.
@@ -957,7 +1006,7 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         fprintf(stderr, "\n");
     }
     if (!unfiltered.empty()) {
-        int rc = build_split(unfiltered, 4096, &plan->groups);
+        int rc = build_pack(unfiltered, 4096, &plan->groups);
         if (rc == SG_OK && getenv("SG_REGEX_DEBUG"))
             for (auto &g : plan->groups) fprintf(stderr, "[regex plan] group states=%u classes=%u\n", g.n_states, g.n_classes);
         return rc;
