@@ -190,7 +190,7 @@ def bench_c4(args):
 
     torch.cuda.set_device(0)
     sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
-    pats = [base64.b64decode(r["p"]) for r in sig["regexes"] if r["dfa_rc"] == 0] + corpus.nmap_signatures()
+    pats = [base64.b64decode(r["p"]) for r in sig["regexes"]] + corpus.nmap_signatures()
     n_lines = args.lines if args.lines != 10_000_000 else 12_500_000
     pool = corpus.banner_pool()
     buf = corpus.lines_from_pool(pool, n_lines, seed=3)

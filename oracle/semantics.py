@@ -245,7 +245,7 @@ def _json_members(rec: bytes):
                 close_pos = i
             depth -= 1
         elif ch == 0x3A and depth == 1:
-            cur = rec[str_s:str_e]
+            cur = _json_key(rec[str_s:str_e])
             val_s = i + 1
         elif ch == 0x2C and depth == 1:
             if cur is not None:
@@ -256,16 +256,23 @@ def _json_members(rec: bytes):
     return members
 
 
-def _json_put_cp(out: bytearray, cp: int) -> None:
+def _json_put_cp(out: bytearray, cp: int, nl: bytes) -> None:
     if cp == 0x0A:
-        out += b"\\n"  # a row stays one line
+        out += nl
     else:
         out += chr(cp).encode("utf-8", "surrogatepass")
 
 
-def json_decode_string(s: bytes) -> bytes:
+def _json_key(raw: bytes) -> bytes:
+    """A member key as json.loads sees it (escapes decoded, a newline stays one byte), in
+    UTF-8; requested keys are compared with this."""
+    return json_decode_string(raw, nl=b"\n") if b"\\" in raw else raw
+
+
+def json_decode_string(s: bytes, nl: bytes = b"\\n") -> bytes:
     """JSON string body (between the quotes) -> bytes, as json.loads + UTF-8 encoding
-    ('surrogatepass' for lone surrogates), newline written as backslash-n."""
+    ('surrogatepass' for lone surrogates); a newline is written as `nl` (backslash-n in
+    rows, so a row stays one line)."""
     out = bytearray()
     p, n = 0, len(s)
     hexd = b"0123456789abcdefABCDEF"
@@ -275,7 +282,7 @@ def json_decode_string(s: bytes) -> bytes:
             return None
         return int(s[q:q + 4], 16)
 
-    simple = {0x22: b'"', 0x5C: b"\\", 0x2F: b"/", 0x62: b"\x08", 0x66: b"\x0c", 0x6E: b"\\n", 0x72: b"\r",
+    simple = {0x22: b'"', 0x5C: b"\\", 0x2F: b"/", 0x62: b"\x08", 0x66: b"\x0c", 0x6E: nl, 0x72: b"\r",
               0x74: b"\t"}
     while p < n:
         ch = s[p]
@@ -299,7 +306,7 @@ def json_decode_string(s: bytes) -> bytes:
                 if lo is not None and 0xDC00 <= lo < 0xE000:
                     v = 0x10000 + ((v - 0xD800) << 10) + (lo - 0xDC00)
                     p += 6
-            _json_put_cp(out, v)
+            _json_put_cp(out, v, nl)
         else:
             out.append(ch)
             p += 1

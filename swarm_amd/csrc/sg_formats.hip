@@ -162,7 +162,6 @@ static int dev_nmap_ports(sg_ctx *c, const uint8_t *d_buf, uint64_t n, sg_dev_te
 }
 
 // ------------------------------------------------------------------ httpx -json
-constexpr int JS_BLOCK = 256;
 constexpr uint32_t JS_MAXKEYS = 64;
 constexpr uint32_t JS_KEYBYTES = 4096;
 constexpr uint32_t JS_NONE = 0xffffffffu;
@@ -190,11 +189,12 @@ __device__ __forceinline__ int js_hex(uint8_t b) {
 // json.loads: \" \\ \/ \b \f \n \r \t and \uXXXX (a high+low surrogate pair combines into
 // one code point; a lone surrogate is encoded as its 3-byte form, like Python's
 // 'surrogatepass'). A decoded U+000A is written as the two bytes '\' 'n' so a row stays
-// one line. Malformed escapes are copied verbatim.
-template <class Put>
+// one line (KEY: as the byte 0x0a, the form a requested key is compared in). Malformed
+// escapes are copied verbatim.
+template <bool KEY = false, class Put>
 __device__ __forceinline__ void js_decode(const uint8_t *buf, uint32_t a, uint32_t b, Put &put) {
     auto put_cp = [&](uint32_t cp) {
-        if (cp == 0x0a) { put('\\'); put('n'); }
+        if (cp == 0x0a && !KEY) { put('\\'); put('n'); }
         else if (cp < 0x80) put((uint8_t)cp);
         else if (cp < 0x800) { put((uint8_t)(0xc0 | (cp >> 6))); put((uint8_t)(0x80 | (cp & 0x3f))); }
         else if (cp < 0x10000) {
@@ -225,7 +225,7 @@ __device__ __forceinline__ void js_decode(const uint8_t *buf, uint32_t a, uint32
             case '"': case '\\': case '/': put(e); p += 2; break;
             case 'b': put(0x08); p += 2; break;
             case 'f': put(0x0c); p += 2; break;
-            case 'n': put('\\'); put('n'); p += 2; break;
+            case 'n': if (KEY) put(0x0a); else { put('\\'); put('n'); } p += 2; break;
             case 'r': put(0x0d); p += 2; break;
             case 't': put(0x09); p += 2; break;
             case 'u':
@@ -290,6 +290,18 @@ __device__ __forceinline__ void js_value(const uint8_t *buf, uint32_t vs, uint32
     }
 }
 
+// Compares a decoded key stream with one requested key.
+struct JsKeyEq {
+    const uint8_t *k;
+    uint32_t n, i = 0;
+    bool ok = true;
+    __device__ void operator()(uint8_t ch) {
+        ok = ok && i < n && k[i] == ch;
+        ++i;
+    }
+    __device__ bool eq() const { return ok && i == n; }
+};
+
 struct JsCount {
     uint32_t rows = 0, bytes = 0, cur = 0;
     __device__ void begin() { cur = 0; }
@@ -297,118 +309,8 @@ struct JsCount {
     __device__ void end() { if (cur) { ++rows; bytes += cur + 1; } }
 };
 
-// One wave per record.
-__global__ __launch_bounds__(JS_BLOCK) void k_json_scan(JsonArgs a) {
-    __shared__ uint8_t s_keys[JS_KEYBYTES];
-    __shared__ uint32_t s_koff[JS_MAXKEYS + 1];
-    for (uint32_t q = threadIdx.x; q <= a.nkeys; q += JS_BLOCK) s_koff[q] = a.key_offs[q];
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < s_koff[a.nkeys]; q += JS_BLOCK) s_keys[q] = a.keys[q];
-    __syncthreads();
-    const int lane = lane_id();
-    const uint32_t nw = gridDim.x * (JS_BLOCK / 64);
-    const uint32_t my_klen = (lane < (int)a.nkeys) ? s_koff[lane + 1] - s_koff[lane] : 0xffffffffu;
-    for (uint32_t r = blockIdx.x * (JS_BLOCK / 64) + (threadIdx.x >> 6); r < a.R; r += nw) {
-        const uint2 sp = a.spans[r];
-        uint32_t my_vs = JS_NONE, my_ve = 0;
-        // wave-uniform walk state
-        uint32_t depth = 0, str_s = 0, str_e = 0, val_s = 0, open_pos = JS_NONE, close_pos = JS_NONE;
-        uint32_t first_nws = JS_NONE, last_nws = 0;
-        int cur_key = -1;
-        bool in_str = false, bad = false, done = false;
-        uint32_t bs_run = 0;  // trailing backslash run length of the previous chunk
-        for (uint32_t base = sp.x; base < sp.y && !bad; base += 64) {
-            const uint32_t pos = base + lane;
-            const bool valid = pos < sp.y;
-            const uint8_t b = valid ? a.buf[pos] : 0;
-            const uint64_t Q = __ballot(valid && b == '"');
-            const uint64_t BS = __ballot(valid && b == '\\');
-            const uint64_t ST = __ballot(valid && (b == '{' || b == '[' || b == '}' || b == ']' || b == ':' || b == ','));
-            const uint64_t NWS = __ballot(valid && !js_ws(b));
-            if (NWS) {
-                if (first_nws == JS_NONE) first_nws = base + (uint32_t)(__ffsll((long long)NWS) - 1);
-                last_nws = base + 63u - (uint32_t)__clzll(NWS);
-            }
-            uint64_t E = Q | ST;
-            while (E) {
-                const uint32_t p = (uint32_t)(__ffsll((long long)E) - 1);
-                E &= E - 1;
-                const uint64_t bit = 1ull << p;
-                if (Q & bit) {
-                    if (!in_str) {
-                        if (depth == 0) { bad = true; break; }
-                        in_str = true;
-                        str_s = base + p + 1;
-                    } else {
-                        // escaped iff preceded by an odd run of backslashes
-                        const uint64_t below = bit - 1;
-                        const uint64_t zeros = ~BS & below;
-                        const uint32_t run = zeros ? p - 1 - (63u - (uint32_t)__clzll(zeros)) : p + bs_run;
-                        if (run & 1u) continue;
-                        in_str = false;
-                        str_e = base + p;
-                    }
-                    continue;
-                }
-                if (in_str) continue;
-                const uint8_t ch = (uint8_t)__shfl((int)b, (int)p, 64);
-                const uint32_t at = base + p;
-                if (done) { bad = true; break; }
-                if (ch == '{' || ch == '[') {
-                    if (depth == 0) {
-                        if (ch != '{') { bad = true; break; }
-                        open_pos = at;
-                    }
-                    ++depth;
-                } else if (ch == '}' || ch == ']') {
-                    if (depth == 0) { bad = true; break; }
-                    if (depth == 1) {
-                        if (ch != '}') { bad = true; break; }
-                        if (cur_key >= 0 && lane == cur_key) { my_vs = val_s; my_ve = at; }
-                        cur_key = -1;
-                        done = true;
-                        close_pos = at;
-                    }
-                    --depth;
-                } else if (ch == ':') {
-                    if (depth == 1) {
-                        // the key is the last string; lane k tests requested key k
-                        const uint32_t kl = str_e - str_s;
-                        bool eq = my_klen == kl;
-                        for (uint32_t q = 0; q < kl && eq; ++q) eq = a.buf[str_s + q] == s_keys[s_koff[lane] + q];
-                        const uint64_t m = __ballot(eq);
-                        cur_key = m ? __ffsll((long long)m) - 1 : -1;
-                        val_s = at + 1;
-                    }
-                } else {  // ','
-                    if (depth == 1) {
-                        if (cur_key >= 0 && lane == cur_key) { my_vs = val_s; my_ve = at; }
-                        cur_key = -1;
-                    }
-                }
-            }
-            // trailing backslash run carried into the next chunk
-            if (BS == ~0ull) bs_run += 64;
-            else bs_run = (uint32_t)__clzll(~BS);
-        }
-        bad = bad || in_str || depth != 0 || !done || first_nws != open_pos || last_nws != close_pos;
-        if (lane < (int)a.nkeys) {
-            uint4 d = make_uint4(0, 0, 0, 0);
-            if (!bad && my_vs != JS_NONE) {
-                uint32_t vs = my_vs, ve = my_ve;
-                while (vs < ve && js_ws(a.buf[vs])) ++vs;
-                while (ve > vs && js_ws(a.buf[ve - 1])) --ve;
-                JsCount cnt;
-                js_value(a.buf, vs, ve, cnt);
-                d = make_uint4(vs, ve, cnt.rows, cnt.bytes);
-            }
-            a.desc[(size_t)r * a.nkeys + lane] = d;
-        }
-    }
-}
-
 // One thread per record: the record is read with aligned 16-byte loads and walked byte by
-// byte with the same state machine as the wave walker (string/escape state, depth, key at a
+// byte with a JSON state machine (string/escape state, depth, key at a
 // depth-1 colon, value end at a depth-1 comma or the closing brace, whitespace-only
 // framing). Per-thread key spans live in LDS. Requested keys are pre-filtered by length
 // and first byte before a byte compare.
@@ -435,7 +337,7 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
         uint32_t depth = 0, str_s = 0, str_e = 0, val_s = 0, open_pos = JS_NONE, close_pos = JS_NONE;
         uint32_t first_nws = JS_NONE, last_nws = 0, c0 = 0;
         int cur_key = -1;
-        bool in_str = false, esc = false, bad = false, done = false;
+        bool in_str = false, esc = false, kesc = false, bad = false, done = false;
         for (uint32_t w = sp.x & ~15u; w < sp.y && !bad; w += 16) {
             const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
             const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
@@ -451,13 +353,14 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
                 if (in_str) {
                     if (q == str_s) c0 = b;
                     if (esc) esc = false;
-                    else if (b == '\\') esc = true;
+                    else if (b == '\\') esc = kesc = true;
                     else if (b == '"') { in_str = false; str_e = q; }
                     continue;
                 }
                 if (b == '"') {
                     if (depth == 0) bad = true;
                     in_str = true;
+                    kesc = false;
                     str_s = q + 1;
                     c0 = 0x100u;
                 } else if (b == '{' || b == '[' || b == '}' || b == ']' || b == ':' || b == ',') {
@@ -484,9 +387,16 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
                             const uint32_t id = kl | ((kl ? c0 : 0x100u) << 16);
                             cur_key = -1;
                             for (uint32_t k = 0; k < nk; ++k) {
-                                if (s_kid[k] != id) continue;
-                                bool eq = true;
-                                for (uint32_t x = 1; x < kl && eq; ++x) eq = a.buf[str_s + x] == s_keys[s_koff[k] + x];
+                                bool eq;
+                                if (kesc) {  // escaped key: compare its decoded form
+                                    JsKeyEq cmp{s_keys + s_koff[k], s_koff[k + 1] - s_koff[k]};
+                                    js_decode<true>(a.buf, str_s, str_e, cmp);
+                                    eq = cmp.eq();
+                                } else {
+                                    if (s_kid[k] != id) continue;
+                                    eq = true;
+                                    for (uint32_t x = 1; x < kl && eq; ++x) eq = a.buf[str_s + x] == s_keys[s_koff[k] + x];
+                                }
                                 if (eq) { cur_key = (int)k; break; }
                             }
                             val_s = q + 1;
@@ -559,14 +469,8 @@ int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *
     *res = sg_dev_rows{};
     if (nkeys == 0 || nkeys > JS_MAXKEYS) { set_error("json fields: 1..%u keys", JS_MAXKEYS); return SG_E_INVAL; }
     if (key_offs[0] != 0 || key_offs[nkeys] > JS_KEYBYTES) { set_error("json fields: keys exceed %u bytes", JS_KEYBYTES); return SG_E_INVAL; }
-    for (uint32_t k = 0; k < nkeys; ++k) {
+    for (uint32_t k = 0; k < nkeys; ++k)
         if (key_offs[k + 1] < key_offs[k]) { set_error("json fields: bad key offsets"); return SG_E_INVAL; }
-        for (uint32_t q = key_offs[k]; q < key_offs[k + 1]; ++q)
-            if (keys[q] == '"' || keys[q] == '\\' || keys[q] < 0x20) {
-                set_error("json fields: key %u needs JSON escaping (unsupported)", k);
-                return SG_E_INVAL;
-            }
-    }
     Lines L;
     SG_TRY(run_lines(c, d_buf, n, FMT_SLOTS, &L, false));
     const uint32_t R = L.n_rec;
@@ -585,15 +489,9 @@ int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *
     SG_TRY(slot(c, S_F_DESC, items + 1, &desc));
     SG_TRY(slot(c, S_F_OFFS, items + 1, &offs));
     JsonArgs ja{d_buf, L.spans, R, d_keys, d_koff, nkeys, desc};
-    static const bool wave_walk = getenv("SG_JSON_WAVE") != nullptr;
-    if (wave_walk) {
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((R + 3) / 4, 256u * 16u);
-        SG_LAUNCH_B(c, "json_scan", (double)n + 16.0 * items, k_json_scan, grid, JS_BLOCK, 0, ja);
-    } else {
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((R + JT_BLOCK - 1) / JT_BLOCK, 256u * 16u);
-        SG_LAUNCH_B(c, "json_scan", (double)n + 16.0 * items, k_json_scan_t, grid, JT_BLOCK,
-                    JT_BLOCK * nkeys * sizeof(uint2), ja);
-    }
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((R + JT_BLOCK - 1) / JT_BLOCK, 256u * 16u);
+    SG_LAUNCH_B(c, "json_scan", (double)n + 16.0 * items, k_json_scan_t, grid, JT_BLOCK,
+                JT_BLOCK * nkeys * sizeof(uint2), ja);
     uint64_t total = 0;
     SG_TRY(run_scan64(c, "json_scan_len", JsonLen{desc}, (uint32_t)items, offs, &total));
     const uint64_t rows = total & 0xffffffffu, bytes = total >> 32;

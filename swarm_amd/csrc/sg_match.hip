@@ -50,12 +50,13 @@ struct sg_matcher {
     std::vector<uint32_t> fac_off, fac_pids;
     std::vector<uint16_t> s_delta;  // single-pattern DFAs have <= 65535 states
     std::vector<uint32_t> s_off, s_C, s_eol, s_acc_off, single_of_pid;
+    std::vector<uint32_t> s_mid;  // anchored: mid-record start states (non-word | word << 16), else ~0
     std::vector<uint8_t> s_cls, s_acc;
     uint32_t n_singles = 0;
     struct DevPlan {
         uint16_t *s_delta = nullptr;
         uint32_t *fac_off = nullptr, *fac_pids = nullptr, *s_off = nullptr, *s_C = nullptr,
-                 *s_eol = nullptr, *s_acc_off = nullptr, *single_of_pid = nullptr;
+                 *s_eol = nullptr, *s_acc_off = nullptr, *single_of_pid = nullptr, *s_mid = nullptr;
         uint8_t *s_cls = nullptr, *s_acc = nullptr;
     } dplan;
     // device copies (one device)
@@ -405,7 +406,8 @@ static void free_dev(sg_matcher *h) {
     h->dtabs.clear();
     auto &p = h->dplan;
     for (void *q : {(void *)p.fac_off, (void *)p.fac_pids, (void *)p.s_delta, (void *)p.s_off, (void *)p.s_C,
-                    (void *)p.s_eol, (void *)p.s_acc_off, (void *)p.single_of_pid, (void *)p.s_cls, (void *)p.s_acc})
+                    (void *)p.s_eol, (void *)p.s_acc_off, (void *)p.single_of_pid, (void *)p.s_cls, (void *)p.s_acc,
+                    (void *)p.s_mid})
         if (q) (void)hipFree(q);
     h->dplan = sg_matcher::DevPlan{};
     for (sg_matcher::Lit *L : {&h->lit, &h->prelit}) {
@@ -434,6 +436,7 @@ static int ensure_device(sg_matcher *h, int dev) {
         SG_TRY(upload_vec(h->s_eol, &p.s_eol));
         SG_TRY(upload_vec(h->s_acc_off, &p.s_acc_off));
         SG_TRY(upload_vec(h->single_of_pid, &p.single_of_pid));
+        SG_TRY(upload_vec(h->s_mid, &p.s_mid));
         SG_TRY(upload_vec(h->s_cls, &p.s_cls));
         SG_TRY(upload_vec(h->s_acc, &p.s_acc));
     }
@@ -1096,7 +1099,7 @@ struct VerifyArgs {
     const unsigned long long *cand;
     uint32_t n_cand;
     const uint16_t *s_delta;
-    const uint32_t *s_off, *s_C, *s_eol, *s_acc_off, *single_of_pid;
+    const uint32_t *s_off, *s_C, *s_eol, *s_acc_off, *single_of_pid, *s_mid;
     const uint8_t *s_cls, *s_acc;
     unsigned long long *hits;
     uint32_t *hit_count;
@@ -1111,7 +1114,27 @@ __device__ __forceinline__ bool verify_one(const VerifyArgs &a, unsigned long lo
     const uint8_t *acc = a.s_acc + a.s_acc_off[k];
     const uint32_t C = a.s_C[k];
     const uint2 sp_ = a.spans[r];
-        const uint32_t s = sp_.x, e = sp_.y;
+    const uint32_t s = sp_.x, e = sp_.y;
+    const uint32_t mid = a.s_mid[k];
+    if (mid != 0xffffffffu) {
+        // anchored DFA: a run from every start offset (most die on their first byte)
+        bool hit = false;
+        for (uint32_t p0 = s; p0 <= e && !hit; ++p0) {
+            uint32_t st = 1;
+            if (p0 > s) {
+                const uint8_t pb = a.buf[p0 - 1];
+                const bool pw = (pb >= '0' && pb <= '9') || ((pb | 0x20) >= 'a' && (pb | 0x20) <= 'z') || pb == '_';
+                st = pw ? (mid >> 16) : (mid & 0xffffu);
+            }
+            hit = acc[st] != 0;
+            for (uint32_t p = p0; p < e && !hit && st != 0; ++p) {
+                st = D[st * C + cls[a.buf[p]]];
+                hit = acc[st] != 0;
+            }
+            if (!hit && st != 0) hit = acc[D[st * C + a.s_eol[k]]] != 0;
+        }
+        return hit;
+    }
     uint32_t st = 1;
     bool hit = acc[st] != 0;
     for (uint32_t w = s & ~15u; w < e && !hit && st != 0; w += 16) {
@@ -1321,7 +1344,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
             if (n_cand) {
                 const auto &p = h->dplan;
                 VerifyArgs v{d_buf, L.spans, vcand, n_cand, p.s_delta, p.s_off, p.s_C, p.s_eol,
-                             p.s_acc_off, p.single_of_pid, p.s_cls, p.s_acc, hits, cnt, (uint32_t)cap};
+                             p.s_acc_off, p.single_of_pid, p.s_mid, p.s_cls, p.s_acc, hits, cnt, (uint32_t)cap};
                 SG_LAUNCH_B(c, "re_verify", n_cand * (16.0 + (double)n / R), k_verify, (n_cand + 255) / 256, 256, 0, v);
             }
         }
@@ -1428,6 +1451,7 @@ int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pat
             m->s_off.push_back((uint32_t)m->s_delta.size());
             m->s_C.push_back(d.n_classes);
             m->s_eol.push_back(d.eol_class);
+            m->s_mid.push_back(d.anchored ? (d.mid_start[0] | (d.mid_start[1] << 16)) : 0xffffffffu);
             if (d.n_states > 65536) { delete m; set_error("regex signature DFA exceeds 65536 states"); return SG_E_STATES; }
             for (uint32_t x : d.delta) m->s_delta.push_back((uint16_t)x);
             m->s_cls.insert(m->s_cls.end(), d.cls, d.cls + 256);

@@ -510,8 +510,8 @@ struct VecHash {
 // entering the successor.
 class SubsetBuilder {
   public:
-    SubsetBuilder(const NFA &A, const std::vector<int> &starts, uint32_t budget)
-        : A_(A), starts_(starts), budget_(budget), mark_(A.st.size(), 0) {}
+    SubsetBuilder(const NFA &A, const std::vector<int> &starts, uint32_t budget, bool anchored = false)
+        : A_(A), starts_(starts), budget_(budget), anchored_(anchored), mark_(A.st.size(), 0) {}
 
     bool run(RegexDFA *out) {
         std::vector<ByteSet> sets = A_.sets;
@@ -564,6 +564,14 @@ class SubsetBuilder {
             return q;
         };
         if (intern(std::move(init), false) != 1) return false;  // state 1 = start
+        out->anchored = anchored_;
+        if (anchored_) {  // start states for a search starting after a non-word / word byte
+            for (int w = 0; w < 2; ++w) {
+                const int64_t t = intern(std::vector<int>(start_nb_), w != 0);
+                if (t < 0) return false;
+                out->mid_start[w] = (uint32_t)t;
+            }
+        }
         std::vector<uint32_t> delta;
         std::map<std::vector<uint32_t>, uint32_t> eol_term;
         for (size_t q = 1; q < states.size(); ++q) {
@@ -582,7 +590,7 @@ class SubsetBuilder {
                         if (A_.st[s].type == NState::MATCH && !std::binary_search(cur.begin(), cur.end(), s)) newly.push_back(s);
                 }
                 std::vector<int> nx = closure(move(res, b), false, false, false, false, false);
-                nx = merge(nx, start_nb_);
+                if (!anchored_) nx = merge(nx, start_nb_);
                 if (!newly.empty()) nx = merge(nx, newly);
                 int64_t t = intern(std::move(nx), nw);
                 if (t < 0) return false;
@@ -627,6 +635,7 @@ class SubsetBuilder {
     const NFA &A_;
     std::vector<int> starts_, start_nb_;
     uint32_t budget_;
+    bool anchored_;
     std::vector<int> rep_;
     std::vector<uint32_t> mark_;
     uint32_t gen_ = 0;
@@ -701,7 +710,8 @@ static int parse_one(const uint8_t *p, uint32_t len, bool nocase, NodeP *out) {
     }
 }
 
-static int build_group(const std::vector<Pat *> &ps, uint32_t budget, RegexDFA *out, bool *fits) {
+static int build_group(const std::vector<Pat *> &ps, uint32_t budget, RegexDFA *out, bool *fits,
+                       bool anchored = false) {
     try {
         NFA A;
         std::vector<int> starts;
@@ -712,7 +722,7 @@ static int build_group(const std::vector<Pat *> &ps, uint32_t budget, RegexDFA *
             A.st[f.end].out = m;
             starts.push_back(f.start);
         }
-        SubsetBuilder sb(A, starts, budget);
+        SubsetBuilder sb(A, starts, budget, anchored);
         *fits = sb.run(out);
         return SG_OK;
     } catch (const ParseError &e) {
@@ -936,6 +946,8 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         }
     }
     plan->single_of_pid.assign(n, 0xffffffffu);
+    // test knob: verify every prefiltered pattern with its anchored DFA
+    const bool force_anchored = getenv("SG_REGEX_ANCHORED") != nullptr;
     std::map<std::string, std::vector<uint32_t>> fac_map;
     std::vector<Pat *> unfiltered;
     // candidate factor sets per pattern; how many patterns could use each string
@@ -977,8 +989,13 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
             RegexDFA d;
             bool fits = false;
             std::vector<Pat *> one{&p};
-            int rc = build_group(one, 65535, &d, &fits);
+            int rc = force_anchored ? SG_OK : build_group(one, 65535, &d, &fits);
             if (rc != SG_OK) return rc;
+            if (!fits) {  // verification runs per candidate: an anchored DFA will do
+                d = RegexDFA();
+                rc = build_group(one, 65535, &d, &fits, true);
+                if (rc != SG_OK) return rc;
+            }
             if (!fits) {
                 filtered = false;
             } else {

@@ -5,7 +5,8 @@
 //   \d \w \s \D \W \S inside, escapes \t \n \r \f \v \xHH \0, anchors ^ $ \A \Z,
 //   groups ( ) (?: ) (?P<name> ), alternation |, quantifiers * + ? {n} {n,} {,m} {n,m}
 //   and their lazy forms (same existence semantics), global (?i) and scoped (?i:...).
-// Rejected with SG_E_UNSUPPORTED: backreferences, lookaround, \b \B, other inline flags.
+//   word boundaries \b \B (ASCII word bytes [0-9A-Za-z_]).
+// Rejected with SG_E_UNSUPPORTED: backreferences, lookaround, other inline flags.
 // Search semantics: a pattern matches a record if some substring matches; '^'/'\A' hold
 // at offset 0 only, '$'/'\Z' at the record end only (records hold no '\n').
 #pragma once
@@ -21,6 +22,12 @@ struct RegexDFA {
     std::vector<uint32_t> delta;    // n_states * n_classes
     std::vector<uint32_t> acc_off;  // n_states + 1
     std::vector<uint32_t> acc_ids;  // pattern ids accepted on entering a state
+    // Anchored DFA (no restart at every byte): a match is searched by running it from
+    // every start offset. State 1 starts at the record start; a start at offset p > 0 uses
+    // mid_start[word(byte p-1)]. Built for a prefiltered pattern whose search DFA exceeds
+    // the state budget (a counted repeat overlapping its own restarts, e.g. <[^>]{1,512}).
+    bool anchored = false;
+    uint32_t mid_start[2] = {0, 0};
 };
 
 // Builds DFAs for all patterns, splitting the set so that no DFA exceeds the state budget.

@@ -146,3 +146,33 @@ def test_json_malformed_lines_yield_nothing(line):
 def test_json_whitespace_around_object_is_valid():
     rows, rrec, rkey = S.json_field_rows(b'  {"a" : "v" }\t\n', [b"a"])
     assert rows == b"v\n" and rrec == [0] and rkey == [0]
+
+
+ESC_KEYS = ["title", 'ti"tle', "a\\b", "k\n", "tab\t", "é", "\U0001F600", "/x", "\x01"]
+
+
+def escaped_key_lines(n, seed):
+    """Objects whose top-level keys need (or are written with) JSON escapes."""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        obj = {rng.choice(ESC_KEYS): _rand_val(rng) for _ in range(rng.randint(1, 5))}
+        s = json.dumps(obj, ensure_ascii=rng.random() < 0.5, separators=rng.choice([(",", ":"), (" , ", " : ")]))
+        if rng.random() < 0.3:  # spell a plain key with escapes, as another writer might
+            s = s.replace('"title"', rng.choice(['"\\u0074itle"', '"t\\u0069tl\\u0065"', '"titl\\u0065"']))
+        if rng.random() < 0.2:
+            s = s.replace('"/x"', '"\\/x"')
+        out.append(s.encode("utf-8", "surrogatepass"))
+    out += [b'{"\\u0074itle":"a","title":"b"}', b'{"title":"a","\\u0074itle":"b"}', b'{"ti\\"tle":"q"}',
+            b'{"\\ud83d\\ude00":"smile"}', b'{"k\\n":"nl","k\\\\n":"bs"}']
+    return out
+
+
+def test_json_escaped_keys_match_json_module():
+    keys = [k.encode("utf-8") for k in ESC_KEYS] + [b"k\\n", b"tit"]
+    for line in escaped_key_lines(1500, seed=5):
+        try:
+            line.decode("utf-8")
+        except UnicodeDecodeError:
+            continue
+        check_line_against_json(line, keys)

@@ -150,3 +150,11 @@ def test_json_long_lines_and_many_rows(sg):
 def test_nmap_many_hosts_crlf(sg):
     txt = corpus.nmap_report(100_000, seed=9).replace(b"\n", b"\r\n")
     assert sg.nmap_ports(txt) == S.nmap_host_ports(txt)
+
+
+def test_json_escaped_keys(sg):
+    """Keys written with JSON escapes (and requested keys that need them) match by their
+    decoded form, as json.loads would."""
+    from test_formats_oracle import ESC_KEYS, escaped_key_lines
+    keys = [k.encode("utf-8") for k in ESC_KEYS] + [b"k\\n", b"tit"]
+    check(sg, b"\n".join(escaped_key_lines(3000, seed=6)) + b"\n", keys)

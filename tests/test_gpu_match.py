@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 GR = load_golden("grep_vectors.json")
 SIG = load_golden("signatures.json")
 WORDS = [base64.b64decode(w) for w in SIG["words"]]
-REGEXES = [base64.b64decode(r["p"]) for r in SIG["regexes"] if r["dfa_rc"] == 0]
+REGEXES = [base64.b64decode(r["p"]) for r in SIG["regexes"]]
 
 
 @pytest.fixture(scope="module", params=["auto", "litfilter"])
@@ -217,3 +217,53 @@ def test_repeated_calls_keep_workspace_bounded():
         r2 = rx.dev_match(ctx, d.data_ptr(), d.numel())
     assert r1.n_hits == 4000 and r2.n_hits == 4000
     ctx.close()
+
+
+OVERSIZE = rb"<[^>]{1,512}\bwire:"  # the corpus regex whose search DFA exceeds 65,535 states
+
+
+def test_regex_oversize_corpus_pattern(sg):
+    """Verified by its anchored DFA from every start offset: '<' at distances around the
+    {1,512} bounds, '>' in between, several '<', word/non-word bytes before 'wire:'."""
+    rng = random.Random(4)
+    lines = []
+    for d in list(range(0, 8)) + list(range(505, 520)) + [rng.randrange(1, 700) for _ in range(200)]:
+        for pre in (b" ", b"x", b"<", b"_", b"-", b">"):
+            body = bytes(rng.choice(b"abc <_/=\"") for _ in range(max(d - 1, 0)))
+            lines.append(b"<" + body[: max(d - 1, 0)] + (pre if d > 0 else b"") + b"wire:x")
+            lines.append(b"<" * rng.randint(1, 3) + body + b">" + pre + b"wire:")
+    lines += [b"wire:", b"<wire:", b"< wire:", b"<a wire:", b"<awire:", b"<a>b wire:", b"<" + b"a" * 511 + b" wire:",
+              b"<" + b"a" * 512 + b" wire:", b"<" + b"a" * 600 + b"<" + b"b wire:"]
+    data = b"\n".join(lines) + b"\n"
+    pats = [OVERSIZE, rb"wire:", rb"<[a-z]+>"]
+    m = sg.Matcher(pats, "regex")
+    assert m.match(data) == S.regex_hits(data, pats)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_regex_fuzz_anchored_verify(sg, seed):
+    """Every prefiltered pattern verified by its anchored DFA (SG_REGEX_ANCHORED, read at
+    compile time): random patterns around a literal factor, with ^ $ \\b \\B and classes."""
+    import os
+    rng = random.Random(2000 + seed)
+    pats = []
+    while len(pats) < 25:
+        p = rand_regex(rng, 1) + rng.choice([b"abc", b"cab", b"xax"]) + rand_regex(rng, 1)
+        if rng.random() < 0.2:
+            p = b"^" + p
+        if rng.random() < 0.2:
+            p = p + b"$"
+        try:
+            re.compile(p)
+        except re.error:
+            continue
+        pats.append(p)
+    lines = [bytes(rng.choice(b"abcx 1_-A") for _ in range(rng.randint(1, 16))) for _ in range(400)]
+    lines += [b"abc", b"cab", b"xax", b" abc ", b"aabcc", b"xaxabcab"]
+    data = b"\n".join(lines) + b"\n"
+    os.environ["SG_REGEX_ANCHORED"] = "1"
+    try:
+        m = sg.Matcher(pats, "regex", nocase=seed % 2 == 1)
+    finally:
+        os.environ.pop("SG_REGEX_ANCHORED", None)
+    assert m.match(data) == S.regex_hits(data, pats, nocase=seed % 2 == 1)

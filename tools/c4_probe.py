@@ -16,7 +16,7 @@ n_lines = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 which = sys.argv[2] if len(sys.argv) > 2 else "all"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sig = json.load(open(os.path.join(root, "tests", "golden", "signatures.json")))
-nuc = [base64.b64decode(r["p"]) for r in sig["regexes"] if r["dfa_rc"] == 0]
+nuc = [base64.b64decode(r["p"]) for r in sig["regexes"]]
 syn = corpus.nmap_signatures()
 pats = {"all": nuc + syn, "nuclei": nuc, "nmap": syn}[which]
 buf = corpus.lines_from_pool(corpus.banner_pool(), n_lines, seed=3)
