@@ -445,6 +445,41 @@ def bench_c5(args):
         dist.destroy_process_group()
 
 
+def gnu_sort_comm(cur: bytes, prior: bytes, want_uniq: bytes, want_fresh: bytes, threads: int = 16):
+    """The shell restatement of A7+A8 timed on the host: LC_ALL=C sort -u --parallel over
+    the whole input, then comm -13 against the prior (SURVEY.md §8(d) CPU baseline).
+    Inputs are staged in a temp dir first (outside the timing); the empty line that sort -u
+    keeps is dropped before the comparison, as A7 defines."""
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("sort") or not shutil.which("comm"):
+        return None
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    env = dict(os.environ, LC_ALL="C")
+    with tempfile.TemporaryDirectory() as d:
+        pc, pp, pu = os.path.join(d, "cur"), os.path.join(d, "prior"), os.path.join(d, "uniq")
+        with open(pc, "wb") as f:
+            f.write(cur)
+        with open(pp, "wb") as f:
+            f.write(prior)
+        t = time.perf_counter()
+        subprocess.run(["sort", "-u", "--parallel=%d" % threads, "-S", "25%", "-T", d, "-o", pu, pc], env=env,
+                       check=True)
+        fresh = subprocess.run(["comm", "-13", pp, pu], env=env, check=True, stdout=subprocess.PIPE).stdout
+        t = time.perf_counter() - t
+        with open(pu, "rb") as f:
+            uniq = f.read()
+    if uniq.startswith(b"\n"):
+        uniq = uniq[1:]
+    if fresh.startswith(b"\n"):
+        fresh = fresh[1:]
+    n = cur.count(b"\n") + (0 if cur.endswith(b"\n") or not cur else 1)
+    return {"value": round(n / t, 1), "unit": "records/s", "cores": threads, "seconds": round(t, 2),
+            "command": "LC_ALL=C sort -u --parallel=%d | comm -13 prior -" % threads,
+            "bit_exact_with_oracle": uniq == want_uniq and fresh == want_fresh}
+
+
 def dev_bytes(b, dev):
     import numpy as np
     import torch
@@ -588,6 +623,7 @@ def main():
             u_gpu = ctx.to_bytes(r.uniq, r.uniq_bytes)
             f_gpu = ctx.to_bytes(r.fresh, r.fresh_bytes)
             cpu["gpu_output_bit_exact"] = (u_gpu == eu and f_gpu == ef)
+            cpu["gnu_sort_comm"] = gnu_sort_comm(cbytes, pbytes, eu, ef)
 
     if rank == 0:
         line = {
