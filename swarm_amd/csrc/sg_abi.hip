@@ -34,6 +34,32 @@ __host__ __device__ __forceinline__ uint64_t hash_words(Load ld, uint32_t len) {
     return mix64(h);
 }
 
+// hash_words over buf[s, e) with aligned 8-byte loads (bit-identical): word o is bytes
+// [s+o, s+o+8) little-endian, joined from at most two aligned words. buf is 8-B aligned; a
+// second word is read only when it holds a byte of the record.
+__device__ __forceinline__ uint64_t hash_record(const uint8_t *__restrict__ buf, uint32_t s, uint32_t e) {
+    const uint32_t len = e - s;
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ ((uint64_t)len * 0xff51afd7ed558ccdull);
+    const uint32_t sh = (s & 7u) * 8u;
+    const uint64_t *wp = reinterpret_cast<const uint64_t *>(buf + (s & ~7u));
+    uint64_t lo = wp[0];
+    for (uint32_t o = 0; o < len; o += 8) {
+        const uint32_t take = (len - o) < 8u ? (len - o) : 8u;
+        uint64_t w = lo >> sh;
+        if (sh && (s & 7u) + take > 8u) {
+            const uint64_t hi = wp[(o >> 3) + 1];
+            w |= hi << (64u - sh);
+            lo = hi;
+        } else if (sh == 0 && o + 8u < len) {
+            lo = wp[(o >> 3) + 1];
+        }
+        if (take < 8u) w &= (1ull << (8u * take)) - 1ull;
+        h = (h ^ mix64(w)) * 0x9fb21c651e98df25ull;
+        h ^= h >> 29;
+    }
+    return mix64(h);
+}
+
 __host__ __device__ __forceinline__ uint32_t part_of(uint64_t h, uint32_t parts) {
     return (uint32_t)(((h >> 32) * (uint64_t)parts) >> 32);
 }
@@ -73,8 +99,7 @@ __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ b
         uint32_t q = 0, bytes = 0;
         if (i < R) {
             const uint32_t s = spans[i].x, e = spans[i].y;
-            const uint8_t *p = buf + s;
-            const uint64_t h = hash_words([&](uint32_t j) { return p[j]; }, e - s);
+            const uint64_t h = hash_record(buf, s, e);
             q = part_of(h, parts);
             keys[i] = q;
             bytes = e - s + 1;

@@ -187,11 +187,12 @@ def test_c2_full_size_bit_exact(sg):
 
 
 # ------------------------------------------------------------------ partition (§8(e))
-@pytest.mark.parametrize("parts", [1, 2, 3, 8])
-def test_partition_matches_hash_oracle(sg, parts):
+@pytest.mark.parametrize("parts,maxlen", [(1, 25), (2, 25), (3, 25), (8, 25), (256, 90), (255, 17)])
+def test_partition_matches_hash_oracle(sg, parts, maxlen):
+    """Records of every length and start alignment (the device hash joins aligned words)."""
     import torch
     rng = random.Random(parts)
-    b = rand_buf(rng, 5000, alphabet=b"abcdef.", maxlen=25, tail=False)
+    b = rand_buf(rng, 5000, alphabet=b"abcdef.", maxlen=maxlen, tail=False)
     recs = S.parse_records(b)
     d = torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
     ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
