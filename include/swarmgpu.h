@@ -204,8 +204,9 @@ typedef struct sg_dev_rows {
  * element (strings decoded, other elements as their raw text); any other value is its raw
  * text. Empty rows are dropped. Rows are ordered by record, then key index, then element.
  * Lines that are not a single JSON object produce no rows. keys: n_keys (<= 64) names,
- * key i = keys[key_offs[i] .. key_offs[i+1]), total <= 4096 bytes, no characters that
- * need JSON escaping. */
+ * key i = keys[key_offs[i] .. key_offs[i+1]), total <= 4096 bytes, given in decoded
+ * UTF-8 form: a member key written with escapes ("title", "ti\"tle") is decoded
+ * before the comparison, as json.loads does. */
 int sg_json_fields(const uint8_t *buf, size_t n, const uint8_t *keys, const uint32_t *key_offs,
                    uint32_t n_keys, uint8_t *out, size_t cap, size_t *out_n,
                    uint32_t *row_rec, uint32_t *row_key, size_t rows_cap, size_t *n_rows);
