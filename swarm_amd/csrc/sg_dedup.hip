@@ -26,6 +26,7 @@
 #include "sg_emit.hpp"
 
 #include <stdlib.h>
+#include <string.h>
 
 namespace sg {
 
@@ -645,15 +646,18 @@ struct ViewSlots {
 static const ViewSlots CUR_VIEW = {CUR_SLOTS, S_OUT_UNIQ, S_U_SPANS, S_U_KEYS};
 static const ViewSlots PRIOR_VIEW = {PRIOR_SLOTS, S_P_UBUF, S_P_USPANS, S_P_UKEYS};
 
+// `pre`: the buffer's lines already parsed (and, for a trusted view, `trust_sorted` already
+// decided by the caller's check_sorted), so no parse or sortedness check is queued here.
 static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
-                        UView *uv) {
+                        UView *uv, const Lines *pre = nullptr) {
     *uv = UView{};
     Lines L;
-    SG_TRY(run_lines(c, d_buf, n, vs.lines, &L));
+    if (pre) L = *pre;
+    else SG_TRY(run_lines(c, d_buf, n, vs.lines, &L));
     const uint32_t R = L.n_rec;
     uv->in_records = R;
     if (R >= (1u << 30)) { set_error("%u records exceed the 2^30 per-call limit", R); return SG_E_TOO_LARGE; }
-    if (trust_sorted && R > 1) {
+    if (trust_sorted && R > 1 && !pre) {
         uint32_t *flag;
         SG_TRY(slot(c, S_M_CNT, 4, &flag));
         SG_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
@@ -765,14 +769,19 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint64_t *uc;
     SG_TRY(run_emit(c, k_emit_uniq, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
                     0.0));
+    // the output count and the run-sort error word come back with one host sync
+    uint8_t *pin = (uint8_t *)c->pinned;
+    SG_HIP(hipMemcpyAsync(pin, uc, 8, hipMemcpyDeviceToHost, c->stream));
+    if (nb) SG_HIP(hipMemcpyAsync(pin + 8, err, 4, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
     uint64_t tt = 0;
-    SG_TRY(ctx_readback(c, &tt, uc, 8));
+    memcpy(&tt, pin, 8);
     const uint32_t t1 = (uint32_t)(tt >> 32), t2 = (uint32_t)tt;
     // model: cached span per record; kept bytes read + written; span + key0 per kept record
     if (c->profile) prof_bytes(c, "emit_uniq", 8.0 * R + 2.0 * t2 + 24.0 * t1);
     if (nb) {
         uint32_t e = 0;
-        SG_TRY(ctx_readback(c, &e, err, 4));
+        memcpy(&e, pin + 8, 4);
         if (e) { set_error("run sort: segment bound violated (0x%x)", e); return SG_E_HIP; }
     }
     *uv = UView{ub, us, uk, t1, t2, R};
@@ -784,9 +793,35 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     *res = sg_dev_result{};
     UView pv;
     const bool have_prior = want_fresh && d_prior && n_prior;
-    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, true, &pv));
+    // Both parses first: the prior's sortedness flag rides back to the host with the current
+    // buffer's record count (one host sync instead of two). Then the prior's view (the input
+    // itself when strictly increasing), then the current scan's sort -u.
+    Lines Lp, Lc;
+    bool prior_sorted = true, flag_pending = false;
+    uint8_t *pin_flag = (uint8_t *)c->pinned + 2048;  // clear of ctx_readback's small copies
+    if (have_prior) {
+        SG_TRY(run_lines(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp));
+        const uint32_t R = Lp.n_rec;
+        if (R > 1 && R < (1u << 30)) {
+            uint32_t *flag;
+            SG_TRY(slot(c, S_M_CNT, 4, &flag));
+            SG_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
+            SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_prior, Lp.spans, Lp.keys,
+                        R, flag);
+            SG_HIP(hipMemcpyAsync(pin_flag, flag, 4, hipMemcpyDeviceToHost, c->stream));
+            flag_pending = true;
+        }
+    }
+    SG_TRY(run_lines(c, d_cur, n_cur, CUR_VIEW.lines, &Lc));
+    if (flag_pending) {
+        SG_HIP(hipStreamSynchronize(c->stream));  // normally already drained by the count readback
+        uint32_t f = 1;
+        memcpy(&f, pin_flag, 4);
+        prior_sorted = (f == 0);
+    }
+    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp));
     UView cu;
-    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu));
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc));
     res->in_records = cu.in_records;
     res->uniq = const_cast<uint8_t *>(cu.buf);
     res->uniq_bytes = cu.bytes;
