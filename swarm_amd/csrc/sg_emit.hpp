@@ -208,6 +208,10 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_count(Item item, uint32_t n, 
     }
 }
 
+// SPARSE (selections that drop items: unique compaction, new records): the wave's kept
+// items are first packed in LDS in output order, then copied 64 per round, so a round is
+// not spent on a 64-item slice that keeps only a few records.
+template <bool SPARSE>
 __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache, uint32_t n,
                                                 const uint64_t *__restrict__ pre,
                                                 const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
@@ -217,6 +221,8 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4][EM_WIN];
     __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
     __shared__ uint64_t s_wt[4];
+    constexpr int CK = SPARSE ? EM_ROUNDS * 64 : 1;
+    __shared__ uint32_t s_cst[4][CK], s_cln[4][CK], s_co[4][CK];
     const uint32_t tile = blockIdx.x;
     const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
     const uint32_t wbase = tile * EM_TILE + wid * 256u;
@@ -243,6 +249,39 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
 #pragma unroll
     for (uint32_t w = 0; w < 4; ++w) woff += (w < wid) ? s_wt[w] : 0ull;
     const uint64_t wpre = pre[tile] + woff;
+    if constexpr (SPARSE) {
+#pragma unroll
+        for (int r = 0; r < EM_ROUNDS; ++r) {
+            if (!((fmask >> r) & 1u)) continue;
+            const uint64_t gp = wpre + loc[r];
+            const uint32_t j = (uint32_t)(gp >> 32);
+            const uint32_t o = (uint32_t)gp;
+            if (out_spans) out_spans[j] = make_uint2(o, o + ln[r]);
+            if (kout) kout[j] = kin[wbase + r * 64u + lane];
+            const uint32_t e = (uint32_t)(loc[r] >> 32);  // kept rank within the wave
+            s_cst[wid][e] = st[r];
+            s_cln[wid][e] = ln[r];
+            s_co[wid][e] = o;
+        }
+        if (dbg & 1) return;  // probe mode: no copy (timing only)
+        const uint32_t kept = (uint32_t)(run >> 32);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (uint32_t k0 = 0; k0 < kept; k0 += 64u) {
+            const uint32_t q = k0 + lane;
+            const bool f = q < kept;
+            const uint32_t s = f ? s_cst[wid][q] : 0u, l = f ? s_cln[wid][q] : 0u, o = f ? s_co[wid][q] : 0u;
+            const uint32_t last = (kept - k0 >= 64u) ? 63u : kept - k0 - 1u;
+            const uint64_t o0 = (uint32_t)__shfl((int)o, 0, 64);
+            const uint64_t oend = (uint32_t)__shfl((int)(o + l + 1u), (int)last, 64);
+            const uint64_t base = o0 & ~15ull;
+            wave_copy_round(src, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
+                            (uint32_t)(o - base), o0, oend, base);
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < EM_ROUNDS; ++r) {
         const bool f = (fmask >> r) & 1u;
@@ -269,17 +308,17 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
 }
 
 // One symbol per use, so rocprofv3 kernel stats and PMC passes attribute each separately.
-#define SG_EMIT_APPLY(NAME)                                                                         \
+#define SG_EMIT_APPLY(NAME, SPARSE)                                                                 \
     __global__ __launch_bounds__(EM_BLOCK) void NAME(                                               \
         const uint2 *__restrict__ cache, uint32_t n, const uint64_t *__restrict__ pre,              \
         const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, uint2 *__restrict__ out_spans,  \
         const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout, int dbg) {                   \
-        emit_apply_body(cache, n, pre, src, dst, out_spans, kin, kout, dbg);                        \
+        emit_apply_body<SPARSE>(cache, n, pre, src, dst, out_spans, kin, kout, dbg);                \
     }
-SG_EMIT_APPLY(k_emit_sorted)
-SG_EMIT_APPLY(k_emit_uniq)
-SG_EMIT_APPLY(k_emit_fresh)
-SG_EMIT_APPLY(k_emit_apply)
+SG_EMIT_APPLY(k_emit_sorted, false)
+SG_EMIT_APPLY(k_emit_uniq, true)
+SG_EMIT_APPLY(k_emit_fresh, true)
+SG_EMIT_APPLY(k_emit_apply, false)
 #undef SG_EMIT_APPLY
 
 // ------------------------------------------------------------------ common items
