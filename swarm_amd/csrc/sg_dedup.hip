@@ -238,11 +238,24 @@ __global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S,
 struct SegPred {
     const uint8_t *brk, *segbad;
     uint32_t n;
+    // A bad head's segment is small iff a break (brk, or the end) lies in (i, i + SEG_SMALL]:
+    // two aligned 16-B loads of brk (the slot has 32 B of tail room) replace a dependent
+    // byte walk.
     __device__ uint32_t operator()(uint32_t i) const {
+        static_assert(SEG_SMALL == 16, "window of two 16-B loads");
         if (!segbad[i]) return 0u;
-        uint32_t j = i + 1;
-        while (j < n && j <= i + SEG_SMALL && !brk[j]) ++j;
-        return (j - i <= SEG_SMALL) ? 1u : 2u;
+        const uint32_t a = (i + 1) & ~15u, sh = (i + 1) - a;
+        const uint4 w0 = *reinterpret_cast<const uint4 *>(brk + a);
+        const uint4 w1 = *reinterpret_cast<const uint4 *>(brk + a + 16);
+        const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t t = (((w[q] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w[q]) & 0x80808080u;  // nonzero bytes
+            m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * q);
+        }
+        if (n - a < 32u) m |= ~0u << (n - a);  // positions >= n end the segment
+        return ((m >> sh) & 0xffffu) ? 1u : 2u;
     }
 };
 
@@ -708,7 +721,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
     uint8_t *brk;
-    SG_TRY(slot(c, S_BRK, R, &brk));
+    SG_TRY(slot(c, S_BRK, (size_t)R + 32, &brk));  // + SegPred's 32-B window
     uint32_t *GS, *GE;
     SG_TRY(slot(c, S_GS, R / 64 + 16, &GS));
     SG_TRY(slot(c, S_GE, R / 64 + 16, &GE));
