@@ -43,8 +43,11 @@ __global__ __launch_bounds__(RS_HBLOCK) void k_rs_hist(const uint64_t *__restric
         for (int u = 0; u < HU; ++u) {
             const bool valid = i0 + u * RS_HBLOCK + threadIdx.x < n;
             const uint32_t cnt = (uint32_t)__popcll(__ballot(valid));
-            for (int p = 0; p < npasses; ++p) {
-                const uint32_t d = (uint32_t)(k[u] >> (begin_bit + 8 * p)) & 255u;
+            const uint64_t kk = k[u] >> begin_bit;
+#pragma unroll
+            for (int p = 0; p < RS_MAXPASS; ++p) {
+                if (p >= npasses) break;
+                const uint32_t d = (uint32_t)(kk >> (8 * p)) & 255u;
                 const uint32_t d0 = (uint32_t)__shfl(d, 0, 64);
                 if (__all(!valid || d == d0)) {
                     if (lane_id() == 0 && cnt) h[wid][p][d0] += cnt;
