@@ -226,8 +226,24 @@ __global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S,
     if (i > 0 && !b) {
         d = ((ki & 0xffu) < 8u) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, 7);
         if (!d) {
+            // segment head = last break at or before i - 1 (position 0 at the latest), found
+            // 16 bytes at a time with aligned loads instead of a dependent byte walk
             uint32_t h = i - 1;
-            while (h > 0 && !brk[h]) --h;
+            for (;;) {
+                const uint32_t a = h & ~15u;
+                const uint4 w = *reinterpret_cast<const uint4 *>(brk + a);
+                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+                uint32_t m = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t t = (((ww[q] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | ww[q]) & 0x80808080u;
+                    m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * q);
+                }
+                m &= (2u << (h - a)) - 1u;  // positions a .. h
+                if (m) { h = a + 31u - (uint32_t)__clz(m); break; }
+                if (a == 0) { h = 0; break; }
+                h = a - 1;
+            }
             segbad[h] = 1;
         }
     }
