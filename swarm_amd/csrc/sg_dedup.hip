@@ -83,14 +83,19 @@ struct BigGroupPred {
     const uint64_t *K;
     uint8_t *brk;
     uint32_t n;
+    // all five keys are loaded unconditionally (clamped indices, one round trip; the
+    // +-64 neighbours are cache hits of adjacent waves) instead of after the head test
     __device__ uint32_t operator()(uint32_t i) const {
         const uint64_t k = K[i];
-        const bool head = (i == 0) || K[i - 1] != k;
+        const uint64_t kp = K[i > 0 ? i - 1 : i], kn = K[i + 1 < n ? i + 1 : i];
+        const uint64_t kp64 = K[i >= WAVE_GROUP ? i - WAVE_GROUP : i];
+        const uint64_t kn64 = K[i + WAVE_GROUP < n ? i + WAVE_GROUP : i];
+        const bool head = (i == 0) || kp != k;
         brk[i] = head ? 1 : 0;
         if ((k & 0xffu) != 8u) return 0u;
-        const bool tail = (i + 1 == n) || K[i + 1] != k;
-        const bool bh = head && (i + WAVE_GROUP < n) && K[i + WAVE_GROUP] == k;
-        const bool bt = tail && (i >= WAVE_GROUP) && K[i - WAVE_GROUP] == k;
+        const bool tail = (i + 1 == n) || kn != k;
+        const bool bh = head && (i + WAVE_GROUP < n) && kn64 == k;
+        const bool bt = tail && (i >= WAVE_GROUP) && kp64 == k;
         return (bh ? 1u : 0u) | (bt ? 2u : 0u);
     }
 };
