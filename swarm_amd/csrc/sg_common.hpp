@@ -323,4 +323,36 @@ __device__ __forceinline__ int rec_cmp_k(const uint8_t *ba, uint32_t sa, uint32_
     }
 }
 
+// rec_cmp_k's order (memcmp of the suffixes from `off`, then length) from one set of wide
+// loads when the common suffix is <= 48 bytes: the first differing byte of the normalised
+// words decides, else the shorter suffix is smaller.
+__device__ __forceinline__ int rec_cmp_w(const uint8_t *ba, uint32_t sa, uint32_t ea, const uint8_t *bb,
+                                         uint32_t sb, uint32_t eb, uint32_t off) {
+    const uint32_t la = ea - sa, lb = eb - sb;
+    const uint32_t ma = la > off ? la - off : 0u, mb = lb > off ? lb - off : 0u;
+    const uint32_t cl = ma < mb ? ma : mb;
+    if (cl > 48u) return rec_cmp_k(ba, sa, ea, bb, sb, eb, off);
+    const int by_len = ma < mb ? -1 : (ma > mb ? 1 : 0);
+    if (cl == 0) return by_len;
+    uint4 ca[4], cb[4];
+    load_chunks(ba, sa + off, cl, ca);
+    load_chunks(bb, sb + off, cl, cb);
+    uint32_t ra[13], rb[13];
+    normalize52(ca, (sa + off) & 15u, ra);
+    normalize52(cb, (sb + off) & 15u, rb);
+#pragma unroll
+    for (uint32_t o = 0; o < 12; ++o) {
+        if (4u * o < cl) {
+            const uint32_t k = cl - 4u * o;
+            const uint32_t m = k >= 4u ? ~0u : ((1u << (8u * k)) - 1u);
+            const uint32_t x = (ra[o] ^ rb[o]) & m;
+            if (x) {
+                const uint32_t sh = (uint32_t)__builtin_ctz(x) & ~7u;
+                return ((ra[o] >> sh) & 0xffu) < ((rb[o] >> sh) & 0xffu) ? -1 : 1;
+            }
+        }
+    }
+    return by_len;
+}
+
 }  // namespace sg

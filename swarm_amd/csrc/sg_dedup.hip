@@ -130,7 +130,7 @@ __device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint2 *spa
                                             uint64_t ka, uint32_t ra, uint64_t kb, uint32_t rb, uint32_t off) {
     if (ka != kb) return ka < kb ? -1 : 1;
     if ((ka & 0xffu) < 8u) return 0;
-    return rec_cmp_k(buf, spans[ra].x, spans[ra].y, buf, spans[rb].x, spans[rb].y, off + 7);
+    return rec_cmp_w(buf, spans[ra].x, spans[ra].y, buf, spans[rb].x, spans[rb].y, off + 7);
 }
 
 // ------------------------------------------------------------------ refinement rounds
