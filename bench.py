@@ -331,9 +331,7 @@ def bench_c5(args):
     from swarm_amd import corpus, sharded
     from swarm_amd import distributed as D
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = dist_setup(args)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         local = local % max(torch.cuda.device_count(), 1)
@@ -486,6 +484,66 @@ def dev_bytes(b, dev):
     return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).to(dev)
 
 
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args, argv) -> int:
+    """`--gpus N` (N > 1) without a torch.distributed launcher around us: start N ranks
+    ourselves, one process per GPU, before this process touches any GPU (the parent only
+    parses arguments), as `torch.distributed.run` on 127.0.0.1 would. Rank 0 prints the
+    JSON line; the exit code is the launcher's."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dist_setup(args):
+    """(world, rank, local) from the launcher's env; initialises the process group when
+    world > 1 and checks it matches --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    return world, rank, local
+
+
+def launcher_check(args):
+    """CPU rehearsal of the N-rank launch and the timing protocol (barrier, max over ranks,
+    one JSON line from rank 0) with no GPU work: what tests/test_bench_launcher.py runs."""
+    import torch
+    import torch.distributed as dist
+    world, rank, _ = dist_setup(args)
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    x = torch.arange(1 << 16, dtype=torch.int64)
+    for _ in range(args.steps):
+        x = (x * 3 + rank) % 1000003
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "records/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+                          "launcher_check": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -498,7 +556,12 @@ def main():
                     help="nccl (= RCCL) for real runs; gloo rehearses N ranks on fewer GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
+    ap.add_argument("--launcher-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, sys.argv[1:])
+    if args.launcher_check:
+        return launcher_check(args)
     if args.workload == "c3":
         return bench_c3(args)
     if args.workload == "c4":
@@ -512,9 +575,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = dist_setup(args)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         local = local % max(torch.cuda.device_count(), 1)
@@ -653,4 +714,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -229,6 +229,26 @@ class Context:
         s = None if stream is None else (C.c_void_p(stream) if stream else C.c_void_p(-1))
         check(lib.sg_ctx_create(device, s, C.byref(self._h)))
         self.device = device
+        self.stream = stream
+
+    def on_torch_stream(self) -> bool:
+        """True when the context's kernels run on torch's current stream of its device, so
+        torch allocations and library writes are ordered without extra synchronisation."""
+        import torch
+        return self.stream is not None and self.stream == torch.cuda.current_stream(self.device).cuda_stream
+
+    def fence_in(self):
+        """Before a library call that reads tensors torch produced (or writes into memory
+        torch may still be reading): drain torch's stream unless the context shares it."""
+        if not self.on_torch_stream():
+            import torch
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def fence_out(self):
+        """After library writes into torch-owned memory that torch will read or free next:
+        drain the context's stream unless it is torch's."""
+        if not self.on_torch_stream():
+            self.sync()
 
     def close(self):
         if self._h:
@@ -428,9 +448,11 @@ class Ingest:
         """(sort -u of the merged body, new records vs `prior`) as bytes."""
         d, n = self.finish()
         pd, pn, keep = 0, 0, None
-        if prior:
+        pv = _view(prior) if prior is not None else None
+        if pv is not None and pv.size:
             import torch
-            keep = torch.from_numpy(np.array(_view(prior))).cuda(self.ctx.device)
+            keep = torch.from_numpy(np.array(pv)).cuda(self.ctx.device)
+            self.ctx.fence_in()
             pd, pn = keep.data_ptr(), keep.numel()
         r = self.ctx.dedup_diff(d, n, pd, pn)
         return self.ctx.to_bytes(r.uniq, r.uniq_bytes), self.ctx.to_bytes(r.fresh, r.fresh_bytes)

@@ -34,8 +34,9 @@ struct TmRun {
     sg_matcher *m = nullptr;
     int stream = 0;
     std::vector<uint32_t> soff, satoms;  // signature -> atoms (CSR)
-    uint32_t *d_soff = nullptr, *d_satoms = nullptr;
 };
+
+constexpr int TM_MAX_DEV = 64;
 
 }  // namespace sg
 
@@ -45,11 +46,14 @@ struct sg_templates {
     std::vector<uint32_t> key_offs;
     std::vector<sg::TmRun> runs;
     std::vector<uint32_t> atom_part, occ_off, occ_m, m_tmpl, m_need, m_flags, t_first, t_count, t_flags, vac;
+    // Device tables, one set per device, uploaded on first use there and kept until
+    // sg_tmpl_free: a call on another device never frees tables an eval may be using.
     struct Dev {
+        bool ready = false;
         uint32_t *atom_part = nullptr, *occ_off = nullptr, *occ_m = nullptr, *m_tmpl = nullptr, *m_need = nullptr,
                  *m_flags = nullptr, *t_first = nullptr, *t_count = nullptr, *t_flags = nullptr, *vac = nullptr;
-    } d;
-    int dev = -1;
+        std::vector<uint32_t *> soff, satoms;  // per run
+    } d[sg::TM_MAX_DEV];
     std::mutex mu;
 };
 
@@ -63,26 +67,16 @@ static int tm_upload(const std::vector<T> &v, T **d) {
     return SG_OK;
 }
 
-static void tm_free_dev(sg_templates *h) {
-    auto &d = h->d;
+static void tm_free_dev(sg_templates::Dev &d) {
     for (void *p : {(void *)d.atom_part, (void *)d.occ_off, (void *)d.occ_m, (void *)d.m_tmpl, (void *)d.m_need,
                     (void *)d.m_flags, (void *)d.t_first, (void *)d.t_count, (void *)d.t_flags, (void *)d.vac})
         if (p) (void)hipFree(p);
+    for (auto *p : d.soff) if (p) (void)hipFree(p);
+    for (auto *p : d.satoms) if (p) (void)hipFree(p);
     d = sg_templates::Dev{};
-    for (auto &r : h->runs) {
-        if (r.d_soff) (void)hipFree(r.d_soff);
-        if (r.d_satoms) (void)hipFree(r.d_satoms);
-        r.d_soff = r.d_satoms = nullptr;
-    }
-    h->dev = -1;
 }
 
-static int tm_ensure_device(sg_templates *h, int dev) {
-    std::lock_guard<std::mutex> g(h->mu);
-    if (h->dev == dev) return SG_OK;
-    if (h->dev >= 0) { (void)hipSetDevice(h->dev); tm_free_dev(h); }
-    SG_HIP(hipSetDevice(dev));
-    auto &d = h->d;
+static int tm_upload_all(sg_templates *h, sg_templates::Dev &d) {
     SG_TRY(tm_upload(h->atom_part, &d.atom_part));
     SG_TRY(tm_upload(h->occ_off, &d.occ_off));
     SG_TRY(tm_upload(h->occ_m, &d.occ_m));
@@ -93,11 +87,28 @@ static int tm_ensure_device(sg_templates *h, int dev) {
     SG_TRY(tm_upload(h->t_count, &d.t_count));
     SG_TRY(tm_upload(h->t_flags, &d.t_flags));
     SG_TRY(tm_upload(h->vac, &d.vac));
-    for (auto &r : h->runs) {
-        SG_TRY(tm_upload(r.soff, &r.d_soff));
-        SG_TRY(tm_upload(r.satoms, &r.d_satoms));
+    d.soff.assign(h->runs.size(), nullptr);
+    d.satoms.assign(h->runs.size(), nullptr);
+    for (size_t i = 0; i < h->runs.size(); ++i) {
+        SG_TRY(tm_upload(h->runs[i].soff, &d.soff[i]));
+        SG_TRY(tm_upload(h->runs[i].satoms, &d.satoms[i]));
     }
-    h->dev = dev;
+    return SG_OK;
+}
+
+// The tables on `dev` (uploaded once, under the handle's lock; a failed upload frees what
+// it allocated and leaves the device not ready, so the next call retries cleanly).
+static int tm_ensure_device(sg_templates *h, int dev, const sg_templates::Dev **out) {
+    if (dev < 0 || dev >= TM_MAX_DEV) { set_error("device %d out of range", dev); return SG_E_INVAL; }
+    std::lock_guard<std::mutex> g(h->mu);
+    auto &d = h->d[dev];
+    if (!d.ready) {
+        SG_HIP(hipSetDevice(dev));
+        const int rc = tm_upload_all(h, d);
+        if (rc != SG_OK) { tm_free_dev(d); return rc; }
+        d.ready = true;
+    }
+    *out = &d;
     return SG_OK;
 }
 
@@ -261,13 +272,15 @@ static int tm_grow(sg_ctx *c, TmAccum *a, uint64_t need) {
 
 static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint64_t n, sg_dev_tmatches *res) {
     *res = sg_dev_tmatches{};
-    SG_TRY(tm_ensure_device(h, c->device));
-    const auto &D = h->d;
+    const sg_templates::Dev *pd = nullptr;
+    SG_TRY(tm_ensure_device(h, c->device, &pd));
+    const auto &D = *pd;
     TmAccum acc;
     uint64_t R = 0;
     bool have_R = false;
     // stream 0: the records themselves
-    for (auto &run : h->runs) {
+    for (size_t ri = 0; ri < h->runs.size(); ++ri) {
+        auto &run = h->runs[ri];
         if (run.stream != 0) continue;
         sg_dev_hits r;
         SG_TRY(dev_match(c, run.m, d_buf, n, &r, false));
@@ -276,7 +289,7 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
         if (!r.n_hits) continue;
         SG_TRY(tm_grow(c, &acc, acc.n + r.n_hits));
         SG_LAUNCH(c, "tm_collect", k_tm_collect, (uint32_t)((r.n_hits + 255) / 256), 256, 0, r.rec_idx, r.sig_id,
-                  (uint32_t)r.n_hits, run.d_soff, run.d_satoms, D.atom_part, (const uint32_t *)nullptr,
+                  (uint32_t)r.n_hits, D.soff[ri], D.satoms[ri], D.atom_part, (const uint32_t *)nullptr,
                   (const uint32_t *)nullptr, acc.p + acc.n);
         acc.n += r.n_hits;
     }
@@ -289,14 +302,15 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
                                &rows));
         R = rows.in_records;
         have_R = true;
-        for (auto &run : h->runs) {
+        for (size_t ri = 0; ri < h->runs.size(); ++ri) {
+            auto &run = h->runs[ri];
             if (run.stream != 1 || rows.bytes == 0) continue;
             sg_dev_hits r;
             SG_TRY(dev_match(c, run.m, rows.data, rows.bytes, &r, false));
             if (!r.n_hits) continue;
             SG_TRY(tm_grow(c, &acc, acc.n + r.n_hits));
             SG_LAUNCH(c, "tm_collect", k_tm_collect, (uint32_t)((r.n_hits + 255) / 256), 256, 0, r.rec_idx, r.sig_id,
-                      (uint32_t)r.n_hits, run.d_soff, run.d_satoms, D.atom_part, rows.row_rec, rows.row_key,
+                      (uint32_t)r.n_hits, D.soff[ri], D.satoms[ri], D.atom_part, rows.row_rec, rows.row_key,
                       acc.p + acc.n);
             acc.n += r.n_hits;
         }
@@ -566,7 +580,8 @@ int sg_tmpl_eval(sg_templates *h, const uint8_t *buf, size_t n, uint32_t *rec_id
 
 void sg_tmpl_free(sg_templates *h) {
     if (!h) return;
-    if (h->dev >= 0) { (void)hipSetDevice(h->dev); tm_free_dev(h); }
+    for (int dv = 0; dv < TM_MAX_DEV; ++dv)
+        if (h->d[dv].ready) { (void)hipSetDevice(dv); tm_free_dev(h->d[dv]); }
     for (auto &r : h->runs) sg_free(r.m);
     delete h;
 }

@@ -51,6 +51,7 @@ def partition_exchange(ctx, buf: torch.Tensor, n: int, group=None) -> torch.Tens
     """GPU partition of `buf[:n]` by record hash, then the all-to-all exchange."""
     world = dist.get_world_size(group)
     send = torch.empty(n + 1, dtype=torch.uint8, device=buf.device)
+    ctx.fence_in()
     pbytes, _ = ctx.partition(buf.data_ptr(), n, world, send.data_ptr(), send.numel())
     return exchange_records(send, pbytes, group)
 
@@ -58,6 +59,7 @@ def partition_exchange(ctx, buf: torch.Tensor, n: int, group=None) -> torch.Tens
 def dedup_diff_step(ctx, cur: torch.Tensor, prior_part: torch.Tensor, group=None):
     """One distributed dedup+diff step. Returns (device result, received byte count)."""
     recv = partition_exchange(ctx, cur, cur.numel(), group)
+    ctx.fence_in()
     r = ctx.dedup_diff(recv.data_ptr(), recv.numel(), prior_part.data_ptr() if prior_part.numel() else 0,
                        prior_part.numel())
     return r, recv
@@ -67,9 +69,11 @@ def build_prior_partition(ctx, candidates: torch.Tensor, group=None) -> torch.Te
     """Setup (untimed): route this rank's prior candidate records to their owners and sort -u
     them there, giving the rank's resident prior partition."""
     recv = partition_exchange(ctx, candidates, candidates.numel(), group)
+    ctx.fence_in()
     r = ctx.dedup_diff(recv.data_ptr(), recv.numel(), 0, 0)
     out = torch.empty(max(int(r.uniq_bytes), 1), dtype=torch.uint8, device=candidates.device)
     if r.uniq_bytes:
+        ctx.fence_in()
         ctx.memcpy(out.data_ptr(), r.uniq, int(r.uniq_bytes))
     return out[: int(r.uniq_bytes)]
 

@@ -19,6 +19,21 @@ from typing import List, Sequence, Tuple
 import numpy as np
 
 PART_LIMIT = 0xFFFF0000  # bytes per library call (include/swarmgpu.h)
+RECORD_LIMIT = 1 << 30   # records per library call (sg_dedup.hip build_unique)
+
+
+def part_overflow_message(splitters: np.ndarray, b: int, cur_bytes: int, prior_bytes: int) -> str:
+    """Why range part b is over the per-call limit, and whether more parts can help: a part
+    whose two bounding splitters are equal is one key0 value (records sharing their first 7
+    bytes), which no number of parts can divide."""
+    lo = int(splitters[b - 1]) if b > 0 else None
+    hi = int(splitters[b]) if b < splitters.size else None
+    one_key = lo is not None and hi is not None and lo == hi
+    msg = "key0 range part %d holds %d cur / %d prior bytes (per-call limit %d bytes, %d records)" % (
+        b, cur_bytes, prior_bytes, PART_LIMIT, RECORD_LIMIT)
+    if one_key or (lo is not None and b + 1 < splitters.size and int(splitters[b + 1]) == lo):
+        return msg + ": its records share one key0 value %#x (first 7 bytes), which range routing cannot split" % lo
+    return msg + ": use more parts (smaller part_bytes)"
 
 
 def split_at_newlines(buf, max_bytes: int = 3 << 30, window: int = 1 << 20) -> List:
@@ -64,6 +79,7 @@ def route(ctx, pieces: Sequence, splitters: np.ndarray) -> List:
         if n == 0:
             continue
         out = torch.empty(n + 16, dtype=torch.uint8, device=p.device)
+        ctx.fence_in()  # `out` may be a block torch's stream is still reading
         pb, _ = ctx.partition_range(p.data_ptr(), n, splitters, out.data_ptr(), out.numel())
         off = 0
         for b in range(parts):
@@ -87,6 +103,7 @@ def _take(ctx, dptr: int, n: int, device):
     import torch
     t = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
     if n:
+        ctx.fence_in()
         ctx.memcpy(t.data_ptr(), dptr, n)
     return t[:n]
 
@@ -115,12 +132,13 @@ def dedup_diff_large(ctx, cur_pieces: Sequence, prior_pieces: Sequence = (), par
     uniq, fresh = [], []
     st = {"parts": splitters.size + 1, "in_records": 0, "uniq_records": 0, "fresh_records": 0,
           "max_part_bytes": 0}
-    for c, p in zip(cur_parts, prior_parts):
+    for b, (c, p) in enumerate(zip(cur_parts, prior_parts)):
         if c is None:
             continue
         if c.numel() > PART_LIMIT or (p is not None and p.numel() > PART_LIMIT):
-            raise ValueError("a key0 range holds more than 4 GiB: use more parts (smaller part_bytes)")
+            raise ValueError(part_overflow_message(splitters, b, c.numel(), p.numel() if p is not None else 0))
         st["max_part_bytes"] = max(st["max_part_bytes"], c.numel())
+        ctx.fence_in()
         try:
             r = ctx.dedup_diff(c.data_ptr(), c.numel(), p.data_ptr() if p is not None else 0,
                                p.numel() if p is not None else 0)

@@ -257,3 +257,41 @@ def test_dedup_slot_width_boundaries(sg, maxlen):
     u, f = sg.dedup_diff(b, prior)
     eu, ef = S.dedup_diff(b, prior)
     assert u == eu and f == ef
+
+
+# ------------------------------------------------------------------ prior sortedness check
+def _swapped_prior(recs, i):
+    r = list(recs)
+    r[i], r[i + 1] = r[i + 1], r[i]
+    return b"".join(x + b"\n" for x in r)
+
+
+@pytest.mark.parametrize("off", list(range(8, 61)) + [70, 100])
+def test_prior_one_swapped_pair_past_key0(sg, off):
+    """A prior sorted except for one adjacent pair that shares key0 (the first 7 bytes) and
+    differs at byte `off` must be detected as unsorted (rec_cmp_w fast path)."""
+    base = b"abcdefg" + bytes(range(0x41, 0x41 + max(0, off - 7)))[: max(0, off - 7)]
+    a, b = base[:off] + b"A" + b"tail", base[:off] + b"B" + b"tail"
+    others = [b"aaa", b"abcdefa", b"zzz-%d" % off, b"zzzz"]
+    recs = sorted(set(others + [a, b]))
+    i = recs.index(a)
+    prior = _swapped_prior(recs, i)
+    cur = b"".join(x + b"\n" for x in [a, b, b"new-1", b"zzz-%d" % off])
+    assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)
+    assert sg.diff(cur, prior) == S.dedup_diff(cur, prior)[1]
+
+
+@pytest.mark.parametrize("pair", [(b"abcdefghX", b"abcdefgh"), (b"abcdefgh" * 7 + b"Z", b"abcdefgh" * 7),
+                                  (b"0123456789abcdef", b"0123456789abcde"), (b"k" * 49, b"k" * 48)])
+@pytest.mark.parametrize("align", range(16))
+def test_prior_length_only_pair_every_alignment(sg, pair, align):
+    """Descending pair differing only in length (a record and its prefix), at every 16-B
+    alignment of the prior's records."""
+    pad = b"p" * align
+    head = [b"!" + pad] if align else []
+    recs = head + [pair[1], pair[0]]  # ascending
+    prior_sorted = b"".join(x + b"\n" for x in recs)
+    prior_bad = b"".join(x + b"\n" for x in head + [pair[0], pair[1]])
+    cur = pair[0] + b"\n" + pair[1] + b"\nother\n"
+    for prior in (prior_sorted, prior_bad):
+        assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)

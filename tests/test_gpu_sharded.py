@@ -88,3 +88,23 @@ def test_many_tiny_parts_and_skewed_keys(ctx):
     assert st["parts"] == 256
     eu, ef = S.dedup_diff(cur, prior)
     assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
+
+
+def test_private_stream_context_is_fenced():
+    """A Context without a stream argument runs on its own non-blocking stream; the sharded
+    path must still order torch allocations against library writes."""
+    import swarm_amd
+    from swarm_amd import sharded
+    c = swarm_amd.Context(0)
+    try:
+        assert not c.on_torch_stream()
+        buf, ids = corpus.subdomains(400_000, seed=36)
+        prior = corpus.prior_of(ids)
+        for _ in range(3):  # reuse of freed torch blocks between rounds is the hazard
+            u, f, _ = sharded.dedup_diff_large(c, sharded.split_at_newlines(dev(buf.tobytes()), 1 << 20),
+                                               sharded.split_at_newlines(dev(prior.tobytes()), 1 << 20),
+                                               part_bytes=1 << 20)
+            eu, ef = S.dedup_diff(buf.tobytes(), prior.tobytes())
+            assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
+    finally:
+        c.close()
