@@ -32,7 +32,9 @@ KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_u
                  "emit_fresh": "k_emit_fresh", "diff_tile": "k_diff_tile", "adjacent": "k_adjacent",
                  "lines": "k_lines", "lit_match": "k_lit_scan", "dfa_match": "k_dfa_match", "ac_match": "k_ac_match",
                  "re_prefilter": "k_lit_scan", "re_verify": "k_verify", "json_scan": "k_json_scan",
-                 "json_emit": "k_json_emit", "tm_eval": "k_tm_eval", "tm_collect": "k_tm_collect"}
+                 "json_emit": "k_json_emit", "tm_eval": "k_tm_eval", "tm_collect": "k_tm_collect",
+                 "bk_sort": "k_bk_sort", "bk_l1_apply": "k_bp_apply", "bk_l2_apply": "k_bp_apply",
+                 "bk_l1_count": "k_bp_count", "bk_l2_count": "k_bp_count", "bk_compact": "k_bk_compact"}
 
 
 def pmc_traffic(workload, kernel):

@@ -293,6 +293,14 @@ class Context:
             self.memcpy(out.ctypes.data, dptr, n)
         return out.tobytes()
 
+    def last_path(self):
+        """(pipeline, flags) of the last dedup_diff on this context: "radix" or "bucket" (the
+        sample sort with splitters from the prior scan), and the bucket path's hand-over
+        reasons (include/swarmgpu.h sg_ctx_last_path)."""
+        p, f = C.c_int(), C.c_uint32()
+        check(lib.sg_ctx_last_path(self._h, C.byref(p), C.byref(f)))
+        return ("bucket" if p.value == 1 else "radix"), f.value
+
     def dedup_diff(self, d_cur: int, n_cur: int, d_prior: int = 0, n_prior: int = 0) -> _abi.DevResult:
         """Device pointers in, device result (context-owned) out."""
         r = _abi.DevResult()

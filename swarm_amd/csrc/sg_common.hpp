@@ -62,6 +62,9 @@ enum Slot : int {
     S_F_SPANS, S_F_LB, S_F_A, S_F_B, S_F_DESC, S_F_OFFS, S_F_OUT, S_F_REC, S_F_KEY, S_F_KEYS,
     S_T_HITS, S_T_EXP, S_T_K2, S_T_V1, S_T_V2, S_T_OUT, S_T_SEL, S_T_E, S_T_E2, S_T_SEG, S_T_FLAG, S_T_O,
     S_T_REC, S_T_TID,
+    // bucket sample sort (sg_bucket.hip)
+    S_BK_SKEY, S_BK_SSPAN, S_BK_CNT1, S_BK_CNT2, S_BK_SMALL, S_BK_TOT2, S_BK_Q, S_BK_NCUR, S_BK_L1, S_BK_L2,
+    S_BK_US, S_BK_FS, S_BK_SPFX, S_BK_DBG, S_BK_RECS, S_BK_NREC,
     S_NSLOTS
 };
 
@@ -82,6 +85,8 @@ struct sg_ctx {
     void *slot_ptr[sg::S_NSLOTS] = {};
     size_t slot_cap[sg::S_NSLOTS] = {};
     void *pinned = nullptr;   // host pinned staging for small readbacks
+    int last_path = 0;        // dedup/diff: 0 = radix pipeline, 1 = bucket sample sort
+    uint32_t last_flags = 0;  // bucket path error word of the last call (0: not declined)
     // profiling
     bool profile = false;
     std::string prof_only;  // non-empty: time only launches with this name

@@ -822,8 +822,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     return SG_OK;
 }
 
-int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
-                   uint64_t n_prior, bool want_fresh, sg_dev_result *res) {
+static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
+                                uint64_t n_prior, bool want_fresh, sg_dev_result *res) {
     *res = sg_dev_result{};
     UView pv;
     const bool have_prior = want_fresh && d_prior && n_prior;
@@ -892,6 +892,25 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
     res->fresh_bytes = (uint32_t)tt;
     res->fresh_records = (uint32_t)(tt >> 32);
     return SG_OK;
+}
+
+// Dedup+diff entry: the bucket sample sort when there is a prior scan to take splitters from
+// and the input is large enough (sg_bucket.hip), else — or when the bucket path meets input
+// outside its LDS bounds — the radix pipeline above.
+int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
+                   uint64_t n_prior, bool want_fresh, sg_dev_result *res) {
+    c->last_path = 0;
+    c->last_flags = 0;
+    if (want_fresh && d_prior && n_prior) {
+        bool used = false;
+        *res = sg_dev_result{};
+        SG_TRY(bucket_dedup_diff(c, d_cur, n_cur, d_prior, n_prior, res, &used));
+        if (used) {
+            c->last_path = 1;
+            return SG_OK;
+        }
+    }
+    return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, want_fresh, res);
 }
 
 }  // namespace sg

@@ -53,6 +53,11 @@ int serialize(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
 int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes);
 
+// Bucket sample sort dedup+diff (sg_bucket.hip). *used = false: declined or outside its
+// bounds (the caller runs the radix pipeline).
+int bucket_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior, uint64_t n_prior,
+                      sg_dev_result *res, bool *used);
+
 // A4 matching of a device line buffer (sg_match.hip); want_lines = false skips the grep
 // output (hits only).
 int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res, bool want_lines);

@@ -237,6 +237,13 @@ int sg_ctx_memcpy(sg_ctx *c, void *dst, const void *src, size_t n) {
     return SG_OK;
 }
 
+int sg_ctx_last_path(sg_ctx *c, int *path, uint32_t *flags) {
+    if (!c) return SG_E_INVAL;
+    if (path) *path = c->last_path;
+    if (flags) *flags = c->last_flags;
+    return SG_OK;
+}
+
 int sg_ctx_reset_stats(sg_ctx *c) {
     if (!c) return SG_E_INVAL;
     SG_TRY(ctx_harvest(c));
