@@ -49,10 +49,10 @@ constexpr uint32_t BP_STAGE = BP_TILE + BP_OVH;
 constexpr uint32_t BP_OUTCAP = BP_STAGE + BP_PAD * BP_MAXB;
 
 // ------------------------------------------------------------------ final bucket geometry
-constexpr int BS_THREADS = 256;
-constexpr uint32_t BS_CCAP = 16384;   // cur bucket bytes (64 B per thread)
-constexpr uint32_t BS_PCAP = 8192;    // prior slice bytes incl. 16-B alignment slack (32 B per thread)
-constexpr uint32_t BS_NP = 320;       // prior records
+constexpr int BS_THREADS = 512;
+constexpr uint32_t BS_CCAP = 32768;   // cur bucket bytes (64 B per thread)
+constexpr uint32_t BS_PCAP = 16384;   // prior slice bytes incl. 16-B alignment slack (32 B per thread)
+constexpr uint32_t BS_NP = 640;       // prior records
 
 constexpr uint32_t BK_SPFX = 32;      // splitter prefix bytes cached for LDS compares
 
@@ -618,7 +618,7 @@ __device__ __forceinline__ int bs_item_cmp(const uint8_t *s, uint64_t ka, uint32
 // Phase timers of k_bk_sort (SG_BK_DEBUG=1): wall-clock ticks (100 MHz) per phase, summed
 // over blocks by thread 0 of each block.
 constexpr int BS_NPH = 6;
-constexpr uint32_t BS_NE = 608;       // cur records per bucket
+constexpr uint32_t BS_NE = 1280;      // cur records per bucket
 constexpr int BS_PT = (BS_NE + BS_THREADS - 1) / BS_THREADS;
 
 // Sort inside a bucket without a comparison network. The prior slice is a sorted sample of
@@ -777,20 +777,25 @@ __global__ __launch_bounds__(BS_THREADS) void k_bk_sort(BSArgs a) {
         if (bs_rec_cmp(s_pb, s_pkey[k - 1], s_pmeta[k - 1], s_pb, s_pkey[k], s_pmeta[k]) >= 0)
             atomicOr(a.flags, BK_F_UNSORTED);
     }
-    if (tid == 0 && npr && has_next) {
+    if (tid < 64 && npr && has_next) {  // wave 0: last slice record vs the next splitter
         const uint32_t ml = s_pmeta[npr - 1];
         const uint32_t la = ml >> 16, sa = ml & 0xffffu;
         const uint2 sp = a.sspan[f + 1];
         const uint32_t lb = sp.y - sp.x;
         const uint32_t m = la < lb ? la : lb;
         const uint32_t mc = m < BK_SPFX ? m : BK_SPFX;
-        int c = 0;
-        for (uint32_t o = 0; o < mc && !c; ++o) {
-            const uint32_t x = s_pb[sa + o], y = s_nx[o];
-            if (x != y) c = x < y ? -1 : 1;
+        const uint32_t o = tid;
+        const bool diff = o < mc && s_pb[sa + o] != s_nx[o];
+        const uint64_t dm = __ballot(diff);
+        int c;
+        if (dm) {
+            const uint32_t fo = (uint32_t)__ffsll((long long)dm) - 1;
+            c = s_pb[sa + fo] < s_nx[fo] ? -1 : 1;
+        } else {
+            c = m <= BK_SPFX ? (la < lb ? -1 : (la > lb ? 1 : 0)) : 2;
         }
-        if (!c) c = m <= BK_SPFX ? (la < lb ? -1 : (la > lb ? 1 : 0)) : lds_glob_cmp(s_pb, sa, la, a.P, sp, BK_SPFX);
-        if (c >= 0) atomicOr(a.flags, BK_F_UNSORTED);
+        if (c == 2 && tid == 0) c = lds_glob_cmp(s_pb, sa, la, a.P, sp, BK_SPFX);
+        if (tid == 0 && c >= 0) atomicOr(a.flags, BK_F_UNSORTED);
     }
     // ---- exact rank among the records sharing the insertion point
     uint32_t pos[BS_PT], dup = 0;
@@ -974,10 +979,10 @@ static uint64_t env_u64(const char *name, uint64_t dflt) {
 int bucket_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior, uint64_t n_prior,
                       sg_dev_result *res, bool *used) {
     *used = false;
-    if (!env_u64("SG_BUCKET", 1)) return SG_OK;
+    if (!env_u64("SG_BUCKET", 0)) return SG_OK;  // opt-in: slower than the radix pipeline so far
     if (!d_prior || n_prior == 0 || n_cur < env_u64("SG_BUCKET_MIN", 8ull << 20)) return SG_OK;
     if (((uintptr_t)d_cur & 15) || ((uintptr_t)d_prior & 15)) return SG_OK;
-    const uint64_t target = env_u64("SG_BUCKET_TARGET", 7500);
+    const uint64_t target = env_u64("SG_BUCKET_TARGET", 15000);
     const uint64_t want = (n_cur + target - 1) / (target ? target : 1);
     uint32_t NB1 = (uint32_t)ceil(sqrt((double)want));
     NB1 = NB1 < 2 ? 2 : (NB1 > BP_MAXB ? BP_MAXB : NB1);

@@ -28,6 +28,7 @@ def ctx():
 
 @pytest.fixture(autouse=True)
 def small_buckets(monkeypatch):
+    monkeypatch.setenv("SG_BUCKET", "1")
     monkeypatch.setenv("SG_BUCKET_MIN", "0")
     monkeypatch.setenv("SG_BUCKET_TARGET", "2500")
 
@@ -103,7 +104,8 @@ def test_lengths_around_key_and_word_sizes(ctx):
     recs = [base[:k] + bytes([c]) for k in range(0, 30) for c in range(0x61, 0x61 + 40)]
     recs += [base[:k] for k in range(1, 36)]
     rng = random.Random(8)
-    cur_l = [rng.choice(recs) for _ in range(20_000)]
+    cur_l = recs * 3
+    rng.shuffle(cur_l)
     prior = b"".join(r + b"\n" for r in sorted(set(recs[::2])))
     check(ctx, b"\n".join(cur_l) + b"\n", prior)
 
@@ -112,6 +114,15 @@ def test_heavy_duplicates(ctx):
     cur, prior = subdomain_pair(5_000, 9)
     cur = cur * 8
     check(ctx, cur, prior)
+
+
+def test_extreme_duplication_hands_over(ctx):
+    """Thousands of copies of a few records land in one bucket past its LDS budget: the radix
+    pipeline takes over, exactly."""
+    cur, prior = subdomain_pair(20_000, 22)
+    recs = S.parse_records(cur)
+    cur = cur + b"".join(recs[i % 7] + b"\n" for i in range(30_000))
+    check(ctx, cur, prior, path=None)
 
 
 def test_records_equal_to_splitters_and_prior_extremes(ctx):
