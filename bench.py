@@ -445,6 +445,183 @@ def bench_c5(args):
         dist.destroy_process_group()
 
 
+def host_cores() -> int:
+    """CPU threads this process may use on the host: the affinity set, capped by the job's
+    thread budget (OMP_NUM_THREADS is the GPU box's per-GPU CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
+
+
+def c3_signatures():
+    """C3's 2,000 literal signatures: sampled (seed 0) from the nuclei template words of length
+    >= 4."""
+    import base64
+    import random
+    sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
+    words = [base64.b64decode(w) for w in sig["words"]]
+    return random.Random(0).sample([w for w in words if len(w) >= 4], 2000)
+
+
+def gnu_grep_sort_comm(data: bytes, sigs, prior: bytes, cores: int):
+    """The shell restatement of the fused step on the host: `LC_ALL=C grep -a -F -f sigs` fanned
+    out over `cores` line-aligned splits (outputs concatenated in input order), then
+    `sort -u --parallel=cores`, then `comm -13 prior -` (SURVEY.md §8(d) CPU baselines).
+    Returns (matched, uniq, fresh, seconds per stage)."""
+    import shutil
+    import subprocess
+    import tempfile
+    if not (shutil.which("grep") and shutil.which("sort") and shutil.which("comm")):
+        return None
+    env = dict(os.environ, LC_ALL="C")
+    with tempfile.TemporaryDirectory() as d:
+        pf, pp = os.path.join(d, "sigs"), os.path.join(d, "prior")
+        with open(pf, "wb") as f:
+            f.write(b"".join(s + b"\n" for s in sigs if s and b"\n" not in s))
+        with open(pp, "wb") as f:
+            f.write(prior)
+        cuts, n = [0], len(data)
+        for k in range(1, cores):
+            c = data.find(b"\n", n * k // cores)
+            cuts.append(n if c < 0 else c + 1)
+        cuts.append(n)
+        names = []
+        for k in range(cores):
+            fn = os.path.join(d, "in%d" % k)
+            with open(fn, "wb") as f:
+                f.write(data[cuts[k]:cuts[k + 1]])
+            names.append(fn)
+        t0 = time.perf_counter()
+        procs = [subprocess.Popen(["grep", "-a", "-F", "-f", pf, fn], env=env, stdout=subprocess.PIPE) for fn in names]
+        outs = [p.communicate()[0] for p in procs]
+        t1 = time.perf_counter()
+        matched = b"".join(outs)
+        pm, pu = os.path.join(d, "matched"), os.path.join(d, "uniq")
+        with open(pm, "wb") as f:
+            f.write(matched)
+        t2 = time.perf_counter()
+        subprocess.run(["sort", "-u", "--parallel=%d" % cores, "-S", "25%", "-T", d, "-o", pu, pm], env=env, check=True)
+        fresh = subprocess.run(["comm", "-13", pp, pu], env=env, check=True, stdout=subprocess.PIPE).stdout
+        t3 = time.perf_counter()
+        with open(pu, "rb") as f:
+            uniq = f.read()
+    if uniq.startswith(b"\n"):
+        uniq = uniq[1:]
+    if fresh.startswith(b"\n"):
+        fresh = fresh[1:]
+    return matched, uniq, fresh, {"grep": round(t1 - t0, 3), "sort_comm": round(t3 - t2, 3)}
+
+
+def bench_x1(args, ctx=None, emit=True):
+    """The metric's fused step (BASELINE.json "match+dedup+diff"): 10M httpx
+    result lines (URLs of subdomains drawn like C2, each URL with a fixed title/server tail)
+    -> A3 parse -> A4 match against C3's 2,000 literal signatures -> A7 sort -u of the matched
+    lines -> A8 diff against the prior scan's matched set (worker/worker.py:83-98 ->
+    server/server.py:399-412 -> README.md:11). One device-resident call per step
+    (sg_dev_match_dedup_diff). Returns the result dict (printed as one JSON line if emit)."""
+    import numpy as np
+    import torch
+
+    import swarm_amd
+    from swarm_amd import corpus
+
+    own = ctx is None
+    if own:
+        torch.cuda.set_device(0)
+        ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    n_lines = args.x1_lines
+    sigs = c3_signatures()
+    tails = corpus.httpx_tails(sigs)
+    buf, ids = corpus.httpx_hosts(n_lines, tails, seed=1234)
+    d = torch.from_numpy(buf).cuda()
+    m = swarm_amd.Matcher(sigs, "literal")
+    # setup (untimed): the prior scan's matched set = sort -u of the matched lines of the
+    # prior's URLs (90 % of this scan's distinct URLs), computed by the same library call
+    pbuf = corpus.httpx_rows(corpus.prior_ids(ids), tails)
+    dp_in = torch.from_numpy(pbuf).cuda()
+    r0, _, _ = m.dev_match_dedup_diff(ctx, dp_in.data_ptr(), dp_in.numel())
+    d_prior = torch.empty(max(int(r0.uniq_bytes), 1), dtype=torch.uint8, device=d.device)
+    if r0.uniq_bytes:
+        ctx.memcpy(d_prior.data_ptr(), r0.uniq, int(r0.uniq_bytes))
+    n_prior = int(r0.uniq_bytes)
+    del dp_in
+    holder = {}
+
+    def run():
+        r, nh, nm = m.dev_match_dedup_diff(ctx, d.data_ptr(), d.numel(), d_prior.data_ptr(), n_prior)
+        holder["h"] = (nh, nm)
+        return r
+    el, full, stats, dominant, r = timed_steps(ctx, run, args)
+    nh, nm = holder["h"]
+    R = int(r.in_records)
+    matched_bytes = None
+    # algorithmic bytes of the step (SURVEY.md §8(d)): match = input + matched output;
+    # dedup+diff = matched + prior + unique + new
+    st = full.get("emit_lines")
+    matched_bytes = int(st[2] / 2) if st and st[2] else None
+    step_bytes = d.numel() + 2 * (matched_bytes or 0) + n_prior + int(r.uniq_bytes) + int(r.fresh_bytes)
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import semantics as S
+        prior_host = ctx.to_bytes(d_prior.data_ptr(), n_prior)
+        m_s = 3000
+        cut = int(np.flatnonzero(buf == 10)[m_s - 1]) + 1
+        sample = buf[:cut].tobytes()
+        tc = time.perf_counter()
+        eu, ef = S.dedup_diff(S.matched_lines(sample, S.literal_hits(sample, sigs)), prior_host)
+        tc = time.perf_counter() - tc
+        ds = torch.from_numpy(buf[:cut].copy()).cuda()
+        rs, _, _ = m.dev_match_dedup_diff(ctx, ds.data_ptr(), ds.numel(), d_prior.data_ptr(), n_prior)
+        cpu = {"value": round(m_s / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d X1 lines: oracle `sig in line` + sorted(set()) + set difference vs the prior matched "
+                         "set, 1 thread, %.2f s" % (m_s, tc), "host_cpus": os.cpu_count(),
+               "gpu_bit_exact_on_sample": (ctx.to_bytes(rs.uniq, rs.uniq_bytes) == eu and
+                                           ctx.to_bytes(rs.fresh, rs.fresh_bytes) == ef)}
+        cores = host_cores()
+        g_lines = min(n_lines, args.gnu_lines)
+        gcut = int(np.flatnonzero(buf == 10)[g_lines - 1]) + 1
+        gdata = buf[:gcut].tobytes()
+        g = gnu_grep_sort_comm(gdata, sigs, prior_host, cores)
+        if g:
+            gm, gu, gf, secs = g
+            dg = torch.from_numpy(buf[:gcut].copy()).cuda()
+            rg, _, _ = m.dev_match_dedup_diff(ctx, dg.data_ptr(), dg.numel(), d_prior.data_ptr(), n_prior)
+            tot = secs["grep"] + secs["sort_comm"]
+            cpu["gnu_grep_sort_comm"] = {
+                "value": round(g_lines / tot, 1), "unit": "records/s", "cores": cores, "seconds": secs,
+                "sample": "%d X1 lines (%d B)" % (g_lines, len(gdata)),
+                "command": "LC_ALL=C grep -a -F -f sigs (x%d line-aligned splits) | sort -u --parallel=%d | "
+                           "comm -13 prior -" % (cores, cores),
+                "bit_exact_vs_gpu": (ctx.to_bytes(rg.uniq, rg.uniq_bytes) == gu and
+                                     ctx.to_bytes(rg.fresh, rg.fresh_bytes) == gf)}
+    out = {
+        "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (httpx lines: C2-style subdomain URLs + fixed per-URL title/server tails, SURVEY.md "
+                "§8(d) C3 signatures)",
+        "config": {"workload": "X1: %dM httpx lines -> match 2000 literals -> sort -u matched -> diff vs prior "
+                               "matched set, 1 GPU" % (n_lines // 1_000_000),
+                   "bytes": int(d.numel()), "prior_bytes": n_prior},
+        "gbps": round(step_bytes * args.steps / el / 1e9, 2),
+        "hbm_frac_step": round(step_bytes * args.steps / el / 1e9 / HBM_PEAK_GBS, 4),
+        "records": {"in": R, "hits": int(nh), "matched": int(nm), "unique_matched": int(r.uniq_records),
+                    "new_matched": int(r.fresh_records)},
+        "roofline": roofline_of(stats, dominant, "x1", full),
+        "cpu_baseline": cpu,
+        "kernels": kernel_table(full),
+        "dedup_path": ctx.last_path()[0],
+    }
+    if emit:
+        print(json.dumps(out), flush=True)
+    if own:
+        ctx.close()
+    return out
+
+
 def gnu_sort_comm(cur: bytes, prior: bytes, want_uniq: bytes, want_fresh: bytes, threads: int = 16):
     """The shell restatement of A7+A8 timed on the host: LC_ALL=C sort -u --parallel over
     the whole input, then comm -13 against the prior (SURVEY.md §8(d) CPU baseline).
@@ -552,7 +729,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lines", type=int, default=10_000_000)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "fields"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "fields", "x1"], default="c2")
+    ap.add_argument("--x1-lines", type=int, default=10_000_000, help="X1 fused-step input lines")
+    ap.add_argument("--gnu-lines", type=int, default=2_000_000, help="lines of the GNU-tool CPU baseline sample")
+    ap.add_argument("--no-x1", action="store_true", help="default run: skip the fused X1 leg")
     ap.add_argument("--c5-hosts", type=int, default=64_000_000, help="C5 hosts (x 4 open-port slots = combos)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real runs; gloo rehearses N ranks on fewer GPUs")
@@ -572,6 +752,9 @@ def main():
         return bench_fields(args)
     if args.workload == "c5":
         return bench_c5(args)
+    if args.workload == "x1":
+        bench_x1(args)
+        return 0
 
     import numpy as np
     import torch
@@ -657,7 +840,8 @@ def main():
     value = total_records / elapsed
 
     # algorithmic bytes of the whole step (this rank): cur + prior + outputs
-    step_bytes = cur.numel() + prior.numel() + r.uniq_bytes + r.fresh_bytes
+    cur_bytes, prior_bytes = int(cur.numel()), int(prior.numel())
+    step_bytes = cur_bytes + prior_bytes + r.uniq_bytes + r.fresh_bytes
     info = {"R": int(r.in_records), "n": int(nrecv), "Rp": int(r.prior_records), "n_prior": int(prior.numel()),
             "U": int(r.uniq_records), "ub": int(r.uniq_bytes), "F": int(r.fresh_records), "fb": int(r.fresh_bytes)}
 
@@ -686,7 +870,17 @@ def main():
             u_gpu = ctx.to_bytes(r.uniq, r.uniq_bytes)
             f_gpu = ctx.to_bytes(r.fresh, r.fresh_bytes)
             cpu["gpu_output_bit_exact"] = (u_gpu == eu and f_gpu == ef)
-            cpu["gnu_sort_comm"] = gnu_sort_comm(cbytes, pbytes, eu, ef)
+            cpu["gnu_sort_comm"] = gnu_sort_comm(cbytes, pbytes, eu, ef, threads=host_cores())
+
+    x1 = None
+    if rank == 0 and world == 1 and not args.no_x1:
+        # the metric's fused step (match+dedup+diff) in the same run, reported beside C2
+        del cur, prior
+        torch.cuda.empty_cache()
+        x1_full = bench_x1(args, ctx=ctx, emit=False)
+        x1 = {k: x1_full[k] for k in ("value", "unit", "ms_per_step", "config", "gbps", "hbm_frac_step", "records",
+                                 "roofline", "cpu_baseline", "dedup_path")}
+        x1["kernels_top"] = dict(list(x1_full["kernels"].items())[:10])
 
     if rank == 0:
         line = {
@@ -696,8 +890,8 @@ def main():
             "data": "synthetic (seeded subdomain corpus, SURVEY.md §8(d) C2)",
             "config": {"workload": "C2: %dM-line subdomain merge + sort -u dedup + new-record diff per GPU"
                                    % (n_lines // 1_000_000),
-                       "lines_per_gpu": n_lines, "bytes_per_gpu": int(cur.numel()),
-                       "prior_bytes": int(prior.numel()),
+                       "lines_per_gpu": n_lines, "bytes_per_gpu": cur_bytes,
+                       "prior_bytes": prior_bytes,
                        "parallelism": "hash-partition all-to-all x%d" % world if world > 1 else "single GPU"},
             "gbps": round(step_bytes * world * args.steps / elapsed / 1e9, 2),
             "hbm_frac_step": round(step_bytes * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4),
@@ -708,6 +902,8 @@ def main():
             "kernels": kernels,
             "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
                             "HIP events only around the dominant kernel",
+            "dedup_path": ctx.last_path()[0],
+            "fused_x1": x1,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

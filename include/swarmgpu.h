@@ -178,6 +178,15 @@ typedef struct sg_dev_hits {
     uint64_t in_records;
 } sg_dev_hits;
 int sg_dev_match(sg_ctx *ctx, sg_matcher *h, const uint8_t *d_buf, size_t n, sg_dev_hits *res);
+/* The metric's fused step (BASELINE.json "match+dedup+diff"), device-resident end to end: raw
+ * module output (worker/worker.py:83-98 uploads it verbatim) -> A3 parse -> A4 signature match
+ * -> A7 sort -u of the MATCHED records (the /raw merge + dedup, server/server.py:399-412) ->
+ * A8 the matched records new since the prior scan's matched set (README.md:11 alerting).
+ * res: as sg_dev_dedup_diff over the matched records, with in_records = the input's records;
+ * *n_hits = (record, signature) hits, *matched_records = records with at least one hit. The
+ * hit arrays themselves are not returned (sg_dev_match gives them). d_prior may be NULL. */
+int sg_dev_match_dedup_diff(sg_ctx *ctx, sg_matcher *h, const uint8_t *d_buf, size_t n, const uint8_t *d_prior,
+                            size_t n_prior, sg_dev_result *res, uint64_t *n_hits, uint64_t *matched_records);
 void sg_free(void *h);  /* frees an sg_matcher */
 
 /* ------------------------------------------------------------------ module-output formats

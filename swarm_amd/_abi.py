@@ -28,7 +28,7 @@ EXPORTS = [
     "sg_ctx_last_path", "sg_lines",
     "sg_dedup", "sg_dedup_chunks", "sg_diff", "sg_dedup_diff", "sg_dev_dedup_diff",
     "sg_dev_partition", "sg_hash64", "sg_ac_compile", "sg_dfa_compile", "sg_matcher_info",
-    "sg_match", "sg_match_lines", "sg_dev_match", "sg_free",
+    "sg_match", "sg_match_lines", "sg_dev_match", "sg_dev_match_dedup_diff", "sg_free",
     "sg_nmap_ports", "sg_dev_nmap_ports", "sg_json_fields", "sg_dev_json_fields",
 ]
 
@@ -103,6 +103,7 @@ def _load():
         "sg_match": (C.c_int, [P, U8P, SZ, U64P, U32P, SZ, SZP]),
         "sg_match_lines": (C.c_int, [P, U8P, SZ, U8P, SZ, SZP]),
         "sg_dev_match": (C.c_int, [P, P, P, SZ, C.POINTER(DevHits)]),
+        "sg_dev_match_dedup_diff": (C.c_int, [P, P, P, SZ, P, SZ, C.POINTER(DevResult), U64P, U64P]),
         "sg_free": (None, [P]),
         "sg_nmap_ports": (C.c_int, [U8P, SZ, U8P, SZ, SZP]),
         "sg_dev_nmap_ports": (C.c_int, [P, P, SZ, C.POINTER(DevText)]),

@@ -164,6 +164,17 @@ class Matcher:
         check(lib.sg_dev_match(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(r)))
         return r
 
+    def dev_match_dedup_diff(self, ctx: "Context", d_buf: int, n: int, d_prior: int = 0, n_prior: int = 0):
+        """The metric's fused step on device buffers: parse -> match -> sort -u of the matched
+        records -> new matched records vs the prior scan's matched set. Returns (DevResult,
+        n_hits, matched_records) (include/swarmgpu.h sg_dev_match_dedup_diff)."""
+        r = _abi.DevResult()
+        nh, nm = C.c_uint64(), C.c_uint64()
+        check(lib.sg_dev_match_dedup_diff(ctx._h, self._h, C.c_void_p(d_buf), n,
+                                          C.c_void_p(d_prior) if d_prior else None, n_prior, C.byref(r),
+                                          C.byref(nh), C.byref(nm)))
+        return r, nh.value, nm.value
+
 
 def nmap_ports(buf) -> bytes:
     """nmap -oN text -> 'host:port' records (one per open port, input order), each

@@ -459,3 +459,47 @@ def hostport_pieces(pool, n: int, lo: int, hi: int, seed: int, per_piece: int = 
         out.append(rows[cols[None, :] < (hl + pl[p])[:, None]])
         del rows, c, h, p, hl
     return out
+
+
+# ------------------------------------------------------------------ X1: httpx host lines
+def httpx_tails(sigs, n_tails: int = 4096, plant: float = 0.05, seed: int = 0) -> tuple:
+    """A pool of httpx result tails `/path [status] [title] [server] [size]` as a masked byte
+    matrix; a `plant` fraction of titles carries one of `sigs`."""
+    rows = [r.split(b".com", 1)[1] for r in httpx_pool(sigs, n_tails, plant, seed=seed)]
+    W = max(len(r) for r in rows)
+    mat = np.zeros((len(rows), W), dtype=np.uint8)
+    lens = np.array([len(r) for r in rows], dtype=np.int64)
+    for i, r in enumerate(rows):
+        mat[i, :len(r)] = np.frombuffer(r, dtype=np.uint8)
+    return mat, np.arange(W)[None, :] < lens[:, None]
+
+
+def httpx_rows(ids: np.ndarray, tails: tuple, chunk: int = 1 << 20) -> np.ndarray:
+    """One httpx line per universe id: `https://` + the id's subdomain name + the tail the id
+    always gets (a URL answers with the same title and server on every scan), so two lines
+    are equal exactly when their ids are. '\\n'-terminated."""
+    tmat, tmsk = tails
+    pre = np.frombuffer(b"https://", dtype=np.uint8)
+    parts = []
+    for i in range(0, ids.size, chunk):
+        sub = ids[i:i + chunk]
+        nmat, nmsk = render_names(sub)
+        t = (_mix(sub.astype(np.uint64) ^ np.uint64(0x5bd1e995)) % np.uint64(tmat.shape[0])).astype(np.int64)
+        m = sub.size
+        mat = np.concatenate([np.broadcast_to(pre, (m, pre.size)), nmat, tmat[t]], axis=1)
+        msk = np.concatenate([np.ones((m, pre.size), dtype=bool), nmsk, tmsk[t]], axis=1)
+        parts.append(_flatten(mat, msk))
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8)
+
+
+def httpx_hosts(n: int, tails: tuple, seed: int = 1234, universe: int | None = None) -> tuple:
+    """(n httpx lines drawn from a universe of n URLs like the C2 subdomains, their ids)."""
+    U = universe or max(n, 1)
+    ids = np.random.default_rng(seed).integers(0, U, size=n, dtype=np.uint64)
+    return httpx_rows(ids, tails), ids
+
+
+def prior_ids(ids: np.ndarray) -> np.ndarray:
+    """The prior scan's ids: this scan's distinct ids except those divisible by 10."""
+    u = np.unique(ids)
+    return u[(u % np.uint64(10)) != 0]

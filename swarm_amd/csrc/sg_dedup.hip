@@ -219,7 +219,8 @@ __device__ __forceinline__ int rec_cmp8(const uint8_t *buf, uint32_t sa, uint32_
 // bad at its head (walk back to the brk, <= 64 positions): segbad[head] = 1.
 __global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S, const uint2 *__restrict__ SS,
                                                   const uint64_t *__restrict__ K, const uint8_t *__restrict__ brk,
-                                                  uint32_t n, uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad) {
+                                                  uint32_t n, uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad,
+                                                  uint32_t base) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     // all first-level loads issued together (one round trip before the byte compare)
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S,
     const uint2 x = SS[ip], y = SS[i];
     bool d = false;
     if (i > 0 && !b) {
-        d = ((ki & 0xffu) < 8u) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, 7);
+        d = ((ki & 0xffu) < 8u) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, base + 7);
         if (!d) {
             // segment head = last break at or before i - 1 (position 0 at the latest), found
             // 16 bytes at a time with aligned loads instead of a dependent byte walk
@@ -290,21 +291,22 @@ struct SegKeys {
     uint64_t c[SEG_CH];
 };
 
-__device__ __forceinline__ SegKeys seg_keys(const uint8_t *S, uint2 x) {
+__device__ __forceinline__ SegKeys seg_keys(const uint8_t *S, uint2 x, uint32_t base) {
     SegKeys k;
 #pragma unroll
-    for (int q = 0; q < SEG_CH; ++q) k.c[q] = chunk_key(S, x.x, x.y, 7u + 7u * q);
+    for (int q = 0; q < SEG_CH; ++q) k.c[q] = chunk_key(S, x.x, x.y, base + 7u + 7u * q);
     return k;
 }
 
 // <0, 0, >0 for record a vs record b (spans xa, xb) given their chunk keys.
-__device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2 xa, const SegKeys &b, uint2 xb) {
+__device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2 xa, const SegKeys &b, uint2 xb,
+                                       uint32_t base) {
 #pragma unroll
     for (int q = 0; q < SEG_CH; ++q) {
         if (a.c[q] != b.c[q]) return a.c[q] < b.c[q] ? -1 : 1;
         if ((a.c[q] & 0xffu) < 8u) return 0;
     }
-    return rec_cmp8(S, xa.x, xa.y - xa.x, xb.x, xb.y - xb.x, 7u + 7u * SEG_CH);
+    return rec_cmp8(S, xa.x, xa.y - xa.x, xb.x, xb.y - xb.x, base + 7u + 7u * SEG_CH);
 }
 
 // Rank the k members a.. of one segment with the G lanes gbase.. of the wave (lane gl of
@@ -313,10 +315,10 @@ __device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2
 template <int G>
 __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                uint8_t *__restrict__ dup, uint32_t a, uint32_t k, uint32_t gl,
-                                               uint32_t gbase, bool live) {
+                                               uint32_t gbase, bool live, uint32_t base) {
     const bool act = live && gl < k;
     const uint2 x = act ? SS[a + gl] : make_uint2(0u, 0u);
-    const SegKeys mk = act ? seg_keys(S, x) : SegKeys{{0, 0, 0, 0}};
+    const SegKeys mk = act ? seg_keys(S, x, base) : SegKeys{{0, 0, 0, 0}};
     uint32_t rank = 0;
     bool d = false;
     const uint32_t kk = live ? k : 0u;
@@ -331,7 +333,7 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
         for (int c = 0; c < SEG_CH; ++c) ok.c[c] = __shfl(mk.c[c], src, 64);
         const uint2 y = make_uint2((uint32_t)__shfl(x.x, src, 64), (uint32_t)__shfl(x.y, src, 64));
         if (act && j < kk && j != gl) {
-            const int c = seg_cmp(S, mk, x, ok, y);
+            const int c = seg_cmp(S, mk, x, ok, y, base);
             if (c > 0 || (c == 0 && j < gl)) ++rank;
             if (c == 0 && j < gl) d = true;
         }
@@ -345,7 +347,8 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
 // 16 lanes per small segment (<= SEG_SMALL members).
 __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                    const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
-                                                   const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n) {
+                                                   const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n,
+                                                   uint32_t base) {
     const uint32_t lane = lane_id(), gl = lane & 15u, gbase = lane & ~15u;
     const uint32_t q = blockIdx.x * 16u + (threadIdx.x >> 4);
     const bool live = q < nh;
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S
     const bool eb = !live || pe >= n || gl == 15u || brk[pe];
     const uint32_t me = (uint32_t)(__ballot(eb) >> gbase) & 0xffffu;
     const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);  // members: a .. a+k-1
-    seg_rank_group<16>(S, SS, dup, a, k, gl, gbase, live);
+    seg_rank_group<16>(S, SS, dup, a, k, gl, gbase, live, base);
 }
 
 // Larger segments (17..64 members), two heads per wave: two half-waves when both segments
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S
 __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                   const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
                                                   const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n,
-                                                  uint32_t *err) {
+                                                  uint32_t *err, uint32_t base) {
     const uint32_t q0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2u;
     const uint32_t lane = lane_id();
     if (q0 >= nh) return;
@@ -379,10 +382,11 @@ __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S,
     }
     if (k[0] <= 32u && k[1] <= 32u) {
         const uint32_t t = lane >> 5;
-        seg_rank_group<32>(S, SS, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u, (t ? k[1] : k[0]) > 0);
+        seg_rank_group<32>(S, SS, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u, (t ? k[1] : k[0]) > 0,
+                           base);
     } else {
-        seg_rank_group<64>(S, SS, dup, a[0], k[0], lane, 0u, true);
-        if (k[1]) seg_rank_group<64>(S, SS, dup, a[1], k[1], lane, 0u, true);
+        seg_rank_group<64>(S, SS, dup, a[0], k[0], lane, 0u, true, base);
+        if (k[1]) seg_rank_group<64>(S, SS, dup, a[1], k[1], lane, 0u, true, base);
     }
 }
 
@@ -417,10 +421,10 @@ __global__ void k_mark(const uint32_t *__restrict__ idx, uint32_t n, uint8_t *fl
 
 // Prior check: flag[0] = 1 if records are not strictly increasing.
 __global__ void k_check_sorted(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, const uint64_t *__restrict__ K,
-                               uint32_t n, uint32_t *flag) {
+                               uint32_t n, uint32_t *flag, uint32_t base) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x + 1;
     if (i >= n) return;
-    if (key_cmp_full(buf, spans, K[i - 1], i - 1, K[i], i, 0) >= 0) atomicOr(flag, 1u);
+    if (key_cmp_full(buf, spans, K[i - 1], i - 1, K[i], i, base) >= 0) atomicOr(flag, 1u);
 }
 
 // ------------------------------------------------------------------ diff
@@ -479,7 +483,7 @@ __global__ __launch_bounds__(256) void k_diff_split(const uint64_t *__restrict__
 }
 
 __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uint32_t *__restrict__ jb,
-                                                   uint8_t *__restrict__ fresh) {
+                                                   uint8_t *__restrict__ fresh, uint32_t base) {
     __shared__ uint64_t s_k[DF_PCAP];
     const uint32_t t = blockIdx.x;
     const uint32_t i0 = t * DF_TILE;
@@ -522,7 +526,7 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
 #pragma unroll
     for (int k = 0; k < DF_PER; ++k) {
         if (!need[k]) continue;
-        if (rec_equal_w(U.buf, us[k].x, us[k].y, P.buf, ps[k].x, ps[k].y, 7)) { pres[k] = true; continue; }
+        if (rec_equal_w(U.buf, us[k].x, us[k].y, P.buf, ps[k].x, ps[k].y, base + 7)) { pres[k] = true; continue; }
         // other P records sharing this key0 (distinct records with the same first 7 bytes):
         // they are sorted by their remaining bytes, so binary-search the run [c+1, c_end)
         // by full compare instead of scanning it
@@ -536,13 +540,28 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
             }
             ce = j0 + lo;
         }
-        if (!staged || ce >= j1)
-            while (ce < P.n && P.K[ce] == ku[k]) ++ce;  // run reaches past the staged keys
+        if (!staged || ce >= j1) {
+            // the run reaches past the staged keys (key0 shared by many prior records, e.g. a
+            // URL scheme): gallop, then bisect, for its end in P.K instead of walking it
+            uint32_t step = 1, lo2 = ce, hi2 = P.n;  // [ce, lo2) all equal ku
+            for (;;) {
+                const uint32_t probe = lo2 + step - 1;
+                if (probe >= P.n) break;
+                if (P.K[probe] != ku[k]) { hi2 = probe; break; }
+                lo2 = probe + 1;
+                step <<= 1;
+            }
+            while (lo2 < hi2) {  // first index in [lo2, hi2) whose key differs
+                const uint32_t mid = (lo2 + hi2) >> 1;
+                if (P.K[mid] == ku[k]) lo2 = mid + 1; else hi2 = mid;
+            }
+            ce = lo2;
+        }
         uint32_t lo = c0, hi = ce;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
             const uint2 x = P.sp[mid];
-            const int cmp = rec_cmp8_2(P.buf, x.x, x.y - x.x, U.buf, us[k].x, us[k].y - us[k].x, 7);
+            const int cmp = rec_cmp8_2(P.buf, x.x, x.y - x.x, U.buf, us[k].x, us[k].y - us[k].x, base + 7);
             if (cmp == 0) { pres[k] = true; break; }
             if (cmp < 0) lo = mid + 1; else hi = mid;
         }
@@ -550,6 +569,37 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
 #pragma unroll
     for (int k = 0; k < DF_PER; ++k)
         if (idx[k] < U.n) fresh[idx[k]] = pres[k] ? 0 : 1;
+}
+
+// ------------------------------------------------------------------ common prefix (URL-like data)
+// L = the longest prefix every record of cur and prior shares (capped at 255). All order and
+// equality questions are then decided from byte L on, and key0 is taken there: for URL lists
+// (every record starts "https://") the first 7 bytes say nothing, and equal-key0 runs would
+// span the whole buffer (binary searches over them in the diff, refinement rounds in the sort).
+__global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, uint32_t n,
+                                             const uint8_t *__restrict__ rbuf, const uint2 *__restrict__ rspans,
+                                             uint32_t *__restrict__ out) {
+    const uint2 r = rspans[0];
+    const uint32_t rl = r.y - r.x;
+    uint32_t best = 255;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint2 x = spans[i];
+        const uint32_t m = min(min(x.y - x.x, rl), best);
+        uint32_t l = 0;
+        while (l < m && buf[x.x + l] == rbuf[r.x + l]) ++l;
+        best = l < best ? l : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    if (lane_id() == 0) atomicMin(out, best);
+}
+
+__global__ __launch_bounds__(256) void k_rekey(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, uint32_t n,
+                                               uint32_t base, uint64_t *__restrict__ keys) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint2 x = spans[i];
+        keys[i] = chunk_key(buf, x.x, x.y, base);
+    }
 }
 
 // ------------------------------------------------------------------ host pipeline
@@ -610,8 +660,8 @@ int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
 // bytes. Each round sorts every group's members by the next 7-byte chunk (stable), marks
 // sub-segment heads in brk, and keeps the sub-segments that are still > 64 records.
 static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, uint32_t *V, uint8_t *brk,
-                             uint32_t *GS, uint32_t *GE, uint32_t B) {
-    uint32_t off = 7;
+                             uint32_t *GS, uint32_t *GE, uint32_t B, uint32_t base) {
+    uint32_t off = base + 7;
     while (B > 0) {
         uint64_t *goff;
         SG_TRY(slot(c, S_R_OFF, (size_t)B + 1, &goff));
@@ -683,7 +733,7 @@ static const ViewSlots PRIOR_VIEW = {PRIOR_SLOTS, S_P_UBUF, S_P_USPANS, S_P_UKEY
 // `pre`: the buffer's lines already parsed (and, for a trusted view, `trust_sorted` already
 // decided by the caller's check_sorted), so no parse or sortedness check is queued here.
 static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
-                        UView *uv, const Lines *pre = nullptr) {
+                        UView *uv, const Lines *pre = nullptr, uint32_t base = 0) {
     *uv = UView{};
     Lines L;
     if (pre) L = *pre;
@@ -695,7 +745,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         uint32_t *flag;
         SG_TRY(slot(c, S_M_CNT, 4, &flag));
         SG_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
-        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, L.spans, L.keys, R, flag);
+        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, L.spans, L.keys, R, flag,
+                    base);
         uint32_t f = 1;
         SG_TRY(ctx_readback(c, &f, flag, 4));
         trust_sorted = (f == 0);
@@ -749,7 +800,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint32_t B = 0, B2 = 0;
     SG_TRY(run_select2(c, "mark_groups", BigGroupPred{K, brk, R}, R, GS, GE, &B, &B2, 9.0));
     if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
-    if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B));
+    if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B, base));
 
     // materialise the records in this order: S (contiguous), SS spans into S
     uint8_t *Sb;
@@ -767,7 +818,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, S_BAD, R, &segbad));
     SG_HIP(hipMemsetAsync(segbad, 0, R, c->stream));
     // model: key0 + brk + span per record, both records' bytes where compared, dup out
-    SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, k_adjacent, grid_for(R, 256), 256, 0, Sb, SS, K, brk, R, dup, segbad);
+    SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, k_adjacent, grid_for(R, 256), 256, 0, Sb, SS, K, brk, R, dup, segbad,
+                base);
     uint32_t *hs, *hb;
     SG_TRY(slot(c, S_SEL, (size_t)R / 2 + 16, &hs));
     SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
@@ -776,8 +828,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint32_t *err;
     SG_TRY(slot(c, S_ERR, 4, &err));
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
-    if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R);
-    if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err);
+    if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
+    if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
     if (c->profile && c->prof_only.empty() && (ns || nb)) {  // full-profile steps only
         // byte model: per member its span read + written, ~4 chunk keys of record bytes, flag
         unsigned long long *mc;
@@ -831,31 +883,44 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     // buffer's record count (one host sync instead of two). Then the prior's view (the input
     // itself when strictly increasing), then the current scan's sort -u.
     Lines Lp, Lc;
-    bool prior_sorted = true, flag_pending = false;
-    uint8_t *pin_flag = (uint8_t *)c->pinned + 2048;  // clear of ctx_readback's small copies
+    bool prior_sorted = true;
+    uint32_t *dflag;  // [0] prior not strictly increasing, [1] common prefix length
+    SG_TRY(slot(c, S_M_CNT, 4, &dflag));
+    const uint32_t init[2] = {0u, 255u};
+    SG_HIP(hipMemcpyAsync(dflag, init, 8, hipMemcpyHostToDevice, c->stream));
     if (have_prior) {
         SG_TRY(run_lines(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp));
         const uint32_t R = Lp.n_rec;
-        if (R > 1 && R < (1u << 30)) {
-            uint32_t *flag;
-            SG_TRY(slot(c, S_M_CNT, 4, &flag));
-            SG_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
+        // keys from byte 0 decide sortedness exactly like keys from the common prefix would
+        if (R > 1 && R < (1u << 30))
             SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_prior, Lp.spans, Lp.keys,
-                        R, flag);
-            SG_HIP(hipMemcpyAsync(pin_flag, flag, 4, hipMemcpyDeviceToHost, c->stream));
-            flag_pending = true;
-        }
+                        R, dflag, 0u);
     }
     SG_TRY(run_lines(c, d_cur, n_cur, CUR_VIEW.lines, &Lc));
-    if (flag_pending) {
-        SG_HIP(hipStreamSynchronize(c->stream));  // normally already drained by the count readback
-        uint32_t f = 1;
-        memcpy(&f, pin_flag, 4);
-        prior_sorted = (f == 0);
+    // common prefix of every record (reference: the first record of cur, else of prior)
+    const bool ref_cur = Lc.n_rec > 0;
+    const uint8_t *rbuf = ref_cur ? d_cur : d_prior;
+    const uint2 *rsp = ref_cur ? Lc.spans : (have_prior ? Lp.spans : nullptr);
+    if (rsp && Lc.n_rec)
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u), 256, 0, d_cur,
+                    Lc.spans, Lc.n_rec, rbuf, rsp, dflag + 1);
+    if (rsp && have_prior && Lp.n_rec)
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior,
+                    Lp.spans, Lp.n_rec, rbuf, rsp, dflag + 1);
+    uint32_t fl[2] = {0u, 0u};
+    SG_TRY(ctx_readback(c, fl, dflag, 8));
+    prior_sorted = fl[0] == 0;
+    const uint32_t base = (rsp && (Lc.n_rec || (have_prior && Lp.n_rec))) ? fl[1] : 0u;
+    if (base) {
+        SG_LAUNCH(c, "rekey", k_rekey, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u), 256, 0, d_cur, Lc.spans, Lc.n_rec,
+                  base, Lc.keys);
+        if (have_prior && Lp.n_rec)
+            SG_LAUNCH(c, "rekey", k_rekey, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior, Lp.spans,
+                      Lp.n_rec, base, Lp.keys);
     }
-    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp));
+    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, base));
     UView cu;
-    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc));
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, base));
     res->in_records = cu.in_records;
     res->uniq = const_cast<uint8_t *>(cu.buf);
     res->uniq_bytes = cu.bytes;
@@ -879,7 +944,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     // model: key + span of every unique cur record, key of every prior record, the compared
     // bytes of both sides (~ the unique output + the prior), one flag per cur record
     SG_LAUNCH_B(c, "diff_tile", 16.0 * cu.n + 8.0 * pv.n + (double)cu.bytes + cu.n, k_diff_tile, ntiles, 256, 0,
-                U, P, jb, fresh);
+                U, P, jb, fresh, base);
     uint8_t *fout;
     SG_TRY(slot(c, S_OUT_FRESH, (size_t)cu.bytes + 64, &fout));
     uint64_t *fc;

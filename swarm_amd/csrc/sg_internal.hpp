@@ -53,6 +53,10 @@ int serialize(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
 int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes);
 
+// A7+A8 on device buffers (sg_dedup.hip): bucket sample sort or radix pipeline.
+int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior, uint64_t n_prior,
+                   bool want_fresh, sg_dev_result *res);
+
 // Bucket sample sort dedup+diff (sg_bucket.hip). *used = false: declined or outside its
 // bounds (the caller runs the radix pipeline).
 int bucket_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior, uint64_t n_prior,

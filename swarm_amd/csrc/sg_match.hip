@@ -1509,6 +1509,37 @@ int sg_dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, size_t n, sg_de
     return dev_match(c, h, b, n, res, true);
 }
 
+int sg_dev_match_dedup_diff(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, size_t n, const uint8_t *d_prior,
+                            size_t n_prior, sg_dev_result *res, uint64_t *n_hits, uint64_t *matched_records) {
+    if (!c || !h || !res || (!d_buf && n) || (!d_prior && n_prior)) {
+        set_error("sg_dev_match_dedup_diff: bad arguments");
+        return SG_E_INVAL;
+    }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b = d_buf, *p = d_prior;
+    if (((uintptr_t)d_buf & 15) != 0) {
+        uint8_t *a;
+        SG_TRY(slot(c, S_IN, n + 16, &a));
+        if (n) SG_HIP(hipMemcpyAsync(a, d_buf, n, hipMemcpyDeviceToDevice, c->stream));
+        b = a;
+    }
+    if (n_prior && ((uintptr_t)d_prior & 15) != 0) {
+        uint8_t *a;
+        SG_TRY(slot(c, S_IN2, n_prior + 16, &a));
+        SG_HIP(hipMemcpyAsync(a, d_prior, n_prior, hipMemcpyDeviceToDevice, c->stream));
+        p = a;
+    }
+    // A3 + A4: the matched records in input order (grep output, context slot S_M_LINES)
+    sg_dev_hits hits;
+    SG_TRY(dev_match(c, h, b, n, &hits, true));
+    if (n_hits) *n_hits = hits.n_hits;
+    if (matched_records) *matched_records = hits.matched_records;
+    // A7 + A8 on them: sort -u and the records new since the prior scan's matched set
+    SG_TRY(dev_dedup_diff(c, hits.lines, hits.lines_bytes, n_prior ? p : nullptr, n_prior, true, res));
+    res->in_records = hits.in_records;
+    return SG_OK;
+}
+
 int sg_match(sg_matcher *h, const uint8_t *buf, size_t n, uint64_t *rec_idx, uint32_t *sig_id, size_t cap,
              size_t *n_hit) {
     if (!h || !n_hit || (!buf && n)) { set_error("sg_match: bad arguments"); return SG_E_INVAL; }

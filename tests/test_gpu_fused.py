@@ -1,0 +1,113 @@
+"""GPU parity of the metric's fused step (sg_dev_match_dedup_diff): raw module output ->
+parse -> signature match -> sort -u of the matched records -> diff against the prior scan's
+matched set, bit-exact against the oracle (`sig in line` / re.search, sorted(set()), set
+difference)."""
+import base64
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import semantics as S
+from swarm_amd import corpus
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    import swarm_amd
+    assert swarm_amd.device_count() > 0
+    c = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def sigs():
+    sig = json.load(open(os.path.join(GOLDEN, "signatures.json")))
+    words = [base64.b64decode(w) for w in sig["words"]]
+    return random.Random(0).sample([w for w in words if len(w) >= 4], 300)
+
+
+def dev(b):
+    import torch
+    return torch.from_numpy(np.frombuffer(b + b"\0", dtype=np.uint8).copy()).cuda()
+
+
+def fused(ctx, m, data, prior):
+    d, p = dev(data), dev(prior)
+    r, nh, nm = m.dev_match_dedup_diff(ctx, d.data_ptr(), len(data), p.data_ptr() if prior else 0, len(prior))
+    return ctx.to_bytes(r.uniq, r.uniq_bytes), ctx.to_bytes(r.fresh, r.fresh_bytes), r, nh, nm
+
+
+def oracle(data, sigs, prior, kind="literal"):
+    hits = S.literal_hits(data, sigs) if kind == "literal" else S.regex_hits(data, sigs)
+    matched = S.matched_lines(data, hits)
+    u, f = S.dedup_diff(matched, prior)
+    return u, f, hits, matched
+
+
+@pytest.mark.parametrize("n,seed", [(1500, 1), (4000, 2)])
+def test_fused_literal_httpx(ctx, sigs, n, seed):
+    import swarm_amd
+    tails = corpus.httpx_tails(sigs, n_tails=512, seed=seed)
+    buf, ids = corpus.httpx_hosts(n, tails, seed=seed, universe=n // 2)
+    data = buf.tobytes()
+    m = swarm_amd.Matcher(sigs, "literal")
+    prior_all = corpus.httpx_rows(corpus.prior_ids(ids), tails).tobytes()
+    prior = S.dedup(S.matched_lines(prior_all, S.literal_hits(prior_all, sigs)))
+    u, f, r, nh, nm = fused(ctx, m, data, prior)
+    eu, ef, hits, matched = oracle(data, sigs, prior)
+    assert u == eu and f == ef
+    assert nh == len(hits) and nm == len(S.parse_records(matched))
+    assert r.in_records == len(S.parse_records(data))
+    assert r.uniq_records == len(S.parse_records(eu)) and r.fresh_records == len(S.parse_records(ef))
+
+
+def test_fused_no_prior_and_no_match(ctx, sigs):
+    import swarm_amd
+    m = swarm_amd.Matcher([b"zzzz-never"], "literal")
+    data = b"alpha\nbeta\nalpha\n"
+    u, f, r, nh, nm = fused(ctx, m, data, b"")
+    assert (u, f, nh, nm) == (b"", b"", 0, 0)
+    m2 = swarm_amd.Matcher([b"alp", b"et"], "literal")
+    u, f, r, nh, nm = fused(ctx, m2, data + b"\r\nalphabet", b"")
+    eu, ef, _, _ = oracle(data + b"\r\nalphabet", [b"alp", b"et"], b"")
+    assert u == eu and f == ef == eu
+
+
+def test_fused_regex_banners(ctx):
+    import swarm_amd
+    pats = corpus.nmap_signatures(n_products=40)
+    rows = corpus.banner_pool(n_products=40, pool=600, match_frac=0.3, seed=3)
+    rng = random.Random(5)
+    data = b"".join(rng.choice(rows) + b"\n" for _ in range(2500))
+    prior_rows = b"".join(r + b"\n" for r in rows[:300])
+    prior = S.dedup(S.matched_lines(prior_rows, S.regex_hits(prior_rows, pats)))
+    m = swarm_amd.Matcher(pats, "regex")
+    u, f, r, nh, nm = fused(ctx, m, data, prior)
+    eu, ef, hits, _ = oracle(data, pats, prior, kind="regex")
+    assert u == eu and f == ef and nh == len(hits)
+
+
+def test_fused_bucket_path(ctx, sigs, monkeypatch):
+    """The dedup stage of the fused step served by the bucket sample sort."""
+    import swarm_amd
+    monkeypatch.setenv("SG_BUCKET", "1")
+    monkeypatch.setenv("SG_BUCKET_MIN", "0")
+    monkeypatch.setenv("SG_BUCKET_TARGET", "2000")
+    tails = corpus.httpx_tails(sigs, n_tails=512, seed=9)
+    buf, ids = corpus.httpx_hosts(6000, tails, seed=9)
+    data = buf.tobytes()
+    m = swarm_amd.Matcher(sigs, "literal")
+    prior_all = corpus.httpx_rows(corpus.prior_ids(ids), tails).tobytes()
+    prior = S.dedup(S.matched_lines(prior_all, S.literal_hits(prior_all, sigs)))
+    u, f, _, _, _ = fused(ctx, m, data, prior)
+    eu, ef, _, _ = oracle(data, sigs, prior)
+    assert u == eu and f == ef
+    assert ctx.last_path()[0] == "bucket"
