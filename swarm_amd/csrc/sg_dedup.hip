@@ -576,22 +576,39 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
 // equality questions are then decided from byte L on, and key0 is taken there: for URL lists
 // (every record starts "https://") the first 7 bytes say nothing, and equal-key0 runs would
 // span the whole buffer (binary searches over them in the diff, refinement rounds in the sort).
-__global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, uint32_t n,
+__global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
+                                             const uint64_t *__restrict__ keys, uint32_t n,
                                              const uint8_t *__restrict__ rbuf, const uint2 *__restrict__ rspans,
-                                             uint32_t *__restrict__ out) {
-    const uint2 r = rspans[0];
-    const uint32_t rl = r.y - r.x;
-    uint32_t best = 255;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint2 x = spans[i];
-        const uint32_t m = min(min(x.y - x.x, rl), best);
-        uint32_t l = 0;
-        while (l < m && buf[x.x + l] == rbuf[r.x + l]) ++l;
-        best = l < best ? l : best;
+                                             const uint64_t *__restrict__ rkeys, uint32_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t l = 255;
+    if (i < n) {
+        // key0 = 7 bytes big-endian << 8 | min(len, 8): the first 7 bytes come from the keys
+        const uint64_t k = keys[i], kr = rkeys[0];
+        const uint64_t x = (k ^ kr) >> 8;
+        const uint32_t tk = (uint32_t)(k & 0xffu), tr = (uint32_t)(kr & 0xffu);
+        if (x) {
+            l = (uint32_t)__builtin_clzll(x << 8) >> 3;
+            l = min(l, min(tk, tr));
+        } else if (tk < 8u || tr < 8u) {
+            l = min(tk, tr);
+        } else {
+            // both share their first 7 bytes (URL schemes): 8 bytes per step from byte 7
+            const uint2 xs = spans[i], r = rspans[0];
+            const uint32_t m = min(min(xs.y - xs.x, r.y - r.x), 255u);
+            l = 7;
+            while (l < m) {
+                const uint32_t t = (m - l) < 8u ? (m - l) : 8u;
+                const uint64_t d = load_le(buf, xs.x + l, t) ^ load_le(rbuf, r.x + l, t);
+                if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
+                l += t;
+            }
+            l = min(l, m);
+        }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
-    if (lane_id() == 0) atomicMin(out, best);
+    for (int o = 32; o > 0; o >>= 1) l = min(l, (uint32_t)__shfl_xor((int)l, o, 64));
+    if (lane_id() == 0 && l < 255u) atomicMin(out, l);
 }
 
 __global__ __launch_bounds__(256) void k_rekey(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, uint32_t n,
@@ -901,12 +918,13 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const bool ref_cur = Lc.n_rec > 0;
     const uint8_t *rbuf = ref_cur ? d_cur : d_prior;
     const uint2 *rsp = ref_cur ? Lc.spans : (have_prior ? Lp.spans : nullptr);
+    const uint64_t *rkeys = ref_cur ? Lc.keys : (have_prior ? Lp.keys : nullptr);
     if (rsp && Lc.n_rec)
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u), 256, 0, d_cur,
-                    Lc.spans, Lc.n_rec, rbuf, rsp, dflag + 1);
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, grid_for(Lc.n_rec, 256), 256, 0, d_cur, Lc.spans, Lc.keys, Lc.n_rec,
+                    rbuf, rsp, rkeys, dflag + 1);
     if (rsp && have_prior && Lp.n_rec)
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior,
-                    Lp.spans, Lp.n_rec, rbuf, rsp, dflag + 1);
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, grid_for(Lp.n_rec, 256), 256, 0, d_prior, Lp.spans, Lp.keys, Lp.n_rec,
+                    rbuf, rsp, rkeys, dflag + 1);
     uint32_t fl[2] = {0u, 0u};
     SG_TRY(ctx_readback(c, fl, dflag, 8));
     prior_sorted = fl[0] == 0;

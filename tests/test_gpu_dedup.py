@@ -295,3 +295,40 @@ def test_prior_length_only_pair_every_alignment(sg, pair, align):
     cur = pair[0] + b"\n" + pair[1] + b"\nother\n"
     for prior in (prior_sorted, prior_bad):
         assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)
+
+
+# ------------------------------------------------------------------ common-prefix keying
+def _url_recs(rng, n, hosts=300, scheme=b"https://"):
+    hs = [b"www.h%d.example.com" % rng.randrange(hosts) for _ in range(hosts)]
+    return [scheme + rng.choice(hs) + b"/" + b"p" * rng.randrange(0, 30) for _ in range(n)]
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_dedup_diff_url_common_prefix(sg, seed):
+    """Every record starts with 'https://www.h' (13 shared bytes): the radix pipeline keys
+    from the common prefix; results stay those of sorted(set())."""
+    rng = random.Random(seed)
+    cur = b"\n".join(_url_recs(rng, 20_000)) + b"\n"
+    prior = b"".join(r + b"\n" for r in sorted(set(_url_recs(rng, 8_000))))
+    assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)
+
+
+@pytest.mark.parametrize("case", ["prefix_is_record", "all_identical", "prior_breaks_prefix", "long_prefix"])
+def test_common_prefix_edges(sg, case):
+    rng = random.Random(11)
+    if case == "prefix_is_record":
+        recs = [b"https://"] + [b"https://" + bytes([rng.randrange(97, 123)]) * rng.randrange(1, 9) for _ in range(3000)]
+        prior = b"https://\nhttps://a\n"
+    elif case == "all_identical":
+        recs = [b"x" * 300] * 500
+        prior = b"x" * 299 + b"\n"
+    elif case == "prior_breaks_prefix":
+        recs = _url_recs(rng, 3000)
+        prior = b"".join(r + b"\n" for r in sorted(set(_url_recs(rng, 500) + [b"http://a", b"zzz"])))
+    else:
+        pre = b"P" * 250
+        recs = [pre + bytes(rng.choice(b"ab\x00\xff") for _ in range(rng.randrange(0, 20))) for _ in range(4000)]
+        prior = b"".join(r + b"\n" for r in sorted(set(recs[::3])))
+    cur = b"\n".join(recs) + b"\n"
+    assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)
+    assert sg.dedup(cur) == S.dedup(cur)
