@@ -159,6 +159,16 @@ class Matcher:
         check(lib.sg_match_lines(self._h, _ptr(a), a.size, out.ctypes.data, out.size, C.byref(n)))
         return out[: n.value].tobytes()
 
+    def match_lines_count(self, buf) -> Tuple[bytes, int]:
+        """(grep output, number of non-empty input records) from one device pass."""
+        import torch
+        a = _view(buf)
+        ctx = _shared_ctx()
+        d = torch.from_numpy(np.array(a) if a.size else np.zeros(1, dtype=np.uint8)).cuda(ctx.device)
+        ctx.fence_in()
+        r = self.dev_match(ctx, d.data_ptr(), a.size)
+        return ctx.to_bytes(r.lines, r.lines_bytes), int(r.in_records)
+
     def dev_match(self, ctx: "Context", d_buf: int, n: int) -> _abi.DevHits:
         r = _abi.DevHits()
         check(lib.sg_dev_match(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(r)))
@@ -227,6 +237,21 @@ def device_count() -> int:
     n = C.c_int(0)
     check(lib.sg_device_count(C.byref(n)))
     return n.value
+
+
+_SHARED = {}
+
+
+def _shared_ctx():
+    """A per-thread context on the current torch device (host helpers that stage through
+    torch tensors)."""
+    import threading
+    import torch
+    key = (threading.get_ident(), torch.cuda.current_device())
+    c = _SHARED.get(key)
+    if c is None:
+        c = _SHARED[key] = Context(key[1], torch.cuda.current_stream().cuda_stream)
+    return c
 
 
 class Context:

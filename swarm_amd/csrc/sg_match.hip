@@ -424,7 +424,11 @@ static void free_dev(sg_matcher *h) {
 static int ensure_device(sg_matcher *h, int dev) {
     std::lock_guard<std::mutex> g(h->mu);
     if (h->dev == dev) return SG_OK;
-    if (h->dev >= 0) { (void)hipSetDevice(h->dev); free_dev(h); }
+    if (h->dev >= 0) {
+        // tables are read by calls in flight on their device: never freed under them
+        set_error("matcher tables live on device %d; compile one matcher per device (asked for %d)", h->dev, dev);
+        return SG_E_INVAL;
+    }
     SG_HIP(hipSetDevice(dev));
     if (h->has_pre) {
         auto &p = h->dplan;

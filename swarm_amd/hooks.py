@@ -24,22 +24,41 @@ def merge_keys(keys: Iterable[str], scan_id: str) -> List[str]:
     return [k for k in listed if k.endswith(".txt")]
 
 
-def raw_merge(objects: Dict[str, bytes], scan_id: str) -> bytes:
+def check_utf8(body: bytes, key: str = "") -> None:
+    """server/server.py:410 decodes every chunk body on its own (`.decode('utf-8')`), so a body
+    that is not valid UTF-8 — including a multibyte character split across two chunk files —
+    makes /raw fail there. The GPU path works on bytes; the hooks keep the reference's
+    behaviour by raising the same UnicodeDecodeError for such a body before any GPU work."""
+    try:
+        body.decode("utf-8")
+    except UnicodeDecodeError as e:
+        raise UnicodeDecodeError(e.encoding, e.object, e.start, e.end, "%s (chunk %s)" % (e.reason, key)) from None
+
+
+def _bodies(objects: Dict[str, bytes], scan_id: str, strict_utf8: bool) -> List[bytes]:
+    keys = merge_keys(objects.keys(), scan_id)
+    if strict_utf8:
+        for k in keys:
+            check_utf8(objects[k], k)
+    return [objects[k] for k in keys]
+
+
+def raw_merge(objects: Dict[str, bytes], scan_id: str, strict_utf8: bool = True) -> bytes:
     """Byte-identical /raw body: concatenation in merge_keys order, no separator
-    (server/server.py:407-410)."""
-    return b"".join(objects[k] for k in merge_keys(objects.keys(), scan_id))
+    (server/server.py:407-410); invalid UTF-8 fails as the reference's decode does."""
+    return b"".join(_bodies(objects, scan_id, strict_utf8))
 
 
-def raw_unique(objects: Dict[str, bytes], scan_id: str) -> bytes:
+def raw_unique(objects: Dict[str, bytes], scan_id: str, strict_utf8: bool = True) -> bytes:
     """sort -u of the /raw body, computed on the GPU straight from the chunk bodies."""
-    return api.dedup_chunks([objects[k] for k in merge_keys(objects.keys(), scan_id)])
+    return api.dedup_chunks(_bodies(objects, scan_id, strict_utf8))
 
 
 def completion_dedup_diff(objects: Dict[str, bytes], scan_id: str,
-                          prior_unique: Optional[bytes]) -> Tuple[bytes, bytes]:
+                          prior_unique: Optional[bytes], strict_utf8: bool = True) -> Tuple[bytes, bytes]:
     """At scan completion: (sort -u of this scan, records new since the prior scan of the
     same module). `prior_unique` is the prior scan's stored sort -u output (or None)."""
-    bodies = [objects[k] for k in merge_keys(objects.keys(), scan_id)]
+    bodies = _bodies(objects, scan_id, strict_utf8)
     merged = b"".join(bodies) if len(bodies) != 1 else bodies[0]
     return api.dedup_diff(merged, prior_unique or b"")
 
@@ -64,15 +83,16 @@ def postprocess_output(output_file: str, matcher=None, matches_file: Optional[st
     module's line-delimited output on the GPU and, if a signature matcher is given, write
     the matched lines (grep output, input order) to `matches_file`. The output file itself
     is left untouched, so the upload contract (uploads/{scan}/output/chunk_{i}.txt) holds.
-    Returns the number of non-empty records."""
+    Returns the number of non-empty records. One GPU pass: the match call parses the
+    records itself (its in_records), so the file is not parsed twice."""
     with open(output_file, "rb") as f:
         data = f.read()
-    n = len(api.lines(data))
     if matcher is not None and matches_file:
-        lines_out = matcher.match_lines(data)
+        lines_out, n = matcher.match_lines_count(data)
         with open(matches_file, "wb") as f:
             f.write(lines_out)
-    return n
+        return n
+    return len(api.lines(data))
 
 
 def raw_stream_dedup_diff(ctx, keys: Iterable[str], scan_id: str, read_body, prior_unique: Optional[bytes] = None,

@@ -59,3 +59,29 @@ def test_a4_regex_vs_grep_P(case):
 def test_record_spans_agree_with_parse():
     buf = b"\n\na\r\nbb\n\n\nccc"
     assert [buf[s:e] for s, e in S.record_spans(buf)] == S.parse_records(buf)
+
+
+def test_prior_scan_id_picks_latest_complete_earlier_scan_of_module():
+    """server/server.py:277-294 writes asm.scans documents; the prior of a scan is the latest
+    completed scan of the same module that started earlier."""
+    from swarm_amd.hooks import prior_scan_id
+    scans = [
+        {"scan_id": "a", "module": "dnsx", "scan_status": "complete", "scan_started": 100},
+        {"scan_id": "b", "module": "dnsx", "scan_status": "complete", "scan_started": 300},
+        {"scan_id": "c", "module": "dnsx", "scan_status": "running", "scan_started": 350},
+        {"scan_id": "d", "module": "httpx", "scan_status": "complete", "scan_started": 390},
+        {"scan_id": "e", "module": "dnsx", "scan_status": "complete", "scan_started": 500},
+        {"scan_id": "f", "module": "dnsx", "scan_status": "complete"},
+    ]
+    assert prior_scan_id(scans, "dnsx", 400) == "b"
+    assert prior_scan_id(scans, "dnsx", 300) == "a"
+    assert prior_scan_id(scans, "dnsx", 100) is None
+    assert prior_scan_id(scans, "httpx", 1000) == "d"
+    assert prior_scan_id(scans, "nmap", 1000) is None
+
+
+def test_check_utf8_matches_reference_decode():
+    from swarm_amd.hooks import check_utf8
+    check_utf8("déjà vu\n".encode())
+    with pytest.raises(UnicodeDecodeError):
+        check_utf8(b"\xe2\x82")  # a character cut at a chunk edge
