@@ -580,22 +580,25 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
                                              const uint64_t *__restrict__ keys, uint32_t n,
                                              const uint8_t *__restrict__ rbuf, const uint2 *__restrict__ rspans,
                                              const uint64_t *__restrict__ rkeys, uint32_t *__restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t l = 255;
-    if (i < n) {
+    __shared__ uint32_t s_min[4];
+    const uint64_t kr = rkeys[0];
+    const uint32_t tr = (uint32_t)(kr & 0xffu);
+    uint32_t best = 255;
+    // grid-stride (at most 512 blocks): at most one memory-side atomic per block
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         // key0 = 7 bytes big-endian << 8 | min(len, 8): the first 7 bytes come from the keys
-        const uint64_t k = keys[i], kr = rkeys[0];
+        const uint64_t k = keys[i];
         const uint64_t x = (k ^ kr) >> 8;
-        const uint32_t tk = (uint32_t)(k & 0xffu), tr = (uint32_t)(kr & 0xffu);
+        const uint32_t tk = (uint32_t)(k & 0xffu);
+        uint32_t l;
         if (x) {
-            l = (uint32_t)__builtin_clzll(x << 8) >> 3;
-            l = min(l, min(tk, tr));
+            l = min((uint32_t)__builtin_clzll(x << 8) >> 3, min(tk, tr));
         } else if (tk < 8u || tr < 8u) {
             l = min(tk, tr);
         } else {
             // both share their first 7 bytes (URL schemes): 8 bytes per step from byte 7
             const uint2 xs = spans[i], r = rspans[0];
-            const uint32_t m = min(min(xs.y - xs.x, r.y - r.x), 255u);
+            const uint32_t m = min(min(xs.y - xs.x, r.y - r.x), best);
             l = 7;
             while (l < m) {
                 const uint32_t t = (m - l) < 8u ? (m - l) : 8u;
@@ -605,10 +608,17 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
             }
             l = min(l, m);
         }
+        best = min(best, l);
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) l = min(l, (uint32_t)__shfl_xor((int)l, o, 64));
-    if (lane_id() == 0 && l < 255u) atomicMin(out, l);
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    if (lane_id() == 0) s_min[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
+        // skip the memory-side atomic when an earlier block already published as small a prefix
+        if (b < 255u && b < __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(out, b);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_rekey(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, uint32_t n,
@@ -920,10 +930,12 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint2 *rsp = ref_cur ? Lc.spans : (have_prior ? Lp.spans : nullptr);
     const uint64_t *rkeys = ref_cur ? Lc.keys : (have_prior ? Lp.keys : nullptr);
     if (rsp && Lc.n_rec)
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, grid_for(Lc.n_rec, 256), 256, 0, d_cur, Lc.spans, Lc.keys, Lc.n_rec,
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 512u), 256, 0, d_cur,
+                    Lc.spans, Lc.keys, Lc.n_rec,
                     rbuf, rsp, rkeys, dflag + 1);
     if (rsp && have_prior && Lp.n_rec)
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, grid_for(Lp.n_rec, 256), 256, 0, d_prior, Lp.spans, Lp.keys, Lp.n_rec,
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 512u), 256, 0, d_prior,
+                    Lp.spans, Lp.keys, Lp.n_rec,
                     rbuf, rsp, rkeys, dflag + 1);
     uint32_t fl[2] = {0u, 0u};
     SG_TRY(ctx_readback(c, fl, dflag, 8));
