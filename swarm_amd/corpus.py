@@ -503,3 +503,29 @@ def prior_ids(ids: np.ndarray) -> np.ndarray:
     """The prior scan's ids: this scan's distinct ids except those divisible by 10."""
     u = np.unique(ids)
     return u[(u % np.uint64(10)) != 0]
+
+
+def generic_regexes(pats, probe_banners: int = 400, max_frac: float = 0.1, seed: int = 17) -> list:
+    """Indices of the regexes that fire on more than `max_frac` of banners from UNKNOWN products
+    (a deterministic probe): extractor-style patterns such as
+    `([a-zA-Z0-9.-]+).([a-z0-9]+).([a-z0-9]+).\\w+` that say nothing about a service. A service
+    fingerprint set (nmap-service-probes `match` lines) has none of them; C4 leaves them out
+    so that the fraction of banners matched reflects the known-product share."""
+    import re
+    probe = banner_pool(pool=probe_banners, match_frac=0.0, seed=seed)
+    out = []
+    for i, p in enumerate(pats):
+        try:
+            c = re.compile(p)
+        except re.error:
+            continue
+        if sum(1 for b in probe if c.search(b)) > max_frac * len(probe):
+            out.append(i)
+    return out
+
+
+def c4_signatures(corpus_regexes) -> tuple:
+    """(C4 signature list, number of corpus regexes left out as generic): the nuclei corpus
+    regexes minus generic_regexes(), plus the nmap-style families."""
+    gen = set(generic_regexes(corpus_regexes))
+    return [p for i, p in enumerate(corpus_regexes) if i not in gen] + nmap_signatures(), len(gen)

@@ -1156,8 +1156,17 @@ __device__ __forceinline__ bool verify_one(const VerifyArgs &a, unsigned long lo
     return hit;
 }
 
+// Blocks are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its own
+// L2. Candidates are sorted by pattern, so giving XCD g the g-th contiguous eighth of them
+// confines each XCD to ~1/8 of the verify automata: their rows stay in that XCD's L2 instead of
+// every XCD streaming every automaton (MI355X_MICROARCH.md: XCD-aware block mapping).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+    const uint32_t g = b & 7u, j = b >> 3, q = nb >> 3, r = nb & 7u;
+    return g * q + (g < r ? g : r) + j;
+}
+
 __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     bool hit = false;
     unsigned long long cd = 0;
     if (i < a.n_cand) {
