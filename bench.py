@@ -190,22 +190,40 @@ def bench_c4(args):
     import swarm_amd
     from swarm_amd import corpus
 
-    torch.cuda.set_device(0)
+    import torch.distributed as dist
+    from swarm_amd import distributed as D
+
+    world, rank, local = dist_setup(args)
+    if world > 1:
+        local = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        dist.init_process_group(args.dist_backend)
+    else:
+        torch.cuda.set_device(0)
     sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
     pats, n_generic = corpus.c4_signatures([base64.b64decode(r["p"]) for r in sig["regexes"]])
     n_lines = args.lines if args.lines != 10_000_000 else 12_500_000
     pool = corpus.banner_pool()
-    buf = corpus.lines_from_pool(pool, n_lines, seed=3)
+    buf = corpus.lines_from_pool(pool, n_lines, seed=3 + rank)  # rank r's contiguous input shard
     d = torch.from_numpy(buf).cuda()
-    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    ctx = swarm_amd.Context(local, torch.cuda.current_stream().cuda_stream)
     tc0 = time.perf_counter()
-    m = swarm_amd.Matcher(pats, "regex")
+    m = swarm_amd.Matcher(pats, "regex")  # replicated automata
     compile_s = time.perf_counter() - tc0
-    run = lambda: m.dev_match(ctx, d.data_ptr(), d.numel())  # noqa: E731
-    el, full, stats, dominant, r = timed_steps(ctx, run, args)
+    tot = {}
+
+    def run():
+        r, tot["g"] = D.match_step(ctx, m, d)
+        return r
+    el, full, stats, dominant, r = timed_steps(ctx, run, args, barrier=dist.barrier if world > 1 else None)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=d.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    g_rec, g_hits, g_matched = tot["g"]
     R = int(r.in_records)
     cpu = None
-    if not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import semantics as S
         m_s = 1000
         cut = int(np.flatnonzero(buf == 10)[m_s - 1]) + 1
@@ -217,8 +235,9 @@ def bench_c4(args):
                "sample": "%d C4 banners x %d regexes, oracle re.search, 1 thread, %.2f s" % (m_s, len(pats), tc),
                "host_cpus": os.cpu_count()}
         cpu["gpu_hits_bit_exact_on_sample"] = (m.match(sample) == hits)
-    print(json.dumps({
-        "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
+    if rank == 0:
+        print(json.dumps({
+        "metric": METRIC, "value": round(g_rec * args.steps / el, 1), "unit": "records/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (nmap-style port banners, ~30 % from known products, SURVEY.md §8(d) C4)",
@@ -226,17 +245,21 @@ def bench_c4(args):
                                % (n_lines / 1e6, len(pats)),
                    "generic_regexes_left_out": n_generic,
                    "bytes": int(d.numel()), "automaton_states": m.info()["states"],
-                   "compile_s": round(compile_s, 2)},
-        "gbps": round(d.numel() * args.steps / el / 1e9, 2),
-        "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records),
-                    "matched_frac": round(int(r.matched_records) / max(R, 1), 4)},
+                   "compile_s": round(compile_s, 2),
+                   "parallelism": ("replicated automata, contiguous input shards, count all-reduce x%d" % world)
+                                  if world > 1 else "single GPU"},
+        "gbps": round(d.numel() * world * args.steps / el / 1e9, 2),
+        "records": {"in": g_rec, "hits": g_hits, "matched": g_matched,
+                    "matched_frac": round(g_matched / max(g_rec, 1), 4)},
         "roofline": roofline_of(stats, dominant, "c4", full),
         "cpu_baseline": cpu,
         "kernels": kernel_table(full),
         "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
                         "HIP events only around the dominant kernel",
-    }), flush=True)
+        }), flush=True)
     ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def field_templates():
@@ -322,11 +345,13 @@ def bench_c5(args):
     a prior scan at 90 % overlap, strong scaling over N ranks. Records are rendered on the
     GPU: 64M hosts x 4 open-port slots (ports from 32 common ones) = 256M distinct combos,
     1B draws (~4 copies each). Each rank routes
-    its draw by key0 ranges agreed across ranks (RCCL all-to-all when N > 1), then processes
+    its draw by byte ranges agreed across ranks (RCCL all-to-all when N > 1), then processes
     its range in local range parts of < 4 GiB (swarm_amd.sharded); rank outputs concatenated
     in rank order are the global sort -u / comm -13 output. Setup (untimed): the prior scan
     = sort -u of another 1B draw over combos shifted by 10 %, routed to its owner ranks, and
-    the splitters (from the prior's key0 samples, known before the scan)."""
+    the splitters (byte quantiles of the prior's sampled records, known before the scan).
+    --c5-data ips: 10.x.y.z:port records (every record shares '10.', most their first 7
+    bytes), the case key0 routing could not divide."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -346,18 +371,23 @@ def bench_c5(args):
     dev = torch.device("cuda", local)
     total = args.lines if args.lines != 10_000_000 else 1_000_000_000
     per = total // world
-    n_hosts = args.c5_hosts
-    K = 4  # open-port slots per host (ports drawn from 32 common ports)
+    if args.c5_data == "ips":
+        # 10.x.y.z:port from an internal-range scan: 16M hosts x 16 open-port slots
+        n_hosts = min(args.c5_hosts, 1 << 24) if args.c5_hosts != 64_000_000 else 15_000_000
+        K = 16
+        pool = corpus.ip_pool_torch(n_hosts + n_hosts // 10 + 1, seed=5, device=dev)
+    else:
+        n_hosts = args.c5_hosts
+        K = 4  # open-port slots per host (ports drawn from 32 common ports)
+        pool = corpus.host_pool_torch(n_hosts + n_hosts // 10 + 1, seed=5, device=dev)
     U = n_hosts * K
-    pool = corpus.host_pool_torch(n_hosts + n_hosts // 10 + 1, seed=5, device=dev)
     ctx = swarm_amd.Context(local, torch.cuda.current_stream(dev).cuda_stream)
     t_setup = time.perf_counter()
     prior_raw = corpus.hostport_pieces(pool, per, U // 10, U + U // 10, seed=900 + rank, ports_per_host=K)
-    gsplit = D.agree_splitters(ctx, prior_raw, world) if world > 1 else np.zeros(0, dtype=np.uint64)
+    gsplit = D.agree_splitters(ctx, prior_raw, world) if world > 1 else []
     mine = D.range_exchange(ctx, prior_raw, gsplit) if world > 1 else prior_raw
     parts = sharded.plan_parts(mine, [], 2 << 30)
-    lsplit = sharded.choose_splitters(np.concatenate(
-        [ctx.key_sample(p.data_ptr(), p.numel(), 1 << 14)[0] for p in mine]), parts)
+    lsplit = sharded.choose_splitters(sharded.sample_records(ctx, mine), parts)
     pu, _, _ = sharded.dedup_diff_large(ctx, mine, (), splitters=lsplit)
     del prior_raw, mine
     prior_local = sharded.split_at_newlines(pu, 3 << 30)
@@ -428,11 +458,18 @@ def bench_c5(args):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (host:port records rendered on the GPU, SURVEY.md §8(d) C5)",
-            "config": {"workload": "C5: %dM host:port records (%.1f GB on rank 0) + prior at 90%% overlap, "
-                                   "key0-range sharded over %d GPU(s)" % (total // 1_000_000, cur_bytes / 1e9, world),
-                       "records_total": total, "prior_bytes_rank0": int(prior_bytes), "local_parts": int(lsplit.size + 1),
+            "config": {"workload": "C5: %dM %s records (%.1f GB on rank 0) + prior at 90%% overlap, "
+                                   "byte-range sharded over %d GPU(s)" % (
+                                       total // 1_000_000, "10.x.y.z:port" if args.c5_data == "ips" else "host:port",
+                                       cur_bytes / 1e9, world),
+                       "records_total": total, "hosts": n_hosts, "ports_per_host": K,
+                       "prior_bytes_rank0": int(prior_bytes), "local_parts": len(lsplit) + 1,
+                       "part_balance_max_over_mean": round(max(st["part_bytes"]) * len(st["part_bytes"])
+                                                           / max(1, sum(st["part_bytes"])), 3)
+                                                     if st["part_bytes"] else None,
+                       "rerouted_parts": st["rerouted_parts"],
                        "setup_s": round(t_setup, 1),
-                       "parallelism": "key0-range all-to-all x%d" % world if world > 1 else "single GPU"},
+                       "parallelism": "byte-range all-to-all x%d" % world if world > 1 else "single GPU"},
             "gbps": round((cur_bytes + prior_bytes + ub + fb) * world * args.steps / el / 1e9, 2),
             "records": {"in_rank0": st["in_records"], "unique_rank0": st["uniq_records"],
                         "new_rank0": st["fresh_records"], "max_part_bytes": st["max_part_bytes"]},
@@ -736,8 +773,12 @@ def main():
     ap.add_argument("--gnu-lines", type=int, default=2_000_000, help="lines of the GNU-tool CPU baseline sample")
     ap.add_argument("--no-x1", action="store_true", help="default run: skip the fused X1 leg")
     ap.add_argument("--c5-hosts", type=int, default=64_000_000, help="C5 hosts (x 4 open-port slots = combos)")
+    ap.add_argument("--c5-data", choices=["hosts", "ips"], default="hosts",
+                    help="C5 records: host:port names, or 10.x.y.z:port (15M hosts x 16 port slots)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real runs; gloo rehearses N ranks on fewer GPUs")
+    ap.add_argument("--route", choices=["range", "hash"], default="range",
+                    help="C2 N>1 record routing: byte ranges (outputs in global byte order) or hash parts")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--launcher-check", action="store_true", help=argparse.SUPPRESS)
@@ -787,8 +828,15 @@ def main():
     else:
         from swarm_amd import distributed as D
         u = np.unique(ids)
-        cand = corpus._flatten(*corpus.render_names(u[(u % np.uint64(10)) != 0]))
-        prior = D.build_prior_partition(ctx, torch.from_numpy(cand).to(dev))
+        cand = torch.from_numpy(corpus._flatten(*corpus.render_names(u[(u % np.uint64(10)) != 0]))).to(dev)
+        if args.route == "range":
+            # splitters from every rank's prior record samples: rank r owns byte range r of the
+            # prior AND of every later scan, so the rank outputs concatenate into global order
+            gsplit = D.agree_splitters(ctx, [cand], world)
+            prior = D.build_prior_range(ctx, cand, gsplit)
+        else:
+            prior = D.build_prior_partition(ctx, cand)
+        del cand
         prior_np = None
     torch.cuda.synchronize()
 
@@ -796,7 +844,10 @@ def main():
         if world == 1:
             return ctx.dedup_diff(cur.data_ptr(), cur.numel(), prior.data_ptr(), prior.numel()), cur.numel()
         from swarm_amd import distributed as D
-        r, recv = D.dedup_diff_step(ctx, cur, prior)
+        if args.route == "range":
+            r, recv = D.dedup_diff_range_shard(ctx, cur, prior, gsplit)
+        else:
+            r, recv = D.dedup_diff_step(ctx, cur, prior)
         return r, recv.numel()
 
     for _ in range(args.warmup):
@@ -894,7 +945,9 @@ def main():
                                    % (n_lines // 1_000_000),
                        "lines_per_gpu": n_lines, "bytes_per_gpu": cur_bytes,
                        "prior_bytes": prior_bytes,
-                       "parallelism": "hash-partition all-to-all x%d" % world if world > 1 else "single GPU"},
+                       "parallelism": ("%s all-to-all x%d" % ("byte-range (global byte order)" if args.route == "range"
+                                                              else "hash-partition", world))
+                                      if world > 1 else "single GPU"},
             "gbps": round(step_bytes * world * args.steps / elapsed / 1e9, 2),
             "hbm_frac_step": round(step_bytes * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4),
             "records": {"in": info["R"], "unique": info["U"], "new": info["F"], "prior": info["Rp"]},

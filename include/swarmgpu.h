@@ -145,6 +145,23 @@ int sg_dev_partition_range(sg_ctx *ctx, const uint8_t *d_buf, size_t n, const ui
  * choosing splitters; *n_rec = the buffer's record count. */
 int sg_dev_key_sample(sg_ctx *ctx, const uint8_t *d_buf, size_t n, uint32_t m, uint64_t *keys,
                       uint64_t *n_rec);
+/* Range routing by byte-string splitters: part(record) = number of splitters <= record in
+ * bytewise order (a shorter string that is a prefix of a longer one sorts first, as in sort).
+ * Splitter q is splitters[split_offs[q] .. split_offs[q+1]) (n_parts entries in split_offs),
+ * cut to its first SG_SPLIT_BYTES bytes; the cut splitters must be non-decreasing. Equal
+ * records share a part and every record of part p sorts below every record of part p+1, so
+ * the per-part sort -u outputs concatenated in part order are the global sort -u output;
+ * unlike key0 splitters, byte splitters divide runs of records sharing their first 7 bytes
+ * (https://..., 10.0.x.y:port). Same output layout as sg_dev_partition. */
+#define SG_SPLIT_BYTES 64
+int sg_dev_partition_bytes(sg_ctx *ctx, const uint8_t *d_buf, size_t n, const uint8_t *splitters,
+                           const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out, size_t out_cap,
+                           uint64_t *part_bytes, uint64_t *part_records);
+/* m evenly spaced records' first SG_SPLIT_BYTES bytes (heads: m x SG_SPLIT_BYTES host bytes,
+ * zero-filled) and min(len, SG_SPLIT_BYTES) (lens), for choosing byte splitters; nothing is
+ * written when the buffer has no records; *n_rec = the buffer's record count. */
+int sg_dev_record_sample(sg_ctx *ctx, const uint8_t *d_buf, size_t n, uint32_t m, uint8_t *heads,
+                         uint32_t *lens, uint64_t *n_rec);
 /* The record hash used by sg_dev_partition, on one host record (for tests/oracles). */
 uint64_t sg_hash64(const uint8_t *rec, size_t len);
 

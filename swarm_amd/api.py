@@ -239,6 +239,7 @@ def device_count() -> int:
     return n.value
 
 
+SPLIT_BYTES = 64  # include/swarmgpu.h SG_SPLIT_BYTES
 _SHARED = {}
 
 
@@ -367,6 +368,31 @@ class Context:
         check(lib.sg_dev_partition_range(self._h, C.c_void_p(d_buf), n, arr, parts, C.c_void_p(d_out), out_cap,
                                          pb, pr))
         return list(pb), list(pr)
+
+    def partition_bytes(self, d_buf: int, n: int, splitters: Sequence[bytes], d_out: int, out_cap: int):
+        """Order-preserving routing by byte-string splitters (len(splitters) + 1 parts, each
+        splitter cut to SPLIT_BYTES); same output layout as partition(). Returns (bytes per
+        part, records per part)."""
+        blob, offs = _keys_blob(list(splitters))
+        parts = len(splitters) + 1
+        pb = (C.c_uint64 * parts)()
+        pr = (C.c_uint64 * parts)()
+        check(lib.sg_dev_partition_bytes(self._h, C.c_void_p(d_buf), n, blob.ctypes.data,
+                                         offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts, C.c_void_p(d_out),
+                                         out_cap, pb, pr))
+        return list(pb), list(pr)
+
+    def record_sample(self, d_buf: int, n: int, m: int) -> Tuple[List[bytes], int]:
+        """(the first SPLIT_BYTES bytes of m evenly spaced records — [] when the buffer has
+        no records —, record count)."""
+        heads = np.zeros((max(1, m), SPLIT_BYTES), dtype=np.uint8)
+        lens = np.zeros(max(1, m), dtype=np.uint32)
+        nr = C.c_uint64()
+        check(lib.sg_dev_record_sample(self._h, C.c_void_p(d_buf), n, m, heads.ctypes.data,
+                                       lens.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(nr)))
+        if nr.value == 0:
+            return [], 0
+        return [heads[k, :lens[k]].tobytes() for k in range(m)], nr.value
 
     def key_sample(self, d_buf: int, n: int, m: int):
         """(m evenly spaced records' key0 values as uint64 (all ~0 if empty), record count)."""

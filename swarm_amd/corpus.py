@@ -423,6 +423,39 @@ def host_pool_torch(n_hosts: int, seed: int = 5, device="cuda", chunk: int = 1 <
     return torch.cat(mats), torch.cat(lens)
 
 
+def ip_pool_torch(n_hosts: int, seed: int = 5, device="cuda", chunk: int = 1 << 23):
+    """n_hosts (<= 2**26) distinct IPv4 addresses rendered on the GPU — all in 10.0.0.0/8
+    when n_hosts <= 2**24 (an internal-range port scan: every record shares its first 3
+    bytes and many their first 7), else 10.x.y.z .. 13.x.y.z — left-aligned: (matrix (n, 15)
+    uint8, lengths). Host h -> address (h * odd + seed) mod 2**bits above 10.0.0.0, a
+    bijection, so hosts never collide."""
+    import torch
+    if n_hosts > 1 << 26:
+        raise ValueError("ip_pool_torch: at most 2**26 hosts")
+    bits = 24 if n_hosts <= 1 << 24 else 26
+    mats, lens = [], []
+    for i in range(0, n_hosts, chunk):
+        ids = torch.arange(i, min(n_hosts, i + chunk), dtype=torch.int64, device=device)
+        x = (ids * 0x2F0B3A5 + seed) & ((1 << bits) - 1)
+        octs = [10 + (x >> 24), (x >> 16) & 255, (x >> 8) & 255, x & 255]
+        m = ids.numel()
+        row = torch.zeros((m, 15), dtype=torch.uint8, device=device)
+        msk = torch.zeros((m, 15), dtype=torch.bool, device=device)
+        col = 0
+        for k, o in enumerate(octs):
+            row[:, col], msk[:, col] = (48 + o // 100).to(torch.uint8), o >= 100
+            row[:, col + 1], msk[:, col + 1] = (48 + (o // 10) % 10).to(torch.uint8), o >= 10
+            row[:, col + 2], msk[:, col + 2] = (48 + o % 10).to(torch.uint8), True
+            col += 3
+            if k < 3:
+                row[:, col], msk[:, col] = 46, True
+                col += 1
+        order = torch.sort((~msk).to(torch.uint8), dim=1, stable=True).indices
+        mats.append(torch.gather(row, 1, order))
+        lens.append(msk.sum(1).to(torch.int32))
+    return torch.cat(mats), torch.cat(lens)
+
+
 def hostport_pieces(pool, n: int, lo: int, hi: int, seed: int, per_piece: int = 50_000_000,
                     ports_per_host: int | None = None):
     """n 'host:port' records ('\\n'-terminated) for combo ids drawn uniformly from [lo, hi),
@@ -443,6 +476,8 @@ def hostport_pieces(pool, n: int, lo: int, hi: int, seed: int, per_piece: int = 
         pl[i] = len(b)
     pm, pl = pm.to(dev), pl.to(dev)
     W = mat.shape[1]
+    if (hi - 1) // K >= mat.shape[0]:  # host ids index the pool on the GPU: check here
+        raise ValueError("combo ids up to %d need %d hosts; the pool has %d" % (hi - 1, (hi - 1) // K + 1, mat.shape[0]))
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     out = []

@@ -147,6 +147,91 @@ __global__ __launch_bounds__(256) void k_range_keys(const uint64_t *__restrict__
     }
 }
 
+// Byte-string splitters (SG_SPLIT_BYTES = 64 bytes each at most): part(record) = number of
+// splitters <= record in bytewise order (shorter-is-smaller). Unlike a key0 splitter, a
+// byte splitter can fall inside a run of records sharing their first 7 bytes (https://...,
+// 10.0.x.y:port), so range parts stay balanced on URL and IP data. Both sides are compared
+// as 8 big-endian words of their first 64 bytes (zero past the end), then by length: words
+// differ => the first differing word decides; all equal => one is a prefix of the other
+// within 64 bytes (or they are equal there) and the longer one is larger, which is exact
+// because a splitter never has more than 64 bytes.
+constexpr uint32_t SPL_W = 64, SPL_WORDS = SPL_W / 8;
+
+__device__ __forceinline__ void head_words(const uint8_t *__restrict__ buf, uint32_t s, uint32_t e,
+                                           uint64_t (&w)[SPL_WORDS]) {
+    const uint32_t len = e - s;
+#pragma unroll
+    for (uint32_t k = 0; k < SPL_WORDS; ++k) {
+        const uint32_t o = 8u * k;
+        w[k] = o < len ? load_le(buf, s + o, min(len - o, 8u)) : 0ull;
+    }
+}
+
+// record < splitter (BE words in LDS)
+__device__ __forceinline__ bool head_less(const uint64_t (&w)[SPL_WORDS], uint32_t len, const uint64_t *sw,
+                                          uint32_t slen) {
+    int r = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SPL_WORDS; ++k) {
+        if (r == 0) {
+            const uint64_t a = w[k], b = sw[k];
+            if (a != b) r = a < b ? -1 : 1;
+        }
+    }
+    return r ? r < 0 : len < slen;
+}
+
+__global__ __launch_bounds__(256) void k_range_bytes(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
+                                                     uint32_t R, const uint64_t *__restrict__ split_w,
+                                                     const uint32_t *__restrict__ split_len, uint32_t ns,
+                                                     uint64_t *keys, unsigned long long *cnt /* [2*parts] */) {
+    __shared__ unsigned long long s_c[2 * 256];
+    __shared__ uint64_t s_w[255 * SPL_WORDS];
+    __shared__ uint32_t s_len[256];
+    for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) s_c[i] = 0;
+    for (uint32_t i = threadIdx.x; i < ns * SPL_WORDS; i += blockDim.x) s_w[i] = split_w[i];
+    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) s_len[i] = split_len[i];
+    __syncthreads();
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < R; i0 += gridDim.x * blockDim.x) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint32_t lo = 0, bytes = 0;
+        if (i < R) {
+            const uint2 x = spans[i];
+            uint64_t w[SPL_WORDS];
+            head_words(buf, x.x, x.y, w);
+#pragma unroll
+            for (uint32_t k = 0; k < SPL_WORDS; ++k) w[k] = __builtin_bswap64(w[k]);
+            uint32_t hi = ns;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (!head_less(w, x.y - x.x, s_w + mid * SPL_WORDS, s_len[mid])) lo = mid + 1; else hi = mid;
+            }
+            keys[i] = lo;
+            bytes = x.y - x.x + 1;
+        }
+        wave_count(s_c, 256, i < R, lo, bytes);
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q <= ns; q += blockDim.x) {
+        if (s_c[q]) atomicAdd(&cnt[q], s_c[q]);
+        if (s_c[256 + q]) atomicAdd(&cnt[ns + 1 + q], s_c[256 + q]);
+    }
+}
+
+// m evenly spaced records' first 64 bytes (zero-filled) and min(len, 64).
+__global__ __launch_bounds__(256) void k_head_sample(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
+                                                     uint32_t R, uint32_t m, uint64_t *__restrict__ heads,
+                                                     uint32_t *__restrict__ lens) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint2 x = spans[(uint32_t)(((uint64_t)k * R) / m)];
+    uint64_t w[SPL_WORDS];
+    head_words(buf, x.x, x.y, w);
+#pragma unroll
+    for (uint32_t j = 0; j < SPL_WORDS; ++j) heads[(size_t)k * SPL_WORDS + j] = w[j];
+    lens[k] = min(x.y - x.x, SPL_W);
+}
+
 __global__ __launch_bounds__(256) void k_key_sample(const uint64_t *__restrict__ key0, uint32_t R, uint32_t m,
                                                     uint64_t *__restrict__ out) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -221,9 +306,17 @@ static int host_dedup_diff(const uint8_t *const *chunks, const size_t *lens, siz
     return SG_OK;
 }
 
-// Hash routing (split == null) or range routing by key0 splitters (parts - 1 of them).
+// Byte splitters packed for k_range_bytes: BE words of the first 64 bytes + lengths.
+struct ByteSplit {
+    uint64_t w[255 * SPL_WORDS];
+    uint32_t len[256];
+};
+
+// Hash routing (split == null), range routing by key0 splitters, or by byte splitters
+// (bsplit) — parts - 1 of them.
 int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, uint8_t *d_out,
-                  size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, const uint64_t *split = nullptr) {
+                  size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, const uint64_t *split = nullptr,
+                  const ByteSplit *bsplit = nullptr) {
     if (parts == 0 || parts > 256) { set_error("n_parts must be in 1..256"); return SG_E_INVAL; }
     if (split)
         for (uint32_t q = 1; q + 1 < parts; ++q)
@@ -240,7 +333,13 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
     SG_TRY(slot(c, S_R_KEY2, R, &keys2));
     SG_TRY(slot(c, S_VALS, R, &v1));
     SG_TRY(slot(c, S_VALS2, R, &v2));
-    if (R && !split) {
+    if (R && bsplit) {
+        uint64_t *d_w;
+        SG_TRY(slot(c, S_M_TMP2, sizeof(ByteSplit) / 8, &d_w));
+        SG_HIP(hipMemcpyAsync(d_w, bsplit, sizeof(ByteSplit), hipMemcpyHostToDevice, c->stream));
+        SG_LAUNCH_B(c, "range_bytes", 24.0 * R, k_range_bytes, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, d_buf,
+                    L.spans, R, d_w, reinterpret_cast<const uint32_t *>(d_w + 255 * SPL_WORDS), parts - 1, keys, cnt);
+    } else if (R && !split) {
         SG_LAUNCH(c, "part_keys", k_part_keys, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, d_buf, L.spans, R,
                   parts, keys, cnt);
     } else if (R) {
@@ -344,6 +443,70 @@ int sg_dev_partition_range(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint
     SG_TRY(aligned_in(c, S_IN, d_buf, n, &b));
     static const uint64_t none = 0;
     return dev_partition(c, b, n, n_parts, d_out, out_cap, part_bytes, part_records, n_parts > 1 ? splitters : &none);
+}
+
+int sg_dev_partition_bytes(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint8_t *splitters,
+                           const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out, size_t out_cap,
+                           uint64_t *part_bytes, uint64_t *part_records) {
+    if (!c || (!d_out && n) || (!d_buf && n) || ((!splitters || !split_offs) && n_parts > 1)) {
+        set_error("sg_dev_partition_bytes: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (n_parts == 0 || n_parts > 256) { set_error("n_parts must be in 1..256"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    static thread_local ByteSplit bs;
+    memset(&bs, 0, sizeof(bs));
+    for (uint32_t q = 0; q + 1 < n_parts; ++q) {
+        if (split_offs[q + 1] < split_offs[q]) { set_error("split_offs must be non-decreasing"); return SG_E_INVAL; }
+        const uint32_t len = std::min<uint32_t>(split_offs[q + 1] - split_offs[q], SPL_W);
+        uint8_t b[SPL_W] = {0};
+        memcpy(b, splitters + split_offs[q], len);
+        for (uint32_t k = 0; k < SPL_WORDS; ++k) {
+            uint64_t v = 0;
+            for (uint32_t j = 0; j < 8; ++j) v = (v << 8) | b[8 * k + j];
+            bs.w[q * SPL_WORDS + k] = v;
+        }
+        bs.len[q] = len;
+        if (q > 0) {  // (cut) splitters must be non-decreasing in byte order
+            const uint64_t *a = bs.w + (q - 1) * SPL_WORDS, *w = bs.w + q * SPL_WORDS;
+            int r = 0;
+            for (uint32_t k = 0; k < SPL_WORDS && !r; ++k)
+                if (a[k] != w[k]) r = a[k] < w[k] ? -1 : 1;
+            if (r > 0 || (r == 0 && bs.len[q - 1] > len)) {
+                set_error("splitters must be non-decreasing in byte order (splitter %u)", q);
+                return SG_E_INVAL;
+            }
+        }
+    }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b;
+    SG_TRY(aligned_in(c, S_IN, d_buf, n, &b));
+    return dev_partition(c, b, n, n_parts, d_out, out_cap, part_bytes, part_records, nullptr, &bs);
+}
+
+int sg_dev_record_sample(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t m, uint8_t *heads, uint32_t *lens,
+                         uint64_t *n_rec) {
+    if (!c || (!heads && m) || (!lens && m) || (!d_buf && n)) {
+        set_error("sg_dev_record_sample: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *b;
+    SG_TRY(aligned_in(c, S_IN, d_buf, n, &b));
+    Lines L;
+    SG_TRY(run_lines(c, b, n, CUR_SLOTS, &L));
+    if (n_rec) *n_rec = L.n_rec;
+    const uint32_t take = L.n_rec ? m : 0u;
+    if (take) {
+        uint64_t *d;
+        SG_TRY(slot(c, S_M_TMP2, (size_t)take * (SPL_WORDS + 1), &d));
+        uint32_t *dl = reinterpret_cast<uint32_t *>(d + (size_t)take * SPL_WORDS);
+        SG_LAUNCH(c, "head_sample", k_head_sample, (take + 255) / 256, 256, 0, b, L.spans, L.n_rec, take, d, dl);
+        SG_TRY(ctx_readback(c, heads, d, (size_t)take * SPL_W));
+        SG_TRY(ctx_readback(c, lens, dl, 4ull * take));
+    }
+    return SG_OK;
 }
 
 int sg_dev_key_sample(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t m, uint64_t *keys, uint64_t *n_rec) {

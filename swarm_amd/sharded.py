@@ -3,11 +3,14 @@ records, ~30 GB per scan) on one GPU, with the global sort -u byte order kept.
 
 One call of the library handles < 4 GiB (32-bit record offsets). A bigger shard arrives in
 pieces anyway (chunk files, S3 bodies); each piece is routed on the GPU into P parts by
-key0 splitters (sg_dev_partition_range): part p holds only records that sort below every
-record of part p+1, and equal records always share a part. Each part (< 4 GiB) is then
-deduped and diffed against the same part of the prior scan, and the part outputs
+byte-string splitters (sg_dev_partition_bytes): part p holds only records that sort below
+every record of part p+1, and equal records always share a part. Each part (< 4 GiB) is
+then deduped and diffed against the same part of the prior scan, and the part outputs
 concatenated in part order ARE the global sort -u / comm -13 output — no merge step.
-Splitters are quantiles of key0 samples taken from every piece (sg_dev_key_sample).
+Splitters are byte quantiles of records sampled from every piece (sg_dev_record_sample,
+first 64 bytes), so runs of records sharing a long prefix (https://..., 10.0.x.y:port) are
+divided too; a part that still ends up over the per-call limit is routed again with
+splitters sampled from that part alone.
 
 All buffers are torch uint8 tensors on the context's device; pieces must end at a record
 boundary (split_at_newlines cuts a long buffer that way).
@@ -20,20 +23,16 @@ import numpy as np
 
 PART_LIMIT = 0xFFFF0000  # bytes per library call (include/swarmgpu.h)
 RECORD_LIMIT = 1 << 30   # records per library call (sg_dedup.hip build_unique)
+SPLIT_BYTES = 64         # bytes of a splitter compared (include/swarmgpu.h SG_SPLIT_BYTES)
 
 
-def part_overflow_message(splitters: np.ndarray, b: int, cur_bytes: int, prior_bytes: int) -> str:
-    """Why range part b is over the per-call limit, and whether more parts can help: a part
-    whose two bounding splitters are equal is one key0 value (records sharing their first 7
-    bytes), which no number of parts can divide."""
-    lo = int(splitters[b - 1]) if b > 0 else None
-    hi = int(splitters[b]) if b < splitters.size else None
-    one_key = lo is not None and hi is not None and lo == hi
-    msg = "key0 range part %d holds %d cur / %d prior bytes (per-call limit %d bytes, %d records)" % (
-        b, cur_bytes, prior_bytes, PART_LIMIT, RECORD_LIMIT)
-    if one_key or (lo is not None and b + 1 < splitters.size and int(splitters[b + 1]) == lo):
-        return msg + ": its records share one key0 value %#x (first 7 bytes), which range routing cannot split" % lo
-    return msg + ": use more parts (smaller part_bytes)"
+def part_overflow_message(splitters, b: int, cur_bytes: int, prior_bytes: int) -> str:
+    """Why range part b is over the per-call limit after re-routing: its records share their
+    first SPLIT_BYTES bytes (every sampled splitter inside it is the same string), which no
+    number of parts can divide."""
+    return ("range part %d holds %d cur / %d prior bytes (per-call limit %d bytes, %d records) and its "
+            "records share their first %d bytes, which range routing cannot split"
+            % (b, cur_bytes, prior_bytes, PART_LIMIT, RECORD_LIMIT, SPLIT_BYTES))
 
 
 def split_at_newlines(buf, max_bytes: int = 3 << 30, window: int = 1 << 20) -> List:
@@ -57,8 +56,15 @@ def split_at_newlines(buf, max_bytes: int = 3 << 30, window: int = 1 << 20) -> L
     return out
 
 
-def choose_splitters(samples: np.ndarray, parts: int) -> np.ndarray:
-    """parts - 1 non-decreasing key0 quantiles of the samples (sentinels ~0 ignored)."""
+def choose_splitters(samples, parts: int):
+    """parts - 1 non-decreasing quantiles of the samples: byte strings (a list of bytes,
+    from sample_records) -> byte splitters; key0 values (uint64 array, sentinels ~0
+    ignored) -> key0 splitters."""
+    if isinstance(samples, (list, tuple)):
+        s = sorted(samples)
+        if parts <= 1 or not s:
+            return []
+        return [s[(k * len(s)) // parts] for k in range(1, parts)]
     s = np.sort(np.asarray(samples, dtype=np.uint64))
     s = s[s != np.uint64(0xFFFFFFFFFFFFFFFF)]
     if parts <= 1 or s.size == 0:
@@ -67,11 +73,33 @@ def choose_splitters(samples: np.ndarray, parts: int) -> np.ndarray:
     return s[idx]
 
 
-def route(ctx, pieces: Sequence, splitters: np.ndarray) -> List:
-    """Route every piece into len(splitters) + 1 parts; returns one device tensor per part
-    (the part's records from all pieces, in piece order)."""
+def sample_records(ctx, pieces: Sequence, per_piece: int = 1 << 12) -> List[bytes]:
+    """First SPLIT_BYTES bytes of per_piece evenly spaced records of every piece."""
+    out: List[bytes] = []
+    for p in pieces:
+        if p is not None and p.numel():
+            out += ctx.record_sample(p.data_ptr(), p.numel(), per_piece)[0]
+    return out
+
+
+def n_splitters(splitters) -> int:
+    return len(splitters) if isinstance(splitters, (list, tuple)) else int(np.asarray(splitters).size)
+
+
+def route_piece(ctx, p, splitters, out_ptr: int, out_cap: int):
+    """Route one piece into out (parts contiguous); returns bytes per part."""
+    if isinstance(splitters, (list, tuple)):
+        pb, _ = ctx.partition_bytes(p.data_ptr(), p.numel(), splitters, out_ptr, out_cap)
+    else:
+        pb, _ = ctx.partition_range(p.data_ptr(), p.numel(), splitters, out_ptr, out_cap)
+    return pb
+
+
+def route(ctx, pieces: Sequence, splitters) -> List:
+    """Route every piece into n_splitters + 1 parts; returns one device tensor per part
+    (the part's records from all pieces, in piece order; None for an empty part)."""
     import torch
-    parts = splitters.size + 1
+    parts = n_splitters(splitters) + 1
     lists: List[list] = [[] for _ in range(parts)]
     keep = []
     for p in pieces:
@@ -80,7 +108,7 @@ def route(ctx, pieces: Sequence, splitters: np.ndarray) -> List:
             continue
         out = torch.empty(n + 16, dtype=torch.uint8, device=p.device)
         ctx.fence_in()  # `out` may be a block torch's stream is still reading
-        pb, _ = ctx.partition_range(p.data_ptr(), n, splitters, out.data_ptr(), out.numel())
+        pb = route_piece(ctx, p, splitters, out.data_ptr(), out.numel())
         off = 0
         for b in range(parts):
             if pb[b]:
@@ -114,44 +142,60 @@ def plan_parts(cur_pieces: Sequence, prior_pieces: Sequence, part_bytes: int) ->
 
 
 def dedup_diff_large(ctx, cur_pieces: Sequence, prior_pieces: Sequence = (), part_bytes: int = 2 << 30,
-                     samples_per_piece: int = 1 << 14, splitters: np.ndarray | None = None):
+                     samples_per_piece: int = 1 << 12, splitters=None):
     """(sort -u of all cur records, new records vs prior, stats) as device tensors, each in
     global byte order, for shards of any size. `prior_pieces` is the prior scan (sorted
-    unique or not). `splitters` may be given (e.g. agreed across ranks); otherwise they are
-    chosen from key0 samples of every piece."""
+    unique or not). `splitters` may be given (byte strings or key0 values, e.g. agreed
+    across ranks); otherwise byte splitters are chosen from records sampled from every
+    piece."""
     import torch
     cur_pieces = [p for p in cur_pieces if p.numel()]
     prior_pieces = [p for p in prior_pieces if p.numel()]
     dev = cur_pieces[0].device if cur_pieces else torch.device("cuda", ctx.device)
     if splitters is None:
         parts = plan_parts(cur_pieces, prior_pieces, part_bytes)
-        samples = [ctx.key_sample(p.data_ptr(), p.numel(), samples_per_piece)[0] for p in cur_pieces + prior_pieces]
-        splitters = choose_splitters(np.concatenate(samples) if samples else np.zeros(0, np.uint64), parts)
-    cur_parts = route(ctx, cur_pieces, splitters)
-    prior_parts = route(ctx, prior_pieces, splitters) if prior_pieces else [None] * (splitters.size + 1)
+        splitters = choose_splitters(sample_records(ctx, cur_pieces + prior_pieces, samples_per_piece), parts)
+    st = {"parts": n_splitters(splitters) + 1, "in_records": 0, "uniq_records": 0, "fresh_records": 0,
+          "max_part_bytes": 0, "rerouted_parts": 0, "part_bytes": []}
     uniq, fresh = [], []
-    st = {"parts": splitters.size + 1, "in_records": 0, "uniq_records": 0, "fresh_records": 0,
-          "max_part_bytes": 0}
+    _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, dev, uniq, fresh, st, samples_per_piece)
+    empty = torch.empty(0, dtype=torch.uint8, device=dev)
+    return (torch.cat(uniq) if uniq else empty), (torch.cat(fresh) if fresh else empty), st
+
+
+def _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, dev, uniq, fresh, st, samples_per_piece,
+                 depth: int = 0):
+    cur_parts = route(ctx, cur_pieces, splitters)
+    prior_parts = route(ctx, prior_pieces, splitters) if prior_pieces else [None] * (n_splitters(splitters) + 1)
     for b, (c, p) in enumerate(zip(cur_parts, prior_parts)):
         if c is None:
             continue
-        if c.numel() > PART_LIMIT or (p is not None and p.numel() > PART_LIMIT):
-            raise ValueError(part_overflow_message(splitters, b, c.numel(), p.numel() if p is not None else 0))
+        pn = p.numel() if p is not None else 0
+        if c.numel() > PART_LIMIT or pn > PART_LIMIT:
+            # route this part again with splitters sampled from it alone
+            big = max(c.numel(), pn)
+            sub_parts = int(min(256, max(2, -(-int(big * 1.25) // (PART_LIMIT // 2)))))
+            sub = choose_splitters(sample_records(ctx, [c] + ([p] if p is not None else []), samples_per_piece),
+                                   sub_parts)
+            if depth >= 3 or not sub:
+                raise ValueError(part_overflow_message(splitters, b, c.numel(), pn))
+            st["rerouted_parts"] += 1
+            _dedup_parts(ctx, [c], [p] if p is not None else [], sub, dev, uniq, fresh, st,
+                         samples_per_piece, depth + 1)
+            continue
         st["max_part_bytes"] = max(st["max_part_bytes"], c.numel())
+        st["part_bytes"].append(int(c.numel()))
         ctx.fence_in()
         try:
-            r = ctx.dedup_diff(c.data_ptr(), c.numel(), p.data_ptr() if p is not None else 0,
-                               p.numel() if p is not None else 0)
+            r = ctx.dedup_diff(c.data_ptr(), c.numel(), p.data_ptr() if p is not None else 0, pn)
         except Exception as e:
             raise type(e)(e.rc, "%s (part of %d bytes at %#x, prior %s)" % (
-                e, c.numel(), c.data_ptr(), None if p is None else p.numel())) if hasattr(e, "rc") else e
+                e, c.numel(), c.data_ptr(), None if p is None else pn)) if hasattr(e, "rc") else e
         uniq.append(_take(ctx, r.uniq, r.uniq_bytes, dev))
         fresh.append(_take(ctx, r.fresh, r.fresh_bytes, dev) if p is not None else uniq[-1])
         st["in_records"] += int(r.in_records)
         st["uniq_records"] += int(r.uniq_records)
         st["fresh_records"] += int(r.fresh_records) if p is not None else int(r.uniq_records)
-    empty = torch.empty(0, dtype=torch.uint8, device=dev)
-    return (torch.cat(uniq) if uniq else empty), (torch.cat(fresh) if fresh else empty), st
 
 
 def pieces_bytes(pieces) -> Tuple[int, int]:

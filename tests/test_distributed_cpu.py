@@ -2,7 +2,10 @@
 with the hash restatement (the GPU partition's own parity is tested in test_gpu_dedup),
 exchanges through swarm_amd.distributed.exchange_records (the same function the bench
 uses over RCCL), dedups+diffs its partition with the oracle, and the union of the ranks'
-outputs must equal the single-process result."""
+outputs must equal the single-process result. The byte-range path (agree_splitters,
+range_exchange: the C2/C5 multi-GPU routing) and match_step run through the real
+swarm_amd.distributed code with the routing / matching restated on the host (FakeCtx):
+rank outputs concatenated in rank order must equal the global oracle output."""
 import os
 import socket
 
@@ -79,3 +82,114 @@ def test_exchange_dedup_diff_gloo(world):
     assert S.serialize(u) == eu and S.serialize(f) == ef
     # partitions are disjoint
     assert len(u) == len(set(u))
+
+
+def url_shard(rank, world):
+    import random
+    rng = random.Random(900 + rank)
+    recs = [b"https://h%d.example.com/%s" % (rng.randrange(4000), b"x" * rng.randrange(3)) for _ in range(3000)]
+    recs += [b"", b"10.0.0.%d:443" % rank, b"\xff"]
+    prior = [b"https://h%d.example.com/" % i for i in range(0, 4000, 3)]
+    return b"\n".join(recs) + b"\n", S.serialize(prior[rank::world])
+
+
+def range_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from route_oracle import FakeCtx
+    from swarm_amd import distributed as D
+    ctx = FakeCtx()
+    cur, prior = url_shard(rank, world)
+    t = lambda b: torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8)[: len(b)]  # noqa: E731
+    gsplit = D.agree_splitters(ctx, [t(prior)], world, samples_per_piece=256)
+    assert len(gsplit) == world - 1
+    mine_p = D.range_exchange(ctx, [t(prior)], gsplit)
+    # this rank sent a second (empty) piece: ranks with fewer pieces still join every exchange
+    pieces = [t(cur[: len(cur) // 2 + cur[len(cur) // 2:].index(b"\n") + 1]),
+              t(cur[len(cur) // 2 + cur[len(cur) // 2:].index(b"\n") + 1:])] if rank == 0 else [t(cur)]
+    mine_c = D.range_exchange(ctx, pieces, gsplit, piece_bytes=4096)
+    got_c = b"".join(bytes(p.numpy().tobytes()) for p in mine_c)
+    got_p = b"".join(bytes(p.numpy().tobytes()) for p in mine_p)
+    u, f = S.dedup_diff(got_c, S.dedup(got_p))
+    out_q.put((rank, u, f, cur, prior, max(p.numel() for p in mine_c)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_range_exchange_global_order_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=range_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cur_all = b"".join(r[3] for r in res)
+    prior_all = S.dedup(b"".join(r[4] for r in res))
+    eu, ef = S.dedup_diff(cur_all, prior_all)
+    assert b"".join(r[1] for r in res) == eu
+    assert b"".join(r[2] for r in res) == ef
+    assert all(r[5] <= 4096 for r in res)  # received ranges re-cut at record boundaries
+
+
+class _Hits:
+    def __init__(self, data, sigs):
+        hits = S.literal_hits(data, sigs)
+        self.in_records = len(S.parse_records(data))
+        self.n_hits = len(hits)
+        self.matched_records = len(S.parse_records(S.matched_lines(data, hits)))
+        self.lines = S.matched_lines(data, hits)
+
+
+class _FakeMatcher:
+    def __init__(self, sigs):
+        self.sigs = sigs
+
+    def dev_match(self, ctx, ptr, n):
+        import ctypes
+        return _Hits(ctypes.string_at(ptr, n) if n else b"", self.sigs)
+
+
+SIGS = [b"target1", b"h7", b".com\r"]
+
+
+def match_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import numpy as np
+    from swarm_amd import distributed as D
+    data, _ = shard(0, 1)
+    data = data + b"h7.com\r\nlast-no-newline-target1"
+    cuts = D.shard_bounds(np.frombuffer(data, dtype=np.uint8), world)
+    assert cuts[0] == 0 and cuts[-1] == len(data)
+    assert all(data[c - 1:c] == b"\n" for c in cuts[1:-1] if 0 < c < len(data))
+    part = data[cuts[rank]:cuts[rank + 1]]
+    t = torch.frombuffer(bytearray(part + b"\0"), dtype=torch.uint8)[: len(part)]
+    r, tot = D.match_step(None, _FakeMatcher(SIGS), t)
+    out_q.put((rank, tot, D.gather_lines(r.lines), data))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_match_step_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=match_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    data = res[0][3]
+    hits = S.literal_hits(data, SIGS)
+    want = (len(S.parse_records(data)), len(hits), len(S.parse_records(S.matched_lines(data, hits))))
+    for _, tot, lines, _ in res:
+        assert tot == want
+        assert lines == S.matched_lines(data, hits)

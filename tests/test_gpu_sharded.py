@@ -1,10 +1,14 @@
 """GPU parity for shards larger than one call (C5 sizes): order-preserving range routing by
-key0 splitters, then per-part dedup/diff whose concatenation is the global sort -u /
-comm -13 output, bit-exact against the oracle."""
+byte-string (and key0) splitters, then per-part dedup/diff whose concatenation is the global
+sort -u / comm -13 output, bit-exact against the oracle. The byte routing itself is checked
+against bisect over the cut splitters (Python bytes order is sort's byte order)."""
+import random
+
 import numpy as np
 import pytest
 
 from oracle import semantics as S
+from route_oracle import route_parts, sample_heads
 from swarm_amd import corpus
 
 pytestmark = pytest.mark.gpu
@@ -76,8 +80,8 @@ def test_dedup_large_unsorted_prior_and_no_prior(ctx):
 
 
 def test_many_tiny_parts_and_skewed_keys(ctx):
-    """Up to 256 parts (the routing maximum), many empty ones, and a key0 value shared by a
-    large run of records (it cannot be split: it stays in one part)."""
+    """Up to 256 parts (the routing maximum), many empty ones, and a large run of records
+    sharing their first 8 bytes (byte splitters divide it; equal records stay together)."""
     from swarm_amd import sharded
     buf, ids = corpus.subdomains(100_000, seed=35)
     same = b"".join(b"samekey-%d.example\n" % (i % 5000) for i in range(60_000))
@@ -108,3 +112,108 @@ def test_private_stream_context_is_fenced():
             assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
     finally:
         c.close()
+
+
+def shared_prefix_records(n, seed):
+    """Records sharing long prefixes: lengths around the 8-byte word and 64-byte cut
+    boundaries, NUL / 0xff bytes, equal 64-byte heads with different tails."""
+    rng = random.Random(seed)
+    heads = [b"https://www.example.com/" + bytes(rng.choice(b"ab\x00\xff/") for _ in range(rng.randint(0, 48)))
+             for _ in range(300)]
+    recs = []
+    for _ in range(n):
+        h = rng.choice(heads)
+        k = rng.random()
+        if k < 0.3:
+            recs.append(h)
+        elif k < 0.6:
+            recs.append((h + b"X" * 80)[:rng.choice([56, 63, 64, 65, 71, 72, 100])])
+        else:
+            recs.append(h + bytes(rng.choice(b"az\x00") for _ in range(rng.randint(1, 30))))
+    return recs
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_byte_partition_matches_bisect(ctx, seed):
+    import torch
+    recs = shared_prefix_records(20_000, seed)
+    data = b"\n".join(recs) + b"\n\n" + b"no-newline-tail"
+    rng = random.Random(seed + 10)
+    sp = sorted(rng.sample(recs, 40) + [b"", b"https://www.example.com/" + b"a" * 70, b"\xff" * 3])
+    d = dev(data)
+    out = torch.empty(d.numel() + 16, dtype=torch.uint8, device=d.device)
+    pb, pr = ctx.partition_bytes(d.data_ptr(), d.numel(), sp, out.data_ptr(), out.numel())
+    want = route_parts(data, sp)
+    assert pb == [len(w) for w in want]
+    assert pr == [len(S.parse_records(w)) for w in want]
+    assert out[: sum(pb)].cpu().numpy().tobytes() == b"".join(want)
+
+
+def test_byte_partition_edge_cases(ctx):
+    import torch
+    from swarm_amd._abi import SGError
+    d = dev(b"b\na\n")
+    out = torch.empty(32, dtype=torch.uint8, device=d.device)
+    assert ctx.partition_bytes(d.data_ptr(), d.numel(), [], out.data_ptr(), out.numel()) == ([4], [2])
+    with pytest.raises(SGError):
+        ctx.partition_bytes(d.data_ptr(), d.numel(), [b"b", b"a"], out.data_ptr(), out.numel())
+    with pytest.raises(SGError):  # equal after the 64-byte cut, then shorter
+        ctx.partition_bytes(d.data_ptr(), d.numel(), [b"x" * 64 + b"1", b"x" * 63], out.data_ptr(), out.numel())
+    e = dev(b"\n\n")
+    assert ctx.partition_bytes(e.data_ptr(), 2, [b"m"], out.data_ptr(), out.numel()) == ([0, 0], [0, 0])
+
+
+def test_record_sample_heads(ctx):
+    recs = shared_prefix_records(5_000, 4)
+    data = b"\n".join(recs) + b"\n"
+    d = dev(data)
+    heads, n = ctx.record_sample(d.data_ptr(), d.numel(), 777)
+    R = S.parse_records(data)
+    assert n == len(R)
+    assert heads == [R[(k * len(R)) // 777][:64] for k in range(777)] == sample_heads(data, 777)[0]
+    e = dev(b"\n\n\n")
+    assert ctx.record_sample(e.data_ptr(), 3, 16) == ([], 0)
+
+
+@pytest.mark.parametrize("kind", ["urls", "ips"])
+def test_shared_prefix_data_splits_evenly(ctx, kind):
+    """URL and 10.x.y.z:port records (key0 = 'https:/' / '10.x.y.' for whole runs) still
+    route into balanced parts, and the part outputs are the global result."""
+    import torch
+    from swarm_amd import sharded
+    if kind == "urls":
+        recs = shared_prefix_records(150_000, 7)
+        cur = b"\n".join(recs) + b"\n"
+        prior = S.dedup(b"\n".join(recs[::3]) + b"\n")
+    else:
+        pool = corpus.ip_pool_torch(56_000, seed=5, device="cuda")
+        cur = b"".join(p.cpu().numpy().tobytes() for p in corpus.hostport_pieces(pool, 200_000, 0, 800_000, seed=1,
+                                                                               ports_per_host=16))
+        prior = S.dedup(b"".join(p.cpu().numpy().tobytes() for p in corpus.hostport_pieces(
+            pool, 150_000, 80_000, 880_000, seed=2, ports_per_host=16)))
+    u, f, st = sharded.dedup_diff_large(ctx, sharded.split_at_newlines(dev(cur), 1 << 20), [dev(prior)],
+                                        part_bytes=len(cur) // 8)
+    eu, ef = S.dedup_diff(cur, prior)
+    assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
+    pbytes = st["part_bytes"]
+    assert len(pbytes) >= 8
+    assert max(pbytes) <= 1.5 * (sum(pbytes) / len(pbytes))
+
+
+def test_oversize_part_is_routed_again(ctx, monkeypatch):
+    from swarm_amd import sharded
+    monkeypatch.setattr(sharded, "PART_LIMIT", 300_000)
+    buf, ids = corpus.subdomains(100_000, seed=37)
+    prior = corpus.prior_of(ids)
+    u, f, st = sharded.dedup_diff_large(ctx, [dev(buf.tobytes())], [dev(prior.tobytes())], splitters=[b"m"])
+    eu, ef = S.dedup_diff(buf.tobytes(), prior.tobytes())
+    assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
+    assert st["rerouted_parts"] >= 2 and max(st["part_bytes"]) <= 300_000
+
+
+def test_identical_records_past_the_limit_raise(ctx, monkeypatch):
+    from swarm_amd import sharded
+    monkeypatch.setattr(sharded, "PART_LIMIT", 100_000)
+    same = b"".join(b"x" * 70 + b"%d\n" % (i % 3) for i in range(5_000))
+    with pytest.raises(ValueError, match="share their first 64 bytes"):
+        sharded.dedup_diff_large(ctx, [dev(same)], (), part_bytes=50_000)
