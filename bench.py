@@ -661,6 +661,74 @@ def bench_x1(args, ctx=None, emit=True):
     return out
 
 
+def bench_urls(args, ctx=None, emit=True):
+    """VERDICT r1 item 6: C2's dedup+diff on 10M httpx -silent URLs ('https://' + the C2
+    subdomain draw), where every record shares its first 8 bytes, so a key0 taken at byte 0
+    is one value for the whole input. The pipeline keys from the common prefix (k_lcp) and
+    the range routing splits with byte splitters. Bit-exact on a 1M-record sample against the
+    oracle; reported as ns/record beside C2's."""
+    import numpy as np
+    import torch
+
+    import swarm_amd
+    from swarm_amd import corpus
+
+    own = ctx is None
+    if own:
+        torch.cuda.set_device(0)
+        ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    n_lines = args.lines
+
+    def urls(a):
+        b = a.tobytes()
+        return np.frombuffer(b"https://" + b[:-1].replace(b"\n", b"\nhttps://") + b"\n", dtype=np.uint8)
+    sub, ids = corpus.subdomains(n_lines, seed=1234)
+    cur_np = urls(sub)
+    prior_np = urls(corpus.prior_of(ids))
+    del sub
+    cur = torch.from_numpy(cur_np).cuda()
+    prior = torch.from_numpy(prior_np).cuda()
+    run = lambda: ctx.dedup_diff(cur.data_ptr(), cur.numel(), prior.data_ptr(), prior.numel())  # noqa: E731
+    el, full, stats, dominant, r = timed_steps(ctx, run, args)
+    step_bytes = cur.numel() + prior.numel() + int(r.uniq_bytes) + int(r.fresh_bytes)
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import semantics as S
+        m = min(1_000_000, n_lines)
+        cut = int(np.flatnonzero(cur_np == 10)[m - 1]) + 1
+        cs, ps = cur_np[:cut].tobytes(), prior_np.tobytes()
+        tc = time.perf_counter()
+        eu, ef = S.dedup_diff(cs, ps)
+        tc = time.perf_counter() - tc
+        dc = torch.from_numpy(cur_np[:cut].copy()).cuda()
+        rs = ctx.dedup_diff(dc.data_ptr(), dc.numel(), prior.data_ptr(), prior.numel())
+        cpu = {"value": round(m / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d URL records + full prior; oracle sorted(set())+set difference, 1 thread, %.2f s" % (m, tc),
+               "gpu_bit_exact_on_sample": (ctx.to_bytes(rs.uniq, rs.uniq_bytes) == eu and
+                                           ctx.to_bytes(rs.fresh, rs.fresh_bytes) == ef)}
+    R = int(r.in_records)
+    out = {
+        "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
+        "ns_per_record": round(el * 1e9 / args.steps / max(R, 1), 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (https:// + the C2 subdomain draw)",
+        "config": {"workload": "URLs: %dM httpx -silent URLs sort -u + new-record diff, 1 GPU" % (n_lines // 1_000_000),
+                   "bytes": int(cur.numel()), "prior_bytes": int(prior.numel())},
+        "gbps": round(step_bytes * args.steps / el / 1e9, 2),
+        "records": {"in": R, "unique": int(r.uniq_records), "new": int(r.fresh_records)},
+        "roofline": roofline_of(stats, dominant, "c2", full),
+        "cpu_baseline": cpu,
+        "kernels": kernel_table(full),
+        "dedup_path": ctx.last_path()[0],
+    }
+    if emit:
+        print(json.dumps(out), flush=True)
+    if own:
+        ctx.close()
+    return out
+
+
 def gnu_sort_comm(cur: bytes, prior: bytes, want_uniq: bytes, want_fresh: bytes, threads: int = 16):
     """The shell restatement of A7+A8 timed on the host: LC_ALL=C sort -u --parallel over
     the whole input, then comm -13 against the prior (SURVEY.md §8(d) CPU baseline).
@@ -768,10 +836,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lines", type=int, default=10_000_000)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "fields", "x1"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "fields", "x1", "urls"], default="c2")
     ap.add_argument("--x1-lines", type=int, default=10_000_000, help="X1 fused-step input lines")
     ap.add_argument("--gnu-lines", type=int, default=2_000_000, help="lines of the GNU-tool CPU baseline sample")
-    ap.add_argument("--no-x1", action="store_true", help="default run: skip the fused X1 leg")
+    ap.add_argument("--no-x1", action="store_true", help="default run: skip the fused X1 and URL legs")
     ap.add_argument("--c5-hosts", type=int, default=64_000_000, help="C5 hosts (x 4 open-port slots = combos)")
     ap.add_argument("--c5-data", choices=["hosts", "ips"], default="hosts",
                     help="C5 records: host:port names, or 10.x.y.z:port (15M hosts x 16 port slots)")
@@ -797,6 +865,9 @@ def main():
         return bench_c5(args)
     if args.workload == "x1":
         bench_x1(args)
+        return 0
+    if args.workload == "urls":
+        bench_urls(args)
         return 0
 
     import numpy as np
@@ -925,10 +996,20 @@ def main():
             cpu["gpu_output_bit_exact"] = (u_gpu == eu and f_gpu == ef)
             cpu["gnu_sort_comm"] = gnu_sort_comm(cbytes, pbytes, eu, ef, threads=host_cores())
 
+    c2_path = ctx.last_path()[0]
+    urls = None
+    if rank == 0 and world == 1 and not args.no_x1:
+        # the same dedup+diff on URL records (one shared 8-byte prefix), reported beside C2
+        del cur, prior
+        torch.cuda.empty_cache()
+        u_full = bench_urls(args, ctx=ctx, emit=False)
+        urls = {k: u_full[k] for k in ("value", "ms_per_step", "ns_per_record", "config", "gbps", "records",
+                                       "roofline", "cpu_baseline", "dedup_path")}
+        urls["ns_per_record_vs_c2"] = round(u_full["ns_per_record"] / (ms_per_step * 1e6 / n_lines), 3)
+
     x1 = None
     if rank == 0 and world == 1 and not args.no_x1:
         # the metric's fused step (match+dedup+diff) in the same run, reported beside C2
-        del cur, prior
         torch.cuda.empty_cache()
         x1_full = bench_x1(args, ctx=ctx, emit=False)
         x1 = {k: x1_full[k] for k in ("value", "unit", "ms_per_step", "config", "gbps", "hbm_frac_step", "records",
@@ -957,8 +1038,9 @@ def main():
             "kernels": kernels,
             "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
                             "HIP events only around the dominant kernel",
-            "dedup_path": ctx.last_path()[0],
+            "dedup_path": c2_path,
             "fused_x1": x1,
+            "urls": urls,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
