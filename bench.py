@@ -590,18 +590,26 @@ def bench_x1(args, ctx=None, emit=True):
     holder = {}
 
     def run():
-        r, nh, nm = m.dev_match_dedup_diff(ctx, d.data_ptr(), d.numel(), d_prior.data_ptr(), n_prior)
-        holder["h"] = (nh, nm)
+        # the step: the hit count is not part of the metric's output, so the literal matcher
+        # only flags matched records (sg_dev_match_dedup_diff with n_hits NULL)
+        r, _, nm = m.dev_match_dedup_diff(ctx, d.data_ptr(), d.numel(), d_prior.data_ptr(), n_prior,
+                                          count_hits=False)
+        holder["h"] = nm
         return r
     el, full, stats, dominant, r = timed_steps(ctx, run, args)
-    nh, nm = holder["h"]
+    nm = holder["h"]
+    uniq_step = ctx.to_bytes(r.uniq, r.uniq_bytes)
+    fresh_step = ctx.to_bytes(r.fresh, r.fresh_bytes)
+    # untimed: the hit count, and the same outputs from the hit-list path
+    r2, nh, nm2 = m.dev_match_dedup_diff(ctx, d.data_ptr(), d.numel(), d_prior.data_ptr(), n_prior)
+    paths_agree = (nm2 == nm and ctx.to_bytes(r2.uniq, r2.uniq_bytes) == uniq_step and
+                   ctx.to_bytes(r2.fresh, r2.fresh_bytes) == fresh_step)
+    del uniq_step, fresh_step
     R = int(r.in_records)
-    matched_bytes = None
-    # algorithmic bytes of the step: match = input + matched output;
-    # dedup+diff = matched + prior + unique + new
-    st = full.get("emit_lines")
-    matched_bytes = int(st[2] / 2) if st and st[2] else None
-    step_bytes = d.numel() + 2 * (matched_bytes or 0) + n_prior + int(r.uniq_bytes) + int(r.fresh_bytes)
+    # algorithmic bytes of the step: the match reads the input; dedup+diff
+    # read the matched records (in place, no copy) + the prior and write unique + new
+    matched_bytes = int(m.dev_match(ctx, d.data_ptr(), d.numel()).lines_bytes)  # untimed
+    step_bytes = d.numel() + matched_bytes + n_prior + int(r.uniq_bytes) + int(r.fresh_bytes)
     cpu = None
     if not args.no_cpu_baseline:
         from oracle import semantics as S
@@ -613,7 +621,8 @@ def bench_x1(args, ctx=None, emit=True):
         eu, ef = S.dedup_diff(S.matched_lines(sample, S.literal_hits(sample, sigs)), prior_host)
         tc = time.perf_counter() - tc
         ds = torch.from_numpy(buf[:cut].copy()).cuda()
-        rs, _, _ = m.dev_match_dedup_diff(ctx, ds.data_ptr(), ds.numel(), d_prior.data_ptr(), n_prior)
+        rs, _, _ = m.dev_match_dedup_diff(ctx, ds.data_ptr(), ds.numel(), d_prior.data_ptr(), n_prior,
+                                         count_hits=False)
         cpu = {"value": round(m_s / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
                "sample": "%d X1 lines: oracle `sig in line` + sorted(set()) + set difference vs the prior matched "
                          "set, 1 thread, %.2f s" % (m_s, tc), "host_cpus": os.cpu_count(),
@@ -627,7 +636,8 @@ def bench_x1(args, ctx=None, emit=True):
         if g:
             gm, gu, gf, secs = g
             dg = torch.from_numpy(buf[:gcut].copy()).cuda()
-            rg, _, _ = m.dev_match_dedup_diff(ctx, dg.data_ptr(), dg.numel(), d_prior.data_ptr(), n_prior)
+            rg, _, _ = m.dev_match_dedup_diff(ctx, dg.data_ptr(), dg.numel(), d_prior.data_ptr(), n_prior,
+                                             count_hits=False)
             tot = secs["grep"] + secs["sort_comm"]
             cpu["gnu_grep_sort_comm"] = {
                 "value": round(g_lines / tot, 1), "unit": "records/s", "cores": cores, "seconds": secs,
@@ -647,6 +657,7 @@ def bench_x1(args, ctx=None, emit=True):
                    "bytes": int(d.numel()), "prior_bytes": n_prior},
         "gbps": round(step_bytes * args.steps / el / 1e9, 2),
         "hbm_frac_step": round(step_bytes * args.steps / el / 1e9 / HBM_PEAK_GBS, 4),
+        "flag_path_equals_hit_list_path": paths_agree,
         "records": {"in": R, "hits": int(nh), "matched": int(nm), "unique_matched": int(r.uniq_records),
                     "new_matched": int(r.fresh_records)},
         "roofline": roofline_of(stats, dominant, "x1", full),

@@ -201,7 +201,9 @@ int sg_dev_match(sg_ctx *ctx, sg_matcher *h, const uint8_t *d_buf, size_t n, sg_
  * A8 the matched records new since the prior scan's matched set (README.md:11 alerting).
  * res: as sg_dev_dedup_diff over the matched records, with in_records = the input's records;
  * *n_hits = (record, signature) hits, *matched_records = records with at least one hit. The
- * hit arrays themselves are not returned (sg_dev_match gives them). d_prior may be NULL. */
+ * hit arrays themselves are not returned (sg_dev_match gives them). d_prior may be NULL.
+ * n_hits may be NULL: a literal matcher then only flags the matched records (no hit list or
+ * hit sort), and the dedup runs on their spans in d_buf (no grep-output copy). */
 int sg_dev_match_dedup_diff(sg_ctx *ctx, sg_matcher *h, const uint8_t *d_buf, size_t n, const uint8_t *d_prior,
                             size_t n_prior, sg_dev_result *res, uint64_t *n_hits, uint64_t *matched_records);
 void sg_free(void *h);  /* frees an sg_matcher */

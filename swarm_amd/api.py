@@ -174,16 +174,19 @@ class Matcher:
         check(lib.sg_dev_match(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(r)))
         return r
 
-    def dev_match_dedup_diff(self, ctx: "Context", d_buf: int, n: int, d_prior: int = 0, n_prior: int = 0):
+    def dev_match_dedup_diff(self, ctx: "Context", d_buf: int, n: int, d_prior: int = 0, n_prior: int = 0,
+                             count_hits: bool = True):
         """The metric's fused step on device buffers: parse -> match -> sort -u of the matched
         records -> new matched records vs the prior scan's matched set. Returns (DevResult,
-        n_hits, matched_records) (include/swarmgpu.h sg_dev_match_dedup_diff)."""
+        n_hits, matched_records) (include/swarmgpu.h sg_dev_match_dedup_diff). With
+        count_hits=False n_hits is None: a literal matcher then only flags matched records
+        (no (record, signature) hit list is built)."""
         r = _abi.DevResult()
         nh, nm = C.c_uint64(), C.c_uint64()
         check(lib.sg_dev_match_dedup_diff(ctx._h, self._h, C.c_void_p(d_buf), n,
                                           C.c_void_p(d_prior) if d_prior else None, n_prior, C.byref(r),
-                                          C.byref(nh), C.byref(nm)))
-        return r, nh.value, nm.value
+                                          C.byref(nh) if count_hits else None, C.byref(nm)))
+        return r, (nh.value if count_hits else None), nm.value
 
 
 def nmap_ports(buf) -> bytes:

@@ -65,6 +65,7 @@ enum Slot : int {
     // bucket sample sort (sg_bucket.hip)
     S_BK_SKEY, S_BK_SSPAN, S_BK_CNT1, S_BK_CNT2, S_BK_SMALL, S_BK_TOT2, S_BK_Q, S_BK_NCUR, S_BK_L1, S_BK_L2,
     S_BK_US, S_BK_FS, S_BK_SPFX, S_BK_DBG, S_BK_RECS, S_BK_NREC,
+    S_M_FLAG, S_M_SP2, S_M_K2,
     S_NSLOTS
 };
 
@@ -289,32 +290,34 @@ __device__ __forceinline__ void load_chunks(const uint8_t *buf, uint32_t p, uint
         c[k] = (16u * k < sh + cl) ? *reinterpret_cast<const uint4 *>(buf + q0 + 16u * k) : make_uint4(0u, 0u, 0u, 0u);
 }
 
-// rec_equal with wide loads: when the compared span (len - off) is <= 48 bytes each side
-// takes at most four 16-B loads and the comparison is a masked XOR of normalised dwords;
-// longer spans use rec_equal. Buffers must be 16-byte aligned.
+// rec_equal with wide loads: the compared span (len - off) goes in windows of 48 bytes,
+// each side taking at most four 16-B loads per window, and a window's comparison is a masked
+// XOR of normalised dwords (long records — URLs with titles — cost 16-B loads instead of
+// 8-B load pairs). Buffers must be 16-byte aligned.
 __device__ __forceinline__ bool rec_equal_w(const uint8_t *ba, uint32_t sa, uint32_t ea, const uint8_t *bb,
                                             uint32_t sb, uint32_t eb, uint32_t off) {
     const uint32_t la = ea - sa;
     if (la != eb - sb) return false;
-    if (la <= off) return true;
-    const uint32_t cl = la - off;
-    if (cl > 48u) return rec_equal(ba, sa, ea, bb, sb, eb, off);
-    uint4 ca[4], cb[4];
-    load_chunks(ba, sa + off, cl, ca);
-    load_chunks(bb, sb + off, cl, cb);
-    uint32_t ra[13], rb[13];
-    normalize52(ca, (sa + off) & 15u, ra);
-    normalize52(cb, (sb + off) & 15u, rb);
-    uint32_t d = 0;
+    for (uint32_t o = off; o < la; o += 48u) {
+        const uint32_t cl = (la - o) < 48u ? (la - o) : 48u;
+        uint4 ca[4], cb[4];
+        load_chunks(ba, sa + o, cl, ca);
+        load_chunks(bb, sb + o, cl, cb);
+        uint32_t ra[13], rb[13];
+        normalize52(ca, (sa + o) & 15u, ra);
+        normalize52(cb, (sb + o) & 15u, rb);
+        uint32_t d = 0;
 #pragma unroll
-    for (uint32_t o = 0; o < 12; ++o) {
-        if (4u * o < cl) {
-            const uint32_t k = cl - 4u * o;
-            const uint32_t m = k >= 4u ? ~0u : ((1u << (8u * k)) - 1u);
-            d |= (ra[o] ^ rb[o]) & m;
+        for (uint32_t q = 0; q < 12; ++q) {
+            if (4u * q < cl) {
+                const uint32_t k = cl - 4u * q;
+                const uint32_t m = k >= 4u ? ~0u : ((1u << (8u * k)) - 1u);
+                d |= (ra[q] ^ rb[q]) & m;
+            }
         }
+        if (d) return false;
     }
-    return d == 0;
+    return true;
 }
 
 // Bytewise compare of the suffixes from `off` by 7-byte chunk keys (memcmp-then-length).
@@ -335,25 +338,26 @@ __device__ __forceinline__ int rec_cmp_w(const uint8_t *ba, uint32_t sa, uint32_
                                          uint32_t sb, uint32_t eb, uint32_t off) {
     const uint32_t la = ea - sa, lb = eb - sb;
     const uint32_t ma = la > off ? la - off : 0u, mb = lb > off ? lb - off : 0u;
-    const uint32_t cl = ma < mb ? ma : mb;
-    if (cl > 48u) return rec_cmp_k(ba, sa, ea, bb, sb, eb, off);
+    const uint32_t cm = ma < mb ? ma : mb;
     const int by_len = ma < mb ? -1 : (ma > mb ? 1 : 0);
-    if (cl == 0) return by_len;
-    uint4 ca[4], cb[4];
-    load_chunks(ba, sa + off, cl, ca);
-    load_chunks(bb, sb + off, cl, cb);
-    uint32_t ra[13], rb[13];
-    normalize52(ca, (sa + off) & 15u, ra);
-    normalize52(cb, (sb + off) & 15u, rb);
+    for (uint32_t o = 0; o < cm; o += 48u) {  // 48-byte windows of 16-B loads
+        const uint32_t cl = (cm - o) < 48u ? (cm - o) : 48u;
+        uint4 ca[4], cb[4];
+        load_chunks(ba, sa + off + o, cl, ca);
+        load_chunks(bb, sb + off + o, cl, cb);
+        uint32_t ra[13], rb[13];
+        normalize52(ca, (sa + off + o) & 15u, ra);
+        normalize52(cb, (sb + off + o) & 15u, rb);
 #pragma unroll
-    for (uint32_t o = 0; o < 12; ++o) {
-        if (4u * o < cl) {
-            const uint32_t k = cl - 4u * o;
-            const uint32_t m = k >= 4u ? ~0u : ((1u << (8u * k)) - 1u);
-            const uint32_t x = (ra[o] ^ rb[o]) & m;
-            if (x) {
-                const uint32_t sh = (uint32_t)__builtin_ctz(x) & ~7u;
-                return ((ra[o] >> sh) & 0xffu) < ((rb[o] >> sh) & 0xffu) ? -1 : 1;
+        for (uint32_t q = 0; q < 12; ++q) {
+            if (4u * q < cl) {
+                const uint32_t k = cl - 4u * q;
+                const uint32_t m = k >= 4u ? ~0u : ((1u << (8u * k)) - 1u);
+                const uint32_t x = (ra[q] ^ rb[q]) & m;
+                if (x) {
+                    const uint32_t sh = (uint32_t)__builtin_ctz(x) & ~7u;
+                    return ((ra[q] >> sh) & 0xffu) < ((rb[q] >> sh) & 0xffu) ? -1 : 1;
+                }
             }
         }
     }

@@ -902,7 +902,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
 }
 
 static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
-                                uint64_t n_prior, bool want_fresh, sg_dev_result *res) {
+                                uint64_t n_prior, bool want_fresh, sg_dev_result *res, const Lines *cur_pre = nullptr) {
     *res = sg_dev_result{};
     UView pv;
     const bool have_prior = want_fresh && d_prior && n_prior;
@@ -923,7 +923,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
             SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_prior, Lp.spans, Lp.keys,
                         R, dflag, 0u);
     }
-    SG_TRY(run_lines(c, d_cur, n_cur, CUR_VIEW.lines, &Lc));
+    if (cur_pre) Lc = *cur_pre;
+    else SG_TRY(run_lines(c, d_cur, n_cur, CUR_VIEW.lines, &Lc));
     // common prefix of every record (reference: the first record of cur, else of prior)
     const bool ref_cur = Lc.n_rec > 0;
     const uint8_t *rbuf = ref_cur ? d_cur : d_prior;
@@ -987,6 +988,13 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     res->fresh_bytes = (uint32_t)tt;
     res->fresh_records = (uint32_t)(tt >> 32);
     return SG_OK;
+}
+
+int dev_dedup_diff_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &cur, const uint8_t *d_prior,
+                         uint64_t n_prior, sg_dev_result *res) {
+    c->last_path = 0;
+    c->last_flags = 0;
+    return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, true, res, &cur);
 }
 
 // Dedup+diff entry: the bucket sample sort when there is a prior scan to take splitters from

@@ -616,6 +616,7 @@ struct LitArgs {
     uint32_t cap;
     const uint32_t *fac_off, *fac_pids;  // regex prefilter expansion (else null)
     uint2 *spans_out;                    // non-null: also write the parse's record spans (fused A3)
+    uint8_t *rec_flag;                   // non-null: mark matched records here instead of listing hits
     unsigned long long *dbg;             // SG_LIT_DEBUG: {candidates, fingerprint matches, hits}
     uint32_t dbg_mode;                   // bit 0: skip pass 2, bit 1: skip pass 1 probes
 };
@@ -686,6 +687,10 @@ __device__ __forceinline__ bool lit_verify(const Args &a, const uint8_t *s_tile,
 template <class Args, class Push>
 __device__ __forceinline__ void lit_emit(const Args &a, Push &push, uint32_t rec, uint32_t pid) {
     if (a.dbg) atomicAdd(&a.dbg[2], 1ull);
+    if (a.rec_flag) {  // idempotent byte store: the set of matched records, no list
+        a.rec_flag[rec] = 1;
+        return;
+    }
     if (a.fac_off) {
         for (uint32_t z = a.fac_off[pid]; z < a.fac_off[pid + 1]; ++z) push(rec, a.fac_pids[z]);
     } else {
@@ -1204,6 +1209,17 @@ __global__ void k_split_hits(const unsigned long long *K, const uint32_t *idx, u
     sig[i] = (uint32_t)k;
 }
 
+// Matched records (input order) -> their spans and key0 from byte 0.
+__global__ __launch_bounds__(256) void k_gather_matched(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
+                                                        const uint32_t *__restrict__ mrec, uint32_t m, uint2 *__restrict__ sp,
+                                                        uint64_t *__restrict__ keys) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const uint2 x = spans[mrec[i]];
+        sp[i] = x;
+        keys[i] = chunk_key(buf, x.x, x.y, 0);
+    }
+}
+
 __global__ void k_rec_of(const unsigned long long *K, const uint32_t *idx, uint32_t n, uint32_t *rec) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) rec[i] = (uint32_t)(K[idx[i]] >> 32);
@@ -1214,7 +1230,12 @@ static int select_one(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint32
     return run_select2(c, name, pred, n, out, (uint32_t *)nullptr, count, nullptr);
 }
 
-int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res, bool want_lines) {
+int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res, bool want_lines,
+              MatchFlags *mf) {
+    if (mf && !(h->lit.on && h->tables.empty() && !h->has_pre)) {
+        set_error("dev_match: record flags need a literal-filter matcher");
+        return SG_E_INVAL;
+    }
     *res = sg_dev_hits{};
     SG_TRY(ensure_device(h, c->device));
     Lines L;
@@ -1258,6 +1279,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         }
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
         a.spans_out = (fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
+        a.rec_flag = mf ? mf->flags : nullptr;
         static const int dbg_mode = getenv("SG_LIT_DEBUG") ? atoi(getenv("SG_LIT_DEBUG")) : -1;
         unsigned long long *dbg = nullptr;
         if (dbg_mode >= 0) a.dbg_mode = (uint32_t)dbg_mode;  // bit 0 skip pass 2, bit 1 skip pass 1, bit 3 count
@@ -1331,6 +1353,13 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         SG_TRY(slot(c, S_R_VAL2, (size_t)n_cand + 1, &w2));
         SG_TRY(radix_sort(c, reinterpret_cast<uint64_t *>(cand), w1, alt, w2, n_cand, 0, pbits, true, &KC, &WV, "rs_cand"));
         vcand = reinterpret_cast<const unsigned long long *>(KC);
+    }
+    if (mf) {
+        SG_TRY(slot(c, S_M_FLAG, (size_t)R + 16, &mf->flags));
+        SG_HIP(hipMemsetAsync(mf->flags, 0, (size_t)R + 16, c->stream));
+        if (R) SG_TRY(run_lit("lit_match", h->lit, nullptr, cnt, 0u, nullptr, nullptr));
+        mf->L = L;
+        return SG_OK;
     }
     for (int attempt = 0; attempt < 2; ++attempt) {
         SG_TRY(slot(c, S_M_HITS, cap, &hits));
@@ -1541,6 +1570,29 @@ int sg_dev_match_dedup_diff(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, size
         SG_TRY(slot(c, S_IN2, n_prior + 16, &a));
         SG_HIP(hipMemcpyAsync(a, d_prior, n_prior, hipMemcpyDeviceToDevice, c->stream));
         p = a;
+    }
+    if (!n_hits && h->lit.on && h->tables.empty() && !h->has_pre) {
+        // literal matcher, hit count not asked: the scan flags matched records, and the
+        // dedup runs on their spans in the input buffer (no hit list, no hit sort, no
+        // grep-output copy and no second parse)
+        sg_dev_hits hits;
+        MatchFlags mf;
+        SG_TRY(dev_match(c, h, b, n, &hits, false, &mf));
+        const uint32_t R = mf.L.n_rec;
+        uint32_t *mrec;
+        SG_TRY(slot(c, S_R_POS, (size_t)R + 1, &mrec));
+        uint32_t M = 0;
+        if (R) SG_TRY(select_flags(c, mf.flags, R, mrec, &M));
+        Lines Lm;
+        SG_TRY(slot(c, S_M_SP2, (size_t)M + 1, &Lm.spans));
+        SG_TRY(slot(c, S_M_K2, (size_t)M + 1, &Lm.keys));
+        Lm.n_rec = M;
+        if (M) SG_LAUNCH_B(c, "gather_matched", 24.0 * M, k_gather_matched, std::min<uint32_t>((M + 255) / 256, 4096u), 256, 0,
+                           b, mf.L.spans, mrec, M, Lm.spans, Lm.keys);
+        if (matched_records) *matched_records = M;
+        SG_TRY(dev_dedup_diff_lines(c, b, n, Lm, n_prior ? p : nullptr, n_prior, res));
+        res->in_records = R;
+        return SG_OK;
     }
     // A3 + A4: the matched records in input order (grep output, context slot S_M_LINES)
     sg_dev_hits hits;

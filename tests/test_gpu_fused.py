@@ -39,9 +39,10 @@ def dev(b):
     return torch.from_numpy(np.frombuffer(b + b"\0", dtype=np.uint8).copy()).cuda()
 
 
-def fused(ctx, m, data, prior):
+def fused(ctx, m, data, prior, count_hits=True):
     d, p = dev(data), dev(prior)
-    r, nh, nm = m.dev_match_dedup_diff(ctx, d.data_ptr(), len(data), p.data_ptr() if prior else 0, len(prior))
+    r, nh, nm = m.dev_match_dedup_diff(ctx, d.data_ptr(), len(data), p.data_ptr() if prior else 0, len(prior),
+                                       count_hits=count_hits)
     return ctx.to_bytes(r.uniq, r.uniq_bytes), ctx.to_bytes(r.fresh, r.fresh_bytes), r, nh, nm
 
 
@@ -52,8 +53,9 @@ def oracle(data, sigs, prior, kind="literal"):
     return u, f, hits, matched
 
 
+@pytest.mark.parametrize("count_hits", [True, False])
 @pytest.mark.parametrize("n,seed", [(1500, 1), (4000, 2)])
-def test_fused_literal_httpx(ctx, sigs, n, seed):
+def test_fused_literal_httpx(ctx, sigs, n, seed, count_hits):
     import swarm_amd
     tails = corpus.httpx_tails(sigs, n_tails=512, seed=seed)
     buf, ids = corpus.httpx_hosts(n, tails, seed=seed, universe=n // 2)
@@ -61,10 +63,11 @@ def test_fused_literal_httpx(ctx, sigs, n, seed):
     m = swarm_amd.Matcher(sigs, "literal")
     prior_all = corpus.httpx_rows(corpus.prior_ids(ids), tails).tobytes()
     prior = S.dedup(S.matched_lines(prior_all, S.literal_hits(prior_all, sigs)))
-    u, f, r, nh, nm = fused(ctx, m, data, prior)
+    u, f, r, nh, nm = fused(ctx, m, data, prior, count_hits)
     eu, ef, hits, matched = oracle(data, sigs, prior)
     assert u == eu and f == ef
-    assert nh == len(hits) and nm == len(S.parse_records(matched))
+    assert nm == len(S.parse_records(matched))
+    assert nh == (len(hits) if count_hits else None)
     assert r.in_records == len(S.parse_records(data))
     assert r.uniq_records == len(S.parse_records(eu)) and r.fresh_records == len(S.parse_records(ef))
 
@@ -111,3 +114,33 @@ def test_fused_bucket_path(ctx, sigs, monkeypatch):
     eu, ef, _, _ = oracle(data, sigs, prior)
     assert u == eu and f == ef
     assert ctx.last_path()[0] == "bucket"
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_fused_flag_path_edge_records(ctx, seed, monkeypatch):
+    """The flag path (no hit count): matched records taken in place from the input — empty
+    lines, CR, an unterminated last record, URL-like shared prefixes, every record matching
+    or none, a record matching several signatures several times."""
+    import swarm_amd
+    monkeypatch.setenv("SG_FORCE_LITFILTER", "1")  # the flag path is the q-gram filter's
+    rng = random.Random(seed)
+    sigs = [b"alpha", b"beta-", b"\r", b"zz", b"https://h1"]
+    recs = []
+    for i in range(3000):
+        k = rng.random()
+        if k < 0.05:
+            recs.append(b"")
+        elif k < 0.5:
+            recs.append(b"https://h%d.example/%s" % (rng.randrange(50), rng.choice([b"alpha", b"betazz", b"x"])))
+        else:
+            recs.append(b"%s beta-beta-%d alpha\r" % (rng.choice([b"a", b"zz", b"q"]), rng.randrange(100)))
+    data = b"\n".join(recs) + b"\nunterminated alpha"
+    prior = S.dedup(S.matched_lines(data[: len(data) // 3], S.literal_hits(data[: len(data) // 3], sigs)))
+    m = swarm_amd.Matcher(sigs, "literal")
+    for pr in (prior, b""):
+        u, f, r, nh, nm = fused(ctx, m, data, pr, count_hits=False)
+        eu, ef, hits, matched = oracle(data, sigs, pr)
+        assert u == eu and f == ef and nm == len(S.parse_records(matched)) and nh is None
+    none = swarm_amd.Matcher([b"never-there"], "literal")
+    u, f, r, nh, nm = fused(ctx, none, data, prior, count_hits=False)
+    assert (u, f, nm) == (b"", b"", 0)
