@@ -414,6 +414,11 @@ __global__ void k_gather_rl(const uint32_t *__restrict__ idx, const uint32_t *__
     L2[i] = L[q];
 }
 
+__global__ __launch_bounds__(256) void k_gather_spans(const uint32_t *__restrict__ V, const uint2 *__restrict__ spans,
+                                                      uint32_t n, uint2 *__restrict__ out) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = spans[V[i]];
+}
+
 __global__ void k_mark(const uint32_t *__restrict__ idx, uint32_t n, uint8_t *flag) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) flag[idx[i]] = 1;
@@ -829,15 +834,27 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
     if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B, base));
 
-    // materialise the records in this order: S (contiguous), SS spans into S
+    // The records in this order: SS = the input spans in sorted order, S = the input itself;
+    // the later passes (adjacent compare, segment sort, unique emit) gather from the input.
+    // Measured cheaper than materialising a sorted copy first (C2 2.51 -> 2.30 ms, X1 4.37 ->
+    // 3.97 ms): the copy gathered every record once and the unique emit copied ~2/3 of them
+    // again, where gathering only the unique records reads each kept record once.
+    // SG_MATERIALIZE=1 restores the copy (S contiguous, SS spans into it).
     uint8_t *Sb;
     uint2 *SS;
-    SG_TRY(slot(c, S_SBUF, (size_t)n + 64, &Sb));
     SG_TRY(slot(c, S_SSPANS, R, &SS));
-    uint64_t *pc;
-    // model: input bytes read + S written once; cached span per record in, span per record out
-    SG_TRY(run_emit(c, k_emit_sorted, "emit_sorted", "emit_sorted.count", S_EMIT, PermItem{V, L.spans}, R, d_buf, Sb, SS, nullptr,
-                    nullptr, &pc, 2.0 * (double)n + 16.0 * R));
+    static const int materialize = getenv("SG_MATERIALIZE") ? atoi(getenv("SG_MATERIALIZE")) : 0;
+    if (materialize) {
+        SG_TRY(slot(c, S_SBUF, (size_t)n + 64, &Sb));
+        uint64_t *pc;
+        // model: input bytes read + S written once; cached span per record in, span per record out
+        SG_TRY(run_emit(c, k_emit_sorted, "emit_sorted", "emit_sorted.count", S_EMIT, PermItem{V, L.spans}, R, d_buf, Sb, SS,
+                        nullptr, nullptr, &pc, 2.0 * (double)n + 16.0 * R));
+    } else {
+        Sb = const_cast<uint8_t *>(d_buf);
+        SG_LAUNCH_B(c, "gather_spans", 16.0 * R, k_gather_spans, std::min<uint32_t>(grid_for(R, 256), 4096u), 256, 0, V, L.spans,
+                    R, SS);
+    }
 
     // adjacent equality inside segments; segments holding two different records -> sort
     uint8_t *dup, *segbad;
