@@ -209,6 +209,9 @@ static uint32_t lit_template(uint32_t cls_mask) {
     return 0x1Fu;
 }
 
+// Bucket of a gram: multiplicative hash. (A shift-xor fold — three full-rate ops instead of
+// the quarter-rate 32-bit multiply — measured no faster on X1: 24.9M candidates per 10M lines
+// against 17.0M, and the extra verifications ate the saved probe cycles.)
 __host__ __device__ __forceinline__ uint32_t lit_h(uint32_t lo, uint32_t hi, uint32_t c, uint32_t bits) {
     if (c <= 1) return lo;
     const uint32_t k = (c == 4) ? (lo ^ ((hi << 13) | (hi >> 19))) : lo;
@@ -227,7 +230,10 @@ static uint32_t gram_commonness(const uint8_t *g, uint32_t L) {
     return s;
 }
 
-static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags, sg_matcher::Lit *T) {
+// extra_bits: bitmap size over the 64-bits-per-pattern base, as a power of two (more bits:
+// fewer false candidates, more LDS per block).
+static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags, sg_matcher::Lit *T,
+                     uint32_t extra_bits = 0) {
     const bool nocase = flags & SG_NOCASE;
     auto fold = [&](uint8_t b) -> uint8_t { return (nocase && b >= 'A' && b <= 'Z') ? (uint8_t)(b + 32) : b; };
     T->on = true;
@@ -256,7 +262,7 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
             } else {
                 b = 10;
                 static const uint32_t cap4 = getenv("SG_LIT_BITS4") ? (uint32_t)atoi(getenv("SG_LIT_BITS4")) : 18u;
-                static const uint32_t extra = getenv("SG_LIT_EXTRA") ? (uint32_t)atoi(getenv("SG_LIT_EXTRA")) : 0u;
+                const uint32_t extra = getenv("SG_LIT_EXTRA") ? (uint32_t)atoi(getenv("SG_LIT_EXTRA")) : extra_bits;
                 while (b < (c == 2 ? 15u : cap4) && (1ull << b) < (64ull << extra) * cnt[c]) ++b;
             }
         }
@@ -1452,7 +1458,8 @@ int sg_ac_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats
     // q-gram filter (independent per-position probes, byte compares on bitmap hits).
     const auto &T = m->tables[0];
     if ((uint64_t)T.n_states * T.n_classes * 2 > AC_HOT_BYTES || getenv("SG_FORCE_LITFILTER")) {
-        rc = build_lit(pats, pat_offs, n_pats, flags, &m->lit);
+        // 128 bitmap bits per pattern: X1 candidates 37M -> 17M per 10M lines for 2 blocks/CU
+        rc = build_lit(pats, pat_offs, n_pats, flags, &m->lit, 1u);
         if (rc == SG_E_UNSUPPORTED) {
             m->lit = sg_matcher::Lit{};  // too many patterns of one length class: keep the automaton
         } else if (rc != SG_OK) {
