@@ -158,6 +158,17 @@ def bench_c3(args):
                "host_cpus": os.cpu_count()}
         gh = m.match(sample)
         cpu["gpu_hits_bit_exact_on_sample"] = (gh == hits)
+        # GNU grep -F over the whole C3 input on the host cores, checked against the GPU's
+        # full matched-line output (full-size parity)
+        cores = host_cores()
+        g = gnu_grep(buf.tobytes(), sigs, cores, "-F")
+        if g:
+            gm, secs = g
+            r_full = m.dev_match(ctx, d.data_ptr(), d.numel())
+            cpu["gnu_grep"] = {"value": round(R / secs, 1), "unit": "records/s", "cores": cores, "seconds": secs,
+                               "sample": "the full input (%d lines, %d B)" % (R, d.numel()),
+                               "command": "LC_ALL=C grep -a -F -f sigs (x%d line-aligned splits)" % cores,
+                               "bit_exact_full": ctx.to_bytes(r_full.lines, r_full.lines_bytes) == gm}
     print(json.dumps({
         "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
@@ -235,6 +246,25 @@ def bench_c4(args):
                "sample": "%d C4 banners x %d regexes, oracle re.search, 1 thread, %.2f s" % (m_s, len(pats), tc),
                "host_cpus": os.cpu_count()}
         cpu["gpu_hits_bit_exact_on_sample"] = (m.match(sample) == hits)
+        # GNU grep -E on the agreeing subset (tests/golden/c4_grep_subset.json: signatures
+        # whose POSIX-ERE reading matches re.search), fanned over the host cores, against a
+        # GPU matcher compiled from the same subset on the same banners
+        sub_idx = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_grep_subset.json")))["subset"]
+        sub = [pats[i] for i in sub_idx]
+        cores = host_cores()
+        g_lines = min(n_lines, max(args.gnu_lines // 5, 1000))
+        gcut = int(np.flatnonzero(buf == 10)[g_lines - 1]) + 1
+        g = gnu_grep(buf[:gcut].tobytes(), sub, cores, "-E")
+        if g:
+            gm, secs = g
+            msub = swarm_amd.Matcher(sub, "regex")
+            dg = torch.from_numpy(buf[:gcut].copy()).cuda()
+            rg = msub.dev_match(ctx, dg.data_ptr(), dg.numel())
+            cpu["gnu_grep"] = {"value": round(g_lines / secs, 1), "unit": "records/s", "cores": cores, "seconds": secs,
+                               "signatures": len(sub),
+                               "sample": "%d C4 banners x the %d-signature grep-agreeing subset" % (g_lines, len(sub)),
+                               "command": "LC_ALL=C grep -a -E -f subset (x%d line-aligned splits)" % cores,
+                               "bit_exact_vs_gpu_same_subset": ctx.to_bytes(rg.lines, rg.lines_bytes) == gm}
     if rank == 0:
         print(json.dumps({
         "metric": METRIC, "value": round(g_rec * args.steps / el, 1), "unit": "records/s", "n_gpus": world,
@@ -388,16 +418,19 @@ def bench_c5(args):
     mine = D.range_exchange(ctx, prior_raw, gsplit) if world > 1 else prior_raw
     parts = sharded.plan_parts(mine, [], 2 << 30)
     lsplit = sharded.choose_splitters(sharded.sample_records(ctx, mine), parts)
-    pu, _, _ = sharded.dedup_diff_large(ctx, mine, (), splitters=lsplit)
+    pu, _, pst = sharded.dedup_diff_large(ctx, mine, (), splitters=lsplit)
     del prior_raw, mine
     prior_local = sharded.split_at_newlines(pu, 3 << 30)
+    # the stored prior is part-ordered output: keep its part boundaries instead of routing it
+    # again every step (falls back to routing when a part had to be split further)
+    prior_parts = sharded.split_parts(pu, pst["uniq_part_bytes"]) if not pst["rerouted_parts"] else None
     cur = corpus.hostport_pieces(pool, per, 0, U, seed=100 + rank, ports_per_host=K)
     del pool
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup
 
     def step():
-        return D.dedup_diff_range_step(ctx, cur, prior_local, gsplit, lsplit)
+        return D.dedup_diff_range_step(ctx, cur, prior_local, gsplit, lsplit, prior_parts=prior_parts)
 
     for _ in range(args.warmup):
         u, f, st = step()
@@ -503,6 +536,38 @@ def c3_signatures():
     sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
     words = [base64.b64decode(w) for w in sig["words"]]
     return random.Random(0).sample([w for w in words if len(w) >= 4], 2000)
+
+
+def gnu_grep(data: bytes, pats, cores: int, flag: str = "-F"):
+    """`LC_ALL=C grep -a <flag> -f pats` fanned out over `cores` line-aligned splits of data
+    (BASELINE.md CPU-baseline plan; outputs concatenated in input order). Returns (matched
+    lines, seconds of the grep stage) or None without grep."""
+    import shutil
+    import subprocess
+    import tempfile
+    if not shutil.which("grep"):
+        return None
+    env = dict(os.environ, LC_ALL="C")
+    with tempfile.TemporaryDirectory() as d:
+        pf = os.path.join(d, "pats")
+        with open(pf, "wb") as f:
+            f.write(b"".join(s + b"\n" for s in pats if s and b"\n" not in s))
+        cuts, n = [0], len(data)
+        for k in range(1, cores):
+            c = data.find(b"\n", n * k // cores)
+            cuts.append(n if c < 0 else c + 1)
+        cuts.append(n)
+        names = []
+        for k in range(cores):
+            fn = os.path.join(d, "in%d" % k)
+            with open(fn, "wb") as f:
+                f.write(data[cuts[k]:cuts[k + 1]])
+            names.append(fn)
+        t0 = time.perf_counter()
+        procs = [subprocess.Popen(["grep", "-a", flag, "-f", pf, fn], env=env, stdout=subprocess.PIPE) for fn in names]
+        outs = [p.communicate()[0] for p in procs]
+        secs = time.perf_counter() - t0
+    return b"".join(outs), round(secs, 3)
 
 
 def gnu_grep_sort_comm(data: bytes, sigs, prior: bytes, cores: int):

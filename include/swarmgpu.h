@@ -124,6 +124,14 @@ typedef struct sg_dev_result {
 /* d_prior may be NULL with n_prior 0 (then fresh == uniq). */
 int sg_dev_dedup_diff(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur,
                       const uint8_t *d_prior, size_t n_prior, sg_dev_result *res);
+/* sg_dev_dedup_diff writing its two outputs into caller device memory at any byte address
+ * (capacities >= n_cur + 1 each): res->uniq = d_uniq, res->fresh = d_fresh (d_fresh may be NULL:
+ * then res->fresh aliases d_uniq when there is no prior, and new records go to a context
+ * buffer otherwise). Consecutive calls can append part outputs to one result buffer without a
+ * copy (swarm_amd.sharded). */
+int sg_dev_dedup_diff_into(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur, const uint8_t *d_prior,
+                           size_t n_prior, uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh,
+                           size_t fresh_cap, sg_dev_result *res);
 
 /* Multi-GPU: route every record of d_buf to partition
  * part(hash64(record), n_parts), n_parts <= 256. Writes '\n'-terminated records grouped by
@@ -157,6 +165,14 @@ int sg_dev_key_sample(sg_ctx *ctx, const uint8_t *d_buf, size_t n, uint32_t m, u
 int sg_dev_partition_bytes(sg_ctx *ctx, const uint8_t *d_buf, size_t n, const uint8_t *splitters,
                            const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out, size_t out_cap,
                            uint64_t *part_bytes, uint64_t *part_records);
+/* Range routing of k pieces (each < 4 GiB, ending at a record boundary) into ONE device
+ * buffer d_out (capacity >= the pieces' bytes + 1 each), part-contiguous across pieces: part
+ * p = the part-p records of piece 0, then of piece 1, ... (input order kept inside a piece),
+ * so every part is one contiguous range ready for a dedup call (replaces per-piece routing
+ * followed by a concatenation). part_bytes / part_records: totals over the pieces. */
+int sg_dev_partition_bytes_pieces(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                  const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
+                                  uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records);
 /* m evenly spaced records' first SG_SPLIT_BYTES bytes (heads: m x SG_SPLIT_BYTES host bytes,
  * zero-filled) and min(len, SG_SPLIT_BYTES) (lens), for choosing byte splitters; nothing is
  * written when the buffer has no records; *n_rec = the buffer's record count. */

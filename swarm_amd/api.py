@@ -385,6 +385,31 @@ class Context:
                                          out_cap, pb, pr))
         return list(pb), list(pr)
 
+    def partition_bytes_pieces(self, pieces: Sequence[Tuple[int, int]], splitters: Sequence[bytes], d_out: int,
+                               out_cap: int):
+        """Route (device pointer, bytes) pieces into one part-contiguous buffer d_out. Returns
+        (bytes per part, records per part), totals over the pieces."""
+        blob, offs = _keys_blob(list(splitters))
+        parts = len(splitters) + 1
+        k = len(pieces)
+        ptrs = (C.c_void_p * max(1, k))(*[C.c_void_p(p) for p, _ in pieces])
+        lens = (C.c_size_t * max(1, k))(*[n for _, n in pieces])
+        pb = (C.c_uint64 * parts)()
+        pr = (C.c_uint64 * parts)()
+        check(lib.sg_dev_partition_bytes_pieces(self._h, ptrs, lens, k, blob.ctypes.data,
+                                                offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts,
+                                                C.c_void_p(d_out) if d_out else None, out_cap, pb, pr))
+        return list(pb), list(pr)
+
+    def dedup_diff_into(self, d_cur: int, n_cur: int, d_prior: int, n_prior: int, d_uniq: int, uniq_cap: int,
+                        d_fresh: int, fresh_cap: int) -> _abi.DevResult:
+        """dedup_diff with both outputs written at caller device addresses (capacities >= n_cur + 1)."""
+        r = _abi.DevResult()
+        check(lib.sg_dev_dedup_diff_into(self._h, C.c_void_p(d_cur) if d_cur else None, n_cur,
+                                         C.c_void_p(d_prior) if d_prior else None, n_prior, C.c_void_p(d_uniq),
+                                         uniq_cap, C.c_void_p(d_fresh) if d_fresh else None, fresh_cap, C.byref(r)))
+        return r
+
     def record_sample(self, d_buf: int, n: int, m: int) -> Tuple[List[bytes], int]:
         """(the first SPLIT_BYTES bytes of m evenly spaced records — [] when the buffer has
         no records —, record count)."""

@@ -181,30 +181,53 @@ __device__ __forceinline__ bool head_less(const uint64_t (&w)[SPL_WORDS], uint32
     return r ? r < 0 : len < slen;
 }
 
+// Ordering by key0 first: record key0 vs splitter key0 (both the first 7 bytes + min(len, 8))
+// decides unless they are equal with tag 8; only then are the first 64 bytes loaded and
+// compared word by word (host:port records: one or two 8-B loads per record instead of
+// eight; URL records share key0 and take the word compare).
 __global__ __launch_bounds__(256) void k_range_bytes(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                                      uint32_t R, const uint64_t *__restrict__ split_w,
                                                      const uint32_t *__restrict__ split_len, uint32_t ns,
                                                      uint64_t *keys, unsigned long long *cnt /* [2*parts] */) {
     __shared__ unsigned long long s_c[2 * 256];
     __shared__ uint64_t s_w[255 * SPL_WORDS];
+    __shared__ uint64_t s_k0[256];
     __shared__ uint32_t s_len[256];
     for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) s_c[i] = 0;
     for (uint32_t i = threadIdx.x; i < ns * SPL_WORDS; i += blockDim.x) s_w[i] = split_w[i];
-    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) s_len[i] = split_len[i];
+    for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
+        const uint32_t l = split_len[i];
+        s_len[i] = l;
+        s_k0[i] = (split_w[i * SPL_WORDS] & ~0xffull) | (uint64_t)(l < 8u ? l : 8u);
+    }
     __syncthreads();
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < R; i0 += gridDim.x * blockDim.x) {
         const uint32_t i = i0 + threadIdx.x;
         uint32_t lo = 0, bytes = 0;
         if (i < R) {
             const uint2 x = spans[i];
+            const uint64_t rk = chunk_key(buf, x.x, x.y, 0);
             uint64_t w[SPL_WORDS];
-            head_words(buf, x.x, x.y, w);
-#pragma unroll
-            for (uint32_t k = 0; k < SPL_WORDS; ++k) w[k] = __builtin_bswap64(w[k]);
+            bool loaded = false;
             uint32_t hi = ns;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (!head_less(w, x.y - x.x, s_w + mid * SPL_WORDS, s_len[mid])) lo = mid + 1; else hi = mid;
+                const uint64_t sk = s_k0[mid];
+                bool less;
+                if (rk != sk) {
+                    less = rk < sk;
+                } else if ((rk & 0xffu) < 8u) {
+                    less = false;  // the same record bytes: splitter <= record
+                } else {
+                    if (!loaded) {
+                        head_words(buf, x.x, x.y, w);
+#pragma unroll
+                        for (uint32_t k = 0; k < SPL_WORDS; ++k) w[k] = __builtin_bswap64(w[k]);
+                        loaded = true;
+                    }
+                    less = head_less(w, x.y - x.x, s_w + mid * SPL_WORDS, s_len[mid]);
+                }
+                if (!less) lo = mid + 1; else hi = mid;
             }
             keys[i] = lo;
             bytes = x.y - x.x + 1;
@@ -311,6 +334,35 @@ struct ByteSplit {
     uint64_t w[255 * SPL_WORDS];
     uint32_t len[256];
 };
+
+// Splitter q = splitters[split_offs[q] .. split_offs[q+1]) cut to SPL_W bytes, packed as BE
+// words; the cut splitters must be non-decreasing in byte order.
+static int pack_byte_splitters(const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, ByteSplit *bs) {
+    memset(bs, 0, sizeof(*bs));
+    for (uint32_t q = 0; q + 1 < n_parts; ++q) {
+        if (split_offs[q + 1] < split_offs[q]) { set_error("split_offs must be non-decreasing"); return SG_E_INVAL; }
+        const uint32_t len = std::min<uint32_t>(split_offs[q + 1] - split_offs[q], SPL_W);
+        uint8_t b[SPL_W] = {0};
+        memcpy(b, splitters + split_offs[q], len);
+        for (uint32_t k = 0; k < SPL_WORDS; ++k) {
+            uint64_t v = 0;
+            for (uint32_t j = 0; j < 8; ++j) v = (v << 8) | b[8 * k + j];
+            bs->w[q * SPL_WORDS + k] = v;
+        }
+        bs->len[q] = len;
+        if (q > 0) {
+            const uint64_t *a = bs->w + (q - 1) * SPL_WORDS, *w = bs->w + q * SPL_WORDS;
+            int r = 0;
+            for (uint32_t k = 0; k < SPL_WORDS && !r; ++k)
+                if (a[k] != w[k]) r = a[k] < w[k] ? -1 : 1;
+            if (r > 0 || (r == 0 && bs->len[q - 1] > len)) {
+                set_error("splitters must be non-decreasing in byte order (splitter %u)", q);
+                return SG_E_INVAL;
+            }
+        }
+    }
+    return SG_OK;
+}
 
 // Hash routing (split == null), range routing by key0 splitters, or by byte splitters
 // (bsplit) — parts - 1 of them.
@@ -431,6 +483,20 @@ int sg_dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, const uint8
     return dev_dedup_diff(c, cur, n_cur, prior, n_prior, true, res);
 }
 
+int sg_dev_dedup_diff_into(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, const uint8_t *d_prior, size_t n_prior,
+                           uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap, sg_dev_result *res) {
+    if (!c || !res || (!d_cur && n_cur) || (!d_prior && n_prior) || !d_uniq) {
+        set_error("sg_dev_dedup_diff_into: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (n_cur > MAX_BYTES || n_prior > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *cur, *prior = nullptr;
+    SG_TRY(aligned_in(c, S_IN, d_cur, n_cur, &cur));
+    if (n_prior) SG_TRY(aligned_in(c, S_IN2, d_prior, n_prior, &prior));
+    return dev_dedup_diff_into(c, cur, n_cur, prior, n_prior, d_uniq, uniq_cap, d_fresh, fresh_cap, res);
+}
+
 int sg_dev_partition_range(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint64_t *splitters, uint32_t n_parts,
                            uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
     if (!c || (!d_out && n) || (!d_buf && n) || (!splitters && n_parts > 1)) {
@@ -455,33 +521,107 @@ int sg_dev_partition_bytes(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint
     if (n_parts == 0 || n_parts > 256) { set_error("n_parts must be in 1..256"); return SG_E_INVAL; }
     if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
     static thread_local ByteSplit bs;
-    memset(&bs, 0, sizeof(bs));
-    for (uint32_t q = 0; q + 1 < n_parts; ++q) {
-        if (split_offs[q + 1] < split_offs[q]) { set_error("split_offs must be non-decreasing"); return SG_E_INVAL; }
-        const uint32_t len = std::min<uint32_t>(split_offs[q + 1] - split_offs[q], SPL_W);
-        uint8_t b[SPL_W] = {0};
-        memcpy(b, splitters + split_offs[q], len);
-        for (uint32_t k = 0; k < SPL_WORDS; ++k) {
-            uint64_t v = 0;
-            for (uint32_t j = 0; j < 8; ++j) v = (v << 8) | b[8 * k + j];
-            bs.w[q * SPL_WORDS + k] = v;
-        }
-        bs.len[q] = len;
-        if (q > 0) {  // (cut) splitters must be non-decreasing in byte order
-            const uint64_t *a = bs.w + (q - 1) * SPL_WORDS, *w = bs.w + q * SPL_WORDS;
-            int r = 0;
-            for (uint32_t k = 0; k < SPL_WORDS && !r; ++k)
-                if (a[k] != w[k]) r = a[k] < w[k] ? -1 : 1;
-            if (r > 0 || (r == 0 && bs.len[q - 1] > len)) {
-                set_error("splitters must be non-decreasing in byte order (splitter %u)", q);
-                return SG_E_INVAL;
-            }
-        }
-    }
+    SG_TRY(pack_byte_splitters(splitters, split_offs, n_parts, &bs));
     SG_HIP(hipSetDevice(c->device));
     const uint8_t *b;
     SG_TRY(aligned_in(c, S_IN, d_buf, n, &b));
     return dev_partition(c, b, n, n_parts, d_out, out_cap, part_bytes, part_records, nullptr, &bs);
+}
+
+int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                  const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out,
+                                  size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
+    if (!c || (k && (!d_pieces || !lens)) || ((!splitters || !split_offs) && n_parts > 1)) {
+        set_error("sg_dev_partition_bytes_pieces: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (n_parts == 0 || n_parts > 256) { set_error("n_parts must be in 1..256"); return SG_E_INVAL; }
+    uint64_t total_in = 0;
+    for (size_t j = 0; j < k; ++j) {
+        if (!d_pieces[j] && lens[j]) { set_error("piece %zu is NULL", j); return SG_E_INVAL; }
+        if (lens[j] > MAX_BYTES) { set_error("piece %zu exceeds 4 GiB", j); return SG_E_TOO_LARGE; }
+        total_in += lens[j];
+    }
+    if (total_in && !d_out) { set_error("sg_dev_partition_bytes_pieces: d_out is NULL"); return SG_E_INVAL; }
+    static thread_local ByteSplit bs;
+    SG_TRY(pack_byte_splitters(splitters, split_offs, n_parts, &bs));
+    SG_HIP(hipSetDevice(c->device));
+    const uint32_t ns = n_parts - 1;
+    uint64_t *d_w;
+    SG_TRY(slot(c, S_M_TMP2, sizeof(ByteSplit) / 8, &d_w));
+    SG_HIP(hipMemcpyAsync(d_w, &bs, sizeof(ByteSplit), hipMemcpyHostToDevice, c->stream));
+    const uint32_t *d_len = reinterpret_cast<const uint32_t *>(d_w + 255 * SPL_WORDS);
+    // pass 1: per-piece (records, bytes) of every part, one readback for all pieces
+    unsigned long long *cnt;
+    SG_TRY(slot(c, S_PART, (size_t)std::max<size_t>(k, 1) * 512, &cnt));
+    SG_HIP(hipMemsetAsync(cnt, 0, std::max<size_t>(k, 1) * 512 * 8, c->stream));
+    for (size_t j = 0; j < k; ++j) {
+        if (!lens[j]) continue;
+        const uint8_t *b;
+        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &b));
+        Lines L;
+        SG_TRY(run_lines(c, b, lens[j], CUR_SLOTS, &L, false, true));
+        if (!L.n_rec) continue;
+        uint64_t *keys;
+        SG_TRY(slot(c, S_KEYS2, L.n_rec, &keys));
+        SG_LAUNCH_B(c, "range_bytes", 24.0 * L.n_rec, k_range_bytes, std::min<uint32_t>((L.n_rec + 255) / 256, 2048u), 256, 0,
+                    b, L.spans, L.n_rec, d_w, d_len, ns, keys, cnt + 512 * j);
+    }
+    std::vector<uint64_t> h(std::max<size_t>(k, 1) * 512, 0);
+    SG_TRY(ctx_readback(c, h.data(), cnt, h.size() * 8));
+    // destinations: part p = pieces' part-p records in piece order
+    std::vector<uint64_t> pbase(n_parts + 1, 0), prec(n_parts, 0);
+    for (uint32_t q = 0; q < n_parts; ++q) {
+        uint64_t bq = 0, rq = 0;
+        for (size_t j = 0; j < k; ++j) { rq += h[512 * j + q]; bq += h[512 * j + n_parts + q]; }
+        pbase[q + 1] = pbase[q] + bq;
+        prec[q] = rq;
+    }
+    if (pbase[n_parts] > out_cap) {
+        set_error("output capacity %zu < %llu", out_cap, (unsigned long long)pbase[n_parts]);
+        return SG_E_CAP;
+    }
+    for (uint32_t q = 0; q < n_parts; ++q) {
+        if (part_bytes) part_bytes[q] = pbase[q + 1] - pbase[q];
+        if (part_records) part_records[q] = prec[q];
+    }
+    // pass 2: per piece, stable sort by part, then each part's records straight to its place
+    std::vector<uint64_t> acc(pbase.begin(), pbase.end() - 1);
+    for (size_t j = 0; j < k; ++j) {
+        if (!lens[j]) continue;
+        const uint8_t *b;
+        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &b));
+        Lines L;
+        SG_TRY(run_lines(c, b, lens[j], CUR_SLOTS, &L, false, true));
+        const uint32_t R = L.n_rec;
+        if (!R) continue;
+        unsigned long long *scr;
+        SG_TRY(slot(c, S_M_CNT, 2 * 256, &scr));
+        SG_HIP(hipMemsetAsync(scr, 0, 2 * 256 * 8, c->stream));
+        uint64_t *keys, *keys2;
+        uint32_t *v1, *v2;
+        SG_TRY(slot(c, S_KEYS2, R, &keys));
+        SG_TRY(slot(c, S_R_KEY2, R, &keys2));
+        SG_TRY(slot(c, S_VALS, R, &v1));
+        SG_TRY(slot(c, S_VALS2, R, &v2));
+        SG_LAUNCH_B(c, "range_bytes", 24.0 * R, k_range_bytes, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, b, L.spans, R,
+                    d_w, d_len, ns, keys, scr);
+        uint64_t *K;
+        uint32_t *V;
+        SG_TRY(radix_sort(c, keys, v1, keys2, v2, R, 0, 8, true, &K, &V, "rs_pass_part"));
+        uint64_t r0 = 0;
+        for (uint32_t q = 0; q < n_parts; ++q) {
+            const uint64_t rq = h[512 * j + q], bq = h[512 * j + n_parts + q];
+            if (rq) {
+                uint8_t *dst = d_out + acc[q];
+                uint8_t *dbase = reinterpret_cast<uint8_t *>((uintptr_t)dst & ~(uintptr_t)15);
+                SG_TRY(emit_into(c, b, L.spans, V + r0, (uint32_t)rq, dbase, (uint32_t)(dst - dbase)));
+                acc[q] += bq;
+            }
+            r0 += rq;
+        }
+    }
+    return SG_OK;
 }
 
 int sg_dev_record_sample(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t m, uint8_t *heads, uint32_t *lens,

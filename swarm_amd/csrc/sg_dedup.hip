@@ -42,10 +42,12 @@ constexpr uint32_t WAVE_GROUP = 64;
 typedef void (*EmitApplyFn)(const uint2 *, uint32_t, const uint64_t *, const uint8_t *, uint8_t *, uint2 *,
                             const uint64_t *, uint64_t *, int);
 
+// dst_shift (< 16): the output starts dst_shift bytes past the 16-B aligned `dst` (byte
+// offsets and out_spans include it; the total does not).
 template <class Item>
 static int run_emit(sg_ctx *c, EmitApplyFn kern, const char *name, const char *cname, int status_slot, Item item, uint32_t n,
                     const uint8_t *src, uint8_t *dst, uint2 *out_spans, const uint64_t *kin, uint64_t *kout,
-                    uint64_t **total_out, double bytes_model) {
+                    uint64_t **total_out, double bytes_model, uint32_t dst_shift = 0) {
     const uint32_t ntiles = (n + EM_TILE - 1) / EM_TILE;
     uint64_t *tp;  // tot[ntiles] | pre[ntiles] | total
     SG_TRY(slot(c, status_slot, 2 * (size_t)ntiles + 4, &tp));
@@ -59,7 +61,7 @@ static int run_emit(sg_ctx *c, EmitApplyFn kern, const char *name, const char *c
     SG_TRY(slot(c, S_ECACHE, (size_t)n + 1, &cache));
     static const int dbg = getenv("SG_EMIT_DEBUG") ? atoi(getenv("SG_EMIT_DEBUG")) : 0;
     SG_LAUNCH(c, cname, k_emit_count<Item>, ntiles, EM_BLOCK, 0, item, n, cache, tot);
-    SG_TRY(tile_scan(c, tot, ntiles, pre, total));
+    SG_TRY(tile_scan(c, tot, ntiles, pre, total, dst_shift));
     SG_LAUNCH_B(c, name, bytes_model, kern, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin,
                 kout, dbg & 1);
     return SG_OK;
@@ -680,6 +682,15 @@ int serialize(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
     return emit_records(c, d_buf, spans, recs, count, out_slot, nullptr, 0, d_out, bytes);
 }
 
+// Records recs[0..count) of d_buf, '\n'-terminated, written from dst_base + shift on (no
+// host sync: the caller knows the byte count).
+int emit_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, const uint32_t *recs, uint32_t count,
+              uint8_t *dst_base, uint32_t shift) {
+    uint64_t *tot;
+    return run_emit(c, k_emit_apply, "part_emit", "part_emit.count", S_EMIT, PermItem{recs, spans}, count, d_buf, dst_base,
+                    nullptr, nullptr, nullptr, &tot, 0.0, shift);
+}
+
 int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes) {
     uint8_t *o;
@@ -764,8 +775,17 @@ static const ViewSlots PRIOR_VIEW = {PRIOR_SLOTS, S_P_UBUF, S_P_USPANS, S_P_UKEY
 
 // `pre`: the buffer's lines already parsed (and, for a trusted view, `trust_sorted` already
 // decided by the caller's check_sorted), so no parse or sortedness check is queued here.
+// A caller output (dst, capacity >= n + 1) replaces the unique-view slot: the unique records
+// are written from dst on (the view's buf is dst rounded down to 16 B, its spans shifted).
+struct OutBuf {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    uint8_t *base() const { return reinterpret_cast<uint8_t *>((uintptr_t)p & ~(uintptr_t)15); }
+    uint32_t shift() const { return (uint32_t)((uintptr_t)p & 15); }
+};
+
 static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
-                        UView *uv, const Lines *pre = nullptr, uint32_t base = 0) {
+                        UView *uv, const Lines *pre = nullptr, uint32_t base = 0, const OutBuf *dst = nullptr) {
     *uv = UView{};
     Lines L;
     if (pre) L = *pre;
@@ -795,12 +815,13 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
                 uint8_t *ub;
                 uint2 *us;
                 uint64_t *uk;
-                SG_TRY(slot(c, vs.ubuf, (size_t)n + 64, &ub));
+                if (dst) ub = dst->base();
+                else SG_TRY(slot(c, vs.ubuf, (size_t)n + 64, &ub));
                 SG_TRY(slot(c, vs.uspans, 1, &us));
                 SG_TRY(slot(c, vs.ukeys, 1, &uk));
                 uint64_t *cnt;
                 SG_TRY(run_emit(c, k_emit_uniq, "emit_uniq", "emit_uniq.count", S_EMIT2, PermItem{nullptr, L.spans}, R, d_buf, ub,
-                                us, L.keys, uk, &cnt, 0.0));
+                                us, L.keys, uk, &cnt, 0.0, dst ? dst->shift() : 0u));
                 uint64_t t = 0;
                 SG_TRY(ctx_readback(c, &t, cnt, 8));
                 *uv = UView{ub, us, uk, (uint32_t)(t >> 32), (uint32_t)t, R};
@@ -808,7 +829,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
             return SG_OK;
         }
         uint8_t *ub;
-        SG_TRY(slot(c, vs.ubuf, 64, &ub));
+        if (dst) ub = dst->base();
+        else SG_TRY(slot(c, vs.ubuf, 64, &ub));
         uv->buf = ub;
         return SG_OK;  // R == 0
     }
@@ -893,12 +915,13 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint8_t *ub;
     uint2 *us;
     uint64_t *uk;
-    SG_TRY(slot(c, vs.ubuf, (size_t)n + 64, &ub));
+    if (dst) ub = dst->base();
+    else SG_TRY(slot(c, vs.ubuf, (size_t)n + 64, &ub));
     SG_TRY(slot(c, vs.uspans, R, &us));
     SG_TRY(slot(c, vs.ukeys, R, &uk));
     uint64_t *uc;
     SG_TRY(run_emit(c, k_emit_uniq, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
-                    0.0));
+                    0.0, dst ? dst->shift() : 0u));
     // the output count and the run-sort error word come back with one host sync
     uint8_t *pin = (uint8_t *)c->pinned;
     SG_HIP(hipMemcpyAsync(pin, uc, 8, hipMemcpyDeviceToHost, c->stream));
@@ -919,7 +942,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
 }
 
 static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
-                                uint64_t n_prior, bool want_fresh, sg_dev_result *res, const Lines *cur_pre = nullptr) {
+                                uint64_t n_prior, bool want_fresh, sg_dev_result *res, const Lines *cur_pre = nullptr,
+                                const OutBuf *ou = nullptr, const OutBuf *of = nullptr) {
     *res = sg_dev_result{};
     UView pv;
     const bool have_prior = want_fresh && d_prior && n_prior;
@@ -968,9 +992,9 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     }
     if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, base));
     UView cu;
-    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, base));
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, base, ou));
     res->in_records = cu.in_records;
-    res->uniq = const_cast<uint8_t *>(cu.buf);
+    res->uniq = ou ? ou->p : const_cast<uint8_t *>(cu.buf);
     res->uniq_bytes = cu.bytes;
     res->uniq_records = cu.n;
     if (!want_fresh) return SG_OK;
@@ -979,6 +1003,12 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         res->fresh = res->uniq;
         res->fresh_bytes = res->uniq_bytes;
         res->fresh_records = res->uniq_records;
+        if (of && res->fresh_bytes) {  // caller outputs: the new records are all of them, copied
+            SG_HIP(hipMemcpyAsync(of->p, res->uniq, res->fresh_bytes, hipMemcpyDeviceToDevice, c->stream));
+            res->fresh = of->p;
+        } else if (of) {
+            res->fresh = of->p;
+        }
         return SG_OK;
     }
     uint8_t *fresh;
@@ -994,17 +1024,30 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     SG_LAUNCH_B(c, "diff_tile", 16.0 * cu.n + 8.0 * pv.n + (double)cu.bytes + cu.n, k_diff_tile, ntiles, 256, 0,
                 U, P, jb, fresh, base);
     uint8_t *fout;
-    SG_TRY(slot(c, S_OUT_FRESH, (size_t)cu.bytes + 64, &fout));
+    if (of) fout = of->base();
+    else SG_TRY(slot(c, S_OUT_FRESH, (size_t)cu.bytes + 64, &fout));
     uint64_t *fc;
     SG_TRY(run_emit(c, k_emit_fresh, "emit_fresh", "emit_fresh.count", S_EMIT3, FlagItem{cu.spans, fresh, 1}, cu.n, cu.buf, fout,
-                    nullptr, nullptr, nullptr, &fc, 0.0));
+                    nullptr, nullptr, nullptr, &fc, 0.0, of ? of->shift() : 0u));
     uint64_t tt = 0;
     SG_TRY(ctx_readback(c, &tt, fc, 8));
     if (c->profile) prof_bytes(c, "emit_fresh", 8.0 * cu.n + 2.0 * (double)(uint32_t)tt);
-    res->fresh = fout;
+    res->fresh = of ? of->p : fout;
     res->fresh_bytes = (uint32_t)tt;
     res->fresh_records = (uint32_t)(tt >> 32);
     return SG_OK;
+}
+
+int dev_dedup_diff_into(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior, uint64_t n_prior,
+                        uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap, sg_dev_result *res) {
+    if (uniq_cap < n_cur + 1 || (d_fresh && fresh_cap < n_cur + 1)) {
+        set_error("output capacities must be >= n_cur + 1 (%llu)", (unsigned long long)(n_cur + 1));
+        return SG_E_CAP;
+    }
+    c->last_path = 0;
+    c->last_flags = 0;
+    const OutBuf ou{d_uniq, uniq_cap}, of{d_fresh, fresh_cap};
+    return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, true, res, nullptr, &ou, d_fresh ? &of : nullptr);
 }
 
 int dev_dedup_diff_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &cur, const uint8_t *d_prior,

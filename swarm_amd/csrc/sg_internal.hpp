@@ -9,7 +9,9 @@ void pool_release(sg_ctx *c);
 int pick_device(int *dev);
 
 // Exclusive scan of nt per-tile u64 aggregates into pre; the sum into *total (device).
-int tile_scan(sg_ctx *c, const uint64_t *tot, uint32_t nt, uint64_t *pre, uint64_t *total);
+// pre[t] = init + exclusive prefix of tot (packed (count << 32 | bytes) aggregates: init
+// shifts the byte offsets, e.g. to a destination that starts mid-word); total excludes init.
+int tile_scan(sg_ctx *c, const uint64_t *tot, uint32_t nt, uint64_t *pre, uint64_t *total, uint64_t init = 0);
 
 // Slot sets let the cur and prior buffers be parsed/sorted without sharing buffers.
 struct SlotSet {
@@ -50,6 +52,10 @@ int serialize(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
               const uint32_t *list, const uint32_t *map, uint32_t count, int out_slot,
               uint8_t **d_out, uint64_t *bytes);
 // Same, into a caller buffer of dst_cap bytes (SG_E_CAP if too small).
+int emit_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, const uint32_t *recs, uint32_t count,
+              uint8_t *dst_base, uint32_t shift);
+int dev_dedup_diff_into(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior, uint64_t n_prior,
+                        uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap, sg_dev_result *res);
 int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes);
 

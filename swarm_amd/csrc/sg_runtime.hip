@@ -256,7 +256,8 @@ int sg_ctx_reset_stats(sg_ctx *c) {
 namespace sg {
 
 __global__ __launch_bounds__(TS_BLOCK) void k_tile_scan(const uint64_t *__restrict__ tot, uint32_t nt,
-                                                        uint64_t *__restrict__ pre, uint64_t *__restrict__ total) {
+                                                        uint64_t *__restrict__ pre, uint64_t *__restrict__ total,
+                                                        uint64_t init) {
     __shared__ uint64_t s_red[TS_BLOCK / 64];
     uint64_t carry = 0;
     for (uint32_t base = 0; base < nt; base += TS_BLOCK * TS_ITEMS) {
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(TS_BLOCK) void k_tile_scan(const uint64_t *__restri
         uint64_t run = carry + ex;
 #pragma unroll
         for (int j = 0; j < TS_ITEMS; ++j) {
-            if (i0 + j < nt) pre[i0 + j] = run;
+            if (i0 + j < nt) pre[i0 + j] = init + run;
             run += v[j];
         }
         carry += btot;
@@ -281,8 +282,8 @@ __global__ __launch_bounds__(TS_BLOCK) void k_tile_scan(const uint64_t *__restri
     if (threadIdx.x == 0) *total = carry;
 }
 
-int tile_scan(sg_ctx *c, const uint64_t *tot, uint32_t nt, uint64_t *pre, uint64_t *total) {
-    SG_LAUNCH(c, "tile_scan", k_tile_scan, 1, TS_BLOCK, 0, tot, nt, pre, total);
+int tile_scan(sg_ctx *c, const uint64_t *tot, uint32_t nt, uint64_t *pre, uint64_t *total, uint64_t init) {
+    SG_LAUNCH(c, "tile_scan", k_tile_scan, 1, TS_BLOCK, 0, tot, nt, pre, total, init);
     return SG_OK;
 }
 

@@ -197,10 +197,13 @@ def gather_lines(local: bytes, group=None) -> bytes:
     return b"".join(allv)
 
 
-def dedup_diff_range_step(ctx, cur_pieces, prior_local, gsplit, lsplit, group=None):
+def dedup_diff_range_step(ctx, cur_pieces, prior_local, gsplit, lsplit, group=None, prior_parts=None):
     """One C5 step on this rank: range exchange (world > 1), then local range parts
-    (sharded.dedup_diff_large with the rank's fixed local splitters)."""
+    (sharded.dedup_diff_large with the rank's fixed local splitters). prior_parts: the
+    rank's stored prior already split by lsplit (then prior_local is not routed again)."""
     from . import sharded
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     mine = range_exchange(ctx, cur_pieces, gsplit, group) if world > 1 else list(cur_pieces)
+    if prior_parts is not None:
+        return sharded.dedup_diff_large(ctx, mine, (), splitters=lsplit, prior_parts=prior_parts)
     return sharded.dedup_diff_large(ctx, mine, prior_local, splitters=lsplit)

@@ -96,18 +96,32 @@ def route_piece(ctx, p, splitters, out_ptr: int, out_cap: int):
 
 
 def route(ctx, pieces: Sequence, splitters) -> List:
-    """Route every piece into n_splitters + 1 parts; returns one device tensor per part
-    (the part's records from all pieces, in piece order; None for an empty part)."""
+    """Route every piece into n_splitters + 1 parts; returns one device tensor per part (the
+    part's records from all pieces, in piece order; None for an empty part). Byte splitters:
+    one sg_dev_partition_bytes_pieces call writes every part contiguously into one buffer
+    (the part tensors are views of it). Key0 splitters: per piece, then joined."""
     import torch
     parts = n_splitters(splitters) + 1
+    live = [p for p in pieces if p is not None and p.numel()]
+    if isinstance(splitters, (list, tuple)):
+        if not live:
+            return [None] * parts
+        total = sum(p.numel() for p in live)
+        out = torch.empty(total + len(live) + 16, dtype=torch.uint8, device=live[0].device)
+        ctx.fence_in()  # `out` may be a block torch's stream is still reading (ADVICE r1)
+        pb, _ = ctx.partition_bytes_pieces([(p.data_ptr(), p.numel()) for p in live], splitters, out.data_ptr(),
+                                           out.numel())
+        res, off = [], 0
+        for b in range(parts):
+            res.append(out[off:off + pb[b]] if pb[b] else None)
+            off += pb[b]
+        return res
     lists: List[list] = [[] for _ in range(parts)]
     keep = []
-    for p in pieces:
+    for p in live:
         n = p.numel()
-        if n == 0:
-            continue
         out = torch.empty(n + 16, dtype=torch.uint8, device=p.device)
-        ctx.fence_in()  # `out` may be a block torch's stream is still reading (ADVICE r1)
+        ctx.fence_in()
         pb = route_piece(ctx, p, splitters, out.data_ptr(), out.numel())
         off = 0
         for b in range(parts):
@@ -127,13 +141,16 @@ def route(ctx, pieces: Sequence, splitters) -> List:
     return res
 
 
-def _take(ctx, dptr: int, n: int, device):
-    import torch
-    t = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
-    if n:
-        ctx.fence_in()
-        ctx.memcpy(t.data_ptr(), dptr, n)
-    return t[:n]
+class _Results:
+    """The unique and new-record outputs of all parts, appended in part order into two
+    preallocated device buffers (each part's dedup call writes there directly)."""
+
+    def __init__(self, cap: int, device, want_fresh: bool):
+        import torch
+        self.u = torch.empty(cap, dtype=torch.uint8, device=device)
+        self.f = torch.empty(cap, dtype=torch.uint8, device=device) if want_fresh else None
+        self.uo = 0
+        self.fo = 0
 
 
 def plan_parts(cur_pieces: Sequence, prior_pieces: Sequence, part_bytes: int) -> int:
@@ -142,12 +159,14 @@ def plan_parts(cur_pieces: Sequence, prior_pieces: Sequence, part_bytes: int) ->
 
 
 def dedup_diff_large(ctx, cur_pieces: Sequence, prior_pieces: Sequence = (), part_bytes: int = 2 << 30,
-                     samples_per_piece: int = 1 << 12, splitters=None):
+                     samples_per_piece: int = 1 << 12, splitters=None, prior_parts: Sequence | None = None):
     """(sort -u of all cur records, new records vs prior, stats) as device tensors, each in
     global byte order, for shards of any size. `prior_pieces` is the prior scan (sorted
     unique or not). `splitters` may be given (byte strings or key0 values, e.g. agreed
     across ranks); otherwise byte splitters are chosen from records sampled from every
-    piece."""
+    piece. `prior_parts` (with `splitters`): the prior already split by those splitters — the
+    stored prior scan is this function's own part-ordered output, so it need not be routed
+    again (st["uniq_part_bytes"] gives the part boundaries)."""
     import torch
     cur_pieces = [p for p in cur_pieces if p.numel()]
     prior_pieces = [p for p in prior_pieces if p.numel()]
@@ -155,19 +174,27 @@ def dedup_diff_large(ctx, cur_pieces: Sequence, prior_pieces: Sequence = (), par
     if splitters is None:
         parts = plan_parts(cur_pieces, prior_pieces, part_bytes)
         splitters = choose_splitters(sample_records(ctx, cur_pieces + prior_pieces, samples_per_piece), parts)
+    have_prior = bool(prior_pieces) or (prior_parts is not None and any(p is not None and p.numel()
+                                                                        for p in prior_parts))
     st = {"parts": n_splitters(splitters) + 1, "in_records": 0, "uniq_records": 0, "fresh_records": 0,
-          "max_part_bytes": 0, "rerouted_parts": 0, "part_bytes": []}
-    uniq, fresh = [], []
-    _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, dev, uniq, fresh, st, samples_per_piece)
-    empty = torch.empty(0, dtype=torch.uint8, device=dev)
-    return (torch.cat(uniq) if uniq else empty), (torch.cat(fresh) if fresh else empty), st
+          "max_part_bytes": 0, "rerouted_parts": 0, "part_bytes": [], "uniq_part_bytes": []}
+    out = _Results(sum(p.numel() for p in cur_pieces) + 4096, dev, have_prior)
+    _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, out, st, samples_per_piece, prior_parts=prior_parts)
+    u = out.u[:out.uo]
+    return u, (out.f[:out.fo] if have_prior else u), st
 
 
-def _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, dev, uniq, fresh, st, samples_per_piece,
-                 depth: int = 0):
+def _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, out, st, samples_per_piece, depth: int = 0,
+                 prior_parts=None):
     cur_parts = route(ctx, cur_pieces, splitters)
-    prior_parts = route(ctx, prior_pieces, splitters) if prior_pieces else [None] * (n_splitters(splitters) + 1)
+    if prior_parts is None:
+        prior_parts = route(ctx, prior_pieces, splitters) if prior_pieces else [None] * len(cur_parts)
+    if len(prior_parts) != len(cur_parts):
+        raise ValueError("prior_parts has %d entries for %d parts" % (len(prior_parts), len(cur_parts)))
     for b, (c, p) in enumerate(zip(cur_parts, prior_parts)):
+        if depth == 0:
+            st["uniq_part_bytes"].append(0)
+            u_start = out.uo
         if c is None:
             continue
         pn = p.numel() if p is not None else 0
@@ -180,22 +207,39 @@ def _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, dev, uniq, fresh, st,
             if depth >= 3 or not sub:
                 raise ValueError(part_overflow_message(splitters, b, c.numel(), pn))
             st["rerouted_parts"] += 1
-            _dedup_parts(ctx, [c], [p] if p is not None else [], sub, dev, uniq, fresh, st,
-                         samples_per_piece, depth + 1)
+            _dedup_parts(ctx, [c], [p] if p is not None else [], sub, out, st, samples_per_piece, depth + 1)
+            if depth == 0:
+                st["uniq_part_bytes"][-1] = out.uo - u_start
             continue
         st["max_part_bytes"] = max(st["max_part_bytes"], c.numel())
         st["part_bytes"].append(int(c.numel()))
         ctx.fence_in()
         try:
-            r = ctx.dedup_diff(c.data_ptr(), c.numel(), p.data_ptr() if p is not None else 0, pn)
+            r = ctx.dedup_diff_into(c.data_ptr(), c.numel(), p.data_ptr() if pn else 0, pn,
+                                    out.u.data_ptr() + out.uo, out.u.numel() - out.uo,
+                                    (out.f.data_ptr() + out.fo) if out.f is not None else 0,
+                                    (out.f.numel() - out.fo) if out.f is not None else 0)
         except Exception as e:
             raise type(e)(e.rc, "%s (part of %d bytes at %#x, prior %s)" % (
                 e, c.numel(), c.data_ptr(), None if p is None else pn)) if hasattr(e, "rc") else e
-        uniq.append(_take(ctx, r.uniq, r.uniq_bytes, dev))
-        fresh.append(_take(ctx, r.fresh, r.fresh_bytes, dev) if p is not None else uniq[-1])
+        out.uo += int(r.uniq_bytes)
+        if depth == 0:
+            st["uniq_part_bytes"][-1] = out.uo - u_start
+        if out.f is not None:
+            out.fo += int(r.fresh_bytes)
         st["in_records"] += int(r.in_records)
         st["uniq_records"] += int(r.uniq_records)
-        st["fresh_records"] += int(r.fresh_records) if p is not None else int(r.uniq_records)
+        st["fresh_records"] += int(r.fresh_records)
+
+
+def split_parts(buf, part_bytes: Sequence[int]) -> List:
+    """Views of a part-ordered buffer (e.g. dedup_diff_large's unique output with
+    st["uniq_part_bytes"]): one per part, None where empty."""
+    res, off = [], 0
+    for n in part_bytes:
+        res.append(buf[off:off + n] if n else None)
+        off += n
+    return res
 
 
 def pieces_bytes(pieces) -> Tuple[int, int]:

@@ -217,3 +217,69 @@ def test_identical_records_past_the_limit_raise(ctx, monkeypatch):
     same = b"".join(b"x" * 70 + b"%d\n" % (i % 3) for i in range(5_000))
     with pytest.raises(ValueError, match="share their first 64 bytes"):
         sharded.dedup_diff_large(ctx, [dev(same)], (), part_bytes=50_000)
+
+
+def test_partition_pieces_part_contiguous(ctx):
+    """k pieces (unaligned starts, an empty piece, no final newline) routed into one buffer:
+    part p = the pieces' part-p records in piece order (route_parts per piece, joined)."""
+    import torch
+    recs = shared_prefix_records(30_000, 11)
+    data = b"\n".join(recs) + b"\n"
+    cuts = [0, 7, len(data) // 3, len(data) // 3, len(data)]
+    cuts = [c if c in (0, len(data)) else data.index(b"\n", c) + 1 for c in cuts]
+    d = dev(b"#" + data)  # pieces start at odd addresses
+    pieces = [d[1 + a:1 + b] for a, b in zip(cuts, cuts[1:])]
+    sp = sorted(random.Random(12).sample(recs, 20))
+    out = torch.full((len(data) + 64,), 0x55, dtype=torch.uint8, device=d.device)
+    pb, pr = ctx.partition_bytes_pieces([(p.data_ptr(), p.numel()) for p in pieces], sp, out.data_ptr(), out.numel())
+    per_piece = [route_parts(data[a:b], sp) for a, b in zip(cuts, cuts[1:])]
+    want = [b"".join(pp[q] for pp in per_piece) for q in range(len(sp) + 1)]
+    assert pb == [len(w) for w in want]
+    assert pr == [len(S.parse_records(w)) for w in want]
+    got = out.cpu().numpy().tobytes()
+    assert got[: sum(pb)] == b"".join(want)
+    assert set(got[sum(pb):]) == {0x55}
+
+
+@pytest.mark.parametrize("shift", [0, 1, 7, 15])
+def test_dedup_diff_into_any_address(ctx, shift):
+    import torch
+    buf, ids = corpus.subdomains(30_000, seed=40 + shift)
+    prior = corpus.prior_of(ids).tobytes()
+    cur = buf.tobytes()
+    dc, dp = dev(cur), dev(prior)
+    cap = len(cur) + 1
+    ub = torch.full((cap + 64,), 0xEE, dtype=torch.uint8, device=dc.device)
+    fb = torch.full((cap + 64,), 0xEE, dtype=torch.uint8, device=dc.device)
+    r = ctx.dedup_diff_into(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior), ub.data_ptr() + shift, cap,
+                            fb.data_ptr() + shift, cap)
+    eu, ef = S.dedup_diff(cur, prior)
+    u, f = ub.cpu().numpy().tobytes(), fb.cpu().numpy().tobytes()
+    assert u[shift:shift + r.uniq_bytes] == eu and f[shift:shift + r.fresh_bytes] == ef
+    assert set(u[:shift] + u[shift + r.uniq_bytes:]) <= {0xEE} and set(f[:shift] + f[shift + r.fresh_bytes:]) <= {0xEE}
+    assert r.uniq == ub.data_ptr() + shift and r.fresh == fb.data_ptr() + shift
+    # no prior: the new records are all unique records, copied into the fresh output
+    r = ctx.dedup_diff_into(dc.data_ptr(), len(cur), 0, 0, ub.data_ptr() + shift, cap, fb.data_ptr() + shift, cap)
+    assert ctx.to_bytes(r.fresh, r.fresh_bytes) == eu == ctx.to_bytes(r.uniq, r.uniq_bytes)
+    from swarm_amd._abi import SGError
+    with pytest.raises(SGError):
+        ctx.dedup_diff_into(dc.data_ptr(), len(cur), 0, 0, ub.data_ptr(), len(cur), fb.data_ptr(), cap)
+
+
+def test_stored_prior_parts_skip_routing(ctx):
+    """The C5 step with the stored prior split at its own part boundaries (no prior routing)
+    equals the routed path and the oracle."""
+    from swarm_amd import sharded
+    buf, ids = corpus.subdomains(400_000, seed=44)
+    prior_raw = corpus.prior_of(ids).tobytes()
+    pieces = sharded.split_at_newlines(dev(prior_raw), 1 << 20)
+    sp = sharded.choose_splitters(sharded.sample_records(ctx, pieces, 256), 6)
+    pu, _, pst = sharded.dedup_diff_large(ctx, pieces, (), splitters=sp)
+    assert len(pst["uniq_part_bytes"]) == len(sp) + 1 and sum(pst["uniq_part_bytes"]) == pu.numel()
+    parts = sharded.split_parts(pu, pst["uniq_part_bytes"])
+    cur = sharded.split_at_newlines(dev(buf.tobytes()), 1 << 20)
+    u, f, _ = sharded.dedup_diff_large(ctx, cur, (), splitters=sp, prior_parts=parts)
+    eu, ef = S.dedup_diff(buf.tobytes(), prior_raw)
+    assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
+    u2, f2, _ = sharded.dedup_diff_large(ctx, cur, [pu], splitters=sp)
+    assert u2.cpu().numpy().tobytes() == eu and f2.cpu().numpy().tobytes() == ef
