@@ -34,7 +34,10 @@ KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_u
                  "re_prefilter": "k_lit_scan", "re_verify": "k_verify", "json_scan": "k_json_scan",
                  "json_emit": "k_json_emit", "tm_eval": "k_tm_eval", "tm_collect": "k_tm_collect",
                  "bk_sort": "k_bk_sort", "bk_l1_apply": "k_bp_apply", "bk_l2_apply": "k_bp_apply",
-                 "bk_l1_count": "k_bp_count", "bk_l2_count": "k_bp_count", "bk_compact": "k_bk_compact"}
+                 "bk_l1_count": "k_bp_count", "bk_l2_count": "k_bp_count", "bk_compact": "k_bk_compact",
+                 "part_emit": "k_emit_apply", "range_bytes": "k_range_bytes", "gather_spans": "k_gather_spans",
+                 "gather_matched": "k_gather_matched", "seg_wave": "k_seg_wave", "seg_small": "k_seg_small",
+                 "rs_up": "k_rs_up", "lcp": "k_lcp", "rekey": "k_rekey"}
 
 
 def pmc_traffic(workload, kernel):
@@ -793,7 +796,7 @@ def bench_urls(args, ctx=None, emit=True):
                    "bytes": int(cur.numel()), "prior_bytes": int(prior.numel())},
         "gbps": round(step_bytes * args.steps / el / 1e9, 2),
         "records": {"in": R, "unique": int(r.uniq_records), "new": int(r.fresh_records)},
-        "roofline": roofline_of(stats, dominant, "c2", full),
+        "roofline": roofline_of(stats, dominant, "urls", full),
         "cpu_baseline": cpu,
         "kernels": kernel_table(full),
         "dedup_path": ctx.last_path()[0],
