@@ -65,7 +65,7 @@ enum Slot : int {
     // bucket sample sort (sg_bucket.hip)
     S_BK_SKEY, S_BK_SSPAN, S_BK_CNT1, S_BK_CNT2, S_BK_SMALL, S_BK_TOT2, S_BK_Q, S_BK_NCUR, S_BK_L1, S_BK_L2,
     S_BK_US, S_BK_FS, S_BK_SPFX, S_BK_DBG, S_BK_RECS, S_BK_NREC,
-    S_M_FLAG, S_M_SP2, S_M_K2,
+    S_M_FLAG, S_M_SP2, S_M_K2, S_R_T2,
     S_NSLOTS
 };
 

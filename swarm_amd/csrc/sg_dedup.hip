@@ -136,13 +136,18 @@ __device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint2 *spa
 }
 
 // ------------------------------------------------------------------ refinement rounds
+// Sorted-order records are ids into `spans` (u32) or the spans themselves (uint2).
+__device__ __forceinline__ uint2 span_of(const uint2 *spans, uint32_t v) { return spans[v]; }
+__device__ __forceinline__ uint2 span_of(const uint2 *, uint2 v) { return v; }
+
 // Expand big groups into member rows: row j -> group index, global position, and the
 // record's chunk key at `off`.
+template <typename VT>
 __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
                                                 const uint2 *__restrict__ spans,
                                                 const uint32_t *__restrict__ GS,
                                                 const uint64_t *__restrict__ goff, uint32_t B,
-                                                const uint32_t *__restrict__ V, uint32_t M,
+                                                const VT *__restrict__ V, uint32_t M,
                                                 uint32_t off, uint64_t *RK, uint32_t *RG,
                                                 uint32_t *RP) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -153,8 +158,8 @@ __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
         if (goff[mid] <= j) lo = mid; else hi = mid;
     }
     const uint32_t pos = GS[lo] + (j - (uint32_t)goff[lo]);
-    const uint32_t r = V[pos];
-    RK[j] = chunk_key(buf, spans[r].x, spans[r].y, off);
+    const uint2 sp = span_of(spans, V[pos]);
+    RK[j] = chunk_key(buf, sp.x, sp.y, off);
     RG[j] = lo;
     RP[j] = pos;
 }
@@ -166,18 +171,21 @@ __global__ void k_gid_keys(const uint32_t *__restrict__ RG, const uint32_t *__re
 }
 
 // Final order of a round: T[i] = record now at final index i; FK its chunk key.
-__global__ void k_round_gather(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, const uint32_t *__restrict__ V,
+template <typename VT>
+__global__ void k_round_gather(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, const VT *__restrict__ V,
                                const uint32_t *__restrict__ RP, const uint32_t *__restrict__ perm,
-                               uint32_t M, uint32_t off, uint32_t *T, uint64_t *FK) {
+                               uint32_t M, uint32_t off, VT *T, uint64_t *FK) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= M) return;
-    const uint32_t r = V[RP[perm[i]]];
+    const VT r = V[RP[perm[i]]];
     T[i] = r;
-    FK[i] = chunk_key(buf, spans[r].x, spans[r].y, off);
+    const uint2 sp = span_of(spans, r);
+    FK[i] = chunk_key(buf, sp.x, sp.y, off);
 }
 
-__global__ void k_round_scatter(const uint32_t *__restrict__ T, const uint32_t *__restrict__ RP,
-                                uint32_t M, uint32_t *V) {
+template <typename VT>
+__global__ void k_round_scatter(const VT *__restrict__ T, const uint32_t *__restrict__ RP,
+                                uint32_t M, VT *V) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < M) V[RP[i]] = T[i];
 }
@@ -702,7 +710,8 @@ int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
 // Positions GS[g]..GE[g] (g < B) are groups of > 64 records sharing their first `off`
 // bytes. Each round sorts every group's members by the next 7-byte chunk (stable), marks
 // sub-segment heads in brk, and keeps the sub-segments that are still > 64 records.
-static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, uint32_t *V, uint8_t *brk,
+template <typename VT>
+static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, VT *V, uint8_t *brk,
                              uint32_t *GS, uint32_t *GE, uint32_t B, uint32_t base) {
     uint32_t off = base + 7;
     while (B > 0) {
@@ -719,7 +728,8 @@ static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans
         SG_TRY(slot(c, S_R_POS, M, &RP));
         SG_TRY(slot(c, S_R_VAL, M, &RV));
         SG_TRY(slot(c, S_R_VAL2, M, &RV2));
-        SG_LAUNCH(c, "round_expand", k_expand, grid_for(M, 256), 256, 0, d_buf, spans, GS, goff, B, V, M, off, RK, RG, RP);
+        SG_LAUNCH(c, "round_expand", k_expand<VT>, grid_for(M, 256), 256, 0, d_buf, spans, GS, goff, B, V, M, off, RK, RG,
+                  RP);
         uint64_t *SK;
         uint32_t *perm;
         SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, 64, true, &SK, &perm, "rs_pass_refine"));
@@ -733,12 +743,15 @@ static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans
         uint64_t *FKs;
         uint32_t *perm2;
         SG_TRY(radix_sort(c, GK, perm, GK2, pv_alt, M, 0, gbits, false, &FKs, &perm2, "rs_pass_refine"));
-        uint32_t *T = (perm2 == perm) ? pv_alt : perm;
+        uint32_t *Tfree = (perm2 == perm) ? pv_alt : perm;
+        VT *T;
+        if constexpr (sizeof(VT) == 4) T = Tfree;
+        else SG_TRY(slot(c, S_R_T2, M, &T));
         uint64_t *FK = (FKs == GK) ? GK2 : GK;
-        SG_LAUNCH(c, "round_gather", k_round_gather, grid_for(M, 256), 256, 0, d_buf, spans, V, RP, perm2, M, off, T, FK);
-        SG_LAUNCH(c, "round_scatter", k_round_scatter, grid_for(M, 256), 256, 0, T, RP, M, V);
-        // perm2/T are free again after the scatter (same stream)
-        uint32_t *NS = perm2, *NE = T;
+        SG_LAUNCH(c, "round_gather", k_round_gather<VT>, grid_for(M, 256), 256, 0, d_buf, spans, V, RP, perm2, M, off, T, FK);
+        SG_LAUNCH(c, "round_scatter", k_round_scatter<VT>, grid_for(M, 256), 256, 0, T, RP, M, V);
+        // perm2 and the free id buffer are reusable after the scatter (same stream)
+        uint32_t *NS = perm2, *NE = Tfree;
         uint32_t B3 = 0, B4 = 0;
         SG_TRY(run_select2(c, "round_mark", RoundGroupPred{FK, RG, RP, brk, M}, M, NS, NE, &B3, &B4));
         if (B3 != B4) { set_error("round group mismatch %u/%u", B3, B4); return SG_E_HIP; }
@@ -835,15 +848,16 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         return SG_OK;  // R == 0
     }
 
-    // sort by key0
+    // sort (key0, span) pairs: the spans come out in sorted order (the records' ids are
+    // never needed, so no gather of spans by id afterwards)
+    // (the parse's span array is the first ping-pong buffer: nothing reads it afterwards)
     uint64_t *k2;
-    uint32_t *v1, *v2;
+    uint2 *v2;
     SG_TRY(slot(c, vs.lines.keys2, R, &k2));
-    SG_TRY(slot(c, vs.lines.vals, R, &v1));
     SG_TRY(slot(c, vs.lines.vals2, R, &v2));
     uint64_t *K;
-    uint32_t *V;
-    SG_TRY(radix_sort(c, L.keys, v1, k2, v2, R, 0, 64, true, &K, &V));
+    uint2 *V;
+    SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V));
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
     uint8_t *brk;
@@ -856,7 +870,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
     if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B, base));
 
-    // The records in this order: SS = the input spans in sorted order, S = the input itself;
+    // The records in this order: SS = the input spans in sorted order (the sort's payload),
+    // S = the input itself;
     // the later passes (adjacent compare, segment sort, unique emit) gather from the input.
     // Measured cheaper than materialising a sorted copy first (C2 2.51 -> 2.30 ms, X1 4.37 ->
     // 3.97 ms): the copy gathered every record once and the unique emit copied ~2/3 of them
@@ -864,18 +879,17 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // SG_MATERIALIZE=1 restores the copy (S contiguous, SS spans into it).
     uint8_t *Sb;
     uint2 *SS;
-    SG_TRY(slot(c, S_SSPANS, R, &SS));
     static const int materialize = getenv("SG_MATERIALIZE") ? atoi(getenv("SG_MATERIALIZE")) : 0;
     if (materialize) {
+        SG_TRY(slot(c, S_SSPANS, R, &SS));
         SG_TRY(slot(c, S_SBUF, (size_t)n + 64, &Sb));
         uint64_t *pc;
         // model: input bytes read + S written once; cached span per record in, span per record out
-        SG_TRY(run_emit(c, k_emit_sorted, "emit_sorted", "emit_sorted.count", S_EMIT, PermItem{V, L.spans}, R, d_buf, Sb, SS,
+        SG_TRY(run_emit(c, k_emit_sorted, "emit_sorted", "emit_sorted.count", S_EMIT, PermItem{nullptr, V}, R, d_buf, Sb, SS,
                         nullptr, nullptr, &pc, 2.0 * (double)n + 16.0 * R));
     } else {
         Sb = const_cast<uint8_t *>(d_buf);
-        SG_LAUNCH_B(c, "gather_spans", 16.0 * R, k_gather_spans, std::min<uint32_t>(grid_for(R, 256), 4096u), 256, 0, V, L.spans,
-                    R, SS);
+        SS = V;  // the segment sorts permute it in place
     }
 
     // adjacent equality inside segments; segments holding two different records -> sort

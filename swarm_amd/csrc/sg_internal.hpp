@@ -39,6 +39,10 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
 // LSD radix sort of (u64 key, u32 val) pairs on bits [begin_bit, end_bit), stable.
 // Ping-pongs between (keys, vals) and (keys_alt, vals_alt); returns the final arrays.
 // iota_vals: vals[i] = i is implied on input (vals need not be initialised).
+// Stable sort of (key, span) pairs: the spans themselves are the payload (no id gather after).
+int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
+                     int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out,
+                     const char *pass_name = "rs_pass");
 int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
                uint32_t n, int begin_bit, int end_bit, bool iota_vals,
                uint64_t **keys_out, uint32_t **vals_out, const char *pass_name = "rs_pass");

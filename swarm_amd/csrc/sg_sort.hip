@@ -143,14 +143,17 @@ __global__ __launch_bounds__(256) void k_rs_cscan(uint32_t *__restrict__ cnt, ui
     }
 }
 
-template <bool IOTA>
+// VT: u32 record ids (IOTA: generated on the first pass) or uint2 spans carried along, so
+// the sorted spans need no gather afterwards (sg_dedup.hip build_unique).
+template <bool IOTA, typename VT = uint32_t>
 __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict__ kin,
-                                                      const uint32_t *__restrict__ vin,
-                                                      uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                      const VT *__restrict__ vin,
+                                                      uint64_t *__restrict__ kout, VT *__restrict__ vout,
                                                       uint32_t n, int shift, uint32_t ntiles,
                                                       const uint32_t *__restrict__ toffs) {
+    static_assert(sizeof(VT) <= sizeof(uint64_t), "values staged in the key buffer");
     __shared__ uint64_t s_k[RD_TILE];  // keys, then (aliased) values
-    uint32_t *s_v = reinterpret_cast<uint32_t *>(s_k);
+    VT *s_v = reinterpret_cast<VT *>(s_k);
     __shared__ uint32_t s_wh[RD_WAVES][256];
     __shared__ uint32_t s_dstart[256];
     __shared__ uint32_t s_gbase[256];
@@ -218,11 +221,12 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
             kout[s_gbase[d] + p] = kk;
         }
     }
-    uint32_t v[RD_ITEMS];
+    VT v[RD_ITEMS];
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane;
-        v[i] = IOTA ? pos : ((pos < n) ? vin[pos] : 0u);
+        if constexpr (IOTA) v[i] = pos;
+        else v[i] = (pos < n) ? vin[pos] : VT{};
     }
     __syncthreads();
 #pragma unroll
@@ -239,9 +243,10 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
     }
 }
 
-int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
-               uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
-               uint32_t **vals_out, const char *pass_name) {
+template <typename VT>
+static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt, VT *vals_alt,
+                        uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
+                        VT **vals_out, const char *pass_name) {
     *keys_out = keys;
     *vals_out = vals;
     if (n == 0) return SG_OK;
@@ -266,31 +271,51 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
     uint32_t *tcnt;
     SG_TRY(slot(c, S_RS_TCNT, (size_t)ntiles * 256 + 64, &tcnt));
     uint64_t *ck = keys, *ak = keys_alt;
-    uint32_t *cv = vals, *av = vals_alt;
+    VT *cv = vals, *av = vals_alt;
     bool iota_pending = iota_vals;
+    constexpr double VB = (double)sizeof(VT);
     for (int q = 0; q < nlive; ++q) {
         const int p = live[q];
         const int shift = begin_bit + 8 * p;
         SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, ntiles, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt);
         SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, offs + p * 256);
-        if (iota_pending)
-            SG_LAUNCH(c, pass_name, k_rs_down<true>, ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt);
-        else
-            SG_LAUNCH(c, pass_name, k_rs_down<false>, ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt);
-        // 12 B read (8 B key + 4 B value; 8 B with implied iota values) + 12 B written per pair
-        prof_bytes(c, pass_name, (iota_pending ? 20.0 : 24.0) * n);
+        if constexpr (sizeof(VT) == 4) {
+            if (iota_pending)
+                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt);
+            else
+                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt);
+        } else {
+            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt);
+        }
+        // 8 B key + the value read (implied for iota ids) and both written, per pair
+        prof_bytes(c, pass_name, (iota_pending ? 16.0 + VB : 16.0 + 2.0 * VB) * n);
         iota_pending = false;
         uint64_t *tk = ck; ck = ak; ak = tk;
-        uint32_t *tv = cv; cv = av; av = tv;
+        VT *tv = cv; cv = av; av = tv;
     }
-    if (iota_pending) {
-        uint32_t g = (n + 255) / 256;
-        if (g > 4096) g = 4096;
-        SG_LAUNCH(c, "iota", k_iota, g, 256, 0, cv, n);
+    if constexpr (sizeof(VT) == 4) {
+        if (iota_pending) {
+            uint32_t g = (n + 255) / 256;
+            if (g > 4096) g = 4096;
+            SG_LAUNCH(c, "iota", k_iota, g, 256, 0, cv, n);
+        }
     }
     *keys_out = ck;
     *vals_out = cv;
     return SG_OK;
+}
+
+int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
+               uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
+               uint32_t **vals_out, const char *pass_name) {
+    return radix_sort_t<uint32_t>(c, keys, vals, keys_alt, vals_alt, n, begin_bit, end_bit, iota_vals, keys_out,
+                                  vals_out, pass_name);
+}
+
+int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
+                     int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out, const char *pass_name) {
+    return radix_sort_t<uint2>(c, keys, spans, keys_alt, spans_alt, n, begin_bit, end_bit, false, keys_out, spans_out,
+                               pass_name);
 }
 
 }  // namespace sg
