@@ -457,8 +457,8 @@ struct RecSet {
     uint32_t n;
 };
 
-constexpr uint32_t DF_TILE = 1024;  // U records per block
-constexpr uint32_t DF_PCAP = 4096;  // P keys staged in LDS per block
+constexpr uint32_t DF_TILE = 256;  // U records per block
+constexpr uint32_t DF_PCAP = 512;  // P keys + spans staged in LDS per block
 constexpr uint32_t DF_PER = DF_TILE / 256;
 
 // One wave per boundary t: jb[t] = lower_bound(P.K, U.K[t * DF_TILE]) (P.n past the end).
@@ -499,23 +499,32 @@ __global__ __launch_bounds__(256) void k_diff_split(const uint64_t *__restrict__
 
 __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uint32_t *__restrict__ jb,
                                                    uint8_t *__restrict__ fresh, uint32_t base) {
+    // the tile's P keys AND spans in LDS: after the key search the candidate's span is an
+    // LDS read, so the byte compare waits one global round trip (U and P bytes together)
+    // instead of two (P span, then bytes); U spans load with the U keys
     __shared__ uint64_t s_k[DF_PCAP];
+    __shared__ uint2 s_sp[DF_PCAP];
     const uint32_t t = blockIdx.x;
     const uint32_t i0 = t * DF_TILE;
     const uint32_t j0 = jb[t], j1 = jb[t + 1];
     const uint32_t np = j1 - j0;
     const bool staged = np <= DF_PCAP;
     if (staged)
-        for (uint32_t q = threadIdx.x; q < np; q += 256) s_k[q] = P.K[j0 + q];
-    __syncthreads();
+        for (uint32_t q = threadIdx.x; q < np; q += 256) {
+            s_k[q] = P.K[j0 + q];
+            s_sp[q] = P.sp[j0 + q];
+        }
     uint32_t idx[DF_PER], cand[DF_PER];
     uint64_t ku[DF_PER];
+    uint2 us[DF_PER];
     bool need[DF_PER], pres[DF_PER];
 #pragma unroll
     for (int k = 0; k < DF_PER; ++k) {
         idx[k] = i0 + threadIdx.x + 256u * k;
         ku[k] = idx[k] < U.n ? U.K[idx[k]] : 0ull;
+        us[k] = idx[k] < U.n ? U.sp[idx[k]] : make_uint2(0u, 0u);
     }
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < DF_PER; ++k) {
         // lower_bound of ku in P[j0, j1) (LDS when staged)
@@ -531,13 +540,12 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
         pres[k] = eq && (ku[k] & 0xffu) < 8u;
         need[k] = eq && !pres[k];
     }
-    // tag-8 candidates: spans of both records, then a wide compare (loads of all items together)
-    uint2 us[DF_PER], ps[DF_PER];
+    // tag-8 candidates: the P span (LDS when staged), then a wide compare (loads of all
+    // items together)
+    uint2 ps[DF_PER];
 #pragma unroll
-    for (int k = 0; k < DF_PER; ++k) {
-        us[k] = need[k] ? U.sp[idx[k]] : make_uint2(0u, 0u);
-        ps[k] = need[k] ? P.sp[cand[k]] : make_uint2(0u, 0u);
-    }
+    for (int k = 0; k < DF_PER; ++k)
+        ps[k] = need[k] ? (staged && cand[k] < j1 ? s_sp[cand[k] - j0] : P.sp[cand[k]]) : make_uint2(0u, 0u);
 #pragma unroll
     for (int k = 0; k < DF_PER; ++k) {
         if (!need[k]) continue;
