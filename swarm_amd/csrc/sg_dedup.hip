@@ -942,7 +942,9 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, vs.uspans, R, &us));
     SG_TRY(slot(c, vs.ukeys, R, &uk));
     uint64_t *uc;
-    SG_TRY(run_emit(c, k_emit_uniq, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
+    // short records: the small-window emit (more blocks per CU for the random gather)
+    const EmitApplyFn uk_kern = (n <= 40ull * R) ? k_emit_uniq_s : k_emit_uniq;
+    SG_TRY(run_emit(c, uk_kern, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
                     0.0, dst ? dst->shift() : 0u));
     // the output count and the run-sort error word come back with one host sync
     uint8_t *pin = (uint8_t *)c->pinned;
@@ -963,9 +965,13 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     return SG_OK;
 }
 
+// cur_lcp (with cur_pre): a device word already holding the common prefix of cur's records
+// vs cur's first record (computed where the records were gathered), so cur is not scanned
+// again for it.
 static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
                                 uint64_t n_prior, bool want_fresh, sg_dev_result *res, const Lines *cur_pre = nullptr,
-                                const OutBuf *ou = nullptr, const OutBuf *of = nullptr) {
+                                const OutBuf *ou = nullptr, const OutBuf *of = nullptr,
+                                const uint32_t *cur_lcp = nullptr) {
     *res = sg_dev_result{};
     UView pv;
     const bool have_prior = want_fresh && d_prior && n_prior;
@@ -978,6 +984,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     SG_TRY(slot(c, S_M_CNT, 4, &dflag));
     const uint32_t init[2] = {0u, 255u};
     SG_HIP(hipMemcpyAsync(dflag, init, 8, hipMemcpyHostToDevice, c->stream));
+    if (cur_lcp) SG_HIP(hipMemcpyAsync(dflag + 1, cur_lcp, 4, hipMemcpyDeviceToDevice, c->stream));
     if (have_prior) {
         SG_TRY(run_lines(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp));
         const uint32_t R = Lp.n_rec;
@@ -993,7 +1000,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint8_t *rbuf = ref_cur ? d_cur : d_prior;
     const uint2 *rsp = ref_cur ? Lc.spans : (have_prior ? Lp.spans : nullptr);
     const uint64_t *rkeys = ref_cur ? Lc.keys : (have_prior ? Lp.keys : nullptr);
-    if (rsp && Lc.n_rec)
+    if (rsp && Lc.n_rec && !cur_lcp)
         SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 512u), 256, 0, d_cur,
                     Lc.spans, Lc.keys, Lc.n_rec,
                     rbuf, rsp, rkeys, dflag + 1);
@@ -1073,10 +1080,10 @@ int dev_dedup_diff_into(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const u
 }
 
 int dev_dedup_diff_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &cur, const uint8_t *d_prior,
-                         uint64_t n_prior, sg_dev_result *res) {
+                         uint64_t n_prior, sg_dev_result *res, const uint32_t *cur_lcp) {
     c->last_path = 0;
     c->last_flags = 0;
-    return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, true, res, &cur);
+    return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, true, res, &cur, nullptr, nullptr, cur_lcp);
 }
 
 // Dedup+diff entry: the bucket sample sort when there is a prior scan to take splitters from

@@ -25,7 +25,12 @@ namespace sg {
 constexpr int EM_BLOCK = 256;
 constexpr int EM_ROUNDS = 4;
 constexpr uint32_t EM_TILE = EM_BLOCK * EM_ROUNDS;
+// Per-wave LDS output window: a round's 64 records are assembled there when their span fits
+// (else written straight from registers). Short-record inputs use the small window, which
+// leaves room for 5 blocks per CU instead of 4 (C2 unique emit 253 -> 239 us); long records
+// (httpx lines, ~100 B) need the large one (X1: 395 us with it, 495 with the small one).
 constexpr uint32_t EM_WIN = 6144;
+constexpr uint32_t EM_WIN_S = 3072;
 constexpr uint64_t EM_ONE = 1ull << 32;
 
 // Per-lane copy of a short record (aligned source span <= 64 B) whose 16-byte source
@@ -105,13 +110,14 @@ __device__ __forceinline__ void put_short_win(uint8_t *win, uint32_t d, const ui
 // chunks (all loads of the wave in flight together) and places the bytes. Longer records:
 // compacted into s_src/s_len/s_dst and copied by 16-lane groups with coalesced word loads.
 // Assembled in the wave's LDS window when the span fits, then written with 16-byte stores.
+template <uint32_t WIN = EM_WIN>
 __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src, uint8_t *__restrict__ out,
                                                 uint8_t *win, uint32_t *s_src, uint32_t *s_len, uint32_t *s_dst,
                                                 bool f, uint32_t s, uint32_t len, uint32_t d, uint64_t o0,
                                                 uint64_t oend, uint64_t base) {
     const uint32_t lane = lane_id();
     const uint64_t span = oend - base;
-    const bool in_lds = span <= EM_WIN;
+    const bool in_lds = span <= WIN;
     const uint32_t q0 = s & ~15u, sh = s - q0;
     const bool shortr = f && (sh + len <= 64u) && (len < 50u);
     uint4 c[4];
@@ -211,14 +217,14 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_count(Item item, uint32_t n, 
 // SPARSE (selections that drop items: unique compaction, new records): the wave's kept
 // items are first packed in LDS in output order, then copied 64 per round, so a round is
 // not spent on a 64-item slice that keeps only a few records.
-template <bool SPARSE>
+template <bool SPARSE, uint32_t WIN = EM_WIN>
 __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache, uint32_t n,
                                                 const uint64_t *__restrict__ pre,
                                                 const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                 uint2 *__restrict__ out_spans,
                                                 const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
                                                 int dbg) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][EM_WIN];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][WIN];
     __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
     __shared__ uint64_t s_wt[4];
     constexpr int CK = SPARSE ? EM_ROUNDS * 64 : 1;
@@ -275,7 +281,7 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
             const uint64_t o0 = (uint32_t)__shfl((int)o, 0, 64);
             const uint64_t oend = (uint32_t)__shfl((int)(o + l + 1u), (int)last, 64);
             const uint64_t base = o0 & ~15ull;
-            wave_copy_round(src, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
+            wave_copy_round<WIN>(src, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
                             (uint32_t)(o - base), o0, oend, base);
             __builtin_amdgcn_wave_barrier();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -300,7 +306,7 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
         const uint64_t o0 = __shfl(o, (int)first, 64);
         const uint64_t oend = __shfl(o + ln[r] + 1u, (int)last, 64);
         const uint64_t base = o0 & ~15ull;
-        wave_copy_round(src, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, st[r], ln[r],
+        wave_copy_round<WIN>(src, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, st[r], ln[r],
                         (uint32_t)(o - base), o0, oend, base);
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -308,17 +314,18 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
 }
 
 // One symbol per use, so rocprofv3 kernel stats and PMC passes attribute each separately.
-#define SG_EMIT_APPLY(NAME, SPARSE)                                                                 \
+#define SG_EMIT_APPLY(NAME, SPARSE, WIN)                                                            \
     __global__ __launch_bounds__(EM_BLOCK) void NAME(                                               \
         const uint2 *__restrict__ cache, uint32_t n, const uint64_t *__restrict__ pre,              \
         const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, uint2 *__restrict__ out_spans,  \
         const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout, int dbg) {                   \
-        emit_apply_body<SPARSE>(cache, n, pre, src, dst, out_spans, kin, kout, dbg);                \
+        emit_apply_body<SPARSE, WIN>(cache, n, pre, src, dst, out_spans, kin, kout, dbg);           \
     }
-SG_EMIT_APPLY(k_emit_sorted, false)
-SG_EMIT_APPLY(k_emit_uniq, true)
-SG_EMIT_APPLY(k_emit_fresh, true)
-SG_EMIT_APPLY(k_emit_apply, false)
+SG_EMIT_APPLY(k_emit_sorted, false, EM_WIN)
+SG_EMIT_APPLY(k_emit_uniq, true, EM_WIN)
+SG_EMIT_APPLY(k_emit_uniq_s, true, EM_WIN_S)
+SG_EMIT_APPLY(k_emit_fresh, true, EM_WIN)
+SG_EMIT_APPLY(k_emit_apply, false, EM_WIN)
 #undef SG_EMIT_APPLY
 
 // ------------------------------------------------------------------ common items

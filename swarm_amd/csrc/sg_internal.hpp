@@ -85,7 +85,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
 // dev_dedup_diff (radix pipeline) for a current scan given as already parsed records of
 // d_cur (spans + key0 from byte 0), e.g. the matched subset of a larger buffer.
 int dev_dedup_diff_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &cur, const uint8_t *d_prior,
-                         uint64_t n_prior, sg_dev_result *res);
+                         uint64_t n_prior, sg_dev_result *res, const uint32_t *cur_lcp = nullptr);
 // httpx -json field rows (sg_formats.hip).
 int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *keys, const uint32_t *key_offs,
                     uint32_t nkeys, sg_dev_rows *res);

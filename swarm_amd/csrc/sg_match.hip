@@ -1215,14 +1215,49 @@ __global__ void k_split_hits(const unsigned long long *K, const uint32_t *idx, u
     sig[i] = (uint32_t)k;
 }
 
-// Matched records (input order) -> their spans and key0 from byte 0.
+// Matched records (input order) -> their spans and key0 from byte 0, and (block minimum, a
+// guarded atomic per block) their common prefix with the first matched record — the dedup's
+// common-prefix scan of these records, done while their first bytes are being read anyway.
 __global__ __launch_bounds__(256) void k_gather_matched(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                                         const uint32_t *__restrict__ mrec, uint32_t m, uint2 *__restrict__ sp,
-                                                        uint64_t *__restrict__ keys) {
+                                                        uint64_t *__restrict__ keys, uint32_t *__restrict__ lcp_out) {
+    __shared__ uint32_t s_min[4];
+    const uint2 r = spans[mrec[0]];
+    const uint64_t kr = chunk_key(buf, r.x, r.y, 0);
+    const uint32_t tr = (uint32_t)(kr & 0xffu);
+    uint32_t best = 255;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
         const uint2 x = spans[mrec[i]];
         sp[i] = x;
-        keys[i] = chunk_key(buf, x.x, x.y, 0);
+        const uint64_t k = chunk_key(buf, x.x, x.y, 0);
+        keys[i] = k;
+        const uint64_t d0 = (k ^ kr) >> 8;
+        const uint32_t tk = (uint32_t)(k & 0xffu);
+        uint32_t l;
+        if (d0) {
+            l = min((uint32_t)__builtin_clzll(d0 << 8) >> 3, min(tk, tr));
+        } else if (tk < 8u || tr < 8u) {
+            l = min(tk, tr);
+        } else {
+            const uint32_t mm = min(min(x.y - x.x, r.y - r.x), best);
+            l = 7;
+            while (l < mm) {
+                const uint32_t t = (mm - l) < 8u ? (mm - l) : 8u;
+                const uint64_t d = load_le(buf, x.x + l, t) ^ load_le(buf, r.x + l, t);
+                if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
+                l += t;
+            }
+            l = min(l, mm);
+        }
+        best = min(best, l);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    if (lane_id() == 0) s_min[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
+        if (b < 255u && b < __hip_atomic_load(lcp_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(lcp_out, b);
     }
 }
 
@@ -1594,10 +1629,14 @@ int sg_dev_match_dedup_diff(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, size
         SG_TRY(slot(c, S_M_SP2, (size_t)M + 1, &Lm.spans));
         SG_TRY(slot(c, S_M_K2, (size_t)M + 1, &Lm.keys));
         Lm.n_rec = M;
-        if (M) SG_LAUNCH_B(c, "gather_matched", 24.0 * M, k_gather_matched, std::min<uint32_t>((M + 255) / 256, 4096u), 256, 0,
-                           b, mf.L.spans, mrec, M, Lm.spans, Lm.keys);
+        uint32_t *lcp;
+        SG_TRY(slot(c, S_M_TMP, 4, &lcp));
+        const uint32_t init = 255u;
+        SG_HIP(hipMemcpyAsync(lcp, &init, 4, hipMemcpyHostToDevice, c->stream));
+        if (M) SG_LAUNCH_B(c, "gather_matched", 24.0 * M, k_gather_matched, std::min<uint32_t>((M + 255) / 256, 2048u), 256, 0,
+                           b, mf.L.spans, mrec, M, Lm.spans, Lm.keys, lcp);
         if (matched_records) *matched_records = M;
-        SG_TRY(dev_dedup_diff_lines(c, b, n, Lm, n_prior ? p : nullptr, n_prior, res));
+        SG_TRY(dev_dedup_diff_lines(c, b, n, Lm, n_prior ? p : nullptr, n_prior, res, M ? lcp : nullptr));
         res->in_records = R;
         return SG_OK;
     }
