@@ -1105,6 +1105,7 @@ def main():
                                    % (n_lines // 1_000_000),
                        "lines_per_gpu": n_lines, "bytes_per_gpu": cur_bytes,
                        "prior_bytes": prior_bytes,
+                       "unique_frac": round(info["U"] / max(info["R"], 1), 4),
                        "parallelism": ("%s all-to-all x%d" % ("byte-range (global byte order)" if args.route == "range"
                                                               else "hash-partition", world))
                                       if world > 1 else "single GPU"},
