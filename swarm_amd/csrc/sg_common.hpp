@@ -88,6 +88,8 @@ struct sg_ctx {
     void *pinned = nullptr;   // host pinned staging for small readbacks
     int last_path = 0;        // dedup/diff: 0 = radix pipeline, 1 = bucket sample sort
     uint32_t last_flags = 0;  // bucket path error word of the last call (0: not declined)
+    uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
+    uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
     // profiling
     bool profile = false;
     std::string prof_only;  // non-empty: time only launches with this name

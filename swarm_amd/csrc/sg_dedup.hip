@@ -26,6 +26,7 @@
 #include "sg_emit.hpp"
 
 #include <stdlib.h>
+#include <cmath>
 #include <string.h>
 
 namespace sg {
@@ -73,6 +74,16 @@ static inline uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap = 0x7ff
     return (uint32_t)(g < cap ? g : cap);
 }
 
+// ------------------------------------------------------------------ key width
+// The sort key of a record ("key0") is its first kw bytes from the common prefix `base`,
+// big-endian in the top bits, with tag = min(remaining bytes, kw + 1) in bits 7..0 (kw = 7:
+// the full-width key of sg_lines; kw = 5/6: narrowed when those bytes already spread the
+// records, so fewer radix passes run). Equal keys with tag kw + 1 need bytes from base + kw.
+// Kernels take both as one word: bk = base | kw << 16.
+__host__ __device__ __forceinline__ uint32_t make_bk(uint32_t base, uint32_t kw) { return base | (kw << 16); }
+__device__ __forceinline__ uint32_t bk_off(uint32_t bk) { return (bk & 0xffffu) + (bk >> 16); }
+__device__ __forceinline__ uint32_t bk_full(uint32_t bk) { return (bk >> 16) + 1u; }
+
 // ------------------------------------------------------------------ predicates / functors
 struct FlagPred {
     const uint8_t *f;
@@ -85,6 +96,7 @@ struct BigGroupPred {
     const uint64_t *K;
     uint8_t *brk;
     uint32_t n;
+    uint32_t kfull;  // tag of a key with more bytes after it (kw + 1)
     // all five keys are loaded unconditionally (clamped indices, one round trip; the
     // +-64 neighbours are cache hits of adjacent waves) instead of after the head test
     __device__ uint32_t operator()(uint32_t i) const {
@@ -94,7 +106,7 @@ struct BigGroupPred {
         const uint64_t kn64 = K[i + WAVE_GROUP < n ? i + WAVE_GROUP : i];
         const bool head = (i == 0) || kp != k;
         brk[i] = head ? 1 : 0;
-        if ((k & 0xffu) != 8u) return 0u;
+        if ((k & 0xffu) != kfull) return 0u;
         const bool tail = (i + 1 == n) || kn != k;
         const bool bh = head && (i + WAVE_GROUP < n) && kn64 == k;
         const bool bt = tail && (i >= WAVE_GROUP) && kp64 == k;
@@ -129,10 +141,10 @@ struct GroupSizeFn {
 };
 
 __device__ __forceinline__ int key_cmp_full(const uint8_t *buf, const uint2 *spans,
-                                            uint64_t ka, uint32_t ra, uint64_t kb, uint32_t rb, uint32_t off) {
+                                            uint64_t ka, uint32_t ra, uint64_t kb, uint32_t rb, uint32_t bk) {
     if (ka != kb) return ka < kb ? -1 : 1;
-    if ((ka & 0xffu) < 8u) return 0;
-    return rec_cmp_w(buf, spans[ra].x, spans[ra].y, buf, spans[rb].x, spans[rb].y, off + 7);
+    if ((ka & 0xffu) < bk_full(bk)) return 0;
+    return rec_cmp_w(buf, spans[ra].x, spans[ra].y, buf, spans[rb].x, spans[rb].y, bk_off(bk));
 }
 
 // ------------------------------------------------------------------ refinement rounds
@@ -240,7 +252,7 @@ __global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S,
     const uint2 x = SS[ip], y = SS[i];
     bool d = false;
     if (i > 0 && !b) {
-        d = ((ki & 0xffu) < 8u) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, base + 7);
+        d = ((ki & 0xffu) < bk_full(base)) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, bk_off(base));
         if (!d) {
             // segment head = last break at or before i - 1 (position 0 at the latest), found
             // 16 bytes at a time with aligned loads instead of a dependent byte walk
@@ -304,7 +316,7 @@ struct SegKeys {
 __device__ __forceinline__ SegKeys seg_keys(const uint8_t *S, uint2 x, uint32_t base) {
     SegKeys k;
 #pragma unroll
-    for (int q = 0; q < SEG_CH; ++q) k.c[q] = chunk_key(S, x.x, x.y, base + 7u + 7u * q);
+    for (int q = 0; q < SEG_CH; ++q) k.c[q] = chunk_key(S, x.x, x.y, bk_off(base) + 7u * q);
     return k;
 }
 
@@ -316,7 +328,7 @@ __device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2
         if (a.c[q] != b.c[q]) return a.c[q] < b.c[q] ? -1 : 1;
         if ((a.c[q] & 0xffu) < 8u) return 0;
     }
-    return rec_cmp8(S, xa.x, xa.y - xa.x, xb.x, xb.y - xb.x, base + 7u + 7u * SEG_CH);
+    return rec_cmp8(S, xa.x, xa.y - xa.x, xb.x, xb.y - xb.x, bk_off(base) + 7u * SEG_CH);
 }
 
 // Rank the k members a.. of one segment with the G lanes gbase.. of the wave (lane gl of
@@ -537,7 +549,7 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
         cand[k] = j0 + lo;
         const uint64_t kp = (lo < np) ? (staged ? s_k[lo] : P.K[j0 + lo]) : (j0 + lo < P.n ? P.K[j0 + lo] : ~ku[k]);
         const bool eq = idx[k] < U.n && j0 + lo < P.n && kp == ku[k];
-        pres[k] = eq && (ku[k] & 0xffu) < 8u;
+        pres[k] = eq && (ku[k] & 0xffu) < bk_full(base);
         need[k] = eq && !pres[k];
     }
     // tag-8 candidates: the P span (LDS when staged), then a wide compare (loads of all
@@ -549,7 +561,7 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
 #pragma unroll
     for (int k = 0; k < DF_PER; ++k) {
         if (!need[k]) continue;
-        if (rec_equal_w(U.buf, us[k].x, us[k].y, P.buf, ps[k].x, ps[k].y, base + 7)) { pres[k] = true; continue; }
+        if (rec_equal_w(U.buf, us[k].x, us[k].y, P.buf, ps[k].x, ps[k].y, bk_off(base))) { pres[k] = true; continue; }
         // other P records sharing this key0 (distinct records with the same first 7 bytes):
         // they are sorted by their remaining bytes, so binary-search the run [c+1, c_end)
         // by full compare instead of scanning it
@@ -584,7 +596,7 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
             const uint2 x = P.sp[mid];
-            const int cmp = rec_cmp8_2(P.buf, x.x, x.y - x.x, U.buf, us[k].x, us[k].y - us[k].x, base + 7);
+            const int cmp = rec_cmp8_2(P.buf, x.x, x.y - x.x, U.buf, us[k].x, us[k].y - us[k].x, bk_off(base));
             if (cmp == 0) { pres[k] = true; break; }
             if (cmp < 0) lo = mid + 1; else hi = mid;
         }
@@ -641,6 +653,16 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
         const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
         // skip the memory-side atomic when an earlier block already published as small a prefix
         if (b < 255u && b < __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(out, b);
+    }
+}
+
+// key0 (7 bytes + min(rem, 8)) -> the kw-byte key (kw bytes + min(rem, kw + 1)).
+__global__ __launch_bounds__(256) void k_narrow_keys(uint64_t *__restrict__ keys, uint32_t n, uint32_t kw) {
+    const uint64_t top = ~0ull << (64u - 8u * kw);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        const uint64_t t = k & 0xffu;
+        keys[i] = (k & top) | (t < kw + 1u ? t : (uint64_t)(kw + 1u));
     }
 }
 
@@ -720,8 +742,8 @@ int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
 // sub-segment heads in brk, and keeps the sub-segments that are still > 64 records.
 template <typename VT>
 static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, VT *V, uint8_t *brk,
-                             uint32_t *GS, uint32_t *GE, uint32_t B, uint32_t base) {
-    uint32_t off = base + 7;
+                             uint32_t *GS, uint32_t *GE, uint32_t B, uint32_t bk) {
+    uint32_t off = (bk & 0xffffu) + (bk >> 16);
     while (B > 0) {
         uint64_t *goff;
         SG_TRY(slot(c, S_R_OFF, (size_t)B + 1, &goff));
@@ -806,7 +828,8 @@ struct OutBuf {
 };
 
 static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
-                        UView *uv, const Lines *pre = nullptr, uint32_t base = 0, const OutBuf *dst = nullptr) {
+                        UView *uv, const Lines *pre = nullptr, uint32_t base = make_bk(0u, 7u), const OutBuf *dst = nullptr,
+                        const uint32_t *host_hist = nullptr) {
     *uv = UView{};
     Lines L;
     if (pre) L = *pre;
@@ -865,7 +888,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, vs.lines.vals2, R, &v2));
     uint64_t *K;
     uint2 *V;
-    SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V));
+    SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V, "rs_pass", host_hist));
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
     uint8_t *brk;
@@ -874,7 +897,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, S_GS, R / 64 + 16, &GS));
     SG_TRY(slot(c, S_GE, R / 64 + 16, &GE));
     uint32_t B = 0, B2 = 0;
-    SG_TRY(run_select2(c, "mark_groups", BigGroupPred{K, brk, R}, R, GS, GE, &B, &B2, 9.0));
+    SG_TRY(run_select2(c, "mark_groups", BigGroupPred{K, brk, R, (base >> 16) + 1u}, R, GS, GE, &B, &B2, 9.0));
     if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
     if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B, base));
 
@@ -991,7 +1014,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         // keys from byte 0 decide sortedness exactly like keys from the common prefix would
         if (R > 1 && R < (1u << 30))
             SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_prior, Lp.spans, Lp.keys,
-                        R, dflag, 0u);
+                        R, dflag, make_bk(0u, 7u));
     }
     if (cur_pre) Lc = *cur_pre;
     else SG_TRY(run_lines(c, d_cur, n_cur, CUR_VIEW.lines, &Lc));
@@ -1019,9 +1042,54 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
             SG_LAUNCH(c, "rekey", k_rekey, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior, Lp.spans,
                       Lp.n_rec, base, Lp.keys);
     }
-    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, base));
+    // Key width: the cur keys' digit histograms (one read, replacing the sort's own) give
+    // each byte position's entropy; when the first 6 (or 5) key bytes already carry well
+    // over as many bits as there are records (expected << 1 record per key value, so few tie
+    // segments), the keys are narrowed to those bytes and the sort runs 1 (or 2) fewer
+    // passes. IP-like text (few distinct bytes per position) keeps the 7-byte key.
+    uint32_t kw = 7;
+    uint32_t *hh = c->hist_host;
+    const uint32_t *cur_hist = nullptr;
+    static const int narrow_env = getenv("SG_NARROW_KEYS") ? atoi(getenv("SG_NARROW_KEYS")) : 1;
+    if (narrow_env && Lc.n_rec >= 4096) {
+        SG_TRY(key_hist8(c, Lc.keys, Lc.n_rec, hh));
+        const double N = (double)Lc.n_rec;
+        double H[8] = {0};
+        for (int p = 0; p < 8; ++p)
+            for (int d = 0; d < 256; ++d)
+                if (hh[p * 256 + d]) {
+                    const double q = hh[p * 256 + d] / N;
+                    H[p] -= q * std::log2(q);
+                }
+        // margins measured on C2/X1: a 5-byte key saved 2 radix passes but its tie segments
+        // (distinct records sharing 5 bytes) cost the segment sort about as much again
+        const double lg = std::log2(N);
+        const double h5 = H[7] + H[6] + H[5] + H[4] + H[3], h6 = h5 + H[2];
+        const bool live2 = H[2] > 0.0, live1 = H[1] > 0.0;  // the passes narrowing removes
+        if (h5 >= lg + 4.0 && (live2 || live1)) kw = 5;
+        else if (h6 >= lg + 2.0 && live1) kw = 6;
+        if (kw < 7) {
+            SG_LAUNCH(c, "narrow_keys", k_narrow_keys, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u), 256, 0, Lc.keys,
+                      Lc.n_rec, kw);
+            if (have_prior && Lp.n_rec)
+                SG_LAUNCH(c, "narrow_keys", k_narrow_keys, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0,
+                          Lp.keys, Lp.n_rec, kw);
+            // the narrowed keys' histograms: bytes kw..6 are zero, the tag is clamped to kw + 1
+            for (int p = 1; p <= 7 - (int)kw; ++p) {
+                for (int d = 0; d < 256; ++d) hh[p * 256 + d] = 0;
+                hh[p * 256] = Lc.n_rec;
+            }
+            uint32_t tg[256] = {0};
+            for (int d = 0; d < 256; ++d) tg[d < (int)kw + 1 ? d : (int)kw + 1] += hh[d];
+            for (int d = 0; d < 256; ++d) hh[d] = tg[d];
+        }
+        cur_hist = hh;
+    }
+    c->last_kw = kw;
+    const uint32_t bk = make_bk(base, kw);
+    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, bk));
     UView cu;
-    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, base, ou));
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, cur_hist));
     res->in_records = cu.in_records;
     res->uniq = ou ? ou->p : const_cast<uint8_t *>(cu.buf);
     res->uniq_bytes = cu.bytes;
@@ -1051,7 +1119,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     // model: key + span of every unique cur record, key of every prior record, the compared
     // bytes of both sides (~ the unique output + the prior), one flag per cur record
     SG_LAUNCH_B(c, "diff_tile", 16.0 * cu.n + 8.0 * pv.n + (double)cu.bytes + cu.n, k_diff_tile, ntiles, 256, 0,
-                U, P, jb, fresh, base);
+                U, P, jb, fresh, bk);
     uint8_t *fout;
     if (of) fout = of->base();
     else SG_TRY(slot(c, S_OUT_FRESH, (size_t)cu.bytes + 64, &fout));

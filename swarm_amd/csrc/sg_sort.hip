@@ -243,26 +243,50 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
     }
 }
 
+int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist) {
+    uint32_t *hist;
+    SG_TRY(slot(c, S_HIST, RS_MAXPASS * 256 * 2 + RS_MAXPASS, &hist));
+    SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
+    uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
+    if (hgrid > 1024) hgrid = 1024;
+    if (n) SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, 0, RS_MAXPASS, hist);
+    return ctx_readback(c, host_hist, hist, RS_MAXPASS * 256 * 4);
+}
+
+// host_hist (optional): the 8 digit histograms of `keys` over bits [0, 64), already on the
+// host (key_hist8, possibly adjusted by the caller) — then the trivial passes are known
+// without a read-back.
 template <typename VT>
 static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt, VT *vals_alt,
                         uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
-                        VT **vals_out, const char *pass_name) {
+                        VT **vals_out, const char *pass_name, const uint32_t *host_hist = nullptr) {
     *keys_out = keys;
     *vals_out = vals;
     if (n == 0) return SG_OK;
     const int npasses = (end_bit - begin_bit + 7) / 8;
     if (npasses <= 0 || npasses > RS_MAXPASS) { set_error("radix_sort: bad bit range"); return SG_E_INVAL; }
+    if (host_hist && (begin_bit != 0 || npasses != RS_MAXPASS)) { set_error("radix_sort: histograms cover 64 bits"); return SG_E_INVAL; }
     uint32_t *hist;
     SG_TRY(slot(c, S_HIST, RS_MAXPASS * 256 * 2 + RS_MAXPASS, &hist));
     uint32_t *offs = hist + RS_MAXPASS * 256;
     uint32_t *triv = offs + RS_MAXPASS * 256;
-    SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
-    uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
-    if (hgrid > 1024) hgrid = 1024;
-    SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, begin_bit, npasses, hist);
-    SG_LAUNCH(c, "rs_scan", k_rs_scan, npasses, 256, 0, hist, offs, triv, n);
     uint32_t trivial[RS_MAXPASS];
-    SG_TRY(ctx_readback(c, trivial, triv, npasses * 4));
+    if (host_hist) {
+        SG_HIP(hipMemcpyAsync(hist, host_hist, RS_MAXPASS * 256 * 4, hipMemcpyHostToDevice, c->stream));
+        SG_LAUNCH(c, "rs_scan", k_rs_scan, npasses, 256, 0, hist, offs, triv, n);
+        for (int p = 0; p < npasses; ++p) {
+            trivial[p] = 0;
+            for (int d = 0; d < 256; ++d)
+                if (host_hist[p * 256 + d] == n) trivial[p] = 1;
+        }
+    } else {
+        SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
+        uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
+        if (hgrid > 1024) hgrid = 1024;
+        SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, begin_bit, npasses, hist);
+        SG_LAUNCH(c, "rs_scan", k_rs_scan, npasses, 256, 0, hist, offs, triv, n);
+        SG_TRY(ctx_readback(c, trivial, triv, npasses * 4));
+    }
     int live[RS_MAXPASS], nlive = 0;
     for (int p = 0; p < npasses; ++p)
         if (!trivial[p]) live[nlive++] = p;
@@ -313,9 +337,10 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
 }
 
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
-                     int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out, const char *pass_name) {
+                     int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out, const char *pass_name,
+                     const uint32_t *host_hist) {
     return radix_sort_t<uint2>(c, keys, spans, keys_alt, spans_alt, n, begin_bit, end_bit, false, keys_out, spans_out,
-                               pass_name);
+                               pass_name, host_hist);
 }
 
 }  // namespace sg
