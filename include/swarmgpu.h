@@ -82,6 +82,9 @@ int sg_ctx_memcpy(sg_ctx *ctx, void *dst, const void *src, size_t n);
 #define SG_PATH_RADIX 0
 #define SG_PATH_BUCKET 1
 int sg_ctx_last_path(sg_ctx *ctx, int *path, uint32_t *flags);
+/* Sort-key width (bytes after the common prefix, 5..7) the last radix dedup chose from the
+ * keys' byte entropies. For tests and benchmarks. */
+int sg_ctx_last_key_width(sg_ctx *ctx, uint32_t *kw);
 
 /* ------------------------------------------------------------------ A3: parse
  * Replaces: nothing in the reference parses module output; it is uploaded verbatim at

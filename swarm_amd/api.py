@@ -341,6 +341,12 @@ class Context:
         check(lib.sg_ctx_last_path(self._h, C.byref(p), C.byref(f)))
         return ("bucket" if p.value == 1 else "radix"), f.value
 
+    def last_key_width(self) -> int:
+        """Sort-key width in bytes (5..7) the last radix dedup chose on this context."""
+        kw = C.c_uint32()
+        check(lib.sg_ctx_last_key_width(self._h, C.byref(kw)))
+        return kw.value
+
     def dedup_diff(self, d_cur: int, n_cur: int, d_prior: int = 0, n_prior: int = 0) -> _abi.DevResult:
         """Device pointers in, device result (context-owned) out."""
         r = _abi.DevResult()

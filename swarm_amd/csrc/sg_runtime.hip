@@ -244,6 +244,12 @@ int sg_ctx_last_path(sg_ctx *c, int *path, uint32_t *flags) {
     return SG_OK;
 }
 
+int sg_ctx_last_key_width(sg_ctx *c, uint32_t *kw) {
+    if (!c || !kw) return SG_E_INVAL;
+    *kw = c->last_kw;
+    return SG_OK;
+}
+
 int sg_ctx_reset_stats(sg_ctx *c) {
     if (!c) return SG_E_INVAL;
     SG_TRY(ctx_harvest(c));

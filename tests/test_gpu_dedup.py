@@ -332,3 +332,58 @@ def test_common_prefix_edges(sg, case):
     cur = b"\n".join(recs) + b"\n"
     assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)
     assert sg.dedup(cur) == S.dedup(cur)
+
+
+def _kw_ctx():
+    import torch
+    import swarm_amd
+    return swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_narrowed_key_widths_with_tie_segments(seed):
+    """High-entropy records (narrowed 6/5-byte sort keys) where many distinct records share
+    exactly 5, 6 or 7 bytes, records shorter than the key, duplicates, NUL/0xff bytes; the
+    width chosen is reported and the result equals the oracle and the 7-byte-key run."""
+    import os
+    import random
+    import numpy as np
+    import torch
+    rng = random.Random(seed)
+    alpha = bytes(range(33, 127)) + b"\x00\xff"
+    heads = [bytes(rng.choice(alpha) for _ in range(rng.choice([5, 6, 7]))) for _ in range(60_000)]
+    recs = []
+    for _ in range(200_000):
+        h = rng.choice(heads)
+        k = rng.random()
+        recs.append(h[: rng.randint(1, len(h))] if k < 0.05 else h + bytes(rng.choice(alpha) for _ in range(rng.randint(0, 9))))
+    recs += recs[: 30_000]  # duplicates
+    rng.shuffle(recs)
+    cur = b"\n".join(recs) + b"\n"
+    prior = S.dedup(b"\n".join(recs[::3]) + b"\n")
+    c = _kw_ctx()
+    try:
+        dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+        dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+        r = c.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+        kw = c.last_key_width()
+        eu, ef = S.dedup_diff(cur, prior)
+        assert c.to_bytes(r.uniq, r.uniq_bytes) == eu and c.to_bytes(r.fresh, r.fresh_bytes) == ef
+        assert kw in (5, 6)
+    finally:
+        c.close()
+
+
+def test_low_entropy_keeps_seven_byte_key():
+    import numpy as np
+    import torch
+    recs = [b"10.%d.%d.%d:%d" % (a, b, d, p) for a in range(4) for b in range(40) for d in range(40) for p in (22, 80, 443)]
+    cur = b"\n".join(recs) + b"\n"
+    c = _kw_ctx()
+    try:
+        dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+        r = c.dedup_diff(dc.data_ptr(), len(cur), 0, 0)
+        assert c.to_bytes(r.uniq, r.uniq_bytes) == S.dedup(cur)
+        assert c.last_key_width() == 7
+    finally:
+        c.close()
