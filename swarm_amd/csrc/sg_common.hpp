@@ -19,6 +19,8 @@
 
 #include "../../include/swarmgpu.h"
 
+#define SG_PINNED_BYTES 16384
+
 namespace sg {
 
 // ------------------------------------------------------------------ errors
@@ -65,7 +67,7 @@ enum Slot : int {
     // bucket sample sort (sg_bucket.hip)
     S_BK_SKEY, S_BK_SSPAN, S_BK_CNT1, S_BK_CNT2, S_BK_SMALL, S_BK_TOT2, S_BK_Q, S_BK_NCUR, S_BK_L1, S_BK_L2,
     S_BK_US, S_BK_FS, S_BK_SPFX, S_BK_DBG, S_BK_RECS, S_BK_NREC,
-    S_M_FLAG, S_M_SP2, S_M_K2, S_R_T2,
+    S_M_FLAG, S_M_SP2, S_M_K2, S_R_T2, S_COUNT2,
     S_NSLOTS
 };
 
@@ -85,7 +87,7 @@ struct sg_ctx {
     bool owns_stream = false;
     void *slot_ptr[sg::S_NSLOTS] = {};
     size_t slot_cap[sg::S_NSLOTS] = {};
-    void *pinned = nullptr;   // host pinned staging for small readbacks
+    void *pinned = nullptr;   // host pinned staging for small readbacks (SG_PINNED_BYTES)
     int last_path = 0;        // dedup/diff: 0 = radix pipeline, 1 = bucket sample sort
     uint32_t last_flags = 0;  // bucket path error word of the last call (0: not declined)
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used

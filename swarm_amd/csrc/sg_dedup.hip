@@ -897,20 +897,58 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, S_GS, R / 64 + 16, &GS));
     SG_TRY(slot(c, S_GE, R / 64 + 16, &GE));
     uint32_t B = 0, B2 = 0;
-    SG_TRY(run_select2(c, "mark_groups", BigGroupPred{K, brk, R, (base >> 16) + 1u}, R, GS, GE, &B, &B2, 9.0));
+    uint32_t ns = 0, nb = 0;
+    uint32_t *hs, *hb;
+    uint8_t *dup, *segbad;
+    SG_TRY(slot(c, S_DUP, R, &dup));
+    SG_TRY(slot(c, S_BAD, R, &segbad));
+    SG_TRY(slot(c, S_SEL, (size_t)R / 2 + 16, &hs));
+    static const int materialize = getenv("SG_MATERIALIZE") ? atoi(getenv("SG_MATERIALIZE")) : 0;
+    // adjacent equality inside segments; segments holding two different records -> sort.
+    // model: key0 + brk + span per record, both records' bytes where compared, dup out
+    auto adjacent_and_heads = [&](const uint8_t *Sb, const uint2 *SSp, uint64_t **seg_total) -> int {
+        SG_HIP(hipMemsetAsync(segbad, 0, R, c->stream));
+        SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, k_adjacent, grid_for(R, 256), 256, 0, Sb, SSp, K, brk, R, dup, segbad,
+                    base);
+        SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
+        return run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, seg_total);
+    };
+    auto read2 = [&](const uint64_t *t1, const uint64_t *t2, uint32_t *a1, uint32_t *b1, uint32_t *a2, uint32_t *b2) -> int {
+        uint8_t *pin = (uint8_t *)c->pinned;
+        SG_HIP(hipMemcpyAsync(pin, t1, 8, hipMemcpyDeviceToHost, c->stream));
+        if (t2) SG_HIP(hipMemcpyAsync(pin + 8, t2, 8, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipStreamSynchronize(c->stream));
+        uint64_t v1 = 0, v2 = 0;
+        memcpy(&v1, pin, 8);
+        if (t2) memcpy(&v2, pin + 8, 8);
+        *a1 = (uint32_t)(v1 >> 31);
+        *b1 = (uint32_t)(v1 & 0x7fffffffu);
+        if (t2) {
+            *a2 = (uint32_t)(v2 >> 31);
+            *b2 = (uint32_t)(v2 & 0x7fffffffu);
+        }
+        return SG_OK;
+    };
+    uint64_t *gtot, *stot = nullptr;
+    SG_TRY(run_select2_nb(c, "mark_groups", BigGroupPred{K, brk, R, (base >> 16) + 1u}, R, GS, GE, S_COUNT, &gtot));
+    prof_bytes(c, "mark_groups", 9.0 * R);
+    // Without a materialised copy the adjacent pass and the segment-head select are queued
+    // before the group count comes back (one host sync for both counts); when big groups
+    // exist (the 7-byte key was kept: low-entropy text) they wait for the refinement instead.
+    const bool speculate = !materialize && (base >> 16) < 7u;
+    if (speculate) SG_TRY(adjacent_and_heads(d_buf, V, &stot));
+    SG_TRY(read2(gtot, stot, &B, &B2, &ns, &nb));
     if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
     if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B, base));
 
     // The records in this order: SS = the input spans in sorted order (the sort's payload),
-    // S = the input itself;
-    // the later passes (adjacent compare, segment sort, unique emit) gather from the input.
-    // Measured cheaper than materialising a sorted copy first (C2 2.51 -> 2.30 ms, X1 4.37 ->
-    // 3.97 ms): the copy gathered every record once and the unique emit copied ~2/3 of them
-    // again, where gathering only the unique records reads each kept record once.
-    // SG_MATERIALIZE=1 restores the copy (S contiguous, SS spans into it).
+    // S = the input itself; the later passes (adjacent compare, segment sort, unique emit)
+    // gather from the input. Measured cheaper than materialising a sorted copy first (C2
+    // 2.51 -> 2.30 ms, X1 4.37 -> 3.97 ms): the copy gathered every record once and the
+    // unique emit copied ~2/3 of them again, where gathering only the unique records reads
+    // each kept record once. SG_MATERIALIZE=1 restores the copy (S contiguous, SS spans into it).
     uint8_t *Sb;
     uint2 *SS;
-    static const int materialize = getenv("SG_MATERIALIZE") ? atoi(getenv("SG_MATERIALIZE")) : 0;
     if (materialize) {
         SG_TRY(slot(c, S_SSPANS, R, &SS));
         SG_TRY(slot(c, S_SBUF, (size_t)n + 64, &Sb));
@@ -922,20 +960,12 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         Sb = const_cast<uint8_t *>(d_buf);
         SS = V;  // the segment sorts permute it in place
     }
-
-    // adjacent equality inside segments; segments holding two different records -> sort
-    uint8_t *dup, *segbad;
-    SG_TRY(slot(c, S_DUP, R, &dup));
-    SG_TRY(slot(c, S_BAD, R, &segbad));
-    SG_HIP(hipMemsetAsync(segbad, 0, R, c->stream));
-    // model: key0 + brk + span per record, both records' bytes where compared, dup out
-    SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, k_adjacent, grid_for(R, 256), 256, 0, Sb, SS, K, brk, R, dup, segbad,
-                base);
-    uint32_t *hs, *hb;
-    SG_TRY(slot(c, S_SEL, (size_t)R / 2 + 16, &hs));
-    SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
-    uint32_t ns = 0, nb = 0;
-    SG_TRY(run_select2(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, &ns, &nb, 1.0));
+    if (!speculate || B) {
+        SG_TRY(adjacent_and_heads(Sb, SS, &stot));
+        uint32_t d0, d1;
+        SG_TRY(read2(stot, nullptr, &ns, &nb, &d0, &d1));
+    }
+    prof_bytes(c, "seg_heads", 1.0 * R);
     uint32_t *err;
     SG_TRY(slot(c, S_ERR, 4, &err));
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
@@ -1009,7 +1039,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     SG_HIP(hipMemcpyAsync(dflag, init, 8, hipMemcpyHostToDevice, c->stream));
     if (cur_lcp) SG_HIP(hipMemcpyAsync(dflag + 1, cur_lcp, 4, hipMemcpyDeviceToDevice, c->stream));
     if (have_prior) {
-        SG_TRY(run_lines(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp));
+        if (!cur_pre) SG_TRY(run_lines2(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp, d_cur, n_cur, CUR_VIEW.lines, &Lc));
+        else SG_TRY(run_lines(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp));
         const uint32_t R = Lp.n_rec;
         // keys from byte 0 decide sortedness exactly like keys from the common prefix would
         if (R > 1 && R < (1u << 30))
@@ -1017,7 +1048,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
                         R, dflag, make_bk(0u, 7u));
     }
     if (cur_pre) Lc = *cur_pre;
-    else SG_TRY(run_lines(c, d_cur, n_cur, CUR_VIEW.lines, &Lc));
+    else if (!have_prior) SG_TRY(run_lines(c, d_cur, n_cur, CUR_VIEW.lines, &Lc));
     // common prefix of every record (reference: the first record of cur, else of prior)
     const bool ref_cur = Lc.n_rec > 0;
     const uint8_t *rbuf = ref_cur ? d_cur : d_prior;

@@ -33,6 +33,8 @@ struct Lines {
 // Split d_buf (16-byte aligned device pointer, n bytes) into non-empty records.
 // apply = false: count and allocate only; the spans are then written by a consumer that
 // re-reads the same tiles anyway (k_lit_scan with LitArgs::spans_out).
+int run_lines2(sg_ctx *c, const uint8_t *a, uint64_t na, const SlotSet &sa, Lines *la, const uint8_t *b, uint64_t nb,
+               const SlotSet &sb, Lines *lb);
 int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys = true,
               bool apply = true);
 

@@ -15,6 +15,7 @@
 #include "sg_internal.hpp"
 
 #include <stdlib.h>
+#include <string.h>
 
 namespace sg {
 
@@ -137,6 +138,53 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
         spans[ei].y = (uint32_t)(my0 + b);
         ++ei;
     }
+}
+
+// Two buffers parsed with ONE host sync for both record counts (the dedup's prior and
+// current scan): both count passes and tile scans are queued, both totals come back
+// together, then both apply passes.
+int run_lines2(sg_ctx *c, const uint8_t *a, uint64_t na, const SlotSet &sa, Lines *la, const uint8_t *b, uint64_t nb,
+               const SlotSet &sb, Lines *lb) {
+    const uint8_t *bufs[2] = {a, b};
+    const uint64_t ns[2] = {na, nb};
+    const SlotSet *ss[2] = {&sa, &sb};
+    Lines *outs[2] = {la, lb};
+    uint64_t *totals[2], *pres[2];
+    uint32_t nts[2];
+    for (int k = 0; k < 2; ++k) {
+        if (ns[k] > MAX_BYTES) { set_error("buffer of %llu bytes exceeds the 4 GiB per-call limit", (unsigned long long)ns[k]); return SG_E_TOO_LARGE; }
+        if (((uintptr_t)bufs[k] & 15) != 0) { set_error("run_lines: device buffer not 16-byte aligned"); return SG_E_INVAL; }
+        const uint32_t ntiles = (uint32_t)(ns[k] / LN_TILE + 1);
+        uint64_t *tp;
+        SG_TRY(slot(c, ss[k]->lb, 2 * (size_t)ntiles + 4, &tp));
+        uint64_t *tot = tp;
+        pres[k] = tp + ntiles;
+        totals[k] = tp + 2 * (size_t)ntiles;
+        nts[k] = ntiles;
+        SG_LAUNCH(c, "lines.count", k_lines_count, ntiles, LN_BLOCK, 0, bufs[k], ns[k], tot);
+        SG_TRY(tile_scan(c, tot, ntiles, pres[k], totals[k]));
+        prof_bytes(c, "lines.count", (double)ns[k]);
+    }
+    uint8_t *pin = (uint8_t *)c->pinned;
+    SG_HIP(hipMemcpyAsync(pin, totals[0], 8, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipMemcpyAsync(pin + 8, totals[1], 8, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 2; ++k) {
+        uint64_t tv;
+        memcpy(&tv, pin + 8 * k, 8);
+        const uint32_t R = (uint32_t)(tv >> 31);
+        if (R != (uint32_t)(tv & 0x7fffffffu)) { set_error("run_lines: start/end count mismatch"); return SG_E_HIP; }
+        Lines *out = outs[k];
+        SG_TRY(slot(c, ss[k]->starts, (size_t)R + 1, &out->spans));
+        SG_TRY(slot(c, ss[k]->keys, (size_t)R + 1, &out->keys));
+        SG_LAUNCH(c, "lines", k_lines, nts[k], LN_BLOCK, 0, bufs[k], ns[k], pres[k], out->spans, out->keys);
+        out->n_rec = R;
+        out->tile_excl = pres[k];
+        out->tile_bytes = LN_TILE;
+        out->n_tiles = nts[k];
+        prof_bytes(c, "lines", (double)ns[k] + 16.0 * R);
+    }
+    return SG_OK;
 }
 
 int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys, bool apply) {

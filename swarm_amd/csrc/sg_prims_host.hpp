@@ -30,6 +30,27 @@ static int run_select2(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint3
     return SG_OK;
 }
 
+// run_select2 without the host sync: returns the device word (countA << 31 | countB) in the
+// given status slot, for the caller to read back together with other counts.
+template <class Pred>
+static int run_select2_nb(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint32_t *outA, uint32_t *outB,
+                          int status_slot, uint64_t **total_out) {
+    const uint32_t ntiles = (n + SEL_TILE - 1) / SEL_TILE;
+    uint64_t *tp;  // tot | pre | total | maskA | maskB
+    SG_TRY(slot(c, status_slot, 2 * (size_t)std::max<uint32_t>(ntiles, 1) + 4 + 2 * (size_t)ntiles * SEL_MASKS, &tp));
+    uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
+    *total_out = total;
+    if (n == 0) {
+        SG_HIP(hipMemsetAsync(total, 0, 8, c->stream));
+        return SG_OK;
+    }
+    uint64_t *mA = total + 4, *mB = mA + (size_t)ntiles * SEL_MASKS;
+    SG_LAUNCH(c, name, k_sel_count<Pred>, ntiles, SEL_BLOCK, 0, pred, n, mA, mB, tot);
+    SG_TRY(tile_scan(c, tot, ntiles, pre, total));
+    SG_LAUNCH(c, "select.apply", k_sel_apply, ntiles, SEL_BLOCK, 0, n, mA, mB, pre, outA, outB);
+    return SG_OK;
+}
+
 // Exclusive scan of fn(i) into out; *total = the sum (one host sync).
 template <class Fn>
 static int run_scan64(sg_ctx *c, const char *name, Fn fn, uint32_t n, uint64_t *out, uint64_t *total_h) {

@@ -42,7 +42,7 @@ int ctx_slot(sg_ctx *c, int s, size_t bytes, void **out) {
 }
 
 int ctx_readback(sg_ctx *c, void *host, const void *dev, size_t bytes) {
-    if (bytes > 4096) {
+    if (bytes > SG_PINNED_BYTES) {
         SG_HIP(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, c->stream));
         SG_HIP(hipStreamSynchronize(c->stream));
         return SG_OK;
@@ -174,7 +174,7 @@ int sg_ctx_create(int device, void *stream, sg_ctx **out) {
         }
         c->owns_stream = true;
     }
-    if (hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(&c->pinned, SG_PINNED_BYTES, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         if (c->owns_stream) (void)hipStreamDestroy(c->stream);
         delete c;
