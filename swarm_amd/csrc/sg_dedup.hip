@@ -1062,8 +1062,21 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 512u), 256, 0, d_prior,
                     Lp.spans, Lp.keys, Lp.n_rec,
                     rbuf, rsp, rkeys, dflag + 1);
+    // the cur keys' digit histograms (for the key width below) are queued now and come back
+    // with the flags; they stay valid when the common prefix turns out to be empty
+    static const int narrow_env = getenv("SG_NARROW_KEYS") ? atoi(getenv("SG_NARROW_KEYS")) : 1;
+    const bool want_hist = narrow_env && Lc.n_rec >= 4096;
+    const uint32_t *dhist = nullptr;
+    if (want_hist) SG_TRY(key_hist8_async(c, Lc.keys, Lc.n_rec, &dhist));
     uint32_t fl[2] = {0u, 0u};
-    SG_TRY(ctx_readback(c, fl, dflag, 8));
+    {
+        uint8_t *pin = (uint8_t *)c->pinned;
+        SG_HIP(hipMemcpyAsync(pin, dflag, 8, hipMemcpyDeviceToHost, c->stream));
+        if (dhist) SG_HIP(hipMemcpyAsync(pin + 64, dhist, 8 * 256 * 4, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipStreamSynchronize(c->stream));
+        memcpy(fl, pin, 8);
+        if (dhist) memcpy(c->hist_host, pin + 64, 8 * 256 * 4);
+    }
     prior_sorted = fl[0] == 0;
     const uint32_t base = (rsp && (Lc.n_rec || (have_prior && Lp.n_rec))) ? fl[1] : 0u;
     if (base) {
@@ -1081,9 +1094,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     uint32_t kw = 7;
     uint32_t *hh = c->hist_host;
     const uint32_t *cur_hist = nullptr;
-    static const int narrow_env = getenv("SG_NARROW_KEYS") ? atoi(getenv("SG_NARROW_KEYS")) : 1;
-    if (narrow_env && Lc.n_rec >= 4096) {
-        SG_TRY(key_hist8(c, Lc.keys, Lc.n_rec, hh));
+    if (want_hist) {
+        if (base) SG_TRY(key_hist8(c, Lc.keys, Lc.n_rec, hh));  // keys changed: histograms again
         const double N = (double)Lc.n_rec;
         double H[8] = {0};
         for (int p = 0; p < 8; ++p)

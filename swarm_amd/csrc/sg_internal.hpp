@@ -47,6 +47,8 @@ int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt
                      const char *pass_name = "rs_pass", const uint32_t *host_hist = nullptr);
 // The 8 digit histograms (bits [0, 64), 8 x 256 counts) of keys, read back to the host.
 int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist);
+// The same histograms queued only (device pointer, 8 x 256 u32), for a combined read-back.
+int key_hist8_async(sg_ctx *c, const uint64_t *keys, uint32_t n, const uint32_t **dev_hist);
 int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
                uint32_t n, int begin_bit, int end_bit, bool iota_vals,
                uint64_t **keys_out, uint32_t **vals_out, const char *pass_name = "rs_pass");

@@ -243,6 +243,17 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
     }
 }
 
+int key_hist8_async(sg_ctx *c, const uint64_t *keys, uint32_t n, const uint32_t **dev_hist) {
+    uint32_t *hist;
+    SG_TRY(slot(c, S_HIST, RS_MAXPASS * 256 * 2 + RS_MAXPASS, &hist));
+    SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
+    uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
+    if (hgrid > 1024) hgrid = 1024;
+    if (n) SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, 0, RS_MAXPASS, hist);
+    *dev_hist = hist;
+    return SG_OK;
+}
+
 int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist) {
     uint32_t *hist;
     SG_TRY(slot(c, S_HIST, RS_MAXPASS * 256 * 2 + RS_MAXPASS, &hist));
