@@ -764,17 +764,33 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
         }
     };
 
+    // software pipelining: the next tile's text is loaded into registers while this tile is
+    // probed and verified (the loads of a persistent block otherwise wait a full HBM round
+    // trip per tile)
+    uint4 nxt[NW / 4];
+    auto prefetch = [&](uint32_t tl) -> bool {
+        const uint64_t b0 = (uint64_t)tl * TILE;
+        if (tl >= a.n_tiles || b0 + TILE + LS_HALO > n) return false;
+        const uint4 *p = reinterpret_cast<const uint4 *>(a.buf + b0 + (uint64_t)t * BPT);
+#pragma unroll
+        for (int j = 0; j < NW / 4; ++j) nxt[j] = p[j];
+        return true;
+    };
+    bool nxt_ok = prefetch(blockIdx.x);
     for (uint32_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
         const uint64_t base = (uint64_t)tile * TILE;
         const uint64_t my0 = base + (uint64_t)t * BPT;
         uint32_t w[NW];
-        if (base + TILE + LS_HALO <= n) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(a.buf + my0);
+        const bool cur_ok = nxt_ok;
+        if (cur_ok) {
 #pragma unroll
             for (int j = 0; j < NW / 4; ++j) {
-                const uint4 v = p[j];
+                const uint4 v = nxt[j];
                 w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
             }
+        }
+        nxt_ok = prefetch(tile + gridDim.x);
+        if (cur_ok) {
         } else {
 #pragma unroll
             for (int j = 0; j < NW; ++j) {
@@ -1119,41 +1135,38 @@ struct VerifyArgs {
     unsigned long long *hits;
     uint32_t *hit_count;
     uint32_t cap;
+    uint32_t n_singles, n_acc;  // automata count, total accept-table entries
 };
 
-__device__ __forceinline__ bool verify_one(const VerifyArgs &a, unsigned long long cd) {
-    const uint32_t r = (uint32_t)(cd >> 32), pid = (uint32_t)cd;
-    const uint32_t k = a.single_of_pid[pid];
-    const uint16_t *D = a.s_delta + a.s_off[k];
-    const uint8_t *cls = a.s_cls + 256u * k;
-    const uint8_t *acc = a.s_acc + a.s_acc_off[k];
-    const uint32_t C = a.s_C[k];
-    const uint2 sp_ = a.spans[r];
-    const uint32_t s = sp_.x, e = sp_.y;
-    const uint32_t mid = a.s_mid[k];
+// Walk automaton (D, cls, acc with C classes, eol column, anchored start states mid) over
+// record [s, e): global tables, or the block's copy in LDS (the same code inlined with LDS
+// pointers, so the lookups are ds_reads).
+template <class DT, class CT, class AT>
+__device__ __forceinline__ bool verify_walk(const uint8_t *__restrict__ buf, DT D, CT cls, AT acc, uint32_t C, uint32_t eol,
+                                            uint32_t mid, uint32_t s, uint32_t e) {
     if (mid != 0xffffffffu) {
         // anchored DFA: a run from every start offset (most die on their first byte)
         bool hit = false;
         for (uint32_t p0 = s; p0 <= e && !hit; ++p0) {
             uint32_t st = 1;
             if (p0 > s) {
-                const uint8_t pb = a.buf[p0 - 1];
+                const uint8_t pb = buf[p0 - 1];
                 const bool pw = (pb >= '0' && pb <= '9') || ((pb | 0x20) >= 'a' && (pb | 0x20) <= 'z') || pb == '_';
                 st = pw ? (mid >> 16) : (mid & 0xffffu);
             }
             hit = acc[st] != 0;
             for (uint32_t p = p0; p < e && !hit && st != 0; ++p) {
-                st = D[st * C + cls[a.buf[p]]];
+                st = D[st * C + cls[buf[p]]];
                 hit = acc[st] != 0;
             }
-            if (!hit && st != 0) hit = acc[D[st * C + a.s_eol[k]]] != 0;
+            if (!hit && st != 0) hit = acc[D[st * C + eol]] != 0;
         }
         return hit;
     }
     uint32_t st = 1;
     bool hit = acc[st] != 0;
     for (uint32_t w = s & ~15u; w < e && !hit && st != 0; w += 16) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
+        const uint4 v = *reinterpret_cast<const uint4 *>(buf + w);
         const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (uint32_t b = 0; b < 16; ++b) {
@@ -1163,7 +1176,7 @@ __device__ __forceinline__ bool verify_one(const VerifyArgs &a, unsigned long lo
             hit = acc[st] != 0;
         }
     }
-    if (!hit && st != 0) hit = acc[D[st * C + a.s_eol[k]]] != 0;
+    if (!hit && st != 0) hit = acc[D[st * C + eol]] != 0;
     return hit;
 }
 
@@ -1176,13 +1189,48 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
     return g * q + (g < r ? g : r) + j;
 }
 
+// Candidates are sorted by pattern, so almost every block verifies one automaton: when it
+// fits, the block copies that automaton (rows, byte classes, accept flags) into LDS once and
+// every lane walks it there — the per-byte transitions were dependent L1/L2 loads.
+constexpr uint32_t VF_D = 12288;   // u16 transition entries staged per block
+constexpr uint32_t VF_ACC = 4096;  // accept flags staged per block
+
 __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
-    const uint32_t i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    __shared__ uint16_t s_D[VF_D];
+    __shared__ uint8_t s_cls[256];
+    __shared__ uint8_t s_acc[VF_ACC];
+    const uint32_t i0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
+    const uint32_t i = i0 + threadIdx.x;
+    const uint32_t il = min(i0 + blockDim.x, a.n_cand) - 1u;
+    const uint32_t k0 = a.single_of_pid[(uint32_t)a.cand[i0]];
+    const uint32_t kl = a.single_of_pid[(uint32_t)a.cand[il]];
+    uint32_t nst = 0, nd = 0;
+    if (k0 == kl) {
+        nst = (k0 + 1u < a.n_singles ? a.s_acc_off[k0 + 1u] : a.n_acc) - a.s_acc_off[k0];
+        nd = nst * a.s_C[k0];
+    }
+    const bool staged = k0 == kl && nd <= VF_D && nst <= VF_ACC;  // block-uniform
+    if (staged) {
+        const uint16_t *D = a.s_delta + a.s_off[k0];
+        for (uint32_t q = threadIdx.x; q < nd; q += blockDim.x) s_D[q] = D[q];
+        const uint8_t *acc = a.s_acc + a.s_acc_off[k0];
+        for (uint32_t q = threadIdx.x; q < nst; q += blockDim.x) s_acc[q] = acc[q];
+        s_cls[threadIdx.x] = a.s_cls[256u * k0 + threadIdx.x];
+        __syncthreads();
+    }
     bool hit = false;
     unsigned long long cd = 0;
     if (i < a.n_cand) {
         cd = a.cand[i];
-        hit = verify_one(a, cd);
+        const uint32_t r = (uint32_t)(cd >> 32), pid = (uint32_t)cd;
+        const uint32_t k = a.single_of_pid[pid];
+        const uint2 sp = a.spans[r];
+        if (staged) {
+            hit = verify_walk(a.buf, s_D, s_cls, s_acc, a.s_C[k], a.s_eol[k], a.s_mid[k], sp.x, sp.y);
+        } else {
+            hit = verify_walk(a.buf, a.s_delta + a.s_off[k], a.s_cls + 256u * k, a.s_acc + a.s_acc_off[k], a.s_C[k],
+                              a.s_eol[k], a.s_mid[k], sp.x, sp.y);
+        }
     }
     // one global append per wave: ballot, lane 0 reserves, each hitting lane its slot
     const uint64_t m = __ballot(hit);
@@ -1427,7 +1475,8 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
             if (n_cand) {
                 const auto &p = h->dplan;
                 VerifyArgs v{d_buf, L.spans, vcand, n_cand, p.s_delta, p.s_off, p.s_C, p.s_eol,
-                             p.s_acc_off, p.single_of_pid, p.s_mid, p.s_cls, p.s_acc, hits, cnt, (uint32_t)cap};
+                             p.s_acc_off, p.single_of_pid, p.s_mid, p.s_cls, p.s_acc, hits, cnt, (uint32_t)cap,
+                             h->n_singles, (uint32_t)h->s_acc.size()};
                 SG_LAUNCH_B(c, "re_verify", n_cand * (16.0 + (double)n / R), k_verify, (n_cand + 255) / 256, 256, 0, v);
             }
         }

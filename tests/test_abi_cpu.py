@@ -58,3 +58,40 @@ def test_choose_splitters_quantiles():
     assert sp.tolist() == [3, 7]
     assert sharded.choose_splitters(s, 1).size == 0
     assert np.all(np.diff(sharded.choose_splitters(np.arange(1000, dtype=np.uint64), 17).astype(np.int64)) >= 0)
+
+
+def test_choose_byte_splitters():
+    from swarm_amd import sharded
+    samples = [b"m", b"a", b"zz", b"b", b"ab", b"ab", b"\x00", b"\xff"]
+    sp = sharded.choose_splitters(samples, 4)
+    assert sp == sorted(sp) and len(sp) == 3
+    assert sharded.choose_splitters([], 4) == [] and sharded.choose_splitters(samples, 1) == []
+    assert sharded.n_splitters(sp) == 3
+
+
+def test_part_overflow_message_names_the_limit():
+    from swarm_amd import sharded
+    msg = sharded.part_overflow_message([b"a"], 1, 10, 20)
+    assert "share their first 64 bytes" in msg and str(sharded.PART_LIMIT) in msg
+
+
+def test_shard_bounds_newline_aligned():
+    import numpy as np
+    from swarm_amd.distributed import shard_bounds
+    data = b"a\nbb\n\nccc\nd"
+    for world in (1, 2, 3, 5, 20):
+        cuts = shard_bounds(np.frombuffer(data, dtype=np.uint8), world)
+        assert cuts[0] == 0 and cuts[-1] == len(data) and len(cuts) == world + 1
+        assert all(b >= a for a, b in zip(cuts, cuts[1:]))
+        assert all(data[c - 1:c] == b"\n" for c in cuts[1:-1] if 0 < c < len(data))
+        assert b"".join(data[a:b] for a, b in zip(cuts, cuts[1:])) == data
+
+
+def test_ip_pool_is_distinct_10_slash_8():
+    import torch
+    from swarm_amd import corpus
+    mat, lens = corpus.ip_pool_torch(5000, seed=5, device="cpu")
+    ips = {bytes(mat[i, :lens[i]].tolist()) for i in range(5000)}
+    assert len(ips) == 5000
+    assert all(ip.startswith(b"10.") and ip.count(b".") == 3 for ip in ips)
+    assert all(0 <= int(o) <= 255 for ip in list(ips)[:500] for o in ip.split(b"."))
