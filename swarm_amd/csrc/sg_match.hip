@@ -764,33 +764,17 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
         }
     };
 
-    // software pipelining: the next tile's text is loaded into registers while this tile is
-    // probed and verified (the loads of a persistent block otherwise wait a full HBM round
-    // trip per tile)
-    uint4 nxt[NW / 4];
-    auto prefetch = [&](uint32_t tl) -> bool {
-        const uint64_t b0 = (uint64_t)tl * TILE;
-        if (tl >= a.n_tiles || b0 + TILE + LS_HALO > n) return false;
-        const uint4 *p = reinterpret_cast<const uint4 *>(a.buf + b0 + (uint64_t)t * BPT);
-#pragma unroll
-        for (int j = 0; j < NW / 4; ++j) nxt[j] = p[j];
-        return true;
-    };
-    bool nxt_ok = prefetch(blockIdx.x);
     for (uint32_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
         const uint64_t base = (uint64_t)tile * TILE;
         const uint64_t my0 = base + (uint64_t)t * BPT;
         uint32_t w[NW];
-        const bool cur_ok = nxt_ok;
-        if (cur_ok) {
+        if (base + TILE + LS_HALO <= n) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(a.buf + my0);
 #pragma unroll
             for (int j = 0; j < NW / 4; ++j) {
-                const uint4 v = nxt[j];
+                const uint4 v = p[j];
                 w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
             }
-        }
-        nxt_ok = prefetch(tile + gridDim.x);
-        if (cur_ok) {
         } else {
 #pragma unroll
             for (int j = 0; j < NW; ++j) {
@@ -1189,8 +1173,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
     return g * q + (g < r ? g : r) + j;
 }
 
-// Candidates are sorted by pattern, so almost every block verifies one automaton: when it
-// fits, the block copies that automaton (rows, byte classes, accept flags) into LDS once and
+// Candidates are sorted by pattern, so almost every block verifies one automaton: when the
+// first and last candidate share it and it fits, the block copies that automaton (rows, byte classes, accept flags) into LDS once and
 // every lane walks it there — the per-byte transitions were dependent L1/L2 loads.
 constexpr uint32_t VF_D = 12288;   // u16 transition entries staged per block
 constexpr uint32_t VF_ACC = 4096;  // accept flags staged per block
@@ -1225,7 +1209,7 @@ __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
         const uint32_t r = (uint32_t)(cd >> 32), pid = (uint32_t)cd;
         const uint32_t k = a.single_of_pid[pid];
         const uint2 sp = a.spans[r];
-        if (staged) {
+        if (staged && k == k0) {  // pids of one automaton need not be contiguous
             hit = verify_walk(a.buf, s_D, s_cls, s_acc, a.s_C[k], a.s_eol[k], a.s_mid[k], sp.x, sp.y);
         } else {
             hit = verify_walk(a.buf, a.s_delta + a.s_off[k], a.s_cls + 256u * k, a.s_acc + a.s_acc_off[k], a.s_C[k],
