@@ -70,6 +70,15 @@ struct sg_matcher {
         uint32_t H = 0;
     };
     std::vector<DevTable> dtabs;
+    // DFA groups walked together by k_dfa_multi (LDS-resident tables, <= 4 per pack)
+    struct DfaPack {
+        uint32_t G = 0, tab[4] = {0, 0, 0, 0}, off[4] = {0, 0, 0, 0}, hot_n = 0;
+        unsigned long long init[4] = {0, 0, 0, 0};
+        uint32_t *d_cls4 = nullptr;
+        uint16_t *d_hot = nullptr;
+    };
+    std::vector<DfaPack> packs;
+    std::vector<uint8_t> packed;  // per table: walked by a pack
     // hashed q-gram literal filter (used instead of the automaton when it does not fit LDS)
     struct Lit {
         bool on = false;
@@ -102,6 +111,8 @@ namespace sg {
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t AC_HOT_BYTES = 64 * 1024;   // LDS budget for hot rows
 constexpr uint32_t AC_BITS_BYTES = 16 * 1024;  // LDS budget for the output bitmap
+constexpr int DFM_BLOCK = 1024;                     // k_dfa_multi block
+constexpr uint32_t DFM_LDS = 163840u - 1024u - 512u;  // hot-row budget of one DFA pack (bytes)
 
 static int build_ac(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags, sg_matcher::Table *T) {
     const bool nocase = flags & SG_NOCASE;
@@ -410,6 +421,9 @@ static void free_dev(sg_matcher *h) {
         (void)hipFree(d.omask); (void)hipFree(d.gpids);
     }
     h->dtabs.clear();
+    for (auto &k : h->packs) { (void)hipFree(k.d_cls4); (void)hipFree(k.d_hot); }
+    h->packs.clear();
+    h->packed.clear();
     auto &p = h->dplan;
     for (void *q : {(void *)p.fac_off, (void *)p.fac_pids, (void *)p.s_delta, (void *)p.s_off, (void *)p.s_C,
                     (void *)p.s_eol, (void *)p.s_acc_off, (void *)p.single_of_pid, (void *)p.s_cls, (void *)p.s_acc,
@@ -425,6 +439,50 @@ static void free_dev(sg_matcher *h) {
         L->d_pat16 = nullptr;
     }
     h->dev = -1;
+}
+
+// Packs for k_dfa_multi: regex groups whose whole table fits LDS as u16 with a spare accept
+// bit (< 32768 states), whose dead row stays dead, greedily in table order while the pack's
+// rows fit one block's LDS.
+static int build_packs(sg_matcher *h) {
+    h->packed.assign(h->tables.size(), 0);
+    if (h->kind != 1) return SG_OK;
+    // test/tuning knob: a smaller pack budget (bytes) trades re-walking the bytes for occupancy
+    const uint32_t budget = getenv("SG_DFM_LDS") ? std::min<uint32_t>(DFM_LDS, (uint32_t)atoi(getenv("SG_DFM_LDS"))) : DFM_LDS;
+    sg_matcher::DfaPack cur;
+    std::vector<uint32_t> cls4(256, 0);
+    std::vector<uint16_t> hot;
+    auto close = [&]() -> int {
+        if (cur.G == 0) return SG_OK;
+        hot.resize((hot.size() + 7) & ~(size_t)7, 0);
+        cur.hot_n = (uint32_t)hot.size();
+        SG_TRY(upload_vec(cls4, &cur.d_cls4));
+        SG_TRY(upload_vec(hot, &cur.d_hot));
+        h->packs.push_back(cur);
+        cur = sg_matcher::DfaPack{};
+        std::fill(cls4.begin(), cls4.end(), 0u);
+        hot.clear();
+        return SG_OK;
+    };
+    for (size_t ti = 0; ti < h->tables.size(); ++ti) {
+        const auto &T = h->tables[ti];
+        const uint64_t ents = (uint64_t)T.n_states * T.n_classes;
+        auto outbit = [&](uint32_t q) { return (T.outbits[q >> 5] >> (q & 31)) & 1u; };
+        bool ok = T.n_states >= 2 && T.n_states <= 32768 && T.n_classes <= 256 && ents * 2 <= budget &&
+                  !outbit(0) && T.omask.size() == T.n_states;
+        for (uint32_t c = 0; ok && c < T.n_classes; ++c) ok = T.delta[c] == 0;
+        if (!ok) continue;
+        if (cur.G == 4 || (hot.size() + ents) * 2 > budget) SG_TRY(close());
+        const uint32_t g = cur.G++;
+        cur.tab[g] = (uint32_t)ti;
+        cur.off[g] = (uint32_t)hot.size();
+        cur.init[g] = outbit(1) ? T.omask[1] : 0ull;
+        for (uint32_t b = 0; b < 256; ++b) cls4[b] |= (uint32_t)T.cls[b] << (8 * g);
+        for (uint64_t q = 0; q < ents; ++q)
+            hot.push_back((uint16_t)(T.delta[q] | (outbit(T.delta[q]) << 15)));
+        h->packed[ti] = 1;
+    }
+    return close();
 }
 
 static int ensure_device(sg_matcher *h, int dev) {
@@ -489,6 +547,7 @@ static int ensure_device(sg_matcher *h, int dev) {
         d.H = H;
         h->dtabs.push_back(d);
     }
+    SG_TRY(build_packs(h));
     h->dev = dev;
     return SG_OK;
 }
@@ -1105,6 +1164,111 @@ __global__ __launch_bounds__(DFA_BLOCK) void k_dfa_match(DFAArgs a) {
     sink.flush(true);
 }
 
+// Several factor-less DFA groups walked together (a pack of G <= 4): one thread walks one
+// record through all G automata at once, so the record's bytes are loaded, split and bounds-
+// checked once, one LDS read gives the byte's class in every group (4 classes packed in a u32),
+// and the G transition chains are independent (G loads in flight per byte). Each hot entry
+// carries the target state's accept flag in bit 15, so accepting costs no outbits lookup.
+// Every group of the pack is fully LDS-resident; the block's records' hits go out with one
+// global atomic per round (no LDS staging: the tables use the LDS).
+struct DFAMultiArgs {
+    const uint8_t *buf;
+    const uint2 *spans;
+    uint32_t R;
+    const uint32_t *cls4;    // per byte: class in group g at bits 8g..8g+7
+    const uint16_t *hot;     // groups' rows back to back: next state | accept << 15
+    uint32_t hot_n;          // entries (multiple of 8)
+    uint32_t off[4], C[4], eol[4];
+    unsigned long long init[4];              // accept mask of the start state
+    const unsigned long long *omask[4];
+    const uint32_t *gpids[4];
+    unsigned long long *hits;
+    uint32_t *hit_count;
+    uint32_t cap;
+};
+
+template <int G>
+__global__ __launch_bounds__(DFM_BLOCK) void k_dfa_multi(DFAMultiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t *s_cls = reinterpret_cast<uint32_t *>(lds);
+    uint16_t *s_hot = reinterpret_cast<uint16_t *>(lds + 1024);
+    __shared__ uint32_t s_red[DFM_BLOCK / 64];
+    __shared__ uint32_t s_base;
+    if (threadIdx.x < 256) s_cls[threadIdx.x] = a.cls4[threadIdx.x];
+    for (uint32_t q = threadIdx.x; q < a.hot_n / 8; q += DFM_BLOCK)
+        reinterpret_cast<uint4 *>(s_hot)[q] = reinterpret_cast<const uint4 *>(a.hot)[q];
+    __syncthreads();
+    for (uint32_t r0 = blockIdx.x * DFM_BLOCK; r0 < a.R; r0 += gridDim.x * DFM_BLOCK) {
+        const uint32_t r = r0 + threadIdx.x;
+        unsigned long long acc[G];
+        uint32_t st[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) { acc[g] = 0; st[g] = 1; }
+        if (r < a.R) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) acc[g] = a.init[g];
+            // all G row reads issue before any accept branch, so a byte costs one LDS round
+            // trip for the class word and one for the G transitions (24-bit multiplies: rows
+            // index < 2^24, and v_mul_u32_u24 is full rate where v_mul_lo_u32 is not)
+            auto feed = [&](uint32_t cw) {
+                uint32_t v[G], any = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g) v[g] = s_hot[__umul24(st[g], a.C[g]) + a.off[g] + ((cw >> (8 * g)) & 0xffu)];
+#pragma unroll
+                for (int g = 0; g < G; ++g) { st[g] = v[g] & 0x7fffu; any |= v[g]; }
+                if (any & 0x8000u) {
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+                        if (v[g] & 0x8000u) acc[g] |= a.omask[g][st[g]];
+                }
+            };
+            const uint2 sp_ = a.spans[r];
+            const uint32_t s = sp_.x, e = sp_.y;
+            for (uint32_t w = s & ~15u; w < e; w += 16) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
+                const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+                // the chunk's 16 class words first (independent reads), then the transitions
+                uint32_t cw[16];
+#pragma unroll
+                for (uint32_t b = 0; b < 16; ++b) cw[b] = s_cls[(xs[b >> 2] >> (8 * (b & 3))) & 0xffu];
+                if (w >= s && w + 16 <= e) {
+#pragma unroll
+                    for (uint32_t b = 0; b < 16; ++b) feed(cw[b]);
+                } else {
+#pragma unroll
+                    for (uint32_t b = 0; b < 16; ++b)
+                        if (w + b >= s && w + b < e) feed(cw[b]);
+                }
+                uint32_t alive = 0;
+#pragma unroll
+                for (int g = 0; g < G; ++g) alive |= st[g];
+                if (!alive) break;  // every group dead (row 0 maps to 0, never accepting)
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (a.eol[g] && st[g]) {
+                    const uint32_t v = s_hot[a.off[g] + st[g] * a.C[g] + a.eol[g]];
+                    if (v & 0x8000u) acc[g] |= a.omask[g][v & 0x7fffu];
+                }
+        }
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) cnt += (uint32_t)__popcll(acc[g]);
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<DFM_BLOCK>(cnt, &tot, s_red);
+        if (tot == 0) continue;  // block-uniform
+        if (threadIdx.x == 0) s_base = atomicAdd(a.hit_count, tot);
+        __syncthreads();
+        uint32_t q = s_base + ex;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            for (unsigned long long m = acc[g]; m; m &= m - 1, ++q)
+                if (q < a.cap) a.hits[q] = ((unsigned long long)r << 32) | a.gpids[g][__ffsll((long long)m) - 1];
+        // s_base is rewritten only after the next round's scan, whose barriers every thread
+        // passes after reading it here
+    }
+}
+
 // Verify prefilter candidates: one thread per (record, pattern) runs that pattern's own
 // DFA over the record (state 0 dead, 1 start, EOL column last) and appends a hit on the
 // first accepting state.
@@ -1439,7 +1603,33 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
         if (R && h->lit.on) SG_TRY(run_lit("lit_match", h->lit, hits, cnt, (uint32_t)cap, nullptr, nullptr));
         if (R) {
+            const char *dm_env = getenv("SG_DFA_MULTI");
+            const bool multi = !dm_env || atoi(dm_env) != 0;
+            if (multi) {
+                for (const auto &k : h->packs) {
+                    DFAMultiArgs a{};
+                    a.buf = d_buf; a.spans = L.spans; a.R = R; a.cls4 = k.d_cls4; a.hot = k.d_hot; a.hot_n = k.hot_n;
+                    for (uint32_t g = 0; g < k.G; ++g) {
+                        const auto &T = h->tables[k.tab[g]];
+                        const auto &D = h->dtabs[k.tab[g]];
+                        a.off[g] = k.off[g]; a.C[g] = T.n_classes; a.eol[g] = T.anchored_eol; a.init[g] = k.init[g];
+                        a.omask[g] = reinterpret_cast<const unsigned long long *>(D.omask);
+                        a.gpids[g] = D.gpids;
+                    }
+                    a.hits = hits; a.hit_count = cnt; a.cap = (uint32_t)cap;
+                    const uint32_t lds = 1024 + k.hot_n * 2;
+                    const uint32_t per_cu = std::max<uint32_t>(1u, 163840u / (lds + 128));
+                    const uint32_t grid = std::min<uint32_t>((R + DFM_BLOCK - 1) / DFM_BLOCK, 256u * per_cu);
+                    switch (k.G) {
+                        case 1: SG_LAUNCH_B(c, "dfa_match", (double)n + 8.0 * R, k_dfa_multi<1>, grid, DFM_BLOCK, lds, a); break;
+                        case 2: SG_LAUNCH_B(c, "dfa_match", (double)n + 8.0 * R, k_dfa_multi<2>, grid, DFM_BLOCK, lds, a); break;
+                        case 3: SG_LAUNCH_B(c, "dfa_match", (double)n + 8.0 * R, k_dfa_multi<3>, grid, DFM_BLOCK, lds, a); break;
+                        default: SG_LAUNCH_B(c, "dfa_match", (double)n + 8.0 * R, k_dfa_multi<4>, grid, DFM_BLOCK, lds, a); break;
+                    }
+                }
+            }
             for (size_t ti = 0; ti < h->tables.size(); ++ti) {
+                if (multi && h->packed[ti]) continue;
                 const auto &T = h->tables[ti];
                 const auto &D = h->dtabs[ti];
                 uint32_t bits_in_lds, lds, grid;

@@ -201,6 +201,28 @@ def test_regex_c4_banners_full_signature_set(sg):
     assert len(exp) > 50
 
 
+@pytest.mark.parametrize("multi", ["1", "0"])
+def test_regex_factorless_groups_packed_and_single(sg, multi, monkeypatch):
+    """Factor-less patterns whose DFAs split into several groups: walked together by the
+    packed multi-group kernel (SG_DFA_MULTI=1, default) or one launch per group (0); both
+    bit-exact vs re.search, including start-state accepts (x?) and end-of-record anchors."""
+    import random
+    monkeypatch.setenv("SG_DFA_MULTI", multi)
+    pats = [rb"[a-z]{%d,9}[0-9]{2,%d}[a-z]" % (i % 3 + 1, i % 4 + 2) for i in range(12)]
+    pats += [rb"^\w+\s\d+$", rb"x?", rb"(a|b)*c$", rb"[0-9]+\.[0-9]+\.[0-9]+"]
+    pats += [rb"[ab][^\n]{%d}[cd]" % k for k in range(6, 12)]
+    m = sg.Matcher(pats, "regex")
+    assert m.info()["automata"] >= 4
+    rng = random.Random(5)
+    alpha = b"abcdxyz0123456789. "
+    lines = [bytes(rng.choice(alpha) for _ in range(rng.randrange(0, 90))) for _ in range(3000)]
+    lines += [b"", b"abc", b"word 123", b"aaaaaaaaaaaac", b"1.2.3", b"b0123456789d"]
+    data = b"\n".join(lines) + b"\n"
+    got = m.match(data)
+    assert got == S.regex_hits(data, pats)
+    assert len(got) > 3000
+
+
 def test_repeated_calls_keep_workspace_bounded():
     """Hundreds of matches on one context reuse the hit workspace instead of growing it
     (a capacity fed back from the slot size used to compound by the slot headroom)."""
