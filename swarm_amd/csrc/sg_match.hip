@@ -1187,85 +1187,111 @@ struct DFAMultiArgs {
     uint32_t cap;
 };
 
+// Lane refill: each wave owns a contiguous range of records and every lane takes the next
+// record of the range the moment its own ends (ranks from a ballot, no atomics), so a wave
+// no longer idles while its longest record finishes (banners: 31..105 B, mean 53). Bytes
+// outside the lane's record leave its states unchanged (a select, not a branch), so lanes
+// at a record's first or last chunk run the same instructions as lanes in its middle.
 template <int G>
 __global__ __launch_bounds__(DFM_BLOCK) void k_dfa_multi(DFAMultiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t *s_cls = reinterpret_cast<uint32_t *>(lds);
     uint16_t *s_hot = reinterpret_cast<uint16_t *>(lds + 1024);
-    __shared__ uint32_t s_red[DFM_BLOCK / 64];
-    __shared__ uint32_t s_base;
     if (threadIdx.x < 256) s_cls[threadIdx.x] = a.cls4[threadIdx.x];
     for (uint32_t q = threadIdx.x; q < a.hot_n / 8; q += DFM_BLOCK)
         reinterpret_cast<uint4 *>(s_hot)[q] = reinterpret_cast<const uint4 *>(a.hot)[q];
     __syncthreads();
-    for (uint32_t r0 = blockIdx.x * DFM_BLOCK; r0 < a.R; r0 += gridDim.x * DFM_BLOCK) {
-        const uint32_t r = r0 + threadIdx.x;
-        unsigned long long acc[G];
-        uint32_t st[G];
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t n_waves = gridDim.x * (DFM_BLOCK / 64);
+    const uint32_t wv = blockIdx.x * (DFM_BLOCK / 64) + (threadIdx.x >> 6);
+    const uint32_t per = (a.R + n_waves - 1) / n_waves;
+    const uint32_t r_hi = min(a.R, (uint32_t)min<uint64_t>((uint64_t)(wv + 1) * per, 0xffffffffull));
+    uint32_t nxt = min(a.R, (uint32_t)min<uint64_t>((uint64_t)wv * per, 0xffffffffull));  // wave-uniform
+    unsigned long long acc[G];
+    uint32_t st[G];
+    uint32_t r = 0, w = 0, s = 0, e = 0;
+    bool busy = false, done = false;
+    while (true) {
+        const uint64_t need = __ballot(!busy && !done);
+        if (need) {
+            if (!busy && !done) {
+                const uint32_t rr = nxt + (uint32_t)__popcll(need & lt);
+                if (rr < r_hi) {
+                    r = rr;
+                    const uint2 sp_ = a.spans[r];
+                    s = sp_.x; e = sp_.y; w = s & ~15u;
 #pragma unroll
-        for (int g = 0; g < G; ++g) { acc[g] = 0; st[g] = 1; }
-        if (r < a.R) {
+                    for (int g = 0; g < G; ++g) { st[g] = 1; acc[g] = a.init[g]; }
+                    busy = true;
+                } else {
+                    done = true;
+                }
+            }
+            nxt += (uint32_t)__popcll(need);
+        }
+        if (!__ballot(busy)) break;
+        bool fin = false;
+        if (busy) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
+            const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t lo = s > w ? s - w : 0u, hi = e - w < 16u ? e - w : 16u;
+            uint32_t cw[16];
 #pragma unroll
-            for (int g = 0; g < G; ++g) acc[g] = a.init[g];
-            // all G row reads issue before any accept branch, so a byte costs one LDS round
-            // trip for the class word and one for the G transitions (24-bit multiplies: rows
-            // index < 2^24, and v_mul_u32_u24 is full rate where v_mul_lo_u32 is not)
-            auto feed = [&](uint32_t cw) {
-                uint32_t v[G], any = 0;
+            for (uint32_t b = 0; b < 16; ++b) cw[b] = s_cls[(xs[b >> 2] >> (8 * (b & 3))) & 0xffu];
 #pragma unroll
-                for (int g = 0; g < G; ++g) v[g] = s_hot[__umul24(st[g], a.C[g]) + a.off[g] + ((cw >> (8 * g)) & 0xffu)];
+            for (uint32_t b = 0; b < 16; ++b) {
+                const bool in = b >= lo && b < hi;
+                uint32_t vv[G], any = 0;
 #pragma unroll
-                for (int g = 0; g < G; ++g) { st[g] = v[g] & 0x7fffu; any |= v[g]; }
+                for (int g = 0; g < G; ++g)
+                    vv[g] = s_hot[__umul24(st[g], a.C[g]) + a.off[g] + ((cw[b] >> (8 * g)) & 0xffu)];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    vv[g] = in ? vv[g] : st[g];  // outside the record: state kept, no accept
+                    st[g] = vv[g] & 0x7fffu;
+                    any |= vv[g];
+                }
                 if (any & 0x8000u) {
 #pragma unroll
                     for (int g = 0; g < G; ++g)
-                        if (v[g] & 0x8000u) acc[g] |= a.omask[g][st[g]];
+                        if (vv[g] & 0x8000u) acc[g] |= a.omask[g][st[g]];
                 }
-            };
-            const uint2 sp_ = a.spans[r];
-            const uint32_t s = sp_.x, e = sp_.y;
-            for (uint32_t w = s & ~15u; w < e; w += 16) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
-                const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
-                // the chunk's 16 class words first (independent reads), then the transitions
-                uint32_t cw[16];
-#pragma unroll
-                for (uint32_t b = 0; b < 16; ++b) cw[b] = s_cls[(xs[b >> 2] >> (8 * (b & 3))) & 0xffu];
-                if (w >= s && w + 16 <= e) {
-#pragma unroll
-                    for (uint32_t b = 0; b < 16; ++b) feed(cw[b]);
-                } else {
-#pragma unroll
-                    for (uint32_t b = 0; b < 16; ++b)
-                        if (w + b >= s && w + b < e) feed(cw[b]);
-                }
-                uint32_t alive = 0;
-#pragma unroll
-                for (int g = 0; g < G; ++g) alive |= st[g];
-                if (!alive) break;  // every group dead (row 0 maps to 0, never accepting)
             }
+            w += 16;
+            uint32_t alive = 0;
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-                if (a.eol[g] && st[g]) {
-                    const uint32_t v = s_hot[a.off[g] + st[g] * a.C[g] + a.eol[g]];
-                    if (v & 0x8000u) acc[g] |= a.omask[g][v & 0x7fffu];
-                }
+            for (int g = 0; g < G; ++g) alive |= st[g];
+            if (w >= e || !alive) {  // every group dead: row 0 maps to 0, never accepting
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (a.eol[g] && st[g]) {
+                        const uint32_t x = s_hot[__umul24(st[g], a.C[g]) + a.off[g] + a.eol[g]];
+                        if (x & 0x8000u) acc[g] |= a.omask[g][x & 0x7fffu];
+                    }
+                fin = true;
+            }
         }
+        // finished lanes append their hits: one atomic per wave step that has any
         uint32_t cnt = 0;
+        if (fin) {
 #pragma unroll
-        for (int g = 0; g < G; ++g) cnt += (uint32_t)__popcll(acc[g]);
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan<DFM_BLOCK>(cnt, &tot, s_red);
-        if (tot == 0) continue;  // block-uniform
-        if (threadIdx.x == 0) s_base = atomicAdd(a.hit_count, tot);
-        __syncthreads();
-        uint32_t q = s_base + ex;
+            for (int g = 0; g < G; ++g) cnt += (uint32_t)__popcll(acc[g]);
+        }
+        if (__ballot(cnt != 0)) {
+            const uint32_t inc = wave_incl_scan(cnt);
+            const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(a.hit_count, tot);
+            uint32_t q = (uint32_t)__shfl((int)base, 0, 64) + inc - cnt;
+            if (cnt) {
 #pragma unroll
-        for (int g = 0; g < G; ++g)
-            for (unsigned long long m = acc[g]; m; m &= m - 1, ++q)
-                if (q < a.cap) a.hits[q] = ((unsigned long long)r << 32) | a.gpids[g][__ffsll((long long)m) - 1];
-        // s_base is rewritten only after the next round's scan, whose barriers every thread
-        // passes after reading it here
+                for (int g = 0; g < G; ++g)
+                    for (unsigned long long m = acc[g]; m; m &= m - 1, ++q)
+                        if (q < a.cap) a.hits[q] = ((unsigned long long)r << 32) | a.gpids[g][__ffsll((long long)m) - 1];
+            }
+        }
+        if (fin) busy = false;
     }
 }
 
