@@ -68,6 +68,9 @@ enum Slot : int {
     S_BK_SKEY, S_BK_SSPAN, S_BK_CNT1, S_BK_CNT2, S_BK_SMALL, S_BK_TOT2, S_BK_Q, S_BK_NCUR, S_BK_L1, S_BK_L2,
     S_BK_US, S_BK_FS, S_BK_SPFX, S_BK_DBG, S_BK_RECS, S_BK_NREC,
     S_M_FLAG, S_M_SP2, S_M_K2, S_R_T2, S_COUNT2,
+    // probe path (sg_dedup.hip: cur records looked up in a sorted prior's hash table)
+    S_PB_TAB, S_PB_BITS, S_PB_NEW, S_PB_IDX, S_PB_SP, S_PB_K, S_PB_INS, S_PB_KB, S_PB_MI, S_PB_STAT,
+    S_PB_H, S_PB_RK, S_PB_CNT, S_PB_OFF, S_PB_E, S_PB_ERR,
     S_NSLOTS
 };
 
@@ -88,7 +91,7 @@ struct sg_ctx {
     void *slot_ptr[sg::S_NSLOTS] = {};
     size_t slot_cap[sg::S_NSLOTS] = {};
     void *pinned = nullptr;   // host pinned staging for small readbacks (SG_PINNED_BYTES)
-    int last_path = 0;        // dedup/diff: 0 = radix pipeline, 1 = bucket sample sort
+    int last_path = 0;        // dedup/diff: 0 = radix pipeline, 1 = bucket sample sort, 2 = probe
     uint32_t last_flags = 0;  // bucket path error word of the last call (0: not declined)
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)

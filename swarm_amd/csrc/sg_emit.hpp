@@ -110,14 +110,18 @@ __device__ __forceinline__ void put_short_win(uint8_t *win, uint32_t d, const ui
 // chunks (all loads of the wave in flight together) and places the bytes. Longer records:
 // compacted into s_src/s_len/s_dst and copied by 16-lane groups with coalesced word loads.
 // Assembled in the wave's LDS window when the span fits, then written with 16-byte stores.
-template <uint32_t WIN = EM_WIN>
-__device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src, uint8_t *__restrict__ out,
+// TWO: records come from two sources, src (start bit 31 clear) and src2 (bit 31 set).
+template <uint32_t WIN = EM_WIN, bool TWO = false>
+__device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src0, const uint8_t *__restrict__ src2,
+                                                uint8_t *__restrict__ out,
                                                 uint8_t *win, uint32_t *s_src, uint32_t *s_len, uint32_t *s_dst,
-                                                bool f, uint32_t s, uint32_t len, uint32_t d, uint64_t o0,
+                                                bool f, uint32_t s_in, uint32_t len, uint32_t d, uint64_t o0,
                                                 uint64_t oend, uint64_t base) {
     const uint32_t lane = lane_id();
     const uint64_t span = oend - base;
     const bool in_lds = span <= WIN;
+    const uint8_t *src = (TWO && (s_in >> 31)) ? src2 : src0;
+    const uint32_t s = TWO ? (s_in & 0x7fffffffu) : s_in;
     const uint32_t q0 = s & ~15u, sh = s - q0;
     const bool shortr = f && (sh + len <= 64u) && (len < 50u);
     uint4 c[4];
@@ -130,7 +134,7 @@ __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src,
     const uint64_t ml = __ballot(longr);
     if (longr) {
         const uint32_t cidx = (uint32_t)__popcll(ml & ((1ull << lane) - 1ull));
-        s_src[cidx] = s;
+        s_src[cidx] = s_in;
         s_len[cidx] = len;
         s_dst[cidx] = d;
     }
@@ -144,12 +148,14 @@ __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src,
         const uint32_t cnt = (uint32_t)__popcll(ml);
         const uint32_t g = lane >> 4, gl = lane & 15;
         for (uint32_t j = g; j < cnt; j += 4) {
-            const uint32_t sj = s_src[j], lj = s_len[j];
+            const uint32_t sjr = s_src[j], lj = s_len[j];
+            const uint8_t *sbj = (TWO && (sjr >> 31)) ? src2 : src0;
+            const uint32_t sj = TWO ? (sjr & 0x7fffffffu) : sjr;
             const uint32_t ej = sj + lj;
             const uint32_t a0 = sj & ~3u;
             uint8_t *dd = (in_lds ? win : out + base) + s_dst[j];
             for (uint32_t a = a0 + 4 * gl; a < ej; a += 64) {
-                const uint32_t x = *reinterpret_cast<const uint32_t *>(src + a);
+                const uint32_t x = *reinterpret_cast<const uint32_t *>(sbj + a);
 #pragma unroll
                 for (uint32_t b = 0; b < 4; ++b) {
                     const uint32_t p = a + b;
@@ -217,10 +223,11 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_count(Item item, uint32_t n, 
 // SPARSE (selections that drop items: unique compaction, new records): the wave's kept
 // items are first packed in LDS in output order, then copied 64 per round, so a round is
 // not spent on a 64-item slice that keeps only a few records.
-template <bool SPARSE, uint32_t WIN = EM_WIN>
+template <bool SPARSE, uint32_t WIN = EM_WIN, bool TWO = false>
 __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache, uint32_t n,
                                                 const uint64_t *__restrict__ pre,
-                                                const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                const uint8_t *__restrict__ src, const uint8_t *__restrict__ src2,
+                                                uint8_t *__restrict__ dst,
                                                 uint2 *__restrict__ out_spans,
                                                 const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
                                                 int dbg) {
@@ -281,7 +288,7 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
             const uint64_t o0 = (uint32_t)__shfl((int)o, 0, 64);
             const uint64_t oend = (uint32_t)__shfl((int)(o + l + 1u), (int)last, 64);
             const uint64_t base = o0 & ~15ull;
-            wave_copy_round<WIN>(src, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
+            wave_copy_round<WIN, TWO>(src, src2, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
                             (uint32_t)(o - base), o0, oend, base);
             __builtin_amdgcn_wave_barrier();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -306,7 +313,7 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
         const uint64_t o0 = __shfl(o, (int)first, 64);
         const uint64_t oend = __shfl(o + ln[r] + 1u, (int)last, 64);
         const uint64_t base = o0 & ~15ull;
-        wave_copy_round<WIN>(src, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, st[r], ln[r],
+        wave_copy_round<WIN, TWO>(src, src2, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, st[r], ln[r],
                         (uint32_t)(o - base), o0, oend, base);
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -319,7 +326,7 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
         const uint2 *__restrict__ cache, uint32_t n, const uint64_t *__restrict__ pre,              \
         const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, uint2 *__restrict__ out_spans,  \
         const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout, int dbg) {                   \
-        emit_apply_body<SPARSE, WIN>(cache, n, pre, src, dst, out_spans, kin, kout, dbg);           \
+        emit_apply_body<SPARSE, WIN>(cache, n, pre, src, nullptr, dst, out_spans, kin, kout, dbg);  \
     }
 SG_EMIT_APPLY(k_emit_sorted, false, EM_WIN)
 SG_EMIT_APPLY(k_emit_uniq, true, EM_WIN)
