@@ -71,6 +71,8 @@ enum Slot : int {
     // probe path (sg_dedup.hip: cur records looked up in a sorted prior's hash table)
     S_PB_TAB, S_PB_BITS, S_PB_NEW, S_PB_IDX, S_PB_SP, S_PB_K, S_PB_INS, S_PB_KB, S_PB_MI, S_PB_STAT,
     S_PB_H, S_PB_RK, S_PB_CNT, S_PB_OFF, S_PB_E, S_PB_ERR,
+    // hit sort by record buckets (sg_match.hip)
+    S_HB_CNT, S_HB_OFF, S_HB_OUT, S_HB_ERR, S_HB_SEL2,
     S_NSLOTS
 };
 

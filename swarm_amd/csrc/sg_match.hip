@@ -1419,6 +1419,11 @@ __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
 }
 
 // ------------------------------------------------------------------ host driver
+struct U32Val {
+    const uint32_t *v;
+    __device__ uint64_t operator()(uint32_t i) const { return v[i]; }
+};
+
 struct HitKeyPred {
     const unsigned long long *K;
     uint32_t n;
@@ -1427,6 +1432,107 @@ struct HitKeyPred {
 struct RecHeadPred {
     const unsigned long long *K;
     __device__ uint32_t operator()(uint32_t i) const { return (i == 0 || (K[i] >> 32) != (K[i - 1] >> 32)) ? 1u : 0u; }
+};
+
+// ------------------------------------------------------------------ hit sort by record buckets
+// The (record << 32 | signature) hits come from the engines in arbitrary order (per-block
+// flushes). Instead of an LSD radix sort over ~37 key bits (6 passes on C3's 33M hits), they
+// are bucketed by record (HB_RB records per bucket): a count pass (per-block LDS histograms),
+// a scan, a scatter pass (LDS ranks), then one block per bucket sorts its hits in LDS — a
+// counting sort by record, then an insertion sort of each record's few signatures. A bucket
+// over HB_CAP hits (one record holding thousands of hits) sets *err and the caller falls back
+// to the radix sort of the original hits.
+constexpr uint32_t HB_RBMAX = 12;     // log2 records per bucket, at most (LDS counters)
+constexpr uint32_t HB_CAP = 6144;     // hits per bucket sorted in LDS
+constexpr uint32_t HB_T = 1024;       // count/scatter/sort block
+constexpr uint32_t HB_NBLK = 256;     // count/scatter blocks
+
+__global__ __launch_bounds__(HB_T) void k_hb_count(const unsigned long long *__restrict__ hits, uint32_t n,
+                                                    uint32_t nb, uint32_t rb, uint32_t *__restrict__ cnt) {
+    extern __shared__ uint32_t s_h[];
+    for (uint32_t x = threadIdx.x; x < nb; x += HB_T) s_h[x] = 0;
+    __syncthreads();
+    const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint32_t a = blockIdx.x * per, e = min(n, a + per);
+    for (uint32_t i = a + threadIdx.x; i < e; i += HB_T) atomicAdd(&s_h[(uint32_t)(hits[i] >> (32 + rb))], 1u);
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < nb; x += HB_T) cnt[(size_t)x * gridDim.x + blockIdx.x] = s_h[x];
+}
+
+__global__ __launch_bounds__(HB_T) void k_hb_scatter(const unsigned long long *__restrict__ hits, uint32_t n,
+                                                      uint32_t nb, uint32_t rb, const uint64_t *__restrict__ off,
+                                                      unsigned long long *__restrict__ out) {
+    extern __shared__ uint32_t s_h[];
+    for (uint32_t x = threadIdx.x; x < nb; x += HB_T) s_h[x] = 0;
+    __syncthreads();
+    const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint32_t a = blockIdx.x * per, e = min(n, a + per);
+    for (uint32_t i = a + threadIdx.x; i < e; i += HB_T) {
+        const unsigned long long k = hits[i];
+        const uint32_t b = (uint32_t)(k >> (32 + rb));
+        const uint32_t r = atomicAdd(&s_h[b], 1u);
+        out[off[(size_t)b * gridDim.x + blockIdx.x] + r] = k;
+    }
+}
+
+// One block per bucket: its hits (m <= HB_CAP) counting-sorted by record in LDS, each
+// record's run insertion-sorted (by signature), written back in place.
+__global__ __launch_bounds__(HB_T) void k_hb_sort(unsigned long long *__restrict__ keys, const uint64_t *__restrict__ off,
+                                                   uint32_t nblk, uint32_t nb, uint32_t rb, uint32_t n,
+                                                   uint32_t *__restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_k[];  // HB_CAP keys
+    uint32_t *s_c = reinterpret_cast<uint32_t *>(s_k + HB_CAP);             // 2^rb counters
+    __shared__ uint32_t s_red[HB_T / 64];
+    constexpr uint32_t PER = (1u << HB_RBMAX) / HB_T;
+    const uint32_t NR = 1u << rb;
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint64_t e0 = off[(size_t)b * nblk];
+    const uint64_t e1 = (b + 1 < nb) ? off[(size_t)(b + 1) * nblk] : (uint64_t)n;
+    const uint32_t m = (uint32_t)(e1 - e0);
+    if (m > HB_CAP) {
+        if (t == 0) *err = 1u;
+        return;
+    }
+    if (m <= 1) return;
+    for (uint32_t x = t; x < NR; x += HB_T) s_c[x] = 0;
+    __syncthreads();
+    for (uint32_t q = t; q < m; q += HB_T) atomicAdd(&s_c[(uint32_t)(keys[e0 + q] >> 32) & (NR - 1u)], 1u);
+    __syncthreads();
+    // exclusive scan of the NR counters: thread t owns counters PER*t .. PER*t + PER - 1
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) { v[j] = (PER * t + j < NR) ? s_c[PER * t + j] : 0u; sum += v[j]; }
+    uint32_t tot;
+    uint32_t run = block_excl_scan<HB_T>(sum, &tot, s_red);
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) { if (PER * t + j < NR) s_c[PER * t + j] = run; run += v[j]; }
+    __syncthreads();
+    for (uint32_t q = t; q < m; q += HB_T) {
+        const unsigned long long k = keys[e0 + q];
+        s_k[atomicAdd(&s_c[(uint32_t)(k >> 32) & (NR - 1u)], 1u)] = k;
+    }
+    __syncthreads();
+    // s_c[r] = end of record r's run = start of r + 1
+    for (uint32_t r = t; r < NR; r += HB_T) {
+        const uint32_t a = r ? s_c[r - 1] : 0u, e = s_c[r];
+        for (uint32_t i = a + 1; i < e; ++i) {
+            const unsigned long long x = s_k[i];
+            uint32_t j = i;
+            while (j > a && s_k[j - 1] > x) { s_k[j] = s_k[j - 1]; --j; }
+            s_k[j] = x;
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < m; q += HB_T) keys[e0 + q] = s_k[q];
+}
+
+// Sorted hits: bit 0 = first of its (record, signature), bit 1 = first of its record.
+struct HitHeadsPred {
+    const unsigned long long *K;
+    __device__ uint32_t operator()(uint32_t i) const {
+        const unsigned long long k = K[i], p = i ? K[i - 1] : ~k;
+        return (k != p ? 1u : 0u) | ((k >> 32) != (p >> 32) ? 2u : 0u);
+    }
 };
 
 __global__ void k_split_hits(const unsigned long long *K, const uint32_t *idx, uint32_t n, uint32_t *rec, uint32_t *sig) {
@@ -1684,22 +1790,64 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         if (total <= cap) break;
         cap = std::min<uint64_t>((uint64_t)total + (total >> 3) + 1024, 0xfffff000ull);
     }
-    // sort (rec << 32 | sig) and de-duplicate
-    uint64_t *k2;
-    uint32_t *v1, *v2;
-    SG_TRY(slot(c, S_R_KEY2, (size_t)total + 1, &k2));
-    SG_TRY(slot(c, S_R_VAL, (size_t)total + 1, &v1));
-    SG_TRY(slot(c, S_R_VAL2, (size_t)total + 1, &v2));
-    int rbits = 1;
-    while (rbits < 32 && (1u << rbits) < R) ++rbits;
-    uint64_t *K;
-    uint32_t *V;
-    SG_TRY(radix_sort(c, reinterpret_cast<uint64_t *>(hits), v1, k2, v2, total, 0, 32 + rbits, true, &K, &V, "rs_pass_hits"));
-    const unsigned long long *KK = reinterpret_cast<const unsigned long long *>(K);
-    uint32_t *sel;
+    // sort (rec << 32 | sig): record buckets sorted in LDS (the radix sort when a bucket
+    // overflows, or with SG_HIT_RADIX=1)
+    const unsigned long long *KK = hits;
+    bool sorted = false;
+    const char *e_hr = getenv("SG_HIT_RADIX");
+    // bucket width: 4096 records, narrower when the hits are dense (about HB_CAP / 2 per bucket)
+    uint32_t rb = HB_RBMAX;
+    while (rb > 4 && (double)total * (1u << rb) / std::max<uint32_t>(R, 1u) > HB_CAP / 2) --rb;
+    const uint32_t nb = (uint32_t)(((uint64_t)R + (1u << rb) - 1) >> rb);
+    if (total > 1 && !(e_hr && atoi(e_hr)) && nb <= 12288) {
+        const uint32_t nblk = std::max<uint32_t>(1u, std::min<uint32_t>(HB_NBLK, (total + 4095) / 4096));
+        const size_t nc = (size_t)nb * nblk;
+        uint32_t *hcnt, *herr;
+        uint64_t *hoff;
+        unsigned long long *hout;
+        SG_TRY(slot(c, S_HB_CNT, nc, &hcnt));
+        SG_TRY(slot(c, S_HB_OFF, nc, &hoff));
+        SG_TRY(slot(c, S_HB_OUT, (size_t)total + 1, &hout));
+        SG_TRY(slot(c, S_HB_ERR, 1, &herr));
+        SG_HIP(hipMemsetAsync(herr, 0, 4, c->stream));
+        SG_LAUNCH_B(c, "hit_count", 8.0 * total, k_hb_count, nblk, HB_T, nb * 4, hits, total, nb, rb, hcnt);
+        const uint32_t nt = (uint32_t)((nc + SCAN_TILE - 1) / SCAN_TILE);
+        uint64_t *tp;
+        SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
+        SG_LAUNCH(c, "scan.count", k_scan64_count<U32Val>, nt, SCAN_BLOCK, 0, U32Val{hcnt}, (uint32_t)nc, tp);
+        SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
+        SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32Val>, nt, SCAN_BLOCK, 0, U32Val{hcnt}, (uint32_t)nc, tp + nt, hoff);
+        SG_LAUNCH_B(c, "hit_scatter", 16.0 * total, k_hb_scatter, nblk, HB_T, nb * 4, hits, total, nb, rb, hoff, hout);
+        const uint32_t lds = HB_CAP * 8 + (4u << HB_RBMAX);
+        SG_HIP(hipFuncSetAttribute((const void *)k_hb_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        SG_LAUNCH_B(c, "hit_sort", 16.0 * total, k_hb_sort, nb, HB_T, lds, hout, hoff, nblk, nb, rb, total, herr);
+        uint32_t ev = 0;
+        SG_TRY(ctx_readback(c, &ev, herr, 4));
+        if (!ev) {
+            KK = hout;
+            sorted = true;
+        }
+    }
+    if (!sorted) {
+        uint64_t *k2;
+        uint32_t *v1, *v2;
+        SG_TRY(slot(c, S_R_KEY2, (size_t)total + 1, &k2));
+        SG_TRY(slot(c, S_R_VAL, (size_t)total + 1, &v1));
+        SG_TRY(slot(c, S_R_VAL2, (size_t)total + 1, &v2));
+        int rbits = 1;
+        while (rbits < 32 && (1u << rbits) < R) ++rbits;
+        uint64_t *K;
+        uint32_t *V;
+        SG_TRY(radix_sort(c, reinterpret_cast<uint64_t *>(hits), v1, k2, v2, total, 0, 32 + rbits, true, &K, &V,
+                          "rs_pass_hits"));
+        KK = reinterpret_cast<const unsigned long long *>(K);
+    }
+    // unique hits and matched records in one selection (one host sync for both counts)
+    uint32_t *sel, *sel2;
     SG_TRY(slot(c, S_SEL, (size_t)total + 16, &sel));
-    uint32_t H = 0;
-    SG_TRY(select_one(c, "hits_unique", HitKeyPred{KK, total}, total, sel, &H));
+    SG_TRY(slot(c, S_HB_SEL2, (size_t)total + 16, &sel2));
+    uint32_t H = 0, M = 0;
+    SG_TRY(run_select2(c, "hits_heads", HitHeadsPred{KK}, total, sel, sel2, &H, &M));
     uint32_t *rec, *sig;
     SG_TRY(slot(c, S_M_SIG, (size_t)H + 1, &sig));
     SG_TRY(slot(c, S_R_GID, (size_t)H + 1, &rec));
@@ -1709,8 +1857,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     res->n_hits = H;
     if (!want_lines) return SG_OK;
     // matched records (input order) -> grep output
-    uint32_t M = 0;
-    SG_TRY(select_one(c, "hits_recs", RecHeadPred{KK}, total, sel, &M));
+    sel = sel2;
     uint32_t *mrec;
     SG_TRY(slot(c, S_R_POS, (size_t)M + 1, &mrec));
     if (M) SG_LAUNCH(c, "rec_of", k_rec_of, (M + 255) / 256, 256, 0, KK, sel, M, mrec);

@@ -289,3 +289,27 @@ def test_regex_fuzz_anchored_verify(sg, seed):
     finally:
         os.environ.pop("SG_REGEX_ANCHORED", None)
     assert m.match(data) == S.regex_hits(data, pats, nocase=seed % 2 == 1)
+
+
+@pytest.mark.parametrize("dense", [False, True])
+def test_hit_sort_buckets_vs_radix(dense, monkeypatch):
+    """Hits sorted by record buckets in LDS equal the radix sort's (SG_HIT_RADIX=1) and the
+    oracle's; the dense case (thousands of hits per record: every occurrence is a hit
+    before de-duplication) overflows the buckets and falls back to the radix sort."""
+    import swarm_amd
+    rng = random.Random(77 + dense)
+    if dense:
+        sigs = [b"a", b"b", b"ab", b"ba", b"aba", b"bab", b"abab"]
+        data = b"\n".join(bytes(rng.choice(b"ab") for _ in range(rng.randint(1, 3000))) for _ in range(300)) + b"\n"
+    else:
+        sigs = rng.sample([w for w in WORDS if len(w) >= 4], 300)
+        data = planted_corpus(rng, 40000, sigs, frac=0.3)
+    m = swarm_amd.Matcher(sigs, "literal")
+    a = m.match(data)
+    la = m.match_lines(data)
+    monkeypatch.setenv("SG_HIT_RADIX", "1")
+    b = m.match(data)
+    hits = S.literal_hits(data, sigs)
+    assert a == b == hits
+    assert la == m.match_lines(data) == S.matched_lines(data, hits)
+    m.close()
