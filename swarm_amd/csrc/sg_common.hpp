@@ -73,6 +73,7 @@ enum Slot : int {
     S_PB_H, S_PB_RK, S_PB_CNT, S_PB_OFF, S_PB_E, S_PB_ERR,
     // hit sort by record buckets (sg_match.hip)
     S_HB_CNT, S_HB_OFF, S_HB_OUT, S_HB_ERR, S_HB_SEL2,
+    S_TS2,  // two-level tile scan scratch
     S_NSLOTS
 };
 

@@ -288,8 +288,60 @@ __global__ __launch_bounds__(TS_BLOCK) void k_tile_scan(const uint64_t *__restri
     if (threadIdx.x == 0) *total = carry;
 }
 
+// Large scans (a 4 GB parse has ~250k tiles: 62 rounds of one block, ~90 us) go in two
+// levels: per-chunk sums by many blocks, the one-block scan of those, then each chunk's
+// exclusive prefixes from its chunk base.
+constexpr uint32_t TS_CHUNK = TS_BLOCK * TS_ITEMS;
+
+__global__ __launch_bounds__(TS_BLOCK) void k_ts_sum(const uint64_t *__restrict__ tot, uint32_t nt,
+                                                     uint64_t *__restrict__ part) {
+    __shared__ uint64_t s_red[TS_BLOCK / 64];
+    const uint32_t i0 = blockIdx.x * TS_CHUNK + threadIdx.x * TS_ITEMS;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < TS_ITEMS; ++j) sum += (i0 + j < nt) ? tot[i0 + j] : 0ull;
+    sum = wave_sum(sum);
+    if (lane_id() == 0) s_red[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < TS_BLOCK / 64; ++w) t += s_red[w];
+        part[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(TS_BLOCK) void k_ts_apply(const uint64_t *__restrict__ tot, uint32_t nt,
+                                                       const uint64_t *__restrict__ ppre, uint64_t *__restrict__ pre,
+                                                       uint64_t init) {
+    __shared__ uint64_t s_red[TS_BLOCK / 64];
+    const uint32_t i0 = blockIdx.x * TS_CHUNK + threadIdx.x * TS_ITEMS;
+    uint64_t v[TS_ITEMS], sum = 0;
+#pragma unroll
+    for (int j = 0; j < TS_ITEMS; ++j) {
+        v[j] = (i0 + j < nt) ? tot[i0 + j] : 0ull;
+        sum += v[j];
+    }
+    uint64_t btot;
+    uint64_t run = init + ppre[blockIdx.x] + block_excl_scan<TS_BLOCK>(sum, &btot, s_red);
+#pragma unroll
+    for (int j = 0; j < TS_ITEMS; ++j) {
+        if (i0 + j < nt) pre[i0 + j] = run;
+        run += v[j];
+    }
+}
+
 int tile_scan(sg_ctx *c, const uint64_t *tot, uint32_t nt, uint64_t *pre, uint64_t *total, uint64_t init) {
-    SG_LAUNCH(c, "tile_scan", k_tile_scan, 1, TS_BLOCK, 0, tot, nt, pre, total, init);
+    if (nt <= 2 * TS_CHUNK) {
+        SG_LAUNCH(c, "tile_scan", k_tile_scan, 1, TS_BLOCK, 0, tot, nt, pre, total, init);
+        return SG_OK;
+    }
+    const uint32_t nc = (nt + TS_CHUNK - 1) / TS_CHUNK;
+    uint64_t *part;
+    SG_TRY(slot(c, S_TS2, 2 * (size_t)nc, &part));
+    SG_LAUNCH(c, "tile_scan", k_ts_sum, nc, TS_BLOCK, 0, tot, nt, part);
+    SG_LAUNCH(c, "tile_scan", k_tile_scan, 1, TS_BLOCK, 0, part, nc, part + nc, total, 0ull);
+    SG_LAUNCH(c, "tile_scan", k_ts_apply, nc, TS_BLOCK, 0, tot, nt, part + nc, pre, init);
     return SG_OK;
 }
 

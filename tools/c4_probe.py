@@ -18,7 +18,9 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sig = json.load(open(os.path.join(root, "tests", "golden", "signatures.json")))
 nuc = [base64.b64decode(r["p"]) for r in sig["regexes"]]
 syn = corpus.nmap_signatures()
-pats = {"all": nuc + syn, "nuclei": nuc, "nmap": syn}[which]
+pats = {"all": nuc + syn, "nuclei": nuc, "nmap": syn, "bench": None}[which]
+if pats is None:  # the bench's C4 set (generic extractor regexes left out)
+    pats, _ = corpus.c4_signatures(nuc)
 buf = corpus.lines_from_pool(corpus.banner_pool(), n_lines, seed=3)
 d = torch.from_numpy(buf).cuda()
 ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
