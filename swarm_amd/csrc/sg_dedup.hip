@@ -703,6 +703,74 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
     }
 }
 
+// k_lcp over cur fused with the 8 digit histograms of cur's keys (k_rs_hist's per-wave LDS
+// counting), so the keys are read once for both (C2: one 80 MB pass and a launch fewer).
+__global__ __launch_bounds__(256) void k_lcp_hist(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
+                                                  const uint64_t *__restrict__ keys, uint32_t n,
+                                                  const uint8_t *__restrict__ rbuf, const uint2 *__restrict__ rspans,
+                                                  const uint64_t *__restrict__ rkeys, uint32_t *__restrict__ out,
+                                                  uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[4][8][256];
+    __shared__ uint32_t s_min[4];
+    for (int x = threadIdx.x; x < 4 * 8 * 256; x += 256) (&h[0][0][0])[x] = 0;
+    __syncthreads();
+    const int wid = threadIdx.x >> 6;
+    const uint64_t kr = rkeys[0];
+    const uint32_t tr = (uint32_t)(kr & 0xffu);
+    uint32_t best = 255;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t n_up = ((n + stride - 1) / stride) * stride;  // every lane runs the same trips (ballots)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
+        const bool valid = i < n;
+        const uint64_t k = valid ? keys[i] : 0ull;
+        if (valid) {
+            const uint64_t x = (k ^ kr) >> 8;
+            const uint32_t tk = (uint32_t)(k & 0xffu);
+            uint32_t l;
+            if (x) {
+                l = min((uint32_t)__builtin_clzll(x << 8) >> 3, min(tk, tr));
+            } else if (tk < 8u || tr < 8u) {
+                l = min(tk, tr);
+            } else {
+                const uint2 xs = spans[i], r = rspans[0];
+                const uint32_t m = min(min(xs.y - xs.x, r.y - r.x), best);
+                l = 7;
+                while (l < m) {
+                    const uint32_t t = (m - l) < 8u ? (m - l) : 8u;
+                    const uint64_t d = load_le(buf, xs.x + l, t) ^ load_le(rbuf, r.x + l, t);
+                    if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
+                    l += t;
+                }
+                l = min(l, m);
+            }
+            best = min(best, l);
+        }
+        const uint32_t cnt = (uint32_t)__popcll(__ballot(valid));
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const uint32_t d = (uint32_t)(k >> (8 * p)) & 255u;
+            const uint32_t d0 = (uint32_t)__shfl(d, 0, 64);
+            if (__all(!valid || d == d0)) {
+                if (lane_id() == 0 && cnt) h[wid][p][d0] += cnt;
+            } else if (valid) {
+                atomicAdd(&h[wid][p][d], 1u);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    if (lane_id() == 0) s_min[wid] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
+        if (b < 255u && b < __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(out, b);
+    }
+    for (int x = threadIdx.x; x < 8 * 256; x += 256) {
+        const uint32_t v = h[0][0][x] + h[1][0][x] + h[2][0][x] + h[3][0][x];
+        if (v) atomicAdd(&hist[x], v);
+    }
+}
+
 // key0 (7 bytes + min(rem, 8)) -> the kw-byte key (kw bytes + min(rem, kw + 1)).
 __global__ __launch_bounds__(256) void k_narrow_keys(uint64_t *__restrict__ keys, uint32_t n, uint32_t kw) {
     const uint64_t top = ~0ull << (64u - 8u * kw);
@@ -1179,7 +1247,10 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
             uv->n = R;
             uv->bytes = R ? (uint64_t)0 : 0;  // not used for an input view
             if (!trust_sorted) {
-                // a single record: serialize it (the caller may return this view)
+                // a single record: serialize it (the caller may return this view); its key
+                // narrowed here (a sort would have done it on its first pass)
+                if ((base >> 16) < 7u)
+                    SG_LAUNCH(c, "narrow_keys", k_narrow_keys, 1, 256, 0, L.keys, R, base >> 16);
                 uint8_t *ub;
                 uint2 *us;
                 uint64_t *uk;
@@ -1212,7 +1283,9 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, vs.lines.vals2, R, &v2));
     uint64_t *K;
     uint2 *V;
-    SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V, "rs_pass", host_hist));
+    // the key narrowing to kw bytes happens in the sort's first pass
+    SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V, "rs_pass", host_hist,
+                            (base >> 16) < 7u ? base >> 16 : 0u));
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
     uint8_t *brk;
@@ -1527,20 +1600,29 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint8_t *rbuf = ref_cur ? d_cur : d_prior;
     const uint2 *rsp = ref_cur ? Lc.spans : (have_prior ? Lp.spans : nullptr);
     const uint64_t *rkeys = ref_cur ? Lc.keys : (have_prior ? Lp.keys : nullptr);
-    if (rsp && Lc.n_rec && !cur_lcp)
+    static const int narrow_env = getenv("SG_NARROW_KEYS") ? atoi(getenv("SG_NARROW_KEYS")) : 1;
+    const bool want_hist = narrow_env && Lc.n_rec >= 4096;
+    const uint32_t *dhist = nullptr;
+    const bool fuse_hist = want_hist && rsp && Lc.n_rec && !cur_lcp;
+    if (fuse_hist) {
+        uint32_t *hist;
+        SG_TRY(slot(c, S_HIST, 8 * 256 * 2 + 8, &hist));
+        SG_HIP(hipMemsetAsync(hist, 0, 8 * 256 * 4, c->stream));
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp_hist, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 1024u), 256, 0, d_cur,
+                    Lc.spans, Lc.keys, Lc.n_rec, rbuf, rsp, rkeys, dflag + 1, hist);
+        dhist = hist;
+    } else if (rsp && Lc.n_rec && !cur_lcp) {
         SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 512u), 256, 0, d_cur,
                     Lc.spans, Lc.keys, Lc.n_rec,
                     rbuf, rsp, rkeys, dflag + 1);
+    }
     if (rsp && have_prior && Lp.n_rec)
         SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 512u), 256, 0, d_prior,
                     Lp.spans, Lp.keys, Lp.n_rec,
                     rbuf, rsp, rkeys, dflag + 1);
     // the cur keys' digit histograms (for the key width below) are queued now and come back
     // with the flags; they stay valid when the common prefix turns out to be empty
-    static const int narrow_env = getenv("SG_NARROW_KEYS") ? atoi(getenv("SG_NARROW_KEYS")) : 1;
-    const bool want_hist = narrow_env && Lc.n_rec >= 4096;
-    const uint32_t *dhist = nullptr;
-    if (want_hist) SG_TRY(key_hist8_async(c, Lc.keys, Lc.n_rec, &dhist));
+    if (want_hist && !dhist) SG_TRY(key_hist8_async(c, Lc.keys, Lc.n_rec, &dhist));
     uint32_t fl[2] = {0u, 0u};
     {
         uint8_t *pin = (uint8_t *)c->pinned;
@@ -1585,8 +1667,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         if (h5 >= lg + 4.0 && (live2 || live1)) kw = 5;
         else if (h6 >= lg + 2.0 && live1) kw = 6;
         if (kw < 7) {
-            SG_LAUNCH(c, "narrow_keys", k_narrow_keys, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u), 256, 0, Lc.keys,
-                      Lc.n_rec, kw);
+            // the cur keys are narrowed by the sort's first pass (build_unique); the prior's
+            // here (its view is the input itself when sorted, and the diff compares keys)
             if (have_prior && Lp.n_rec)
                 SG_LAUNCH(c, "narrow_keys", k_narrow_keys, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0,
                           Lp.keys, Lp.n_rec, kw);

@@ -1419,9 +1419,11 @@ __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
 }
 
 // ------------------------------------------------------------------ host driver
-struct U32Val {
+// The count pass's block-major counters read in bucket-major order (i = bucket * nblk + block).
+struct HbCountT {
     const uint32_t *v;
-    __device__ uint64_t operator()(uint32_t i) const { return v[i]; }
+    uint32_t nblk, nb;
+    __device__ uint64_t operator()(uint32_t i) const { return v[(size_t)(i % nblk) * nb + i / nblk]; }
 };
 
 struct HitKeyPred {
@@ -1456,7 +1458,8 @@ __global__ __launch_bounds__(HB_T) void k_hb_count(const unsigned long long *__r
     const uint32_t a = blockIdx.x * per, e = min(n, a + per);
     for (uint32_t i = a + threadIdx.x; i < e; i += HB_T) atomicAdd(&s_h[(uint32_t)(hits[i] >> (32 + rb))], 1u);
     __syncthreads();
-    for (uint32_t x = threadIdx.x; x < nb; x += HB_T) cnt[(size_t)x * gridDim.x + blockIdx.x] = s_h[x];
+    // block-major (one contiguous row per block; the scan reads it bucket-major)
+    for (uint32_t x = threadIdx.x; x < nb; x += HB_T) cnt[(size_t)blockIdx.x * nb + x] = s_h[x];
 }
 
 __global__ __launch_bounds__(HB_T) void k_hb_scatter(const unsigned long long *__restrict__ hits, uint32_t n,
@@ -1814,9 +1817,9 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         const uint32_t nt = (uint32_t)((nc + SCAN_TILE - 1) / SCAN_TILE);
         uint64_t *tp;
         SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
-        SG_LAUNCH(c, "scan.count", k_scan64_count<U32Val>, nt, SCAN_BLOCK, 0, U32Val{hcnt}, (uint32_t)nc, tp);
+        SG_LAUNCH(c, "scan.count", k_scan64_count<HbCountT>, nt, SCAN_BLOCK, 0, HbCountT{hcnt, nblk, nb}, (uint32_t)nc, tp);
         SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
-        SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32Val>, nt, SCAN_BLOCK, 0, U32Val{hcnt}, (uint32_t)nc, tp + nt, hoff);
+        SG_LAUNCH(c, "scan.apply", k_scan64_apply<HbCountT>, nt, SCAN_BLOCK, 0, HbCountT{hcnt, nblk, nb}, (uint32_t)nc, tp + nt, hoff);
         SG_LAUNCH_B(c, "hit_scatter", 16.0 * total, k_hb_scatter, nblk, HB_T, nb * 4, hits, total, nb, rb, hoff, hout);
         const uint32_t lds = HB_CAP * 8 + (4u << HB_RBMAX);
         SG_HIP(hipFuncSetAttribute((const void *)k_hb_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

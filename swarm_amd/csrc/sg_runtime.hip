@@ -288,7 +288,7 @@ __global__ __launch_bounds__(TS_BLOCK) void k_tile_scan(const uint64_t *__restri
     if (threadIdx.x == 0) *total = carry;
 }
 
-// Large scans (a 4 GB parse has ~250k tiles: 62 rounds of one block, ~90 us) go in two
+// Large scans (> 32k tiles; a 4 GB parse has ~250k: 62 rounds of one block, ~90 us) go in two
 // levels: per-chunk sums by many blocks, the one-block scan of those, then each chunk's
 // exclusive prefixes from its chunk base.
 constexpr uint32_t TS_CHUNK = TS_BLOCK * TS_ITEMS;
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(TS_BLOCK) void k_ts_apply(const uint64_t *__restric
 }
 
 int tile_scan(sg_ctx *c, const uint64_t *tot, uint32_t nt, uint64_t *pre, uint64_t *total, uint64_t init) {
-    if (nt <= 2 * TS_CHUNK) {
+    if (nt <= 8 * TS_CHUNK) {  // up to 8 rounds of one block beat 3 launches
         SG_LAUNCH(c, "tile_scan", k_tile_scan, 1, TS_BLOCK, 0, tot, nt, pre, total, init);
         return SG_OK;
     }

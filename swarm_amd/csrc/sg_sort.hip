@@ -22,10 +22,19 @@ namespace sg {
 // Algorithmic bytes per pass: 12 B read + 12 B written per pair.
 
 constexpr int RS_MAXPASS = 8;
+
+// The dedup's key narrowing (sg_dedup.hip k_narrow_keys), applied while the first live pass
+// reads the keys (kw 0: none): bytes kw..6 cleared, the tag clamped to kw + 1.
+__device__ __forceinline__ uint64_t rs_narrow(uint64_t k, uint32_t kw) {
+    if (!kw) return k;
+    const uint64_t top = ~0ull << (64u - 8u * kw);
+    const uint64_t t = k & 0xffu;
+    return (k & top) | (t < kw + 1u ? t : (uint64_t)(kw + 1u));
+}
 constexpr int RS_HBLOCK = 256;
 
 __global__ __launch_bounds__(RS_HBLOCK) void k_rs_hist(const uint64_t *__restrict__ keys, uint32_t n,
-                                                       int begin_bit, int npasses, uint32_t *hist) {
+                                                       int begin_bit, int npasses, uint32_t *hist, uint32_t kw) {
     __shared__ uint32_t h[RS_HBLOCK / 64][RS_MAXPASS][256];
     for (int i = threadIdx.x; i < (RS_HBLOCK / 64) * RS_MAXPASS * 256; i += RS_HBLOCK) (&h[0][0][0])[i] = 0;
     __syncthreads();
@@ -37,7 +46,7 @@ __global__ __launch_bounds__(RS_HBLOCK) void k_rs_hist(const uint64_t *__restric
 #pragma unroll
         for (int u = 0; u < HU; ++u) {
             const uint32_t i = i0 + u * RS_HBLOCK + threadIdx.x;
-            k[u] = (i < n) ? keys[i] : 0ull;
+            k[u] = (i < n) ? rs_narrow(keys[i], kw) : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < HU; ++u) {
@@ -92,7 +101,7 @@ constexpr int RD_WAVES = RD_BLOCK / 64;
 // wave-row whose lanes share one digit adds once (skewed digits: '.' or 't' at fixed
 // positions of host names).
 __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__ keys, uint32_t n, int shift,
-                                                    uint32_t ntiles, uint32_t *__restrict__ cnt) {
+                                                    uint32_t ntiles, uint32_t *__restrict__ cnt, uint32_t kw) {
     __shared__ uint32_t h[RD_WAVES][256];
     const int wid = threadIdx.x >> 6;
     for (int x = threadIdx.x; x < RD_WAVES * 256; x += RD_BLOCK) (&h[0][0])[x] = 0;
@@ -102,7 +111,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane_id();
-        dd[i] = (pos < n) ? ((uint32_t)(keys[pos] >> shift) & 255u) : 256u;
+        dd[i] = (pos < n) ? ((uint32_t)(rs_narrow(keys[pos], kw) >> shift) & 255u) : 256u;
     }
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
@@ -150,7 +159,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
                                                       const VT *__restrict__ vin,
                                                       uint64_t *__restrict__ kout, VT *__restrict__ vout,
                                                       uint32_t n, int shift, uint32_t ntiles,
-                                                      const uint32_t *__restrict__ toffs) {
+                                                      const uint32_t *__restrict__ toffs, uint32_t kw) {
     static_assert(sizeof(VT) <= sizeof(uint64_t), "values staged in the key buffer");
     __shared__ uint64_t s_k[RD_TILE];  // keys, then (aliased) values
     VT *s_v = reinterpret_cast<VT *>(s_k);
@@ -172,7 +181,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane;
-        k[i] = (pos < n) ? kin[pos] : ~0ull;
+        k[i] = (pos < n) ? rs_narrow(kin[pos], kw) : ~0ull;
     }
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
@@ -249,7 +258,7 @@ int key_hist8_async(sg_ctx *c, const uint64_t *keys, uint32_t n, const uint32_t 
     SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
     uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
     if (hgrid > 1024) hgrid = 1024;
-    if (n) SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, 0, RS_MAXPASS, hist);
+    if (n) SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, 0, RS_MAXPASS, hist, 0u);
     *dev_hist = hist;
     return SG_OK;
 }
@@ -260,7 +269,7 @@ int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist) 
     SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
     uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
     if (hgrid > 1024) hgrid = 1024;
-    if (n) SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, 0, RS_MAXPASS, hist);
+    if (n) SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, 0, RS_MAXPASS, hist, 0u);
     return ctx_readback(c, host_hist, hist, RS_MAXPASS * 256 * 4);
 }
 
@@ -270,7 +279,8 @@ int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist) 
 template <typename VT>
 static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt, VT *vals_alt,
                         uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
-                        VT **vals_out, const char *pass_name, const uint32_t *host_hist = nullptr) {
+                        VT **vals_out, const char *pass_name, const uint32_t *host_hist = nullptr,
+                        uint32_t narrow_kw = 0) {
     *keys_out = keys;
     *vals_out = vals;
     if (n == 0) return SG_OK;
@@ -294,7 +304,8 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
         SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
         uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
         if (hgrid > 1024) hgrid = 1024;
-        SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, begin_bit, npasses, hist);
+        SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, begin_bit, npasses, hist,
+                    narrow_kw);
         SG_LAUNCH(c, "rs_scan", k_rs_scan, npasses, 256, 0, hist, offs, triv, n);
         SG_TRY(ctx_readback(c, trivial, triv, npasses * 4));
     }
@@ -309,18 +320,21 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     VT *cv = vals, *av = vals_alt;
     bool iota_pending = iota_vals;
     constexpr double VB = (double)sizeof(VT);
+    if (narrow_kw && begin_bit != 0) { set_error("radix_sort: narrowing needs the keys' bit 0"); return SG_E_INVAL; }
+    if (narrow_kw && nlive == 0) live[nlive++] = 0;  // one (no-op) pass still writes the narrowed keys
     for (int q = 0; q < nlive; ++q) {
         const int p = live[q];
         const int shift = begin_bit + 8 * p;
-        SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, ntiles, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt);
+        const uint32_t kw = q == 0 ? narrow_kw : 0u;  // the first pass narrows as it reads
+        SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, ntiles, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, kw);
         SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, offs + p * 256);
         if constexpr (sizeof(VT) == 4) {
             if (iota_pending)
-                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt);
+                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw);
             else
-                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt);
+                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw);
         } else {
-            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt);
+            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw);
         }
         // 8 B key + the value read (implied for iota ids) and both written, per pair
         prof_bytes(c, pass_name, (iota_pending ? 16.0 + VB : 16.0 + 2.0 * VB) * n);
@@ -349,9 +363,9 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
 
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out, const char *pass_name,
-                     const uint32_t *host_hist) {
+                     const uint32_t *host_hist, uint32_t narrow_kw) {
     return radix_sort_t<uint2>(c, keys, spans, keys_alt, spans_alt, n, begin_bit, end_bit, false, keys_out, spans_out,
-                               pass_name, host_hist);
+                               pass_name, host_hist, narrow_kw);
 }
 
 }  // namespace sg
