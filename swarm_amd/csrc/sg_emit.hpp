@@ -105,6 +105,76 @@ __device__ __forceinline__ void put_short_win(uint8_t *win, uint32_t d, const ui
     }
 }
 
+// One 64-byte window of a medium record: bytes [sh, sh + len) of the window c[] (len <=
+// 64 - sh) written at base + d, then '\n' when nl. Same normalise / mask / funnel scheme as
+// put_short_win, for up to 64 bytes (17 destination dwords); base is an LDS window or HBM.
+__device__ __forceinline__ void put_win64(uint8_t *base, uint32_t d, const uint4 (&c)[4], uint32_t sh, uint32_t len,
+                                          bool nl) {
+    const uint32_t dw[20] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w,
+                             c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w, 0u, 0u, 0u, 0u};
+    const uint32_t t = sh >> 2, e = sh & 3u;
+    const uint32_t m2 = (t & 2u) ? ~0u : 0u, m1 = (t & 1u) ? ~0u : 0u;
+    uint32_t s1[18], s2[17], rec[17];
+#pragma unroll
+    for (int o = 0; o < 18; ++o) s1[o] = dw[o] ^ ((dw[o] ^ dw[o + 2]) & m2);
+#pragma unroll
+    for (int o = 0; o < 17; ++o) s2[o] = s1[o] ^ ((s1[o] ^ s1[o + 1]) & m1);
+#pragma unroll
+    for (int o = 0; o < 17; ++o) {
+        uint32_t x = (o < 16) ? __builtin_amdgcn_alignbyte(s2[o + 1], s2[o], e) : 0u;
+        const uint32_t b0 = 4u * o;
+        if (b0 + 4u > len) {
+            if (b0 <= len) {
+                const uint32_t k = len - b0;
+                x = (x & ((1u << (8u * k)) - 1u)) | (nl ? (0x0au << (8u * k)) : 0u);
+            } else {
+                x = 0u;
+            }
+        }
+        rec[o] = x;
+    }
+    const uint32_t f = d & 3u, D = d - f, end = f + len + (nl ? 1u : 0u);
+    const uint32_t mf = f ? ~0u : 0u;
+#pragma unroll
+    for (int j = 0; j < 18; ++j) {
+        const uint32_t b0 = 4u * j;
+        if (b0 >= end) break;
+        const uint32_t cur = (j < 17) ? rec[j] : 0u;
+        const uint32_t lo = (j > 0) ? rec[j - 1] : 0u;
+        const uint32_t sh_v = __builtin_amdgcn_alignbyte(cur, lo, (4u - f) & 3u);
+        const uint32_t v = (cur & ~mf) | (sh_v & mf);
+        if (b0 >= f && b0 + 4u <= end) {
+            *reinterpret_cast<uint32_t *>(base + D + b0) = v;
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b)
+                if (b0 + b >= f && b0 + b < end) base[D + b0 + b] = (uint8_t)(v >> (8 * b));
+        }
+    }
+}
+
+// A medium record (longer than the short path, <= EM_MED bytes) copied by its own lane in
+// 64-byte windows: each window's four 16-B loads are issued together, and all lanes of the
+// wave copy their records at once (the 16-lane group path copies one record per group at a
+// time: a load latency per record).
+constexpr uint32_t EM_MED = 1024;
+__device__ __forceinline__ void put_medium(const uint8_t *src, uint8_t *base, uint32_t d, uint32_t s, uint32_t len) {
+    const uint32_t q0 = s & ~15u, sh = s - q0;
+    uint32_t done = 0;
+    for (uint32_t wo = 0;; wo += 64u) {
+        const uint32_t ws = wo ? 0u : sh;
+        const uint32_t wl = min(64u - ws, len - done);
+        uint4 c[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            c[k] = (16u * k < ws + wl) ? *reinterpret_cast<const uint4 *>(src + q0 + wo + 16u * k) : make_uint4(0u, 0u, 0u, 0u);
+        const bool nl = done + wl == len;
+        put_win64(base, d + done, c, ws, wl, nl);
+        done += wl;
+        if (nl) break;
+    }
+}
+
 // Copy the records of one round into out[o0..oend) (base = o0 & ~15): lane-owned record
 // (f, s, len, dst offset d from base). Short records: the lane loads its aligned 16-byte
 // chunks (all loads of the wave in flight together) and places the bytes. Longer records:
@@ -130,7 +200,8 @@ __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src0
         c[k] = make_uint4(0u, 0u, 0u, 0u);
         if (shortr && 16u * k < sh + len) c[k] = *reinterpret_cast<const uint4 *>(src + q0 + 16u * k);
     }
-    const bool longr = f && !shortr;
+    const bool medr = f && !shortr && len <= EM_MED;
+    const bool longr = f && !shortr && !medr;
     const uint64_t ml = __ballot(longr);
     if (longr) {
         const uint32_t cidx = (uint32_t)__popcll(ml & ((1ull << lane) - 1ull));
@@ -142,6 +213,7 @@ __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src0
         if (in_lds) put_short_win(win, d, c, sh, len);
         else put_short(out + base + d, c, sh, len);
     }
+    if (medr) put_medium(src, in_lds ? win : out + base, d, s, len);
     if (ml) {
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
