@@ -74,6 +74,7 @@ enum Slot : int {
     // hit sort by record buckets (sg_match.hip)
     S_HB_CNT, S_HB_OFF, S_HB_OUT, S_HB_ERR, S_HB_SEL2,
     S_TS2,  // two-level tile scan scratch
+    S_PT_CNT, S_PT_PRE, S_PT_BASE,  // piece partition multi-split
     S_NSLOTS
 };
 

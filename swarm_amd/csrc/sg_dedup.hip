@@ -313,10 +313,27 @@ struct SegKeys {
     uint64_t c[SEG_CH];
 };
 
+// The four chunk keys from one set of wide loads: the suffix's first 28 bytes in at most
+// three aligned 16-B loads (normalised), instead of up to eight scattered 8-B loads.
 __device__ __forceinline__ SegKeys seg_keys(const uint8_t *S, uint2 x, uint32_t base) {
     SegKeys k;
+    const uint32_t off = bk_off(base), len = x.y - x.x;
+    const uint32_t rem = len > off ? len - off : 0u;
+    uint4 c[4];
+    load_chunks(S, x.x + off, rem < 28u ? rem : 28u, c);
+    uint32_t r[13];
+    normalize52(c, (x.x + off) & 15u, r);
 #pragma unroll
-    for (int q = 0; q < SEG_CH; ++q) k.c[q] = chunk_key(S, x.x, x.y, bk_off(base) + 7u * q);
+    for (int q = 0; q < SEG_CH; ++q) {
+        const uint32_t rq = rem > 7u * q ? rem - 7u * q : 0u;
+        const uint32_t d = 7u * q, a = d >> 2, sh = d & 3u;
+        const uint32_t lo = __builtin_amdgcn_alignbyte(r[a + 1], r[a], sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(r[a + 2], r[a + 1], sh);
+        uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        const uint32_t take = rq < 7u ? rq : 7u;
+        v &= (1ull << (8u * take)) - 1ull;
+        k.c[q] = rq ? ((__builtin_bswap64(v) & ~0xffull) | (rq < 8u ? rq : 8u)) : 0ull;
+    }
     return k;
 }
 

@@ -392,6 +392,7 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
     }
 }
 
+#ifndef SG_EMIT_DEVICE_ONLY  // (a translation unit that only needs the copy helpers)
 // One symbol per use, so rocprofv3 kernel stats and PMC passes attribute each separately.
 #define SG_EMIT_APPLY(NAME, SPARSE, WIN)                                                            \
     __global__ __launch_bounds__(EM_BLOCK) void NAME(                                               \
@@ -406,6 +407,7 @@ SG_EMIT_APPLY(k_emit_uniq_s, true, EM_WIN_S)
 SG_EMIT_APPLY(k_emit_fresh, true, EM_WIN)
 SG_EMIT_APPLY(k_emit_apply, false, EM_WIN)
 #undef SG_EMIT_APPLY
+#endif
 
 // ------------------------------------------------------------------ common items
 // Sorted position i -> input record V[i] (V null: record i).
