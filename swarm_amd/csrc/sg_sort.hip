@@ -92,6 +92,15 @@ __global__ void k_iota(uint32_t *v, uint32_t n) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = i;
 }
 
+// XCD-aware tile order: blocks are dispatched round-robin over the 8 XCDs (block b on XCD
+// b % 8), so block b takes tile (b % 8) * per + b / 8 — each XCD works a contiguous eighth of
+// the tiles, and the per-tile digit counts of 16 neighbouring tiles (one 64-B line of a
+// digit's row) are written through one L2 instead of eight partial lines in eight L2s.
+__device__ __forceinline__ uint32_t rs_tile_of(uint32_t b, uint32_t ntiles) {
+    const uint32_t per = (ntiles + 7u) / 8u;
+    return (b & 7u) * per + (b >> 3);
+}
+
 constexpr int RD_BLOCK = 256;
 constexpr int RD_ITEMS = 16;
 constexpr int RD_TILE = RD_BLOCK * RD_ITEMS;
@@ -101,12 +110,14 @@ constexpr int RD_WAVES = RD_BLOCK / 64;
 // wave-row whose lanes share one digit adds once (skewed digits: '.' or 't' at fixed
 // positions of host names).
 __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__ keys, uint32_t n, int shift,
-                                                    uint32_t ntiles, uint32_t *__restrict__ cnt, uint32_t kw) {
+                                                    uint32_t ntiles, uint32_t *__restrict__ cnt, uint32_t kw, bool xcd) {
     __shared__ uint32_t h[RD_WAVES][256];
     const int wid = threadIdx.x >> 6;
+    const uint32_t tile = xcd ? rs_tile_of(blockIdx.x, ntiles) : blockIdx.x;
+    if (tile >= ntiles) return;
     for (int x = threadIdx.x; x < RD_WAVES * 256; x += RD_BLOCK) (&h[0][0])[x] = 0;
     __syncthreads();
-    const uint32_t wbase = blockIdx.x * RD_TILE + wid * (RD_ITEMS * 64);
+    const uint32_t wbase = tile * RD_TILE + wid * (RD_ITEMS * 64);
     uint32_t dd[RD_ITEMS];
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
@@ -128,7 +139,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__
     uint32_t v = 0;
 #pragma unroll
     for (int w = 0; w < RD_WAVES; ++w) v += h[w][threadIdx.x];
-    cnt[(size_t)threadIdx.x * ntiles + blockIdx.x] = v;
+    cnt[(size_t)threadIdx.x * ntiles + tile] = v;
 }
 
 // One block per digit d: cnt[d][t] -> exclusive prefix over tiles + goffs[d].
@@ -159,7 +170,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
                                                       const VT *__restrict__ vin,
                                                       uint64_t *__restrict__ kout, VT *__restrict__ vout,
                                                       uint32_t n, int shift, uint32_t ntiles,
-                                                      const uint32_t *__restrict__ toffs, uint32_t kw) {
+                                                      const uint32_t *__restrict__ toffs, uint32_t kw, bool xcd) {
     static_assert(sizeof(VT) <= sizeof(uint64_t), "values staged in the key buffer");
     __shared__ uint64_t s_k[RD_TILE];  // keys, then (aliased) values
     VT *s_v = reinterpret_cast<VT *>(s_k);
@@ -171,7 +182,8 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
     for (int x = tid; x < RD_WAVES * 256; x += RD_BLOCK) (&s_wh[0][0])[x] = 0;
     __syncthreads();
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = xcd ? rs_tile_of(blockIdx.x, ntiles) : blockIdx.x;
+    if (tile >= ntiles) return;
     const uint32_t tbase = tile * RD_TILE;
     const uint32_t wbase = tbase + wid * (RD_ITEMS * 64);
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -320,21 +332,24 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     VT *cv = vals, *av = vals_alt;
     bool iota_pending = iota_vals;
     constexpr double VB = (double)sizeof(VT);
+    const char *e_x = getenv("SG_RS_XCD");
+    const bool xcd = e_x ? atoi(e_x) != 0 : true;
+    const uint32_t grid = xcd ? 8u * ((ntiles + 7u) / 8u) : ntiles;
     if (narrow_kw && begin_bit != 0) { set_error("radix_sort: narrowing needs the keys' bit 0"); return SG_E_INVAL; }
     if (narrow_kw && nlive == 0) live[nlive++] = 0;  // one (no-op) pass still writes the narrowed keys
     for (int q = 0; q < nlive; ++q) {
         const int p = live[q];
         const int shift = begin_bit + 8 * p;
         const uint32_t kw = q == 0 ? narrow_kw : 0u;  // the first pass narrows as it reads
-        SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, ntiles, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, kw);
+        SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, grid, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, kw, xcd);
         SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, offs + p * 256);
         if constexpr (sizeof(VT) == 4) {
             if (iota_pending)
-                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw);
+                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
             else
-                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw);
+                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
         } else {
-            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), ntiles, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw);
+            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
         }
         // 8 B key + the value read (implied for iota ids) and both written, per pair
         prof_bytes(c, pass_name, (iota_pending ? 16.0 + VB : 16.0 + 2.0 * VB) * n);
