@@ -339,75 +339,101 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
         uint32_t first_nws = JS_NONE, last_nws = 0, c0 = 0;
         int cur_key = -1;
         bool in_str = false, esc = false, kesc = false, bad = false, done = false;
+        // Per 16-byte chunk, SWAR masks of the event bytes (quote, backslash, { [ } ] : ,) and
+        // only those positions walked through the state machine — JSON lines hold an event
+        // every few bytes, and every other byte only matters for the line's first and last
+        // non-blank bytes (found after the walk). Escapes act inside strings only, as in a
+        // byte walk: a backslash escapes the next byte, whatever it is.
+        uint32_t esc_pos = JS_NONE;
         for (uint32_t w = sp.x & ~15u; w < sp.y && !bad; w += 16) {
             const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
+            uint32_t ev = 0;
             const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t x = wd[d];
+                auto eqm = [](uint32_t y) -> uint32_t {  // high bit of each zero byte of y
+                    return ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
+                };
+                const uint32_t lx = x | 0x20202020u;  // '[' -> '{', ']' -> '}'
+                const uint32_t z = eqm(x ^ 0x22222222u) | eqm(x ^ 0x5c5c5c5cu) | eqm(lx ^ 0x7b7b7b7bu) |
+                                   eqm(lx ^ 0x7d7d7d7du) | eqm(x ^ 0x3a3a3a3au) | eqm(x ^ 0x2c2c2c2cu);
+                ev |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * d);
+            }
+            if (w < sp.x) ev &= ~0u << (sp.x - w);
+            if (sp.y - w < 16u) ev &= (1u << (sp.y - w)) - 1u;
+            while (ev && !bad) {
+                const uint32_t j = (uint32_t)__builtin_ctz(ev);
+                ev &= ev - 1u;
                 const uint32_t q = w + j;
-                if (q < sp.x || q >= sp.y || bad) continue;
-                const uint32_t b = (wd[j >> 2] >> (8 * (j & 3))) & 0xffu;
-                if (!js_ws((uint8_t)b)) {
-                    if (first_nws == JS_NONE) first_nws = q;
-                    last_nws = q;
-                }
+                const uint32_t xw = (j < 8u) ? ((j < 4u) ? v.x : v.y) : ((j < 12u) ? v.z : v.w);
+                const uint32_t b = (xw >> (8u * (j & 3u))) & 0xffu;
                 if (in_str) {
-                    if (q == str_s) c0 = b;
-                    if (esc) esc = false;
-                    else if (b == '\\') esc = kesc = true;
+                    if (q == esc_pos) continue;  // the escaped byte
+                    if (b == '\\') { esc_pos = q + 1; kesc = true; }
                     else if (b == '"') { in_str = false; str_e = q; }
                     continue;
                 }
+                if (b == '\\') continue;  // outside strings a backslash is no event
                 if (b == '"') {
                     if (depth == 0) bad = true;
                     in_str = true;
                     kesc = false;
                     str_s = q + 1;
-                    c0 = 0x100u;
-                } else if (b == '{' || b == '[' || b == '}' || b == ']' || b == ':' || b == ',') {
-                    if (done) { bad = true; continue; }
-                    if (b == '{' || b == '[') {
-                        if (depth == 0) {
-                            if (b != '{') bad = true;
-                            open_pos = q;
-                        }
-                        ++depth;
-                    } else if (b == '}' || b == ']') {
-                        if (depth == 0) { bad = true; continue; }
-                        if (depth == 1) {
-                            if (b != '}') bad = true;
-                            if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
-                            cur_key = -1;
-                            done = true;
-                            close_pos = q;
-                        }
-                        --depth;
-                    } else if (depth == 1) {
-                        if (b == ':') {
-                            const uint32_t kl = str_e - str_s;
-                            const uint32_t id = kl | ((kl ? c0 : 0x100u) << 16);
-                            cur_key = -1;
-                            for (uint32_t k = 0; k < nk; ++k) {
-                                bool eq;
-                                if (kesc) {  // escaped key: compare its decoded form
-                                    JsKeyEq cmp{s_keys + s_koff[k], s_koff[k + 1] - s_koff[k]};
-                                    js_decode<true>(a.buf, str_s, str_e, cmp);
-                                    eq = cmp.eq();
-                                } else {
-                                    if (s_kid[k] != id) continue;
-                                    eq = true;
-                                    for (uint32_t x = 1; x < kl && eq; ++x) eq = a.buf[str_s + x] == s_keys[s_koff[k] + x];
-                                }
-                                if (eq) { cur_key = (int)k; break; }
+                    esc_pos = JS_NONE;
+                    continue;
+                }
+                if (done) { bad = true; continue; }
+                if (b == '{' || b == '[') {
+                    if (depth == 0) {
+                        if (b != '{') bad = true;
+                        open_pos = q;
+                    }
+                    ++depth;
+                } else if (b == '}' || b == ']') {
+                    if (depth == 0) { bad = true; continue; }
+                    if (depth == 1) {
+                        if (b != '}') bad = true;
+                        if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
+                        cur_key = -1;
+                        done = true;
+                        close_pos = q;
+                    }
+                    --depth;
+                } else if (depth == 1) {
+                    if (b == ':') {
+                        const uint32_t kl = str_e - str_s;
+                        const uint32_t c0 = kl ? (uint32_t)a.buf[str_s] : 0x100u;
+                        const uint32_t id = kl | (c0 << 16);
+                        cur_key = -1;
+                        for (uint32_t k = 0; k < nk; ++k) {
+                            bool eq;
+                            if (kesc) {  // escaped key: compare its decoded form
+                                JsKeyEq cmp{s_keys + s_koff[k], s_koff[k + 1] - s_koff[k]};
+                                js_decode<true>(a.buf, str_s, str_e, cmp);
+                                eq = cmp.eq();
+                            } else {
+                                if (s_kid[k] != id) continue;
+                                eq = true;
+                                for (uint32_t x = 1; x < kl && eq; ++x) eq = a.buf[str_s + x] == s_keys[s_koff[k] + x];
                             }
-                            val_s = q + 1;
-                        } else {  // ','
-                            if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
-                            cur_key = -1;
+                            if (eq) { cur_key = (int)k; break; }
                         }
+                        val_s = q + 1;
+                    } else {  // ','
+                        if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
+                        cur_key = -1;
                     }
                 }
             }
+        }
+        // the line's first and last non-blank bytes (a JSON line starts with '{' and ends
+        // with '}', so these loops stop at once)
+        if (!bad) {
+            for (uint32_t q = sp.x; q < sp.y; ++q)
+                if (!js_ws(a.buf[q])) { first_nws = q; break; }
+            for (uint32_t q = sp.y; q > sp.x; --q)
+                if (!js_ws(a.buf[q - 1])) { last_nws = q - 1; break; }
         }
         const bool ok = !bad && !in_str && depth == 0 && done && first_nws == open_pos && last_nws == close_pos;
         for (uint32_t k = 0; k < nk; ++k) {
