@@ -345,8 +345,11 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
         // non-blank bytes (found after the walk). Escapes act inside strings only, as in a
         // byte walk: a backslash escapes the next byte, whatever it is.
         uint32_t esc_pos = JS_NONE;
+        // two chunks' loads in flight per step (the walk of one chunk hides the next's latency)
+        uint4 vn = *reinterpret_cast<const uint4 *>(a.buf + (sp.x & ~15u));
         for (uint32_t w = sp.x & ~15u; w < sp.y && !bad; w += 16) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(a.buf + w);
+            const uint4 v = vn;
+            if (w + 16u < sp.y) vn = *reinterpret_cast<const uint4 *>(a.buf + w + 16u);
             uint32_t ev = 0;
             const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
