@@ -331,6 +331,43 @@ static int host_dedup_diff(const uint8_t *const *chunks, const size_t *lens, siz
     return SG_OK;
 }
 
+// Byte splitters packed for k_range_bytes: BE words of the first 64 bytes + lengths.
+struct ByteSplit {
+    uint64_t w[255 * SPL_WORDS];
+    uint32_t len[256];
+};
+
+// Splitter q = splitters[split_offs[q] .. split_offs[q+1]) cut to SPL_W bytes, packed as BE
+// words; the cut splitters must be non-decreasing in byte order.
+static int pack_byte_splitters(const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, ByteSplit *bs) {
+    memset(bs, 0, sizeof(*bs));
+    for (uint32_t q = 0; q + 1 < n_parts; ++q) {
+        if (split_offs[q + 1] < split_offs[q]) { set_error("split_offs must be non-decreasing"); return SG_E_INVAL; }
+        const uint32_t len = std::min<uint32_t>(split_offs[q + 1] - split_offs[q], SPL_W);
+        uint8_t b[SPL_W] = {0};
+        memcpy(b, splitters + split_offs[q], len);
+        for (uint32_t k = 0; k < SPL_WORDS; ++k) {
+            uint64_t v = 0;
+            for (uint32_t j = 0; j < 8; ++j) v = (v << 8) | b[8 * k + j];
+            bs->w[q * SPL_WORDS + k] = v;
+        }
+        bs->len[q] = len;
+        if (q > 0) {
+            const uint64_t *a = bs->w + (q - 1) * SPL_WORDS, *w = bs->w + q * SPL_WORDS;
+            int r = 0;
+            for (uint32_t k = 0; k < SPL_WORDS && !r; ++k)
+                if (a[k] != w[k]) r = a[k] < w[k] ? -1 : 1;
+            if (r > 0 || (r == 0 && bs->len[q - 1] > len)) {
+                set_error("splitters must be non-decreasing in byte order (splitter %u)", q);
+                return SG_E_INVAL;
+            }
+        }
+    }
+    return SG_OK;
+}
+
+// Hash routing (split == null), range routing by key0 splitters, or by byte splitters
+// (bsplit) — parts - 1 of them.
 // ------------------------------------------------------------------ part multi-split
 // Pass 2 of the piece partition, one tile of PT_TILE records per block (the piece's records in
 // input order): each record's part (k_range_bytes' key), a stable rank by part inside the tile
@@ -369,7 +406,7 @@ struct U32AsU64P {
 };
 
 // pre: exclusive prefix of cnt (flat, part-major); pbase[q]: where part q's bytes of this
-// piece start in the output.
+// piece start in the output (null: a single buffer, parts back to back from offset 0).
 __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                                           const uint64_t *__restrict__ part, uint32_t R, uint32_t ntiles,
                                                           const uint64_t *__restrict__ pre,
@@ -439,8 +476,9 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     // destination of each part's run: its piece base + this tile's prefix inside the part,
     // minus the tile-local byte offset where the part's run starts
     if (tid < 256 && s_dstart[tid] < n_t && (tid == 255 || s_dstart[tid + 1] > s_dstart[tid])) {
-        const uint64_t pt = pre[(size_t)tid * ntiles + tile] - pre[(size_t)tid * ntiles];
-        s_dst[tid] = pbase[tid] + pt - s_off[s_dstart[tid]];
+        // pbase null: one buffer, parts in part order (pre is already the global offset)
+        const uint64_t pt = pre[(size_t)tid * ntiles + tile] - (pbase ? pre[(size_t)tid * ntiles] : 0ull);
+        s_dst[tid] = (pbase ? pbase[tid] : 0ull) + pt - s_off[s_dstart[tid]];
     }
     __syncthreads();
     // copy: sorted position q by lane q (consecutive lanes, consecutive bytes of one part)
@@ -459,43 +497,6 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     }
 }
 
-// Byte splitters packed for k_range_bytes: BE words of the first 64 bytes + lengths.
-struct ByteSplit {
-    uint64_t w[255 * SPL_WORDS];
-    uint32_t len[256];
-};
-
-// Splitter q = splitters[split_offs[q] .. split_offs[q+1]) cut to SPL_W bytes, packed as BE
-// words; the cut splitters must be non-decreasing in byte order.
-static int pack_byte_splitters(const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, ByteSplit *bs) {
-    memset(bs, 0, sizeof(*bs));
-    for (uint32_t q = 0; q + 1 < n_parts; ++q) {
-        if (split_offs[q + 1] < split_offs[q]) { set_error("split_offs must be non-decreasing"); return SG_E_INVAL; }
-        const uint32_t len = std::min<uint32_t>(split_offs[q + 1] - split_offs[q], SPL_W);
-        uint8_t b[SPL_W] = {0};
-        memcpy(b, splitters + split_offs[q], len);
-        for (uint32_t k = 0; k < SPL_WORDS; ++k) {
-            uint64_t v = 0;
-            for (uint32_t j = 0; j < 8; ++j) v = (v << 8) | b[8 * k + j];
-            bs->w[q * SPL_WORDS + k] = v;
-        }
-        bs->len[q] = len;
-        if (q > 0) {
-            const uint64_t *a = bs->w + (q - 1) * SPL_WORDS, *w = bs->w + q * SPL_WORDS;
-            int r = 0;
-            for (uint32_t k = 0; k < SPL_WORDS && !r; ++k)
-                if (a[k] != w[k]) r = a[k] < w[k] ? -1 : 1;
-            if (r > 0 || (r == 0 && bs->len[q - 1] > len)) {
-                set_error("splitters must be non-decreasing in byte order (splitter %u)", q);
-                return SG_E_INVAL;
-            }
-        }
-    }
-    return SG_OK;
-}
-
-// Hash routing (split == null), range routing by key0 splitters, or by byte splitters
-// (bsplit) — parts - 1 of them.
 int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, uint8_t *d_out,
                   size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, const uint64_t *split = nullptr,
                   const ByteSplit *bsplit = nullptr) {
@@ -509,12 +510,8 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
     unsigned long long *cnt;
     SG_TRY(slot(c, S_M_CNT, 2 * 256, &cnt));
     SG_HIP(hipMemsetAsync(cnt, 0, 2 * 256 * 8, c->stream));
-    uint64_t *keys, *keys2;
-    uint32_t *v1, *v2;
+    uint64_t *keys;
     SG_TRY(slot(c, S_KEYS2, R, &keys));
-    SG_TRY(slot(c, S_R_KEY2, R, &keys2));
-    SG_TRY(slot(c, S_VALS, R, &v1));
-    SG_TRY(slot(c, S_VALS2, R, &v2));
     if (R && bsplit) {
         uint64_t *d_w;
         SG_TRY(slot(c, S_M_TMP2, sizeof(ByteSplit) / 8, &d_w));
@@ -531,11 +528,26 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
         SG_LAUNCH_B(c, "range_keys", 24.0 * R, k_range_keys, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, L.keys, L.spans, R,
                   d_split, parts - 1, keys, cnt);
     }
-    uint64_t *K;
-    uint32_t *V;
-    SG_TRY(radix_sort(c, keys, v1, keys2, v2, R, 0, 8, true, &K, &V, "rs_pass_part"));
-    uint64_t bytes = 0;
-    SG_TRY(serialize_into(c, d_buf, L.spans, V, R, d_out, out_cap, &bytes));
+    // the multi-split: per-tile part byte counts, their scan (= each part's offset in the
+    // output), every record copied straight to its place (no sort of ids by part, no gather)
+    if (R) {
+        if (out_cap < n + 1) { set_error("output capacity %zu < %llu", out_cap, (unsigned long long)(n + 1)); return SG_E_CAP; }
+        const uint32_t ntiles = (R + PT_TILE - 1) / PT_TILE;
+        const size_t nflat = (size_t)parts * ntiles;
+        uint32_t *pcnt;
+        uint64_t *ppre;
+        SG_TRY(slot(c, S_PT_CNT, nflat, &pcnt));
+        SG_TRY(slot(c, S_PT_PRE, nflat, &ppre));
+        SG_LAUNCH_B(c, "part_count", 16.0 * R, k_part_count, ntiles, PT_BLOCK, 0, L.spans, keys, R, parts, ntiles, pcnt);
+        const uint32_t nt = (uint32_t)((nflat + SCAN_TILE - 1) / SCAN_TILE);
+        uint64_t *tp;
+        SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
+        SG_LAUNCH(c, "scan.count", k_scan64_count<U32AsU64P>, nt, SCAN_BLOCK, 0, U32AsU64P{pcnt}, (uint32_t)nflat, tp);
+        SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
+        SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64P>, nt, SCAN_BLOCK, 0, U32AsU64P{pcnt}, (uint32_t)nflat, tp + nt, ppre);
+        SG_LAUNCH_B(c, "part_emit", 16.0 * R + 2.0 * (double)n, k_part_apply, ntiles, PT_BLOCK, 0, d_buf, L.spans, keys, R,
+                    ntiles, ppre, (const uint64_t *)nullptr, d_out);
+    }
     uint64_t h[2 * 256];
     SG_TRY(ctx_readback(c, h, cnt, 2 * parts * 8));
     for (uint32_t q = 0; q < parts; ++q) {
