@@ -38,6 +38,23 @@ struct TmRun {
 
 constexpr int TM_MAX_DEV = 64;
 
+// Record-wave evaluation (one wave per record). LDS per block: the packed tables (atom ->
+// occurrence offsets (16-bit), occurrences (matcher | template << 16), template (first
+// matcher | count << 16 | and << 31), matcher (need | and | negative), vacuous bitmap), then
+// per wave the matchers' 8-bit counters four to a word (a count never exceeds the matcher's
+// distinct words, at most 255 here), the touched and true template bitmaps and the list of
+// templates to evaluate (16-bit ids). Twelve waves and at most 80 KB per block: 24 waves per CU.
+constexpr uint32_t TMW_WAVES = 12;          // waves per block
+constexpr uint32_t TMW_WORDS_MAX = 20480;   // 80 KB per block (two blocks per CU)
+constexpr uint32_t TMW_NEED_AND = 1u << 16, TMW_NEED_NEG = 1u << 17;
+constexpr uint32_t tm_wave_words(uint32_t n_match, uint32_t n_tmpl) {
+    return (n_match + 3) / 4 + 2 * ((n_tmpl + 31) / 32) + (n_tmpl + 1) / 2;
+}
+constexpr uint64_t tm_block_words(uint32_t n_atoms, uint32_t n_occ, uint32_t n_match, uint32_t n_tmpl) {
+    return (uint64_t)(n_atoms + 2) / 2 + n_occ + n_tmpl + n_match + (n_tmpl + 31) / 32 +
+           (uint64_t)TMW_WAVES * tm_wave_words(n_match, n_tmpl);
+}
+
 }  // namespace sg
 
 struct sg_templates {
@@ -46,12 +63,16 @@ struct sg_templates {
     std::vector<uint32_t> key_offs;
     std::vector<sg::TmRun> runs;
     std::vector<uint32_t> atom_part, occ_off, occ_m, m_tmpl, m_need, m_flags, t_first, t_count, t_flags, vac;
+    std::vector<uint32_t> vacm;  // record-wave tables: vacuous bitmap, occurrence (m | t << 16),
+    std::vector<uint32_t> occ_mt, tinfo, minfo, occ16;  // template (first, count | and << 31), matcher (need | flags)
+    bool rec_wave = false;       // tables fit the record-wave evaluation (LDS counters, 16-bit counts)
     // Device tables, one set per device, uploaded on first use there and kept until
     // sg_tmpl_free: a call on another device never frees tables an eval may be using.
     struct Dev {
         bool ready = false;
         uint32_t *atom_part = nullptr, *occ_off = nullptr, *occ_m = nullptr, *m_tmpl = nullptr, *m_need = nullptr,
-                 *m_flags = nullptr, *t_first = nullptr, *t_count = nullptr, *t_flags = nullptr, *vac = nullptr;
+                 *m_flags = nullptr, *t_first = nullptr, *t_count = nullptr, *t_flags = nullptr, *vac = nullptr,
+                 *vacm = nullptr, *occ_mt = nullptr, *tinfo = nullptr, *minfo = nullptr, *occ16 = nullptr;
         std::vector<uint32_t *> soff, satoms;  // per run
     } d[sg::TM_MAX_DEV];
     std::mutex mu;
@@ -69,7 +90,8 @@ static int tm_upload(const std::vector<T> &v, T **d) {
 
 static void tm_free_dev(sg_templates::Dev &d) {
     for (void *p : {(void *)d.atom_part, (void *)d.occ_off, (void *)d.occ_m, (void *)d.m_tmpl, (void *)d.m_need,
-                    (void *)d.m_flags, (void *)d.t_first, (void *)d.t_count, (void *)d.t_flags, (void *)d.vac})
+                    (void *)d.m_flags, (void *)d.t_first, (void *)d.t_count, (void *)d.t_flags, (void *)d.vac,
+                    (void *)d.vacm, (void *)d.occ_mt, (void *)d.tinfo, (void *)d.minfo, (void *)d.occ16})
         if (p) (void)hipFree(p);
     for (auto *p : d.soff) if (p) (void)hipFree(p);
     for (auto *p : d.satoms) if (p) (void)hipFree(p);
@@ -87,6 +109,11 @@ static int tm_upload_all(sg_templates *h, sg_templates::Dev &d) {
     SG_TRY(tm_upload(h->t_count, &d.t_count));
     SG_TRY(tm_upload(h->t_flags, &d.t_flags));
     SG_TRY(tm_upload(h->vac, &d.vac));
+    SG_TRY(tm_upload(h->vacm, &d.vacm));
+    SG_TRY(tm_upload(h->occ_mt, &d.occ_mt));
+    SG_TRY(tm_upload(h->tinfo, &d.tinfo));
+    SG_TRY(tm_upload(h->minfo, &d.minfo));
+    SG_TRY(tm_upload(h->occ16, &d.occ16));
     d.soff.assign(h->runs.size(), nullptr);
     d.satoms.assign(h->runs.size(), nullptr);
     for (size_t i = 0; i < h->runs.size(); ++i) {
@@ -251,6 +278,149 @@ __global__ __launch_bounds__(256) void k_tm_split(const uint64_t *__restrict__ K
     tid[i] = (uint32_t)k;
 }
 
+// ------------------------------------------------------------------ record-wave evaluation
+// The default evaluation after the (record, atom) sort: instead of expanding to (record,
+// matcher) pairs, sorting them, evaluating segments, adding the vacuous templates by binary
+// search and sorting the union, one wave takes one record's atom hits, counts them per
+// matcher in LDS, evaluates every touched or vacuous template and writes the record's true
+// templates as a bitmap; a scan of the per-record counts places each record's pairs, which
+// the emit pass writes in (record, template) order — the sorted output without a sort.
+
+// off[r] .. off[r + 1] = record r's entries in K (sorted (record << 32 | atom), sentinels last).
+__global__ __launch_bounds__(256) void k_tm_rec_off(const uint64_t *__restrict__ K, uint32_t n, uint32_t R,
+                                                    uint32_t *__restrict__ off) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    const uint32_t cur = i < n ? (uint32_t)min<uint64_t>(K[i] >> 32, R) : R;
+    const uint32_t lo = i ? (uint32_t)min<uint64_t>(K[i - 1] >> 32, R) + 1 : 0u;
+    for (uint32_t r = lo; r <= cur; ++r) off[r] = i;
+}
+
+__device__ __forceinline__ void tm_wave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
+    const uint64_t *__restrict__ K, const uint32_t *__restrict__ roff, uint32_t R, const uint32_t *__restrict__ occ_off,
+    const uint32_t *__restrict__ occ_mt, const uint32_t *__restrict__ tinfo, const uint32_t *__restrict__ minfo,
+    const uint32_t *__restrict__ vacm, uint32_t n_atoms, uint32_t n_occ, uint32_t n_match, uint32_t n_tmpl,
+    uint32_t *__restrict__ G,
+    uint32_t *__restrict__ rcnt) {
+    extern __shared__ uint32_t s_w[];
+    const uint32_t ntw = (n_tmpl + 31) / 32, cw = (n_match + 3) / 4;
+    uint32_t *s_occw = s_w, *s_mt = s_occw + (n_atoms + 2) / 2, *s_ti = s_mt + n_occ, *s_mi = s_ti + n_tmpl,
+             *s_vac = s_mi + n_match;
+    const uint16_t *s_occ = reinterpret_cast<const uint16_t *>(s_occw);
+    const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t *cnt = s_vac + ntw + wid * tm_wave_words(n_match, n_tmpl), *tch = cnt + cw, *res = tch + ntw;
+    uint16_t *list = reinterpret_cast<uint16_t *>(res + ntw);
+    for (uint32_t x = threadIdx.x; x < (n_atoms + 2) / 2; x += blockDim.x) s_occw[x] = occ_off[x];
+    for (uint32_t x = threadIdx.x; x < n_occ; x += blockDim.x) s_mt[x] = occ_mt[x];
+    for (uint32_t x = threadIdx.x; x < n_tmpl; x += blockDim.x) s_ti[x] = tinfo[x];
+    for (uint32_t x = threadIdx.x; x < n_match; x += blockDim.x) s_mi[x] = minfo[x];
+    for (uint32_t x = threadIdx.x; x < ntw; x += blockDim.x) s_vac[x] = vacm[x];
+    __syncthreads();
+    const uint32_t nw = gridDim.x * TMW_WAVES, r0 = blockIdx.x * TMW_WAVES + wid;
+    // the next record's range and first 64 hits are loaded while this record is evaluated
+    uint32_t a = r0 < R ? roff[r0] : 0u, e = r0 < R ? roff[r0 + 1] : 0u;
+    unsigned long long kf = (a + lane < e) ? K[a + lane] : ~0ull;
+    for (uint32_t r = r0; r < R; r += nw) {
+        const uint32_t rn = r + nw;
+        uint32_t an = 0, en = 0;
+        if (rn < R) { an = roff[rn]; en = roff[rn + 1]; }
+        for (uint32_t x = lane; x < cw; x += 64) cnt[x] = 0;
+        for (uint32_t x = lane; x < ntw; x += 64) { tch[x] = 0; res[x] = 0; }
+        tm_wave_sync();
+        unsigned long long carry = ~0ull;  // no (record, atom) equals it
+        for (uint32_t base = a; base < e; base += 64) {
+            const uint32_t i = base + lane;
+            const unsigned long long k = base == a ? kf : (i < e ? (unsigned long long)K[i] : ~0ull);
+            unsigned long long kp = __shfl_up(k, 1, 64);
+            if (lane == 0) kp = carry;
+            carry = __shfl(k, 63, 64);
+            if (i >= e || k == kp) continue;  // a repeated (record, atom) counts once
+            const uint32_t at = (uint32_t)k;
+            for (uint32_t q = s_occ[at], qe = s_occ[at + 1]; q < qe; ++q) {
+                const uint32_t mt = s_mt[q], m = mt & 0xffffu, t = mt >> 16;
+                atomicAdd(&cnt[m >> 2], 1u << (8 * (m & 3)));
+                atomicOr(&tch[t >> 5], 1u << (t & 31));
+            }
+        }
+        kf = (an + lane < en) ? (unsigned long long)K[an + lane] : ~0ull;
+        tm_wave_sync();
+        // the templates to evaluate: touched, or vacuous (true with every count 0)
+        uint32_t nl = 0;
+        for (uint32_t w0 = 0; w0 < ntw; w0 += 64) {
+            const uint32_t w = w0 + lane;
+            uint32_t bits = w < ntw ? (tch[w] | s_vac[w]) : 0u;
+            const uint32_t c = (uint32_t)__popc(bits), inc = wave_incl_scan(c);
+            uint32_t p = nl + inc - c;
+            while (bits) {
+                list[p++] = (uint16_t)(32 * w + (uint32_t)__builtin_ctz(bits));
+                bits &= bits - 1;
+            }
+            nl += __shfl(inc, 63, 64);
+        }
+        tm_wave_sync();
+        for (uint32_t j = lane; j < nl; j += 64) {
+            const uint32_t t = list[j], ti = s_ti[t], m0 = ti & 0xffffu;
+            const bool and_t = ti >> 31;
+            bool acc = and_t;
+            for (uint32_t m = m0, me = m0 + ((ti >> 16) & 0x7fffu); m < me; ++m) {
+                const uint32_t c = (cnt[m >> 2] >> (8 * (m & 3))) & 0xffu, mi = s_mi[m];
+                bool hit = (mi & TMW_NEED_AND) ? c >= (mi & 0xffffu) : c > 0;
+                if (mi & TMW_NEED_NEG) hit = !hit;
+                acc = and_t ? (acc && hit) : (acc || hit);
+                if (acc != and_t) break;  // and: a false matcher decides; or: a true one
+            }
+            if (acc) atomicOr(&res[t >> 5], 1u << (t & 31));
+        }
+        tm_wave_sync();
+        uint32_t tot = 0;
+        for (uint32_t w = lane; w < ntw; w += 64) {
+            const uint32_t tr = res[w];
+            G[(size_t)r * ntw + w] = tr;
+            tot += (uint32_t)__popc(tr);
+        }
+        tot = wave_sum(tot);
+        if (lane == 0) rcnt[r] = tot;
+        tm_wave_sync();
+        a = an;
+        e = en;
+    }
+}
+
+struct TmRecCnt {
+    const uint32_t *rcnt;
+    __device__ uint64_t operator()(uint32_t i) const { return rcnt[i]; }
+};
+
+__global__ __launch_bounds__(256) void k_tm_rec_emit(const uint32_t *__restrict__ G, const uint64_t *__restrict__ off,
+                                                     uint32_t R, uint32_t ntw, uint32_t *__restrict__ rec,
+                                                     uint32_t *__restrict__ tid) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < R; r += nw) {
+        uint64_t base = off[r];
+        for (uint32_t w0 = 0; w0 < ntw; w0 += 64) {
+            const uint32_t w = w0 + lane;
+            uint32_t bits = w < ntw ? G[(size_t)r * ntw + w] : 0u;
+            const uint32_t c = (uint32_t)__popc(bits);
+            const uint32_t inc = wave_incl_scan(c);
+            uint64_t p = base + inc - c;
+            while (bits) {
+                const uint32_t b = (uint32_t)__builtin_ctz(bits);
+                bits &= bits - 1;
+                rec[p] = r;
+                tid[p] = 32 * w + b;
+                ++p;
+            }
+            base += __shfl(inc, 63, 64);
+        }
+    }
+}
+
 struct TmAccum {
     int slot_id = S_T_HITS;
     uint64_t *p = nullptr;
@@ -267,6 +437,41 @@ static int tm_grow(sg_ctx *c, TmAccum *a, uint64_t need) {
     a->slot_id = other;
     a->p = np;
     a->cap = cap;
+    return SG_OK;
+}
+
+// The record-wave evaluation of the sorted (record, atom) hits K[0, n1) (see k_tm_rec_eval).
+static int tm_rec_wave(sg_ctx *c, const sg_templates *h, const sg_templates::Dev &D, const uint64_t *K, uint32_t n1,
+                       uint64_t R, sg_dev_tmatches *res) {
+    const uint32_t ntw = (h->n_tmpl + 31) / 32;
+    if (R * ntw >= (1ull << 40)) { set_error("template eval: records x templates too large"); return SG_E_TOO_LARGE; }
+    uint32_t *roff, *G, *rcnt;
+    uint64_t *off;
+    SG_TRY(slot(c, S_T_SEG, R + 16, &roff));
+    SG_TRY(slot(c, S_T_E, R * ntw + 16, &G));
+    SG_TRY(slot(c, S_T_FLAG, R + 16, &rcnt));
+    SG_TRY(slot(c, S_T_O, R + 16, &off));
+    const uint32_t Ru = (uint32_t)R;
+    SG_LAUNCH(c, "tm_rec_off", k_tm_rec_off, (n1 + 1 + 255) / 256, 256, 0, K, n1, Ru, roff);
+    const uint32_t n_occ = (uint32_t)h->occ_m.size();
+    const size_t lds = (size_t)tm_block_words(h->n_atoms, n_occ, h->n_match, h->n_tmpl) * 4;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((R + TMW_WAVES - 1) / TMW_WAVES, 8192);
+    if (lds > 65536)
+        SG_HIP(hipFuncSetAttribute((const void *)k_tm_rec_eval, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    SG_LAUNCH(c, "tm_rec_eval", k_tm_rec_eval, blocks, 64 * TMW_WAVES, lds, K, roff, Ru, D.occ16, D.occ_mt, D.tinfo,
+              D.minfo, D.vacm, h->n_atoms, n_occ, h->n_match, h->n_tmpl, G, rcnt);
+    uint64_t nout = 0;
+    SG_TRY(run_scan64(c, "tm_rec_scan", TmRecCnt{rcnt}, Ru, off, &nout));
+    res->n = nout;
+    if (nout == 0) return SG_OK;
+    uint32_t *rec, *tid;
+    SG_TRY(slot(c, S_T_REC, nout + 1, &rec));
+    SG_TRY(slot(c, S_T_TID, nout + 1, &tid));
+    const uint32_t eblocks = (uint32_t)std::min<uint64_t>((R + 3) / 4, 16384);
+    SG_LAUNCH_B(c, "tm_rec_emit", 8.0 * nout + 4.0 * R * ntw, k_tm_rec_emit, eblocks, 256, 0, G, off, Ru, ntw, rec,
+                tid);
+    res->rec_idx = rec;
+    res->tmpl_id = tid;
     return SG_OK;
 }
 
@@ -339,6 +544,8 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
         SG_TRY(slot(c, S_T_V1, (size_t)n1 + 1, &v1));
         SG_TRY(slot(c, S_T_V2, (size_t)n1 + 1, &v2));
         SG_TRY(radix_sort(c, acc.p, v1, k2, v2, n1, 0, kbits, true, &K, &V, "tm_rs_atoms"));
+        const char *e_ts = getenv("SG_TM_SORT");  // 1: the sort-based evaluation below
+        if (h->rec_wave && !(e_ts && atoi(e_ts))) return tm_rec_wave(c, h, D, K, n1, R, res);
         SG_TRY(slot(c, S_T_SEL, (size_t)n1 + 16, &sel));
         SG_TRY(run_select2(c, "tm_unique", TmUniqPred{K}, n1, sel, (uint32_t *)nullptr, &nu, nullptr, 16.0));
         if (nu) {
@@ -526,6 +733,22 @@ int sg_tmpl_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pa
             acc = and_t ? (acc && hit) : (acc || hit);
         }
         if (acc) h->vac.push_back(t);
+    }
+    h->vacm.assign((n_templates + 31) / 32, 0);
+    for (uint32_t t : h->vac) h->vacm[t >> 5] |= 1u << (t & 31);
+    uint32_t max_need = 0;
+    for (uint32_t v : h->m_need) max_need = std::max(max_need, v);
+    h->rec_wave = max_need <= 0xffu && n_matchers <= 0x7fffu && n_templates <= 0xffffu && h->occ_m.size() <= 0xffffu &&
+                  tm_block_words(h->n_atoms, (uint32_t)h->occ_m.size(), n_matchers, n_templates) <= TMW_WORDS_MAX;
+    if (h->rec_wave) {
+        for (uint32_t m : h->occ_m) h->occ_mt.push_back(m | (h->m_tmpl[m] << 16));
+        for (uint32_t t = 0; t < n_templates; ++t)
+            h->tinfo.push_back(h->t_first[t] | (h->t_count[t] << 16) | ((h->t_flags[t] & SG_TM_AND) ? 1u << 31 : 0u));
+        for (uint32_t a = 0; a <= h->n_atoms; a += 2)
+            h->occ16.push_back(h->occ_off[a] | (a + 1 <= h->n_atoms ? h->occ_off[a + 1] << 16 : 0u));
+        for (uint32_t m = 0; m < n_matchers; ++m)
+            h->minfo.push_back(h->m_need[m] | ((h->m_flags[m] & SG_TM_AND) ? TMW_NEED_AND : 0u) |
+                               ((h->m_flags[m] & SG_TM_NEGATIVE) ? TMW_NEED_NEG : 0u));
     }
     *out = h.release();
     return SG_OK;

@@ -129,3 +129,56 @@ def test_edges(sg, data):
     T = [{"condition": "or", "matchers": [W(b"nginx", negative=True)]},
          {"condition": "and", "matchers": [W(b"line"), W(b"one")]}]
     assert sg.Templates(T).match(data) == S.template_matches(data, T)
+
+
+@pytest.mark.parametrize("case", ["records", "fields", "corpus"])
+def test_record_wave_matches_sort_path(sg, monkeypatch, case):
+    """The record-wave evaluation (default: per-record LDS matcher counts, no expansion sort)
+    and the sort-based evaluation (SG_TM_SORT=1) give the same pairs, both equal to the
+    oracle's."""
+    rng = random.Random(11)
+    keys = None
+    if case == "records":
+        T = random_templates(rng, 400, ["body"])
+        data = b"\n".join(random_lines(rng, 4000)) + b"\n"
+    elif case == "fields":
+        keys = [b"title", b"webserver", b"tech"]
+        T = random_templates(rng, 300, ["body", "title", "webserver", "tech"])
+        data = b"\n".join(corpus.httpx_json_pool(3000, seed=17)) + b"\n"
+    else:
+        T = corpus_templates()
+        data = b"\n".join(planted_lines(rng, T, 3000)) + b"\n"
+    want = S.template_matches(data, T, keys) if keys else S.template_matches(data, T)
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SG_TM_SORT", mode)
+        tm = sg.Templates(T, keys) if keys else sg.Templates(T)
+        outs.append(tm.match(data))
+    assert outs[0] == want
+    assert outs[1] == want
+
+
+def test_record_wave_many_hits_per_record(sg):
+    """Records holding every word of every matcher (long per-record hit lists, every template
+    touched, `and` matchers at their full count) next to empty and hit-free records."""
+    words = [b"w%03d" % i for i in range(120)]
+    T = []
+    for i in range(0, 120, 4):
+        T.append({"condition": "and", "matchers": [W(*words[i:i + 4], condition="and"), W(words[(i + 7) % 120])]})
+        T.append({"condition": "or", "matchers": [W(*words[i:i + 2], condition="and", negative=True)]})
+    full = b" ".join(words)
+    lines = [full, b"", b"nothing here", full[: len(full) // 2], b" ".join(reversed(words))] * 40
+    data = b"\n".join(lines) + b"\n"
+    assert sg.Templates(T).match(data) == S.template_matches(data, T)
+
+
+def test_wide_matcher_uses_sort_path(sg):
+    """A matcher with more than 255 distinct words does not fit the record-wave 8-bit counts:
+    the handle evaluates with the sort-based path, same results."""
+    words = [b"k%04d" % i for i in range(300)]
+    T = [{"condition": "or", "matchers": [W(*words, condition="and")]},
+         {"condition": "or", "matchers": [W(*words[:10])]},
+         {"condition": "and", "matchers": [W(*words[:20], condition="and"), W(b"zz", negative=True)]}]
+    lines = [b" ".join(words), b" ".join(words[:299]), b" ".join(words[:20]), b"zz " + b" ".join(words[:20]), b""] * 20
+    data = b"\n".join(lines) + b"\n"
+    assert sg.Templates(T).match(data) == S.template_matches(data, T)
