@@ -42,17 +42,17 @@ constexpr int TM_MAX_DEV = 64;
 // occurrence offsets (16-bit), occurrences (matcher | template << 16), template (first
 // matcher | count << 16 | and << 31), matcher (need | and | negative), vacuous bitmap), then
 // per wave the matchers' 8-bit counters four to a word (a count never exceeds the matcher's
-// distinct words, at most 255 here), the touched and true template bitmaps and the list of
-// templates to evaluate (16-bit ids). Twelve waves and at most 80 KB per block: 24 waves per CU.
+// distinct words, at most 255 here), the touched and true template bitmaps, the atoms seen and
+// the list of templates to evaluate (16-bit ids). Twelve waves and at most 80 KB per block: 24 waves per CU.
 constexpr uint32_t TMW_WAVES = 12;          // waves per block
 constexpr uint32_t TMW_WORDS_MAX = 20480;   // 80 KB per block (two blocks per CU)
 constexpr uint32_t TMW_NEED_AND = 1u << 16, TMW_NEED_NEG = 1u << 17;
-constexpr uint32_t tm_wave_words(uint32_t n_match, uint32_t n_tmpl) {
-    return (n_match + 3) / 4 + 2 * ((n_tmpl + 31) / 32) + (n_tmpl + 1) / 2;
+constexpr uint32_t tm_wave_words(uint32_t n_match, uint32_t n_tmpl, uint32_t n_atoms) {
+    return (n_match + 3) / 4 + 2 * ((n_tmpl + 31) / 32) + (n_atoms + 31) / 32 + (n_tmpl + 1) / 2;
 }
 constexpr uint64_t tm_block_words(uint32_t n_atoms, uint32_t n_occ, uint32_t n_match, uint32_t n_tmpl) {
     return (uint64_t)(n_atoms + 2) / 2 + n_occ + n_tmpl + n_match + (n_tmpl + 31) / 32 +
-           (uint64_t)TMW_WAVES * tm_wave_words(n_match, n_tmpl);
+           (uint64_t)TMW_WAVES * tm_wave_words(n_match, n_tmpl, n_atoms);
 }
 
 }  // namespace sg
@@ -140,10 +140,12 @@ static int tm_ensure_device(sg_templates *h, int dev, const sg_templates::Dev **
 }
 
 // ------------------------------------------------------------------ device
-constexpr uint64_t TM_NONE = ~0ull;
+constexpr uint32_t TM_NO_ATOM = ~0u;
 
 // hits (record or row, signature) -> (record << 32 | atom); a field-row hit keeps the atom
-// whose part is the row's field (none: sentinel, dropped by the unique pass).
+// whose part is the row's field (none: atom TM_NO_ATOM, skipped by both evaluations). Each
+// engine's hits arrive sorted by record (rows map to records monotonically), so every
+// collect launch leaves one record-ordered segment.
 __global__ __launch_bounds__(256) void k_tm_collect(const uint32_t *__restrict__ rec_idx, const uint32_t *__restrict__ sig,
                                                     uint32_t nh, const uint32_t *__restrict__ soff,
                                                     const uint32_t *__restrict__ satoms,
@@ -153,11 +155,12 @@ __global__ __launch_bounds__(256) void k_tm_collect(const uint32_t *__restrict__
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nh) return;
     const uint32_t r = rec_idx[i], s = sig[i];
-    uint64_t key = TM_NONE;
+    uint64_t key;
     if (!row_rec) {
         key = ((uint64_t)r << 32) | satoms[soff[s]];
     } else {
         const uint32_t want = row_key[r] + 1;
+        key = ((uint64_t)row_rec[r] << 32) | TM_NO_ATOM;
         for (uint32_t q = soff[s]; q < soff[s + 1]; ++q)
             if (apart[satoms[q]] == want) { key = ((uint64_t)row_rec[r] << 32) | satoms[q]; break; }
     }
@@ -168,7 +171,7 @@ struct TmUniqPred {
     const uint64_t *K;
     __device__ uint32_t operator()(uint32_t i) const {
         const uint64_t k = K[i];
-        return (k != TM_NONE && (i == 0 || k != K[i - 1])) ? 1u : 0u;
+        return ((uint32_t)k != TM_NO_ATOM && (i == 0 || k != K[i - 1])) ? 1u : 0u;
     }
 };
 
@@ -279,21 +282,23 @@ __global__ __launch_bounds__(256) void k_tm_split(const uint64_t *__restrict__ K
 }
 
 // ------------------------------------------------------------------ record-wave evaluation
-// The default evaluation after the (record, atom) sort: instead of expanding to (record,
-// matcher) pairs, sorting them, evaluating segments, adding the vacuous templates by binary
-// search and sorting the union, one wave takes one record's atom hits, counts them per
-// matcher in LDS, evaluates every touched or vacuous template and writes the record's true
-// templates as a bitmap; a scan of the per-record counts places each record's pairs, which
-// the emit pass writes in (record, template) order — the sorted output without a sort.
+// The default evaluation: no sort at all. Instead of sorting the (record, atom) hits,
+// expanding them to (record, matcher) pairs, sorting those, evaluating segments, adding the
+// vacuous templates by binary search and sorting the union, one wave takes one record's
+// hits from every engine's record-ordered segment, drops repeated atoms with an LDS bitmap,
+// counts them per matcher in LDS, evaluates every touched or vacuous template and writes the
+// record's true templates as a bitmap; a scan of the per-record counts places each record's
+// pairs, which the emit pass writes in (record, template) order — the sorted output.
 
-// off[r] .. off[r + 1] = record r's entries in K (sorted (record << 32 | atom), sentinels last).
+// off[r] .. off[r + 1] = record r's entries of the segment K[0, n) (record-ordered), as
+// absolute indices (+ start).
 __global__ __launch_bounds__(256) void k_tm_rec_off(const uint64_t *__restrict__ K, uint32_t n, uint32_t R,
-                                                    uint32_t *__restrict__ off) {
+                                                    uint32_t start, uint32_t *__restrict__ off) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
     const uint32_t cur = i < n ? (uint32_t)min<uint64_t>(K[i] >> 32, R) : R;
     const uint32_t lo = i ? (uint32_t)min<uint64_t>(K[i - 1] >> 32, R) + 1 : 0u;
-    for (uint32_t r = lo; r <= cur; ++r) off[r] = i;
+    for (uint32_t r = lo; r <= cur; ++r) off[r] = start + i;
 }
 
 __device__ __forceinline__ void tm_wave_sync() {
@@ -302,7 +307,8 @@ __device__ __forceinline__ void tm_wave_sync() {
 }
 
 __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
-    const uint64_t *__restrict__ K, const uint32_t *__restrict__ roff, uint32_t R, const uint32_t *__restrict__ occ_off,
+    const uint64_t *__restrict__ K, const uint32_t *__restrict__ roff, uint32_t nseg, uint32_t R,
+    const uint32_t *__restrict__ occ_off,
     const uint32_t *__restrict__ occ_mt, const uint32_t *__restrict__ tinfo, const uint32_t *__restrict__ minfo,
     const uint32_t *__restrict__ vacm, uint32_t n_atoms, uint32_t n_occ, uint32_t n_match, uint32_t n_tmpl,
     uint32_t *__restrict__ G,
@@ -313,41 +319,35 @@ __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
              *s_vac = s_mi + n_match;
     const uint16_t *s_occ = reinterpret_cast<const uint16_t *>(s_occw);
     const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t *cnt = s_vac + ntw + wid * tm_wave_words(n_match, n_tmpl), *tch = cnt + cw, *res = tch + ntw;
-    uint16_t *list = reinterpret_cast<uint16_t *>(res + ntw);
+    uint32_t *cnt = s_vac + ntw + wid * tm_wave_words(n_match, n_tmpl, n_atoms), *tch = cnt + cw, *res = tch + ntw;
+    const uint32_t naw = (n_atoms + 31) / 32;
+    uint32_t *seen = res + ntw;
+    uint16_t *list = reinterpret_cast<uint16_t *>(seen + naw);
     for (uint32_t x = threadIdx.x; x < (n_atoms + 2) / 2; x += blockDim.x) s_occw[x] = occ_off[x];
     for (uint32_t x = threadIdx.x; x < n_occ; x += blockDim.x) s_mt[x] = occ_mt[x];
     for (uint32_t x = threadIdx.x; x < n_tmpl; x += blockDim.x) s_ti[x] = tinfo[x];
     for (uint32_t x = threadIdx.x; x < n_match; x += blockDim.x) s_mi[x] = minfo[x];
     for (uint32_t x = threadIdx.x; x < ntw; x += blockDim.x) s_vac[x] = vacm[x];
     __syncthreads();
-    const uint32_t nw = gridDim.x * TMW_WAVES, r0 = blockIdx.x * TMW_WAVES + wid;
-    // the next record's range and first 64 hits are loaded while this record is evaluated
-    uint32_t a = r0 < R ? roff[r0] : 0u, e = r0 < R ? roff[r0 + 1] : 0u;
-    unsigned long long kf = (a + lane < e) ? K[a + lane] : ~0ull;
-    for (uint32_t r = r0; r < R; r += nw) {
-        const uint32_t rn = r + nw;
-        uint32_t an = 0, en = 0;
-        if (rn < R) { an = roff[rn]; en = roff[rn + 1]; }
+    const uint32_t nw = gridDim.x * TMW_WAVES;
+    for (uint32_t r = blockIdx.x * TMW_WAVES + wid; r < R; r += nw) {
         for (uint32_t x = lane; x < cw; x += 64) cnt[x] = 0;
         for (uint32_t x = lane; x < ntw; x += 64) { tch[x] = 0; res[x] = 0; }
+        for (uint32_t x = lane; x < naw; x += 64) seen[x] = 0;
         tm_wave_sync();
-        unsigned long long carry = ~0ull;  // no (record, atom) equals it
-        for (uint32_t base = a; base < e; base += 64) {
-            const uint32_t i = base + lane;
-            const unsigned long long k = base == a ? kf : (i < e ? (unsigned long long)K[i] : ~0ull);
-            unsigned long long kp = __shfl_up(k, 1, 64);
-            if (lane == 0) kp = carry;
-            carry = __shfl(k, 63, 64);
-            if (i >= e || k == kp) continue;  // a repeated (record, atom) counts once
-            const uint32_t at = (uint32_t)k;
-            for (uint32_t q = s_occ[at], qe = s_occ[at + 1]; q < qe; ++q) {
-                const uint32_t mt = s_mt[q], m = mt & 0xffffu, t = mt >> 16;
-                atomicAdd(&cnt[m >> 2], 1u << (8 * (m & 3)));
-                atomicOr(&tch[t >> 5], 1u << (t & 31));
+        for (uint32_t sg = 0; sg < nseg; ++sg) {
+            const uint32_t *ro = roff + (size_t)sg * (R + 1);
+            const uint32_t a = ro[r], e = ro[r + 1];
+            for (uint32_t i = a + lane; i < e; i += 64) {
+                const uint32_t at = (uint32_t)K[i], bit = 1u << (at & 31);
+                if (at == TM_NO_ATOM || (atomicOr(&seen[at >> 5], bit) & bit)) continue;  // counted once
+                for (uint32_t q = s_occ[at], qe = s_occ[at + 1]; q < qe; ++q) {
+                    const uint32_t mt = s_mt[q], m = mt & 0xffffu, t = mt >> 16;
+                    atomicAdd(&cnt[m >> 2], 1u << (8 * (m & 3)));
+                    atomicOr(&tch[t >> 5], 1u << (t & 31));
+                }
             }
         }
-        kf = (an + lane < en) ? (unsigned long long)K[an + lane] : ~0ull;
         tm_wave_sync();
         // the templates to evaluate: touched, or vacuous (true with every count 0)
         uint32_t nl = 0;
@@ -386,8 +386,6 @@ __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
         tot = wave_sum(tot);
         if (lane == 0) rcnt[r] = tot;
         tm_wave_sync();
-        a = an;
-        e = en;
     }
 }
 
@@ -440,25 +438,29 @@ static int tm_grow(sg_ctx *c, TmAccum *a, uint64_t need) {
     return SG_OK;
 }
 
-// The record-wave evaluation of the sorted (record, atom) hits K[0, n1) (see k_tm_rec_eval).
-static int tm_rec_wave(sg_ctx *c, const sg_templates *h, const sg_templates::Dev &D, const uint64_t *K, uint32_t n1,
-                       uint64_t R, sg_dev_tmatches *res) {
+// The record-wave evaluation of the collected hits K: segs = each collect launch's (start,
+// count), record-ordered within (see k_tm_rec_eval).
+static int tm_rec_wave(sg_ctx *c, const sg_templates *h, const sg_templates::Dev &D, const uint64_t *K,
+                       const std::vector<std::pair<uint32_t, uint32_t>> &segs, uint64_t R, sg_dev_tmatches *res) {
     const uint32_t ntw = (h->n_tmpl + 31) / 32;
     if (R * ntw >= (1ull << 40)) { set_error("template eval: records x templates too large"); return SG_E_TOO_LARGE; }
     uint32_t *roff, *G, *rcnt;
     uint64_t *off;
-    SG_TRY(slot(c, S_T_SEG, R + 16, &roff));
+    const uint32_t nseg = (uint32_t)segs.size();
+    SG_TRY(slot(c, S_T_SEG, (R + 1) * nseg + 16, &roff));
     SG_TRY(slot(c, S_T_E, R * ntw + 16, &G));
     SG_TRY(slot(c, S_T_FLAG, R + 16, &rcnt));
     SG_TRY(slot(c, S_T_O, R + 16, &off));
     const uint32_t Ru = (uint32_t)R;
-    SG_LAUNCH(c, "tm_rec_off", k_tm_rec_off, (n1 + 1 + 255) / 256, 256, 0, K, n1, Ru, roff);
+    for (uint32_t g = 0; g < nseg; ++g)
+        SG_LAUNCH(c, "tm_rec_off", k_tm_rec_off, (segs[g].second + 1 + 255) / 256, 256, 0, K + segs[g].first,
+                  segs[g].second, Ru, segs[g].first, roff + (size_t)g * (R + 1));
     const uint32_t n_occ = (uint32_t)h->occ_m.size();
     const size_t lds = (size_t)tm_block_words(h->n_atoms, n_occ, h->n_match, h->n_tmpl) * 4;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((R + TMW_WAVES - 1) / TMW_WAVES, 8192);
     if (lds > 65536)
         SG_HIP(hipFuncSetAttribute((const void *)k_tm_rec_eval, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    SG_LAUNCH(c, "tm_rec_eval", k_tm_rec_eval, blocks, 64 * TMW_WAVES, lds, K, roff, Ru, D.occ16, D.occ_mt, D.tinfo,
+    SG_LAUNCH(c, "tm_rec_eval", k_tm_rec_eval, blocks, 64 * TMW_WAVES, lds, K, roff, nseg, Ru, D.occ16, D.occ_mt, D.tinfo,
               D.minfo, D.vacm, h->n_atoms, n_occ, h->n_match, h->n_tmpl, G, rcnt);
     uint64_t nout = 0;
     SG_TRY(run_scan64(c, "tm_rec_scan", TmRecCnt{rcnt}, Ru, off, &nout));
@@ -481,6 +483,7 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
     SG_TRY(tm_ensure_device(h, c->device, &pd));
     const auto &D = *pd;
     TmAccum acc;
+    std::vector<std::pair<uint32_t, uint32_t>> segs;  // each collect launch's hits in acc
     uint64_t R = 0;
     bool have_R = false;
     // stream 0: the records themselves
@@ -496,6 +499,7 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
         SG_LAUNCH(c, "tm_collect", k_tm_collect, (uint32_t)((r.n_hits + 255) / 256), 256, 0, r.rec_idx, r.sig_id,
                   (uint32_t)r.n_hits, D.soff[ri], D.satoms[ri], D.atom_part, (const uint32_t *)nullptr,
                   (const uint32_t *)nullptr, acc.p + acc.n);
+        segs.emplace_back((uint32_t)acc.n, (uint32_t)r.n_hits);
         acc.n += r.n_hits;
     }
     // stream 1: httpx -json field rows
@@ -517,6 +521,7 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
             SG_LAUNCH(c, "tm_collect", k_tm_collect, (uint32_t)((r.n_hits + 255) / 256), 256, 0, r.rec_idx, r.sig_id,
                       (uint32_t)r.n_hits, D.soff[ri], D.satoms[ri], D.atom_part, rows.row_rec, rows.row_key,
                       acc.p + acc.n);
+            segs.emplace_back((uint32_t)acc.n, (uint32_t)r.n_hits);
             acc.n += r.n_hits;
         }
     }
@@ -536,6 +541,8 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
     uint64_t n2 = 0;
     uint32_t *seg = nullptr, *flag = nullptr, *sel = nullptr;
     uint64_t *segkey = nullptr;
+    const char *e_ts = getenv("SG_TM_SORT");  // 1: the sort-based evaluation below
+    if (acc.n && h->rec_wave && !(e_ts && atoi(e_ts))) return tm_rec_wave(c, h, D, acc.p, segs, R, res);
     if (acc.n) {
         const uint32_t n1 = (uint32_t)acc.n;
         uint64_t *k2, *K;
@@ -544,8 +551,6 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
         SG_TRY(slot(c, S_T_V1, (size_t)n1 + 1, &v1));
         SG_TRY(slot(c, S_T_V2, (size_t)n1 + 1, &v2));
         SG_TRY(radix_sort(c, acc.p, v1, k2, v2, n1, 0, kbits, true, &K, &V, "tm_rs_atoms"));
-        const char *e_ts = getenv("SG_TM_SORT");  // 1: the sort-based evaluation below
-        if (h->rec_wave && !(e_ts && atoi(e_ts))) return tm_rec_wave(c, h, D, K, n1, R, res);
         SG_TRY(slot(c, S_T_SEL, (size_t)n1 + 16, &sel));
         SG_TRY(run_select2(c, "tm_unique", TmUniqPred{K}, n1, sel, (uint32_t *)nullptr, &nu, nullptr, 16.0));
         if (nu) {

@@ -182,3 +182,20 @@ def test_wide_matcher_uses_sort_path(sg):
     lines = [b" ".join(words), b" ".join(words[:299]), b" ".join(words[:20]), b"zz " + b" ".join(words[:20]), b""] * 20
     data = b"\n".join(lines) + b"\n"
     assert sg.Templates(T).match(data) == S.template_matches(data, T)
+
+
+def test_field_rows_repeat_atoms(sg):
+    """One record's field rows hit the same word several times (array rows, repeated keys'
+    rows) across engines: each (record, atom) counts once for `and` matchers."""
+    keys = [b"title", b"tech"]
+    lines = [b'{"title":"nginx nginx","tech":["nginx","nginx:1.2","PHP","nginx"]}',
+             b'{"title":"x","tech":["PHP","PHP"]}',
+             b'{"tech":["a","b"],"title":"PHP nginx"}',
+             b'{"title":"none"}', b"not json nginx PHP"]
+    T = [{"condition": "or", "matchers": [W(b"nginx", b"PHP", part="tech", condition="and")]},
+         {"condition": "or", "matchers": [W(b"nginx", part="title"), W(b"PHP", part="tech")]},
+         {"condition": "and", "matchers": [W(b"nginx", part="title"), W(b"nginx"), W(b"PHP", part="tech")]},
+         {"condition": "or", "matchers": [R(rb"ngin.", part="tech"), W(b"zzz", part="title", negative=True)]},
+         {"condition": "or", "matchers": [W(b"nginx", b"PHP", b"Apache", condition="and")]}]
+    data = b"\n".join(lines * 30) + b"\n"
+    assert sg.Templates(T, keys).match(data) == S.template_matches(data, T, keys)
