@@ -697,18 +697,40 @@ int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, con
     unsigned long long *cnt;
     SG_TRY(slot(c, S_PART, (size_t)std::max<size_t>(k, 1) * 512, &cnt));
     SG_HIP(hipMemsetAsync(cnt, 0, std::max<size_t>(k, 1) * 512 * 8, c->stream));
+    // Pass 1's spans and parts are kept for pass 2 (no second parse or routing) while they
+    // fit the two keep slots, sized by the last call's record count (the first call of a
+    // size, or a larger one, parses the pieces that did not fit again).
+    uint2 *keep_sp = nullptr;
+    uint64_t *keep_k = nullptr, keep_cap = 0, kept = 0, all_rec = 0;
+    if (c->pt_keep_recs) {
+        SG_TRY(slot(c, S_PT_SP, c->pt_keep_recs, &keep_sp));
+        SG_TRY(slot(c, S_PT_KEYS, c->pt_keep_recs, &keep_k));
+        keep_cap = std::min(slot_elems<uint2>(c, S_PT_SP), slot_elems<uint64_t>(c, S_PT_KEYS));
+    }
+    std::vector<uint64_t> keep_off(k, ~0ull), keep_n(k, 0);
     for (size_t j = 0; j < k; ++j) {
         if (!lens[j]) continue;
         const uint8_t *b;
         SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &b));
         Lines L;
         SG_TRY(run_lines(c, b, lens[j], CUR_SLOTS, &L, false, true));
+        all_rec += L.n_rec;
         if (!L.n_rec) continue;
         uint64_t *keys;
-        SG_TRY(slot(c, S_KEYS2, L.n_rec, &keys));
+        if (kept + L.n_rec <= keep_cap) {
+            SG_HIP(hipMemcpyAsync(keep_sp + kept, L.spans, (size_t)L.n_rec * sizeof(uint2), hipMemcpyDeviceToDevice,
+                                  c->stream));
+            keys = keep_k + kept;
+            keep_off[j] = kept;
+            keep_n[j] = L.n_rec;
+            kept += L.n_rec;
+        } else {
+            SG_TRY(slot(c, S_KEYS2, L.n_rec, &keys));
+        }
         SG_LAUNCH_B(c, "range_bytes", 24.0 * L.n_rec, k_range_bytes, std::min<uint32_t>((L.n_rec + 255) / 256, 2048u), 256, 0,
                     b, L.spans, L.n_rec, d_w, d_len, ns, keys, cnt + 512 * j);
     }
+    c->pt_keep_recs = std::max<uint64_t>(c->pt_keep_recs, all_rec);
     std::vector<uint64_t> h(std::max<size_t>(k, 1) * 512, 0);
     SG_TRY(ctx_readback(c, h.data(), cnt, h.size() * 8));
     // destinations: part p = pieces' part-p records in piece order
@@ -744,24 +766,33 @@ int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, con
         if (!lens[j]) continue;
         const uint8_t *b;
         SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &b));
-        Lines L;
-        SG_TRY(run_lines(c, b, lens[j], CUR_SLOTS, &L, false, true));
-        const uint32_t R = L.n_rec;
-        if (!R) continue;
-        unsigned long long *scr;
-        SG_TRY(slot(c, S_M_CNT, 2 * 256, &scr));
-        SG_HIP(hipMemsetAsync(scr, 0, 2 * 256 * 8, c->stream));
+        const uint2 *spans;
         uint64_t *keys;
-        SG_TRY(slot(c, S_KEYS2, R, &keys));
-        SG_LAUNCH_B(c, "range_bytes", 24.0 * R, k_range_bytes, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, b, L.spans, R,
-                    d_w, d_len, ns, keys, scr);
+        uint32_t R;
+        if (keep_off[j] != ~0ull) {
+            spans = keep_sp + keep_off[j];
+            keys = keep_k + keep_off[j];
+            R = (uint32_t)keep_n[j];
+        } else {
+            Lines L;
+            SG_TRY(run_lines(c, b, lens[j], CUR_SLOTS, &L, false, true));
+            R = L.n_rec;
+            if (!R) continue;
+            unsigned long long *scr;
+            SG_TRY(slot(c, S_M_CNT, 2 * 256, &scr));
+            SG_HIP(hipMemsetAsync(scr, 0, 2 * 256 * 8, c->stream));
+            SG_TRY(slot(c, S_KEYS2, R, &keys));
+            SG_LAUNCH_B(c, "range_bytes", 24.0 * R, k_range_bytes, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, b,
+                        L.spans, R, d_w, d_len, ns, keys, scr);
+            spans = L.spans;
+        }
         const uint32_t ntiles = (R + PT_TILE - 1) / PT_TILE;
         const size_t nflat = (size_t)n_parts * ntiles;
         uint32_t *pcnt;
         uint64_t *ppre;
         SG_TRY(slot(c, S_PT_CNT, nflat, &pcnt));
         SG_TRY(slot(c, S_PT_PRE, nflat, &ppre));
-        SG_LAUNCH_B(c, "part_count", 16.0 * R, k_part_count, ntiles, PT_BLOCK, 0, L.spans, keys, R, n_parts, ntiles, pcnt);
+        SG_LAUNCH_B(c, "part_count", 16.0 * R, k_part_count, ntiles, PT_BLOCK, 0, spans, keys, R, n_parts, ntiles, pcnt);
         const uint32_t nt = (uint32_t)((nflat + SCAN_TILE - 1) / SCAN_TILE);
         uint64_t *tp;
         SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
@@ -769,7 +800,7 @@ int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, con
         SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
         SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64P>, nt, SCAN_BLOCK, 0, U32AsU64P{pcnt}, (uint32_t)nflat, tp + nt, ppre);
         // model: span + part read, the record's bytes read and written
-        SG_LAUNCH_B(c, "part_emit", 16.0 * R + 2.0 * (double)lens[j], k_part_apply, ntiles, PT_BLOCK, 0, b, L.spans, keys, R,
+        SG_LAUNCH_B(c, "part_emit", 16.0 * R + 2.0 * (double)lens[j], k_part_apply, ntiles, PT_BLOCK, 0, b, spans, keys, R,
                     ntiles, ppre, d_pb + j * n_parts, d_out);
     }
     return SG_OK;

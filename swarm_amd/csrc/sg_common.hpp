@@ -75,6 +75,7 @@ enum Slot : int {
     S_HB_CNT, S_HB_OFF, S_HB_OUT, S_HB_ERR, S_HB_SEL2,
     S_TS2,  // two-level tile scan scratch
     S_PT_CNT, S_PT_PRE, S_PT_BASE,  // piece partition multi-split
+    S_PT_SP, S_PT_KEYS,             // piece partition: spans and parts kept from pass 1 for pass 2
     S_NSLOTS
 };
 
@@ -99,6 +100,7 @@ struct sg_ctx {
     uint32_t last_flags = 0;  // bucket path error word of the last call (0: not declined)
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
+    uint64_t pt_keep_recs = 0;  // piece partition: records the last call kept between its passes
     // profiling
     bool profile = false;
     std::string prof_only;  // non-empty: time only launches with this name
