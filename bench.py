@@ -427,6 +427,9 @@ def bench_c5(args):
     # the stored prior is part-ordered output: keep its part boundaries instead of routing it
     # again every step (falls back to routing when a part had to be split further)
     prior_parts = sharded.split_parts(pu, pst["uniq_part_bytes"]) if not pst["rerouted_parts"] else None
+    if prior_parts is not None:
+        # stored one part per 16-byte aligned buffer, so each step's dedup reads it in place
+        prior_parts = [p.clone() if p is not None and p.data_ptr() % 16 else p for p in prior_parts]
     cur = corpus.hostport_pieces(pool, per, 0, U, seed=100 + rank, ports_per_host=K)
     del pool
     torch.cuda.synchronize()

@@ -179,6 +179,12 @@ int sg_dev_partition_bytes(sg_ctx *ctx, const uint8_t *d_buf, size_t n, const ui
 int sg_dev_partition_bytes_pieces(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
                                   const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
                                   uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records);
+/* Same, with part p starting at the 16-byte aligned offset after part p - 1's bytes (d_out
+ * 16-byte aligned; capacity >= the pieces' bytes + 1 each + 16 per part): every part is a
+ * dedup-ready aligned buffer, used in place with no staging copy. */
+int sg_dev_partition_bytes_pieces_a16(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                      const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
+                                      uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records);
 /* m evenly spaced records' first SG_SPLIT_BYTES bytes (heads: m x SG_SPLIT_BYTES host bytes,
  * zero-filled) and min(len, SG_SPLIT_BYTES) (lens), for choosing byte splitters; nothing is
  * written when the buffer has no records; *n_rec = the buffer's record count. */

@@ -24,6 +24,18 @@ from . import _abi
 from ._abi import check, lib
 
 
+def part_offsets(part_bytes: Sequence[int], align16: bool = False) -> List[int]:
+    """Start offset of every part in a partition_bytes_pieces output (align16: each part
+    starts at the 16-byte aligned offset after the previous one)."""
+    out, off = [], 0
+    for n in part_bytes:
+        out.append(off)
+        off += n
+        if align16:
+            off = (off + 15) & ~15
+    return out
+
+
 def _view(b) -> np.ndarray:
     if isinstance(b, np.ndarray):
         a = b.reshape(-1)
@@ -393,9 +405,10 @@ class Context:
         return list(pb), list(pr)
 
     def partition_bytes_pieces(self, pieces: Sequence[Tuple[int, int]], splitters: Sequence[bytes], d_out: int,
-                               out_cap: int):
+                               out_cap: int, align16: bool = False):
         """Route (device pointer, bytes) pieces into one part-contiguous buffer d_out. Returns
-        (bytes per part, records per part), totals over the pieces."""
+        (bytes per part, records per part), totals over the pieces. align16: part p starts at
+        the 16-byte aligned offset after part p - 1 (part_offsets gives the starts)."""
         blob, offs = _keys_blob(list(splitters))
         parts = len(splitters) + 1
         k = len(pieces)
@@ -403,9 +416,9 @@ class Context:
         lens = (C.c_size_t * max(1, k))(*[n for _, n in pieces])
         pb = (C.c_uint64 * parts)()
         pr = (C.c_uint64 * parts)()
-        check(lib.sg_dev_partition_bytes_pieces(self._h, ptrs, lens, k, blob.ctypes.data,
-                                                offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts,
-                                                C.c_void_p(d_out) if d_out else None, out_cap, pb, pr))
+        fn = lib.sg_dev_partition_bytes_pieces_a16 if align16 else lib.sg_dev_partition_bytes_pieces
+        check(fn(self._h, ptrs, lens, k, blob.ctypes.data, offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts,
+                 C.c_void_p(d_out) if d_out else None, out_cap, pb, pr))
         return list(pb), list(pr)
 
     def dedup_diff_into(self, d_cur: int, n_cur: int, d_prior: int, n_prior: int, d_uniq: int, uniq_cap: int,

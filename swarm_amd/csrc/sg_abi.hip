@@ -670,9 +670,13 @@ int sg_dev_partition_bytes(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint
     return dev_partition(c, b, n, n_parts, d_out, out_cap, part_bytes, part_records, nullptr, &bs);
 }
 
-int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
-                                  const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out,
-                                  size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
+}  // extern "C"
+
+// a16: part q starts at the 16-byte aligned offset after part q - 1 (parts usable in place
+// by the dedup, which takes 16-byte aligned buffers).
+static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                            const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out,
+                            size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, bool a16) {
     if (!c || (k && (!d_pieces || !lens)) || ((!splitters || !split_offs) && n_parts > 1)) {
         set_error("sg_dev_partition_bytes_pieces: bad arguments");
         return SG_E_INVAL;
@@ -739,6 +743,7 @@ int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, con
         uint64_t bq = 0, rq = 0;
         for (size_t j = 0; j < k; ++j) { rq += h[512 * j + q]; bq += h[512 * j + n_parts + q]; }
         pbase[q + 1] = pbase[q] + bq;
+        if (a16 && q + 1 < n_parts) pbase[q + 1] = (pbase[q + 1] + 15) & ~15ull;
         prec[q] = rq;
     }
     if (pbase[n_parts] > out_cap) {
@@ -746,7 +751,11 @@ int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, con
         return SG_E_CAP;
     }
     for (uint32_t q = 0; q < n_parts; ++q) {
-        if (part_bytes) part_bytes[q] = pbase[q + 1] - pbase[q];
+        if (part_bytes) {
+            uint64_t bq = 0;
+            for (size_t j = 0; j < k; ++j) bq += h[512 * j + n_parts + q];
+            part_bytes[q] = bq;
+        }
         if (part_records) part_records[q] = prec[q];
     }
     // pass 2: per piece, the multi-split: per-tile part byte counts, their scan, then every
@@ -804,6 +813,22 @@ int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, con
                     ntiles, ppre, d_pb + j * n_parts, d_out);
     }
     return SG_OK;
+}
+
+extern "C" {
+
+int sg_dev_partition_bytes_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                  const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out,
+                                  size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
+    return partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
+                            part_records, false);
+}
+
+int sg_dev_partition_bytes_pieces_a16(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                      const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
+                                      uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
+    return partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
+                            part_records, true);
 }
 
 int sg_dev_record_sample(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t m, uint8_t *heads, uint32_t *lens,

@@ -21,6 +21,8 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 
+from .api import part_offsets
+
 PART_LIMIT = 0xFFFF0000  # bytes per library call (include/swarmgpu.h)
 RECORD_LIMIT = 1 << 30   # records per library call (sg_dedup.hip build_unique)
 SPLIT_BYTES = 64         # bytes of a splitter compared (include/swarmgpu.h SG_SPLIT_BYTES)
@@ -107,15 +109,13 @@ def route(ctx, pieces: Sequence, splitters) -> List:
         if not live:
             return [None] * parts
         total = sum(p.numel() for p in live)
-        out = torch.empty(total + len(live) + 16, dtype=torch.uint8, device=live[0].device)
+        out = torch.empty(total + len(live) + 16 * (parts + 1), dtype=torch.uint8, device=live[0].device)
         ctx.fence_in()  # `out` may be a block torch's stream is still reading
+        # parts at 16-byte aligned offsets: each dedup call then reads its part in place
         pb, _ = ctx.partition_bytes_pieces([(p.data_ptr(), p.numel()) for p in live], splitters, out.data_ptr(),
-                                           out.numel())
-        res, off = [], 0
-        for b in range(parts):
-            res.append(out[off:off + pb[b]] if pb[b] else None)
-            off += pb[b]
-        return res
+                                           out.numel(), align16=True)
+        offs = part_offsets(pb, align16=True)
+        return [out[o:o + n] if n else None for o, n in zip(offs, pb)]
     lists: List[list] = [[] for _ in range(parts)]
     keep = []
     for p in live:

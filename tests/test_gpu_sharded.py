@@ -283,3 +283,34 @@ def test_stored_prior_parts_skip_routing(ctx):
     assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
     u2, f2, _ = sharded.dedup_diff_large(ctx, cur, [pu], splitters=sp)
     assert u2.cpu().numpy().tobytes() == eu and f2.cpu().numpy().tobytes() == ef
+
+
+def test_partition_pieces_aligned_parts(ctx):
+    """align16: every part starts at a 16-byte aligned offset of the output, bytes and
+    records as the back-to-back variant, padding untouched."""
+    import torch
+    from swarm_amd.api import part_offsets
+    recs = shared_prefix_records(20_000, 13)
+    data = b"\n".join(recs) + b"\n"
+    cuts = [0, len(data) // 4, len(data) // 2, len(data)]
+    cuts = [c if c in (0, len(data)) else data.index(b"\n", c) + 1 for c in cuts]
+    d = dev(b"#" + data)
+    pieces = [d[1 + a:1 + b] for a, b in zip(cuts, cuts[1:])]
+    sp = sorted(random.Random(14).sample(recs, 12))
+    out = torch.full((len(data) + 16 * 14 + 64,), 0x55, dtype=torch.uint8, device=d.device)
+    pb, pr = ctx.partition_bytes_pieces([(p.data_ptr(), p.numel()) for p in pieces], sp, out.data_ptr(), out.numel(),
+                                        align16=True)
+    per_piece = [route_parts(data[a:b], sp) for a, b in zip(cuts, cuts[1:])]
+    want = [b"".join(pp[q] for pp in per_piece) for q in range(len(sp) + 1)]
+    assert pb == [len(w) for w in want]
+    assert pr == [len(S.parse_records(w)) for w in want]
+    got = out.cpu().numpy().tobytes()
+    offs = part_offsets(pb, align16=True)
+    for o, w in zip(offs, want):
+        assert o % 16 == 0
+        assert got[o:o + len(w)] == w
+    # the padding between parts is never written
+    used = set()
+    for o, w in zip(offs, want):
+        used.update(range(o, o + len(w)))
+    assert {got[i] for i in range(len(got)) if i not in used} == {0x55}
