@@ -138,6 +138,12 @@ int sg_dev_dedup_diff(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur,
 int sg_dev_dedup_diff_into(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur, const uint8_t *d_prior,
                            size_t n_prior, uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh,
                            size_t fresh_cap, sg_dev_result *res);
+/* sg_dev_dedup_diff_into for a 16-byte aligned d_cur already parsed by
+ * sg_dev_partition_bytes_pieces_spans (its part's n_rec spans and keys): no second parse. */
+int sg_dev_dedup_diff_spans_into(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur, const uint32_t *d_spans,
+                                 const uint64_t *d_keys, size_t n_rec, const uint8_t *d_prior, size_t n_prior,
+                                 uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap,
+                                 sg_dev_result *res);
 
 /* Multi-GPU: route every record of d_buf to partition
  * part(hash64(record), n_parts), n_parts <= 256. Writes '\n'-terminated records grouped by
@@ -185,6 +191,14 @@ int sg_dev_partition_bytes_pieces(sg_ctx *ctx, const uint8_t *const *d_pieces, c
 int sg_dev_partition_bytes_pieces_a16(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
                                       const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
                                       uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records);
+/* The _a16 routing that also hands over every part's parse: *d_spans (context-owned, valid
+ * until the next _spans call on ctx) holds 2 x uint32 (start, end of the record before its
+ * '\n', relative to its part's start) per record and *d_keys its first-chunk sort key,
+ * part p's records at [sum of part_records[< p], + part_records[p]), in part order. */
+int sg_dev_partition_bytes_pieces_spans(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens,
+                                        size_t k, const uint8_t *splitters, const uint32_t *split_offs,
+                                        uint32_t n_parts, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
+                                        uint64_t *part_records, const uint32_t **d_spans, const uint64_t **d_keys);
 /* m evenly spaced records' first SG_SPLIT_BYTES bytes (heads: m x SG_SPLIT_BYTES host bytes,
  * zero-filled) and min(len, SG_SPLIT_BYTES) (lens), for choosing byte splitters; nothing is
  * written when the buffer has no records; *n_rec = the buffer's record count. */

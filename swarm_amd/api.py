@@ -421,6 +421,39 @@ class Context:
                  C.c_void_p(d_out) if d_out else None, out_cap, pb, pr))
         return list(pb), list(pr)
 
+    def partition_bytes_pieces_spans(self, pieces: Sequence[Tuple[int, int]], splitters: Sequence[bytes], d_out: int,
+                                     out_cap: int):
+        """partition_bytes_pieces(align16=True) that also returns the parts' parse: (bytes per
+        part, records per part, device spans pointer, device keys pointer); part p's records
+        start at index sum(records[:p]) (8 bytes per record in each array; context-owned until
+        the next call of this kind)."""
+        blob, offs = _keys_blob(list(splitters))
+        parts = len(splitters) + 1
+        k = len(pieces)
+        ptrs = (C.c_void_p * max(1, k))(*[C.c_void_p(p) for p, _ in pieces])
+        lens = (C.c_size_t * max(1, k))(*[n for _, n in pieces])
+        pb = (C.c_uint64 * parts)()
+        pr = (C.c_uint64 * parts)()
+        sp, kp = C.c_void_p(), C.c_void_p()
+        check(lib.sg_dev_partition_bytes_pieces_spans(self._h, ptrs, lens, k, blob.ctypes.data,
+                                                      offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts,
+                                                      C.c_void_p(d_out) if d_out else None, out_cap, pb, pr,
+                                                      C.byref(sp), C.byref(kp)))
+        return list(pb), list(pr), sp.value or 0, kp.value or 0
+
+    def dedup_diff_spans_into(self, d_cur: int, n_cur: int, d_spans: int, d_keys: int, n_rec: int, d_prior: int,
+                              n_prior: int, d_uniq: int, uniq_cap: int, d_fresh: int, fresh_cap: int) -> _abi.DevResult:
+        """dedup_diff_into for an aligned part whose records partition_bytes_pieces_spans
+        already parsed (its n_rec spans and keys)."""
+        r = _abi.DevResult()
+        check(lib.sg_dev_dedup_diff_spans_into(self._h, C.c_void_p(d_cur) if d_cur else None, n_cur,
+                                               C.c_void_p(d_spans) if d_spans else None,
+                                               C.c_void_p(d_keys) if d_keys else None, n_rec,
+                                               C.c_void_p(d_prior) if d_prior else None, n_prior, C.c_void_p(d_uniq),
+                                               uniq_cap, C.c_void_p(d_fresh) if d_fresh else None, fresh_cap,
+                                               C.byref(r)))
+        return r
+
     def dedup_diff_into(self, d_cur: int, n_cur: int, d_prior: int, n_prior: int, d_uniq: int, uniq_cap: int,
                         d_fresh: int, fresh_cap: int) -> _abi.DevResult:
         """dedup_diff with both outputs written at caller device addresses (capacities >= n_cur + 1)."""

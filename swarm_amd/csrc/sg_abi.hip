@@ -381,11 +381,21 @@ constexpr int PT_ITEMS = 16;
 constexpr uint32_t PT_TILE = PT_BLOCK * PT_ITEMS;
 
 // bytes (record + '\n') per (part, tile), part-major: cnt[q * ntiles + t]
+// Optional span output of k_part_apply (sp null: none): rpre = exclusive prefix of the
+// per-(part, tile) record counts (part-major), rbase[p] = index of part p's first record of
+// this piece among all parts' records, pstart[p] = part p's start in the output.
+struct PartSpansOut {
+    const uint64_t *rpre = nullptr, *rbase = nullptr, *pstart = nullptr;
+    uint2 *sp = nullptr;
+    uint64_t *keys = nullptr;
+};
+
 __global__ __launch_bounds__(PT_BLOCK) void k_part_count(const uint2 *__restrict__ spans, const uint64_t *__restrict__ part,
                                                           uint32_t R, uint32_t nparts, uint32_t ntiles,
-                                                          uint32_t *__restrict__ cnt) {
-    __shared__ uint32_t s_b[256];
+                                                          uint32_t *__restrict__ cnt, uint32_t *__restrict__ rcnt) {
+    __shared__ uint32_t s_b[256], s_r[256];
     s_b[threadIdx.x] = 0;
+    s_r[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t t0 = blockIdx.x * PT_TILE;
 #pragma unroll 4
@@ -394,10 +404,14 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_count(const uint2 *__restrict
         if (i < R) {
             const uint2 x = spans[i];
             atomicAdd(&s_b[(uint32_t)part[i]], x.y - x.x + 1u);
+            if (rcnt) atomicAdd(&s_r[(uint32_t)part[i]], 1u);
         }
     }
     __syncthreads();
-    if (threadIdx.x < nparts) cnt[(size_t)threadIdx.x * ntiles + blockIdx.x] = s_b[threadIdx.x];
+    if (threadIdx.x < nparts) {
+        cnt[(size_t)threadIdx.x * ntiles + blockIdx.x] = s_b[threadIdx.x];
+        if (rcnt) rcnt[(size_t)threadIdx.x * ntiles + blockIdx.x] = s_r[threadIdx.x];
+    }
 }
 
 struct U32AsU64P {
@@ -410,11 +424,13 @@ struct U32AsU64P {
 __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                                           const uint64_t *__restrict__ part, uint32_t R, uint32_t ntiles,
                                                           const uint64_t *__restrict__ pre,
-                                                          const uint64_t *__restrict__ pbase, uint8_t *__restrict__ out) {
+                                                          const uint64_t *__restrict__ pbase, uint8_t *__restrict__ out,
+                                                          const PartSpansOut so) {
     constexpr int NW = PT_BLOCK / 64;
     __shared__ uint32_t s_wh[NW][256];
     __shared__ uint32_t s_dstart[256];
     __shared__ uint64_t s_dst[256];
+    __shared__ uint64_t s_g0[256], s_pst[256];
     __shared__ uint32_t s_red[NW];
     __shared__ uint2 s_sp[PT_TILE];
     __shared__ uint32_t s_off[PT_TILE];
@@ -479,6 +495,11 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         // pbase null: one buffer, parts in part order (pre is already the global offset)
         const uint64_t pt = pre[(size_t)tid * ntiles + tile] - (pbase ? pre[(size_t)tid * ntiles] : 0ull);
         s_dst[tid] = (pbase ? pbase[tid] : 0ull) + pt - s_off[s_dstart[tid]];
+        if (so.sp) {  // record index of sorted position q = s_g0[part] + q; span base = part start
+            s_g0[tid] = so.rbase[tid] + (so.rpre[(size_t)tid * ntiles + tile] - so.rpre[(size_t)tid * ntiles]) -
+                        s_dstart[tid];
+            s_pst[tid] = so.pstart[tid];
+        }
     }
     __syncthreads();
     // copy: sorted position q by lane q (consecutive lanes, consecutive bytes of one part)
@@ -494,6 +515,12 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         const uint2 x = s_sp[q];
         const uint64_t dst = s_dst[lo] + s_off[q];
         put_medium(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
+        if (so.sp) {  // the record's span inside its part and its key, at its index in the parts
+            const uint64_t g = s_g0[lo] + q;
+            const uint32_t rel = (uint32_t)(dst - s_pst[lo]);
+            so.sp[g] = make_uint2(rel, rel + (x.y - x.x));
+            so.keys[g] = chunk_key(buf, x.x, x.y, 0);
+        }
     }
 }
 
@@ -538,7 +565,8 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
         uint64_t *ppre;
         SG_TRY(slot(c, S_PT_CNT, nflat, &pcnt));
         SG_TRY(slot(c, S_PT_PRE, nflat, &ppre));
-        SG_LAUNCH_B(c, "part_count", 16.0 * R, k_part_count, ntiles, PT_BLOCK, 0, L.spans, keys, R, parts, ntiles, pcnt);
+        SG_LAUNCH_B(c, "part_count", 16.0 * R, k_part_count, ntiles, PT_BLOCK, 0, L.spans, keys, R, parts, ntiles, pcnt,
+                    (uint32_t *)nullptr);
         const uint32_t nt = (uint32_t)((nflat + SCAN_TILE - 1) / SCAN_TILE);
         uint64_t *tp;
         SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
@@ -546,7 +574,7 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
         SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
         SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64P>, nt, SCAN_BLOCK, 0, U32AsU64P{pcnt}, (uint32_t)nflat, tp + nt, ppre);
         SG_LAUNCH_B(c, "part_emit", 16.0 * R + 2.0 * (double)n, k_part_apply, ntiles, PT_BLOCK, 0, d_buf, L.spans, keys, R,
-                    ntiles, ppre, (const uint64_t *)nullptr, d_out);
+                    ntiles, ppre, (const uint64_t *)nullptr, d_out, PartSpansOut{});
     }
     uint64_t h[2 * 256];
     SG_TRY(ctx_readback(c, h, cnt, 2 * parts * 8));
@@ -676,7 +704,8 @@ int sg_dev_partition_bytes(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint
 // by the dedup, which takes 16-byte aligned buffers).
 static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
                             const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out,
-                            size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, bool a16) {
+                            size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, bool a16,
+                            const uint2 **sp_out = nullptr, const uint64_t **k_out = nullptr) {
     if (!c || (k && (!d_pieces || !lens)) || ((!splitters || !split_offs) && n_parts > 1)) {
         set_error("sg_dev_partition_bytes_pieces: bad arguments");
         return SG_E_INVAL;
@@ -768,9 +797,30 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
             acc[q] += h[512 * j + n_parts + q];
         }
     }
+    // span output: part q's records at [rstart[q], rstart[q + 1]) of the parts' records;
+    // piece j's part-q records from rb_all[j][q] on
+    const bool want_sp = sp_out != nullptr;
+    uint2 *d_sp = nullptr;
+    uint64_t *d_k = nullptr;
+    if (want_sp) {
+        uint64_t rtot = 0;
+        std::vector<uint64_t> racc(n_parts);
+        for (uint32_t q = 0; q < n_parts; ++q) { racc[q] = rtot; rtot += prec[q]; }
+        for (size_t j = 0; j < k; ++j)
+            for (uint32_t q = 0; q < n_parts; ++q) {
+                pb_all.push_back(racc[q]);
+                racc[q] += h[512 * j + q];
+            }
+        for (uint32_t q = 0; q < n_parts; ++q) pb_all.push_back(pbase[q]);
+        SG_TRY(slot(c, S_PT_SPOUT, rtot + 1, &d_sp));
+        SG_TRY(slot(c, S_PT_KOUT, rtot + 1, &d_k));
+        *sp_out = d_sp;
+        *k_out = d_k;
+    }
     uint64_t *d_pb;
     SG_TRY(slot(c, S_PT_BASE, pb_all.size(), &d_pb));
     SG_HIP(hipMemcpy(d_pb, pb_all.data(), pb_all.size() * 8, hipMemcpyHostToDevice));
+    const uint64_t *d_rb = d_pb + (size_t)k * n_parts, *d_pstart = d_pb + 2 * (size_t)k * n_parts;
     for (size_t j = 0; j < k; ++j) {
         if (!lens[j]) continue;
         const uint8_t *b;
@@ -801,16 +851,29 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
         uint64_t *ppre;
         SG_TRY(slot(c, S_PT_CNT, nflat, &pcnt));
         SG_TRY(slot(c, S_PT_PRE, nflat, &ppre));
-        SG_LAUNCH_B(c, "part_count", 16.0 * R, k_part_count, ntiles, PT_BLOCK, 0, spans, keys, R, n_parts, ntiles, pcnt);
+        uint32_t *rcnt = nullptr;
+        uint64_t *rpre = nullptr;
+        if (want_sp) {
+            SG_TRY(slot(c, S_PT_RCNT, nflat, &rcnt));
+            SG_TRY(slot(c, S_PT_RPRE, nflat, &rpre));
+        }
+        SG_LAUNCH_B(c, "part_count", 16.0 * R, k_part_count, ntiles, PT_BLOCK, 0, spans, keys, R, n_parts, ntiles, pcnt,
+                    rcnt);
         const uint32_t nt = (uint32_t)((nflat + SCAN_TILE - 1) / SCAN_TILE);
         uint64_t *tp;
         SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
-        SG_LAUNCH(c, "scan.count", k_scan64_count<U32AsU64P>, nt, SCAN_BLOCK, 0, U32AsU64P{pcnt}, (uint32_t)nflat, tp);
-        SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
-        SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64P>, nt, SCAN_BLOCK, 0, U32AsU64P{pcnt}, (uint32_t)nflat, tp + nt, ppre);
-        // model: span + part read, the record's bytes read and written
-        SG_LAUNCH_B(c, "part_emit", 16.0 * R + 2.0 * (double)lens[j], k_part_apply, ntiles, PT_BLOCK, 0, b, spans, keys, R,
-                    ntiles, ppre, d_pb + j * n_parts, d_out);
+        for (int pass = 0; pass < (want_sp ? 2 : 1); ++pass) {
+            const U32AsU64P src{pass ? rcnt : pcnt};
+            SG_LAUNCH(c, "scan.count", k_scan64_count<U32AsU64P>, nt, SCAN_BLOCK, 0, src, (uint32_t)nflat, tp);
+            SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
+            SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64P>, nt, SCAN_BLOCK, 0, src, (uint32_t)nflat, tp + nt,
+                      pass ? rpre : ppre);
+        }
+        PartSpansOut so;
+        if (want_sp) so = PartSpansOut{rpre, d_rb + j * n_parts, d_pstart, d_sp, d_k};
+        // model: span + part read, the record's bytes read and written (+ span and key out)
+        SG_LAUNCH_B(c, "part_emit", (want_sp ? 32.0 : 16.0) * R + 2.0 * (double)lens[j], k_part_apply, ntiles, PT_BLOCK,
+                    0, b, spans, keys, R, ntiles, ppre, d_pb + j * n_parts, d_out, so);
     }
     return SG_OK;
 }
@@ -829,6 +892,43 @@ int sg_dev_partition_bytes_pieces_a16(sg_ctx *c, const uint8_t *const *d_pieces,
                                       uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records) {
     return partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
                             part_records, true);
+}
+
+int sg_dev_partition_bytes_pieces_spans(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                        const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
+                                        uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records,
+                                        const uint32_t **d_spans, const uint64_t **d_keys) {
+    if (!d_spans || !d_keys) { set_error("sg_dev_partition_bytes_pieces_spans: bad arguments"); return SG_E_INVAL; }
+    *d_spans = nullptr;
+    *d_keys = nullptr;
+    const uint2 *sp = nullptr;
+    SG_TRY(partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
+                            part_records, true, &sp, d_keys));
+    *d_spans = reinterpret_cast<const uint32_t *>(sp);
+    return SG_OK;
+}
+
+int sg_dev_dedup_diff_spans_into(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, const uint32_t *d_spans,
+                                 const uint64_t *d_keys, size_t n_rec, const uint8_t *d_prior, size_t n_prior,
+                                 uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap,
+                                 sg_dev_result *res) {
+    if (!c || !res || (!d_cur && n_cur) || (!d_prior && n_prior) || !d_uniq || (n_rec && (!d_spans || !d_keys))) {
+        set_error("sg_dev_dedup_diff_spans_into: bad arguments");
+        return SG_E_INVAL;
+    }
+    if (((uintptr_t)d_cur & 15) != 0) { set_error("sg_dev_dedup_diff_spans_into: d_cur must be 16-byte aligned"); return SG_E_INVAL; }
+    if (n_cur > MAX_BYTES || n_prior > MAX_BYTES || n_rec >= (1ull << 32)) {
+        set_error("input exceeds 4 GiB per call");
+        return SG_E_TOO_LARGE;
+    }
+    SG_HIP(hipSetDevice(c->device));
+    const uint8_t *prior = nullptr;
+    if (n_prior) SG_TRY(aligned_in(c, S_IN2, d_prior, n_prior, &prior));
+    Lines L;
+    L.spans = const_cast<uint2 *>(reinterpret_cast<const uint2 *>(d_spans));
+    L.keys = const_cast<uint64_t *>(d_keys);
+    L.n_rec = (uint32_t)n_rec;
+    return dev_dedup_diff_into_lines(c, d_cur, n_cur, L, prior, n_prior, d_uniq, uniq_cap, d_fresh, fresh_cap, res);
 }
 
 int sg_dev_record_sample(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t m, uint8_t *heads, uint32_t *lens,

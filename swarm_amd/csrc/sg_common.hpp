@@ -76,6 +76,7 @@ enum Slot : int {
     S_TS2,  // two-level tile scan scratch
     S_PT_CNT, S_PT_PRE, S_PT_BASE,  // piece partition multi-split
     S_PT_SP, S_PT_KEYS,             // piece partition: spans and parts kept from pass 1 for pass 2
+    S_PT_RCNT, S_PT_RPRE, S_PT_SPOUT, S_PT_KOUT,  // piece partition: the parts' record spans/keys out
     S_NSLOTS
 };
 

@@ -1771,6 +1771,19 @@ int dev_dedup_diff_into(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const u
     return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, true, res, nullptr, &ou, d_fresh ? &of : nullptr);
 }
 
+int dev_dedup_diff_into_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &cur, const uint8_t *d_prior,
+                              uint64_t n_prior, uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap,
+                              sg_dev_result *res) {
+    if (uniq_cap < n_cur + 1 || (d_fresh && fresh_cap < n_cur + 1)) {
+        set_error("output capacities must be >= n_cur + 1 (%llu)", (unsigned long long)(n_cur + 1));
+        return SG_E_CAP;
+    }
+    c->last_path = 0;
+    c->last_flags = 0;
+    const OutBuf ou{d_uniq, uniq_cap}, of{d_fresh, fresh_cap};
+    return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, true, res, &cur, &ou, d_fresh ? &of : nullptr);
+}
+
 int dev_dedup_diff_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &cur, const uint8_t *d_prior,
                          uint64_t n_prior, sg_dev_result *res, const uint32_t *cur_lcp) {
     c->last_path = 0;

@@ -91,6 +91,10 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
               MatchFlags *mf = nullptr);
 // dev_dedup_diff (radix pipeline) for a current scan given as already parsed records of
 // d_cur (spans + key0 from byte 0), e.g. the matched subset of a larger buffer.
+// dev_dedup_diff_into with cur's records already parsed (spans + byte-0 keys).
+int dev_dedup_diff_into_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &cur, const uint8_t *d_prior,
+                              uint64_t n_prior, uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap,
+                              sg_dev_result *res);
 int dev_dedup_diff_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &cur, const uint8_t *d_prior,
                          uint64_t n_prior, sg_dev_result *res, const uint32_t *cur_lcp = nullptr);
 // httpx -json field rows (sg_formats.hip).

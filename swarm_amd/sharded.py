@@ -141,6 +141,28 @@ def route(ctx, pieces: Sequence, splitters) -> List:
     return res
 
 
+def route_spans(ctx, pieces: Sequence, splitters):
+    """route() with byte splitters that also returns every part's parse from the routing
+    pass: (parts, [(device spans, device keys, records) or None per part]). The parse lives
+    in context buffers until the next route_spans call on ctx."""
+    import torch
+    parts = n_splitters(splitters) + 1
+    live = [p for p in pieces if p is not None and p.numel()]
+    if not live:
+        return [None] * parts, [None] * parts
+    total = sum(p.numel() for p in live)
+    out = torch.empty(total + len(live) + 16 * (parts + 1), dtype=torch.uint8, device=live[0].device)
+    ctx.fence_in()
+    pb, pr, sp, kp = ctx.partition_bytes_pieces_spans([(p.data_ptr(), p.numel()) for p in live], splitters,
+                                                      out.data_ptr(), out.numel())
+    res, parse, r0 = [], [], 0
+    for o, n, nr in zip(part_offsets(pb, align16=True), pb, pr):
+        res.append(out[o:o + n] if n else None)
+        parse.append((sp + 8 * r0, kp + 8 * r0, nr) if n else None)
+        r0 += nr
+    return res, parse
+
+
 class _Results:
     """The unique and new-record outputs of all parts, appended in part order into two
     preallocated device buffers (each part's dedup call writes there directly)."""
@@ -186,9 +208,17 @@ def dedup_diff_large(ctx, cur_pieces: Sequence, prior_pieces: Sequence = (), par
 
 def _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, out, st, samples_per_piece, depth: int = 0,
                  prior_parts=None):
-    cur_parts = route(ctx, cur_pieces, splitters)
+    if prior_parts is None and prior_pieces:
+        prior_parts = route(ctx, prior_pieces, splitters)
+    # byte splitters at the top level: the routing pass hands each part's parse to its dedup
+    # (a rerouted part's recursion routes without it, so this parse stays valid)
+    parse = None
+    if depth == 0 and isinstance(splitters, (list, tuple)):
+        cur_parts, parse = route_spans(ctx, cur_pieces, splitters)
+    else:
+        cur_parts = route(ctx, cur_pieces, splitters)
     if prior_parts is None:
-        prior_parts = route(ctx, prior_pieces, splitters) if prior_pieces else [None] * len(cur_parts)
+        prior_parts = [None] * len(cur_parts)
     if len(prior_parts) != len(cur_parts):
         raise ValueError("prior_parts has %d entries for %d parts" % (len(prior_parts), len(cur_parts)))
     for b, (c, p) in enumerate(zip(cur_parts, prior_parts)):
@@ -215,10 +245,15 @@ def _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, out, st, samples_per_
         st["part_bytes"].append(int(c.numel()))
         ctx.fence_in()
         try:
-            r = ctx.dedup_diff_into(c.data_ptr(), c.numel(), p.data_ptr() if pn else 0, pn,
-                                    out.u.data_ptr() + out.uo, out.u.numel() - out.uo,
-                                    (out.f.data_ptr() + out.fo) if out.f is not None else 0,
-                                    (out.f.numel() - out.fo) if out.f is not None else 0)
+            outs = (out.u.data_ptr() + out.uo, out.u.numel() - out.uo,
+                    (out.f.data_ptr() + out.fo) if out.f is not None else 0,
+                    (out.f.numel() - out.fo) if out.f is not None else 0)
+            if parse is not None and parse[b] is not None:
+                sp, kp, nr = parse[b]
+                r = ctx.dedup_diff_spans_into(c.data_ptr(), c.numel(), sp, kp, nr, p.data_ptr() if pn else 0, pn,
+                                              *outs)
+            else:
+                r = ctx.dedup_diff_into(c.data_ptr(), c.numel(), p.data_ptr() if pn else 0, pn, *outs)
         except Exception as e:
             raise type(e)(e.rc, "%s (part of %d bytes at %#x, prior %s)" % (
                 e, c.numel(), c.data_ptr(), None if p is None else pn)) if hasattr(e, "rc") else e

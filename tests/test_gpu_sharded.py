@@ -314,3 +314,44 @@ def test_partition_pieces_aligned_parts(ctx):
     for o, w in zip(offs, want):
         used.update(range(o, o + len(w)))
     assert {got[i] for i in range(len(got)) if i not in used} == {0x55}
+
+
+def test_partition_spans_handover(ctx):
+    """partition_bytes_pieces_spans: aligned parts plus every part's parse (spans relative
+    to the part, equal to the parser's on that part; keys as the dedup's own), and the dedup
+    fed that parse (dedup_diff_spans_into) equals the oracle's sort -u / comm -13 per part."""
+    import swarm_amd
+    import torch
+    from swarm_amd.api import part_offsets
+    recs = shared_prefix_records(25_000, 17) + [b"", b"x", b"x" * 300]
+    random.Random(18).shuffle(recs)
+    data = b"\n".join(recs) + b"\n"
+    cuts = [0, len(data) // 3, 2 * len(data) // 3, len(data)]
+    cuts = [c if c in (0, len(data)) else data.index(b"\n", c) + 1 for c in cuts]
+    d = dev(b"#" + data)
+    pieces = [d[1 + a:1 + b] for a, b in zip(cuts, cuts[1:])]
+    sp = sorted(random.Random(19).sample([r for r in recs if r], 9))
+    out = torch.full((len(data) + 16 * 11 + 64,), 0x55, dtype=torch.uint8, device=d.device)
+    pb, pr, dsp, dkp = ctx.partition_bytes_pieces_spans([(p.data_ptr(), p.numel()) for p in pieces], sp,
+                                                        out.data_ptr(), out.numel())
+    nrec = sum(pr)
+    spans = np.frombuffer(ctx.to_bytes(dsp, 8 * nrec), dtype=np.uint32).reshape(-1, 2)
+    got = out.cpu().numpy().tobytes()
+    prior_recs = sorted(set(random.Random(20).sample([r for r in recs if r], 5000)))
+    r0 = 0
+    for o, n, nr in zip(part_offsets(pb, align16=True), pb, pr):
+        part = got[o:o + n]
+        assert np.array_equal(spans[r0:r0 + nr].astype(np.uint64), swarm_amd.lines(part))
+        if n:
+            lo, hi = S.parse_records(part)[0], S.parse_records(part)[-1]
+            prior = b"".join(r + b"\n" for r in prior_recs if lo <= r <= hi)
+            dp = dev(prior)
+            ub = torch.empty(n + 64, dtype=torch.uint8, device=d.device)
+            fb = torch.empty(n + 64, dtype=torch.uint8, device=d.device)
+            r = ctx.dedup_diff_spans_into(out.data_ptr() + o, n, dsp + 8 * r0, dkp + 8 * r0, nr, dp.data_ptr(),
+                                          len(prior), ub.data_ptr() + 3, n + 1, fb.data_ptr() + 5, n + 1)
+            eu, ef = S.dedup_diff(part, prior)
+            assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+            assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+        r0 += nr
+    assert r0 == len(S.parse_records(data))
