@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 profiles: rocprofv3 kernel stats and the HBM traffic counters (FETCH_SIZE and
 # WRITE_SIZE, one counter per pass as MI355X_MICROARCH.md prescribes) for the C2, X1, URLs,
-# C3, C4 and C5 legs. Summaries: python3 tools/pmc_summary.py gpurun_out/<tag> profiles/r02/<name> c2 x1 ...
+# C3, C4, C5 and fields legs. Summaries: python3 tools/pmc_summary.py gpurun_out/<tag> profiles/r02/<name> c2 x1 ...
 #   gpurun --timeout 1200 -- 'bash tools/r2_profile.sh <tag> [legs...]'
 set -o pipefail
 TAG=${1:-r2prof}; shift
@@ -18,6 +18,7 @@ args_of() {
     c3) echo "--workload c3 --steps 3 --warmup 1 --no-cpu-baseline" ;;
     c4) echo "--workload c4 --steps 2 --warmup 1 --no-cpu-baseline" ;;
     c5) echo "--workload c5 --steps 1 --warmup 1 --no-cpu-baseline" ;;
+    fields) echo "--workload fields --steps 2 --warmup 1 --no-cpu-baseline" ;;
   esac
 }
 for wl in $LEGS; do
