@@ -349,11 +349,13 @@ __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
             }
         }
         tm_wave_sync();
-        // the templates to evaluate: touched, or vacuous (true with every count 0)
+        // the templates to evaluate: the touched ones. An untouched template sees every count
+        // 0, so it holds iff it is vacuous: those start true.
         uint32_t nl = 0;
         for (uint32_t w0 = 0; w0 < ntw; w0 += 64) {
             const uint32_t w = w0 + lane;
-            uint32_t bits = w < ntw ? (tch[w] | s_vac[w]) : 0u;
+            uint32_t bits = w < ntw ? tch[w] : 0u;
+            if (w < ntw) res[w] = s_vac[w] & ~bits;
             const uint32_t c = (uint32_t)__popc(bits), inc = wave_incl_scan(c);
             uint32_t p = nl + inc - c;
             while (bits) {
