@@ -514,12 +514,15 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         // whose run is non-empty (s_dstart is non-decreasing, so lo is that part)
         const uint2 x = s_sp[q];
         const uint64_t dst = s_dst[lo] + s_off[q];
-        put_medium(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
-        if (so.sp) {  // the record's span inside its part and its key, at its index in the parts
+        if (so.sp) {  // also the record's span inside its part and its key, at its index in the parts
+            uint64_t k0;
+            put_medium<true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
             const uint64_t g = s_g0[lo] + q;
             const uint32_t rel = (uint32_t)(dst - s_pst[lo]);
             so.sp[g] = make_uint2(rel, rel + (x.y - x.x));
-            so.keys[g] = chunk_key(buf, x.x, x.y, 0);
+            so.keys[g] = k0;
+        } else {
+            put_medium(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
         }
     }
 }
