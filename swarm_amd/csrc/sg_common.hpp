@@ -68,6 +68,7 @@ enum Slot : int {
     S_BK_SKEY, S_BK_SSPAN, S_BK_CNT1, S_BK_CNT2, S_BK_SMALL, S_BK_TOT2, S_BK_Q, S_BK_NCUR, S_BK_L1, S_BK_L2,
     S_BK_US, S_BK_FS, S_BK_SPFX, S_BK_DBG, S_BK_RECS, S_BK_NREC,
     S_M_FLAG, S_M_SP2, S_M_K2, S_R_T2, S_COUNT2,
+    S_R_ALPHA,  // refinement rounds: byte alphabet mask + rank table of the chunk keys
     // probe path (sg_dedup.hip: cur records looked up in a sorted prior's hash table)
     S_PB_TAB, S_PB_BITS, S_PB_NEW, S_PB_IDX, S_PB_SP, S_PB_K, S_PB_INS, S_PB_KB, S_PB_MI, S_PB_STAT,
     S_PB_H, S_PB_RK, S_PB_CNT, S_PB_OFF, S_PB_E, S_PB_ERR,

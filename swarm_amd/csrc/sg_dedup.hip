@@ -1145,6 +1145,63 @@ int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
 }
 
 
+// Order-preserving packing of a round's chunk keys (7 big-endian bytes + tag): each byte is
+// replaced by its rank in the alphabet the keys use (0 always present: the filler past a
+// record's end), s bits per byte, the tag kept in the low 4 bits. IP or digit-heavy chunks
+// (13 symbols: 4 bits) then sort in 4 radix passes instead of 8.
+__global__ __launch_bounds__(256) void k_alpha_mask(const uint64_t *__restrict__ K, uint32_t M, uint32_t *__restrict__ mask) {
+    __shared__ unsigned long long s_m[4];
+    if (threadIdx.x < 4) s_m[threadIdx.x] = threadIdx.x == 0 ? 1ull : 0ull;
+    __syncthreads();
+    // per thread in registers (selects, no indexed arrays), then OR-reduced over the wave
+    uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < M; j += gridDim.x * blockDim.x) {
+        const uint64_t k = K[j];
+#pragma unroll
+        for (int b = 1; b < 8; ++b) {
+            const uint32_t v = (uint32_t)(k >> (8 * b)) & 0xffu;
+            const uint64_t bit = 1ull << (v & 63u);
+            const uint32_t q = v >> 6;
+            m0 |= q == 0 ? bit : 0ull;
+            m1 |= q == 1 ? bit : 0ull;
+            m2 |= q == 2 ? bit : 0ull;
+            m3 |= q == 3 ? bit : 0ull;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m0 |= __shfl_xor((unsigned long long)m0, o, 64);
+        m1 |= __shfl_xor((unsigned long long)m1, o, 64);
+        m2 |= __shfl_xor((unsigned long long)m2, o, 64);
+        m3 |= __shfl_xor((unsigned long long)m3, o, 64);
+    }
+    if (lane_id() == 0) {
+        atomicOr(&s_m[0], (unsigned long long)m0);
+        atomicOr(&s_m[1], (unsigned long long)m1);
+        atomicOr(&s_m[2], (unsigned long long)m2);
+        atomicOr(&s_m[3], (unsigned long long)m3);
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) {
+        const uint32_t w = (uint32_t)(s_m[threadIdx.x >> 1] >> (32 * (threadIdx.x & 1)));
+        if (w) atomicOr(&mask[threadIdx.x], w);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_alpha_pack(uint64_t *__restrict__ K, uint32_t M, const uint8_t *__restrict__ rank,
+                                                    uint32_t sbits) {
+    __shared__ uint8_t s_r[256];
+    s_r[threadIdx.x] = rank[threadIdx.x];
+    __syncthreads();
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < M; j += gridDim.x * blockDim.x) {
+        const uint64_t k = K[j];
+        uint64_t p = 0;
+#pragma unroll
+        for (int b = 7; b >= 1; --b) p = (p << sbits) | s_r[(k >> (8 * b)) & 0xffu];
+        K[j] = (p << 4) | (k & 0xfu);
+    }
+}
+
 // ------------------------------------------------------------------ big-group rounds
 // Positions GS[g]..GE[g] (g < B) are groups of > 64 records sharing their first `off`
 // bytes. Each round sorts every group's members by the next 7-byte chunk (stable), marks
@@ -1169,9 +1226,32 @@ static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans
         SG_TRY(slot(c, S_R_VAL2, M, &RV2));
         SG_LAUNCH(c, "round_expand", k_expand<VT>, grid_for(M, 256), 256, 0, d_buf, spans, GS, goff, B, V, M, off, RK, RG,
                   RP);
+        // the chunk keys' byte alphabet: packed keys when it is small enough to save passes
+        uint32_t *amask;
+        SG_TRY(slot(c, S_R_ALPHA, 8 + 64, &amask));
+        SG_HIP(hipMemsetAsync(amask, 0, 32, c->stream));
+        SG_LAUNCH(c, "round_alpha", k_alpha_mask, std::min<uint32_t>(grid_for(M, 256), 512u), 256, 0, RK, M, amask);
+        uint32_t hm[8];
+        SG_TRY(ctx_readback(c, hm, amask, 32));
+        uint8_t rank[256];
+        uint32_t na = 0;
+        for (uint32_t v = 0; v < 256; ++v) {
+            rank[v] = (uint8_t)na;
+            if ((hm[v >> 5] >> (v & 31)) & 1u) ++na;
+        }
+        uint32_t sbits = 1;
+        while ((1u << sbits) < na) ++sbits;
+        int kbits = 64;
+        if (7 * sbits + 4 <= 56) {  // at least one radix pass fewer
+            uint8_t *drank = reinterpret_cast<uint8_t *>(amask + 8);
+            SG_HIP(hipMemcpy(drank, rank, 256, hipMemcpyHostToDevice));  // from the stack: complete before reuse
+            SG_LAUNCH(c, "round_alpha", k_alpha_pack, std::min<uint32_t>(grid_for(M, 256), 2048u), 256, 0, RK, M, drank,
+                      sbits);
+            kbits = (int)(7 * sbits + 4);
+        }
         uint64_t *SK;
         uint32_t *perm;
-        SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, 64, true, &SK, &perm, "rs_pass_refine"));
+        SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, kbits, true, &SK, &perm, "rs_pass_refine"));
         // stable by group index on top: keys = gid of each row in current order
         uint64_t *GK = (SK == RK) ? RK2 : RK;
         uint32_t *pv_alt = (perm == RV) ? RV2 : RV;

@@ -387,3 +387,24 @@ def test_low_entropy_keeps_seven_byte_key():
         assert c.last_key_width() == 7
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("alpha", ["ip", "wide", "nul_bytes"])
+def test_refinement_packed_chunk_keys(sg, alpha):
+    """Big groups whose next chunks use a small alphabet (IP digits: 4-bit packed keys), a
+    wide one (no packing) or NUL bytes inside records (rank 0 shared with the filler past a
+    record's end, told apart by the tag): dedup and diff equal the oracle's."""
+    rng = random.Random(71)
+    if alpha == "ip":
+        recs = [b"10.%d.%d.%d:%d" % (rng.randrange(3), rng.randrange(256), rng.randrange(256),
+                                     rng.choice([22, 80, 443, 8080, 3389])) for _ in range(60000)]
+    elif alpha == "wide":
+        recs = [b"shared-prefix/" + bytes(rng.choice(range(1, 256)) for _ in range(rng.randint(0, 12))).replace(b"\n", b"")
+                for _ in range(30000)]
+    else:
+        recs = [b"grp" + bytes(rng.choice(b"\x00a1") for _ in range(rng.randint(0, 14))) for _ in range(30000)]
+    prior_recs = sorted(set(rng.sample(recs, len(recs) // 3)))
+    cur = b"\n".join(recs) + b"\n"
+    prior = b"".join(r + b"\n" for r in prior_recs)
+    assert sg.dedup(cur) == S.dedup(cur)
+    assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)
