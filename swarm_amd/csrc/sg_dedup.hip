@@ -153,7 +153,10 @@ __device__ __forceinline__ uint2 span_of(const uint2 *spans, uint32_t v) { retur
 __device__ __forceinline__ uint2 span_of(const uint2 *, uint2 v) { return v; }
 
 // Expand big groups into member rows: row j -> group index, global position, and the
-// record's chunk key at `off`.
+// record's chunk key at `off`. One wave per 1024 consecutive rows: the group of its first
+// row by binary search, then each lane walks its rows forward (groups hold > 64 rows, so a
+// lane's group index only advances), instead of a binary search per row.
+constexpr uint32_t EXP_ROWS = 1024;
 template <typename VT>
 __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
                                                 const uint2 *__restrict__ spans,
@@ -162,18 +165,22 @@ __global__ __launch_bounds__(256) void k_expand(const uint8_t *__restrict__ buf,
                                                 const VT *__restrict__ V, uint32_t M,
                                                 uint32_t off, uint64_t *RK, uint32_t *RG,
                                                 uint32_t *RP) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= M) return;
-    uint32_t lo = 0, hi = B;  // last k with goff[k] <= j
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (goff[mid] <= j) lo = mid; else hi = mid;
+    const uint32_t j0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * EXP_ROWS;
+    if (j0 >= M) return;
+    uint32_t g = 0, hi = B;  // last k with goff[k] <= j0
+    while (hi - g > 1) {
+        const uint32_t mid = (g + hi) >> 1;
+        if (goff[mid] <= j0) g = mid; else hi = mid;
     }
-    const uint32_t pos = GS[lo] + (j - (uint32_t)goff[lo]);
-    const uint2 sp = span_of(spans, V[pos]);
-    RK[j] = chunk_key(buf, sp.x, sp.y, off);
-    RG[j] = lo;
-    RP[j] = pos;
+    const uint32_t je = min(M, j0 + EXP_ROWS);
+    for (uint32_t j = j0 + lane_id(); j < je; j += 64) {
+        while (g + 1 < B && goff[g + 1] <= j) ++g;
+        const uint32_t pos = GS[g] + (j - (uint32_t)goff[g]);
+        const uint2 sp = span_of(spans, V[pos]);
+        RK[j] = chunk_key(buf, sp.x, sp.y, off);
+        RG[j] = g;
+        RP[j] = pos;
+    }
 }
 
 __global__ void k_gid_keys(const uint32_t *__restrict__ RG, const uint32_t *__restrict__ perm,
@@ -1188,8 +1195,10 @@ __global__ __launch_bounds__(256) void k_alpha_mask(const uint64_t *__restrict__
     }
 }
 
+// RG (optional): each row's group index placed above the packed key (bit kb on), so one
+// sort orders rows by (group, chunk).
 __global__ __launch_bounds__(256) void k_alpha_pack(uint64_t *__restrict__ K, uint32_t M, const uint8_t *__restrict__ rank,
-                                                    uint32_t sbits) {
+                                                    uint32_t sbits, const uint32_t *__restrict__ RG, uint32_t kb) {
     __shared__ uint8_t s_r[256];
     s_r[threadIdx.x] = rank[threadIdx.x];
     __syncthreads();
@@ -1198,7 +1207,8 @@ __global__ __launch_bounds__(256) void k_alpha_pack(uint64_t *__restrict__ K, ui
         uint64_t p = 0;
 #pragma unroll
         for (int b = 7; b >= 1; --b) p = (p << sbits) | s_r[(k >> (8 * b)) & 0xffu];
-        K[j] = (p << 4) | (k & 0xfu);
+        p = (p << 4) | (k & 0xfu);
+        K[j] = RG ? (((uint64_t)RG[j] << kb) | p) : p;
     }
 }
 
@@ -1224,8 +1234,8 @@ static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans
         SG_TRY(slot(c, S_R_POS, M, &RP));
         SG_TRY(slot(c, S_R_VAL, M, &RV));
         SG_TRY(slot(c, S_R_VAL2, M, &RV2));
-        SG_LAUNCH(c, "round_expand", k_expand<VT>, grid_for(M, 256), 256, 0, d_buf, spans, GS, goff, B, V, M, off, RK, RG,
-                  RP);
+        SG_LAUNCH(c, "round_expand", k_expand<VT>, (M + 4 * EXP_ROWS - 1) / (4 * EXP_ROWS), 256, 0, d_buf, spans, GS, goff,
+                  B, V, M, off, RK, RG, RP);
         // the chunk keys' byte alphabet: packed keys when it is small enough to save passes
         uint32_t *amask;
         SG_TRY(slot(c, S_R_ALPHA, 8 + 64, &amask));
@@ -1241,32 +1251,42 @@ static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans
         }
         uint32_t sbits = 1;
         while ((1u << sbits) < na) ++sbits;
+        int gbits = 1;
+        while (gbits < 32 && (1u << gbits) < B) ++gbits;
         int kbits = 64;
+        bool joint = false;  // (group, packed chunk) in one key: one sort, no group pass
         if (7 * sbits + 4 <= 56) {  // at least one radix pass fewer
+            kbits = (int)(7 * sbits + 4);
+            joint = kbits + gbits <= 64;
             uint8_t *drank = reinterpret_cast<uint8_t *>(amask + 8);
             SG_HIP(hipMemcpy(drank, rank, 256, hipMemcpyHostToDevice));  // from the stack: complete before reuse
             SG_LAUNCH(c, "round_alpha", k_alpha_pack, std::min<uint32_t>(grid_for(M, 256), 2048u), 256, 0, RK, M, drank,
-                      sbits);
-            kbits = (int)(7 * sbits + 4);
+                      sbits, joint ? RG : (const uint32_t *)nullptr, (uint32_t)kbits);
         }
-        uint64_t *SK;
-        uint32_t *perm;
-        SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, kbits, true, &SK, &perm, "rs_pass_refine"));
-        // stable by group index on top: keys = gid of each row in current order
-        uint64_t *GK = (SK == RK) ? RK2 : RK;
-        uint32_t *pv_alt = (perm == RV) ? RV2 : RV;
-        SG_LAUNCH(c, "round_gid", k_gid_keys, grid_for(M, 256), 256, 0, RG, perm, GK, M);
-        int gbits = 1;
-        while (gbits < 32 && (1u << gbits) < B) ++gbits;
-        uint64_t *GK2 = (GK == RK) ? RK2 : RK;
-        uint64_t *FKs;
-        uint32_t *perm2;
-        SG_TRY(radix_sort(c, GK, perm, GK2, pv_alt, M, 0, gbits, false, &FKs, &perm2, "rs_pass_refine"));
-        uint32_t *Tfree = (perm2 == perm) ? pv_alt : perm;
+        uint64_t *FK;
+        uint32_t *perm2, *Tfree;
+        if (joint) {
+            uint64_t *SK;
+            SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, kbits + gbits, true, &SK, &perm2, "rs_pass_refine"));
+            Tfree = (perm2 == RV) ? RV2 : RV;
+            FK = (SK == RK) ? RK2 : RK;
+        } else {
+            uint64_t *SK;
+            uint32_t *perm;
+            SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, kbits, true, &SK, &perm, "rs_pass_refine"));
+            // stable by group index on top: keys = gid of each row in current order
+            uint64_t *GK = (SK == RK) ? RK2 : RK;
+            uint32_t *pv_alt = (perm == RV) ? RV2 : RV;
+            SG_LAUNCH(c, "round_gid", k_gid_keys, grid_for(M, 256), 256, 0, RG, perm, GK, M);
+            uint64_t *GK2 = (GK == RK) ? RK2 : RK;
+            uint64_t *FKs;
+            SG_TRY(radix_sort(c, GK, perm, GK2, pv_alt, M, 0, gbits, false, &FKs, &perm2, "rs_pass_refine"));
+            Tfree = (perm2 == perm) ? pv_alt : perm;
+            FK = (FKs == GK) ? GK2 : GK;
+        }
         VT *T;
         if constexpr (sizeof(VT) == 4) T = Tfree;
         else SG_TRY(slot(c, S_R_T2, M, &T));
-        uint64_t *FK = (FKs == GK) ? GK2 : GK;
         SG_LAUNCH(c, "round_gather", k_round_gather<VT>, grid_for(M, 256), 256, 0, d_buf, spans, V, RP, perm2, M, off, T, FK);
         SG_LAUNCH(c, "round_scatter", k_round_scatter<VT>, grid_for(M, 256), 256, 0, T, RP, M, V);
         // perm2 and the free id buffer are reusable after the scatter (same stream)
