@@ -117,17 +117,18 @@ struct BigGroupPred {
 // Over the final order of a refinement round: sub-segments by (group, chunk key). brk at
 // every sub-segment head; A/B = bounds of tag-8 sub-segments of more than WAVE_GROUP rows.
 struct RoundGroupPred {
-    const uint64_t *FK;     // chunk key, final order
+    const uint64_t *FK;     // chunk key (or its packed form), final order
     const uint32_t *G;      // group index, final order
     const uint32_t *P;      // global position, final order
     uint8_t *brk;
     uint32_t n;
+    uint64_t tagmask;       // the tag's bits: 0xff, or 0xf in a packed key
     __device__ uint32_t operator()(uint32_t i) const {
         const uint64_t k = FK[i];
         const uint32_t g = G[i];
         const bool head = (i == 0) || FK[i - 1] != k || G[i - 1] != g;
         brk[P[i]] = head ? 1 : 0;
-        if ((k & 0xffu) != 8u) return 0u;
+        if ((k & tagmask) != 8u) return 0u;
         const bool tail = (i + 1 == n) || FK[i + 1] != k || G[i + 1] != g;
         const bool bh = head && (i + WAVE_GROUP < n) && FK[i + WAVE_GROUP] == k && G[i + WAVE_GROUP] == g;
         const bool bt = tail && (i >= WAVE_GROUP) && FK[i - WAVE_GROUP] == k && G[i - WAVE_GROUP] == g;
@@ -198,6 +199,7 @@ __global__ void k_round_gather(const uint8_t *__restrict__ buf, const uint2 *__r
     if (i >= M) return;
     const VT r = V[RP[perm[i]]];
     T[i] = r;
+    if (!FK) return;  // the sorted packed keys serve as the final keys
     const uint2 sp = span_of(spans, r);
     FK[i] = chunk_key(buf, sp.x, sp.y, off);
 }
@@ -1265,11 +1267,13 @@ static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans
         }
         uint64_t *FK;
         uint32_t *perm2, *Tfree;
+        uint64_t *FKw;  // the round_gather's key output (null: FK = the sorted packed keys)
         if (joint) {
             uint64_t *SK;
             SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, kbits + gbits, true, &SK, &perm2, "rs_pass_refine"));
             Tfree = (perm2 == RV) ? RV2 : RV;
-            FK = (SK == RK) ? RK2 : RK;
+            FK = SK;  // (group, packed chunk): equal iff same group and same chunk; tag in bits 0..3
+            FKw = nullptr;
         } else {
             uint64_t *SK;
             uint32_t *perm;
@@ -1283,16 +1287,18 @@ static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans
             SG_TRY(radix_sort(c, GK, perm, GK2, pv_alt, M, 0, gbits, false, &FKs, &perm2, "rs_pass_refine"));
             Tfree = (perm2 == perm) ? pv_alt : perm;
             FK = (FKs == GK) ? GK2 : GK;
+            FKw = FK;
         }
         VT *T;
         if constexpr (sizeof(VT) == 4) T = Tfree;
         else SG_TRY(slot(c, S_R_T2, M, &T));
-        SG_LAUNCH(c, "round_gather", k_round_gather<VT>, grid_for(M, 256), 256, 0, d_buf, spans, V, RP, perm2, M, off, T, FK);
+        SG_LAUNCH(c, "round_gather", k_round_gather<VT>, grid_for(M, 256), 256, 0, d_buf, spans, V, RP, perm2, M, off, T, FKw);
         SG_LAUNCH(c, "round_scatter", k_round_scatter<VT>, grid_for(M, 256), 256, 0, T, RP, M, V);
         // perm2 and the free id buffer are reusable after the scatter (same stream)
         uint32_t *NS = perm2, *NE = Tfree;
         uint32_t B3 = 0, B4 = 0;
-        SG_TRY(run_select2(c, "round_mark", RoundGroupPred{FK, RG, RP, brk, M}, M, NS, NE, &B3, &B4));
+        SG_TRY(run_select2(c, "round_mark", RoundGroupPred{FK, RG, RP, brk, M, joint ? 0xfull : 0xffull}, M, NS, NE, &B3,
+                           &B4));
         if (B3 != B4) { set_error("round group mismatch %u/%u", B3, B4); return SG_E_HIP; }
         if (B3) {
             SG_LAUNCH(c, "round_pos", k_pos_of, grid_for(B3, 256), 256, 0, NS, RP, B3, GS);
