@@ -1,17 +1,25 @@
 #!/usr/bin/env python3
-"""Benchmark: scan-result dedup + new-record diff (BASELINE.json configs[1], "C2"):
-10M synthetic subdomain lines per GPU, sort -u + diff against the prior scan (90 % of the
-unique set), inputs resident in HBM before the timed region.
+"""Benchmark of the scan-result hot path (BASELINE.json metric: records/s and GB/s vs the HBM
+roofline for match+dedup+diff, 1 and 8 GPUs).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-       (records hash-partitioned over the GPUs with one RCCL all-to-all per step; weak
-       scaling: every rank brings its own 10M lines drawn from one global universe)
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ...]
 
-Prints ONE JSON line (rank 0). `roofline` is the dominant kernel's algorithmic bytes ÷
-its average launch time (HIP events on the launch stream, live in the timed region);
-`cpu_baseline` is the oracle's Python restatement of the reference semantics
-(sorted(set()) + set difference) timed on this host, single thread, on rank 0 at N=1.
+N = 1 (default workload c2): ONE JSON line whose headline is BASELINE configs[1] ("C2": 10M
+synthetic subdomain lines, sort -u + diff against the prior scan, inputs resident in HBM),
+carrying the other configs measured in the same run as sub-objects, each with its own
+roofline and CPU baseline: `c1` (configs[0], the reference's CPU-runnable case through the
+drop-in completion hook), `c3` (configs[2], 50M httpx lines x 2,000 literals), `c5`
+(configs[4], 1B host:port records on one GPU), `fused_x1` (the metric's match+dedup+diff as
+one call) and `urls`.
+N > 1 (default workload c5): C5 STRONG scaling — 1B host:port records in total, byte-range
+sharded over the N ranks with the round-pipelined RCCL all-to-all (swarm_amd.distributed
+.dedup_diff_rounds_step) — with the C2 weak-scaling step (10M lines per rank) as a `c2_weak`
+sub-object. The launcher starts N ranks itself when no torch.distributed launcher wraps it.
+
+`roofline` is the dominant kernel's algorithmic bytes ÷ its average launch time (HIP events
+on the launch stream, live in the timed region); `cpu_baseline` is the oracle's Python
+restatement of the reference semantics timed on this host (1 thread), plus GNU coreutils /
+grep across the host's core share.
 """
 import argparse
 import json
@@ -35,7 +43,7 @@ KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_u
                  "json_emit": "k_json_emit", "tm_eval": "k_tm_eval", "tm_collect": "k_tm_collect",
                  "bk_sort": "k_bk_sort", "bk_l1_apply": "k_bp_apply", "bk_l2_apply": "k_bp_apply",
                  "bk_l1_count": "k_bp_count", "bk_l2_count": "k_bp_count", "bk_compact": "k_bk_compact",
-                 "part_emit": "k_emit_apply", "range_bytes": "k_range_bytes", "gather_spans": "k_gather_spans",
+                 "part_emit": "k_part_apply", "range_bytes": "k_range_bytes", "gather_spans": "k_gather_spans",
                  "gather_matched": "k_gather_matched", "seg_wave": "k_seg_wave", "seg_small": "k_seg_small",
                  "rs_up": "k_rs_up", "lcp": "k_lcp", "rekey": "k_rekey"}
 
@@ -90,63 +98,98 @@ def kernel_table(stats):
     return out
 
 
-def timed_steps(ctx, run, args, barrier=None):
-    """W warmup steps; one fully profiled untimed step (per-kernel table, dominant kernel);
-    then K timed steps with HIP events only around the dominant kernel's launches.
-    Returns (elapsed_s, full_stats, timed_stats, dominant, last_result)."""
+def timed_steps(ctx, run, args, world: int = 1):
+    """W warmup steps; one fully profiled untimed step (per-kernel table, dominant kernel:
+    rank 0's, agreed across ranks); then K timed steps with HIP events only around the
+    dominant kernel's launches, bracketed by a barrier + device sync on both sides; the
+    elapsed time is the max over ranks. Returns (elapsed_s, full_stats, timed_stats,
+    dominant, last_result)."""
     import torch
+    import torch.distributed as dist
     r = None
     for _ in range(args.warmup):
+        r = None
         r = run()
     torch.cuda.synchronize()
     ctx.reset_stats()
     ctx.profile(True)
+    r = None
     r = run()
     torch.cuda.synchronize()
     ctx.profile(False)
     full = ctx.kernel_stats()
     dominant = max(full.items(), key=lambda kv: kv[1][1])[0] if full else None
+    if world > 1:
+        names = [None] * world
+        dist.all_gather_object(names, dominant)
+        dominant = names[0]
     ctx.reset_stats()
     ctx.profile(True, only=dominant)
-    if barrier:
-        barrier()
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        r = None
         r = run()
     torch.cuda.synchronize()
-    if barrier:
-        barrier()
+    if world > 1:
+        dist.barrier()
     el = time.perf_counter() - t0
     ctx.profile(False)
+    if world > 1:
+        from swarm_amd import distributed as D
+        el = D.all_max_float(el)
     return el, full, ctx.kernel_stats(), dominant, r
 
 
-def bench_c3(args):
-    """BASELINE.json configs[2] (C3): httpx-style response lines x 2,000 literal signatures
-    (sampled, seed 0, from the nuclei template words of length >= 4), Aho-Corasick, 1 GPU."""
-    import base64
-    import random
+def sub_leg(name, fn, keys=None):
+    """Run one sub-leg of the default line; a failure is recorded in the line (never hidden,
+    never fatal to the headline). keys: the fields of the leg's own line to keep."""
+    import torch
+    try:
+        torch.cuda.empty_cache()
+        out = fn()
+        if keys:
+            out = {k: out[k] for k in keys if k in out}
+        return out
+    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+        import traceback
+        traceback.print_exc()
+        return {"error": "%s: %s" % (type(e).__name__, e)}
+    finally:
+        torch.cuda.empty_cache()
 
+
+SUB_KEYS = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "gbps", "hbm_frac_step", "records",
+            "roofline", "cpu_baseline", "dedup_path", "kernels_top", "scaling", "n_gpus")
+
+
+def bench_c3(args, ctx=None, emit=True):
+    """BASELINE.json configs[2] (C3): 50M httpx-style response lines x 2,000 literal
+    signatures (sampled, seed 0, from the nuclei template words of length >= 4), 1 GPU. One
+    step = parse + match + hits sorted by record + the matched lines serialised (grep
+    output). Algorithmic bytes (SURVEY.md §8(d) match model): input + matched output."""
     import numpy as np
     import torch
 
     import swarm_amd
     from swarm_amd import corpus
 
-    torch.cuda.set_device(0)
-    sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
-    words = [base64.b64decode(w) for w in sig["words"]]
-    sigs = random.Random(0).sample([w for w in words if len(w) >= 4], 2000)
-    n_lines = args.lines if args.lines != 10_000_000 else 50_000_000
+    own = ctx is None
+    if own:
+        torch.cuda.set_device(0)
+        ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    sigs = c3_signatures()
+    n_lines = args.c3_lines
     pool = corpus.httpx_pool(sigs, 1 << 16, 0.01, seed=0)
     buf = corpus.lines_from_pool(pool, n_lines, seed=1)
     d = torch.from_numpy(buf).cuda()
-    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
     m = swarm_amd.Matcher(sigs, "literal")
     run = lambda: m.dev_match(ctx, d.data_ptr(), d.numel())  # noqa: E731
     el, full, stats, dominant, r = timed_steps(ctx, run, args)
     R = int(r.in_records)
+    step_bytes = int(d.numel()) + int(r.lines_bytes)
     cpu = None
     if not args.no_cpu_baseline:
         from oracle import semantics as S
@@ -159,20 +202,21 @@ def bench_c3(args):
         cpu = {"value": round(m_s / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
                "sample": "%d C3 lines x 2000 literals, oracle `sig in line`, 1 thread, %.2f s" % (m_s, tc),
                "host_cpus": os.cpu_count()}
-        gh = m.match(sample)
-        cpu["gpu_hits_bit_exact_on_sample"] = (gh == hits)
-        # GNU grep -F over the whole C3 input on the host cores, checked against the GPU's
-        # full matched-line output (full-size parity)
-        cores = host_cores()
-        g = gnu_grep(buf.tobytes(), sigs, cores, "-F")
-        if g:
-            gm, secs = g
-            r_full = m.dev_match(ctx, d.data_ptr(), d.numel())
-            cpu["gnu_grep"] = {"value": round(R / secs, 1), "unit": "records/s", "cores": cores, "seconds": secs,
-                               "sample": "the full input (%d lines, %d B)" % (R, d.numel()),
-                               "command": "LC_ALL=C grep -a -F -f sigs (x%d line-aligned splits)" % cores,
-                               "bit_exact_full": ctx.to_bytes(r_full.lines, r_full.lines_bytes) == gm}
-    print(json.dumps({
+        cpu["gpu_hits_bit_exact_on_sample"] = (m.match(sample) == hits)
+        if not args.no_gnu:
+            # GNU grep -F over the whole C3 input on the host cores, checked against the GPU's
+            # full matched-line output (full-size parity)
+            cores = host_cores()
+            g = gnu_grep(buf.tobytes(), sigs, cores, "-F")
+            if g:
+                gm, secs = g
+                r_full = m.dev_match(ctx, d.data_ptr(), d.numel())
+                cpu["gnu_grep"] = {"value": round(R / secs, 1), "unit": "records/s", "cores": cores, "seconds": secs,
+                                   "sample": "the full input (%d lines, %d B)" % (R, d.numel()),
+                                   "command": "LC_ALL=C grep -a -F -f sigs (x%d line-aligned splits)" % cores,
+                                   "bit_exact_full": ctx.to_bytes(r_full.lines, r_full.lines_bytes) == gm}
+                del gm
+    out = {
         "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
@@ -180,15 +224,24 @@ def bench_c3(args):
         "config": {"workload": "C3: %dM httpx lines x 2000 literal signatures, 1 GPU" % (n_lines // 1_000_000),
                    "engine": "lit_match" if "lit_match" in full else "ac_match",
                    "bytes": int(d.numel()), "automaton_states": m.info()["states"]},
-        "gbps": round(d.numel() * args.steps / el / 1e9, 2),
-        "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records)},
+        "gbps": round(step_bytes * args.steps / el / 1e9, 2),
+        "hbm_frac_step": round(step_bytes * args.steps / el / 1e9 / HBM_PEAK_GBS, 4),
+        "records": {"in": R, "hits": int(r.n_hits), "matched": int(r.matched_records),
+                    "matched_bytes": int(r.lines_bytes)},
         "roofline": roofline_of(stats, dominant, "c3", full),
         "cpu_baseline": cpu,
         "kernels": kernel_table(full),
         "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
                         "HIP events only around the dominant kernel",
-    }), flush=True)
-    ctx.close()
+    }
+    out["kernels_top"] = dict(list(out["kernels"].items())[:8])
+    if emit:
+        print(json.dumps(out), flush=True)
+    del d, buf, r
+    m.close()
+    if own:
+        ctx.close()
+    return out
 
 
 def bench_c4(args):
@@ -216,7 +269,7 @@ def bench_c4(args):
         torch.cuda.set_device(0)
     sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
     pats, n_generic = corpus.c4_signatures([base64.b64decode(r["p"]) for r in sig["regexes"]])
-    n_lines = args.lines if args.lines != 10_000_000 else 12_500_000
+    n_lines = args.c4_lines
     pool = corpus.banner_pool()
     buf = corpus.lines_from_pool(pool, n_lines, seed=3 + rank)  # rank r's contiguous input shard
     d = torch.from_numpy(buf).cuda()
@@ -229,11 +282,7 @@ def bench_c4(args):
     def run():
         r, tot["g"] = D.match_step(ctx, m, d)
         return r
-    el, full, stats, dominant, r = timed_steps(ctx, run, args, barrier=dist.barrier if world > 1 else None)
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=d.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el, full, stats, dominant, r = timed_steps(ctx, run, args, world)
     g_rec, g_hits, g_matched = tot["g"]
     R = int(r.in_records)
     cpu = None
@@ -326,7 +375,7 @@ def bench_fields(args):
     from swarm_amd import corpus
 
     torch.cuda.set_device(0)
-    n_lines = args.lines if args.lines != 10_000_000 else 4_000_000
+    n_lines = args.fields_lines
     buf = corpus.lines_from_pool(corpus.httpx_json_pool(1 << 14, seed=5), n_lines, seed=6)
     d = torch.from_numpy(buf).cuda()
     ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
@@ -373,39 +422,38 @@ def bench_fields(args):
     ctx.close()
 
 
-def bench_c5(args):
-    """BASELINE.json configs[4] (C5): 1B host:port records (~31 GB) deduped and diffed against
-    a prior scan at 90 % overlap, strong scaling over N ranks. Records are rendered on the
-    GPU: 64M hosts x 4 open-port slots (ports from 32 common ones) = 256M distinct combos,
-    1B draws (~4 copies each). Each rank routes
-    its draw by byte ranges agreed across ranks (RCCL all-to-all when N > 1), then processes
-    its range in local range parts of < 4 GiB (swarm_amd.sharded); rank outputs concatenated
-    in rank order are the global sort -u / comm -13 output. Setup (untimed): the prior scan
-    = sort -u of another 1B draw over combos shifted by 10 %, routed to its owner ranks, and
-    the splitters (byte quantiles of the prior's sampled records, known before the scan).
+def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
+    """BASELINE.json configs[4] (C5): 1B host:port records (~31 GB) in total, deduped and
+    diffed against a prior scan at 90 % overlap; STRONG scaling: the N ranks share the 1B
+    records. Records are rendered on the GPU: 64M hosts x 4 open-port slots (ports from 32
+    common ones) = 256M distinct combos, 1B draws (~4 copies each).
+    N = 1: the shard (in pieces of 50M records) is routed into local byte-range parts of
+    < 4 GiB by one partition call that hands each part's parse to its dedup
+    (swarm_amd.sharded.dedup_diff_large); the stored prior is kept one aligned part each.
+    N > 1: one partition call routes the rank's pieces into N x R byte ranges, one all-to-all
+    of the part sizes, R all-to-alls of bytes queued on RCCL's stream, each local part deduped
+    as soon as its round arrives (swarm_amd.distributed.dedup_diff_rounds_step); rank
+    outputs concatenated in rank order are the global sort -u / comm -13 output. Setup
+    (untimed): the prior scan = sort -u of another 1B draw over combos shifted by 10 %,
+    routed to its owner ranks and parts by the same splitters (byte quantiles of the prior's
+    sampled records, agreed across ranks), and stored.
     --c5-data ips: 10.x.y.z:port records (every record shares '10.', most their first 7
     bytes), the case key0 routing could not divide."""
     import numpy as np
     import torch
-    import torch.distributed as dist
 
     import swarm_amd
     from swarm_amd import corpus, sharded
     from swarm_amd import distributed as D
 
-    world, rank, local = dist_setup(args)
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        local = local % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.dist_backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
-    total = args.lines if args.lines != 10_000_000 else 1_000_000_000
-    per = total // world
+    dev = dev or torch.device("cuda", 0)
+    own = ctx is None
+    if own:
+        ctx = swarm_amd.Context(dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    total = args.c5_records
+    per = total // world + (1 if rank < total % world else 0)
     if args.c5_data == "ips":
-        # 10.x.y.z:port from an internal-range scan: 16M hosts x 16 open-port slots
+        # 10.x.y.z:port from an internal-range scan: 15M hosts x 16 open-port slots
         n_hosts = min(args.c5_hosts, 1 << 24) if args.c5_hosts != 64_000_000 else 15_000_000
         K = 16
         pool = corpus.ip_pool_torch(n_hosts + n_hosts // 10 + 1, seed=5, device=dev)
@@ -414,74 +462,56 @@ def bench_c5(args):
         K = 4  # open-port slots per host (ports drawn from 32 common ports)
         pool = corpus.host_pool_torch(n_hosts + n_hosts // 10 + 1, seed=5, device=dev)
     U = n_hosts * K
-    ctx = swarm_amd.Context(local, torch.cuda.current_stream(dev).cuda_stream)
     t_setup = time.perf_counter()
     prior_raw = corpus.hostport_pieces(pool, per, U // 10, U + U // 10, seed=900 + rank, ports_per_host=K)
-    gsplit = D.agree_splitters(ctx, prior_raw, world) if world > 1 else []
-    mine = D.range_exchange(ctx, prior_raw, gsplit) if world > 1 else prior_raw
-    parts = sharded.plan_parts(mine, [], 2 << 30)
-    lsplit = sharded.choose_splitters(sharded.sample_records(ctx, mine), parts)
-    pu, _, pst = sharded.dedup_diff_large(ctx, mine, (), splitters=lsplit)
-    del prior_raw, mine
-    prior_local = sharded.split_at_newlines(pu, 3 << 30)
-    # the stored prior is part-ordered output: keep its part boundaries instead of routing it
-    # again every step (falls back to routing when a part had to be split further)
-    prior_parts = sharded.split_parts(pu, pst["uniq_part_bytes"]) if not pst["rerouted_parts"] else None
-    if prior_parts is not None:
-        # stored one part per 16-byte aligned buffer, so each step's dedup reads it in place
-        prior_parts = [p.clone() if p is not None and p.data_ptr() % 16 else p for p in prior_parts]
     cur = corpus.hostport_pieces(pool, per, 0, U, seed=100 + rank, ports_per_host=K)
     del pool
+    cur_bytes = sum(p.numel() for p in cur)
+    if world == 1:
+        parts = sharded.plan_parts(prior_raw, [], 2 << 30)
+        split = sharded.choose_splitters(sharded.sample_records(ctx, prior_raw), parts)
+        pu, _, pst = sharded.dedup_diff_large(ctx, prior_raw, (), splitters=split, align_parts=True)
+        del prior_raw
+        # the stored prior is this path's own part-ordered output: one 16-byte aligned part
+        # per local range, read in place by every step (never routed again)
+        prior_parts = sharded.stored_parts(pu, pst) if not pst["rerouted_parts"] else None
+        prior_store = pu
+        rounds = len(split) + 1
+
+        def step():
+            if prior_parts is not None:
+                return sharded.dedup_diff_large(ctx, cur, (), splitters=split, prior_parts=prior_parts)
+            return sharded.dedup_diff_large(ctx, cur, [pu], splitters=split)
+    else:
+        rounds = D.all_max_int(D.plan_rounds(max(cur_bytes, 1), world))
+        split = D.agree_splitters(ctx, prior_raw, world * rounds)
+        prior_parts, prior_store = D.build_prior_rounds(ctx, prior_raw, split, rounds)
+        del prior_raw
+
+        def step():
+            return D.dedup_diff_rounds_step(ctx, cur, prior_parts, split, rounds)
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup
+    prior_bytes = int(prior_store.numel())
 
-    def step():
-        return D.dedup_diff_range_step(ctx, cur, prior_local, gsplit, lsplit, prior_parts=prior_parts)
+    holder = {}
 
-    for _ in range(args.warmup):
+    def run():
         u, f, st = step()
-        del u, f
-    torch.cuda.synchronize()
-    ctx.reset_stats()
-    ctx.profile(True)
-    u, f, st = step()
-    torch.cuda.synchronize()
-    ctx.profile(False)
-    full = ctx.kernel_stats()
-    ub, fb = int(u.numel()), int(f.numel())
-    del u, f
-    dominant = max(full.items(), key=lambda kv: kv[1][1])[0] if full else None
+        holder["st"], holder["ub"], holder["fb"] = st, int(u.numel()), int(f.numel())
+        return None
+    el, full, stats, dominant, _ = timed_steps(ctx, run, args, world)
+    st, ub, fb = holder["st"], holder["ub"], holder["fb"]
+    step_bytes = cur_bytes + prior_bytes + ub + fb
     if world > 1:
-        names = [None] * world
-        dist.all_gather_object(names, dominant)
-        dominant = names[0]
-    ctx.reset_stats()
-    ctx.profile(True, only=dominant)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        u, f, st = step()
-        del u, f
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    ctx.profile(False)
-    stats = ctx.kernel_stats()
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    cur_bytes = sum(p.numel() for p in cur)
-    prior_bytes = sum(p.numel() for p in prior_local)
+        step_bytes = D.all_max_int(step_bytes) * world  # reported as the whole job's (max rank x N)
+        tot_in = D.all_max_int(st["in_records"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import semantics as S
         m = 2_000_000
         c0 = cur[0][: int(torch.nonzero(cur[0][: 40 * m] == 10)[m - 1].item()) + 1].cpu().numpy().tobytes()
-        p0 = prior_local[0][:40 * m].cpu().numpy().tobytes()
+        p0 = prior_store[:40 * m].cpu().numpy().tobytes()
         p0 = p0[: p0.rfind(b"\n") + 1]
         tc = time.perf_counter()
         eu, ef = S.dedup_diff(c0, p0)
@@ -491,25 +521,29 @@ def bench_c5(args):
                          "1 thread, %.2f s" % tc, "host_cpus": os.cpu_count()}
         gu, gf, _ = sharded.dedup_diff_large(ctx, [dev_bytes(c0, dev)], [dev_bytes(p0, dev)], part_bytes=16 << 20)
         cpu["gpu_bit_exact_on_sample"] = (gu.cpu().numpy().tobytes() == eu and gf.cpu().numpy().tobytes() == ef)
+        del gu, gf
+    out = None
     if rank == 0:
-        print(json.dumps({
+        pb = st["part_bytes"]
+        out = {
             "metric": METRIC, "value": round(total * args.steps / el, 1), "unit": "records/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (host:port records rendered on the GPU, SURVEY.md §8(d) C5)",
-            "config": {"workload": "C5: %dM %s records (%.1f GB on rank 0) + prior at 90%% overlap, "
+            "config": {"workload": "C5: %dM %s records in total (%.1f GB on rank 0) + prior at 90%% overlap, "
                                    "byte-range sharded over %d GPU(s)" % (
                                        total // 1_000_000, "10.x.y.z:port" if args.c5_data == "ips" else "host:port",
                                        cur_bytes / 1e9, world),
                        "records_total": total, "hosts": n_hosts, "ports_per_host": K,
-                       "prior_bytes_rank0": int(prior_bytes), "local_parts": len(lsplit) + 1,
-                       "part_balance_max_over_mean": round(max(st["part_bytes"]) * len(st["part_bytes"])
-                                                           / max(1, sum(st["part_bytes"])), 3)
-                                                     if st["part_bytes"] else None,
+                       "prior_bytes_rank0": prior_bytes, "local_parts": rounds,
+                       "part_balance_max_over_mean": round(max(pb) * len(pb) / max(1, sum(pb)), 3) if pb else None,
                        "rerouted_parts": st["rerouted_parts"],
                        "setup_s": round(t_setup, 1),
-                       "parallelism": "byte-range all-to-all x%d" % world if world > 1 else "single GPU"},
-            "gbps": round((cur_bytes + prior_bytes + ub + fb) * world * args.steps / el / 1e9, 2),
+                       "parallelism": ("byte-range sharding, %d exchange rounds of RCCL all-to-all x%d "
+                                       "(backend %s, world size %d)" % (rounds, world, args.dist_backend, world))
+                                      if world > 1 else "single GPU"},
+            "gbps": round(step_bytes * args.steps / el / 1e9, 2),
+            "hbm_frac_step": round(step_bytes * args.steps / el / 1e9 / (HBM_PEAK_GBS * world), 4),
             "records": {"in_rank0": st["in_records"], "unique_rank0": st["uniq_records"],
                         "new_rank0": st["fresh_records"], "max_part_bytes": st["max_part_bytes"]},
             "roofline": roofline_of(stats, dominant, "c5", full),
@@ -517,10 +551,166 @@ def bench_c5(args):
             "kernels": kernel_table(full),
             "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
                             "HIP events only around the dominant kernel",
-        }), flush=True)
-    ctx.close()
+        }
+        if world > 1:
+            out["records"]["in_max_rank"] = tot_in
+            out["records"]["recv_bytes_rank0"] = st.get("recv_bytes")
+        out["kernels_top"] = dict(list(out["kernels"].items())[:10])
+        if emit:
+            print(json.dumps(out), flush=True)
+    del cur, prior_parts, prior_store
+    if own:
+        ctx.close()
+    return out
+
+
+def bench_c1(args, ctx):
+    """BASELINE.json configs[0] (C1), the reference's CPU-runnable case: 1M synthetic
+    subdomain lines written with the A1 chunk layout into 16 worker chunks (client/swarm:147-148
+    readlines keeps each '\n', server/server.py:447 joins them with '\n': a blank line between
+    records), the chunk outputs (identity module) merged in A5 key order (server/server.py:
+    403-410), sort -u, then the diff against the prior scan. Timed three ways on the same
+    bytes: the oracle (1 thread), GNU sort -u --parallel + comm -13 on the merged body, and
+    the drop-in completion hook (swarm_amd.hooks.completion_dedup_diff: key order, UTF-8
+    check, H2D, GPU dedup+diff, D2H — PCIe inclusive, host buffers in and out)."""
+    from swarm_amd import corpus, hooks
+    from oracle import semantics as S
+    n = args.c1_lines
+    sub, ids = corpus.subdomains(n, seed=1234)
+    prior = corpus.prior_of(ids).tobytes()
+    chunks = S.server_chunks(S.client_readlines(sub.tobytes()), max(1, n // 16))
+    objects = {"c1scan/output/chunk_%d.txt" % i: b for i, b in enumerate(chunks)}
+    # GPU: the hook, K timed calls after W warmups (host-buffer API)
+    for _ in range(max(1, args.warmup)):
+        gu, gf = hooks.completion_dedup_diff(objects, "c1scan", prior)
+    K = max(1, min(args.steps, 10))
+    t0 = time.perf_counter()
+    for _ in range(K):
+        gu, gf = hooks.completion_dedup_diff(objects, "c1scan", prior)
+    tg = (time.perf_counter() - t0) / K
+    out = {"value": round(n / tg, 1), "unit": "records/s", "ms_per_step": round(tg * 1e3, 3), "steps": K,
+           "config": {"workload": "C1: %dM subdomain lines, A1 layout in %d chunks, A5 merge, sort -u, diff vs the "
+                                  "prior scan (90 %% of the unique set)" % (n // 1_000_000, len(chunks)),
+                      "chunks": len(chunks), "merged_bytes": sum(len(b) for b in chunks), "prior_bytes": len(prior),
+                      "gpu_path": "swarm_amd.hooks.completion_dedup_diff (host buffers, PCIe inclusive)"},
+           "records": {"in": n, "unique": gu.count(b"\n"), "new": gf.count(b"\n")}}
+    if not args.no_cpu_baseline:
+        tc = time.perf_counter()
+        merged = S.merge_chunks(objects, "c1scan")
+        eu, ef = S.dedup_diff(merged, prior)
+        tc = time.perf_counter() - tc
+        out["cpu_baseline"] = {"value": round(n / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+                               "sample": "the whole C1 input: oracle A5 merge + sorted(set()) + set difference, "
+                                         "1 thread, %.2f s" % tc, "host_cpus": os.cpu_count(),
+                               "gpu_bit_exact": gu == eu and gf == ef}
+        if not args.no_gnu:
+            out["cpu_baseline"]["gnu_sort_comm"] = gnu_sort_comm(merged, prior, eu, ef, threads=host_cores())
+    return out
+
+
+def bench_c2(args, world, rank, dev, ctx):
+    """BASELINE.json configs[1] (C2): 10M synthetic subdomain lines per GPU + the prior scan
+    (90 % of the unique set), sort -u + diff, inputs resident in HBM. N > 1: WEAK scaling,
+    every rank brings 10M lines drawn from one global universe; records routed by byte range
+    (one partition, one all-to-all: dedup_diff_rounds_step with one round) or by hash."""
+    import numpy as np
+    import torch
+
+    from swarm_amd import corpus
+
+    n_lines = args.lines
+    cur_np, ids = corpus.subdomains(n_lines, seed=1234 + rank, universe=n_lines * world)
+    cur = torch.from_numpy(cur_np).to(dev)
+    prior_np = None
+    if world == 1:
+        prior_np = corpus.prior_of(ids)
+        prior = torch.from_numpy(prior_np).to(dev)
+    else:
+        from swarm_amd import distributed as D
+        u = np.unique(ids)
+        cand = torch.from_numpy(corpus._flatten(*corpus.render_names(u[(u % np.uint64(10)) != 0]))).to(dev)
+        if args.route == "range":
+            # splitters from every rank's prior record samples: rank r owns byte range r of the
+            # prior AND of every later scan, so the rank outputs concatenate into global order
+            gsplit = D.agree_splitters(ctx, [cand], world)
+            prior_parts, prior = D.build_prior_rounds(ctx, [cand], gsplit, 1)
+        else:
+            prior = D.build_prior_partition(ctx, cand)
+        del cand
+    torch.cuda.synchronize()
+    holder = {}
+
+    def run():
+        if world == 1:
+            r = ctx.dedup_diff(cur.data_ptr(), cur.numel(), prior.data_ptr(), prior.numel())
+            holder.update(R=int(r.in_records), U=int(r.uniq_records), F=int(r.fresh_records), Rp=int(r.prior_records),
+                          ub=int(r.uniq_bytes), fb=int(r.fresh_bytes))
+            return r
+        from swarm_amd import distributed as D
+        if args.route == "range":
+            u, f, st = D.dedup_diff_rounds_step(ctx, [cur], prior_parts, gsplit, 1)
+            holder.update(R=st["in_records"], U=st["uniq_records"], F=st["fresh_records"], Rp=None,
+                          ub=int(u.numel()), fb=int(f.numel()))
+            return None
+        r, recv = D.dedup_diff_step(ctx, cur, prior)
+        holder.update(R=int(r.in_records), U=int(r.uniq_records), F=int(r.fresh_records), Rp=int(r.prior_records),
+                      ub=int(r.uniq_bytes), fb=int(r.fresh_bytes))
+        return r
+    elapsed, full, stats, dominant, r = timed_steps(ctx, run, args, world)
+    ms_per_step = elapsed * 1e3 / args.steps
+    cur_bytes, prior_bytes = int(cur.numel()), int(prior.numel())
+    step_bytes = cur_bytes + prior_bytes + holder["ub"] + holder["fb"]
     if world > 1:
-        dist.destroy_process_group()
+        from swarm_amd import distributed as D
+        step_bytes = D.all_max_int(step_bytes) * world
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import semantics as S  # CPU baseline leg only
+        m = min(args.cpu_sample, n_lines)
+        if m < n_lines:
+            cut = int(np.flatnonzero(cur_np == 10)[m - 1]) + 1
+            cbytes = cur_np[:cut].tobytes()
+        else:
+            cbytes = cur_np.tobytes()
+        pbytes = prior_np.tobytes()
+        tc = time.perf_counter()
+        eu, ef = S.dedup_diff(cbytes, pbytes)
+        tc = time.perf_counter() - tc
+        cpu = {"value": round(m / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
+               "sample": "%d C2 lines + full prior (%d B); oracle sorted(set())+set difference, 1 thread, %.2f s"
+                         % (m, len(pbytes), tc),
+               "host_cpus": os.cpu_count()}
+        if m == n_lines:
+            cpu["gpu_output_bit_exact"] = (ctx.to_bytes(r.uniq, r.uniq_bytes) == eu and
+                                           ctx.to_bytes(r.fresh, r.fresh_bytes) == ef)
+            if not args.no_gnu:
+                cpu["gnu_sort_comm"] = gnu_sort_comm(cbytes, pbytes, eu, ef, threads=host_cores())
+    line = {
+        "metric": METRIC, "value": round(n_lines * world * args.steps / elapsed, 1), "unit": "records/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded subdomain corpus, SURVEY.md §8(d) C2)",
+        "config": {"workload": "C2: %dM-line subdomain merge + sort -u dedup + new-record diff per GPU"
+                               % (n_lines // 1_000_000),
+                   "lines_per_gpu": n_lines, "bytes_per_gpu": cur_bytes, "prior_bytes": prior_bytes,
+                   "unique_frac": round(holder["U"] / max(holder["R"], 1), 4),
+                   "parallelism": ("%s all-to-all x%d (backend %s)" % (
+                       "byte-range (global byte order)" if args.route == "range" else "hash-partition", world,
+                       args.dist_backend)) if world > 1 else "single GPU"},
+        "gbps": round(step_bytes * args.steps / elapsed / 1e9, 2),
+        "hbm_frac_step": round(step_bytes * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world), 4),
+        "records": {"in": holder["R"], "unique": holder["U"], "new": holder["F"], "prior": holder["Rp"]},
+        "roofline": roofline_of(stats, dominant, "c2", full),
+        "cpu_baseline": cpu,
+        "gpu_kernel_ms_per_step": round(sum(v[1] for v in full.values()), 4),
+        "kernels": kernel_table(full),
+        "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
+                        "HIP events only around the dominant kernel",
+        "dedup_path": ctx.last_path()[0],
+    }
+    line["kernels_top"] = dict(list(line["kernels"].items())[:10])
+    del cur, prior, r
+    return line
 
 
 def host_cores() -> int:
@@ -798,6 +988,7 @@ def bench_urls(args, ctx=None, emit=True):
         "config": {"workload": "URLs: %dM httpx -silent URLs sort -u + new-record diff, 1 GPU" % (n_lines // 1_000_000),
                    "bytes": int(cur.numel()), "prior_bytes": int(prior.numel())},
         "gbps": round(step_bytes * args.steps / el / 1e9, 2),
+        "hbm_frac_step": round(step_bytes * args.steps / el / 1e9 / HBM_PEAK_GBS, 4),
         "records": {"in": R, "unique": int(r.uniq_records), "new": int(r.fresh_records)},
         "roofline": roofline_of(stats, dominant, "urls", full),
         "cpu_baseline": cpu,
@@ -907,9 +1098,29 @@ def launcher_check(args):
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "records/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
-                          "launcher_check": True}), flush=True)
+                          "launcher_check": True, "workload": args.workload,
+                          "world_size_seen": dist.get_world_size() if world > 1 else 1}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def init_dist(args):
+    """(world, rank, local, device): one process per GPU; the process group (RCCL = "nccl",
+    or gloo rehearsals) is initialised when world > 1 and must match --gpus."""
+    import torch
+    import torch.distributed as dist
+    world, rank, local = dist_setup(args)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        local = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        dist.init_process_group(args.dist_backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit("bench.py: the process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
+        world = dist.get_world_size()
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local, torch.device("cuda", local)
 
 
 def main():
@@ -917,11 +1128,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--lines", type=int, default=10_000_000)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "fields", "x1", "urls"], default="c2")
+    ap.add_argument("--lines", type=int, default=10_000_000, help="C2 / URL lines per GPU")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "fields", "x1", "urls"], default=None,
+                    help="default: c2 (+ every other config as sub-objects) at --gpus 1, c5 strong scaling at N > 1")
     ap.add_argument("--x1-lines", type=int, default=10_000_000, help="X1 fused-step input lines")
+    ap.add_argument("--c1-lines", type=int, default=1_000_000, help="C1 lines")
+    ap.add_argument("--c3-lines", type=int, default=50_000_000, help="C3 lines")
+    ap.add_argument("--c4-lines", type=int, default=12_500_000, help="C4 banners per GPU")
+    ap.add_argument("--c5-records", type=int, default=1_000_000_000, help="C5 records in total (all ranks)")
+    ap.add_argument("--fields-lines", type=int, default=4_000_000, help="fields leg httpx -json lines")
     ap.add_argument("--gnu-lines", type=int, default=2_000_000, help="lines of the GNU-tool CPU baseline sample")
     ap.add_argument("--no-x1", action="store_true", help="default run: skip the fused X1 and URL legs")
+    ap.add_argument("--no-sub", action="store_true", help="default run: headline only (no c1/c3/c5/x1/urls legs)")
+    ap.add_argument("--no-c2-weak", action="store_true", help="N > 1 c5 run: skip the C2 weak-scaling sub-object")
     ap.add_argument("--c5-hosts", type=int, default=64_000_000, help="C5 hosts (x 4 open-port slots = combos)")
     ap.add_argument("--c5-data", choices=["hosts", "ips"], default="hosts",
                     help="C5 records: host:port names, or 10.x.y.z:port (15M hosts x 16 port slots)")
@@ -930,21 +1149,23 @@ def main():
     ap.add_argument("--route", choices=["range", "hash"], default="range",
                     help="C2 N>1 record routing: byte ranges (outputs in global byte order) or hash parts")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gnu", action="store_true", help="skip the GNU coreutils/grep baselines")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--launcher-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.workload is None:
+        args.workload = "c2" if args.gpus == 1 else "c5"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args, sys.argv[1:])
     if args.launcher_check:
         return launcher_check(args)
     if args.workload == "c3":
-        return bench_c3(args)
+        bench_c3(args)
+        return 0
     if args.workload == "c4":
         return bench_c4(args)
     if args.workload == "fields":
         return bench_fields(args)
-    if args.workload == "c5":
-        return bench_c5(args)
     if args.workload == "x1":
         bench_x1(args)
         return 0
@@ -952,183 +1173,53 @@ def main():
         bench_urls(args)
         return 0
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
-    world, rank, local = dist_setup(args)
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        local = local % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.dist_backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
-
     import swarm_amd
-    from swarm_amd import corpus
 
-    n_lines = args.lines
-    cur_np, ids = corpus.subdomains(n_lines, seed=1234 + rank, universe=n_lines * world)
-    cur = torch.from_numpy(cur_np).to(dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    ctx = swarm_amd.Context(local, stream)
+    world, rank, local, dev = init_dist(args)
+    ctx = swarm_amd.Context(local, torch.cuda.current_stream(dev).cuda_stream)
 
-    if world == 1:
-        prior_np = corpus.prior_of(ids)
-        prior = torch.from_numpy(prior_np).to(dev)
-    else:
-        from swarm_amd import distributed as D
-        u = np.unique(ids)
-        cand = torch.from_numpy(corpus._flatten(*corpus.render_names(u[(u % np.uint64(10)) != 0]))).to(dev)
-        if args.route == "range":
-            # splitters from every rank's prior record samples: rank r owns byte range r of the
-            # prior AND of every later scan, so the rank outputs concatenate into global order
-            gsplit = D.agree_splitters(ctx, [cand], world)
-            prior = D.build_prior_range(ctx, cand, gsplit)
-        else:
-            prior = D.build_prior_partition(ctx, cand)
-        del cand
-        prior_np = None
-    torch.cuda.synchronize()
-
-    def step():
-        if world == 1:
-            return ctx.dedup_diff(cur.data_ptr(), cur.numel(), prior.data_ptr(), prior.numel()), cur.numel()
-        from swarm_amd import distributed as D
-        if args.route == "range":
-            r, recv = D.dedup_diff_range_shard(ctx, cur, prior, gsplit)
-        else:
-            r, recv = D.dedup_diff_step(ctx, cur, prior)
-        return r, recv.numel()
-
-    for _ in range(args.warmup):
-        r, nrecv = step()
-    torch.cuda.synchronize()
-
-    # one fully profiled step (untimed): per-kernel breakdown, and the dominant kernel
-    ctx.reset_stats()
-    ctx.profile(True)
-    step()
-    torch.cuda.synchronize()
-    ctx.profile(False)
-    full = ctx.kernel_stats()
-    dominant = max(full.items(), key=lambda kv: kv[1][1])[0] if full else None
-    if world > 1:
-        names = [None] * world
-        dist.all_gather_object(names, dominant)
-        dominant = names[0]
-
-    # timed region: HIP events only around the dominant kernel's launches (on its stream)
-    ctx.reset_stats()
-    ctx.profile(True, only=dominant)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        r, nrecv = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    ctx.profile(False)
-    elapsed = t1 - t0
-    stats = ctx.kernel_stats()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    total_records = n_lines * world * args.steps
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = total_records / elapsed
-
-    # algorithmic bytes of the whole step (this rank): cur + prior + outputs
-    cur_bytes, prior_bytes = int(cur.numel()), int(prior.numel())
-    step_bytes = cur_bytes + prior_bytes + r.uniq_bytes + r.fresh_bytes
-    info = {"R": int(r.in_records), "n": int(nrecv), "Rp": int(r.prior_records), "n_prior": int(prior.numel()),
-            "U": int(r.uniq_records), "ub": int(r.uniq_bytes), "F": int(r.fresh_records), "fb": int(r.fresh_bytes)}
-
-    roofline = roofline_of(stats, dominant, "c2", full)
-    kernels = kernel_table(full)
-    gpu_ms_sum = sum(v[1] for v in full.values())
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import semantics as S  # CPU baseline leg only
-        m = min(args.cpu_sample, n_lines)
-        if m < n_lines:
-            cut = int(np.flatnonzero(cur_np == 10)[m - 1]) + 1
-            cbytes = cur_np[:cut].tobytes()
-        else:
-            cbytes = cur_np.tobytes()
-        pbytes = prior_np.tobytes()
-        tc = time.perf_counter()
-        eu, ef = S.dedup_diff(cbytes, pbytes)
-        tc = time.perf_counter() - tc
-        cpu = {"value": round(m / tc, 1), "unit": "records/s", "cores": 1, "kind": "port",
-               "sample": "%d C2 lines + full prior (%d B); oracle sorted(set())+set difference, 1 thread, %.2f s"
-                         % (m, len(pbytes), tc),
-               "host_cpus": os.cpu_count()}
-        if m == n_lines:
-            u_gpu = ctx.to_bytes(r.uniq, r.uniq_bytes)
-            f_gpu = ctx.to_bytes(r.fresh, r.fresh_bytes)
-            cpu["gpu_output_bit_exact"] = (u_gpu == eu and f_gpu == ef)
-            cpu["gnu_sort_comm"] = gnu_sort_comm(cbytes, pbytes, eu, ef, threads=host_cores())
-
-    c2_path = ctx.last_path()[0]
-    urls = None
-    if rank == 0 and world == 1 and not args.no_x1:
-        # the same dedup+diff on URL records (one shared 8-byte prefix), reported beside C2
-        del cur, prior
+    if args.workload == "c5":
+        line = bench_c5(args, world, rank, dev, ctx, emit=False)
         torch.cuda.empty_cache()
-        u_full = bench_urls(args, ctx=ctx, emit=False)
-        urls = {k: u_full[k] for k in ("value", "ms_per_step", "ns_per_record", "config", "gbps", "records",
-                                       "roofline", "cpu_baseline", "dedup_path")}
-        urls["ns_per_record_vs_c2"] = round(u_full["ns_per_record"] / (ms_per_step * 1e6 / n_lines), 3)
+        if world > 1 and not args.no_c2_weak:
+            # the C2 weak-scaling step beside C5's strong scaling (every rank runs it)
+            c2 = bench_c2(args, world, rank, dev, ctx)
+            if rank == 0:
+                line["c2_weak"] = {k: c2[k] for k in SUB_KEYS if k in c2}
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        ctx.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
 
-    x1 = None
-    if rank == 0 and world == 1 and not args.no_x1:
-        # the metric's fused step (match+dedup+diff) in the same run, reported beside C2
-        torch.cuda.empty_cache()
-        x1_full = bench_x1(args, ctx=ctx, emit=False)
-        x1 = {k: x1_full[k] for k in ("value", "unit", "ms_per_step", "config", "gbps", "hbm_frac_step", "records",
-                                 "roofline", "cpu_baseline", "dedup_path")}
-        x1["kernels_top"] = dict(list(x1_full["kernels"].items())[:10])
-
+    # c2: the headline (configs[1]); at N = 1 every other config rides along as a sub-object
+    line = bench_c2(args, world, rank, dev, ctx)
+    torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_sub:
+        if not args.no_x1:
+            u_full = sub_leg("urls", lambda: bench_urls(args, ctx=ctx, emit=False))
+            if "ns_per_record" in u_full:
+                u_full["ns_per_record_vs_c2"] = round(u_full["ns_per_record"] / (line["ms_per_step"] * 1e6 /
+                                                                                 args.lines), 3)
+            line["urls"] = {k: u_full[k] for k in SUB_KEYS + ("ns_per_record", "ns_per_record_vs_c2", "error")
+                            if k in u_full}
+            x1 = sub_leg("x1", lambda: bench_x1(args, ctx=ctx, emit=False))
+            if "kernels" in x1:
+                x1["kernels_top"] = dict(list(x1["kernels"].items())[:10])
+            line["fused_x1"] = {k: x1[k] for k in SUB_KEYS + ("error",) if k in x1}
+        line["c1"] = sub_leg("c1", lambda: bench_c1(args, ctx))
+        line["c3"] = sub_leg("c3", lambda: bench_c3(args, ctx=ctx, emit=False), SUB_KEYS + ("error",))
+        line["c5"] = sub_leg("c5", lambda: bench_c5(args, 1, 0, dev, ctx, emit=False), SUB_KEYS + ("error",))
     if rank == 0:
-        line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "records/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (seeded subdomain corpus, SURVEY.md §8(d) C2)",
-            "config": {"workload": "C2: %dM-line subdomain merge + sort -u dedup + new-record diff per GPU"
-                                   % (n_lines // 1_000_000),
-                       "lines_per_gpu": n_lines, "bytes_per_gpu": cur_bytes,
-                       "prior_bytes": prior_bytes,
-                       "unique_frac": round(info["U"] / max(info["R"], 1), 4),
-                       "parallelism": ("%s all-to-all x%d" % ("byte-range (global byte order)" if args.route == "range"
-                                                              else "hash-partition", world))
-                                      if world > 1 else "single GPU"},
-            "gbps": round(step_bytes * world * args.steps / elapsed / 1e9, 2),
-            "hbm_frac_step": round(step_bytes * world * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 4),
-            "records": {"in": info["R"], "unique": info["U"], "new": info["F"], "prior": info["Rp"]},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "gpu_kernel_ms_per_step": round(gpu_ms_sum, 4),
-            "kernels": kernels,
-            "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
-                            "HIP events only around the dominant kernel",
-            "dedup_path": c2_path,
-            "fused_x1": x1,
-            "urls": urls,
-        }
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

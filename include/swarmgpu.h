@@ -199,6 +199,20 @@ int sg_dev_partition_bytes_pieces_spans(sg_ctx *ctx, const uint8_t *const *d_pie
                                         size_t k, const uint8_t *splitters, const uint32_t *split_offs,
                                         uint32_t n_parts, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
                                         uint64_t *part_records, const uint32_t **d_spans, const uint64_t **d_keys);
+/* Range routing for a multi-GPU exchange in rounds (swarm_amd.distributed.dedup_diff_rounds_step):
+ * n_parts = G x rounds byte-range parts, part q = g * rounds + p being local range p of rank g
+ * (so rank g owns parts g * rounds .. g * rounds + rounds - 1, in byte order). The parts are
+ * laid out ROUND-major in d_out: round p = parts (0, p), (1, p), ..., (G - 1, p) back to back,
+ * each round starting at a 16-byte aligned offset, so one round is one contiguous
+ * all-to-all send buffer whose split sizes are part_bytes[g * rounds + p]; the receiver's
+ * buffer for round p is then its local range p, whole. Capacity >= the pieces' bytes + 1 each
+ * + 16 per round. part_bytes / part_records in part order. Replaces the per-piece routing +
+ * exchange + local re-routing of the round-2 path (server/server.py:185-187's chunk
+ * parallelism, across GPUs). */
+int sg_dev_partition_bytes_pieces_rounds(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                         const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
+                                         uint32_t rounds, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
+                                         uint64_t *part_records);
 /* m evenly spaced records' first SG_SPLIT_BYTES bytes (heads: m x SG_SPLIT_BYTES host bytes,
  * zero-filled) and min(len, SG_SPLIT_BYTES) (lens), for choosing byte splitters; nothing is
  * written when the buffer has no records; *n_rec = the buffer's record count. */

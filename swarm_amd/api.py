@@ -16,6 +16,7 @@ uint8 arrays; outputs are bytes.
 from __future__ import annotations
 
 import ctypes as C
+import threading
 from typing import List, Sequence, Tuple
 
 import numpy as np
@@ -33,6 +34,20 @@ def part_offsets(part_bytes: Sequence[int], align16: bool = False) -> List[int]:
         off += n
         if align16:
             off = (off + 15) & ~15
+    return out
+
+
+def round_offsets(part_bytes: Sequence[int], rounds: int) -> List[int]:
+    """Start offset of every round in a partition_bytes_pieces_rounds output (G x rounds parts,
+    part q = g * rounds + p; round p = parts (0, p) .. (G - 1, p) back to back, each round at
+    the 16-byte aligned offset after the previous one). rounds + 1 entries (the last = end)."""
+    G = len(part_bytes) // rounds
+    out, off = [], 0
+    for p in range(rounds):
+        off = (off + 15) & ~15
+        out.append(off)
+        off += sum(part_bytes[g * rounds + p] for g in range(G))
+    out.append(off)
     return out
 
 
@@ -255,18 +270,25 @@ def device_count() -> int:
 
 
 SPLIT_BYTES = 64  # include/swarmgpu.h SG_SPLIT_BYTES
-_SHARED = {}
+_TLS = threading.local()
 
 
 def _shared_ctx():
-    """A per-thread context on the current torch device (host helpers that stage through
-    torch tensors)."""
-    import threading
+    """A per-thread context on torch's current device and stream (host helpers that stage
+    through torch tensors). Held in thread-local storage: when a (short-lived request)
+    thread ends, its contexts are released with it (Context.__del__ frees the HBM
+    workspaces); a thread that switches streams gets a context on the new stream."""
     import torch
-    key = (threading.get_ident(), torch.cuda.current_device())
-    c = _SHARED.get(key)
+    dev = torch.cuda.current_device()
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    pool = getattr(_TLS, "ctx", None)
+    if pool is None:
+        pool = _TLS.ctx = {}
+    c = pool.get(key)
     if c is None:
-        c = _SHARED[key] = Context(key[1], torch.cuda.current_stream().cuda_stream)
+        for k in [k for k in pool if k[0] == dev]:  # one context per device per thread
+            pool.pop(k).close()
+        c = pool[key] = Context(dev, key[1])
     return c
 
 
@@ -282,6 +304,12 @@ class Context:
         check(lib.sg_ctx_create(device, s, C.byref(self._h)))
         self.device = device
         self.stream = stream
+
+    @property
+    def torch_device(self):
+        """The context's device as a torch.device (where buffers for its calls are allocated)."""
+        import torch
+        return torch.device("cuda", self.device)
 
     def on_torch_stream(self) -> bool:
         """True when the context's kernels run on torch's current stream of its device, so
@@ -419,6 +447,23 @@ class Context:
         fn = lib.sg_dev_partition_bytes_pieces_a16 if align16 else lib.sg_dev_partition_bytes_pieces
         check(fn(self._h, ptrs, lens, k, blob.ctypes.data, offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts,
                  C.c_void_p(d_out) if d_out else None, out_cap, pb, pr))
+        return list(pb), list(pr)
+
+    def partition_bytes_pieces_rounds(self, pieces: Sequence[Tuple[int, int]], splitters: Sequence[bytes], rounds: int,
+                                      d_out: int, out_cap: int):
+        """Route pieces into G x rounds byte-range parts laid out round-major (include/swarmgpu.h
+        sg_dev_partition_bytes_pieces_rounds; round_offsets gives each round's start). Returns
+        (bytes per part, records per part) in part order."""
+        blob, offs = _keys_blob(list(splitters))
+        parts = len(splitters) + 1
+        k = len(pieces)
+        ptrs = (C.c_void_p * max(1, k))(*[C.c_void_p(p) for p, _ in pieces])
+        lens = (C.c_size_t * max(1, k))(*[n for _, n in pieces])
+        pb = (C.c_uint64 * parts)()
+        pr = (C.c_uint64 * parts)()
+        check(lib.sg_dev_partition_bytes_pieces_rounds(self._h, ptrs, lens, k, blob.ctypes.data,
+                                                       offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts, rounds,
+                                                       C.c_void_p(d_out) if d_out else None, out_cap, pb, pr))
         return list(pb), list(pr)
 
     def partition_bytes_pieces_spans(self, pieces: Sequence[Tuple[int, int]], splitters: Sequence[bytes], d_out: int,

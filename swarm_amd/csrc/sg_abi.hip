@@ -705,15 +705,23 @@ int sg_dev_partition_bytes(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint
 
 // a16: part q starts at the 16-byte aligned offset after part q - 1 (parts usable in place
 // by the dedup, which takes 16-byte aligned buffers).
+// rounds > 1 (multi-GPU exchange rounds): n_parts = G x rounds, part q = g * rounds + p is
+// range p of rank g, and the parts are laid out round-major: round p's parts (0, p), (1, p),
+// ..., (G - 1, p) back to back (one contiguous all-to-all send buffer per round), each round
+// starting at a 16-byte aligned offset.
 static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
                             const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out,
                             size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, bool a16,
-                            const uint2 **sp_out = nullptr, const uint64_t **k_out = nullptr) {
+                            const uint2 **sp_out = nullptr, const uint64_t **k_out = nullptr, uint32_t rounds = 1) {
     if (!c || (k && (!d_pieces || !lens)) || ((!splitters || !split_offs) && n_parts > 1)) {
         set_error("sg_dev_partition_bytes_pieces: bad arguments");
         return SG_E_INVAL;
     }
     if (n_parts == 0 || n_parts > 256) { set_error("n_parts must be in 1..256"); return SG_E_INVAL; }
+    if (rounds == 0 || n_parts % rounds || (rounds > 1 && sp_out)) {
+        set_error("n_parts (%u) must be a multiple of rounds (%u)", n_parts, rounds);
+        return SG_E_INVAL;
+    }
     uint64_t total_in = 0;
     for (size_t j = 0; j < k; ++j) {
         if (!d_pieces[j] && lens[j]) { set_error("piece %zu is NULL", j); return SG_E_INVAL; }
@@ -770,29 +778,37 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
     std::vector<uint64_t> h(std::max<size_t>(k, 1) * 512, 0);
     SG_TRY(ctx_readback(c, h.data(), cnt, h.size() * 8));
     // destinations: part p = pieces' part-p records in piece order
-    std::vector<uint64_t> pbase(n_parts + 1, 0), prec(n_parts, 0);
-    for (uint32_t q = 0; q < n_parts; ++q) {
-        uint64_t bq = 0, rq = 0;
-        for (size_t j = 0; j < k; ++j) { rq += h[512 * j + q]; bq += h[512 * j + n_parts + q]; }
-        pbase[q + 1] = pbase[q] + bq;
-        if (a16 && q + 1 < n_parts) pbase[q + 1] = (pbase[q + 1] + 15) & ~15ull;
-        prec[q] = rq;
+    std::vector<uint64_t> pbase(n_parts, 0), pbytes(n_parts, 0), prec(n_parts, 0);
+    for (uint32_t q = 0; q < n_parts; ++q)
+        for (size_t j = 0; j < k; ++j) { prec[q] += h[512 * j + q]; pbytes[q] += h[512 * j + n_parts + q]; }
+    uint64_t end = 0;
+    if (rounds > 1) {
+        const uint32_t G = n_parts / rounds;
+        for (uint32_t p = 0; p < rounds; ++p) {
+            end = (end + 15) & ~15ull;
+            for (uint32_t g = 0; g < G; ++g) {
+                pbase[g * rounds + p] = end;
+                end += pbytes[g * rounds + p];
+            }
+        }
+    } else {
+        for (uint32_t q = 0; q < n_parts; ++q) {
+            pbase[q] = end;
+            end += pbytes[q];
+            if (a16 && q + 1 < n_parts) end = (end + 15) & ~15ull;
+        }
     }
-    if (pbase[n_parts] > out_cap) {
-        set_error("output capacity %zu < %llu", out_cap, (unsigned long long)pbase[n_parts]);
+    if (end > out_cap) {
+        set_error("output capacity %zu < %llu", out_cap, (unsigned long long)end);
         return SG_E_CAP;
     }
     for (uint32_t q = 0; q < n_parts; ++q) {
-        if (part_bytes) {
-            uint64_t bq = 0;
-            for (size_t j = 0; j < k; ++j) bq += h[512 * j + n_parts + q];
-            part_bytes[q] = bq;
-        }
+        if (part_bytes) part_bytes[q] = pbytes[q];
         if (part_records) part_records[q] = prec[q];
     }
     // pass 2: per piece, the multi-split: per-tile part byte counts, their scan, then every
     // record copied straight to its part's place (k_part_apply)
-    std::vector<uint64_t> acc(pbase.begin(), pbase.end() - 1);
+    std::vector<uint64_t> acc(pbase);
     std::vector<uint64_t> pb_all((size_t)k * n_parts, 0);
     for (size_t j = 0; j < k; ++j) {
         for (uint32_t q = 0; q < n_parts; ++q) {
@@ -822,7 +838,7 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
     }
     uint64_t *d_pb;
     SG_TRY(slot(c, S_PT_BASE, pb_all.size(), &d_pb));
-    SG_HIP(hipMemcpy(d_pb, pb_all.data(), pb_all.size() * 8, hipMemcpyHostToDevice));
+    SG_TRY(ctx_upload(c, d_pb, pb_all.data(), pb_all.size() * 8));
     const uint64_t *d_rb = d_pb + (size_t)k * n_parts, *d_pstart = d_pb + 2 * (size_t)k * n_parts;
     for (size_t j = 0; j < k; ++j) {
         if (!lens[j]) continue;
@@ -909,6 +925,14 @@ int sg_dev_partition_bytes_pieces_spans(sg_ctx *c, const uint8_t *const *d_piece
                             part_records, true, &sp, d_keys));
     *d_spans = reinterpret_cast<const uint32_t *>(sp);
     return SG_OK;
+}
+
+int sg_dev_partition_bytes_pieces_rounds(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                         const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
+                                         uint32_t rounds, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
+                                         uint64_t *part_records) {
+    return partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
+                            part_records, false, nullptr, nullptr, rounds);
 }
 
 int sg_dev_dedup_diff_spans_into(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, const uint32_t *d_spans,

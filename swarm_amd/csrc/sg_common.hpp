@@ -103,6 +103,11 @@ struct sg_ctx {
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
     uint64_t pt_keep_recs = 0;  // piece partition: records the last call kept between its passes
+    // pinned staging for host-to-device uploads on the context stream (ctx_upload): grown on
+    // demand; up_ev marks the last upload's copy so the buffer is not rewritten under it
+    void *up_pin = nullptr;
+    size_t up_cap = 0;
+    hipEvent_t up_ev = nullptr;
     // profiling
     bool profile = false;
     std::string prof_only;  // non-empty: time only launches with this name
@@ -130,6 +135,9 @@ inline uint64_t slot_elems(const sg_ctx *c, int s) {
     return c->slot_cap[s] > 64 ? (c->slot_cap[s] - 64) / sizeof(T) : 0;
 }
 int ctx_readback(sg_ctx *c, void *host, const void *dev, size_t bytes);  // sync on stream
+// Async host-to-device copy on the context stream through pinned staging: the host bytes
+// may be reused as soon as it returns, and nothing waits on the device (or the null stream).
+int ctx_upload(sg_ctx *c, void *dev, const void *host, size_t bytes);
 int ctx_harvest(sg_ctx *c);
 int prof_begin(sg_ctx *c, const char *name, int *stat, hipEvent_t *a);
 void prof_end(sg_ctx *c, int stat, hipEvent_t a);

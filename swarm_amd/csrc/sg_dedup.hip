@@ -1261,7 +1261,7 @@ static int refine_big_groups(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans
             kbits = (int)(7 * sbits + 4);
             joint = kbits + gbits <= 64;
             uint8_t *drank = reinterpret_cast<uint8_t *>(amask + 8);
-            SG_HIP(hipMemcpy(drank, rank, 256, hipMemcpyHostToDevice));  // from the stack: complete before reuse
+            SG_TRY(ctx_upload(c, drank, rank, 256));  // staged: the stack copy may go
             SG_LAUNCH(c, "round_alpha", k_alpha_pack, std::min<uint32_t>(grid_for(M, 256), 2048u), 256, 0, RK, M, drank,
                       sbits, joint ? RG : (const uint32_t *)nullptr, (uint32_t)kbits);
         }
@@ -1832,6 +1832,9 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         res->fresh_records = res->uniq_records;
         if (of && res->fresh_bytes) {  // caller outputs: the new records are all of them, copied
             SG_HIP(hipMemcpyAsync(of->p, res->uniq, res->fresh_bytes, hipMemcpyDeviceToDevice, c->stream));
+            // every other route returns after a host sync: the caller may hand the buffer
+            // to another stream (or free it) as soon as this returns
+            SG_HIP(hipStreamSynchronize(c->stream));
             res->fresh = of->p;
         } else if (of) {
             res->fresh = of->p;

@@ -6,6 +6,8 @@
 
 #include <string.h>
 
+#include <algorithm>
+
 namespace sg {
 
 static thread_local std::string g_err;
@@ -50,6 +52,28 @@ int ctx_readback(sg_ctx *c, void *host, const void *dev, size_t bytes) {
     SG_HIP(hipMemcpyAsync(c->pinned, dev, bytes, hipMemcpyDeviceToHost, c->stream));
     SG_HIP(hipStreamSynchronize(c->stream));
     memcpy(host, c->pinned, bytes);
+    return SG_OK;
+}
+
+int ctx_upload(sg_ctx *c, void *dev, const void *host, size_t bytes) {
+    if (!bytes) return SG_OK;
+    if (c->up_ev) SG_HIP(hipEventSynchronize(c->up_ev));  // the previous upload has left the buffer
+    if (bytes > c->up_cap) {
+        if (c->up_pin) (void)hipHostFree(c->up_pin);
+        c->up_pin = nullptr;
+        c->up_cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 2, 64 << 10);
+        if (hipHostMalloc(&c->up_pin, want, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("hipHostMalloc(%zu) failed for upload staging", want);
+            return SG_E_NOMEM;
+        }
+        c->up_cap = want;
+    }
+    if (!c->up_ev) SG_HIP(hipEventCreateWithFlags(&c->up_ev, hipEventDisableTiming));
+    memcpy(c->up_pin, host, bytes);
+    SG_HIP(hipMemcpyAsync(dev, c->up_pin, bytes, hipMemcpyHostToDevice, c->stream));
+    SG_HIP(hipEventRecord(c->up_ev, c->stream));
     return SG_OK;
 }
 
@@ -194,6 +218,8 @@ int sg_ctx_destroy(sg_ctx *c) {
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->free_events) (void)hipEventDestroy(e);
     if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->up_pin) (void)hipHostFree(c->up_pin);
+    if (c->up_ev) (void)hipEventDestroy(c->up_ev);
     if (c->owns_stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return SG_OK;

@@ -1,24 +1,27 @@
 """Multi-GPU dedup+diff: one process per GPU, torch.distributed with the
-"nccl" backend (RCCL over xGMI on ROCm).
+"nccl" backend (RCCL over xGMI on ROCm). The reference's only parallelism is chunked data
+parallelism (server/server.py:185-187 splits the target list, :414-461 queues the chunks);
+here the records themselves are sharded, by byte range, so the global sort -u survives.
 
-Per step and rank:
-  1. sg_dev_partition routes each record of the rank's shard to part(hash64(record), G),
-     grouped by destination, '\\n'-terminated (the wire format IS the line format, so the
-     received buffer feeds dedup directly);
-  2. all_to_all_single of the G byte counts, then one all_to_all_single of the records —
-     every peer pair on its own xGMI link;
-  3. local sort -u + diff against the rank's partition of the prior scan (partitioned by
-     the same hash once, and kept resident).
-The union of the ranks' outputs is the global result; rank r owns the records that hash
-to r. (A byte-ordered global file is a k-way merge of the G sorted outputs, done where the
-file is written, outside this path.)
+C5 step on every rank (dedup_diff_rounds_step, BASELINE configs[4]):
+  1. ONE partition call routes all of the rank's pieces into world x R byte ranges (byte
+     splitters agreed across ranks at setup) laid out round-major: round p = range p of
+     rank 0, of rank 1, ... back to back (sg_dev_partition_bytes_pieces_rounds);
+  2. ONE all-to-all of the world x R part sizes (host ints);
+  3. R all-to-alls of bytes queued at once on RCCL's stream, straight from the partition
+     output; round p's receive buffer IS the rank's local range p;
+  4. part p is deduped and diffed against the rank's stored prior part p as soon as round p
+     has arrived (work.wait() orders the compute stream after it), while rounds p+1.. are
+     still on the xGMI links: the exchange hides behind the dedup.
+Rank r ends with byte range r, so the ranks' outputs concatenated in rank order are the
+global sort -u / comm -13 output: no merge exists because none is needed.
 
-Range routing (sg_dev_partition_bytes with byte splitters agreed across ranks) keeps the
-global byte order instead: rank r owns key range r, so the ranks' outputs concatenated in rank order
-are the global sort -u output with no merge. The bench's C2 multi-GPU step uses it
-(dedup_diff_range_shard); the C5 path (1B host:port records, shards larger than one 4 GiB
-call) adds local range parts of < 4 GiB per rank (swarm_amd.sharded). Matching (match_step)
-needs no record exchange: replicated automata, contiguous input shards, summed counts.
+The gloo backend (CPU tests, several ranks rehearsing on one GPU) runs the same code; only
+the transport differs (host staging in all_to_all_bytes / exchange_counts).
+
+Also here: hash routing (sg_dev_partition by hash64, dedup_diff_step) and the single-call C2
+shard path (dedup_diff_range_shard); matching (match_step) needs no record exchange:
+replicated automata, contiguous input shards, summed counts.
 """
 from __future__ import annotations
 
@@ -28,24 +31,64 @@ import torch
 import torch.distributed as dist
 
 
+def host_staged(group=None) -> bool:
+    """gloo rehearsals (several ranks sharing one GPU, or CPU tests): the collectives take host
+    tensors. This is the only place the gloo and nccl (RCCL) paths differ: the transport."""
+    return dist.get_backend(group) == "gloo"
+
+
+def _coll_device(group=None):
+    return torch.device("cpu") if host_staged(group) else torch.device("cuda", torch.cuda.current_device())
+
+
+def all_max_float(x: float, group=None) -> float:
+    """max over ranks of a host float (the bench's elapsed time)."""
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_coll_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def all_max_int(x: int, group=None) -> int:
+    t = torch.tensor([int(x)], dtype=torch.int64, device=_coll_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def exchange_counts(counts: Sequence[int], group=None) -> List[int]:
+    """All-to-all of host integers: `counts` holds world x m values (m for each peer, in rank
+    order); returns the world x m values the peers sent to this rank (source-rank order)."""
+    t = torch.tensor([int(x) for x in counts], dtype=torch.int64, device=_coll_device(group))
+    o = torch.empty_like(t)
+    dist.all_to_all_single(o, t, group=group)
+    return [int(x) for x in o.tolist()]
+
+
+def all_to_all_bytes(recv: torch.Tensor, send: torch.Tensor, out_splits: Sequence[int], in_splits: Sequence[int],
+                     group=None, async_op: bool = False):
+    """One all_to_all_single of byte buffers with host split sizes (sum(in_splits) ==
+    send.numel(), sum(out_splits) == recv.numel()). RCCL: straight between the device
+    buffers, optionally async (the returned work's wait() orders the caller's stream after
+    it). gloo with device buffers: staged through host copies, synchronously (returns None)."""
+    out_splits, in_splits = [int(x) for x in out_splits], [int(x) for x in in_splits]
+    if host_staged(group) and (send.is_cuda or recv.is_cuda):
+        h = torch.empty(recv.numel(), dtype=torch.uint8)
+        dist.all_to_all_single(h, send.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                               group=group)
+        recv.copy_(h)
+        return None
+    return dist.all_to_all_single(recv, send, output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                  group=group, async_op=async_op)
+
+
 def exchange_records(send: torch.Tensor, part_bytes: Sequence[int], group=None) -> torch.Tensor:
     """All-to-all of a partitioned byte buffer: `send` holds part 0's bytes, then part 1's,
     ... (part_bytes[i] each). Returns the bytes all ranks sent to this rank, in rank order."""
     world = dist.get_world_size(group)
     if len(part_bytes) != world:
         raise ValueError("part_bytes has %d entries for world size %d" % (len(part_bytes), world))
-    if send.is_cuda and dist.get_backend(group) == "gloo":
-        # rehearsal mode (several ranks sharing one GPU): the collective runs on host copies
-        return exchange_records(send.cpu(), part_bytes, group).to(send.device)
-    dev = send.device
-    in_splits = torch.tensor(list(part_bytes), dtype=torch.int64, device=dev)
-    out_splits = torch.empty_like(in_splits)
-    dist.all_to_all_single(out_splits, in_splits, group=group)
-    out_list: List[int] = [int(x) for x in out_splits.tolist()]
-    total_in = int(sum(part_bytes))
-    recv = torch.empty(sum(out_list), dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(recv, send[:total_in], output_split_sizes=out_list,
-                           input_split_sizes=[int(x) for x in part_bytes], group=group)
+    out_list = exchange_counts(part_bytes, group)
+    recv = torch.empty(sum(out_list), dtype=torch.uint8, device=send.device)
+    all_to_all_bytes(recv, send[: int(sum(part_bytes))], out_list, part_bytes, group)
     return recv
 
 
@@ -103,11 +146,10 @@ def range_exchange(ctx, pieces: Sequence[torch.Tensor], gsplit, group=None, piec
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world == 1:
         return [q for p in pieces if p.numel() for q in sharded.split_at_newlines(p, piece_bytes)]
-    dev = pieces[0].device if len(pieces) else torch.device("cuda", ctx.device)
-    npieces = torch.tensor([len(pieces)], dtype=torch.int64, device=dev if dist.get_backend(group) != "gloo" else "cpu")
-    dist.all_reduce(npieces, op=dist.ReduceOp.MAX, group=group)
+    dev = pieces[0].device if len(pieces) else ctx.torch_device
+    npieces = exchange_counts([len(pieces)] * world, group)
     out_pieces = []
-    for i in range(int(npieces.item())):
+    for i in range(max(npieces)):
         p = pieces[i] if i < len(pieces) else torch.empty(0, dtype=torch.uint8, device=dev)
         n = int(p.numel())
         send = torch.empty(n + 16, dtype=torch.uint8, device=dev)
@@ -121,6 +163,92 @@ def range_exchange(ctx, pieces: Sequence[torch.Tensor], gsplit, group=None, piec
         if recv.numel():
             out_pieces += sharded.split_at_newlines(recv, piece_bytes)
     return out_pieces
+
+
+# ------------------------------------------------------------------ exchange in rounds (C5)
+def plan_rounds(bytes_per_rank: int, world: int, part_bytes: int = 2 << 30, min_rounds: int = 4) -> int:
+    """Local range parts per rank: enough that each stays well under one library call
+    (part_bytes, with 25 % headroom for imbalance), and at least min_rounds when there is an
+    exchange to hide (round p + 1 travels while round p is deduped); G x rounds <= 256."""
+    r = max(1, -(-int(bytes_per_rank * 1.25) // part_bytes))
+    if world > 1:
+        r = max(r, min_rounds)
+    return int(max(1, min(r, 256 // max(world, 1))))
+
+
+def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int, group=None):
+    """Route this rank's pieces into world x rounds byte ranges with ONE partition call (the
+    parts laid out round-major, sg_dev_partition_bytes_pieces_rounds), exchange every part's
+    size with ONE all-to-all, then queue one all-to-all per round, all at once (async on RCCL's
+    stream). Returns ([(work or None, receive tensor) per round], send buffer): the receive
+    tensor of round p is this rank's local range p (every source's records of it, in source
+    rank order), and work.wait() orders the caller's stream after its arrival. The send buffer
+    must stay referenced until every round has been waited for."""
+    from .api import round_offsets
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    live = [p for p in pieces if p is not None and p.numel()]
+    dev = pieces[0].device if len(pieces) else ctx.torch_device
+    nparts = world * rounds
+    if len(splitters) != nparts - 1:
+        raise ValueError("%d splitters for %d ranks x %d rounds" % (len(splitters), world, rounds))
+    total = sum(int(p.numel()) for p in live)
+    send = torch.empty(total + len(live) + 16 * (rounds + 1), dtype=torch.uint8, device=dev)
+    if live:
+        ctx.fence_in()
+        pb, _ = ctx.partition_bytes_pieces_rounds([(p.data_ptr(), p.numel()) for p in live], splitters, rounds,
+                                                  send.data_ptr(), send.numel())
+    else:
+        pb = [0] * nparts
+    if world == 1:
+        offs = round_offsets(pb, rounds)
+        return [(None, send[offs[p]:offs[p] + pb[p]]) for p in range(rounds)], send
+    # rc[s * rounds + p]: bytes source s sends this rank in round p (peer g's slice of pb is
+    # its rounds parts g * rounds .. + rounds - 1, contiguous)
+    rc = exchange_counts(pb, group)
+    offs = round_offsets(pb, rounds)
+    out = []
+    for p in range(rounds):
+        ins = [pb[g * rounds + p] for g in range(world)]
+        outs = [rc[s * rounds + p] for s in range(world)]
+        recv = torch.empty(sum(outs), dtype=torch.uint8, device=dev)
+        w = all_to_all_bytes(recv, send[offs[p]:offs[p] + sum(ins)], outs, ins, group, async_op=True)
+        out.append((w, recv))
+    return out, send
+
+
+def dedup_diff_rounds_step(ctx, cur_pieces, prior_parts, splitters, rounds: int, group=None, align_parts=False):
+    """One multi-GPU dedup+diff step in exchange rounds: rank r ends with byte range r split
+    into `rounds` local parts; each part is deduped and diffed against the rank's stored prior
+    part as soon as its round has arrived, while the later rounds are still on the wire. The
+    ranks' outputs concatenated in rank order are the global sort -u / comm -13 output.
+    prior_parts: this rank's stored prior, one tensor (or None) per local part (None: no
+    prior). Returns (unique, new, stats) device tensors (new is unique without a prior)."""
+    from . import sharded
+    recvd, send = exchange_rounds(ctx, cur_pieces, splitters, rounds, group)
+    have_prior = prior_parts is not None and any(p is not None and p.numel() for p in prior_parts)
+    if prior_parts is not None and len(prior_parts) != rounds:
+        raise ValueError("prior_parts has %d entries for %d rounds" % (len(prior_parts), rounds))
+    dev = recvd[0][1].device
+    st = sharded.new_stats(rounds)
+    st["recv_bytes"] = [int(r.numel()) for _, r in recvd]
+    out = sharded._Results(sum(st["recv_bytes"]) + 4096, dev, have_prior, align16=align_parts)
+    for p, (w, recv) in enumerate(recvd):
+        if w is not None:
+            w.wait()
+        sharded.dedup_part(ctx, recv if recv.numel() else None, prior_parts[p] if have_prior else None, out, st)
+    del send, recvd
+    u = out.u[:out.uo]
+    return u, (out.f[:out.fo] if have_prior else u), st
+
+
+def build_prior_rounds(ctx, prior_pieces, splitters, rounds: int, group=None):
+    """Setup (untimed): route the rank's share of the prior scan's records to their owners
+    with the same splitters and sort -u them there: returns the rank's stored prior, one
+    16-byte aligned tensor per local part (read in place by every later step), and the
+    stored bytes."""
+    from . import sharded
+    u, _, st = dedup_diff_rounds_step(ctx, prior_pieces, None, splitters, rounds, group, align_parts=True)
+    return sharded.stored_parts(u, st), u
 
 
 def build_prior_range(ctx, candidates: torch.Tensor, gsplit, group=None) -> torch.Tensor:
@@ -179,12 +307,12 @@ def match_step(ctx, matcher, shard: torch.Tensor, group=None):
     (records, hits, matched records)). The global grep output is the ranks' matched lines
     concatenated in rank order (gather_lines)."""
     r = matcher.dev_match(ctx, shard.data_ptr() if shard.numel() else 0, shard.numel())
-    t = torch.tensor([int(r.in_records), int(r.n_hits), int(r.matched_records)], dtype=torch.int64)
+    vals = [int(r.in_records), int(r.n_hits), int(r.matched_records)]
     if dist.is_initialized() and dist.get_world_size(group) > 1:
-        if dist.get_backend(group) != "gloo":
-            t = t.to(shard.device)
+        t = torch.tensor(vals, dtype=torch.int64, device=_coll_device(group))
         dist.all_reduce(t, group=group)
-    return r, tuple(int(x) for x in t.tolist())
+        vals = [int(x) for x in t.tolist()]
+    return r, tuple(vals)
 
 
 def gather_lines(local: bytes, group=None) -> bytes:

@@ -165,14 +165,27 @@ def route_spans(ctx, pieces: Sequence, splitters):
 
 class _Results:
     """The unique and new-record outputs of all parts, appended in part order into two
-    preallocated device buffers (each part's dedup call writes there directly)."""
+    preallocated device buffers (each part's dedup call writes there directly).
+    align16: every top-level part's unique output starts at a 16-byte aligned offset (the
+    gap filled with '\n', i.e. empty records, which no consumer sees): a stored prior kept
+    this way is read in place, part by part, with no copy into an aligned slot."""
 
-    def __init__(self, cap: int, device, want_fresh: bool):
+    def __init__(self, cap: int, device, want_fresh: bool, align16: bool = False):
         import torch
+        self.align16 = align16
+        cap += 16 * 257 if align16 else 0
         self.u = torch.empty(cap, dtype=torch.uint8, device=device)
         self.f = torch.empty(cap, dtype=torch.uint8, device=device) if want_fresh else None
         self.uo = 0
         self.fo = 0
+
+    def begin_part(self) -> int:
+        """Start of the next top-level part's unique output."""
+        if self.align16 and self.uo & 15:
+            a = (self.uo + 15) & ~15
+            self.u[self.uo:a].fill_(10)
+            self.uo = a
+        return self.uo
 
 
 def plan_parts(cur_pieces: Sequence, prior_pieces: Sequence, part_bytes: int) -> int:
@@ -180,15 +193,29 @@ def plan_parts(cur_pieces: Sequence, prior_pieces: Sequence, part_bytes: int) ->
     return int(min(256, max(1, -(-int(big * 1.25) // part_bytes))))
 
 
+def new_stats(parts: int) -> dict:
+    return {"parts": parts, "in_records": 0, "uniq_records": 0, "fresh_records": 0, "max_part_bytes": 0,
+            "rerouted_parts": 0, "part_bytes": [], "uniq_part_bytes": [], "uniq_part_offs": []}
+
+
+def stored_parts(u, st) -> List:
+    """The per-part views of a unique output (st from dedup_diff_large / a rounds step): a
+    stored prior kept this way is handed back as prior_parts, never routed again."""
+    return [u[o:o + n] if n else None for o, n in zip(st["uniq_part_offs"], st["uniq_part_bytes"])]
+
+
 def dedup_diff_large(ctx, cur_pieces: Sequence, prior_pieces: Sequence = (), part_bytes: int = 2 << 30,
-                     samples_per_piece: int = 1 << 12, splitters=None, prior_parts: Sequence | None = None):
+                     samples_per_piece: int = 1 << 12, splitters=None, prior_parts: Sequence | None = None,
+                     align_parts: bool = False):
     """(sort -u of all cur records, new records vs prior, stats) as device tensors, each in
     global byte order, for shards of any size. `prior_pieces` is the prior scan (sorted
     unique or not). `splitters` may be given (byte strings or key0 values, e.g. agreed
     across ranks); otherwise byte splitters are chosen from records sampled from every
     piece. `prior_parts` (with `splitters`): the prior already split by those splitters — the
     stored prior scan is this function's own part-ordered output, so it need not be routed
-    again (st["uniq_part_bytes"] gives the part boundaries)."""
+    again (stored_parts(u, st) gives the part views). align_parts: every part's unique output
+    starts 16-byte aligned ('\n' padding between parts, so u is a line buffer holding the
+    sort -u records but not byte-identical to the sort -u output): for storing a prior."""
     import torch
     cur_pieces = [p for p in cur_pieces if p.numel()]
     prior_pieces = [p for p in prior_pieces if p.numel()]
@@ -198,9 +225,8 @@ def dedup_diff_large(ctx, cur_pieces: Sequence, prior_pieces: Sequence = (), par
         splitters = choose_splitters(sample_records(ctx, cur_pieces + prior_pieces, samples_per_piece), parts)
     have_prior = bool(prior_pieces) or (prior_parts is not None and any(p is not None and p.numel()
                                                                         for p in prior_parts))
-    st = {"parts": n_splitters(splitters) + 1, "in_records": 0, "uniq_records": 0, "fresh_records": 0,
-          "max_part_bytes": 0, "rerouted_parts": 0, "part_bytes": [], "uniq_part_bytes": []}
-    out = _Results(sum(p.numel() for p in cur_pieces) + 4096, dev, have_prior)
+    st = new_stats(n_splitters(splitters) + 1)
+    out = _Results(sum(p.numel() for p in cur_pieces) + 4096, dev, have_prior, align16=align_parts)
     _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, out, st, samples_per_piece, prior_parts=prior_parts)
     u = out.u[:out.uo]
     return u, (out.f[:out.fo] if have_prior else u), st
@@ -222,49 +248,57 @@ def _dedup_parts(ctx, cur_pieces, prior_pieces, splitters, out, st, samples_per_
     if len(prior_parts) != len(cur_parts):
         raise ValueError("prior_parts has %d entries for %d parts" % (len(prior_parts), len(cur_parts)))
     for b, (c, p) in enumerate(zip(cur_parts, prior_parts)):
-        if depth == 0:
-            st["uniq_part_bytes"].append(0)
-            u_start = out.uo
-        if c is None:
-            continue
-        pn = p.numel() if p is not None else 0
-        if c.numel() > PART_LIMIT or pn > PART_LIMIT:
-            # route this part again with splitters sampled from it alone
-            big = max(c.numel(), pn)
-            sub_parts = int(min(256, max(2, -(-int(big * 1.25) // (PART_LIMIT // 2)))))
-            sub = choose_splitters(sample_records(ctx, [c] + ([p] if p is not None else []), samples_per_piece),
-                                   sub_parts)
-            if depth >= 3 or not sub:
-                raise ValueError(part_overflow_message(splitters, b, c.numel(), pn))
-            st["rerouted_parts"] += 1
-            _dedup_parts(ctx, [c], [p] if p is not None else [], sub, out, st, samples_per_piece, depth + 1)
-            if depth == 0:
-                st["uniq_part_bytes"][-1] = out.uo - u_start
-            continue
-        st["max_part_bytes"] = max(st["max_part_bytes"], c.numel())
-        st["part_bytes"].append(int(c.numel()))
-        ctx.fence_in()
-        try:
-            outs = (out.u.data_ptr() + out.uo, out.u.numel() - out.uo,
-                    (out.f.data_ptr() + out.fo) if out.f is not None else 0,
-                    (out.f.numel() - out.fo) if out.f is not None else 0)
-            if parse is not None and parse[b] is not None:
-                sp, kp, nr = parse[b]
-                r = ctx.dedup_diff_spans_into(c.data_ptr(), c.numel(), sp, kp, nr, p.data_ptr() if pn else 0, pn,
-                                              *outs)
-            else:
-                r = ctx.dedup_diff_into(c.data_ptr(), c.numel(), p.data_ptr() if pn else 0, pn, *outs)
-        except Exception as e:
-            raise type(e)(e.rc, "%s (part of %d bytes at %#x, prior %s)" % (
-                e, c.numel(), c.data_ptr(), None if p is None else pn)) if hasattr(e, "rc") else e
-        out.uo += int(r.uniq_bytes)
+        dedup_part(ctx, c, p, out, st, samples_per_piece, depth, parse[b] if parse is not None else None,
+                   label=(splitters, b))
+
+
+def dedup_part(ctx, c, p, out, st, samples_per_piece: int = 1 << 12, depth: int = 0, parse=None, label=None):
+    """sort -u + diff of one range part `c` (device tensor or None) against the prior's same
+    part `p`, appended to `out`; a part over the per-call limit is routed again with
+    splitters sampled from it alone. depth 0 = a top-level part (its unique output's offset
+    and size are recorded in st for stored_parts)."""
+    if depth == 0:
+        st["uniq_part_offs"].append(out.begin_part())
+        st["uniq_part_bytes"].append(0)
+        u_start = out.uo
+    if c is None or not c.numel():
+        return
+    pn = p.numel() if p is not None else 0
+    if c.numel() > PART_LIMIT or pn > PART_LIMIT:
+        big = max(c.numel(), pn)
+        sub_parts = int(min(256, max(2, -(-int(big * 1.25) // (PART_LIMIT // 2)))))
+        sub = choose_splitters(sample_records(ctx, [c] + ([p] if pn else []), samples_per_piece), sub_parts)
+        if depth >= 3 or not sub:
+            sp, b = label if label else ([], 0)
+            raise ValueError(part_overflow_message(sp, b, c.numel(), pn))
+        st["rerouted_parts"] += 1
+        _dedup_parts(ctx, [c], [p] if pn else [], sub, out, st, samples_per_piece, depth + 1)
         if depth == 0:
             st["uniq_part_bytes"][-1] = out.uo - u_start
-        if out.f is not None:
-            out.fo += int(r.fresh_bytes)
-        st["in_records"] += int(r.in_records)
-        st["uniq_records"] += int(r.uniq_records)
-        st["fresh_records"] += int(r.fresh_records)
+        return
+    st["max_part_bytes"] = max(st["max_part_bytes"], c.numel())
+    st["part_bytes"].append(int(c.numel()))
+    ctx.fence_in()
+    try:
+        outs = (out.u.data_ptr() + out.uo, out.u.numel() - out.uo,
+                (out.f.data_ptr() + out.fo) if out.f is not None else 0,
+                (out.f.numel() - out.fo) if out.f is not None else 0)
+        if parse is not None:
+            sp, kp, nr = parse
+            r = ctx.dedup_diff_spans_into(c.data_ptr(), c.numel(), sp, kp, nr, p.data_ptr() if pn else 0, pn, *outs)
+        else:
+            r = ctx.dedup_diff_into(c.data_ptr(), c.numel(), p.data_ptr() if pn else 0, pn, *outs)
+    except Exception as e:
+        raise type(e)(e.rc, "%s (part of %d bytes at %#x, prior %s)" % (
+            e, c.numel(), c.data_ptr(), None if p is None else pn)) if hasattr(e, "rc") else e
+    out.uo += int(r.uniq_bytes)
+    if depth == 0:
+        st["uniq_part_bytes"][-1] = out.uo - u_start
+    if out.f is not None:
+        out.fo += int(r.fresh_bytes)
+    st["in_records"] += int(r.in_records)
+    st["uniq_records"] += int(r.uniq_records)
+    st["fresh_records"] += int(r.fresh_records)
 
 
 def split_parts(buf, part_bytes: Sequence[int]) -> List:

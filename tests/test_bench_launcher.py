@@ -27,6 +27,9 @@ def test_gpus_n_launches_n_ranks(n):
     assert len(lines) == 1, p.stdout.decode()
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["steps"] == 3 and d["launcher_check"]
+    assert d["world_size_seen"] == n
+    # N > 1 measures the target config by default: C5 (1B records) strong scaling
+    assert d["workload"] == "c5"
 
 
 def test_gpus_1_runs_in_process():
@@ -34,6 +37,7 @@ def test_gpus_1_runs_in_process():
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     d = json.loads([ln for ln in p.stdout.decode().splitlines() if ln.startswith("{")][0])
     assert d["n_gpus"] == 1
+    assert d["workload"] == "c2"  # the headline at N = 1 is BASELINE configs[1]
 
 
 def test_world_size_mismatch_is_refused():

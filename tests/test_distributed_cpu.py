@@ -136,6 +136,78 @@ def test_range_exchange_global_order_gloo(world):
     assert all(r[5] <= 4096 for r in res)  # received ranges re-cut at record boundaries
 
 
+def rounds_shard(rank, world):
+    """Unequal pieces per rank: rank 0 three pieces (one empty), rank 1 none at all (an empty
+    rank), the others one; records share long prefixes (URLs) and include CR / 0xff bytes."""
+    import random
+    rng = random.Random(500 + rank)
+    recs = [b"https://h%d.example.com/%s" % (rng.randrange(2500), b"x" * rng.randrange(3)) for _ in range(1500)]
+    recs += [b"10.0.%d.%d:443" % (rank, rng.randrange(9)) for _ in range(50)] + [b"\xff", b"x\r", b""]
+    cur = b"\n".join(recs) + b"\n"
+    if rank == 1:
+        return []
+    if rank == 0:
+        cut = cur.index(b"\n", len(cur) // 3) + 1
+        return [cur[:cut], b"", cur[cut:]]
+    return [cur]
+
+
+def rounds_worker(rank, world, rounds, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from route_oracle import FakeCtx
+    from swarm_amd import distributed as D
+    ctx = FakeCtx()
+    t = lambda b: torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8)[: len(b)]  # noqa: E731
+    prior_raw = [b"https://h%d.example.com/\n" % i for i in range(rank, 2500, 2 * world)]
+    prior_raw = b"".join(prior_raw) + (b"10.0.0.1:443\n" if rank == world - 1 else b"")
+    split = D.agree_splitters(ctx, [t(prior_raw)], world * rounds, samples_per_piece=64)
+    assert len(split) == world * rounds - 1
+    prior_parts, stored = D.build_prior_rounds(ctx, [t(prior_raw)], split, rounds)
+    assert len(prior_parts) == rounds
+    cur = rounds_shard(rank, world)
+    u, f, st = D.dedup_diff_rounds_step(ctx, [t(c) for c in cur], prior_parts, split, rounds)
+    out_q.put((rank, bytes(u.numpy().tobytes()), bytes(f.numpy().tobytes()), b"".join(cur), prior_raw,
+               bytes(stored.numpy().tobytes()), st["parts"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,rounds", [(2, 3), (3, 2), (2, 1)])
+def test_rounds_step_global_order_gloo(world, rounds):
+    """dedup_diff_rounds_step (the C5 multi-GPU step: one partition into world x rounds ranges,
+    one size exchange, one all-to-all per round, each part deduped as its round arrives): the
+    ranks' outputs concatenated in rank order equal the global oracle output, with unequal
+    piece counts, an empty piece and a rank holding nothing."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=rounds_worker, args=(r, world, rounds, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cur_all = b"".join(r[3] for r in res)
+    prior_all = b"".join(r[4] for r in res)
+    eu, ef = S.dedup_diff(cur_all, prior_all)
+    assert b"".join(r[1] for r in res) == eu
+    assert b"".join(r[2] for r in res) == ef
+    # the stored prior: 16-byte aligned parts padded with empty lines = the prior's sort -u
+    assert S.serialize(S.parse_records(b"".join(r[5] for r in res))) == S.dedup(prior_all)
+    assert all(r[6] == rounds for r in res)
+
+
+def test_plan_rounds():
+    from swarm_amd.distributed import plan_rounds
+    assert plan_rounds(1 << 20, 1) == 1
+    assert plan_rounds(31_500_000_000, 1) == 19
+    assert plan_rounds(4_000_000_000, 8) == 4          # at least 4 rounds to hide the exchange
+    assert plan_rounds(16_000_000_000, 2) == 10
+    assert plan_rounds(10 ** 12, 8) == 32              # world x rounds <= 256
+
+
 class _Hits:
     def __init__(self, data, sigs):
         hits = S.literal_hits(data, sigs)

@@ -132,6 +132,50 @@ def test_two_ranks_range_sharded_global_order():
     assert b"".join(r[2] for r in res) == ef
 
 
+def rounds_worker(rank, world, port, q, rounds):
+    """The C5 multi-GPU step (bench.py --gpus N): one partition into world x rounds ranges,
+    one size exchange, one all-to-all per round, each part deduped as its round arrives,
+    against the stored prior built the same way; rank 1 holds an empty piece besides its
+    records. Rank outputs concatenated in rank order = the global sort -u / comm -13."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import swarm_amd
+    from swarm_amd import corpus
+    from swarm_amd import distributed as D
+    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    pool = corpus.host_pool_gpu(20_000, seed=5)
+    U = 20_000 * len(corpus.PORTS)
+    prior_raw = corpus.hostport_pieces(pool, 150_000, U // 10, U, seed=900 + rank, per_piece=40_000)
+    cur = corpus.hostport_pieces(pool, 200_000 + 30_000 * rank, 0, U, seed=100 + rank, per_piece=60_000)
+    if rank == 1:
+        cur = cur[:1] + [torch.empty(0, dtype=torch.uint8, device="cuda")] + cur[1:]
+    split = D.agree_splitters(ctx, prior_raw, world * rounds)
+    prior_parts, stored = D.build_prior_rounds(ctx, prior_raw, split, rounds)
+    assert all(p is None or p.data_ptr() % 16 == 0 for p in prior_parts)
+    u, f, st = D.dedup_diff_rounds_step(ctx, cur, prior_parts, split, rounds)
+    torch.cuda.synchronize()
+    q.put((rank, u.cpu().numpy().tobytes(), f.cpu().numpy().tobytes(),
+           b"".join(p.cpu().numpy().tobytes() for p in cur), b"".join(p.cpu().numpy().tobytes() for p in prior_raw),
+           st["parts"]))
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("rounds", [1, 3])
+def test_two_ranks_rounds_step_global_order(rounds):
+    res = spawn(rounds_worker, 2, rounds)
+    cur_all = b"".join(r[3] for r in res)
+    prior_all = S.dedup(b"".join(r[4] for r in res))
+    eu, ef = S.dedup_diff(cur_all, prior_all)
+    assert b"".join(r[1] for r in res) == eu
+    assert b"".join(r[2] for r in res) == ef
+    assert all(r[5] == rounds for r in res)
+
+
 def spawn(target, world, *extra):
     import torch.multiprocessing as mp
     mctx = mp.get_context("spawn")

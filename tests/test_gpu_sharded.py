@@ -355,3 +355,83 @@ def test_partition_spans_handover(ctx):
             assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
         r0 += nr
     assert r0 == len(S.parse_records(data))
+
+
+@pytest.mark.parametrize("world,rounds", [(2, 3), (3, 1), (1, 4)])
+def test_partition_pieces_rounds_layout(ctx, world, rounds):
+    """sg_dev_partition_bytes_pieces_rounds: world x rounds byte ranges, part q = g * rounds
+    + p, laid out round-major (round p = parts (0, p) .. (world - 1, p) back to back, every
+    round 16-byte aligned): each round is one contiguous all-to-all send buffer. Checked
+    against route_parts per piece; padding between rounds never written."""
+    import torch
+    from swarm_amd.api import round_offsets
+    from route_oracle import FakeCtx
+    recs = shared_prefix_records(20_000, 21 + world)
+    data = b"\n".join(recs) + b"\n"
+    cuts = [0, len(data) // 3, len(data) // 3, len(data)]  # an empty piece in the middle
+    cuts = [c if c in (0, len(data)) else data.index(b"\n", c) + 1 for c in cuts]
+    d = dev(b"#" + data)
+    pieces = [d[1 + a:1 + b] for a, b in zip(cuts, cuts[1:])]
+    sp = sorted(random.Random(22).sample(recs, world * rounds - 1))
+    cap = len(data) + len(pieces) + 16 * (rounds + 1)
+    out = torch.full((cap + 64,), 0x55, dtype=torch.uint8, device=d.device)
+    pb, pr = ctx.partition_bytes_pieces_rounds([(p.data_ptr(), p.numel()) for p in pieces], sp, rounds,
+                                               out.data_ptr(), cap)
+    got = out.cpu().numpy().tobytes()
+    host = np.frombuffer(bytearray(data), dtype=np.uint8)
+    want_buf = bytearray(b"\x55" * (cap + 64))
+    wb = (np.frombuffer(want_buf, dtype=np.uint8))
+    hp = [np.frombuffer(bytearray(data[a:b] or b"\0"), dtype=np.uint8) for a, b in zip(cuts, cuts[1:])]
+    wpb, wpr = FakeCtx().partition_bytes_pieces_rounds([(h.ctypes.data, b - a) for h, (a, b) in
+                                                        zip(hp, zip(cuts, cuts[1:]))], sp, rounds, wb.ctypes.data, cap)
+    assert (pb, pr) == (wpb, wpr)
+    assert got == bytes(want_buf)
+    offs = round_offsets(pb, rounds)
+    assert all(o % 16 == 0 for o in offs[:-1]) and offs[-1] <= cap
+    del host
+
+
+def test_stored_prior_aligned_parts(ctx):
+    """dedup_diff_large(align_parts=True): every part's unique output starts 16-byte aligned
+    ('\\n' padding: the buffer's records are still the sort -u records) and those parts,
+    handed back as prior_parts, are read in place with results equal to the oracle."""
+    from swarm_amd import sharded
+    buf, ids = corpus.subdomains(300_000, seed=45)
+    prior_raw = corpus.prior_of(ids).tobytes()
+    pieces = sharded.split_at_newlines(dev(prior_raw), 1 << 20)
+    sp = sharded.choose_splitters(sharded.sample_records(ctx, pieces, 256), 7)
+    pu, _, pst = sharded.dedup_diff_large(ctx, pieces, (), splitters=sp, align_parts=True)
+    parts = sharded.stored_parts(pu, pst)
+    assert len(parts) == len(sp) + 1
+    assert all(p is None or p.data_ptr() % 16 == 0 for p in parts)
+    assert S.serialize(S.parse_records(pu.cpu().numpy().tobytes())) == S.dedup(prior_raw)
+    cur = sharded.split_at_newlines(dev(buf.tobytes()), 1 << 20)
+    u, f, _ = sharded.dedup_diff_large(ctx, cur, (), splitters=sp, prior_parts=parts)
+    eu, ef = S.dedup_diff(buf.tobytes(), prior_raw)
+    assert u.cpu().numpy().tobytes() == eu and f.cpu().numpy().tobytes() == ef
+
+
+def test_private_stream_last_part_without_prior():
+    """on a context with its own stream, a part with no prior records copies its
+    unique output into the caller's new-record buffer; the call must not return before that
+    copy has landed (torch reads or frees the buffer next)."""
+    import swarm_amd
+    import torch
+    from swarm_amd import sharded
+    c = swarm_amd.Context(0)
+    try:
+        assert not c.on_torch_stream()
+        buf, ids = corpus.subdomains(300_000, seed=46)
+        cur = buf.tobytes()
+        # the prior only holds records below "m": every part above has no prior records
+        prior = b"".join(r + b"\n" for r in S.parse_records(corpus.prior_of(ids).tobytes()) if r < b"m")
+        for _ in range(3):
+            u, f, st = sharded.dedup_diff_large(c, sharded.split_at_newlines(dev(cur), 1 << 20), [dev(prior)],
+                                                splitters=[b"f", b"m", b"t"])
+            fh = f.cpu().numpy().tobytes()  # read on torch's stream right away
+            del f
+            torch.empty(len(fh) + 4096, dtype=torch.uint8, device="cuda").fill_(0)  # reuse freed blocks
+            eu, ef = S.dedup_diff(cur, prior)
+            assert u.cpu().numpy().tobytes() == eu and fh == ef
+    finally:
+        c.close()

@@ -60,7 +60,8 @@ def main():
                  "per launch (average over the PMC pass's launches). Traffic GB/s = (fetch+write) / avg duration.", "",
                  "| kernel | calls | avg µs | % time | fetch MB/launch | write MB/launch | traffic GB/s |",
                  "|---|---|---|---|---|---|---|"]
-        traffic.setdefault(wl, {})
+        if fe or wr:  # a fresh PMC pass replaces the workload's rows (no stale kernels survive)
+            traffic[wl] = {}
         for k, (calls, avg_us, pct) in sorted(st.items(), key=lambda kv: -kv[1][2]):
             f = fe.get(k)
             w = wr.get(k)
@@ -71,11 +72,12 @@ def main():
                 "%.2f" % (2.0 * f / 1e6) if f is not None else "-",
                 "%.2f" % (w / 1e6) if w is not None else "-",
                 "%.0f" % gbs if gbs is not None else "-"))
-            if f is not None or w is not None:
+            if (f is not None or w is not None) and wl in traffic:
                 traffic[wl][k] = {"fetch_bytes": round(2.0 * f) if f is not None else None,
                                   "write_bytes": round(w) if w is not None else None,
                                   "bytes": round(tb), "avg_us": round(avg_us, 2),
-                                  "source": os.path.basename(dst) + "_" + wl + "_summary.md"}
+                                  "source": os.path.join(os.path.basename(os.path.dirname(dst)),
+                                                         os.path.basename(dst) + "_" + wl + "_summary.md")}
         with open("%s_%s_summary.md" % (dst, wl), "w") as f:
             f.write("\n".join(lines) + "\n")
         print("\n".join(lines[:16]))
