@@ -74,16 +74,10 @@ int sg_ctx_kernel_stat(sg_ctx *ctx, int idx, const char **name, uint64_t *launch
 int sg_ctx_reset_stats(sg_ctx *ctx);
 /* Synchronous copy on the context's stream (any direction: hipMemcpyDefault). */
 int sg_ctx_memcpy(sg_ctx *ctx, void *dst, const void *src, size_t n);
-/* Which dedup/diff pipeline served the context's last sg_dev_dedup_diff: *path = 0 the radix
- * pipeline, 1 the bucket sample sort (splitters from the prior scan), 2 the probe path (a
- * strictly increasing prior: current records looked up in a hash table of it, only the new
- * ones sorted, the unique output merged from both); *flags = why the bucket
- * path handed over to the radix pipeline (0 when it did not; bit 0 a record longer than the
- * tile overhang, 1 a bucket over its LDS budget, 2 a prior slice over its budget, 3 a prior
- * that is not strictly increasing). For tests and benchmarks. */
+/* Which dedup/diff pipeline served the context's last sg_dev_dedup_diff: *path = 0, the radix
+ * pipeline — since round 3 the only one in the library (the bucket sample sort and the probe
+ * path, both measured slower, live in tools/experiments/); *flags = 0. For tests/benchmarks. */
 #define SG_PATH_RADIX 0
-#define SG_PATH_BUCKET 1
-#define SG_PATH_PROBE 2
 int sg_ctx_last_path(sg_ctx *ctx, int *path, uint32_t *flags);
 /* Sort-key width (bytes after the common prefix, 5..7) the last radix dedup chose from the
  * keys' byte entropies. For tests and benchmarks. */

@@ -374,13 +374,11 @@ class Context:
         return out.tobytes()
 
     def last_path(self):
-        """(pipeline, flags) of the last dedup_diff on this context: "radix", "bucket" (the
-        sample sort with splitters from the prior scan) or "probe" (a sorted prior: records
-        looked up in a hash table of it, only the new ones sorted), and the bucket path's
-        hand-over reasons (include/swarmgpu.h sg_ctx_last_path)."""
+        """(pipeline, flags) of the last dedup_diff on this context: ("radix", 0) — the only
+        pipeline in the library (include/swarmgpu.h sg_ctx_last_path)."""
         p, f = C.c_int(), C.c_uint32()
         check(lib.sg_ctx_last_path(self._h, C.byref(p), C.byref(f)))
-        return {1: "bucket", 2: "probe"}.get(p.value, "radix"), f.value
+        return {0: "radix"}.get(p.value, str(p.value)), f.value
 
     def last_key_width(self) -> int:
         """Sort-key width in bytes (5..7) the last radix dedup chose on this context."""

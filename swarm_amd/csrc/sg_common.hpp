@@ -64,14 +64,8 @@ enum Slot : int {
     S_F_SPANS, S_F_LB, S_F_A, S_F_B, S_F_DESC, S_F_OFFS, S_F_OUT, S_F_REC, S_F_KEY, S_F_KEYS,
     S_T_HITS, S_T_EXP, S_T_K2, S_T_V1, S_T_V2, S_T_OUT, S_T_SEL, S_T_E, S_T_E2, S_T_SEG, S_T_FLAG, S_T_O,
     S_T_REC, S_T_TID,
-    // bucket sample sort (sg_bucket.hip)
-    S_BK_SKEY, S_BK_SSPAN, S_BK_CNT1, S_BK_CNT2, S_BK_SMALL, S_BK_TOT2, S_BK_Q, S_BK_NCUR, S_BK_L1, S_BK_L2,
-    S_BK_US, S_BK_FS, S_BK_SPFX, S_BK_DBG, S_BK_RECS, S_BK_NREC,
     S_M_FLAG, S_M_SP2, S_M_K2, S_R_T2, S_COUNT2,
     S_R_ALPHA,  // refinement rounds: byte alphabet mask + rank table of the chunk keys
-    // probe path (sg_dedup.hip: cur records looked up in a sorted prior's hash table)
-    S_PB_TAB, S_PB_BITS, S_PB_NEW, S_PB_IDX, S_PB_SP, S_PB_K, S_PB_INS, S_PB_KB, S_PB_MI, S_PB_STAT,
-    S_PB_H, S_PB_RK, S_PB_CNT, S_PB_OFF, S_PB_E, S_PB_ERR,
     // hit sort by record buckets (sg_match.hip)
     S_HB_CNT, S_HB_OFF, S_HB_OUT, S_HB_ERR, S_HB_SEL2,
     S_TS2,  // two-level tile scan scratch
@@ -98,8 +92,8 @@ struct sg_ctx {
     void *slot_ptr[sg::S_NSLOTS] = {};
     size_t slot_cap[sg::S_NSLOTS] = {};
     void *pinned = nullptr;   // host pinned staging for small readbacks (SG_PINNED_BYTES)
-    int last_path = 0;        // dedup/diff: 0 = radix pipeline, 1 = bucket sample sort, 2 = probe
-    uint32_t last_flags = 0;  // bucket path error word of the last call (0: not declined)
+    int last_path = 0;        // dedup/diff pipeline of the last call: 0 = the radix pipeline (the only one)
+    uint32_t last_flags = 0;  // always 0 since round 3 (the bucket path's hand-over reasons)
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
     uint64_t pt_keep_recs = 0;  // piece partition: records the last call kept between its passes

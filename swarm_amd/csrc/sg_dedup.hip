@@ -41,7 +41,7 @@ constexpr uint32_t WAVE_GROUP = 64;
 // (records << 32 | bytes). `bytes_model`: algorithmic bytes credited to the apply launch
 // (DESIGN.md §4).
 typedef void (*EmitApplyFn)(const uint2 *, uint32_t, const uint64_t *, const uint8_t *, uint8_t *, uint2 *,
-                            const uint64_t *, uint64_t *, int);
+                            const uint64_t *, uint64_t *);
 
 // dst_shift (< 16): the output starts dst_shift bytes past the 16-B aligned `dst` (byte
 // offsets and out_spans include it; the total does not).
@@ -60,11 +60,10 @@ static int run_emit(sg_ctx *c, EmitApplyFn kern, const char *name, const char *c
     }
     uint2 *cache;
     SG_TRY(slot(c, S_ECACHE, (size_t)n + 1, &cache));
-    static const int dbg = getenv("SG_EMIT_DEBUG") ? atoi(getenv("SG_EMIT_DEBUG")) : 0;
     SG_LAUNCH(c, cname, k_emit_count<Item>, ntiles, EM_BLOCK, 0, item, n, cache, tot);
     SG_TRY(tile_scan(c, tot, ntiles, pre, total, dst_shift));
     SG_LAUNCH_B(c, name, bytes_model, kern, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin,
-                kout, dbg & 1);
+                kout);
     return SG_OK;
 }
 
@@ -535,11 +534,8 @@ __global__ __launch_bounds__(256) void k_diff_split(const uint64_t *__restrict__
     if (lane == 0) jb[t] = lo;
 }
 
-// INS (U records known to be absent from P, the probe path): ins[i] = the insertion point
-// of U record i in P (the first P record greater than it) instead of a presence flag.
-template <bool INS>
 __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_t *__restrict__ jb,
-                                               uint8_t *__restrict__ fresh, uint32_t *__restrict__ ins, uint32_t base) {
+                                               uint8_t *__restrict__ fresh, uint32_t base) {
     // the tile's P keys AND spans in LDS: after the key search the candidate's span is an
     // LDS read, so the byte compare waits one global round trip (U and P bytes together)
     // instead of two (P span, then bytes); U spans load with the U keys
@@ -580,40 +576,6 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
         const bool eq = idx[k] < U.n && j0 + lo < P.n && kp == ku[k];
         pres[k] = eq && (ku[k] & 0xffu) < bk_full(base);
         need[k] = eq && !pres[k];
-    }
-    if constexpr (INS) {
-        // a key-equal run [cand, ce) of P (tag kw + 1: more bytes follow): the insertion point
-        // inside it by a bytewise binary search; otherwise the key's lower bound is the answer
-#pragma unroll
-        for (int k = 0; k < DF_PER; ++k) {
-            if (idx[k] >= U.n) continue;
-            uint32_t at = cand[k];
-            if (need[k]) {
-                uint32_t lo2 = cand[k], hi2 = P.n;  // run end: gallop, then bisect
-                uint32_t step = 1;
-                for (;;) {
-                    const uint32_t probe = lo2 + step - 1;
-                    if (probe >= P.n) break;
-                    if (P.K[probe] != ku[k]) { hi2 = probe; break; }
-                    lo2 = probe + 1;
-                    step <<= 1;
-                }
-                while (lo2 < hi2) {
-                    const uint32_t mid = (lo2 + hi2) >> 1;
-                    if (P.K[mid] == ku[k]) lo2 = mid + 1; else hi2 = mid;
-                }
-                uint32_t lo = cand[k], hi = lo2;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    const uint2 x = P.sp[mid];
-                    if (rec_cmp8_2(P.buf, x.x, x.y - x.x, U.buf, us[k].x, us[k].y - us[k].x, bk_off(base)) < 0) lo = mid + 1;
-                    else hi = mid;
-                }
-                at = lo;
-            }
-            ins[idx[k]] = at;
-        }
-        return;
     }
     // tag-8 candidates: the P span (LDS when staged), then a wide compare (loads of all
     // items together)
@@ -671,13 +633,9 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
 
 __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uint32_t *__restrict__ jb,
                                                    uint8_t *__restrict__ fresh, uint32_t base) {
-    diff_tile_body<false>(U, P, jb, fresh, nullptr, base);
+    diff_tile_body(U, P, jb, fresh, base);
 }
 
-__global__ __launch_bounds__(256) void k_ins_tile(RecSet U, RecSet P, const uint32_t *__restrict__ jb,
-                                                  uint32_t *__restrict__ ins, uint32_t base) {
-    diff_tile_body<true>(U, P, jb, nullptr, ins, base);
-}
 
 // ------------------------------------------------------------------ common prefix (URL-like data)
 // L = the longest prefix every record of cur and prior shares (capped at 255). All order and
@@ -815,283 +773,6 @@ __global__ __launch_bounds__(256) void k_rekey(const uint8_t *__restrict__ buf, 
     }
 }
 
-// ------------------------------------------------------------------ probe path
-// When the prior scan is sorted and duplicate-free (the previous run's sort -u output), the
-// current scan's records are looked up in a hash table of the prior instead of sorting all
-// of them: a record found there belongs to the output at the prior record's place, so only
-// the records NOT in the prior (the new ones, ~10 % on a recurring scan) are sorted. The
-// unique output is the prior's found records merged with the sorted new records (each new
-// record's insertion point in the prior from the same key0 search the diff uses); the new
-// records ARE the diff. Equality is decided by bytes (the hash only picks the candidate).
-//
-// Table: 2^tb 16-B slots {fp, start, record index, length} (fp 0 = empty) in segments of
-// 2^sb slots (sb <= 12: one segment is 64 KB of LDS). A record's segment is the top bits of
-// its first hash, its home slot the low sb bits; linear probing wraps inside the segment.
-// fp = the second hash's top 20 bits | the home slot (never 0).
-// No global atomics: device-scope atomics execute memory-side on MI355X (one CAS per prior
-// record took 0.49 ms for 5.7M records, an atomicOr per found record 0.77 ms). Instead the
-// prior records are partitioned by segment (count pass with LDS ranks -> scan -> scatter) and
-// one block per segment fills its 64 KB of slots with LDS atomics, then writes them out.
-constexpr uint32_t PB_SB = 12;           // max log2 slots per segment
-constexpr uint32_t PB_THREADS = 1024;    // count/scatter pass block
-constexpr uint32_t PB_PER = 16;          // records per thread in the count/scatter passes
-constexpr uint32_t PB_BLK = PB_THREADS * PB_PER;
-constexpr uint32_t PB_MAXSEG = 16384;    // LDS histogram bound of the count pass
-
-__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
-    h ^= h >> 16;
-    h *= 0x85EBCA6Bu;
-    h ^= h >> 13;
-    h *= 0xC2B2AE35u;
-    h ^= h >> 16;
-    return h;
-}
-
-// Two 32-bit hashes of the record's bytes (48-byte windows of 16-B loads).
-__device__ __forceinline__ uint2 rec_hash(const uint8_t *__restrict__ buf, uint32_t s, uint32_t len) {
-    uint32_t h1 = 0x9E3779B9u ^ len, h2 = 0x7F4A7C15u + len * 0x85EBCA77u;
-    for (uint32_t o = 0; o < len; o += 48u) {
-        const uint32_t cl = (len - o) < 48u ? (len - o) : 48u;
-        uint4 c[4];
-        load_chunks(buf, s + o, cl, c);
-        uint32_t r[13];
-        normalize52(c, (s + o) & 15u, r);
-#pragma unroll
-        for (uint32_t q = 0; q < 12; ++q) {
-            if (4u * q < cl) {
-                const uint32_t k = cl - 4u * q;
-                const uint32_t w = r[q] & (k >= 4u ? ~0u : ((1u << (8u * k)) - 1u));
-                h1 = __builtin_rotateleft32(h1 ^ w, 13) * 0x9E3779B1u;
-                h2 = (h2 + w) * 0xC2B2AE3Du;
-                h2 ^= h2 >> 15;
-            }
-        }
-    }
-    return make_uint2(fmix32(h1), fmix32(h2 ^ (h1 >> 7)));
-}
-
-// Table geometry: tb = log2 slots, sb = log2 slots per segment; fpm masks the fingerprint
-// (tests narrow it so every probe takes the byte compare).
-struct PbGeom {
-    uint32_t tb, sb, fpm;
-    __device__ uint32_t seg(uint32_t hx) const { return tb > sb ? hx >> (32u - (tb - sb)) : 0u; }
-    __device__ uint32_t home(uint32_t hx) const { return hx & ((1u << sb) - 1u); }
-    __device__ uint32_t fp(uint2 h) const {
-        const uint32_t t = h.y & fpm & 0xFFFFF000u;
-        return (t ? t : 0x1000u) | home(h.x);
-    }
-};
-
-// Count pass: per record its hash pair and its rank among the block's records of the same
-// segment (LDS atomics); per (segment, block) the count, segment-major for the scan.
-__global__ __launch_bounds__(PB_THREADS) void k_pb_count(const uint8_t *__restrict__ P, const uint2 *__restrict__ sp,
-                                                          uint32_t n, PbGeom g, uint2 *__restrict__ H,
-                                                          uint16_t *__restrict__ rk, uint32_t *__restrict__ cnt,
-                                                          uint32_t nblk) {
-    extern __shared__ uint32_t s_h[];
-    const uint32_t nseg = 1u << (g.tb - g.sb);
-    for (uint32_t x = threadIdx.x; x < nseg; x += PB_THREADS) s_h[x] = 0;
-    __syncthreads();
-    const uint32_t b0 = blockIdx.x * PB_BLK;
-#pragma unroll 4
-    for (uint32_t r = 0; r < PB_PER; ++r) {
-        const uint32_t i = b0 + r * PB_THREADS + threadIdx.x;
-        if (i >= n) break;
-        const uint2 x = sp[i];
-        const uint2 h = rec_hash(P, x.x, x.y - x.x);
-        H[i] = h;
-        rk[i] = (uint16_t)atomicAdd(&s_h[g.seg(h.x)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t x = threadIdx.x; x < nseg; x += PB_THREADS) cnt[(size_t)x * nblk + blockIdx.x] = s_h[x];
-}
-
-struct U32AsU64 {
-    const uint32_t *v;
-    __device__ uint64_t operator()(uint32_t i) const { return v[i]; }
-};
-
-// Scatter pass: record -> its segment's slice of E (order inside a segment is immaterial).
-__global__ __launch_bounds__(PB_THREADS) void k_pb_scatter(const uint2 *__restrict__ sp, uint32_t n, PbGeom g,
-                                                            const uint2 *__restrict__ H, const uint16_t *__restrict__ rk,
-                                                            const uint64_t *__restrict__ off, uint32_t nblk,
-                                                            uint4 *__restrict__ E) {
-    const uint32_t b0 = blockIdx.x * PB_BLK;
-#pragma unroll 4
-    for (uint32_t r = 0; r < PB_PER; ++r) {
-        const uint32_t i = b0 + r * PB_THREADS + threadIdx.x;
-        if (i >= n) break;
-        const uint2 h = H[i];
-        const uint2 x = sp[i];
-        const uint64_t pos = off[(size_t)g.seg(h.x) * nblk + blockIdx.x] + rk[i];
-        E[pos] = make_uint4(g.fp(h), x.x, i, x.y - x.x);
-    }
-}
-
-// Fill pass: one block per segment inserts the segment's records into its LDS slots, then
-// writes all 2^sb slots (empty ones as zeros: the table needs no memset). A segment with no
-// free slot left sets *err (the caller falls back to the radix pipeline).
-__global__ __launch_bounds__(256) void k_pb_fill(const uint4 *__restrict__ E, const uint64_t *__restrict__ off,
-                                                 uint32_t nblk, uint32_t n, PbGeom g, uint4 *__restrict__ T,
-                                                 uint32_t *__restrict__ err) {
-    __shared__ uint32_t s_fp[1u << PB_SB], s_st[1u << PB_SB], s_ix[1u << PB_SB], s_ln[1u << PB_SB];
-    const uint32_t S = 1u << g.sb, seg = blockIdx.x, nseg = 1u << (g.tb - g.sb);
-    for (uint32_t x = threadIdx.x; x < S; x += 256) s_fp[x] = 0;
-    __syncthreads();
-    const uint64_t e0 = off[(size_t)seg * nblk];
-    const uint64_t e1 = (seg + 1 < nseg) ? off[(size_t)(seg + 1) * nblk] : (uint64_t)n;
-    if (e1 - e0 >= S) {
-        if (threadIdx.x == 0) *err = 1u;
-        return;
-    }
-    for (uint64_t q = e0 + threadIdx.x; q < e1; q += 256) {
-        const uint4 e = E[q];
-        uint32_t at = e.x & (S - 1u);
-        for (;;) {
-            if (atomicCAS(&s_fp[at], 0u, e.x) == 0u) break;
-            at = (at + 1u) & (S - 1u);
-        }
-        s_st[at] = e.y;
-        s_ix[at] = e.z;
-        s_ln[at] = e.w;
-    }
-    __syncthreads();
-    uint4 *out = T + (size_t)seg * S;
-    for (uint32_t x = threadIdx.x; x < S; x += 256)
-        out[x] = s_fp[x] ? make_uint4(s_fp[x], s_st[x], s_ix[x], s_ln[x]) : make_uint4(0u, 0u, 0u, 0u);
-}
-
-// new[i] = record i of cur is not in the prior; a found prior record j gets pflag[j] = 1
-// (plain byte stores: every writer stores the same value).
-__global__ __launch_bounds__(256) void k_probe_lookup(const uint8_t *__restrict__ C, const uint2 *__restrict__ csp,
-                                                      uint32_t n, const uint8_t *__restrict__ P, PbGeom g,
-                                                      const uint4 *__restrict__ T, uint8_t *__restrict__ pflag,
-                                                      uint8_t *__restrict__ fresh) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint2 x = csp[i];
-    const uint32_t len = x.y - x.x;
-    const uint2 h = rec_hash(C, x.x, len);
-    const uint32_t fp = g.fp(h), S = 1u << g.sb;
-    const uint4 *seg = T + (size_t)g.seg(h.x) * S;
-    uint32_t at = g.home(h.x);
-    bool found = false;
-    for (uint32_t k = 0; k < S; ++k) {  // a segment always keeps a free slot (k_pb_fill)
-        const uint4 e = seg[at];
-        if (e.x == 0u) break;
-        if (e.x == fp && e.w == len && rec_equal_w(C, x.x, x.y, P, e.y, e.y + len, 0u)) {
-            found = true;
-            pflag[e.z] = 1;
-            break;
-        }
-        at = (at + 1u) & (S - 1u);
-    }
-    fresh[i] = found ? 0 : 1;
-}
-
-__global__ __launch_bounds__(256) void k_gather_sk(const uint32_t *__restrict__ idx, uint32_t n,
-                                                   const uint2 *__restrict__ sp, const uint64_t *__restrict__ K,
-                                                   uint2 *__restrict__ osp, uint64_t *__restrict__ oK) {
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const uint32_t i = idx[k];
-        osp[k] = sp[i];
-        oK[k] = K[i];
-    }
-}
-
-// Merged output order: prior record j (kept iff its bit is set) and new record k placed
-// right before prior record ins[k] (ins non-decreasing, n_p = after the last), so new record
-// k sits at merged position pos(k) = k + ins[k] (strictly increasing). kb[t] = the number
-// of new records before merged position t * EM_TILE: one wave per tile boundary, a 64-ary
-// search over pos (as k_diff_split).
-__global__ __launch_bounds__(256) void k_merge_split(const uint32_t *__restrict__ ins, uint32_t nu, uint32_t nb,
-                                                     uint32_t *__restrict__ kb) {
-    const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const uint32_t lane = lane_id();
-    if (t >= nb) return;
-    const uint64_t m0 = (uint64_t)t * EM_TILE;
-    uint32_t lo = 0, hi = nu;  // first k with pos(k) >= m0, in [lo, hi]
-    while (hi > lo) {
-        const uint32_t span = hi - lo;
-        if (span <= 64) {
-            const uint32_t p = lo + lane;
-            const bool ge = (p >= hi) || (uint64_t)p + ins[p] >= m0;
-            const uint64_t m = __ballot(ge);
-            lo = m ? lo + (uint32_t)(__ffsll((long long)m) - 1) : hi;  // span 64, all below: hi
-            break;
-        }
-        const uint32_t p = lo + (uint32_t)(((uint64_t)span * (lane + 1)) / 65);
-        const bool ge = (uint64_t)p + ins[p] >= m0;
-        const uint64_t m = __ballot(ge);
-        if (!m) {
-            lo = (uint32_t)__shfl((int)p, 63, 64) + 1;
-        } else {
-            const int f = __ffsll((long long)m) - 1;
-            const uint32_t pf = (uint32_t)__shfl((int)p, f, 64);
-            const uint32_t pp = (uint32_t)__shfl((int)p, f > 0 ? f - 1 : 0, 64);
-            hi = pf;
-            if (f > 0) lo = pp + 1;
-        }
-    }
-    if (lane == 0) kb[t] = lo;
-}
-
-// One block per EM_TILE merged positions: each position's item (start | source bit, length)
-// or a dropped prior record, written as the emit cache, and the tile's (count, bytes) total
-// (k_emit_count's job, so the merged output goes straight to the emit apply pass).
-constexpr uint32_t MG_PER = EM_TILE / 256;
-__global__ __launch_bounds__(256) void k_merge_items(const uint2 *__restrict__ psp, uint32_t np,
-                                                     const uint8_t *__restrict__ pflag, const uint2 *__restrict__ usp,
-                                                     const uint32_t *__restrict__ ins, const uint32_t *__restrict__ kb,
-                                                     uint32_t M, uint2 *__restrict__ cache, uint64_t *__restrict__ tot) {
-    __shared__ uint8_t s_take[EM_TILE];
-    __shared__ uint32_t s_red[4];
-    __shared__ uint64_t s_r64[4];
-    const uint32_t t = threadIdx.x, tile = blockIdx.x;
-    const uint32_t m0 = tile * EM_TILE;
-    const uint32_t k0 = kb[tile], k1 = kb[tile + 1];
-    for (uint32_t x = t; x < EM_TILE; x += 256) s_take[x] = 0;
-    __syncthreads();
-    for (uint32_t k = k0 + t; k < k1; k += 256) s_take[k + ins[k] - m0] = 1;
-    __syncthreads();
-    // thread t: positions m0 + MG_PER*t .. + MG_PER - 1
-    uint32_t tk = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < MG_PER; ++q) tk += s_take[MG_PER * t + q];
-    uint32_t ttot;
-    uint32_t before = block_excl_scan<256>(tk, &ttot, s_red);  // new records before my first
-    uint64_t sum = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < MG_PER; ++q) {
-        const uint32_t lm = MG_PER * t + q, m = m0 + lm;
-        if (m >= M) break;
-        uint2 it;
-        if (s_take[lm]) {
-            const uint2 u = usp[k0 + before];
-            it = make_uint2(u.x | 0x80000000u, u.y - u.x);
-            ++before;
-        } else {
-            const uint32_t j = (m0 - k0) + (lm - before);
-            const uint2 p = psp[j];
-            const bool keep = pflag[j] != 0;
-            it = make_uint2(p.x, keep ? p.y - p.x : EM_DROP);
-        }
-        cache[m] = it;
-        sum += (it.y != EM_DROP) ? (EM_ONE | (uint64_t)(it.y + 1u)) : 0ull;
-    }
-    sum = wave_sum(sum);
-    if (lane_id() == 0) s_r64[t >> 6] = sum;
-    __syncthreads();
-    if (t == 0) tot[tile] = s_r64[0] + s_r64[1] + s_r64[2] + s_r64[3];
-}
-
-template <uint32_t WIN>
-__global__ __launch_bounds__(EM_BLOCK) void k_emit_merge(const uint2 *__restrict__ cache, uint32_t n,
-                                                         const uint64_t *__restrict__ pre, const uint8_t *__restrict__ srcP,
-                                                         const uint8_t *__restrict__ srcU, uint8_t *__restrict__ dst) {
-    emit_apply_body<true, WIN, true>(cache, n, pre, srcP, srcU, dst, nullptr, nullptr, nullptr, 0);
-}
-
 // ------------------------------------------------------------------ host pipeline
 int select_flags(sg_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out_idx, uint32_t *count) {
     return run_select2(c, "select", FlagPred{flags}, n, out_idx, (uint32_t *)nullptr, count, nullptr);
@@ -1127,7 +808,7 @@ static int emit_records(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans, con
     }
     // model: each output byte read once and written once, plus the cached (start, len)
     SG_LAUNCH_B(c, "emit_lines", 2.0 * nb + 8.0 * count, k_emit_apply, ntiles, EM_BLOCK, 0, cache, count, pre, d_buf,
-                *d_out, (uint2 *)nullptr, (const uint64_t *)nullptr, (uint64_t *)nullptr, 0);
+                *d_out, (uint2 *)nullptr, (const uint64_t *)nullptr, (uint64_t *)nullptr);
     *bytes = nb;
     return SG_OK;
 }
@@ -1423,7 +1104,6 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, S_DUP, R, &dup));
     SG_TRY(slot(c, S_BAD, R, &segbad));
     SG_TRY(slot(c, S_SEL, (size_t)R / 2 + 16, &hs));
-    static const int materialize = getenv("SG_MATERIALIZE") ? atoi(getenv("SG_MATERIALIZE")) : 0;
     // adjacent equality inside segments; segments holding two different records -> sort.
     // model: key0 + brk + span per record, both records' bytes where compared, dup out
     auto adjacent_and_heads = [&](const uint8_t *Sb, const uint2 *SSp, uint64_t **seg_total) -> int {
@@ -1455,7 +1135,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // Without a materialised copy the adjacent pass and the segment-head select are queued
     // before the group count comes back (one host sync for both counts); when big groups
     // exist (the 7-byte key was kept: low-entropy text) they wait for the refinement instead.
-    const bool speculate = !materialize && (base >> 16) < 7u;
+    const bool speculate = (base >> 16) < 7u;
     if (speculate) SG_TRY(adjacent_and_heads(d_buf, V, &stot));
     SG_TRY(read2(gtot, stot, &B, &B2, &ns, &nb));
     if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
@@ -1466,20 +1146,9 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // gather from the input. Measured cheaper than materialising a sorted copy first (C2
     // 2.51 -> 2.30 ms, X1 4.37 -> 3.97 ms): the copy gathered every record once and the
     // unique emit copied ~2/3 of them again, where gathering only the unique records reads
-    // each kept record once. SG_MATERIALIZE=1 restores the copy (S contiguous, SS spans into it).
-    uint8_t *Sb;
-    uint2 *SS;
-    if (materialize) {
-        SG_TRY(slot(c, S_SSPANS, R, &SS));
-        SG_TRY(slot(c, S_SBUF, (size_t)n + 64, &Sb));
-        uint64_t *pc;
-        // model: input bytes read + S written once; cached span per record in, span per record out
-        SG_TRY(run_emit(c, k_emit_sorted, "emit_sorted", "emit_sorted.count", S_EMIT, PermItem{nullptr, V}, R, d_buf, Sb, SS,
-                        nullptr, nullptr, &pc, 2.0 * (double)n + 16.0 * R));
-    } else {
-        Sb = const_cast<uint8_t *>(d_buf);
-        SS = V;  // the segment sorts permute it in place
-    }
+    // each kept record once.
+    uint8_t *Sb = const_cast<uint8_t *>(d_buf);
+    uint2 *SS = V;  // the segment sorts permute it in place
     if (!speculate || B) {
         SG_TRY(adjacent_and_heads(Sb, SS, &stot));
         uint32_t d0, d1;
@@ -1538,154 +1207,6 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     return SG_OK;
 }
 
-// The probe path (see the kernels above). Lc/Lp: both buffers parsed, keyed with bk (the
-// common prefix and key width every later compare uses); the prior is strictly increasing.
-// *used = false: the prior does not fit the table's bounds (a segment without a free slot,
-// more segments than the count pass's LDS histogram): nothing was changed, the caller runs
-// the radix pipeline.
-static int probe_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const Lines &Lc, const uint8_t *d_prior,
-                            uint64_t n_prior, const Lines &Lp, uint32_t bk, sg_dev_result *res, const OutBuf *ou,
-                            const OutBuf *of, bool *used) {
-    *used = false;
-    const uint32_t R = Lc.n_rec, NP = Lp.n_rec;
-    // table slots per prior record (>= 1.25: a load <= 0.8, so the longest probe runs stay
-    // short) and the fingerprint mask: tests shrink both (SG_PROBE_SLOTS, SG_PROBE_FPMASK)
-    const char *e_sl = getenv("SG_PROBE_SLOTS"), *e_fp = getenv("SG_PROBE_FPMASK");
-    const double load = e_sl ? std::max(1.01, atof(e_sl)) : 1.25;
-    PbGeom g;
-    g.fpm = e_fp ? (uint32_t)strtoul(e_fp, nullptr, 0) : 0xffffffffu;
-    g.tb = 4;
-    while ((double)(1ull << g.tb) < load * NP + 1.0) ++g.tb;
-    const char *e_sb = getenv("SG_PROBE_SEGBITS");  // tests: tiny segments overflow -> radix
-    g.sb = std::min(g.tb, e_sb ? std::max(1u, std::min(PB_SB, (uint32_t)atoi(e_sb))) : PB_SB);
-    const uint32_t nseg = 1u << (g.tb - g.sb);
-    if (g.tb > 31 || nseg > PB_MAXSEG) return SG_OK;
-    const uint32_t nblk = (NP + PB_BLK - 1) / PB_BLK;
-    const size_t nc = (size_t)nseg * nblk;
-    uint4 *T, *E;
-    uint2 *H;
-    uint16_t *rk;
-    uint32_t *cnt, *err;
-    uint64_t *off;
-    uint8_t *pflag, *nf;
-    SG_TRY(slot(c, S_PB_TAB, (size_t)1 << g.tb, &T));
-    SG_TRY(slot(c, S_PB_E, NP, &E));
-    SG_TRY(slot(c, S_PB_H, NP, &H));
-    SG_TRY(slot(c, S_PB_RK, NP, &rk));
-    SG_TRY(slot(c, S_PB_CNT, nc, &cnt));
-    SG_TRY(slot(c, S_PB_OFF, nc, &off));
-    SG_TRY(slot(c, S_PB_ERR, 1, &err));
-    SG_TRY(slot(c, S_PB_BITS, NP, &pflag));
-    SG_TRY(slot(c, S_PB_NEW, R, &nf));
-    SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
-    SG_HIP(hipMemsetAsync(pflag, 0, NP, c->stream));
-    // model: prior records + spans read, hash pair + rank written
-    SG_LAUNCH_B(c, "probe_count", (double)n_prior + 18.0 * NP, k_pb_count, nblk, PB_THREADS, nseg * 4, d_prior, Lp.spans,
-                NP, g, H, rk, cnt, nblk);
-    {
-        const uint32_t nt = (uint32_t)((nc + SCAN_TILE - 1) / SCAN_TILE);
-        uint64_t *tp;
-        SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
-        SG_LAUNCH(c, "scan.count", k_scan64_count<U32AsU64>, nt, SCAN_BLOCK, 0, U32AsU64{cnt}, (uint32_t)nc, tp);
-        SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
-        SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64>, nt, SCAN_BLOCK, 0, U32AsU64{cnt}, (uint32_t)nc, tp + nt, off);
-    }
-    // model: hash pair + rank + span read, one 16-B entry written
-    SG_LAUNCH_B(c, "probe_scatter", 34.0 * NP, k_pb_scatter, nblk, PB_THREADS, 0, Lp.spans, NP, g, H, rk, off, nblk, E);
-    // model: entries read, the whole table written
-    SG_LAUNCH_B(c, "probe_fill", 16.0 * NP + 16.0 * (double)(1ull << g.tb), k_pb_fill, nseg, 256, 0, E, off, nblk, NP, g, T,
-                err);
-    // model: cur records + spans read, a 16-B slot and the prior record per found record, a flag
-    SG_LAUNCH_B(c, "probe_lookup", (double)n_cur + 25.0 * R, k_probe_lookup, grid_for(R, 256), 256, 0, d_cur, Lc.spans, R,
-                d_prior, g, T, pflag, nf);
-    // the new records (not in the prior): their count comes back with the table's error word
-    uint32_t *idx;
-    SG_TRY(slot(c, S_PB_IDX, R, &idx));
-    uint64_t *stot;
-    SG_TRY(run_select2_nb(c, "probe_select", FlagPred{nf}, R, idx, nullptr, S_PB_STAT, &stot));
-    uint32_t nn = 0;
-    {
-        uint8_t *pin = (uint8_t *)c->pinned;
-        SG_HIP(hipMemcpyAsync(pin, stot, 8, hipMemcpyDeviceToHost, c->stream));
-        SG_HIP(hipMemcpyAsync(pin + 8, err, 4, hipMemcpyDeviceToHost, c->stream));
-        SG_HIP(hipStreamSynchronize(c->stream));
-        uint64_t tv = 0;
-        uint32_t ev = 0;
-        memcpy(&tv, pin, 8);
-        memcpy(&ev, pin + 8, 4);
-        if (ev) return SG_OK;  // a full segment: the radix pipeline instead
-        nn = (uint32_t)(tv >> 31);
-    }
-    *used = true;
-    // the new records, sorted and deduplicated: the fresh output (into the caller's buffer)
-    OutBuf fo;
-    if (of) {
-        fo = *of;
-    } else {
-        uint8_t *fb;
-        SG_TRY(slot(c, S_OUT_FRESH, (size_t)n_cur + 64, &fb));
-        fo = OutBuf{fb, (size_t)n_cur + 64};
-    }
-    UView nu;
-    nu.buf = fo.base();
-    if (nn) {
-        Lines Ls;
-        SG_TRY(slot(c, S_PB_SP, nn, &Ls.spans));
-        SG_TRY(slot(c, S_PB_K, nn, &Ls.keys));
-        Ls.n_rec = nn;
-        SG_LAUNCH_B(c, "probe_gather", 20.0 * nn, k_gather_sk, grid_for(nn, 256, 4096), 256, 0, idx, nn, Lc.spans, Lc.keys,
-                    Ls.spans, Ls.keys);
-        SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &nu, &Ls, bk, &fo, nullptr));
-    }
-    if ((uint64_t)nu.bytes + 16 >= (1ull << 31)) { set_error("probe: new records exceed 2 GiB"); return SG_E_TOO_LARGE; }
-    // each new record's insertion point in the prior
-    uint32_t *ins;
-    SG_TRY(slot(c, S_PB_INS, (size_t)nu.n + 1, &ins));
-    if (nu.n) {
-        const uint32_t ntiles = (nu.n + DF_TILE - 1) / DF_TILE;
-        uint32_t *jb;
-        SG_TRY(slot(c, S_R_OFF, (size_t)ntiles + 2, &jb));
-        SG_LAUNCH(c, "diff_split", k_diff_split, grid_for(ntiles + 1, 4), 256, 0, nu.keys, nu.n, Lp.keys, NP, ntiles + 1, jb);
-        RecSet U{nu.buf, nu.spans, nu.keys, nu.n};
-        RecSet P{d_prior, Lp.spans, Lp.keys, NP};
-        SG_LAUNCH_B(c, "ins_tile", 16.0 * nu.n + 8.0 * NP, k_ins_tile, ntiles, 256, 0, U, P, jb, ins, bk);
-    }
-    // the merged unique output
-    const uint32_t M = NP + nu.n;
-    const uint32_t mt = (M + EM_TILE - 1) / EM_TILE;
-    uint32_t *kb;
-    SG_TRY(slot(c, S_PB_KB, (size_t)mt + 2, &kb));
-    SG_LAUNCH(c, "merge_split", k_merge_split, grid_for(mt + 1, 4), 256, 0, ins, nu.n, mt + 1, kb);
-    uint2 *cache;
-    SG_TRY(slot(c, S_PB_MI, (size_t)M + 1, &cache));
-    uint64_t *tp;
-    SG_TRY(slot(c, S_PB_STAT, 2 * (size_t)mt + 4, &tp));
-    uint64_t *tot = tp, *pre = tp + mt, *total = tp + 2 * (size_t)mt;
-    SG_LAUNCH_B(c, "merge_items", 13.0 * M, k_merge_items, mt, 256, 0, Lp.spans, NP, pflag, nu.spans, ins, kb, M,
-                cache, tot);
-    SG_TRY(tile_scan(c, tot, mt, pre, total, ou ? ou->shift() : 0u));
-    uint8_t *ub;
-    if (ou) ub = ou->base();
-    else SG_TRY(slot(c, S_OUT_UNIQ, (size_t)n_cur + 64, &ub));
-    const bool shortr = n_prior <= 40ull * NP;
-    if (shortr)
-        SG_LAUNCH(c, "emit_merge", k_emit_merge<EM_WIN_S>, mt, EM_BLOCK, 0, cache, M, pre, d_prior, nu.buf, ub);
-    else
-        SG_LAUNCH(c, "emit_merge", k_emit_merge<EM_WIN>, mt, EM_BLOCK, 0, cache, M, pre, d_prior, nu.buf, ub);
-    uint64_t tt = 0;
-    SG_TRY(ctx_readback(c, &tt, total, 8));
-    if (c->profile) prof_bytes(c, "emit_merge", 8.0 * M + 2.0 * (double)(uint32_t)tt);
-    res->in_records = R;
-    res->uniq = ou ? ou->p : ub;
-    res->uniq_bytes = (uint32_t)tt;
-    res->uniq_records = (uint32_t)(tt >> 32);
-    res->prior_records = NP;
-    res->fresh = of ? of->p : fo.base();
-    res->fresh_bytes = nu.bytes;
-    res->fresh_records = nu.n;
-    c->last_path = SG_PATH_PROBE;
-    return SG_OK;
-}
 
 // cur_lcp (with cur_pre): a device word already holding the common prefix of cur's records
 // vs cur's first record (computed where the records were gathered), so cur is not scanned
@@ -1723,8 +1244,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint8_t *rbuf = ref_cur ? d_cur : d_prior;
     const uint2 *rsp = ref_cur ? Lc.spans : (have_prior ? Lp.spans : nullptr);
     const uint64_t *rkeys = ref_cur ? Lc.keys : (have_prior ? Lp.keys : nullptr);
-    static const int narrow_env = getenv("SG_NARROW_KEYS") ? atoi(getenv("SG_NARROW_KEYS")) : 1;
-    const bool want_hist = narrow_env && Lc.n_rec >= 4096;
+    const bool want_hist = Lc.n_rec >= 4096;
     const uint32_t *dhist = nullptr;
     const bool fuse_hist = want_hist && rsp && Lc.n_rec && !cur_lcp;
     if (fuse_hist) {
@@ -1808,15 +1328,6 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     }
     c->last_kw = kw;
     const uint32_t bk = make_bk(base, kw);
-    // a sorted prior: look the current records up in it (only the new ones are sorted).
-    // Opt-in (SG_PROBE=1): measured slower than the radix pipeline
-    const char *e_pb = getenv("SG_PROBE");
-    if (e_pb && atoi(e_pb) && have_prior && prior_sorted && Lp.n_rec >= 1 && Lc.n_rec >= 1 && n_prior < (1ull << 31) &&
-        n_cur < (1ull << 31)) {
-        bool used = false;
-        SG_TRY(probe_dedup_diff(c, d_cur, n_cur, Lc, d_prior, n_prior, Lp, bk, res, ou, of, &used));
-        if (used) return SG_OK;
-    }
     if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, bk));
     UView cu;
     SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, cur_hist));
@@ -1900,22 +1411,11 @@ int dev_dedup_diff_lines(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const 
     return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, true, res, &cur, nullptr, nullptr, cur_lcp);
 }
 
-// Dedup+diff entry: the bucket sample sort when there is a prior scan to take splitters from
-// and the input is large enough (sg_bucket.hip), else — or when the bucket path meets input
-// outside its LDS bounds — the radix pipeline above.
+// Dedup+diff entry (the radix pipeline above).
 int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior,
                    uint64_t n_prior, bool want_fresh, sg_dev_result *res) {
     c->last_path = 0;
     c->last_flags = 0;
-    if (want_fresh && d_prior && n_prior) {
-        bool used = false;
-        *res = sg_dev_result{};
-        SG_TRY(bucket_dedup_diff(c, d_cur, n_cur, d_prior, n_prior, res, &used));
-        if (used) {
-            c->last_path = 1;
-            return SG_OK;
-        }
-    }
     return dev_dedup_diff_radix(c, d_cur, n_cur, d_prior, n_prior, want_fresh, res);
 }
 

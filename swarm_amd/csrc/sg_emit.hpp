@@ -319,8 +319,7 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
                                                 const uint8_t *__restrict__ src, const uint8_t *__restrict__ src2,
                                                 uint8_t *__restrict__ dst,
                                                 uint2 *__restrict__ out_spans,
-                                                const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
-                                                int dbg) {
+                                                const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4][WIN];
     __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
     __shared__ uint64_t s_wt[4];
@@ -366,7 +365,6 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
             s_cln[wid][e] = ln[r];
             s_co[wid][e] = o;
         }
-        if (dbg & 1) return;  // probe mode: no copy (timing only)
         const uint32_t kept = (uint32_t)(run >> 32);
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -397,7 +395,6 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
             if (out_spans) out_spans[j] = make_uint2((uint32_t)o, (uint32_t)o + ln[r]);
             if (kout) kout[j] = kin[wbase + r * 64u + lane];
         }
-        if (dbg & 1) continue;  // probe mode: no copy (timing only)
         const uint32_t first = (uint32_t)(__ffsll((long long)m) - 1);
         const uint32_t last = 63u - (uint32_t)__clzll((long long)m);
         const uint64_t o0 = __shfl(o, (int)first, 64);
@@ -416,10 +413,9 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
     __global__ __launch_bounds__(EM_BLOCK) void NAME(                                               \
         const uint2 *__restrict__ cache, uint32_t n, const uint64_t *__restrict__ pre,              \
         const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, uint2 *__restrict__ out_spans,  \
-        const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout, int dbg) {                   \
-        emit_apply_body<SPARSE, WIN>(cache, n, pre, src, nullptr, dst, out_spans, kin, kout, dbg);  \
+        const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout) {                            \
+        emit_apply_body<SPARSE, WIN>(cache, n, pre, src, nullptr, dst, out_spans, kin, kout);       \
     }
-SG_EMIT_APPLY(k_emit_sorted, false, EM_WIN)
 SG_EMIT_APPLY(k_emit_uniq, true, EM_WIN)
 SG_EMIT_APPLY(k_emit_uniq_s, true, EM_WIN_S)
 SG_EMIT_APPLY(k_emit_fresh, true, EM_WIN)

@@ -70,14 +70,9 @@ int dev_dedup_diff_into(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const u
 int serialize_into(sg_ctx *c, const uint8_t *d_buf, const uint2 *spans,
                    const uint32_t *recs, uint32_t count, uint8_t *dst, size_t dst_cap, uint64_t *bytes);
 
-// A7+A8 on device buffers (sg_dedup.hip): bucket sample sort or radix pipeline.
+// A7+A8 on device buffers (sg_dedup.hip): the radix pipeline.
 int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior, uint64_t n_prior,
                    bool want_fresh, sg_dev_result *res);
-
-// Bucket sample sort dedup+diff (sg_bucket.hip). *used = false: declined or outside its
-// bounds (the caller runs the radix pipeline).
-int bucket_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_t *d_prior, uint64_t n_prior,
-                      sg_dev_result *res, bool *used);
 
 // A4 matching of a device line buffer (sg_match.hip); want_lines = false skips the grep
 // output (hits only).

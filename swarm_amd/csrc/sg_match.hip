@@ -14,6 +14,7 @@
 // radix-sorted and de-duplicated, so hits come out sorted by (record, signature) and the
 // matched lines in input order (grep's output).
 #include "sg_internal.hpp"
+#include "sg_switches.hpp"
 #include "sg_prims_host.hpp"
 
 #include <algorithm>
@@ -272,9 +273,8 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
                 b = 8 * (c + 1);
             } else {
                 b = 10;
-                static const uint32_t cap4 = getenv("SG_LIT_BITS4") ? (uint32_t)atoi(getenv("SG_LIT_BITS4")) : 18u;
-                const uint32_t extra = getenv("SG_LIT_EXTRA") ? (uint32_t)atoi(getenv("SG_LIT_EXTRA")) : extra_bits;
-                while (b < (c == 2 ? 15u : cap4) && (1ull << b) < (64ull << extra) * cnt[c]) ++b;
+                constexpr uint32_t cap4 = 18u;
+                while (b < (c == 2 ? 15u : cap4) && (1ull << b) < (64ull << extra_bits) * cnt[c]) ++b;
             }
         }
         T->bits[c] = b;
@@ -344,7 +344,7 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         for (uint32_t o = 0; o <= last && o < 256; ++o) {  // anchor fits the bucket record's 8 bits
             const uint32_t lo = word_at(i, o, L), hi = (L == 8) ? word_at(i, o + 4, 4) : 0u;
             const uint32_t h = lit_h(lo, hi, c, T->bits[c]);
-            static const uint32_t w_share = getenv("SG_LIT_SHARE_W") ? (uint32_t)atoi(getenv("SG_LIT_SHARE_W")) : 64u;
+            constexpr uint32_t w_share = 64u;  // cost of one more pattern sharing the gram
             const uint64_t cost = (uint64_t)(std::max(shared_by(i, o, L), 1u) - 1) * w_share + (uint64_t)load[c][h] * 16 +
                                   gram_commonness(&T->pat[T->pat_off[i] + o], L);
             if (cost < best) { best = cost; anc[i] = o; hb[i] = h; fp[i] = lit_fp(lo, hi, c); }
@@ -447,8 +447,7 @@ static void free_dev(sg_matcher *h) {
 static int build_packs(sg_matcher *h) {
     h->packed.assign(h->tables.size(), 0);
     if (h->kind != 1) return SG_OK;
-    // test/tuning knob: a smaller pack budget (bytes) trades re-walking the bytes for occupancy
-    const uint32_t budget = getenv("SG_DFM_LDS") ? std::min<uint32_t>(DFM_LDS, (uint32_t)atoi(getenv("SG_DFM_LDS"))) : DFM_LDS;
+    const uint32_t budget = DFM_LDS;
     sg_matcher::DfaPack cur;
     std::vector<uint32_t> cls4(256, 0);
     std::vector<uint16_t> hot;
@@ -682,8 +681,6 @@ struct LitArgs {
     const uint32_t *fac_off, *fac_pids;  // regex prefilter expansion (else null)
     uint2 *spans_out;                    // non-null: also write the parse's record spans (fused A3)
     uint8_t *rec_flag;                   // non-null: mark matched records here instead of listing hits
-    unsigned long long *dbg;             // SG_LIT_DEBUG: {candidates, fingerprint matches, hits}
-    uint32_t dbg_mode;                   // bit 0: skip pass 2, bit 1: skip pass 1 probes
 };
 
 constexpr uint32_t LS_HB = 256;    // per-block LDS hit buffer (entries)
@@ -751,7 +748,6 @@ __device__ __forceinline__ bool lit_verify(const Args &a, const uint8_t *s_tile,
 
 template <class Args, class Push>
 __device__ __forceinline__ void lit_emit(const Args &a, Push &push, uint32_t rec, uint32_t pid) {
-    if (a.dbg) atomicAdd(&a.dbg[2], 1ull);
     if (a.rec_flag) {  // idempotent byte store: the set of matched records, no list
         a.rec_flag[rec] = 1;
         return;
@@ -902,7 +898,6 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
         }
         // pass 1: bitmap probes
         uint64_t cand[LIT_CLASSES] = {};
-        if (!(a.dbg_mode & 2u))
 #pragma unroll
         for (int b = 0; b < BPT; ++b) {
             const int i0 = b >> 2;
@@ -928,21 +923,6 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
             const uint64_t valid = (my0 >= n) ? 0ull : ((1ull << (n - my0)) - 1);
 #pragma unroll
             for (uint32_t c = 0; c < LIT_CLASSES; ++c) cand[c] &= valid;
-        }
-        if (a.dbg_mode & 1u) {
-            uint32_t cc = 0;
-#pragma unroll
-            for (uint32_t c = 0; c < LIT_CLASSES; ++c) cc += (uint32_t)__popcll(cand[c]);
-            if (cc == 0xffffffffu) a.hits[0] = 0;  // keep pass 1 live
-#pragma unroll
-            for (uint32_t c = 0; c < LIT_CLASSES; ++c) cand[c] = 0;
-        }
-        if (a.dbg) {
-            uint32_t cc = 0;
-#pragma unroll
-            for (uint32_t c = 0; c < LIT_CLASSES; ++c) cc += (uint32_t)__popcll(cand[c]);
-            cc = wave_sum(cc);
-            if (lane_id() == 0 && cc) atomicAdd(&a.dbg[0], (unsigned long long)cc);
         }
         // pass 2: queue the tile's candidates, then confirm/verify them across all lanes
         uint32_t ncand = 0;
@@ -1025,7 +1005,6 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
                     const uint32_t rec = s_base + (ent & 0x3fffu) - 1;
                     const uint64_t p = base + q;
                     if (br[u].x == fpv[u]) {
-                        if (a.dbg) atomicAdd(&a.dbg[1], 1ull);
                         if (lit_verify(a, s_tile, base, TILE, p, br[u].z >> 24, br[u].z & 0xffffffu, br[u].w & 0x7fffffffu,
                                        c, r0w[u], r1w[u]))
                             lit_emit(a, push, rec, br[u].y);
@@ -1636,7 +1615,6 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     // prefilter candidates (regex plans): factor filter -> (record, pattern) pairs
     unsigned long long *cand = nullptr;
     uint32_t n_cand = 0;
-    static const int ls_block_env = getenv("SG_LS_BLOCK") ? atoi(getenv("SG_LS_BLOCK")) : 0;
     auto run_lit = [&](const char *name, const sg_matcher::Lit &Lt, unsigned long long *out, uint32_t *counter,
                        uint32_t ocap, const uint32_t *fo, const uint32_t *fp) -> int {
         LitArgs a{};
@@ -1652,14 +1630,6 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
         a.spans_out = (fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
         a.rec_flag = mf ? mf->flags : nullptr;
-        static const int dbg_mode = getenv("SG_LIT_DEBUG") ? atoi(getenv("SG_LIT_DEBUG")) : -1;
-        unsigned long long *dbg = nullptr;
-        if (dbg_mode >= 0) a.dbg_mode = (uint32_t)dbg_mode;  // bit 0 skip pass 2, bit 1 skip pass 1, bit 3 count
-        if (dbg_mode >= 0 && (dbg_mode & 8)) {
-            SG_TRY(slot(c, S_M_TMP2, 4, &dbg));
-            SG_HIP(hipMemsetAsync(dbg, 0, 32, c->stream));
-            a.dbg = dbg;
-        }
         const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + 64;
         const uint32_t dyn = lit_lds_bytes(Lt);
         const uint32_t bpc = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
@@ -1668,7 +1638,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         // sets: the regex prefilter), 512-thread blocks double the waves that hide the
         // candidate stage's L2 latency (C4 prefilter 2.71 -> 1.84 ms per 4M banners); with
         // room for 3+ blocks, 256 threads x 64 positions probe faster (C3 1.35 vs 1.54 ms).
-        const int ls_block = ls_block_env ? ls_block_env : (bpc <= 2 ? 512 : 256);
+        const int ls_block = bpc <= 2 ? 512 : 256;
         const int bpt = (int)(L.tile_bytes / ls_block);
         const double bytes = (double)n + 8.0 * R;
         auto launch = [&](auto kern, int blk) -> int {
@@ -1688,13 +1658,6 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         else if (ls_block == 256 && bpt == 32) SG_TRY(by_tmpl(k_lit_scan<256, 32, 0x18u>, k_lit_scan<256, 32, 0x1Cu>, k_lit_scan<256, 32, 0x1Fu>, 256));
         else if (ls_block == 256 && bpt == 64) SG_TRY(by_tmpl(k_lit_scan<256, 64, 0x18u>, k_lit_scan<256, 64, 0x1Cu>, k_lit_scan<256, 64, 0x1Fu>, 256));
         else { set_error("k_lit_scan: unsupported tile geometry"); return SG_E_INVAL; }
-        if (dbg) {
-            unsigned long long d[3];
-            SG_TRY(ctx_readback(c, d, dbg, 24));
-            fprintf(stderr, "[%s] grid=%u lds=%u+%u cand=%llu fp=%llu hits=%llu bm_words=%u classes=%x bits=%u,%u,%u,%u,%u\n",
-                    name, grid, dyn, stat, d[0], d[1], d[2], a.bm_words, a.cls_mask, a.bits[0], a.bits[1], a.bits[2],
-                    a.bits[3], a.bits[4]);
-        }
         return SG_OK;
     };
     if (h->has_pre && R) {
@@ -1714,8 +1677,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     // a wave then walk the same DFA, so its rows are shared in L1/L2 instead of every lane
     // pulling a different automaton's rows from HBM.
     const unsigned long long *vcand = cand;
-    static const bool vsort = !getenv("SG_VERIFY_SORT") || atoi(getenv("SG_VERIFY_SORT")) != 0;
-    if (vsort && n_cand > 4096) {
+    if (n_cand > 4096) {
         int pbits = 1;
         while (pbits < 32 && (1u << pbits) < h->n_pats) ++pbits;
         uint64_t *alt, *KC;
@@ -1738,8 +1700,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
         if (R && h->lit.on) SG_TRY(run_lit("lit_match", h->lit, hits, cnt, (uint32_t)cap, nullptr, nullptr));
         if (R) {
-            const char *dm_env = getenv("SG_DFA_MULTI");
-            const bool multi = !dm_env || atoi(dm_env) != 0;
+            const bool multi = sw_dfa_multi();
             if (multi) {
                 for (const auto &k : h->packs) {
                     DFAMultiArgs a{};
@@ -1797,12 +1758,11 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     // overflows, or with SG_HIT_RADIX=1)
     const unsigned long long *KK = hits;
     bool sorted = false;
-    const char *e_hr = getenv("SG_HIT_RADIX");
     // bucket width: 4096 records, narrower when the hits are dense (about HB_CAP / 2 per bucket)
     uint32_t rb = HB_RBMAX;
     while (rb > 4 && (double)total * (1u << rb) / std::max<uint32_t>(R, 1u) > HB_CAP / 2) --rb;
     const uint32_t nb = (uint32_t)(((uint64_t)R + (1u << rb) - 1) >> rb);
-    if (total > 1 && !(e_hr && atoi(e_hr)) && nb <= 12288) {
+    if (total > 1 && !sw_hit_radix() && nb <= 12288) {
         const uint32_t nblk = std::max<uint32_t>(1u, std::min<uint32_t>(HB_NBLK, (total + 4095) / 4096));
         const size_t nc = (size_t)nb * nblk;
         uint32_t *hcnt, *herr;
@@ -1891,7 +1851,7 @@ int sg_ac_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats
     // would chase dependent HBM/L2 rows on every byte, so it is replaced by the hashed
     // q-gram filter (independent per-position probes, byte compares on bitmap hits).
     const auto &T = m->tables[0];
-    if ((uint64_t)T.n_states * T.n_classes * 2 > AC_HOT_BYTES || getenv("SG_FORCE_LITFILTER")) {
+    if ((uint64_t)T.n_states * T.n_classes * 2 > AC_HOT_BYTES || sw_force_litfilter()) {
         // 128 bitmap bits per pattern: X1 candidates 37M -> 17M per 10M lines for 2 blocks/CU
         rc = build_lit(pats, pat_offs, n_pats, flags, &m->lit, 1u);
         if (rc == SG_E_UNSUPPORTED) {

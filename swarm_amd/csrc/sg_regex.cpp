@@ -1,5 +1,6 @@
 // sg_regex.cpp — regex signatures -> byte-class DFAs for k_dfa_match (see sg_regex.hpp).
 #include "sg_regex.hpp"
+#include "sg_switches.hpp"
 
 #include <stdint.h>
 #include <stdio.h>
@@ -946,8 +947,7 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         }
     }
     plan->single_of_pid.assign(n, 0xffffffffu);
-    // test knob: verify every prefiltered pattern with its anchored DFA
-    const bool force_anchored = getenv("SG_REGEX_ANCHORED") != nullptr;
+    const bool force_anchored = sw_regex_anchored();  // test switch
     std::map<std::string, std::vector<uint32_t>> fac_map;
     std::vector<Pat *> unfiltered;
     // candidate factor sets per pattern; how many patterns could use each string
@@ -1016,17 +1016,8 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         plan->fac_pids.insert(plan->fac_pids.end(), ids.begin(), ids.end());
         plan->fac_off.push_back((uint32_t)plan->fac_pids.size());
     }
-    if (getenv("SG_REGEX_DEBUG")) {
-        fprintf(stderr, "[regex plan] %zu filtered, %zu factors, %zu unfiltered:", plan->singles.size(),
-                plan->factors.size(), unfiltered.size());
-        for (Pat *p : unfiltered) fprintf(stderr, " %u", p->id);
-        fprintf(stderr, "\n");
-    }
     if (!unfiltered.empty()) {
-        int rc = build_pack(unfiltered, 4096, &plan->groups);
-        if (rc == SG_OK && getenv("SG_REGEX_DEBUG"))
-            for (auto &g : plan->groups) fprintf(stderr, "[regex plan] group states=%u classes=%u\n", g.n_states, g.n_classes);
-        return rc;
+        return build_pack(unfiltered, 4096, &plan->groups);
     }
     return SG_OK;
 }

@@ -332,8 +332,7 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     VT *cv = vals, *av = vals_alt;
     bool iota_pending = iota_vals;
     constexpr double VB = (double)sizeof(VT);
-    const char *e_x = getenv("SG_RS_XCD");
-    const bool xcd = e_x ? atoi(e_x) != 0 : true;
+    const bool xcd = true;  // XCD-aware tile order
     const uint32_t grid = xcd ? 8u * ((ntiles + 7u) / 8u) : ntiles;
     if (narrow_kw && begin_bit != 0) { set_error("radix_sort: narrowing needs the keys' bit 0"); return SG_E_INVAL; }
     if (narrow_kw && nlive == 0) live[nlive++] = 0;  // one (no-op) pass still writes the narrowed keys

@@ -1,0 +1,31 @@
+// sg_switches.hpp — the library's ONLY environment reads: test switches that force an
+// alternative engine which is exact on its own, so the parity tests can compare both paths
+// on the same inputs. None changes results; none is a tuning knob (those were removed in
+// round 3 with their losing pipelines, tools/experiments/). Each is read once per process.
+#pragma once
+#include <stdlib.h>
+
+namespace sg {
+
+inline bool env_switch(const char *name, bool dflt) {
+    const char *v = getenv(name);
+    return v ? atoi(v) != 0 : dflt;
+}
+
+// SG_FORCE_LITFILTER=1: literal matchers use the hashed q-gram filter even when the
+// Aho-Corasick automaton fits the LDS hot table (tests/test_gpu_match.py, test_gpu_fused.py).
+inline bool sw_force_litfilter() { return env_switch("SG_FORCE_LITFILTER", false); }
+// SG_DFA_MULTI=0: factor-less regex groups walked one launch per automaton instead of the
+// packed multi-automaton kernel (tests/test_gpu_match.py).
+inline bool sw_dfa_multi() { return env_switch("SG_DFA_MULTI", true); }
+// SG_HIT_RADIX=1: (record, signature) hits sorted by the LSD radix sort instead of the
+// record-bucket LDS sort (tests/test_gpu_match.py).
+inline bool sw_hit_radix() { return env_switch("SG_HIT_RADIX", false); }
+// SG_REGEX_ANCHORED=1: every prefiltered regex verified by its anchored DFA
+// (tests/test_gpu_match.py).
+inline bool sw_regex_anchored() { return env_switch("SG_REGEX_ANCHORED", false); }
+// SG_TM_SORT=1: nuclei templates evaluated through the sort path instead of the
+// record-wave evaluator (tests/test_gpu_templates.py).
+inline bool sw_tm_sort() { return env_switch("SG_TM_SORT", false); }
+
+}  // namespace sg

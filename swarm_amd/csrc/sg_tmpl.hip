@@ -20,6 +20,7 @@
 //   are added for every record without a segment for them (binary search).
 // Output: (record, template) pairs, sorted.
 #include "sg_internal.hpp"
+#include "sg_switches.hpp"
 #include "sg_prims_host.hpp"
 
 #include <algorithm>
@@ -543,8 +544,8 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
     uint64_t n2 = 0;
     uint32_t *seg = nullptr, *flag = nullptr, *sel = nullptr;
     uint64_t *segkey = nullptr;
-    const char *e_ts = getenv("SG_TM_SORT");  // 1: the sort-based evaluation below
-    if (acc.n && h->rec_wave && !(e_ts && atoi(e_ts))) return tm_rec_wave(c, h, D, acc.p, segs, R, res);
+    static const bool tm_sort = sw_tm_sort();  // test switch: the sort-based evaluation below
+    if (acc.n && h->rec_wave && !tm_sort) return tm_rec_wave(c, h, D, acc.p, segs, R, res);
     if (acc.n) {
         const uint32_t n1 = (uint32_t)acc.n;
         uint64_t *k2, *K;

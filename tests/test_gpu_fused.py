@@ -98,24 +98,6 @@ def test_fused_regex_banners(ctx):
     assert u == eu and f == ef and nh == len(hits)
 
 
-def test_fused_bucket_path(ctx, sigs, monkeypatch):
-    """The dedup stage of the fused step served by the bucket sample sort."""
-    import swarm_amd
-    monkeypatch.setenv("SG_BUCKET", "1")
-    monkeypatch.setenv("SG_BUCKET_MIN", "0")
-    monkeypatch.setenv("SG_BUCKET_TARGET", "2000")
-    tails = corpus.httpx_tails(sigs, n_tails=512, seed=9)
-    buf, ids = corpus.httpx_hosts(6000, tails, seed=9)
-    data = buf.tobytes()
-    m = swarm_amd.Matcher(sigs, "literal")
-    prior_all = corpus.httpx_rows(corpus.prior_ids(ids), tails).tobytes()
-    prior = S.dedup(S.matched_lines(prior_all, S.literal_hits(prior_all, sigs)))
-    u, f, _, _, _ = fused(ctx, m, data, prior)
-    eu, ef, _, _ = oracle(data, sigs, prior)
-    assert u == eu and f == ef
-    assert ctx.last_path()[0] == "bucket"
-
-
 @pytest.mark.parametrize("seed", [3, 4])
 def test_fused_flag_path_edge_records(ctx, seed, monkeypatch):
     """The flag path (no hit count): matched records taken in place from the input — empty
