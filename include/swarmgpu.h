@@ -82,11 +82,6 @@ int sg_ctx_last_path(sg_ctx *ctx, int *path, uint32_t *flags);
 /* Sort-key width (bytes after the common prefix, 5..7) the last radix dedup chose from the
  * keys' byte entropies. For tests and benchmarks. */
 int sg_ctx_last_key_width(sg_ctx *ctx, uint32_t *kw);
-/* Bits per key byte of the last radix dedup's sort key: 0 when the key bytes were kept as
- * bytes (narrowed to sg_ctx_last_key_width), else s < 8 — the key's first kw bytes were
- * packed as order-preserving s-bit codes of the byte values cur and prior hold there, so
- * the sort ran ceil(kw * s / 8) digit passes instead of kw. For tests and benchmarks. */
-int sg_ctx_last_key_pack(sg_ctx *ctx, uint32_t *bits);
 
 /* ------------------------------------------------------------------ A3: parse
  * Replaces: nothing in the reference parses module output; it is uploaded verbatim at

@@ -25,7 +25,7 @@ ERRNAMES = {1: "SG_E_INVAL", 2: "SG_E_CAP", 3: "SG_E_HIP", 4: "SG_E_NOMEM", 5: "
 EXPORTS = [
     "sg_last_error", "sg_version", "sg_device_count", "sg_ctx_create", "sg_ctx_destroy",
     "sg_ctx_sync", "sg_ctx_profile", "sg_ctx_profile_only", "sg_ctx_kernel_stat", "sg_ctx_reset_stats", "sg_ctx_memcpy",
-    "sg_ctx_last_path", "sg_ctx_last_key_width", "sg_ctx_last_key_pack", "sg_lines",
+    "sg_ctx_last_path", "sg_ctx_last_key_width", "sg_lines",
     "sg_dedup", "sg_dedup_chunks", "sg_diff", "sg_dedup_diff", "sg_dev_dedup_diff",
     "sg_dev_partition", "sg_hash64", "sg_ac_compile", "sg_dfa_compile", "sg_matcher_info",
     "sg_match", "sg_match_lines", "sg_dev_match", "sg_dev_match_dedup_diff", "sg_free",
@@ -90,7 +90,6 @@ def _load():
         "sg_ctx_memcpy": (C.c_int, [P, P, P, SZ]),
         "sg_ctx_last_path": (C.c_int, [P, C.POINTER(C.c_int), U32P]),
         "sg_ctx_last_key_width": (C.c_int, [P, U32P]),
-        "sg_ctx_last_key_pack": (C.c_int, [P, U32P]),
         "sg_lines": (C.c_int, [U8P, SZ, U64P, SZ, SZP]),
         "sg_dedup": (C.c_int, [U8P, SZ, U8P, SZ, SZP]),
         "sg_dedup_chunks": (C.c_int, [C.POINTER(P), SZP, SZ, U8P, SZ, SZP]),

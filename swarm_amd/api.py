@@ -386,12 +386,6 @@ class Context:
         check(lib.sg_ctx_last_key_width(self._h, C.byref(kw)))
         return kw.value
 
-    def last_key_pack(self) -> int:
-        """Bits per key byte of the last radix dedup's packed sort key (0: bytes kept)."""
-        b = C.c_uint32()
-        check(lib.sg_ctx_last_key_pack(self._h, C.byref(b)))
-        return b.value
-
     def dedup_diff(self, d_cur: int, n_cur: int, d_prior: int = 0, n_prior: int = 0) -> _abi.DevResult:
         """Device pointers in, device result (context-owned) out."""
         r = _abi.DevResult()

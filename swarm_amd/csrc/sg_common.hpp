@@ -19,7 +19,7 @@
 
 #include "../../include/swarmgpu.h"
 
-#define SG_PINNED_BYTES 32768
+#define SG_PINNED_BYTES 16384
 
 namespace sg {
 
@@ -50,7 +50,7 @@ enum Slot : int {
     // dedup / refinement
     S_UNIQ, S_GS, S_GE, S_SEL, S_OFFS, S_OUT_UNIQ, S_OUT_FRESH, S_FRESH_IDX,
     S_R_POS, S_R_KEY, S_R_KEY2, S_R_VAL, S_R_VAL2, S_R_GID, S_R_OFF,
-    S_HIST, S_ALIGN, S_PACK,
+    S_HIST, S_ALIGN,
     // prior
     S_P_STARTS, S_P_ENDS, S_P_KEYS, S_P_REC, S_P_FLAG, S_P_KEYS2, S_P_VALS, S_P_VALS2,
     S_P_UNIQ, S_P_SORTED_KEYS,
@@ -96,8 +96,6 @@ struct sg_ctx {
     uint32_t last_flags = 0;  // always 0 since round 3 (the bucket path's hand-over reasons)
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
-    uint32_t hist_prior[8 * 256] = {};  // dedup: the same for the prior's keys (alphabet packing)
-    uint32_t last_pack_bits = 0;        // dedup: bits per char of the last call's packed key (0: narrowed)
     uint64_t pt_keep_recs = 0;  // piece partition: records the last call kept between its passes
     // pinned staging for host-to-device uploads on the context stream (ctx_upload): grown on
     // demand; up_ev marks the last upload's copy so the buffer is not rewritten under it
@@ -164,25 +162,6 @@ void prof_bytes(sg_ctx *c, const char *name, double bytes);
         SG_LAUNCH(ctx, name, kernel, grid, block, lds, __VA_ARGS__);                  \
         if ((ctx)->profile) ::sg::prof_bytes((ctx), (name), (double)(bytes));         \
     } while (0)
-
-// ------------------------------------------------------------------ key packing
-// The dedup's alphabet packing (sg_dedup.hip choose_pack): the sort's first live pass
-// applies it as it reads the keys (sg_sort.hip), k_pack_keys to the prior's: the first m key bytes (past the record's end: 0) as s-bit codes
-// (code[byte] >= 1, order-preserving) above the tag, the tag clamped to m + 1. Same order and
-// equality as the m-byte narrowed key, in m * s bits instead of 8 m: C2's subdomain alphabet
-// (s = 6) sorts 6 bytes in 5 passes, IP text (s = 4) 7 bytes in 4.
-__device__ __forceinline__ uint64_t key_pack(uint64_t k, const uint8_t *code, uint32_t m, uint32_t sbits) {
-    const uint32_t t = (uint32_t)k & 0xffu;
-    uint64_t out = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 7; ++j) {
-        if (j < m) {
-            const uint32_t b = (uint32_t)(k >> (56 - 8 * j)) & 0xffu;
-            out = (out << sbits) | (j < t ? (uint64_t)code[b] : 0ull);
-        }
-    }
-    return (out << 8) | (t < m + 1 ? t : m + 1);
-}
 
 // ------------------------------------------------------------------ limits
 constexpr uint64_t MAX_BYTES = 0xFFFF0000ull;  // 32-bit record offsets with headroom

@@ -755,59 +755,6 @@ __global__ __launch_bounds__(256) void k_lcp_hist(const uint8_t *__restrict__ bu
     }
 }
 
-// key0 -> the alphabet-packed key (key_pack, the prior's side of a packed sort).
-__global__ __launch_bounds__(256) void k_pack_keys(uint64_t *__restrict__ keys, uint32_t n, const uint8_t *__restrict__ code,
-                                                   uint32_t m, uint32_t sbits) {
-    __shared__ uint8_t s_code[256];
-    s_code[threadIdx.x] = code[threadIdx.x];
-    __syncthreads();
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        keys[i] = key_pack(keys[i], s_code, m, sbits);
-}
-
-// Alphabet packing for the dedup sort (KeyPack, sg_common.hpp key_pack): from the key-byte
-// histograms of cur (hc) and prior (hp, may be null), for the first m key bytes the set of
-// byte values either holds (a 0 may be a NUL or the record's end: kept conservatively) gets
-// order-preserving codes 1..A; s = bits for A + 1 codes. Chosen when it sorts in fewer
-// passes than the kw-byte narrowed key (ceil(m s / 8) < kw digits above the tag), taking as
-// many chars (<= 7) as those passes hold. Returns false (narrowing stays) otherwise.
-static bool choose_pack(const uint32_t *hc, const uint32_t *hp, uint32_t kw, KeyPack *pk) {
-    *pk = KeyPack{};
-    uint32_t best_digits = kw, best_m = 0, best_s = 0;
-    for (uint32_t m = 7; m >= kw; --m) {
-        bool used[256] = {};
-        uint32_t A = 0;
-        for (uint32_t j = 0; j < m; ++j)
-            for (uint32_t d = 0; d < 256; ++d)
-                if ((hc[(7 - j) * 256 + d] || (hp && hp[(7 - j) * 256 + d])) && !used[d]) { used[d] = true; ++A; }
-        uint32_t sb = 1;
-        while ((1u << sb) < A + 1) ++sb;
-        const uint32_t digits = (m * sb + 7) / 8;
-        if (digits < best_digits || (digits == best_digits && best_m && m > best_m)) {
-            best_digits = digits;
-            best_m = m;
-            best_s = sb;
-        }
-        if (m == 1) break;
-    }
-    if (!best_m) return false;
-    // the largest m the chosen digit count holds at that alphabet
-    pk->m = best_m;
-    pk->s = best_s;
-    bool used[256] = {};
-    for (uint32_t j = 0; j < pk->m; ++j)
-        for (uint32_t d = 0; d < 256; ++d)
-            if (hc[(7 - j) * 256 + d] || (hp && hp[(7 - j) * 256 + d])) used[d] = true;
-    uint32_t code = 0;
-    for (uint32_t d = 0; d < 256; ++d) pk->code[d] = used[d] ? (uint8_t)(++code) : (uint8_t)code;
-    // the tag digit (min(rem, m + 1)) is skipped when every cur key has the same one
-    uint32_t tg[10] = {0};
-    uint32_t tot = 0;
-    for (uint32_t d = 0; d < 256; ++d) { tg[d < pk->m + 1 ? d : pk->m + 1] += hc[d]; tot += hc[d]; }
-    for (uint32_t q = 0; q <= pk->m + 1; ++q) if (tg[q] == tot) pk->tag_trivial = 1;
-    return true;
-}
-
 // key0 (7 bytes + min(rem, 8)) -> the kw-byte key (kw bytes + min(rem, kw + 1)).
 __global__ __launch_bounds__(256) void k_narrow_keys(uint64_t *__restrict__ keys, uint32_t n, uint32_t kw) {
     const uint64_t top = ~0ull << (64u - 8u * kw);
@@ -1076,13 +1023,9 @@ struct OutBuf {
     uint32_t shift() const { return (uint32_t)((uintptr_t)p & 15); }
 };
 
-// pack: the keys are packed by the sort's first pass (and a single record's key here);
-// keys_final: the keys already are in the call's key form (a prior narrowed or packed by the
-// caller), so nothing narrows them again.
 static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
                         UView *uv, const Lines *pre = nullptr, uint32_t base = make_bk(0u, 7u), const OutBuf *dst = nullptr,
-                        const uint32_t *host_hist = nullptr, const KeyPack *pack = nullptr, bool keys_final = false,
-                        const uint8_t *d_code = nullptr) {
+                        const uint32_t *host_hist = nullptr) {
     *uv = UView{};
     Lines L;
     if (pre) L = *pre;
@@ -1110,9 +1053,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
             if (!trust_sorted) {
                 // a single record: serialize it (the caller may return this view); its key
                 // narrowed here (a sort would have done it on its first pass)
-                if (pack && pack->m)
-                    SG_LAUNCH(c, "pack_keys", k_pack_keys, 1, 256, 0, L.keys, R, d_code, pack->m, pack->s);
-                else if (!keys_final && (base >> 16) < 7u)
+                if ((base >> 16) < 7u)
                     SG_LAUNCH(c, "narrow_keys", k_narrow_keys, 1, 256, 0, L.keys, R, base >> 16);
                 uint8_t *ub;
                 uint2 *us;
@@ -1146,10 +1087,9 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, vs.lines.vals2, R, &v2));
     uint64_t *K;
     uint2 *V;
-    // the key narrowing to kw bytes (or the packing) happens in the sort's first pass
+    // the key narrowing to kw bytes happens in the sort's first pass
     SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V, "rs_pass", host_hist,
-                            (!keys_final && !(pack && pack->m) && (base >> 16) < 7u) ? base >> 16 : 0u,
-                            pack && pack->m ? pack : nullptr));
+                            (base >> 16) < 7u ? base >> 16 : 0u));
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
     uint8_t *brk;
@@ -1319,21 +1259,10 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
                     Lc.spans, Lc.keys, Lc.n_rec,
                     rbuf, rsp, rkeys, dflag + 1);
     }
-    // the prior's key-byte histograms too (the alphabet packing must cover its bytes)
-    const uint32_t *phist = nullptr;
-    if (rsp && have_prior && Lp.n_rec && want_hist) {
-        uint32_t *hist;
-        SG_TRY(slot(c, S_HIST, 8 * 256 * 2 + 8, &hist));
-        hist += 8 * 256;
-        SG_HIP(hipMemsetAsync(hist, 0, 8 * 256 * 4, c->stream));
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp_hist, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 1024u), 256, 0,
-                    d_prior, Lp.spans, Lp.keys, Lp.n_rec, rbuf, rsp, rkeys, dflag + 1, hist);
-        phist = hist;
-    } else if (rsp && have_prior && Lp.n_rec) {
+    if (rsp && have_prior && Lp.n_rec)
         SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 512u), 256, 0, d_prior,
                     Lp.spans, Lp.keys, Lp.n_rec,
                     rbuf, rsp, rkeys, dflag + 1);
-    }
     // the cur keys' digit histograms (for the key width below) are queued now and come back
     // with the flags; they stay valid when the common prefix turns out to be empty
     if (want_hist && !dhist) SG_TRY(key_hist8_async(c, Lc.keys, Lc.n_rec, &dhist));
@@ -1342,11 +1271,9 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         uint8_t *pin = (uint8_t *)c->pinned;
         SG_HIP(hipMemcpyAsync(pin, dflag, 8, hipMemcpyDeviceToHost, c->stream));
         if (dhist) SG_HIP(hipMemcpyAsync(pin + 64, dhist, 8 * 256 * 4, hipMemcpyDeviceToHost, c->stream));
-        if (phist) SG_HIP(hipMemcpyAsync(pin + 64 + 8 * 256 * 4, phist, 8 * 256 * 4, hipMemcpyDeviceToHost, c->stream));
         SG_HIP(hipStreamSynchronize(c->stream));
         memcpy(fl, pin, 8);
         if (dhist) memcpy(c->hist_host, pin + 64, 8 * 256 * 4);
-        if (phist) memcpy(c->hist_prior, pin + 64 + 8 * 256 * 4, 8 * 256 * 4);
     }
     prior_sorted = fl[0] == 0;
     const uint32_t base = (rsp && (Lc.n_rec || (have_prior && Lp.n_rec))) ? fl[1] : 0u;
@@ -1365,13 +1292,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     uint32_t kw = 7;
     uint32_t *hh = c->hist_host;
     const uint32_t *cur_hist = nullptr;
-    KeyPack pack;
-    uint8_t *d_code = nullptr;
     if (want_hist) {
-        if (base) {  // keys changed: histograms again
-            SG_TRY(key_hist8(c, Lc.keys, Lc.n_rec, hh));
-            if (phist) SG_TRY(key_hist8(c, Lp.keys, Lp.n_rec, c->hist_prior));
-        }
+        if (base) SG_TRY(key_hist8(c, Lc.keys, Lc.n_rec, hh));  // keys changed: histograms again
         const double N = (double)Lc.n_rec;
         double H[8] = {0};
         for (int p = 0; p < 8; ++p)
@@ -1387,15 +1309,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         const bool live2 = H[2] > 0.0, live1 = H[1] > 0.0;  // the passes narrowing removes
         if (h5 >= lg + 4.0 && (live2 || live1)) kw = 5;
         else if (h6 >= lg + 2.0 && live1) kw = 6;
-        if (choose_pack(hh, (have_prior && Lp.n_rec) ? c->hist_prior : nullptr, kw, &pack)) {
-            // packed: the cur keys by the sort's first pass, the prior's here
-            kw = pack.m;
-            SG_TRY(slot(c, S_PACK, 256, &d_code));
-            SG_TRY(ctx_upload(c, d_code, pack.code, 256));
-            if (have_prior && Lp.n_rec)
-                SG_LAUNCH(c, "pack_keys", k_pack_keys, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, Lp.keys,
-                          Lp.n_rec, d_code, pack.m, pack.s);
-        } else if (kw < 7) {
+        if (kw < 7) {
             // the cur keys are narrowed by the sort's first pass (build_unique); the prior's
             // here (its view is the input itself when sorted, and the diff compares keys)
             if (have_prior && Lp.n_rec)
@@ -1410,15 +1324,13 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
             for (int d = 0; d < 256; ++d) tg[d < (int)kw + 1 ? d : (int)kw + 1] += hh[d];
             for (int d = 0; d < 256; ++d) hh[d] = tg[d];
         }
-        cur_hist = pack.m ? nullptr : hh;
+        cur_hist = hh;
     }
     c->last_kw = kw;
-    c->last_pack_bits = pack.m ? pack.s : 0u;
     const uint32_t bk = make_bk(base, kw);
-    // the prior's keys are final here (narrowed or packed above)
-    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, bk, nullptr, nullptr, nullptr, true));
+    if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, bk));
     UView cu;
-    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, cur_hist, &pack, false, d_code));
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, cur_hist));
     res->in_records = cu.in_records;
     res->uniq = ou ? ou->p : const_cast<uint8_t *>(cu.buf);
     res->uniq_bytes = cu.bytes;

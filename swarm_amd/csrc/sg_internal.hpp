@@ -41,17 +41,11 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
 // LSD radix sort of (u64 key, u32 val) pairs on bits [begin_bit, end_bit), stable.
 // Ping-pongs between (keys, vals) and (keys_alt, vals_alt); returns the final arrays.
 // iota_vals: vals[i] = i is implied on input (vals need not be initialised).
-// Order-preserving alphabet packing of key0 for the dedup sort (sg_sort.hip rs_pack).
-struct KeyPack {
-    uint32_t m = 0, s = 0;     // chars packed (0: off) and bits per char
-    uint32_t tag_trivial = 0;  // every key has the same (clamped) tag: its digit pass is skipped
-    uint8_t code[256] = {};    // byte -> 1 .. 2^s - 1, increasing with the byte
-};
 // Stable sort of (key, span) pairs: the spans themselves are the payload (no id gather after).
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out,
                      const char *pass_name = "rs_pass", const uint32_t *host_hist = nullptr,
-                     uint32_t narrow_kw = 0, const KeyPack *pack = nullptr);
+                     uint32_t narrow_kw = 0);
 // The 8 digit histograms (bits [0, 64), 8 x 256 counts) of keys, read back to the host.
 int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist);
 // The same histograms queued only (device pointer, 8 x 256 u32), for a combined read-back.

@@ -276,12 +276,6 @@ int sg_ctx_last_key_width(sg_ctx *c, uint32_t *kw) {
     return SG_OK;
 }
 
-int sg_ctx_last_key_pack(sg_ctx *c, uint32_t *bits) {
-    if (!c || !bits) return SG_E_INVAL;
-    *bits = c->last_pack_bits;
-    return SG_OK;
-}
-
 int sg_ctx_reset_stats(sg_ctx *c) {
     if (!c) return SG_E_INVAL;
     SG_TRY(ctx_harvest(c));

@@ -19,8 +19,7 @@ namespace sg {
 //                           written contiguously
 // No inter-block waits (a single-pass look-back over 4096-item tiles waited cross-XCD
 // round trips per tile on MI355X: 88 µs/pass vs 55 µs for this downsweep at 10M pairs).
-// Algorithmic bytes per pass: 8 B key + the value (4 B id or 8 B span) read and both written,
-// per pair: 16 + 16 B with span values (the dedup sort), 12 + 12 B with ids.
+// Algorithmic bytes per pass: 12 B read + 12 B written per pair.
 
 constexpr int RS_MAXPASS = 8;
 
@@ -31,13 +30,6 @@ __device__ __forceinline__ uint64_t rs_narrow(uint64_t k, uint32_t kw) {
     const uint64_t top = ~0ull << (64u - 8u * kw);
     const uint64_t t = k & 0xffu;
     return (k & top) | (t < kw + 1u ? t : (uint64_t)(kw + 1u));
-}
-struct RsXform {
-    const uint8_t *code = nullptr;  // non-null: pack (device table of 256 codes), else narrow to kw
-    uint32_t m = 0, s = 0, kw = 0;
-};
-__device__ __forceinline__ uint64_t rs_xform(uint64_t k, const RsXform &x, const uint8_t *s_code) {
-    return x.code ? key_pack(k, s_code, x.m, x.s) : rs_narrow(k, x.kw);
 }
 constexpr int RS_HBLOCK = 256;
 
@@ -118,21 +110,19 @@ constexpr int RD_WAVES = RD_BLOCK / 64;
 // wave-row whose lanes share one digit adds once (skewed digits: '.' or 't' at fixed
 // positions of host names).
 __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__ keys, uint32_t n, int shift,
-                                                    uint32_t ntiles, uint32_t *__restrict__ cnt, RsXform xf, bool xcd) {
+                                                    uint32_t ntiles, uint32_t *__restrict__ cnt, uint32_t kw, bool xcd) {
     __shared__ uint32_t h[RD_WAVES][256];
-    __shared__ uint8_t s_code[256];
     const int wid = threadIdx.x >> 6;
     const uint32_t tile = xcd ? rs_tile_of(blockIdx.x, ntiles) : blockIdx.x;
     if (tile >= ntiles) return;
     for (int x = threadIdx.x; x < RD_WAVES * 256; x += RD_BLOCK) (&h[0][0])[x] = 0;
-    if (xf.code) s_code[threadIdx.x] = xf.code[threadIdx.x];
     __syncthreads();
     const uint32_t wbase = tile * RD_TILE + wid * (RD_ITEMS * 64);
     uint32_t dd[RD_ITEMS];
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane_id();
-        dd[i] = (pos < n) ? ((uint32_t)(rs_xform(keys[pos], xf, s_code) >> shift) & 255u) : 256u;
+        dd[i] = (pos < n) ? ((uint32_t)(rs_narrow(keys[pos], kw) >> shift) & 255u) : 256u;
     }
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
@@ -152,15 +142,13 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__
     cnt[(size_t)threadIdx.x * ntiles + tile] = v;
 }
 
-// One block per digit d: cnt[d][t] -> exclusive prefix over tiles + goffs[d]; goffs null:
-// prefix from 0 and the digit's total into dtot[d] (the downsweep then adds the digit bases
-// itself — no histogram pass needed, e.g. for packed keys).
+// One block per digit d: cnt[d][t] -> exclusive prefix over tiles + goffs[d].
 __global__ __launch_bounds__(256) void k_rs_cscan(uint32_t *__restrict__ cnt, uint32_t ntiles,
-                                                  const uint32_t *__restrict__ goffs, uint32_t *__restrict__ dtot) {
+                                                  const uint32_t *__restrict__ goffs) {
     __shared__ uint32_t s_red[4];
     const uint32_t d = blockIdx.x;
     uint32_t *row = cnt + (size_t)d * ntiles;
-    uint32_t carry = goffs ? goffs[d] : 0u;
+    uint32_t carry = goffs[d];
     for (uint32_t b = 0; b < ntiles; b += 256 * 4) {
         const uint32_t i0 = b + threadIdx.x * 4;
         uint32_t v[4], sum = 0;
@@ -173,7 +161,6 @@ __global__ __launch_bounds__(256) void k_rs_cscan(uint32_t *__restrict__ cnt, ui
         for (int j = 0; j < 4; ++j) { if (i0 + j < ntiles) row[i0 + j] = run; run += v[j]; }
         carry += tot;
     }
-    if (!goffs && threadIdx.x == 0) dtot[d] = carry;
 }
 
 // VT: u32 record ids (IOTA: generated on the first pass) or uint2 spans carried along, so
@@ -183,8 +170,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
                                                       const VT *__restrict__ vin,
                                                       uint64_t *__restrict__ kout, VT *__restrict__ vout,
                                                       uint32_t n, int shift, uint32_t ntiles,
-                                                      const uint32_t *__restrict__ toffs, RsXform xf, bool xcd,
-                                                      const uint32_t *__restrict__ dtot) {
+                                                      const uint32_t *__restrict__ toffs, uint32_t kw, bool xcd) {
     static_assert(sizeof(VT) <= sizeof(uint64_t), "values staged in the key buffer");
     __shared__ uint64_t s_k[RD_TILE];  // keys, then (aliased) values
     VT *s_v = reinterpret_cast<VT *>(s_k);
@@ -192,11 +178,9 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
     __shared__ uint32_t s_dstart[256];
     __shared__ uint32_t s_gbase[256];
     __shared__ uint32_t s_red[RD_WAVES];
-    __shared__ uint8_t s_code[256];
 
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
     for (int x = tid; x < RD_WAVES * 256; x += RD_BLOCK) (&s_wh[0][0])[x] = 0;
-    if (xf.code) s_code[tid] = xf.code[tid];
     __syncthreads();
     const uint32_t tile = xcd ? rs_tile_of(blockIdx.x, ntiles) : blockIdx.x;
     if (tile >= ntiles) return;
@@ -209,7 +193,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane;
-        k[i] = (pos < n) ? rs_xform(kin[pos], xf, s_code) : ~0ull;
+        k[i] = (pos < n) ? rs_narrow(kin[pos], kw) : ~0ull;
     }
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
@@ -233,13 +217,8 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
     for (int w = 0; w < RD_WAVES; ++w) { const uint32_t x = s_wh[w][tid]; s_wh[w][tid] = run; run += x; }
     uint32_t blk_total;
     const uint32_t dstart = block_excl_scan<RD_BLOCK>(run, &blk_total, s_red);
-    uint32_t dbase = 0;
-    if (dtot) {  // digit bases from the column totals (no histogram pass)
-        uint32_t all;
-        dbase = block_excl_scan<RD_BLOCK>(dtot[tid], &all, s_red);
-    }
     s_dstart[tid] = dstart;
-    s_gbase[tid] = dbase + toffs[(size_t)tid * ntiles + tile] - dstart;
+    s_gbase[tid] = toffs[(size_t)tid * ntiles + tile] - dstart;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
@@ -306,47 +285,6 @@ int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist) 
     return ctx_readback(c, host_hist, hist, RS_MAXPASS * 256 * 4);
 }
 
-// Sort by packed keys (KeyPack): the first pass packs the raw key0 values as it reads them
-// (rs_pack); the live digits are the tag (unless every key has the same one) and the
-// ceil(m * s / 8) digits above it. No histogram pass: the column scan also leaves each
-// digit's total and every downsweep block adds the digit bases itself.
-template <typename VT>
-static int radix_sort_packed(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt, VT *vals_alt, uint32_t n,
-                             uint64_t **keys_out, VT **vals_out, const char *pass_name, const KeyPack &pk) {
-    *keys_out = keys;
-    *vals_out = vals;
-    if (n == 0) return SG_OK;
-    uint8_t *d_code;
-    uint32_t *dtot;
-    SG_TRY(slot(c, S_RS_DIGITS, 256 + 256 * 4, &d_code));
-    dtot = reinterpret_cast<uint32_t *>(d_code + 256);
-    SG_TRY(ctx_upload(c, d_code, pk.code, 256));
-    const int top = (int)((8 + pk.m * pk.s + 7) / 8);  // digits 0 .. top - 1
-    const uint32_t ntiles = (n + RD_TILE - 1) / RD_TILE;
-    uint32_t *tcnt;
-    SG_TRY(slot(c, S_RS_TCNT, (size_t)ntiles * 256 + 64, &tcnt));
-    const uint32_t grid = 8u * ((ntiles + 7u) / 8u);  // XCD-aware tile order
-    uint64_t *ck = keys, *ak = keys_alt;
-    VT *cv = vals, *av = vals_alt;
-    constexpr double VB = (double)sizeof(VT);
-    bool first = true;
-    for (int p = pk.tag_trivial ? 1 : 0; p < top; ++p) {
-        RsXform xf;
-        if (first) { xf.code = d_code; xf.m = pk.m; xf.s = pk.s; }
-        first = false;
-        SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, grid, RD_BLOCK, 0, ck, n, 8 * p, ntiles, tcnt, xf, true);
-        SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, (const uint32_t *)nullptr, dtot);
-        SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, 8 * p, ntiles, tcnt, xf, true,
-                  (const uint32_t *)dtot);
-        prof_bytes(c, pass_name, (16.0 + 2.0 * VB) * n);
-        uint64_t *tk = ck; ck = ak; ak = tk;
-        VT *tv = cv; cv = av; av = tv;
-    }
-    *keys_out = ck;
-    *vals_out = cv;
-    return SG_OK;
-}
-
 // host_hist (optional): the 8 digit histograms of `keys` over bits [0, 64), already on the
 // host (key_hist8, possibly adjusted by the caller) — then the trivial passes are known
 // without a read-back.
@@ -354,11 +292,10 @@ template <typename VT>
 static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt, VT *vals_alt,
                         uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
                         VT **vals_out, const char *pass_name, const uint32_t *host_hist = nullptr,
-                        uint32_t narrow_kw = 0, const KeyPack *pack = nullptr) {
+                        uint32_t narrow_kw = 0) {
     *keys_out = keys;
     *vals_out = vals;
     if (n == 0) return SG_OK;
-    if (pack && pack->m) return radix_sort_packed(c, keys, vals, keys_alt, vals_alt, n, keys_out, vals_out, pass_name, *pack);
     const int npasses = (end_bit - begin_bit + 7) / 8;
     if (npasses <= 0 || npasses > RS_MAXPASS) { set_error("radix_sort: bad bit range"); return SG_E_INVAL; }
     if (host_hist && (begin_bit != 0 || npasses != RS_MAXPASS)) { set_error("radix_sort: histograms cover 64 bits"); return SG_E_INVAL; }
@@ -402,18 +339,16 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     for (int q = 0; q < nlive; ++q) {
         const int p = live[q];
         const int shift = begin_bit + 8 * p;
-        RsXform xf;
-        xf.kw = q == 0 ? narrow_kw : 0u;  // the first pass narrows as it reads
-        const uint32_t *nod = nullptr;
-        SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, grid, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, xf, xcd);
-        SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, offs + p * 256, (uint32_t *)nullptr);
+        const uint32_t kw = q == 0 ? narrow_kw : 0u;  // the first pass narrows as it reads
+        SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, grid, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, kw, xcd);
+        SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, offs + p * 256);
         if constexpr (sizeof(VT) == 4) {
             if (iota_pending)
-                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, xf, xcd, nod);
+                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
             else
-                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, xf, xcd, nod);
+                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
         } else {
-            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, xf, xcd, nod);
+            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
         }
         // 8 B key + the value read (implied for iota ids) and both written, per pair
         prof_bytes(c, pass_name, (iota_pending ? 16.0 + VB : 16.0 + 2.0 * VB) * n);
@@ -442,9 +377,9 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
 
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out, const char *pass_name,
-                     const uint32_t *host_hist, uint32_t narrow_kw, const KeyPack *pack) {
+                     const uint32_t *host_hist, uint32_t narrow_kw) {
     return radix_sort_t<uint2>(c, keys, spans, keys_alt, spans_alt, n, begin_bit, end_bit, false, keys_out, spans_out,
-                               pass_name, host_hist, narrow_kw, pack);
+                               pass_name, host_hist, narrow_kw);
 }
 
 }  // namespace sg

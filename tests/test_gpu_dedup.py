@@ -408,68 +408,3 @@ def test_refinement_packed_chunk_keys(sg, alpha):
     prior = b"".join(r + b"\n" for r in prior_recs)
     assert sg.dedup(cur) == S.dedup(cur)
     assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)
-
-
-@pytest.mark.parametrize("case", ["subdomains", "short_nul", "prior_extra", "unsorted_prior", "urls", "ips"])
-def test_alphabet_packed_sort_key(case):
-    """The radix dedup's alphabet-packed sort key (sg_common.hpp key_pack): the first kw key
-    bytes as order-preserving s-bit codes of the byte values cur AND prior hold there. Cases:
-    C2-like subdomains (s = 6: 6 bytes in 5 passes), records shorter than the key with NUL
-    bytes (0 = NUL or past the end, told apart by the tag), a prior holding bytes cur lacks,
-    an unsorted prior (sorted on packed keys), URLs (common prefix first) and IP text
-    (s = 4). Results equal the oracle; the packing is reported where it must happen."""
-    import random
-    import numpy as np
-    import torch
-    from swarm_amd import corpus
-    rng = random.Random(hash(case) & 0xffff)
-    if case == "subdomains":
-        buf, ids = corpus.subdomains(300_000, seed=5)
-        cur, prior = buf.tobytes(), corpus.prior_of(ids).tobytes()
-        want_bits = 6
-    elif case == "short_nul":
-        al = b"abc\x00xyz.-"
-        recs = [bytes(rng.choice(al) for _ in range(rng.randint(1, 12))) for _ in range(150_000)]
-        cur = b"\n".join(recs) + b"\n"
-        prior = S.dedup(b"\n".join(recs[::4]) + b"\n")
-        want_bits = 4
-    elif case == "prior_extra":
-        al = b"abcdefghijklmno"  # 15 bytes: cur alone packs in 4 bits
-        recs = [bytes(rng.choice(al) for _ in range(rng.randint(6, 14))) for _ in range(150_000)]
-        extra = [bytes(rng.choice(b"aZ~!") for _ in range(rng.randint(3, 10))) for _ in range(20_000)]
-        cur = b"\n".join(recs) + b"\n"
-        prior = S.dedup(b"\n".join(recs[::3] + extra) + b"\n")  # bytes 'Z', '~', '!' only in the prior
-        want_bits = 5
-    elif case == "unsorted_prior":
-        al = b"0123456789abcdef"
-        recs = [bytes(rng.choice(al) for _ in range(rng.randint(5, 16))) for _ in range(150_000)]
-        cur = b"\n".join(recs) + b"\n"
-        pr = recs[::3] + recs[::7]
-        rng.shuffle(pr)
-        prior = b"\n".join(pr) + b"\n"
-        want_bits = 5
-    elif case == "urls":
-        buf, ids = corpus.subdomains(200_000, seed=6)
-        u = lambda b: b"https://" + b[:-1].replace(b"\n", b"\nhttps://") + b"\n"  # noqa: E731
-        cur, prior = u(buf.tobytes()), u(corpus.prior_of(ids).tobytes())
-        want_bits = None
-    else:
-        recs = [b"10.%d.%d.%d:%d" % (rng.randrange(4), rng.randrange(256), rng.randrange(256), rng.choice([22, 80, 443]))
-                for _ in range(200_000)]
-        cur = b"\n".join(recs) + b"\n"
-        prior = S.dedup(b"\n".join(recs[::3]) + b"\n")
-        want_bits = 4
-    c = _kw_ctx()
-    try:
-        dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
-        dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
-        r = c.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
-        eu, ef = S.dedup_diff(cur, prior)
-        assert c.to_bytes(r.uniq, r.uniq_bytes) == eu and c.to_bytes(r.fresh, r.fresh_bytes) == ef
-        if want_bits is not None:
-            assert c.last_key_pack() == want_bits
-        # no prior: the packing covers cur's bytes alone
-        r = c.dedup_diff(dc.data_ptr(), len(cur), 0, 0)
-        assert c.to_bytes(r.uniq, r.uniq_bytes) == eu
-    finally:
-        c.close()
