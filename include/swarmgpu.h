@@ -338,6 +338,12 @@ typedef struct sg_dev_tmatches {
     uint64_t in_records;
 } sg_dev_tmatches;
 int sg_dev_tmpl_eval(sg_ctx *ctx, sg_templates *h, const uint8_t *d_buf, size_t n, sg_dev_tmatches *res);
+/* sg_dev_tmpl_eval with the field rows already built: `rows` is the result of the caller's
+ * own sg_dev_json_fields call on the same ctx, d_buf (16-byte aligned) and n, with the keys
+ * the handle was compiled with, in the same order — the httpx -json fields step then parses
+ * every line once for its rows and its template evaluation together. */
+int sg_dev_tmpl_eval_rows(sg_ctx *ctx, sg_templates *h, const uint8_t *d_buf, size_t n, const sg_dev_rows *rows,
+                          sg_dev_tmatches *res);
 int sg_tmpl_eval(sg_templates *h, const uint8_t *buf, size_t n, uint32_t *rec_idx, uint32_t *tmpl_id,
                  size_t cap, size_t *n_out);
 void sg_tmpl_free(sg_templates *h);

@@ -137,13 +137,16 @@ class DevTMatches(C.Structure):
 
 SG_TM_WORD, SG_TM_REGEX = 0, 1
 SG_TM_AND, SG_TM_NEGATIVE, SG_TM_NOCASE = 1, 2, 4
-EXPORTS += ["sg_tmpl_compile", "sg_tmpl_info", "sg_dev_tmpl_eval", "sg_tmpl_eval", "sg_tmpl_free"]
+EXPORTS += ["sg_tmpl_compile", "sg_tmpl_info", "sg_dev_tmpl_eval", "sg_dev_tmpl_eval_rows", "sg_tmpl_eval",
+            "sg_tmpl_free"]
 for _name, (_res, _args) in {
     "sg_tmpl_compile": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(TmMatcher), C.c_uint32,
                                   C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32,
                                   C.POINTER(C.c_void_p)]),
     "sg_tmpl_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "sg_dev_tmpl_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(DevTMatches)]),
+    "sg_dev_tmpl_eval_rows": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(DevRows),
+                                        C.POINTER(DevTMatches)]),
     "sg_tmpl_eval": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                C.c_size_t, C.POINTER(C.c_size_t)]),
     "sg_tmpl_free": (None, [C.c_void_p]),

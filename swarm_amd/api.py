@@ -612,9 +612,18 @@ class Templates:
             check(rc)
             return list(zip(rec[: n.value].tolist(), tid[: n.value].tolist()))
 
-    def dev_match(self, ctx: "Context", d_buf: int, n: int) -> _abi.DevTMatches:
+    def dev_match(self, ctx: "Context", d_buf: int, n: int, rows: _abi.DevRows = None,
+                  rows_keys: Sequence[bytes] = None) -> _abi.DevTMatches:
+        """rows (with rows_keys, the keys they were built with): the result of
+        ctx.json_fields(d_buf, n, rows_keys) just before on the same context — the field
+        rows are then not built a second time (include/swarmgpu.h sg_dev_tmpl_eval_rows)."""
         r = _abi.DevTMatches()
-        check(lib.sg_dev_tmpl_eval(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(r)))
+        if rows is not None:
+            if [bytes(k) for k in (rows_keys or [])] != self.keys:
+                raise ValueError("rows were built for keys %r, the templates use %r" % (rows_keys, self.keys))
+            check(lib.sg_dev_tmpl_eval_rows(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(rows), C.byref(r)))
+        else:
+            check(lib.sg_dev_tmpl_eval(ctx._h, self._h, C.c_void_p(d_buf), n, C.byref(r)))
         return r
 
 

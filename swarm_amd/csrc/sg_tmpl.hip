@@ -480,7 +480,11 @@ static int tm_rec_wave(sg_ctx *c, const sg_templates *h, const sg_templates::Dev
     return SG_OK;
 }
 
-static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint64_t n, sg_dev_tmatches *res) {
+// given_rows: the field rows of d_buf for the handle's keys, from the caller's own
+// sg_dev_json_fields call on this context (the fields step parses the JSON once); null: the
+// rows are built here.
+static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint64_t n, sg_dev_tmatches *res,
+                         const sg_dev_rows *given_rows = nullptr) {
     *res = sg_dev_tmatches{};
     const sg_templates::Dev *pd = nullptr;
     SG_TRY(tm_ensure_device(h, c->device, &pd));
@@ -510,8 +514,9 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
     for (auto &run : h->runs) any1 |= run.stream == 1;
     if (any1) {
         sg_dev_rows rows;
-        SG_TRY(dev_json_fields(c, d_buf, n, h->key_blob.data(), h->key_offs.data(), (uint32_t)h->key_offs.size() - 1,
-                               &rows));
+        if (given_rows) rows = *given_rows;
+        else SG_TRY(dev_json_fields(c, d_buf, n, h->key_blob.data(), h->key_offs.data(), (uint32_t)h->key_offs.size() - 1,
+                                    &rows));
         R = rows.in_records;
         have_R = true;
         for (size_t ri = 0; ri < h->runs.size(); ++ri) {
@@ -768,6 +773,15 @@ int sg_tmpl_info(const sg_templates *h, uint32_t *n_atoms, uint32_t *n_engines, 
     if (n_engines) *n_engines = (uint32_t)h->runs.size();
     if (n_vacuous) *n_vacuous = (uint32_t)h->vac.size();
     return SG_OK;
+}
+
+int sg_dev_tmpl_eval_rows(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, size_t n, const sg_dev_rows *rows,
+                          sg_dev_tmatches *res) {
+    if (!c || !h || !res || !rows || (!d_buf && n)) { set_error("sg_dev_tmpl_eval_rows: bad arguments"); return SG_E_INVAL; }
+    if (n > MAX_BYTES) { set_error("input exceeds 4 GiB per call"); return SG_E_TOO_LARGE; }
+    if (((uintptr_t)d_buf & 15) != 0) { set_error("sg_dev_tmpl_eval_rows: d_buf must be 16-byte aligned"); return SG_E_INVAL; }
+    SG_HIP(hipSetDevice(c->device));
+    return dev_tmpl_eval(c, h, d_buf, n, res, rows);
 }
 
 int sg_dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, size_t n, sg_dev_tmatches *res) {

@@ -199,3 +199,30 @@ def test_field_rows_repeat_atoms(sg):
          {"condition": "or", "matchers": [W(b"nginx", b"PHP", b"Apache", condition="and")]}]
     data = b"\n".join(lines * 30) + b"\n"
     assert sg.Templates(T, keys).match(data) == S.template_matches(data, T, keys)
+
+
+def test_device_eval_with_given_field_rows(sg):
+    """The fields step parses the JSON once: the rows of ctx.json_fields handed to the
+    template evaluation (sg_dev_tmpl_eval_rows) give the same (record, template) pairs as
+    building them inside, and as the oracle; rows built for other keys are refused."""
+    import torch
+    rng = random.Random(31)
+    keys = [b"title", b"webserver", b"tech"]
+    T = random_templates(rng, 80, ["body", "title", "webserver", "tech"])
+    data = b"\n".join(corpus.httpx_json_pool(4000, seed=23)) + b"\n"
+    d = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        tm = sg.Templates(T, keys)
+        r1 = tm.dev_match(ctx, d.data_ptr(), d.numel())
+        pairs1 = list(zip(np.frombuffer(ctx.to_bytes(r1.rec_idx, 4 * r1.n), dtype=np.uint32).tolist(),
+                          np.frombuffer(ctx.to_bytes(r1.tmpl_id, 4 * r1.n), dtype=np.uint32).tolist()))
+        rows = ctx.json_fields(d.data_ptr(), d.numel(), keys)
+        r2 = tm.dev_match(ctx, d.data_ptr(), d.numel(), rows=rows, rows_keys=keys)
+        pairs2 = list(zip(np.frombuffer(ctx.to_bytes(r2.rec_idx, 4 * r2.n), dtype=np.uint32).tolist(),
+                          np.frombuffer(ctx.to_bytes(r2.tmpl_id, 4 * r2.n), dtype=np.uint32).tolist()))
+        assert pairs1 == pairs2 == S.template_matches(data, T, keys)
+        with pytest.raises(ValueError):
+            tm.dev_match(ctx, d.data_ptr(), d.numel(), rows=rows, rows_keys=[b"url"])
+    finally:
+        ctx.close()
