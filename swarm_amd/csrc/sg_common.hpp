@@ -63,7 +63,7 @@ enum Slot : int {
     // module-output formats (nmap -oN, httpx -json) and template evaluation
     S_F_SPANS, S_F_LB, S_F_A, S_F_B, S_F_DESC, S_F_OFFS, S_F_OUT, S_F_REC, S_F_KEY, S_F_KEYS,
     S_T_HITS, S_T_EXP, S_T_K2, S_T_V1, S_T_V2, S_T_OUT, S_T_SEL, S_T_E, S_T_E2, S_T_SEG, S_T_FLAG, S_T_O,
-    S_T_REC, S_T_TID, S_F_TILES,
+    S_T_REC, S_T_TID,
     S_M_FLAG, S_M_SP2, S_M_K2, S_R_T2, S_COUNT2,
     S_R_ALPHA,  // refinement rounds: byte alphabet mask + rank table of the chunk keys
     // hit sort by record buckets (sg_match.hip)

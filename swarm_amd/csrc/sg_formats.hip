@@ -310,49 +310,14 @@ struct JsCount {
     __device__ void end() { if (cur) { ++rows; bytes += cur + 1; } }
 };
 
-// Bytes of the input seen through a byte tile staged in LDS: positions in [t0, t1) read the
-// LDS copy, others (a record running past the tile's overhang) read HBM.
-struct JsTileBuf {
-    const uint8_t *g;
-    const uint8_t *s;
-    uint32_t t0, t1;
-    __device__ __forceinline__ uint8_t operator[](uint32_t q) const { return (q - t0 < t1 - t0) ? s[q - t0] : g[q]; }
-    __device__ __forceinline__ uint4 chunk(uint32_t w) const {  // 16-B aligned w
-        return (w - t0 < t1 - t0 && w + 16u <= t1) ? *reinterpret_cast<const uint4 *>(s + (w - t0))
-                                                   : *reinterpret_cast<const uint4 *>(g + w);
-    }
-};
-
-// Records are handed to byte tiles by their start: first[t] = the first record starting at
-// or after t * JT_TILE (first[ntiles] = R).
-constexpr uint32_t JT_TILE = 16384;   // bytes per tile (records starting here)
-constexpr uint32_t JT_OVER = 4096;    // staged past the tile for the records crossing its end
-constexpr int JT_BLOCK = 64;          // one wave per tile: ~27 httpx lines of ~600 B per tile
-__global__ __launch_bounds__(256) void k_json_tile_first(const uint2 *__restrict__ spans, uint32_t R, uint32_t ntiles,
-                                                         uint32_t *__restrict__ first) {
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < R; r += gridDim.x * blockDim.x) {
-        const uint32_t t = spans[r].x / JT_TILE;
-        const uint32_t tp = r ? spans[r - 1].x / JT_TILE + 1 : 0u;
-        for (uint32_t q = tp; q <= t && q < ntiles; ++q) first[q] = r;
-        if (r == R - 1)
-            for (uint32_t q = t + 1; q <= ntiles; ++q) first[q] = R;
-    }
-}
-
-// One wave per byte tile: the tile (plus JT_OVER bytes) is staged in LDS with coalesced 16-B
-// loads, then each lane walks one record starting in the tile from LDS (round 2 walked every
-// record from HBM, one lane per line: each lane's 16-B loads 600 B apart, every line's cache
-// lines evicted between a lane's loads — 14.9 GB fetched for 2.4 GB of lines). The walk: per
-// 16-byte chunk, SWAR masks of the event bytes (quote, backslash, { [ } ] : ,) and only those
-// positions through a JSON state machine (string/escape state, depth, key at a depth-1
-// colon, value end at a depth-1 comma or the closing brace, whitespace-only framing);
-// requested keys pre-filtered by length and first byte before a byte compare; per-lane key
-// spans in LDS. Escapes act inside strings only, as in a byte walk: a backslash escapes the
-// next byte, whatever it is.
-__global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a, const uint32_t *__restrict__ first, uint32_t ntiles,
-                                                          uint64_t n) {
+// One thread per record: the record is read with aligned 16-byte loads and walked byte by
+// byte with a JSON state machine (string/escape state, depth, key at a
+// depth-1 colon, value end at a depth-1 comma or the closing brace, whitespace-only
+// framing). Per-thread key spans live in LDS. Requested keys are pre-filtered by length
+// and first byte before a byte compare.
+constexpr int JT_BLOCK = 128;
+__global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
     extern __shared__ uint2 s_span[];  // JT_BLOCK * nkeys
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[JT_TILE + JT_OVER];
     __shared__ uint8_t s_keys[JS_KEYBYTES];
     __shared__ uint32_t s_koff[JS_MAXKEYS + 1];
     __shared__ uint32_t s_kid[JS_MAXKEYS];  // klen | first byte << 16
@@ -364,130 +329,128 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a, const uint
         const uint32_t kl = s_koff[q + 1] - s_koff[q];
         s_kid[q] = kl | ((kl ? (uint32_t)s_keys[s_koff[q]] : 0x100u) << 16);
     }
+    __syncthreads();
     const uint32_t nk = a.nkeys;
     uint2 *my = s_span + threadIdx.x * nk;
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint32_t r0 = first[tile], r1 = first[tile + 1];
-        if (r0 == r1) continue;  // block-uniform
-        const uint32_t t0 = tile * JT_TILE;
-        const uint32_t t1 = (uint32_t)min<uint64_t>((uint64_t)t0 + JT_TILE + JT_OVER, n & ~15ull);
-        __syncthreads();  // the previous tile's walks are done with s_tile
-        for (uint32_t q = threadIdx.x * 16u; t0 + q < t1; q += JT_BLOCK * 16u)
-            *reinterpret_cast<uint4 *>(s_tile + q) = *reinterpret_cast<const uint4 *>(a.buf + t0 + q);
-        __syncthreads();
-        const JsTileBuf B{a.buf, s_tile, t0, t1 > t0 ? t1 : t0};
-        for (uint32_t r = r0 + threadIdx.x; r < r1; r += JT_BLOCK) {
-            const uint2 sp = a.spans[r];
-            for (uint32_t k = 0; k < nk; ++k) my[k] = make_uint2(JS_NONE, 0);
-            uint32_t depth = 0, str_s = 0, str_e = 0, val_s = 0, open_pos = JS_NONE, close_pos = JS_NONE;
-            uint32_t first_nws = JS_NONE, last_nws = 0;
-            int cur_key = -1;
-            bool in_str = false, kesc = false, bad = false, done = false;
-            uint32_t esc_pos = JS_NONE;
-            for (uint32_t w = sp.x & ~15u; w < sp.y && !bad; w += 16) {
-                const uint4 v = B.chunk(w);
-                uint32_t ev = 0;
-                const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+    for (uint32_t r = blockIdx.x * JT_BLOCK + threadIdx.x; r < a.R; r += gridDim.x * JT_BLOCK) {
+        const uint2 sp = a.spans[r];
+        for (uint32_t k = 0; k < nk; ++k) my[k] = make_uint2(JS_NONE, 0);
+        uint32_t depth = 0, str_s = 0, str_e = 0, val_s = 0, open_pos = JS_NONE, close_pos = JS_NONE;
+        uint32_t first_nws = JS_NONE, last_nws = 0, c0 = 0;
+        int cur_key = -1;
+        bool in_str = false, esc = false, kesc = false, bad = false, done = false;
+        // Per 16-byte chunk, SWAR masks of the event bytes (quote, backslash, { [ } ] : ,) and
+        // only those positions walked through the state machine — JSON lines hold an event
+        // every few bytes, and every other byte only matters for the line's first and last
+        // non-blank bytes (found after the walk). Escapes act inside strings only, as in a
+        // byte walk: a backslash escapes the next byte, whatever it is.
+        uint32_t esc_pos = JS_NONE;
+        // two chunks' loads in flight per step (the walk of one chunk hides the next's latency)
+        uint4 vn = *reinterpret_cast<const uint4 *>(a.buf + (sp.x & ~15u));
+        for (uint32_t w = sp.x & ~15u; w < sp.y && !bad; w += 16) {
+            const uint4 v = vn;
+            if (w + 16u < sp.y) vn = *reinterpret_cast<const uint4 *>(a.buf + w + 16u);
+            uint32_t ev = 0;
+            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const uint32_t x = wd[d];
-                    auto eqm = [](uint32_t y) -> uint32_t {  // high bit of each zero byte of y
-                        return ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
-                    };
-                    const uint32_t lx = x | 0x20202020u;  // '[' -> '{', ']' -> '}'
-                    const uint32_t z = eqm(x ^ 0x22222222u) | eqm(x ^ 0x5c5c5c5cu) | eqm(lx ^ 0x7b7b7b7bu) |
-                                       eqm(lx ^ 0x7d7d7d7du) | eqm(x ^ 0x3a3a3a3au) | eqm(x ^ 0x2c2c2c2cu);
-                    ev |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * d);
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t x = wd[d];
+                auto eqm = [](uint32_t y) -> uint32_t {  // high bit of each zero byte of y
+                    return ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
+                };
+                const uint32_t lx = x | 0x20202020u;  // '[' -> '{', ']' -> '}'
+                const uint32_t z = eqm(x ^ 0x22222222u) | eqm(x ^ 0x5c5c5c5cu) | eqm(lx ^ 0x7b7b7b7bu) |
+                                   eqm(lx ^ 0x7d7d7d7du) | eqm(x ^ 0x3a3a3a3au) | eqm(x ^ 0x2c2c2c2cu);
+                ev |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * d);
+            }
+            if (w < sp.x) ev &= ~0u << (sp.x - w);
+            if (sp.y - w < 16u) ev &= (1u << (sp.y - w)) - 1u;
+            while (ev && !bad) {
+                const uint32_t j = (uint32_t)__builtin_ctz(ev);
+                ev &= ev - 1u;
+                const uint32_t q = w + j;
+                const uint32_t xw = (j < 8u) ? ((j < 4u) ? v.x : v.y) : ((j < 12u) ? v.z : v.w);
+                const uint32_t b = (xw >> (8u * (j & 3u))) & 0xffu;
+                if (in_str) {
+                    if (q == esc_pos) continue;  // the escaped byte
+                    if (b == '\\') { esc_pos = q + 1; kesc = true; }
+                    else if (b == '"') { in_str = false; str_e = q; }
+                    continue;
                 }
-                if (w < sp.x) ev &= ~0u << (sp.x - w);
-                if (sp.y - w < 16u) ev &= (1u << (sp.y - w)) - 1u;
-                while (ev && !bad) {
-                    const uint32_t j = (uint32_t)__builtin_ctz(ev);
-                    ev &= ev - 1u;
-                    const uint32_t q = w + j;
-                    const uint32_t xw = (j < 8u) ? ((j < 4u) ? v.x : v.y) : ((j < 12u) ? v.z : v.w);
-                    const uint32_t b = (xw >> (8u * (j & 3u))) & 0xffu;
-                    if (in_str) {
-                        if (q == esc_pos) continue;  // the escaped byte
-                        if (b == '\\') { esc_pos = q + 1; kesc = true; }
-                        else if (b == '"') { in_str = false; str_e = q; }
-                        continue;
+                if (b == '\\') continue;  // outside strings a backslash is no event
+                if (b == '"') {
+                    if (depth == 0) bad = true;
+                    in_str = true;
+                    kesc = false;
+                    str_s = q + 1;
+                    esc_pos = JS_NONE;
+                    continue;
+                }
+                if (done) { bad = true; continue; }
+                if (b == '{' || b == '[') {
+                    if (depth == 0) {
+                        if (b != '{') bad = true;
+                        open_pos = q;
                     }
-                    if (b == '\\') continue;  // outside strings a backslash is no event
-                    if (b == '"') {
-                        if (depth == 0) bad = true;
-                        in_str = true;
-                        kesc = false;
-                        str_s = q + 1;
-                        esc_pos = JS_NONE;
-                        continue;
+                    ++depth;
+                } else if (b == '}' || b == ']') {
+                    if (depth == 0) { bad = true; continue; }
+                    if (depth == 1) {
+                        if (b != '}') bad = true;
+                        if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
+                        cur_key = -1;
+                        done = true;
+                        close_pos = q;
                     }
-                    if (done) { bad = true; continue; }
-                    if (b == '{' || b == '[') {
-                        if (depth == 0) {
-                            if (b != '{') bad = true;
-                            open_pos = q;
-                        }
-                        ++depth;
-                    } else if (b == '}' || b == ']') {
-                        if (depth == 0) { bad = true; continue; }
-                        if (depth == 1) {
-                            if (b != '}') bad = true;
-                            if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
-                            cur_key = -1;
-                            done = true;
-                            close_pos = q;
-                        }
-                        --depth;
-                    } else if (depth == 1) {
-                        if (b == ':') {
-                            const uint32_t kl = str_e - str_s;
-                            const uint32_t c0 = kl ? (uint32_t)B[str_s] : 0x100u;
-                            const uint32_t id = kl | (c0 << 16);
-                            cur_key = -1;
-                            for (uint32_t k = 0; k < nk; ++k) {
-                                bool eq;
-                                if (kesc) {  // escaped key: compare its decoded form
-                                    JsKeyEq cmp{s_keys + s_koff[k], s_koff[k + 1] - s_koff[k]};
-                                    js_decode<true>(B, str_s, str_e, cmp);
-                                    eq = cmp.eq();
-                                } else {
-                                    if (s_kid[k] != id) continue;
-                                    eq = true;
-                                    for (uint32_t x = 1; x < kl && eq; ++x) eq = B[str_s + x] == s_keys[s_koff[k] + x];
-                                }
-                                if (eq) { cur_key = (int)k; break; }
+                    --depth;
+                } else if (depth == 1) {
+                    if (b == ':') {
+                        const uint32_t kl = str_e - str_s;
+                        const uint32_t c0 = kl ? (uint32_t)a.buf[str_s] : 0x100u;
+                        const uint32_t id = kl | (c0 << 16);
+                        cur_key = -1;
+                        for (uint32_t k = 0; k < nk; ++k) {
+                            bool eq;
+                            if (kesc) {  // escaped key: compare its decoded form
+                                JsKeyEq cmp{s_keys + s_koff[k], s_koff[k + 1] - s_koff[k]};
+                                js_decode<true>(a.buf, str_s, str_e, cmp);
+                                eq = cmp.eq();
+                            } else {
+                                if (s_kid[k] != id) continue;
+                                eq = true;
+                                for (uint32_t x = 1; x < kl && eq; ++x) eq = a.buf[str_s + x] == s_keys[s_koff[k] + x];
                             }
-                            val_s = q + 1;
-                        } else {  // ','
-                            if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
-                            cur_key = -1;
+                            if (eq) { cur_key = (int)k; break; }
                         }
+                        val_s = q + 1;
+                    } else {  // ','
+                        if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
+                        cur_key = -1;
                     }
                 }
             }
-            // the line's first and last non-blank bytes (a JSON line starts with '{' and ends
-            // with '}', so these loops stop at once)
-            if (!bad) {
-                for (uint32_t q = sp.x; q < sp.y; ++q)
-                    if (!js_ws(B[q])) { first_nws = q; break; }
-                for (uint32_t q = sp.y; q > sp.x; --q)
-                    if (!js_ws(B[q - 1])) { last_nws = q - 1; break; }
+        }
+        // the line's first and last non-blank bytes (a JSON line starts with '{' and ends
+        // with '}', so these loops stop at once)
+        if (!bad) {
+            for (uint32_t q = sp.x; q < sp.y; ++q)
+                if (!js_ws(a.buf[q])) { first_nws = q; break; }
+            for (uint32_t q = sp.y; q > sp.x; --q)
+                if (!js_ws(a.buf[q - 1])) { last_nws = q - 1; break; }
+        }
+        const bool ok = !bad && !in_str && depth == 0 && done && first_nws == open_pos && last_nws == close_pos;
+        for (uint32_t k = 0; k < nk; ++k) {
+            uint4 d = make_uint4(0, 0, 0, 0);
+            const uint2 vsp = my[k];
+            if (ok && vsp.x != JS_NONE) {
+                uint32_t vs = vsp.x, ve = vsp.y;
+                while (vs < ve && js_ws(a.buf[vs])) ++vs;
+                while (ve > vs && js_ws(a.buf[ve - 1])) --ve;
+                JsCount cnt;
+                js_value(a.buf, vs, ve, cnt);
+                d = make_uint4(vs, ve, cnt.rows, cnt.bytes);
             }
-            const bool ok = !bad && !in_str && depth == 0 && done && first_nws == open_pos && last_nws == close_pos;
-            for (uint32_t k = 0; k < nk; ++k) {
-                uint4 d = make_uint4(0, 0, 0, 0);
-                const uint2 vsp = my[k];
-                if (ok && vsp.x != JS_NONE) {
-                    uint32_t vs = vsp.x, ve = vsp.y;
-                    while (vs < ve && js_ws(B[vs])) ++vs;
-                    while (ve > vs && js_ws(B[ve - 1])) --ve;
-                    JsCount cnt;
-                    js_value(B, vs, ve, cnt);
-                    d = make_uint4(vs, ve, cnt.rows, cnt.bytes);
-                }
-                a.desc[(size_t)r * nk + k] = d;
-            }
+            a.desc[(size_t)r * nk + k] = d;
         }
     }
 }
@@ -518,33 +481,17 @@ struct JsWrite {
     }
 };
 
-// The rows of every (record, key) value, per byte tile as k_json_scan_t: the tile staged in
-// LDS, one lane per (record starting in the tile, key) item decoding from it.
-__global__ __launch_bounds__(JT_BLOCK) void k_json_emit(const uint8_t *__restrict__ buf, const uint4 *__restrict__ desc,
-                                                        const uint64_t *__restrict__ offs, uint32_t nkeys,
-                                                        uint8_t *__restrict__ out, uint32_t *__restrict__ row_rec,
-                                                        uint32_t *__restrict__ row_key, const uint32_t *__restrict__ first,
-                                                        uint32_t ntiles, uint64_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[JT_TILE + JT_OVER];
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint32_t r0 = first[tile], r1 = first[tile + 1];
-        if (r0 == r1) continue;  // block-uniform
-        const uint32_t t0 = tile * JT_TILE;
-        const uint32_t t1 = (uint32_t)min<uint64_t>((uint64_t)t0 + JT_TILE + JT_OVER, n & ~15ull);
-        __syncthreads();
-        for (uint32_t q = threadIdx.x * 16u; t0 + q < t1; q += JT_BLOCK * 16u)
-            *reinterpret_cast<uint4 *>(s_tile + q) = *reinterpret_cast<const uint4 *>(buf + t0 + q);
-        __syncthreads();
-        const JsTileBuf B{buf, s_tile, t0, t1 > t0 ? t1 : t0};
-        const uint32_t i1 = r1 * nkeys;
-        for (uint32_t i = r0 * nkeys + threadIdx.x; i < i1; i += JT_BLOCK) {
-            const uint4 d = desc[i];
-            if (d.z == 0) continue;
-            const uint64_t off = offs[i];
-            JsWrite w{out, row_rec, row_key, off >> 32, (uint32_t)off, i / nkeys, i % nkeys};
-            js_value(B, d.x, d.y, w);
-        }
-    }
+__global__ __launch_bounds__(256) void k_json_emit(const uint8_t *__restrict__ buf, const uint4 *__restrict__ desc,
+                                                   const uint64_t *__restrict__ offs, uint32_t nitems, uint32_t nkeys,
+                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ row_rec,
+                                                   uint32_t *__restrict__ row_key) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nitems) return;
+    const uint4 d = desc[i];
+    if (d.z == 0) return;
+    const uint64_t off = offs[i];
+    JsWrite w{out, row_rec, row_key, off >> 32, (uint32_t)off, i / nkeys, i % nkeys};
+    js_value(buf, d.x, d.y, w);
 }
 
 int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *keys, const uint32_t *key_offs,
@@ -572,14 +519,9 @@ int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *
     SG_TRY(slot(c, S_F_DESC, items + 1, &desc));
     SG_TRY(slot(c, S_F_OFFS, items + 1, &offs));
     JsonArgs ja{d_buf, L.spans, R, d_keys, d_koff, nkeys, desc};
-    const uint32_t ntiles = (uint32_t)((n + JT_TILE - 1) / JT_TILE);
-    uint32_t *first;
-    SG_TRY(slot(c, S_F_TILES, (size_t)ntiles + 2, &first));
-    SG_LAUNCH(c, "json_tiles", k_json_tile_first, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, L.spans, R, ntiles,
-              first);
-    const uint32_t grid = std::min<uint32_t>(ntiles, 256u * 32u);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((R + JT_BLOCK - 1) / JT_BLOCK, 256u * 16u);
     SG_LAUNCH_B(c, "json_scan", (double)n + 16.0 * items, k_json_scan_t, grid, JT_BLOCK,
-                JT_BLOCK * nkeys * sizeof(uint2), ja, (const uint32_t *)first, ntiles, (uint64_t)n);
+                JT_BLOCK * nkeys * sizeof(uint2), ja);
     uint64_t total = 0;
     SG_TRY(run_scan64(c, "json_scan_len", JsonLen{desc}, (uint32_t)items, offs, &total));
     const uint64_t rows = total & 0xffffffffu, bytes = total >> 32;
@@ -588,8 +530,8 @@ int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *
     SG_TRY(slot(c, S_F_OUT, bytes + 16, &out));
     SG_TRY(slot(c, S_F_REC, rows + 1, &rrec));
     SG_TRY(slot(c, S_F_KEY, rows + 1, &rkey));
-    SG_LAUNCH_B(c, "json_emit", 2.0 * bytes + 8.0 * rows, k_json_emit, grid, JT_BLOCK, 0, d_buf, desc, offs, nkeys, out,
-                rrec, rkey, (const uint32_t *)first, ntiles, (uint64_t)n);
+    SG_LAUNCH_B(c, "json_emit", 2.0 * bytes + 8.0 * rows, k_json_emit, (uint32_t)((items + 255) / 256), 256, 0, d_buf,
+                desc, offs, (uint32_t)items, nkeys, out, rrec, rkey);
     res->data = out;
     res->bytes = bytes;
     res->rows = rows;
