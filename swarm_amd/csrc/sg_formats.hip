@@ -339,21 +339,45 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
         uint32_t first_nws = JS_NONE, last_nws = 0, c0 = 0;
         int cur_key = -1;
         bool in_str = false, esc = false, kesc = false, bad = false, done = false;
+        // vbs: a backslash (in or out of a string) inside the current member's value; escm:
+        // per requested key, whether its (last) value held one — a value without any takes
+        // the counting fast path below (its rows are its raw text, no byte walk)
+        bool vbs = false;
+        uint64_t escm = 0;
         // Per 16-byte chunk, SWAR masks of the event bytes (quote, backslash, { [ } ] : ,) and
         // only those positions walked through the state machine — JSON lines hold an event
         // every few bytes, and every other byte only matters for the line's first and last
         // non-blank bytes (found after the walk). Escapes act inside strings only, as in a
         // byte walk: a backslash escapes the next byte, whatever it is.
         uint32_t esc_pos = JS_NONE;
-        // two chunks' loads in flight per step (the walk of one chunk hides the next's latency)
-        uint4 vn = *reinterpret_cast<const uint4 *>(a.buf + (sp.x & ~15u));
-        for (uint32_t w = sp.x & ~15u; w < sp.y && !bad; w += 16) {
-            const uint4 v = vn;
-            if (w + 16u < sp.y) vn = *reinterpret_cast<const uint4 *>(a.buf + w + 16u);
-            uint32_t ev = 0;
-            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        // 64-byte steps: a lane's four 16-B loads of a step are issued together (a half cache
+        // line per request instead of 16 B, so a line evicted between a lane's steps is
+        // fetched 2x rather than 8x), and the next step's four are in flight while this one
+        // is walked
+        const uint4 *gb = reinterpret_cast<const uint4 *>(a.buf);
+        const uint32_t w0 = sp.x & ~63u;
+        uint4 n0, n1, n2, n3;
+        {
+            const uint32_t c = w0 >> 4;
+            n0 = w0 + 16u > sp.x && w0 < sp.y ? gb[c] : make_uint4(0, 0, 0, 0);
+            n1 = w0 + 32u > sp.x && w0 + 16u < sp.y ? gb[c + 1] : make_uint4(0, 0, 0, 0);
+            n2 = w0 + 48u > sp.x && w0 + 32u < sp.y ? gb[c + 2] : make_uint4(0, 0, 0, 0);
+            n3 = w0 + 64u > sp.x && w0 + 48u < sp.y ? gb[c + 3] : make_uint4(0, 0, 0, 0);
+        }
+        for (uint32_t w = w0; w < sp.y && !bad; w += 64) {
+            const uint4 v0 = n0, v1 = n1, v2 = n2, v3 = n3;
+            {
+                const uint32_t wn = w + 64u, c = wn >> 4;
+                n0 = wn < sp.y ? gb[c] : make_uint4(0, 0, 0, 0);
+                n1 = wn + 16u < sp.y ? gb[c + 1] : make_uint4(0, 0, 0, 0);
+                n2 = wn + 32u < sp.y ? gb[c + 2] : make_uint4(0, 0, 0, 0);
+                n3 = wn + 48u < sp.y ? gb[c + 3] : make_uint4(0, 0, 0, 0);
+            }
+            uint64_t ev = 0;
+            const uint32_t wd[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                                     v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
+            for (int d = 0; d < 16; ++d) {
                 const uint32_t x = wd[d];
                 auto eqm = [](uint32_t y) -> uint32_t {  // high bit of each zero byte of y
                     return ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
@@ -361,23 +385,29 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
                 const uint32_t lx = x | 0x20202020u;  // '[' -> '{', ']' -> '}'
                 const uint32_t z = eqm(x ^ 0x22222222u) | eqm(x ^ 0x5c5c5c5cu) | eqm(lx ^ 0x7b7b7b7bu) |
                                    eqm(lx ^ 0x7d7d7d7du) | eqm(x ^ 0x3a3a3a3au) | eqm(x ^ 0x2c2c2c2cu);
-                ev |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * d);
+                ev |= (uint64_t)(((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * d);
             }
-            if (w < sp.x) ev &= ~0u << (sp.x - w);
-            if (sp.y - w < 16u) ev &= (1u << (sp.y - w)) - 1u;
+            if (w < sp.x) ev &= ~0ull << (sp.x - w);
+            if (sp.y - w < 64u) ev &= (1ull << (sp.y - w)) - 1ull;
             while (ev && !bad) {
-                const uint32_t j = (uint32_t)__builtin_ctz(ev);
+                const uint32_t j = (uint32_t)__builtin_ctzll(ev);
                 ev &= ev - 1u;
                 const uint32_t q = w + j;
-                const uint32_t xw = (j < 8u) ? ((j < 4u) ? v.x : v.y) : ((j < 12u) ? v.z : v.w);
+                // word j / 4 of the step by a select tree on values (register-resident)
+                const bool o1 = (j >> 2) & 1u, o2 = (j >> 3) & 1u;
+                const uint32_t s0 = o2 ? (o1 ? v0.w : v0.z) : (o1 ? v0.y : v0.x);
+                const uint32_t s1 = o2 ? (o1 ? v1.w : v1.z) : (o1 ? v1.y : v1.x);
+                const uint32_t s2 = o2 ? (o1 ? v2.w : v2.z) : (o1 ? v2.y : v2.x);
+                const uint32_t s3 = o2 ? (o1 ? v3.w : v3.z) : (o1 ? v3.y : v3.x);
+                const uint32_t xw = (j & 32u) ? ((j & 16u) ? s3 : s2) : ((j & 16u) ? s1 : s0);
                 const uint32_t b = (xw >> (8u * (j & 3u))) & 0xffu;
                 if (in_str) {
                     if (q == esc_pos) continue;  // the escaped byte
-                    if (b == '\\') { esc_pos = q + 1; kesc = true; }
+                    if (b == '\\') { esc_pos = q + 1; kesc = true; vbs = true; }
                     else if (b == '"') { in_str = false; str_e = q; }
                     continue;
                 }
-                if (b == '\\') continue;  // outside strings a backslash is no event
+                if (b == '\\') { vbs = true; continue; }  // outside strings a backslash is no event
                 if (b == '"') {
                     if (depth == 0) bad = true;
                     in_str = true;
@@ -397,7 +427,10 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
                     if (depth == 0) { bad = true; continue; }
                     if (depth == 1) {
                         if (b != '}') bad = true;
-                        if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
+                        if (cur_key >= 0) {
+                            my[cur_key] = make_uint2(val_s, q);
+                            escm = (escm & ~(1ull << cur_key)) | ((uint64_t)vbs << cur_key);
+                        }
                         cur_key = -1;
                         done = true;
                         close_pos = q;
@@ -423,8 +456,12 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
                             if (eq) { cur_key = (int)k; break; }
                         }
                         val_s = q + 1;
+                        vbs = false;
                     } else {  // ','
-                        if (cur_key >= 0) my[cur_key] = make_uint2(val_s, q);
+                        if (cur_key >= 0) {
+                            my[cur_key] = make_uint2(val_s, q);
+                            escm = (escm & ~(1ull << cur_key)) | ((uint64_t)vbs << cur_key);
+                        }
                         cur_key = -1;
                     }
                 }
@@ -446,9 +483,21 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
                 uint32_t vs = vsp.x, ve = vsp.y;
                 while (vs < ve && js_ws(a.buf[vs])) ++vs;
                 while (ve > vs && js_ws(a.buf[ve - 1])) --ve;
-                JsCount cnt;
-                js_value(a.buf, vs, ve, cnt);
-                d = make_uint4(vs, ve, cnt.rows, cnt.bytes);
+                // rows without a walk: a value with no backslash that is not an array is one
+                // row of its raw text, or of the text between its quotes (js_value: a string
+                // without escapes decodes to itself; "" gives no row)
+                const uint8_t c0 = vs < ve ? a.buf[vs] : 0;
+                const bool strv = c0 == '"' && ve - vs >= 2 && a.buf[ve - 1] == '"';
+                if (vs >= ve) {
+                    d = make_uint4(vs, ve, 0, 0);
+                } else if (c0 != '[' && !((escm >> k) & 1u)) {
+                    const uint32_t len = strv ? ve - vs - 2 : ve - vs;
+                    d = make_uint4(vs, ve, len ? 1u : 0u, len ? len + 1u : 0u);
+                } else {
+                    JsCount cnt;
+                    js_value(a.buf, vs, ve, cnt);
+                    d = make_uint4(vs, ve, cnt.rows, cnt.bytes);
+                }
             }
             a.desc[(size_t)r * nk + k] = d;
         }
