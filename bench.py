@@ -468,7 +468,7 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
     cur = corpus.hostport_pieces(pool, per, 0, U, seed=100 + rank, ports_per_host=K)
     del pool
     cur_bytes = sum(p.numel() for p in cur)
-    if world == 1:
+    if world == 1 and args.c5_path == "local":
         parts = sharded.plan_parts(prior_raw, [], 2 << 30)
         split = sharded.choose_splitters(sharded.sample_records(ctx, prior_raw), parts)
         pu, _, pst = sharded.dedup_diff_large(ctx, prior_raw, (), splitters=split, align_parts=True)
@@ -484,7 +484,10 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
                 return sharded.dedup_diff_large(ctx, cur, (), splitters=split, prior_parts=prior_parts)
             return sharded.dedup_diff_large(ctx, cur, [pu], splitters=split)
     else:
-        rounds = D.all_max_int(D.plan_rounds(max(cur_bytes, 1), world))
+        # N > 1 (or --c5-path rounds at N = 1: the per-rank compute of the N-GPU step with no
+        # exchange, for the modelled multi-GPU step in DESIGN.md §5)
+        rounds = D.all_max_int(D.plan_rounds(max(cur_bytes, 1), world)) if world > 1 else \
+            D.plan_rounds(max(cur_bytes, 1), 8)
         split = D.agree_splitters(ctx, prior_raw, world * rounds)
         prior_parts, prior_store = D.build_prior_rounds(ctx, prior_raw, split, rounds)
         del prior_raw
@@ -542,7 +545,9 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
                        "setup_s": round(t_setup, 1),
                        "parallelism": ("byte-range sharding, %d exchange rounds of RCCL all-to-all x%d "
                                        "(backend %s, world size %d)" % (rounds, world, args.dist_backend, world))
-                                      if world > 1 else "single GPU"},
+                                      if world > 1 else ("single GPU" if args.c5_path == "local" else
+                                                         "single GPU, the N-rank step's local path (%d rounds, "
+                                                         "no exchange)" % rounds)},
             "gbps": round(step_bytes * args.steps / el / 1e9, 2),
             "hbm_frac_step": round(step_bytes * args.steps / el / 1e9 / (HBM_PEAK_GBS * world), 4),
             "records": {"in_rank0": st["in_records"], "unique_rank0": st["uniq_records"],
@@ -1145,6 +1150,9 @@ def main():
     ap.add_argument("--c5-hosts", type=int, default=64_000_000, help="C5 hosts (x 4 open-port slots = combos)")
     ap.add_argument("--c5-data", choices=["hosts", "ips"], default="hosts",
                     help="C5 records: host:port names, or 10.x.y.z:port (15M hosts x 16 port slots)")
+    ap.add_argument("--c5-path", choices=["local", "rounds"], default="local",
+                    help="C5 at N = 1: local range parts with the parse handed over (default), or the N-rank "
+                         "rounds step without its exchange (per-rank compute model)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real runs; gloo rehearses N ranks on fewer GPUs")
     ap.add_argument("--route", choices=["range", "hash"], default="range",
