@@ -19,7 +19,8 @@ namespace sg {
 //                           written contiguously
 // No inter-block waits (a single-pass look-back over 4096-item tiles waited cross-XCD
 // round trips per tile on MI355X: 88 µs/pass vs 55 µs for this downsweep at 10M pairs).
-// Algorithmic bytes per pass: 12 B read + 12 B written per pair.
+// Algorithmic bytes per pass: 8 B key + the value read and written per pair (the dedup
+// carries the 8-B span: 16 B read + 16 B written; iota ids: 12 B written).
 
 constexpr int RS_MAXPASS = 8;
 

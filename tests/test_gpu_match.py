@@ -187,6 +187,34 @@ def test_literal_tile_edges(sg, nocase):
     assert m.match(data + b"\n") == S.literal_hits(data + b"\n", sigs, nocase=nocase)
 
 
+@pytest.mark.parametrize("nocase", [False, True])
+def test_literal_strided_class_alignments(sg, nocase):
+    """The 8-gram class is probed at every 4th position only (its patterns file 4 consecutive
+    grams): patterns of lengths 10..20, periodic ones among them, planted at every start
+    residue, overlapping each other and at record/buffer ends."""
+    rng = random.Random(4242 + nocase)
+    sigs = [b"abababababab", b"aaaaaaaaaaaaaaa", b"xyzxyzxyzxyz", b"0123456789", b"01234567890",
+            b"abcdefghijklmnopqrst", b"Hello-World!", b"aaaaaaaaaab"]
+    sigs += [bytes(rng.choice(b"abcdef") for _ in range(L)) for L in range(10, 21)]
+    sigs = list(dict.fromkeys(sigs))
+    lines = []
+    for i in range(400):
+        line = bytearray(rng.choice(b"abcdefxyz ") for _ in range(rng.randint(0, 60)))
+        for _ in range(rng.randint(0, 3)):
+            s = rng.choice(sigs)
+            if nocase:
+                s = bytes(c ^ 0x20 if 97 <= c <= 122 and rng.random() < 0.5 else c for c in s)
+            k = rng.randrange(len(line) + 1)
+            line[k:k] = s
+        lines.append(bytes(line))
+    for pad in range(8):  # every start residue mod 4, twice
+        lines.append(b"." * pad + b"abababababababab" + b"aaaaaaaaaaaaaaaaaaab")
+    data = b"\n".join(lines)
+    m = sg.Matcher(sigs, "literal", nocase=nocase)
+    assert m.match(data) == S.literal_hits(data, sigs, nocase=nocase)
+    assert m.match(data + b"\n") == S.literal_hits(data + b"\n", sigs, nocase=nocase)
+
+
 def test_regex_c4_banners_full_signature_set(sg):
     """C4 shape: nmap-style banners against the full ~10k regex set (corpus regexes +
     synthetic nmap `match` families), bit-exact vs re.search on a sample."""
