@@ -76,7 +76,11 @@ int sg_ctx_reset_stats(sg_ctx *ctx);
 int sg_ctx_memcpy(sg_ctx *ctx, void *dst, const void *src, size_t n);
 /* Which dedup/diff pipeline served the context's last sg_dev_dedup_diff: *path = 0, the radix
  * pipeline — since round 3 the only one in the library (the bucket sample sort and the probe
- * path, both measured slower, live in tools/experiments/); *flags = 0. For tests/benchmarks. */
+ * path, both measured slower, live in tools/experiments/); *flags: bit 0 (SG_SORT_HYBRID) the
+ * current scan's sort ran its top digits globally and finished each group in LDS, bit 1
+ * (SG_SORT_RESORTED) a group did not fit and the plain LSD sort ran again. For tests/benchmarks. */
+#define SG_SORT_HYBRID 1u
+#define SG_SORT_RESORTED 2u
 #define SG_PATH_RADIX 0
 int sg_ctx_last_path(sg_ctx *ctx, int *path, uint32_t *flags);
 /* Sort-key width (bytes after the common prefix, 5..7) the last radix dedup chose from the

@@ -374,8 +374,10 @@ class Context:
         return out.tobytes()
 
     def last_path(self):
-        """(pipeline, flags) of the last dedup_diff on this context: ("radix", 0) — the only
-        pipeline in the library (include/swarmgpu.h sg_ctx_last_path)."""
+        """(pipeline, flags) of the last dedup_diff on this context: ("radix", flags) — the only
+        pipeline in the library; flags bit 0: hybrid sort (top digits global, groups finished
+        in LDS), bit 1: a group overflowed the LDS and the plain LSD sort ran again
+        (include/swarmgpu.h sg_ctx_last_path)."""
         p, f = C.c_int(), C.c_uint32()
         check(lib.sg_ctx_last_path(self._h, C.byref(p), C.byref(f)))
         return {0: "radix"}.get(p.value, str(p.value)), f.value

@@ -72,6 +72,7 @@ enum Slot : int {
     S_PT_CNT, S_PT_PRE, S_PT_BASE,  // piece partition multi-split
     S_PT_SP, S_PT_KEYS,             // piece partition: spans and parts kept from pass 1 for pass 2
     S_PT_RCNT, S_PT_RPRE, S_PT_SPOUT, S_PT_KOUT,  // piece partition: the parts' record spans/keys out
+    S_LS_ERR,  // hybrid radix sort: a group did not fit the local (LDS) sort
     S_NSLOTS
 };
 
@@ -93,7 +94,7 @@ struct sg_ctx {
     size_t slot_cap[sg::S_NSLOTS] = {};
     void *pinned = nullptr;   // host pinned staging for small readbacks (SG_PINNED_BYTES)
     int last_path = 0;        // dedup/diff pipeline of the last call: 0 = the radix pipeline (the only one)
-    uint32_t last_flags = 0;  // always 0 since round 3 (the bucket path's hand-over reasons)
+    uint32_t last_flags = 0;  // dedup sort of the last call: bit 0 hybrid (local LDS sort), bit 1 its overflow re-sort
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
     uint64_t pt_keep_recs = 0;  // piece partition: records the last call kept between its passes

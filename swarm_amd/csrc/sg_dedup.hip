@@ -1087,9 +1087,13 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     SG_TRY(slot(c, vs.lines.vals2, R, &v2));
     uint64_t *K;
     uint2 *V;
-    // the key narrowing to kw bytes happens in the sort's first pass
+    // the key narrowing to kw bytes happens in the sort's first pass; with the key histograms
+    // on the host the sort may finish its low digits per group in LDS (lerr: checked with
+    // the group counts below, before anything trusts the order)
+    uint32_t *lerr = nullptr;
     SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V, "rs_pass", host_hist,
-                            (base >> 16) < 7u ? base >> 16 : 0u));
+                            (base >> 16) < 7u ? base >> 16 : 0u, host_hist ? &lerr : nullptr));
+    if (lerr) c->last_flags |= 1u;
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
     uint8_t *brk;
@@ -1113,14 +1117,18 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
         return run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, seg_total);
     };
+    uint32_t lerr_v = 0;
     auto read2 = [&](const uint64_t *t1, const uint64_t *t2, uint32_t *a1, uint32_t *b1, uint32_t *a2, uint32_t *b2) -> int {
         uint8_t *pin = (uint8_t *)c->pinned;
         SG_HIP(hipMemcpyAsync(pin, t1, 8, hipMemcpyDeviceToHost, c->stream));
         if (t2) SG_HIP(hipMemcpyAsync(pin + 8, t2, 8, hipMemcpyDeviceToHost, c->stream));
+        if (lerr) SG_HIP(hipMemcpyAsync(pin + 16, lerr, 4, hipMemcpyDeviceToHost, c->stream));
         SG_HIP(hipStreamSynchronize(c->stream));
         uint64_t v1 = 0, v2 = 0;
         memcpy(&v1, pin, 8);
         if (t2) memcpy(&v2, pin + 8, 8);
+        lerr_v = 0;
+        if (lerr) memcpy(&lerr_v, pin + 16, 4);
         *a1 = (uint32_t)(v1 >> 31);
         *b1 = (uint32_t)(v1 & 0x7fffffffu);
         if (t2) {
@@ -1130,14 +1138,24 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         return SG_OK;
     };
     uint64_t *gtot, *stot = nullptr;
-    SG_TRY(run_select2_nb(c, "mark_groups", BigGroupPred{K, brk, R, (base >> 16) + 1u}, R, GS, GE, S_COUNT, &gtot));
-    prof_bytes(c, "mark_groups", 9.0 * R);
     // Without a materialised copy the adjacent pass and the segment-head select are queued
     // before the group count comes back (one host sync for both counts); when big groups
     // exist (the 7-byte key was kept: low-entropy text) they wait for the refinement instead.
     const bool speculate = (base >> 16) < 7u;
-    if (speculate) SG_TRY(adjacent_and_heads(d_buf, V, &stot));
-    SG_TRY(read2(gtot, stot, &B, &B2, &ns, &nb));
+    for (;;) {
+        SG_TRY(run_select2_nb(c, "mark_groups", BigGroupPred{K, brk, R, (base >> 16) + 1u}, R, GS, GE, S_COUNT, &gtot));
+        prof_bytes(c, "mark_groups", 9.0 * R);
+        if (speculate) SG_TRY(adjacent_and_heads(d_buf, V, &stot));
+        SG_TRY(read2(gtot, stot, &B, &B2, &ns, &nb));
+        if (!lerr_v) break;
+        // a group outgrew the local sort's LDS (the pairs are intact, unsorted there): the
+        // plain LSD sort of the same pairs (keys already narrowed, histograms unchanged)
+        uint64_t *Ka = (K == L.keys) ? k2 : L.keys;
+        uint2 *Va = (V == L.spans) ? v2 : L.spans;
+        SG_TRY(radix_sort_spans(c, K, V, Ka, Va, R, 0, 64, &K, &V, "rs_pass", host_hist, 0u, nullptr));
+        lerr = nullptr;
+        c->last_flags |= 2u;
+    }
     if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
     if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B, base));
 

@@ -45,7 +45,11 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out,
                      const char *pass_name = "rs_pass", const uint32_t *host_hist = nullptr,
-                     uint32_t narrow_kw = 0);
+                     uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr);
+// lsort_err (with host_hist): allows the hybrid sort (global passes over the top digits, the
+// rest per group in LDS); *lsort_err is then the device word that turns nonzero when a group
+// did not fit the LDS — the pairs are a valid permutation but not sorted, and the caller must
+// sort them again with lsort_err = nullptr (null when the plain LSD sort ran).
 // The 8 digit histograms (bits [0, 64), 8 x 256 counts) of keys, read back to the host.
 int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist);
 // The same histograms queued only (device pointer, 8 x 256 u32), for a combined read-back.

@@ -5,6 +5,8 @@
 
 #include <stdlib.h>
 
+#include <cmath>
+
 namespace sg {
 
 // sg_sort: stable LSD radix sort of (u64 key, u32 value) pairs, reduce-then-scan.
@@ -265,6 +267,210 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
     }
 }
 
+// ------------------------------------------------------------------ hybrid: top digits globally, the rest in LDS
+// When the keys' top m live digits already split them into small groups (expected group
+// size <= 2^HY_SLACK_BITS by the digit entropies), only those m digits get global LSD
+// passes; every group is then finished inside one block's LDS by the remaining live digits
+// (<= 4, packed into a u32 local key). A global pass moves 16 B + 16 B per pair and its
+// up-sweep reads 8 B more; the local sort reads each pair once and writes it once.
+// The result equals the full LSD sort's, ties included (both sorts are stable).
+//
+// Tiles: groups (runs of equal top-m digits) that start in [t * LS_T, (t + 1) * LS_T) are
+// block t's: it sorts [s_t, e_t), s_t = head(t * LS_T), e_t = head((t + 1) * LS_T), where
+// head(x) = the first group start in [x, x + LS_CAP] (else x + LS_CAP, clamped to n). head
+// is monotone, so the tiles partition [0, n) whatever the data; a tile over LS_CAP pairs
+// (a group too large for the LDS) is copied unsorted and flagged, and the caller re-sorts.
+constexpr int LS_BLOCK = 256;
+constexpr int LS_CAP = 4096;           // pairs sorted in one block's LDS
+constexpr int LS_T = 3072;             // base tile (LS_CAP - LS_T: room for the last group)
+constexpr int LS_ITEMS = LS_CAP / LS_BLOCK;
+constexpr int LS_WCH = LS_ITEMS * 64;  // positions per wave (wave-major, row, lane)
+
+// The first group start in [x, min(x + LS_CAP, n)) (n past the end, 0 at 0); *real = 0 when
+// none was found (a group of >= LS_CAP pairs: the tile cannot be sorted in LDS).
+__device__ __forceinline__ uint32_t ls_head(const uint64_t *__restrict__ K, uint32_t n, uint32_t x, uint64_t gmask,
+                                            uint32_t *real) {
+    const uint32_t lane = lane_id();
+    *real = 1;
+    if (x >= n) return n;
+    if (x == 0) return 0;
+    const uint32_t lim = min(n, x + (uint32_t)LS_CAP);
+    for (uint32_t i0 = x; i0 < lim; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool h = i < lim && ((K[i] ^ K[i - 1]) & gmask) != 0;
+        const uint64_t m = __ballot(h);
+        if (m) return i0 + (uint32_t)(__ffsll((long long)m) - 1);
+    }
+    *real = lim == n ? 1u : 0u;
+    return lim;
+}
+
+// lpos: the local key's digit positions (byte q of lpos = key byte of local digit q, LSD
+// order), nloc of them. A tile holds several groups: its pairs are sorted by the local key,
+// then (stable) by their group ordinal in the tile (1 or 2 more digits), which restores the
+// groups' order with each group sorted inside.
+__global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
+                                                       uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t n,
+                                                       uint64_t gmask, uint32_t lpos, uint32_t nloc,
+                                                       uint32_t *__restrict__ err) {
+    __shared__ uint32_t s_key[LS_CAP];
+    __shared__ uint16_t s_idx[LS_CAP];
+    __shared__ uint16_t s_grp[LS_CAP];
+    __shared__ uint32_t s_wh[LS_BLOCK / 64][256];
+    __shared__ uint32_t s_dstart[256];
+    __shared__ uint32_t s_red[LS_BLOCK / 64];
+    __shared__ uint32_t s_se[4];
+    const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
+    const uint32_t t = blockIdx.x;
+    if (wid < 2) {
+        uint32_t real;
+        const uint32_t h = ls_head(K, n, (t + (uint32_t)wid) * (uint32_t)LS_T, gmask, &real);
+        if (lane == 0) { s_se[wid] = h; s_se[2 + wid] = real; }
+    }
+    for (int x = tid; x < (LS_BLOCK / 64) * 256; x += LS_BLOCK) (&s_wh[0][0])[x] = 0;
+    __syncthreads();
+    const uint32_t s = s_se[0], e = max(s_se[1], s);
+    const uint32_t nt = e - s;
+    if (nt == 0) return;
+    if (nt > (uint32_t)LS_CAP || !s_se[2] || !s_se[3]) {
+        // a group larger than the LDS: keep the pairs (a valid permutation), flag the sort
+        for (uint32_t i = s + tid; i < e; i += LS_BLOCK) { Ko[i] = K[i]; Vo[i] = V[i]; }
+        if (tid == 0) atomicOr(err, 1u);
+        return;
+    }
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const uint32_t wbase = (uint32_t)wid * LS_WCH;
+    uint32_t lk[LS_ITEMS], ix[LS_ITEMS], gp[LS_ITEMS];
+    uint32_t wheads = 0;  // group starts in this wave's earlier rows
+#pragma unroll
+    for (int i = 0; i < LS_ITEMS; ++i) {
+        const uint32_t pos = wbase + i * 64 + lane;
+        uint32_t v = 0;
+        bool head = false;
+        if (pos < nt) {
+            const uint64_t k = K[s + pos];
+            head = pos == 0 || ((k ^ K[s + pos - 1]) & gmask) != 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < (int)nloc) v |= (uint32_t)((k >> (8 * ((lpos >> (8 * q)) & 255u))) & 255u) << (8 * q);
+        }
+        const uint64_t hm = __ballot(head);
+        gp[i] = wheads + (uint32_t)__popcll(hm & (lt_mask | (1ull << lane)));  // inclusive, this wave
+        wheads += (uint32_t)__popcll(hm);
+        lk[i] = v;
+        ix[i] = pos;
+    }
+    if (lane == 0) s_red[wid] = wheads;
+    __syncthreads();
+    uint32_t before = 0, ngroups = 0;
+#pragma unroll
+    for (int w = 0; w < LS_BLOCK / 64; ++w) {
+        const uint32_t x = s_red[w];
+        before += (w < wid) ? x : 0u;
+        ngroups += x;
+    }
+#pragma unroll
+    for (int i = 0; i < LS_ITEMS; ++i) gp[i] = gp[i] + before - 1u;  // group ordinal in the tile
+    __syncthreads();  // s_red is reused by the scans below
+    const uint32_t npass = nloc + (ngroups > 1 ? (ngroups > 256 ? 2u : 1u) : 0u);
+    for (uint32_t q = 0; q < npass; ++q) {
+        const bool on_grp = q >= nloc;
+        const int sh = on_grp ? 8 * (int)(q - nloc) : 8 * (int)q;
+        uint32_t r[LS_ITEMS];
+#pragma unroll
+        for (int i = 0; i < LS_ITEMS; ++i) {
+            if (wbase + i * 64 >= nt) { r[i] = 0; continue; }  // wave-uniform: row past the tile
+            const bool valid = (wbase + i * 64 + lane) < nt;
+            const uint32_t d = ((on_grp ? gp[i] : lk[i]) >> sh) & 255u;
+            uint64_t m = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint64_t bb = __ballot((d >> b) & 1u);
+                m &= ((d >> b) & 1u) ? bb : ~bb;
+            }
+            const uint32_t ltc = (uint32_t)__popcll(m & lt_mask);
+            const uint32_t c = s_wh[wid][d];
+            r[i] = c + ltc;
+            if (valid && ltc == 0) s_wh[wid][d] = c + (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < LS_BLOCK / 64; ++w) { const uint32_t x = s_wh[w][tid]; s_wh[w][tid] = run; run += x; }
+        uint32_t tot;
+        s_dstart[tid] = block_excl_scan<LS_BLOCK>(run, &tot, s_red);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < LS_ITEMS; ++i) {
+            if ((wbase + i * 64 + lane) < nt) {
+                const uint32_t d = ((on_grp ? gp[i] : lk[i]) >> sh) & 255u;
+                const uint32_t slot_i = s_dstart[d] + s_wh[wid][d] + r[i];
+                s_key[slot_i] = lk[i];
+                s_idx[slot_i] = (uint16_t)ix[i];
+                s_grp[slot_i] = (uint16_t)gp[i];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < LS_ITEMS; ++i) {
+            const uint32_t pos = wbase + i * 64 + lane;
+            if (pos < nt) { lk[i] = s_key[pos]; ix[i] = s_idx[pos]; gp[i] = s_grp[pos]; }
+        }
+        for (int x = tid; x < (LS_BLOCK / 64) * 256; x += LS_BLOCK) (&s_wh[0][0])[x] = 0;
+        __syncthreads();
+    }
+    // pairs out in sorted order, fetched by their tile offset (the tile was just read: L2)
+#pragma unroll
+    for (int i = 0; i < LS_ITEMS; ++i) {
+        const uint32_t pos = wbase + i * 64 + lane;
+        if (pos < nt) {
+            Ko[s + pos] = K[s + ix[i]];
+            Vo[s + pos] = V[s + ix[i]];
+        }
+    }
+}
+
+// Host plan: the top live digits (in descending significance) until their entropy leaves
+// groups of about 2^HY_SLACK_BITS pairs; hybrid only when 2..4 live digits remain below
+// them (each one a global pass saved). top[]: the global passes (LSD order), lpos/nloc: the
+// local key's digit positions.
+constexpr double HY_SLACK_BITS = 8.0;
+struct HybridPlan {
+    bool on = false;
+    int top[RS_MAXPASS];
+    int ntop = 0;
+    uint32_t lpos = 0, nloc = 0;
+    uint64_t gmask = 0;
+};
+
+static HybridPlan plan_hybrid(const uint32_t *hh, uint32_t n, const int *live, int nlive) {
+    HybridPlan hp;
+    if (n < (1u << 20) || nlive < 3) return hp;
+    const double need = std::log2((double)n) - HY_SLACK_BITS;
+    double acc = 0;
+    int q = nlive;  // live[q..nlive) are the top digits taken
+    while (q > 0 && acc < need) {
+        --q;
+        const int p = live[q];
+        double H = 0;
+        for (int d = 0; d < 256; ++d)
+            if (hh[p * 256 + d]) {
+                const double f = hh[p * 256 + d] / (double)n;
+                H -= f * std::log2(f);
+            }
+        acc += H;
+    }
+    if (acc < need) return hp;
+    const int nl = q;  // live digits below the top ones: sorted locally
+    if (nl < 2 || nl > 4) return hp;
+    hp.on = true;
+    for (int i = q; i < nlive; ++i) hp.top[hp.ntop++] = live[i];
+    for (int i = 0; i < nl; ++i) hp.lpos |= (uint32_t)live[i] << (8 * i);
+    hp.nloc = (uint32_t)nl;
+    hp.gmask = ~0ull << (8 * live[q]);
+    return hp;
+}
+
 int key_hist8_async(sg_ctx *c, const uint64_t *keys, uint32_t n, const uint32_t **dev_hist) {
     uint32_t *hist;
     SG_TRY(slot(c, S_HIST, RS_MAXPASS * 256 * 2 + RS_MAXPASS, &hist));
@@ -293,7 +499,8 @@ template <typename VT>
 static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt, VT *vals_alt,
                         uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
                         VT **vals_out, const char *pass_name, const uint32_t *host_hist = nullptr,
-                        uint32_t narrow_kw = 0) {
+                        uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr) {
+    if (lsort_err) *lsort_err = nullptr;
     *keys_out = keys;
     *vals_out = vals;
     if (n == 0) return SG_OK;
@@ -337,8 +544,16 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     const uint32_t grid = xcd ? 8u * ((ntiles + 7u) / 8u) : ntiles;
     if (narrow_kw && begin_bit != 0) { set_error("radix_sort: narrowing needs the keys' bit 0"); return SG_E_INVAL; }
     if (narrow_kw && nlive == 0) live[nlive++] = 0;  // one (no-op) pass still writes the narrowed keys
-    for (int q = 0; q < nlive; ++q) {
-        const int p = live[q];
+    // hybrid (spans payload, host histograms, a caller that checks the local sort's flag):
+    // global passes over the top digits only, the rest sorted per group in LDS
+    HybridPlan hp;
+    if constexpr (sizeof(VT) == 8) {
+        if (host_hist && lsort_err && begin_bit == 0) hp = plan_hybrid(host_hist, n, live, nlive);
+    }
+    const int *passes = hp.on ? hp.top : live;
+    const int npass = hp.on ? hp.ntop : nlive;
+    for (int q = 0; q < npass; ++q) {
+        const int p = passes[q];
         const int shift = begin_bit + 8 * p;
         const uint32_t kw = q == 0 ? narrow_kw : 0u;  // the first pass narrows as it reads
         SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, grid, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, kw, xcd);
@@ -356,6 +571,20 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
         iota_pending = false;
         uint64_t *tk = ck; ck = ak; ak = tk;
         VT *tv = cv; cv = av; av = tv;
+    }
+    if constexpr (sizeof(VT) == 8) {
+        if (hp.on) {
+            uint32_t *err;
+            SG_TRY(slot(c, S_LS_ERR, 1, &err));
+            SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
+            const uint32_t g = (n + LS_T - 1) / LS_T;
+            // model: key read, key + span fetched in sorted order, both written
+            SG_LAUNCH_B(c, "rs_lsort", 40.0 * n, k_rs_lsort, g, LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask, hp.lpos, hp.nloc,
+                        err);
+            uint64_t *tk = ck; ck = ak; ak = tk;
+            VT *tv = cv; cv = av; av = tv;
+            *lsort_err = err;
+        }
     }
     if constexpr (sizeof(VT) == 4) {
         if (iota_pending) {
@@ -378,9 +607,9 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
 
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out, const char *pass_name,
-                     const uint32_t *host_hist, uint32_t narrow_kw) {
+                     const uint32_t *host_hist, uint32_t narrow_kw, uint32_t **lsort_err) {
     return radix_sort_t<uint2>(c, keys, spans, keys_alt, spans_alt, n, begin_bit, end_bit, false, keys_out, spans_out,
-                               pass_name, host_hist, narrow_kw);
+                               pass_name, host_hist, narrow_kw, lsort_err);
 }
 
 }  // namespace sg

@@ -408,3 +408,67 @@ def test_refinement_packed_chunk_keys(sg, alpha):
     prior = b"".join(r + b"\n" for r in prior_recs)
     assert sg.dedup(cur) == S.dedup(cur)
     assert sg.dedup_diff(cur, prior) == S.dedup_diff(cur, prior)
+
+
+# ------------------------------------------------------------------ hybrid radix sort
+def test_hybrid_sort_subdomains(sg):
+    """1.5M C2-shaped records: the sort runs its top key digits globally and finishes every
+    group in LDS (flags bit 0); output equals the independent numpy reference."""
+    import torch
+    from swarm_amd import corpus
+    buf, ids = corpus.subdomains(1_500_000, seed=77)
+    prior = corpus.prior_of(ids)
+    d_cur = torch.from_numpy(buf).cuda()
+    d_pri = torch.from_numpy(prior).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        r = ctx.dedup_diff(d_cur.data_ptr(), d_cur.numel(), d_pri.data_ptr(), d_pri.numel())
+        assert ctx.last_path()[1] & 3 == 1
+        urows = corpus.sorted_unique_rows(ids)
+        frows = urows[~np.isin(urows, corpus.prior_rows(ids))]
+        assert ctx.to_bytes(r.uniq, r.uniq_bytes) == corpus.serialize_rows(urows).tobytes()
+        assert ctx.to_bytes(r.fresh, r.fresh_bytes) == corpus.serialize_rows(frows).tobytes()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("shape", ["overflow", "ties"])
+def test_hybrid_sort_overflow_and_ties(sg, shape):
+    """overflow: half the records share their first 3 bytes, so the groups the global digits
+    leave are far larger than one block's LDS: the local sort flags it and the plain LSD sort
+    runs again (flags bits 0 and 1). ties: distinct records sharing all sorted key bytes,
+    short records (live length tag), duplicates: the local sort keeps them in input order
+    like the full sort. Both equal the oracle."""
+    import torch
+    rng = np.random.default_rng(5 if shape == "overflow" else 6)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", dtype=np.uint8)
+    n = 1_200_000
+    if shape == "overflow":
+        body = alpha[rng.integers(0, 36, size=(n, 11))]
+        body[: n // 2, :3] = ord("a")
+        recs = [bytes(r) for r in body]
+    else:
+        heads = alpha[rng.integers(0, 36, size=(n // 3, 8))]
+        recs = []
+        for i in range(n):
+            h = bytes(heads[rng.integers(0, n // 3)])
+            k = int(rng.integers(0, 10))
+            recs.append(h[: 3 + k % 5] if k < 2 else h + bytes(alpha[rng.integers(0, 36, size=k % 4)]))
+    rng.shuffle(recs)
+    cur = b"\n".join(recs) + b"\n"
+    prior = S.dedup(b"\n".join(recs[::4]) + b"\n")
+    dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+    dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        r = ctx.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+        flags = ctx.last_path()[1]
+        eu, ef = S.dedup_diff(cur, prior)
+        assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+        assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+        if shape == "overflow":
+            assert flags & 3 == 3
+        else:
+            assert flags & 1
+    finally:
+        ctx.close()
