@@ -72,7 +72,7 @@ enum Slot : int {
     S_PT_CNT, S_PT_PRE, S_PT_BASE,  // piece partition multi-split
     S_PT_SP, S_PT_KEYS,             // piece partition: spans and parts kept from pass 1 for pass 2
     S_PT_RCNT, S_PT_RPRE, S_PT_SPOUT, S_PT_KOUT,  // piece partition: the parts' record spans/keys out
-    S_LS_ERR,  // hybrid radix sort: a group did not fit the local (LDS) sort
+    S_LS_ERR, S_LS_BOUNDS,  // hybrid radix sort: overflow flag, local-sort tile bounds
     S_NSLOTS
 };
 

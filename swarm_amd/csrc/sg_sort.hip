@@ -280,9 +280,15 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
 // head(x) = the first group start in [x, x + LS_CAP] (else x + LS_CAP, clamped to n). head
 // is monotone, so the tiles partition [0, n) whatever the data; a tile over LS_CAP pairs
 // (a group too large for the LDS) is copied unsorted and flagged, and the caller re-sorts.
-constexpr int LS_BLOCK = 256;
+#ifndef SG_LS_BLOCK
+#define SG_LS_BLOCK 512
+#endif
+constexpr int LS_BLOCK = SG_LS_BLOCK;  // 256 or 512 (digit owners: the first 256 threads)
 constexpr int LS_CAP = 4096;           // pairs sorted in one block's LDS
-constexpr int LS_T = 3072;             // base tile (LS_CAP - LS_T: room for the last group)
+#ifndef SG_LS_T
+#define SG_LS_T 3584
+#endif
+constexpr int LS_T = SG_LS_T;          // base tile (LS_CAP - LS_T: room for the last group)
 constexpr int LS_ITEMS = LS_CAP / LS_BLOCK;
 constexpr int LS_WCH = LS_ITEMS * 64;  // positions per wave (wave-major, row, lane)
 
@@ -305,6 +311,18 @@ __device__ __forceinline__ uint32_t ls_head(const uint64_t *__restrict__ K, uint
     return lim;
 }
 
+// bounds[t] = head(t * LS_T) | real << 31, t = 0 .. ntiles (one wave per boundary): the group
+// search runs as its own launch, many waves in flight, instead of at the head of every
+// local-sort block.
+__global__ __launch_bounds__(256) void k_rs_lbounds(const uint64_t *__restrict__ K, uint32_t n, uint64_t gmask,
+                                                    uint32_t nb, uint32_t *__restrict__ bounds) {
+    const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= nb) return;
+    uint32_t real;
+    const uint32_t h = ls_head(K, n, t * (uint32_t)LS_T, gmask, &real);
+    if (lane_id() == 0) bounds[t] = h | (real << 31);
+}
+
 // lpos: the local key's digit positions (byte q of lpos = key byte of local digit q, LSD
 // order), nloc of them. A tile holds several groups: its pairs are sorted by the local key,
 // then (stable) by their group ordinal in the tile (1 or 2 more digits), which restores the
@@ -312,36 +330,35 @@ __device__ __forceinline__ uint32_t ls_head(const uint64_t *__restrict__ K, uint
 __global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
                                                        uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t n,
                                                        uint64_t gmask, uint32_t lpos, uint32_t nloc,
-                                                       uint32_t *__restrict__ err) {
+                                                       const uint32_t *__restrict__ bounds, uint32_t *__restrict__ err) {
     __shared__ uint32_t s_key[LS_CAP];
-    __shared__ uint16_t s_idx[LS_CAP];
-    __shared__ uint16_t s_grp[LS_CAP];
+    __shared__ uint32_t s_ig[LS_CAP];  // tile offset | group ordinal << 16
     __shared__ uint32_t s_wh[LS_BLOCK / 64][256];
     __shared__ uint32_t s_dstart[256];
     __shared__ uint32_t s_red[LS_BLOCK / 64];
-    __shared__ uint32_t s_se[4];
+    __shared__ uint32_t s_bits[2][LS_BLOCK / 64];
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
     const uint32_t t = blockIdx.x;
-    if (wid < 2) {
-        uint32_t real;
-        const uint32_t h = ls_head(K, n, (t + (uint32_t)wid) * (uint32_t)LS_T, gmask, &real);
-        if (lane == 0) { s_se[wid] = h; s_se[2 + wid] = real; }
-    }
-    for (int x = tid; x < (LS_BLOCK / 64) * 256; x += LS_BLOCK) (&s_wh[0][0])[x] = 0;
-    __syncthreads();
-    const uint32_t s = s_se[0], e = max(s_se[1], s);
+    const uint32_t b0 = bounds[t], b1 = bounds[t + 1];
+    const uint32_t s = b0 & 0x7fffffffu, e = max(b1 & 0x7fffffffu, s);
     const uint32_t nt = e - s;
     if (nt == 0) return;
-    if (nt > (uint32_t)LS_CAP || !s_se[2] || !s_se[3]) {
+    if (nt > (uint32_t)LS_CAP || !(b0 >> 31) || !(b1 >> 31)) {
         // a group larger than the LDS: keep the pairs (a valid permutation), flag the sort
         for (uint32_t i = s + tid; i < e; i += LS_BLOCK) { Ko[i] = K[i]; Vo[i] = V[i]; }
         if (tid == 0) atomicOr(err, 1u);
         return;
     }
+    for (int x = tid; x < (LS_BLOCK / 64) * 256; x += LS_BLOCK) (&s_wh[0][0])[x] = 0;
+    // touch the tile's spans now (one load per 128-B line): the sorted-order gather at the
+    // end then hits L2 instead of waiting on HBM after the last pass
+    uint32_t touch = 0;
+    if ((uint32_t)tid * 16u < nt) touch = V[s + (uint32_t)tid * 16u].x;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     const uint32_t wbase = (uint32_t)wid * LS_WCH;
-    uint32_t lk[LS_ITEMS], ix[LS_ITEMS], gp[LS_ITEMS];
-    uint32_t wheads = 0;  // group starts in this wave's earlier rows
+    uint32_t lk[LS_ITEMS], ig[LS_ITEMS];
+    uint32_t wheads = 0;              // group starts in this wave's earlier rows
+    uint32_t kor = 0, kand = ~0u;     // local-key bits that vary over the tile
 #pragma unroll
     for (int i = 0; i < LS_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane;
@@ -353,38 +370,55 @@ __global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restric
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 if (q < (int)nloc) v |= (uint32_t)((k >> (8 * ((lpos >> (8 * q)) & 255u))) & 255u) << (8 * q);
+            kor |= v;
+            kand &= v;
         }
         const uint64_t hm = __ballot(head);
-        gp[i] = wheads + (uint32_t)__popcll(hm & (lt_mask | (1ull << lane)));  // inclusive, this wave
+        ig[i] = pos | ((wheads + (uint32_t)__popcll(hm & (lt_mask | (1ull << lane)))) << 16);  // inclusive, this wave
         wheads += (uint32_t)__popcll(hm);
         lk[i] = v;
-        ix[i] = pos;
     }
-    if (lane == 0) s_red[wid] = wheads;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kor |= (uint32_t)__shfl_xor((int)kor, o, 64);
+        kand &= (uint32_t)__shfl_xor((int)kand, o, 64);
+    }
+    if (lane == 0) { s_red[wid] = wheads; s_bits[0][wid] = kor; s_bits[1][wid] = kand; }
     __syncthreads();
     uint32_t before = 0, ngroups = 0;
+    kor = 0;
+    kand = ~0u;
 #pragma unroll
     for (int w = 0; w < LS_BLOCK / 64; ++w) {
         const uint32_t x = s_red[w];
         before += (w < wid) ? x : 0u;
         ngroups += x;
+        kor |= s_bits[0][w];
+        kand &= s_bits[1][w];
     }
 #pragma unroll
-    for (int i = 0; i < LS_ITEMS; ++i) gp[i] = gp[i] + before - 1u;  // group ordinal in the tile
+    for (int i = 0; i < LS_ITEMS; ++i) ig[i] = ig[i] + ((before - 1u) << 16);  // group ordinal in the tile
     __syncthreads();  // s_red is reused by the scans below
+    const uint32_t lvary = kor ^ kand;
     const uint32_t npass = nloc + (ngroups > 1 ? (ngroups > 256 ? 2u : 1u) : 0u);
     for (uint32_t q = 0; q < npass; ++q) {
         const bool on_grp = q >= nloc;
-        const int sh = on_grp ? 8 * (int)(q - nloc) : 8 * (int)q;
+        const int sh = on_grp ? 16 + 8 * (int)(q - nloc) : 8 * (int)q;
+        // digit bits that vary over the tile (block-uniform): only those need a ballot
+        const uint32_t gh = on_grp ? (ngroups - 1u) >> (sh - 16) : 0u;  // highest group ordinal's digit
+        const uint32_t vb = on_grp ? (gh >= 128u ? 0xffu : (2u << (31 - __builtin_clz(gh | 1u))) - 1u)
+                                   : ((lvary >> sh) & 255u);
+        if (!on_grp && vb == 0) continue;  // a local digit constant over the tile
         uint32_t r[LS_ITEMS];
 #pragma unroll
         for (int i = 0; i < LS_ITEMS; ++i) {
             if (wbase + i * 64 >= nt) { r[i] = 0; continue; }  // wave-uniform: row past the tile
             const bool valid = (wbase + i * 64 + lane) < nt;
-            const uint32_t d = ((on_grp ? gp[i] : lk[i]) >> sh) & 255u;
+            const uint32_t d = ((on_grp ? ig[i] : lk[i]) >> sh) & 255u;
             uint64_t m = __ballot(valid);
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
+                if (!((vb >> b) & 1u)) continue;
                 const uint64_t bb = __ballot((d >> b) & 1u);
                 m &= ((d >> b) & 1u) ? bb : ~bb;
             }
@@ -395,26 +429,28 @@ __global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restric
         }
         __syncthreads();
         uint32_t run = 0;
+        if (tid < 256) {
 #pragma unroll
-        for (int w = 0; w < LS_BLOCK / 64; ++w) { const uint32_t x = s_wh[w][tid]; s_wh[w][tid] = run; run += x; }
+            for (int w = 0; w < LS_BLOCK / 64; ++w) { const uint32_t x = s_wh[w][tid]; s_wh[w][tid] = run; run += x; }
+        }
         uint32_t tot;
-        s_dstart[tid] = block_excl_scan<LS_BLOCK>(run, &tot, s_red);
+        const uint32_t dst = block_excl_scan<LS_BLOCK>(run, &tot, s_red);
+        if (tid < 256) s_dstart[tid] = dst;
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < LS_ITEMS; ++i) {
             if ((wbase + i * 64 + lane) < nt) {
-                const uint32_t d = ((on_grp ? gp[i] : lk[i]) >> sh) & 255u;
+                const uint32_t d = ((on_grp ? ig[i] : lk[i]) >> sh) & 255u;
                 const uint32_t slot_i = s_dstart[d] + s_wh[wid][d] + r[i];
                 s_key[slot_i] = lk[i];
-                s_idx[slot_i] = (uint16_t)ix[i];
-                s_grp[slot_i] = (uint16_t)gp[i];
+                s_ig[slot_i] = ig[i];
             }
         }
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < LS_ITEMS; ++i) {
             const uint32_t pos = wbase + i * 64 + lane;
-            if (pos < nt) { lk[i] = s_key[pos]; ix[i] = s_idx[pos]; gp[i] = s_grp[pos]; }
+            if (pos < nt) { lk[i] = s_key[pos]; ig[i] = s_ig[pos]; }
         }
         for (int x = tid; x < (LS_BLOCK / 64) * 256; x += LS_BLOCK) (&s_wh[0][0])[x] = 0;
         __syncthreads();
@@ -424,10 +460,12 @@ __global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restric
     for (int i = 0; i < LS_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane;
         if (pos < nt) {
-            Ko[s + pos] = K[s + ix[i]];
-            Vo[s + pos] = V[s + ix[i]];
+            const uint32_t ix = ig[i] & 0xffffu;
+            Ko[s + pos] = K[s + ix];
+            Vo[s + pos] = V[s + ix];
         }
     }
+    asm volatile("" ::"v"(touch));  // keeps the touch load (its result is not needed)
 }
 
 // Host plan: the top live digits (in descending significance) until their entropy leaves
@@ -578,9 +616,12 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
             SG_TRY(slot(c, S_LS_ERR, 1, &err));
             SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
             const uint32_t g = (n + LS_T - 1) / LS_T;
+            uint32_t *bounds;
+            SG_TRY(slot(c, S_LS_BOUNDS, (size_t)g + 1, &bounds));
+            SG_LAUNCH(c, "rs_lbounds", k_rs_lbounds, (g + 1 + 3) / 4, 256, 0, ck, n, hp.gmask, g + 1, bounds);
             // model: key read, key + span fetched in sorted order, both written
             SG_LAUNCH_B(c, "rs_lsort", 40.0 * n, k_rs_lsort, g, LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask, hp.lpos, hp.nloc,
-                        err);
+                        bounds, err);
             uint64_t *tk = ck; ck = ak; ak = tk;
             VT *tv = cv; cv = av; av = tv;
             *lsort_err = err;
