@@ -82,6 +82,13 @@ static inline uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap = 0x7ff
 __host__ __device__ __forceinline__ uint32_t make_bk(uint32_t base, uint32_t kw) { return base | (kw << 16); }
 __device__ __forceinline__ uint32_t bk_off(uint32_t bk) { return (bk & 0xffffu) + (bk >> 16); }
 __device__ __forceinline__ uint32_t bk_full(uint32_t bk) { return (bk >> 16) + 1u; }
+// key0 (kw = 7) -> the kw-byte key: bytes kw..6 cleared, the tag clamped to kw + 1 (as the
+// sort's first pass narrows; idempotent, so narrowed keys pass through unchanged).
+__device__ __forceinline__ uint64_t key_narrow(uint64_t k, uint32_t kw) {
+    if (kw >= 7u) return k;
+    const uint64_t t = k & 0xffu;
+    return (k & (~0ull << (64u - 8u * kw))) | (t < kw + 1u ? t : (uint64_t)(kw + 1u));
+}
 
 // ------------------------------------------------------------------ predicates / functors
 struct FlagPred {
@@ -501,7 +508,7 @@ constexpr uint32_t DF_PER = DF_TILE / 256;
 // One wave per boundary t: jb[t] = lower_bound(P.K, U.K[t * DF_TILE]) (P.n past the end).
 __global__ __launch_bounds__(256) void k_diff_split(const uint64_t *__restrict__ UK, uint32_t nu,
                                                     const uint64_t *__restrict__ PK, uint32_t np, uint32_t nb,
-                                                    uint32_t *__restrict__ jb) {
+                                                    uint32_t *__restrict__ jb, uint32_t kw) {
     const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = lane_id();
     if (t >= nb) return;
@@ -513,13 +520,13 @@ __global__ __launch_bounds__(256) void k_diff_split(const uint64_t *__restrict__
         const uint32_t span = hi - lo;
         if (span <= 64) {
             const uint32_t p = lo + lane;
-            const bool ge = (p >= hi) || PK[p] >= key;
+            const bool ge = (p >= hi) || key_narrow(PK[p], kw) >= key;
             const uint64_t m = __ballot(ge);
             lo = m ? lo + (uint32_t)(__ffsll((long long)m) - 1) : hi;  // span 64, all below: hi
             break;
         }
         const uint32_t p = lo + (uint32_t)(((uint64_t)span * (lane + 1)) / 65);
-        const bool ge = PK[p] >= key;
+        const bool ge = key_narrow(PK[p], kw) >= key;
         const uint64_t m = __ballot(ge);
         if (!m) {
             lo = (uint32_t)__shfl((int)p, 63, 64) + 1;
@@ -541,6 +548,7 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
     // instead of two (P span, then bytes); U spans load with the U keys
     __shared__ uint64_t s_k[DF_PCAP];
     __shared__ uint2 s_sp[DF_PCAP];
+    const uint32_t kw = base >> 16;  // the prior's keys are narrowed here, as they are read
     const uint32_t t = blockIdx.x;
     const uint32_t i0 = t * DF_TILE;
     const uint32_t j0 = jb[t], j1 = jb[t + 1];
@@ -548,7 +556,7 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
     const bool staged = np <= DF_PCAP;
     if (staged)
         for (uint32_t q = threadIdx.x; q < np; q += 256) {
-            s_k[q] = P.K[j0 + q];
+            s_k[q] = key_narrow(P.K[j0 + q], kw);
             s_sp[q] = P.sp[j0 + q];
         }
     uint32_t idx[DF_PER], cand[DF_PER];
@@ -568,11 +576,12 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
         uint32_t lo = 0, hi = np;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
-            const uint64_t v = staged ? s_k[mid] : P.K[j0 + mid];
+            const uint64_t v = staged ? s_k[mid] : key_narrow(P.K[j0 + mid], kw);
             if (v < ku[k]) lo = mid + 1; else hi = mid;
         }
         cand[k] = j0 + lo;
-        const uint64_t kp = (lo < np) ? (staged ? s_k[lo] : P.K[j0 + lo]) : (j0 + lo < P.n ? P.K[j0 + lo] : ~ku[k]);
+        const uint64_t kp = (lo < np) ? (staged ? s_k[lo] : key_narrow(P.K[j0 + lo], kw))
+                                      : (j0 + lo < P.n ? key_narrow(P.K[j0 + lo], kw) : ~ku[k]);
         const bool eq = idx[k] < U.n && j0 + lo < P.n && kp == ku[k];
         pres[k] = eq && (ku[k] & 0xffu) < bk_full(base);
         need[k] = eq && !pres[k];
@@ -607,13 +616,13 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
             for (;;) {
                 const uint32_t probe = lo2 + step - 1;
                 if (probe >= P.n) break;
-                if (P.K[probe] != ku[k]) { hi2 = probe; break; }
+                if (key_narrow(P.K[probe], kw) != ku[k]) { hi2 = probe; break; }
                 lo2 = probe + 1;
                 step <<= 1;
             }
             while (lo2 < hi2) {  // first index in [lo2, hi2) whose key differs
                 const uint32_t mid = (lo2 + hi2) >> 1;
-                if (P.K[mid] == ku[k]) lo2 = mid + 1; else hi2 = mid;
+                if (key_narrow(P.K[mid], kw) == ku[k]) lo2 = mid + 1; else hi2 = mid;
             }
             ce = lo2;
         }
@@ -1329,10 +1338,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         else if (h6 >= lg + 2.0 && live1) kw = 6;
         if (kw < 7) {
             // the cur keys are narrowed by the sort's first pass (build_unique); the prior's
-            // here (its view is the input itself when sorted, and the diff compares keys)
-            if (have_prior && Lp.n_rec)
-                SG_LAUNCH(c, "narrow_keys", k_narrow_keys, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0,
-                          Lp.keys, Lp.n_rec, kw);
+            // as the diff reads them (key_narrow: its view is the input itself when sorted)
             // the narrowed keys' histograms: bytes kw..6 are zero, the tag is clamped to kw + 1
             for (int p = 1; p <= 7 - (int)kw; ++p) {
                 for (int d = 0; d < 256; ++d) hh[p * 256 + d] = 0;
@@ -1377,7 +1383,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint32_t ntiles = (cu.n + DF_TILE - 1) / DF_TILE;
     uint32_t *jb;
     SG_TRY(slot(c, S_R_OFF, (size_t)ntiles + 2, &jb));
-    SG_LAUNCH(c, "diff_split", k_diff_split, grid_for(ntiles + 1, 4), 256, 0, cu.keys, cu.n, pv.keys, pv.n, ntiles + 1, jb);
+    SG_LAUNCH(c, "diff_split", k_diff_split, grid_for(ntiles + 1, 4), 256, 0, cu.keys, cu.n, pv.keys, pv.n, ntiles + 1, jb,
+              bk >> 16);
     // model: key + span of every unique cur record, key of every prior record, the compared
     // bytes of both sides (~ the unique output + the prior), one flag per cur record
     SG_LAUNCH_B(c, "diff_tile", 16.0 * cu.n + 8.0 * pv.n + (double)cu.bytes + cu.n, k_diff_tile, ntiles, 256, 0,

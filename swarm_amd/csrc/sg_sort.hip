@@ -104,8 +104,11 @@ __device__ __forceinline__ uint32_t rs_tile_of(uint32_t b, uint32_t ntiles) {
     return (b & 7u) * per + (b >> 3);
 }
 
-constexpr int RD_BLOCK = 256;
-constexpr int RD_ITEMS = 16;
+#ifndef SG_RD_BLOCK
+#define SG_RD_BLOCK 512
+#endif
+constexpr int RD_BLOCK = SG_RD_BLOCK;  // 256 or 512 threads per 4096-pair tile (digit owners: tid < 256)
+constexpr int RD_ITEMS = 4096 / RD_BLOCK;
 constexpr int RD_TILE = RD_BLOCK * RD_ITEMS;
 constexpr int RD_WAVES = RD_BLOCK / 64;
 
@@ -139,10 +142,12 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__
         }
     }
     __syncthreads();
-    uint32_t v = 0;
+    if (threadIdx.x < 256) {
+        uint32_t v = 0;
 #pragma unroll
-    for (int w = 0; w < RD_WAVES; ++w) v += h[w][threadIdx.x];
-    cnt[(size_t)threadIdx.x * ntiles + tile] = v;
+        for (int w = 0; w < RD_WAVES; ++w) v += h[w][threadIdx.x];
+        cnt[(size_t)threadIdx.x * ntiles + tile] = v;
+    }
 }
 
 // One block per digit d: cnt[d][t] -> exclusive prefix over tiles + goffs[d].
@@ -216,12 +221,16 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
     __syncthreads();
     // thread tid owns digit tid
     uint32_t run = 0;
+    if (tid < 256) {
 #pragma unroll
-    for (int w = 0; w < RD_WAVES; ++w) { const uint32_t x = s_wh[w][tid]; s_wh[w][tid] = run; run += x; }
+        for (int w = 0; w < RD_WAVES; ++w) { const uint32_t x = s_wh[w][tid]; s_wh[w][tid] = run; run += x; }
+    }
     uint32_t blk_total;
     const uint32_t dstart = block_excl_scan<RD_BLOCK>(run, &blk_total, s_red);
-    s_dstart[tid] = dstart;
-    s_gbase[tid] = toffs[(size_t)tid * ntiles + tile] - dstart;
+    if (tid < 256) {
+        s_dstart[tid] = dstart;
+        s_gbase[tid] = toffs[(size_t)tid * ntiles + tile] - dstart;
+    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
