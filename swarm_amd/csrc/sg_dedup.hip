@@ -96,30 +96,6 @@ struct FlagPred {
     __device__ uint32_t operator()(uint32_t i) const { return f[i] ? 1u : 0u; }
 };
 
-// Over the key0-sorted order: brk[i] = i starts a new key0 group; A/B = first/last
-// position of a tag-8 group of more than WAVE_GROUP records (they share 7 bytes).
-struct BigGroupPred {
-    const uint64_t *K;
-    uint8_t *brk;
-    uint32_t n;
-    uint32_t kfull;  // tag of a key with more bytes after it (kw + 1)
-    // all five keys are loaded unconditionally (clamped indices, one round trip; the
-    // +-64 neighbours are cache hits of adjacent waves) instead of after the head test
-    __device__ uint32_t operator()(uint32_t i) const {
-        const uint64_t k = K[i];
-        const uint64_t kp = K[i > 0 ? i - 1 : i], kn = K[i + 1 < n ? i + 1 : i];
-        const uint64_t kp64 = K[i >= WAVE_GROUP ? i - WAVE_GROUP : i];
-        const uint64_t kn64 = K[i + WAVE_GROUP < n ? i + WAVE_GROUP : i];
-        const bool head = (i == 0) || kp != k;
-        brk[i] = head ? 1 : 0;
-        if ((k & 0xffu) != kfull) return 0u;
-        const bool tail = (i + 1 == n) || kn != k;
-        const bool bh = head && (i + WAVE_GROUP < n) && kn64 == k;
-        const bool bt = tail && (i >= WAVE_GROUP) && kp64 == k;
-        return (bh ? 1u : 0u) | (bt ? 2u : 0u);
-    }
-};
-
 // Over the final order of a refinement round: sub-segments by (group, chunk key). brk at
 // every sub-segment head; A/B = bounds of tag-8 sub-segments of more than WAVE_GROUP rows.
 struct RoundGroupPred {
@@ -251,70 +227,120 @@ __device__ __forceinline__ int rec_cmp8(const uint8_t *buf, uint32_t sa, uint32_
     return rec_cmp8_2(buf, sa, la, buf, sb, lb, off);
 }
 
-// dup[i] = record i equals record i-1 inside its segment (tag < 8 key0: whole record).
-// A position whose bytes differ from its predecessor's inside a segment marks the segment
-// bad at its head (walk back to the brk, <= 64 positions): segbad[head] = 1.
-__global__ __launch_bounds__(256) void k_adjacent(const uint8_t *__restrict__ S, const uint2 *__restrict__ SS,
-                                                  const uint64_t *__restrict__ K, const uint8_t *__restrict__ brk,
-                                                  uint32_t n, uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad,
-                                                  uint32_t base) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    // all first-level loads issued together (one round trip before the byte compare)
-    const uint32_t ip = i > 0 ? i - 1 : 0;
-    const uint8_t b = brk[i];
-    const uint64_t ki = K[i];
-    const uint2 x = SS[ip], y = SS[i];
-    bool d = false;
-    if (i > 0 && !b) {
-        d = ((ki & 0xffu) < bk_full(base)) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, bk_off(base));
-        if (!d) {
-            // segment head = last break at or before i - 1 (position 0 at the latest), found
-            // 16 bytes at a time with aligned loads instead of a dependent byte walk
-            uint32_t h = i - 1;
-            for (;;) {
-                const uint32_t a = h & ~15u;
-                const uint4 w = *reinterpret_cast<const uint4 *>(brk + a);
-                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-                uint32_t m = 0;
+// The adjacent pass with the group marking folded in (no count/scan/apply select for the
+// group marks).
+// KEYS: group starts come from the keys (brk[i] = K[i] != K[i-1] is written here) and groups
+// of more than WAVE_GROUP records with a full tag are appended as (GS, GE) pairs for the
+// refinement rounds (rare: wave-aggregated atomics, unordered — the refinement rounds place
+// each group's rows by their positions); otherwise brk is given (after refinement:
+// sub-segment heads) and read.
+// DUP: dup[i] = record i equals record i-1 inside its segment; segbad[i] = it differs (the
+// segment needs sorting; SegHeadPred lists its head).
+// cnt[2] = big groups (zeroed by the caller).
+// Bit j (0..15) = byte j of the 16-B word is nonzero.
+__device__ __forceinline__ uint32_t swar_nonzero16(uint4 w) {
+    const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+    uint32_t m = 0;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t t = (((ww[q] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | ww[q]) & 0x80808080u;
-                    m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * q);
-                }
-                m &= (2u << (h - a)) - 1u;  // positions a .. h
-                if (m) { h = a + 31u - (uint32_t)__clz(m); break; }
-                if (a == 0) { h = 0; break; }
-                h = a - 1;
-            }
-            segbad[h] = 1;
-        }
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t t = (((ww[q] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | ww[q]) & 0x80808080u;
+        m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * q);
     }
-    dup[i] = d ? 1 : 0;
+    return m;
 }
 
-// Heads of bad segments: A = up to SEG_SMALL members, B = more (<= 64).
-struct SegPred {
+struct AdjLists {
+    uint32_t *hs, *hb, *gs, *ge, *cnt;
+    uint32_t cap_s, cap_b, cap_g;
+};
+
+template <bool KEYS, bool DUP>
+__global__ __launch_bounds__(256) void k_adjacent2(const uint8_t *__restrict__ S, const uint2 *__restrict__ SS,
+                                                   const uint64_t *__restrict__ K, uint8_t *__restrict__ brk, uint32_t n,
+                                                   uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad, AdjLists L,
+                                                   uint32_t base) {
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i0 < n;  // no early return: the appends below are wave-wide
+    const uint32_t i = live ? i0 : n - 1;
+    const uint32_t ip = i > 0 ? i - 1 : 0;
+    const uint64_t ki = K[i];
+    uint2 x = make_uint2(0u, 0u), y = make_uint2(0u, 0u);
+    bool head;
+    if constexpr (KEYS) {
+        const uint64_t kp = K[ip];
+        if constexpr (DUP) { x = SS[ip]; y = SS[i]; }
+        head = (i == 0) || kp != ki;
+        if (live) brk[i] = head ? 1 : 0;
+        // a group of > WAVE_GROUP records sharing a full-tag key (rare): its last position by
+        // galloping then bisecting over the sorted keys
+        const bool big = live && head && (ki & 0xffu) == bk_full(base) && i + WAVE_GROUP < n && K[i + WAVE_GROUP] == ki;
+        uint32_t last = 0;
+        if (big) {
+            uint32_t lo = i + WAVE_GROUP, step = WAVE_GROUP;  // K[lo] == ki
+            while (lo + step < n && K[lo + step] == ki) { lo += step; step <<= 1; }
+            uint32_t hi = min(n, lo + step);  // K[hi] != ki (or hi == n)
+            while (hi - lo > 1) {
+                const uint32_t mid = lo + (hi - lo) / 2;
+                if (K[mid] == ki) lo = mid; else hi = mid;
+            }
+            last = lo;
+        }
+        // (start, end) pairs: one append per wave for both lists, same order
+        const uint64_t m = __ballot(big);
+        if (m) {
+            const int lead = __ffsll((long long)m) - 1;
+            uint32_t b = 0;
+            if (lane_id() == lead) b = atomicAdd(&L.cnt[2], (uint32_t)__popcll(m));
+            b = (uint32_t)__shfl((int)b, lead, 64);
+            if (big) {
+                const uint32_t q = b + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+                if (q < L.cap_g) { L.gs[q] = i; L.ge[q] = last; }
+            }
+        }
+    } else {
+        const uint8_t bb = brk[i];
+        if constexpr (DUP) { x = SS[ip]; y = SS[i]; }
+        head = (i == 0) || bb;
+    }
+    if constexpr (!DUP) return;
+    bool d = false;
+    if (live && !head) d = ((ki & 0xffu) < bk_full(base)) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, bk_off(base));
+    if (live) {
+        dup[i] = d ? 1 : 0;
+        segbad[i] = (!head && !d) ? 1 : 0;  // i differs from i - 1 inside one segment
+    }
+}
+
+// Heads of the segments holding a bad pair (k_adjacent2's segbad[i]: record i differs from
+// record i - 1 in its segment): A = up to SEG_SMALL members, B = up to WAVE_GROUP. A head
+// looks at its segment's brk and segbad bytes 16 at a time (aligned loads, SWAR; the slots
+// have 16 B of tail room). Segments over WAVE_GROUP records are skipped: big groups, refined
+// first (and the adjacent pass run again).
+struct SegHeadPred {
     const uint8_t *brk, *segbad;
     uint32_t n;
-    // A bad head's segment is small iff a break (brk, or the end) lies in (i, i + SEG_SMALL]:
-    // two aligned 16-B loads of brk (the slot has 32 B of tail room) replace a dependent
-    // byte walk.
-    __device__ uint32_t operator()(uint32_t i) const {
-        static_assert(SEG_SMALL == 16, "window of two 16-B loads");
-        if (!segbad[i]) return 0u;
-        const uint32_t a = (i + 1) & ~15u, sh = (i + 1) - a;
-        const uint4 w0 = *reinterpret_cast<const uint4 *>(brk + a);
-        const uint4 w1 = *reinterpret_cast<const uint4 *>(brk + a + 16);
-        const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        uint32_t m = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint32_t t = (((w[q] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w[q]) & 0x80808080u;  // nonzero bytes
-            m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * q);
+    __device__ uint32_t operator()(uint32_t j) const {
+        if (j != 0 && !brk[j]) return 0u;
+        if (j + 1 >= n || brk[j + 1]) return 0u;  // one member (most heads): never bad
+        // members j .. e-1: e = the next break after j (or n); bad iff a segbad byte in (j, e)
+        uint32_t a = (j + 1) & ~15u, sh = (j + 1) - a;
+        bool bad = false, ended = false;
+        uint32_t len = 1;
+        for (uint32_t step = 0; step < (WAVE_GROUP + 31) / 16 && !ended; ++step) {
+            uint32_t mb = swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a));
+            const uint32_t mg = swar_nonzero16(*reinterpret_cast<const uint4 *>(segbad + a));
+            if (n - a < 16u) mb |= ~0u << (n - a);  // positions >= n end the segment
+            mb = (mb >> sh) << sh;
+            const uint32_t stop = mb ? (uint32_t)__ffs((int)mb) - 1u : 16u;  // first break in this window
+            const uint32_t inside = ((stop >= 16u) ? 0xffffu : ((1u << stop) - 1u)) & ~((1u << sh) - 1u);
+            if (mg & inside) bad = true;
+            len += stop - sh;
+            if (stop < 16u) ended = true;
+            a += 16;
+            sh = 0;
         }
-        if (n - a < 32u) m |= ~0u << (n - a);  // positions >= n end the segment
-        return ((m >> sh) & 0xffffu) ? 1u : 2u;
+        if (!bad || !ended || len > WAVE_GROUP) return 0u;
+        return len <= SEG_SMALL ? 1u : 2u;
     }
 };
 
@@ -1106,56 +1132,69 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
     uint8_t *brk;
-    SG_TRY(slot(c, S_BRK, (size_t)R + 32, &brk));  // + SegPred's 32-B window
+    SG_TRY(slot(c, S_BRK, (size_t)R + 32, &brk));  // + the 16-B windows of the brk scans
     uint32_t *GS, *GE;
     SG_TRY(slot(c, S_GS, R / 64 + 16, &GS));
     SG_TRY(slot(c, S_GE, R / 64 + 16, &GE));
-    uint32_t B = 0, B2 = 0;
+    uint32_t B = 0;
     uint32_t ns = 0, nb = 0;
     uint32_t *hs, *hb;
     uint8_t *dup, *segbad;
     SG_TRY(slot(c, S_DUP, R, &dup));
-    SG_TRY(slot(c, S_BAD, R, &segbad));
+    // segbad (a flag per position) with the three list counters after it
+    const size_t cnt_off = ((size_t)R + 15) & ~(size_t)15;
+    SG_TRY(slot(c, S_BAD, cnt_off + 16, &segbad));
+    uint32_t *acnt = reinterpret_cast<uint32_t *>(segbad + cnt_off);
     SG_TRY(slot(c, S_SEL, (size_t)R / 2 + 16, &hs));
+    SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
+    const AdjLists AL{hs, hb, GS, GE, acnt, R / 2 + 16, R / 17 + 16, R / 64 + 16};
     // adjacent equality inside segments; segments holding two different records -> sort.
     // model: key0 + brk + span per record, both records' bytes where compared, dup out
-    auto adjacent_and_heads = [&](const uint8_t *Sb, const uint2 *SSp, uint64_t **seg_total) -> int {
-        SG_HIP(hipMemsetAsync(segbad, 0, R, c->stream));
-        SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, k_adjacent, grid_for(R, 256), 256, 0, Sb, SSp, K, brk, R, dup, segbad,
-                    base);
-        SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
-        return run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, seg_total);
-    };
-    uint32_t lerr_v = 0;
-    auto read2 = [&](const uint64_t *t1, const uint64_t *t2, uint32_t *a1, uint32_t *b1, uint32_t *a2, uint32_t *b2) -> int {
-        uint8_t *pin = (uint8_t *)c->pinned;
-        SG_HIP(hipMemcpyAsync(pin, t1, 8, hipMemcpyDeviceToHost, c->stream));
-        if (t2) SG_HIP(hipMemcpyAsync(pin + 8, t2, 8, hipMemcpyDeviceToHost, c->stream));
-        if (lerr) SG_HIP(hipMemcpyAsync(pin + 16, lerr, 4, hipMemcpyDeviceToHost, c->stream));
-        SG_HIP(hipStreamSynchronize(c->stream));
-        uint64_t v1 = 0, v2 = 0;
-        memcpy(&v1, pin, 8);
-        if (t2) memcpy(&v2, pin + 8, 8);
-        lerr_v = 0;
-        if (lerr) memcpy(&lerr_v, pin + 16, 4);
-        *a1 = (uint32_t)(v1 >> 31);
-        *b1 = (uint32_t)(v1 & 0x7fffffffu);
-        if (t2) {
-            *a2 = (uint32_t)(v2 >> 31);
-            *b2 = (uint32_t)(v2 & 0x7fffffffu);
-        }
+    uint64_t *stot = nullptr;
+    auto adjacent = [&](bool keys, bool with_dup, const uint8_t *Sb, const uint2 *SSp) -> int {
+        SG_HIP(hipMemsetAsync(acnt, 0, 16, c->stream));
+        if (keys && with_dup)
+            SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, (k_adjacent2<true, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
+                        brk, R, dup, segbad, AL, base);
+        else if (keys)
+            SG_LAUNCH_B(c, "mark_groups", 9.0 * R, (k_adjacent2<true, false>), grid_for(R, 256), 256, 0, Sb, SSp, K, brk, R,
+                        dup, segbad, AL, base);
+        else
+            SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, (k_adjacent2<false, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
+                        brk, R, dup, segbad, AL, base);
+        if (with_dup) SG_TRY(run_select2_nb(c, "seg_heads", SegHeadPred{brk, segbad, R}, R, hs, hb, S_COUNT2, &stot));
         return SG_OK;
     };
-    uint64_t *gtot, *stot = nullptr;
-    // Without a materialised copy the adjacent pass and the segment-head select are queued
-    // before the group count comes back (one host sync for both counts); when big groups
-    // exist (the 7-byte key was kept: low-entropy text) they wait for the refinement instead.
+    uint32_t lerr_v = 0;
+    // the big-group count, the segment-head select's counts and the local sort's overflow
+    // word with one host sync
+    auto read_counts = [&](bool with_heads) -> int {
+        uint8_t *pin = (uint8_t *)c->pinned;
+        SG_HIP(hipMemcpyAsync(pin, acnt, 12, hipMemcpyDeviceToHost, c->stream));
+        if (with_heads) SG_HIP(hipMemcpyAsync(pin + 16, stot, 8, hipMemcpyDeviceToHost, c->stream));
+        if (lerr) SG_HIP(hipMemcpyAsync(pin + 24, lerr, 4, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipStreamSynchronize(c->stream));
+        uint32_t v[3];
+        memcpy(v, pin, 12);
+        lerr_v = 0;
+        if (lerr) memcpy(&lerr_v, pin + 24, 4);
+        B = v[2];
+        if (with_heads) {
+            uint64_t t = 0;
+            memcpy(&t, pin + 16, 8);
+            ns = (uint32_t)(t >> 31);
+            nb = (uint32_t)(t & 0x7fffffffu);
+        }
+        if (B > R / 64 + 16) { set_error("adjacent: big-group list overflow (%u)", B); return SG_E_HIP; }
+        return SG_OK;
+    };
+    // With narrowed keys (kw < 7: few big groups) the adjacent compare runs before the group
+    // count comes back (one host sync for everything); when big groups exist (the 7-byte key
+    // was kept: low-entropy text) the groups are marked first and compared after refinement.
     const bool speculate = (base >> 16) < 7u;
     for (;;) {
-        SG_TRY(run_select2_nb(c, "mark_groups", BigGroupPred{K, brk, R, (base >> 16) + 1u}, R, GS, GE, S_COUNT, &gtot));
-        prof_bytes(c, "mark_groups", 9.0 * R);
-        if (speculate) SG_TRY(adjacent_and_heads(d_buf, V, &stot));
-        SG_TRY(read2(gtot, stot, &B, &B2, &ns, &nb));
+        SG_TRY(adjacent(true, speculate, d_buf, V));
+        SG_TRY(read_counts(speculate));
         if (!lerr_v) break;
         // a group outgrew the local sort's LDS (the pairs are intact, unsorted there): the
         // plain LSD sort of the same pairs (keys already narrowed, histograms unchanged)
@@ -1165,7 +1204,6 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         lerr = nullptr;
         c->last_flags |= 2u;
     }
-    if (B != B2) { set_error("group start/end mismatch %u/%u", B, B2); return SG_E_HIP; }
     if (B) SG_TRY(refine_big_groups(c, d_buf, L.spans, V, brk, GS, GE, B, base));
 
     // The records in this order: SS = the input spans in sorted order (the sort's payload),
@@ -1177,11 +1215,9 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint8_t *Sb = const_cast<uint8_t *>(d_buf);
     uint2 *SS = V;  // the segment sorts permute it in place
     if (!speculate || B) {
-        SG_TRY(adjacent_and_heads(Sb, SS, &stot));
-        uint32_t d0, d1;
-        SG_TRY(read2(stot, nullptr, &ns, &nb, &d0, &d1));
+        SG_TRY(adjacent(false, true, Sb, SS));
+        SG_TRY(read_counts(true));
     }
-    prof_bytes(c, "seg_heads", 1.0 * R);
     uint32_t *err;
     SG_TRY(slot(c, S_ERR, 4, &err));
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
