@@ -36,8 +36,9 @@ METRIC = "scan records/sec + GB/s (vs HBM roofline) for match+dedup+diff, 1 and 
 
 
 # library stat name -> HIP kernel symbol (rocprofv3 -T names) for the PMC traffic lookup
-KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_uniq": "k_emit_uniq",
-                 "emit_fresh": "k_emit_fresh", "diff_tile": "k_diff_tile", "adjacent": "k_adjacent",
+KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_uniq": ("k_emit_uniq_s", "k_emit_uniq"),
+                 "emit_fresh": "k_emit_fresh", "diff_tile": "k_diff_tile", "adjacent": ("k_adjacent2", "k_adjacent"),
+                 "rs_lsort": "k_rs_lsort", "rs_lbounds": "k_rs_lbounds", "seg_heads": "k_sel_count",
                  "lines": "k_lines", "lit_match": "k_lit_scan", "dfa_match": "k_dfa_match", "ac_match": "k_ac_match",
                  "re_prefilter": "k_lit_scan", "re_verify": "k_verify", "json_scan": "k_json_scan",
                  "json_emit": "k_json_emit", "tm_eval": "k_tm_eval", "tm_collect": "k_tm_collect",
@@ -53,11 +54,15 @@ def pmc_traffic(workload, kernel):
     passes (profiles/pmc_traffic.json, written by tools/pmc_summary.py; FETCH_SIZE doubled per
     MI355X_MICROARCH.md). None when no pass covers this kernel."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    syms = KERNEL_SYMBOL.get(kernel, kernel)
     try:
-        t = json.load(open(path))[workload][KERNEL_SYMBOL.get(kernel, kernel)]
+        table = json.load(open(path))[workload]
     except (OSError, KeyError, ValueError):
         return None
-    return t
+    for sym in ((syms,) if isinstance(syms, str) else syms):  # launch form first (template variants)
+        if sym in table:
+            return table[sym]
+    return None
 
 
 def roofline_of(stats, kernel=None, workload=None, full=None):

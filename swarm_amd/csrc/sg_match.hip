@@ -18,6 +18,8 @@
 #include "sg_prims_host.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <type_traits>
 #include <deque>
 #include <map>
 #include <unordered_map>
@@ -86,11 +88,12 @@ struct sg_matcher {
         bool nocase = false;
         uint32_t cls_mask = 0;               // bit c: some pattern is filed in class c (LIT_CLASSES)
         uint32_t tmpl = 0;                   // class set the scan kernel is compiled for
-        uint32_t bits[5] = {0, 0, 0, 0, 0};  // log2 bitmap size per class
-        uint32_t bm_off[5] = {0, 0, 0, 0, 0};
+        bool joint = false;                  // class scheme: {4-gram, 8-gram} (false) or joint (true)
+        uint32_t bits[6] = {0, 0, 0, 0, 0, 0};  // log2 bitmap size per class
+        uint32_t bm_off[6] = {0, 0, 0, 0, 0, 0};
         std::vector<uint32_t> bitmap;        // all classes, word-concatenated
         std::vector<uint16_t> rank;          // per bitmap word: set bits in earlier words of its class
-        uint32_t rank_base[5] = {0, 0, 0, 0, 0};  // entries (buckets) of all earlier classes
+        uint32_t rank_base[6] = {0, 0, 0, 0, 0, 0};  // entries (buckets) of all earlier classes
         std::vector<uint32_t> eoff;          // per non-empty bucket: entry range (CSR)
         std::vector<uint32_t> efp;           // per entry: gram fingerprint (the gram itself for L <= 4)
         std::vector<uint32_t> einfo;         // per entry: {pid, anchor, len, 16-B pattern row}
@@ -102,8 +105,11 @@ struct sg_matcher {
         uint16_t *d_rank = nullptr;
         uint8_t *d_pat16 = nullptr;
     };
-    Lit lit;      // literal signatures
-    Lit prelit;   // regex prefilter factors
+    // Each filter is built in both class schemes; the first device call times both on the
+    // caller's data and keeps the faster (mode: -1 undecided, 0 two-class, 1 joint).
+    Lit lit, lit_j;        // literal signatures
+    Lit prelit, prelit_j;  // regex prefilter factors
+    std::atomic<int> lit_mode{-1}, prelit_mode{-1};
     std::mutex mu;
 };
 
@@ -203,34 +209,49 @@ static int build_ac(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint3
 }
 
 // ------------------------------------------------------------------ hashed q-gram literal filter
-// Every pattern is filed under ONE gram, in one of five classes (LIT_CLASSES):
-//   len 1, 2, 3   -> the whole pattern (classes 1 and 2 index exactly, 3 hashes);
-//   len 4..7      -> one of its 4-byte grams (hashed);
-//   len >= 8      -> one of its 8-byte grams (hashed).
-// The anchor offset is chosen per pattern to balance the buckets and to avoid bytes that
-// are frequent in banners (shared prefixes such as "https://" would otherwise pile up and
-// be confirmed at every line). Device side: one LDS bitmap bit per (class, bucket); a set
-// bit is confirmed against the bucket's entry fingerprints (rank + CSR, in LDS), then the
+// Every pattern is filed under ONE gram. Two class schemes:
+//   two-class: len 1, 2, 3 -> the whole pattern (classes 0 and 1 index exactly, 2 hashes);
+//              len 4..7   -> class 3: one of its 4-byte grams (hashed);
+//              len >= 8   -> class 4: one of its 8-byte grams (hashed);
+//   joint:     len 1, 2, 3 as above; len >= 4 -> class 5: a 4-byte gram and the byte after it
+//              in ONE bitmap: a 32-bit row per 4-gram hash bucket, a bit per value of the next
+//              byte's low 5 bits (a 4-byte pattern sets its whole row).
+// The probe pass reads a random LDS word per class per text position and is bound by those
+// reads' bank conflicts: the joint scheme reads one where the two-class one reads two (C3
+// 5.5 -> 4.4 ms), but its 5-byte anchors are less selective than 8-grams, which costs more
+// than it saves on some texts (C4 banners 3.5 -> 6.6 ms, the fields JSON 8.1 -> 18.4 ms).
+// So both are built, and the first device call times both on its data (sg_matcher::lit_mode).
+// Patterns of 8 bytes and more keep an 8-gram fingerprint in both, checked before their
+// bytes are. The anchor offset is chosen per pattern to balance the buckets and to avoid
+// bytes that are frequent in banners (shared prefixes such as "https://" would otherwise pile
+// up and be confirmed at every line). Device side: one LDS bitmap bit per (class, bucket);
+// a set bit is confirmed against the bucket's entry fingerprints (rank + CSR), then the
 // whole pattern is byte-compared.
-constexpr uint32_t LIT_CLASSES = 5;
-__host__ __device__ constexpr uint32_t lit_len(uint32_t c) { return c < 4 ? c + 1 : 8; }
-// class-set templates of k_lit_scan: {4-7, 8+}, {3, 4-7, 8+}, all
-static uint32_t lit_template(uint32_t cls_mask) {
-    if ((cls_mask & ~0x18u) == 0) return 0x18u;
-    if ((cls_mask & ~0x1Cu) == 0) return 0x1Cu;
-    return 0x1Fu;
+constexpr uint32_t LIT_CLASSES = 6;
+constexpr uint32_t LIT_J = 5;  // the joint class
+__host__ __device__ constexpr uint32_t lit_len(uint32_t c) { return c < 3 ? c + 1 : (c == 3 ? 4 : (c == 4 ? 8 : 5)); }
+// class-set templates of k_lit_scan: two-class {4-7, 8+}, {3, 4-7, 8+}, all; joint {J},
+// {3, J}, {1, 2, 3, J}
+static uint32_t lit_template(uint32_t cls_mask, bool joint) {
+    const uint32_t hi = joint ? 0x20u : 0x18u;
+    if ((cls_mask & ~hi) == 0) return hi;
+    if ((cls_mask & ~(hi | 0x04u)) == 0) return hi | 0x04u;
+    return hi | 0x07u;
 }
 
-// Bucket of a gram: multiplicative hash. (A shift-xor fold — three full-rate ops instead of
-// the quarter-rate 32-bit multiply — measured no faster on X1: 24.9M candidates per 10M lines
-// against 17.0M, and the extra verifications ate the saved probe cycles.)
+// Bucket of a gram: multiplicative hash (a shift-xor fold measured no faster on X1: more
+// false candidates). The joint class's row is the 4-gram's hash (bits - 5 bits), its bit the
+// next byte's low 5 bits.
+constexpr uint32_t LIT_MUL = 0x9E3779B1u;
 __host__ __device__ __forceinline__ uint32_t lit_h(uint32_t lo, uint32_t hi, uint32_t c, uint32_t bits) {
     if (c <= 1) return lo;
-    const uint32_t k = (c == 4) ? (lo ^ ((hi << 13) | (hi >> 19))) : lo;
-    return (k * 0x9E3779B1u) >> (32u - bits);
+    if (c == 4) return ((lo ^ ((hi << 13) | (hi >> 19))) * LIT_MUL) >> (32u - bits);
+    if (c == LIT_J) return (((lo * LIT_MUL) >> (37u - bits)) << 5) | (hi & 31u);
+    return (lo * LIT_MUL) >> (32u - bits);
 }
-__host__ __device__ __forceinline__ uint32_t lit_fp(uint32_t lo, uint32_t hi, uint32_t c) {
-    return (c == 4) ? (lo ^ ((hi << 13) | (hi >> 19)) ^ (hi * 0xC2B2AE35u)) : lo;
+// Fingerprint for entries of 8 bytes and more (the 8-gram's); shorter entries use the gram.
+__host__ __device__ __forceinline__ uint32_t lit_fp8(uint32_t lo, uint32_t hi) {
+    return lo ^ ((hi << 13) | (hi >> 19)) ^ (hi * 0xC2B2AE35u);
 }
 
 static uint32_t gram_commonness(const uint8_t *g, uint32_t L) {
@@ -243,16 +264,19 @@ static uint32_t gram_commonness(const uint8_t *g, uint32_t L) {
 }
 
 // extra_bits: bitmap size over the 64-bits-per-pattern base, as a power of two (more bits:
-// fewer false candidates, more LDS per block).
+// fewer false candidates, more LDS per block). joint: the class scheme.
 static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint32_t flags, sg_matcher::Lit *T,
-                     uint32_t extra_bits = 0) {
+                     uint32_t extra_bits, bool joint) {
     const bool nocase = flags & SG_NOCASE;
     auto fold = [&](uint8_t b) -> uint8_t { return (nocase && b >= 'A' && b <= 'Z') ? (uint8_t)(b + 32) : b; };
     T->on = true;
+    T->joint = joint;
     T->nocase = nocase;
     T->pat.clear();
     T->pat_off.assign(1, 0);
-    auto cls_of_len = [](uint32_t len) -> uint32_t { return len < 4 ? len - 1 : (len < 8 ? 3u : 4u); };
+    auto cls_of_len = [joint](uint32_t len) -> uint32_t {
+        return len < 4 ? len - 1 : (joint ? LIT_J : (len < 8 ? 3u : 4u));
+    };
     uint32_t cnt[LIT_CLASSES] = {};
     for (uint32_t i = 0; i < n; ++i) {
         if (offs[i + 1] <= offs[i]) { set_error("signature %u is empty", i); return SG_E_INVAL; }
@@ -273,8 +297,8 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
                 b = 8 * (c + 1);
             } else {
                 b = 10;
-                constexpr uint32_t cap4 = 18u;
-                while (b < (c == 2 ? 15u : cap4) && (1ull << b) < (64ull << extra_bits) * cnt[c]) ++b;
+                constexpr uint32_t cap = 18u;
+                while (b < (c == 2 ? 15u : cap) && (1ull << b) < (64ull << extra_bits) * cnt[c]) ++b;
             }
         }
         T->bits[c] = b;
@@ -283,10 +307,10 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
     }
     // The scan kernel is compiled for a superset of the present classes (lit_template);
     // a class of the superset with no pattern probes an all-zero region of its size.
-    T->tmpl = lit_template(T->cls_mask);
+    T->tmpl = lit_template(T->cls_mask, joint);
     for (uint32_t c = 0; c < LIT_CLASSES; ++c) {
         if (cnt[c] || !((T->tmpl >> c) & 1u)) continue;
-        T->bits[c] = (c <= 1) ? 8 * (c + 1) : 5;
+        T->bits[c] = (c <= 1) ? 8 * (c + 1) : (c == LIT_J ? 10 : 5);
         T->bm_off[c] = words;
         words += std::max<uint32_t>((1u << T->bits[c]) / 32, 1);
     }
@@ -296,26 +320,20 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         for (uint32_t j = 0; j < L && j < 4; ++j) key |= (uint32_t)T->pat[T->pat_off[i] + o + j] << (8 * j);
         return key;
     };
+    auto len_of = [&](uint32_t i) { return T->pat_off[i + 1] - T->pat_off[i]; };
     // anchors: shortest patterns (fewest choices) first, each on its least-loaded gram
-    std::vector<uint32_t> anc(n, 0), cls(n), hb(n), fp(n);
-    std::vector<uint32_t> order;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t len = T->pat_off[i + 1] - T->pat_off[i];
-        cls[i] = cls_of_len(len);
-        order.push_back(i);
-    }
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
-        return T->pat_off[x + 1] - T->pat_off[x] < T->pat_off[y + 1] - T->pat_off[y];
-    });
-    // How many patterns contain each 4-/8-byte gram: a gram that many signatures share is
-    // a common substring of the domain ("openssh_", "server: "), so text holds it far more
-    // often than a gram unique to one signature (C4 factors: 8.7 confirmed grams per banner
-    // for 1 factor hit when anchors ignored this).
+    std::vector<uint32_t> order(n);
+    for (uint32_t i = 0; i < n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return len_of(x) < len_of(y); });
+    // How many patterns contain each anchor gram: a gram that many signatures share is a
+    // common substring of the domain ("openssh_", "server: "), so text holds it far more often
+    // than a gram unique to one signature (C4 factors: 8.7 confirmed grams per banner for 1
+    // factor hit when anchors ignored this).
     std::unordered_map<uint64_t, uint32_t> share;
     for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t len = T->pat_off[i + 1] - T->pat_off[i];
+        const uint32_t len = len_of(i);
         const uint32_t c = cls_of_len(len);
-        if (c < 3) continue;
+        if (c < 3 || (c == LIT_J && len < 5)) continue;
         const uint32_t L = lit_len(c);
         std::vector<uint64_t> mine;
         for (uint32_t o = 0; o + L <= len; ++o) {
@@ -328,37 +346,66 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         for (uint64_t g : mine) share[g]++;
     }
     auto shared_by = [&](uint32_t i, uint32_t o, uint32_t L) -> uint32_t {
-        if (L < 4) return 0;
         uint64_t g = 0;
         memcpy(&g, &T->pat[T->pat_off[i] + o], L);
         auto it = share.find(g | ((uint64_t)L << 60));
         return it == share.end() ? 0u : it->second;
     };
+    struct Ent {
+        uint32_t pid, cls, anc, hb, fp;
+    };
+    std::vector<Ent> ents;
+    ents.reserve(n + 32);
     std::vector<std::vector<uint32_t>> load(LIT_CLASSES);
     for (uint32_t c = 0; c < LIT_CLASSES; ++c) load[c].assign(cnt[c] ? (1u << T->bits[c]) : 1, 0);
     for (uint32_t i : order) {
-        const uint32_t len = T->pat_off[i + 1] - T->pat_off[i];
-        const uint32_t c = cls[i], L = lit_len(c);
-        const uint32_t last = (c < 3) ? 0 : len - L;
+        const uint32_t len = len_of(i);
+        const uint32_t c = cls_of_len(len);
+        if (c < 3) {
+            const uint32_t lo = word_at(i, 0, len);
+            const uint32_t h = lit_h(lo, 0u, c, T->bits[c]);
+            ents.push_back(Ent{i, c, 0u, h, lo});
+            load[c][h]++;
+            continue;
+        }
+        if (c == LIT_J && len == 4) {  // no next byte: the whole row
+            const uint32_t lo = word_at(i, 0, 4);
+            const uint32_t h0 = lit_h(lo, 0u, c, T->bits[c]) & ~31u;
+            for (uint32_t y = 0; y < 32; ++y) {
+                ents.push_back(Ent{i, c, 0u, h0 | y, lo});
+                load[c][h0 | y]++;
+            }
+            continue;
+        }
+        // anchor range: the gram inside the pattern, and for 8+ byte patterns the 8-gram
+        // fingerprint too
+        const uint32_t L = lit_len(c);
+        const uint32_t last = (len >= 8) ? len - 8 : len - L;
         uint64_t best = ~0ull;
+        uint32_t bo = 0, bh = 0;
         for (uint32_t o = 0; o <= last && o < 256; ++o) {  // anchor fits the bucket record's 8 bits
-            const uint32_t lo = word_at(i, o, L), hi = (L == 8) ? word_at(i, o + 4, 4) : 0u;
+            const uint32_t lo = word_at(i, o, 4);
+            const uint32_t hi = (c == 4) ? word_at(i, o + 4, 4) : (c == LIT_J ? (uint32_t)T->pat[T->pat_off[i] + o + 4] : 0u);
             const uint32_t h = lit_h(lo, hi, c, T->bits[c]);
             constexpr uint32_t w_share = 64u;  // cost of one more pattern sharing the gram
             const uint64_t cost = (uint64_t)(std::max(shared_by(i, o, L), 1u) - 1) * w_share + (uint64_t)load[c][h] * 16 +
                                   gram_commonness(&T->pat[T->pat_off[i] + o], L);
-            if (cost < best) { best = cost; anc[i] = o; hb[i] = h; fp[i] = lit_fp(lo, hi, c); }
+            if (cost < best) { best = cost; bo = o; bh = h; }
         }
-        load[c][hb[i]]++;
+        const uint32_t lo = word_at(i, bo, 4);
+        const uint32_t fp = len >= 8 ? lit_fp8(lo, word_at(i, bo + 4, 4)) : lo;
+        ents.push_back(Ent{i, c, bo, bh, fp});
+        load[c][bh]++;
     }
     // entries sorted by (class, bucket); the bitmap word order is the same
-    std::vector<uint32_t> ids(n);
-    for (uint32_t i = 0; i < n; ++i) {
-        ids[i] = i;
-        T->bitmap[T->bm_off[cls[i]] + (hb[i] >> 5)] |= 1u << (hb[i] & 31);
+    const uint32_t ne = (uint32_t)ents.size();
+    std::vector<uint32_t> ids(ne);
+    for (uint32_t q = 0; q < ne; ++q) {
+        ids[q] = q;
+        T->bitmap[T->bm_off[ents[q].cls] + (ents[q].hb >> 5)] |= 1u << (ents[q].hb & 31);
     }
     std::stable_sort(ids.begin(), ids.end(), [&](uint32_t x, uint32_t y) {
-        return cls[x] != cls[y] ? cls[x] < cls[y] : hb[x] < hb[y];
+        return ents[x].cls != ents[y].cls ? ents[x].cls < ents[y].cls : ents[x].hb < ents[y].hb;
     });
     T->rank.assign(words, 0);
     uint32_t acc = 0;
@@ -384,13 +431,13 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         T->pat16.insert(T->pat16.end(), T->pat.begin() + T->pat_off[i], T->pat.begin() + T->pat_off[i + 1]);
         T->pat16.resize((T->pat16.size() + 15) & ~(size_t)15, 0);
     }
-    for (uint32_t q = 0; q < n; ++q) {
-        const uint32_t i = ids[q];
-        if (q > 0 && (cls[ids[q - 1]] != cls[i] || hb[ids[q - 1]] != hb[i])) T->eoff.push_back(q);
-        T->efp.push_back(fp[i]);
-        T->einfo.insert(T->einfo.end(), {i, anc[i], T->pat_off[i + 1] - T->pat_off[i], row[i]});
+    for (uint32_t q = 0; q < ne; ++q) {
+        const Ent &e = ents[ids[q]];
+        if (q > 0 && (ents[ids[q - 1]].cls != e.cls || ents[ids[q - 1]].hb != e.hb)) T->eoff.push_back(q);
+        T->efp.push_back(e.fp);
+        T->einfo.insert(T->einfo.end(), {e.pid, e.anc, len_of(e.pid), row[e.pid]});
     }
-    if (n) T->eoff.push_back(n);
+    if (ne) T->eoff.push_back(ne);
     if (T->eoff.size() != (size_t)acc + 1) { set_error("build_lit: bucket bookkeeping mismatch"); return SG_E_INVAL; }
     // one 16-B record per bucket: its first entry, plus a flag when more entries follow
     T->brec.assign((size_t)acc * 4, 0);
@@ -430,7 +477,7 @@ static void free_dev(sg_matcher *h) {
                     (void *)p.s_mid})
         if (q) (void)hipFree(q);
     h->dplan = sg_matcher::DevPlan{};
-    for (sg_matcher::Lit *L : {&h->lit, &h->prelit}) {
+    for (sg_matcher::Lit *L : {&h->lit, &h->lit_j, &h->prelit, &h->prelit_j}) {
         for (void *q : {(void *)L->d_bitmap, (void *)L->d_rank, (void *)L->d_eoff, (void *)L->d_efp,
                         (void *)L->d_einfo, (void *)L->d_pat16, (void *)L->d_brec})
             if (q) (void)hipFree(q);
@@ -507,7 +554,7 @@ static int ensure_device(sg_matcher *h, int dev) {
         SG_TRY(upload_vec(h->s_cls, &p.s_cls));
         SG_TRY(upload_vec(h->s_acc, &p.s_acc));
     }
-    for (sg_matcher::Lit *L : {&h->lit, &h->prelit}) {
+    for (sg_matcher::Lit *L : {&h->lit, &h->lit_j, &h->prelit, &h->prelit_j}) {
         if (!L->on) continue;
         SG_TRY(upload_vec(L->bitmap, &L->d_bitmap));
         SG_TRY(upload_vec(L->rank, &L->d_rank));
@@ -775,7 +822,7 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t s_t[LS_HALO + TILE + LS_HALO];
     __shared__ unsigned long long s_hits[LS_HB];
     __shared__ uint32_t s_q[LS_Q];
-    __shared__ uint2 s_kf[LS_Q];  // per queued candidate: (bucket, fingerprint)
+    __shared__ uint2 s_kf[LS_Q];  // per queued candidate: (bucket, 8-gram fingerprint)
     __shared__ uint32_t s_red[BLK / 64];
     __shared__ uint32_t s_hn, s_g, s_base, s_ebase;
     uint32_t *s_bm = s_dyn;
@@ -896,27 +943,40 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
             wn0 = fold4(wn0);
             wn1 = fold4(wn1);
         }
-        // pass 1: bitmap probes
-        uint64_t cand[LIT_CLASSES] = {};
+        // pass 1: bitmap probes. g[b] = the 4-byte word at b times LIT_MUL (the joint class's
+        // row hash); the byte at b + 4 picks the row's bit
+        auto word_at = [&](int b) -> uint32_t {
+            const int i0 = b >> 2;
+            const uint32_t x0 = (i0 < NW) ? w[i0] : (i0 == NW ? wn0 : wn1);
+            const uint32_t x1 = (i0 + 1 < NW) ? w[i0 + 1] : (i0 + 1 == NW ? wn0 : wn1);
+            return (b & 3) ? __builtin_amdgcn_alignbyte(x1, x0, b & 3) : x0;
+        };
+        // candidate bit masks per class: 32-bit words when a thread holds <= 32 positions
+        using CT = typename std::conditional<(BPT <= 32), uint32_t, uint64_t>::type;
+        CT cand[LIT_CLASSES] = {};
+        // g[b] = the 4-byte word at b times LIT_MUL (b = 0 .. BPT + 3): the 4-gram class's
+        // bucket and the joint class's row
+        uint32_t g[BPT + 4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) g[b] = word_at(b) * LIT_MUL;
 #pragma unroll
         for (int b = 0; b < BPT; ++b) {
-            const int i0 = b >> 2;
-            const uint32_t x0 = w[i0];
-            const uint32_t x1 = (i0 + 1 < NW) ? w[i0 + 1] : wn0;
-            const uint32_t x2 = (i0 + 2 < NW) ? w[i0 + 2] : (i0 + 2 == NW ? wn0 : wn1);
-            const uint32_t lo = (b & 3) ? __builtin_amdgcn_alignbyte(x1, x0, b & 3) : x0;
+            const uint32_t lo = word_at(b);
+            const uint32_t w4 = word_at(b + 4);
+            g[b + 4] = w4 * LIT_MUL;
 #pragma unroll
             for (uint32_t c = 0; c < LIT_CLASSES; ++c) {
                 if (!((CM >> c) & 1u)) continue;
-                uint32_t h;
-                if (c == 4) {
-                    const uint32_t hi = (b & 3) ? __builtin_amdgcn_alignbyte(x2, x1, b & 3) : x1;
-                    h = lit_h(lo, hi, c, a.bits[c]);
-                } else {
-                    const uint32_t key = (c == 3) ? lo : (lo & ((1u << (8 * (c + 1))) - 1u));
-                    h = lit_h(key, 0u, c, a.bits[c]);
+                if (c == LIT_J) {  // one read: the 4-gram's row, the next byte's bit
+                    const uint32_t row = s_bm[a.bm_off[c] + (g[b] >> (37u - a.bits[c]))];
+                    cand[c] |= (CT)((row >> (w4 & 31u)) & 1u) << b;
+                    continue;
                 }
-                cand[c] |= (uint64_t)((s_bm[a.bm_off[c] + (h >> 5)] >> (h & 31)) & 1u) << b;
+                uint32_t h;
+                if (c == 4) h = lit_h(lo, w4, 4u, a.bits[c]);
+                else if (c == 3) h = g[b] >> (32u - a.bits[c]);
+                else h = lit_h(lo & ((1u << (8 * (c + 1))) - 1u), 0u, c, a.bits[c]);
+                cand[c] |= (CT)((s_bm[a.bm_off[c] + (h >> 5)] >> (h & 31)) & 1u) << b;
             }
         }
         if (my0 + BPT > n) {
@@ -968,24 +1028,39 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
                 const uint32_t h = lit_h(key, k1, c, a.bits[c]);
                 const uint32_t wi = a.bm_off[c] + (h >> 5);
                 const uint32_t k = a.rank_base[c] + s_rank[wi] + (uint32_t)__popc(s_bm[wi] & ((1u << (h & 31)) - 1u));
-                s_kf[i] = make_uint2(k, lit_fp(key, k1, c));
+                // fingerprints: the gram itself (entries shorter than 8) and the 8-gram's
+                s_kf[i] = make_uint2(k, lit_fp8(k0, k1));
             }
             // stage 2: LS_BATCH candidates per lane, their bucket records and first pattern
             // rows loaded together, then verified against the LDS text
             for (uint32_t i0 = t; i0 < qn; i0 += LS_BATCH * BLK) {
                 uint4 br[LS_BATCH];
-                uint32_t fpv[LS_BATCH];
+                uint32_t fp8[LS_BATCH], fp4[LS_BATCH];
 #pragma unroll
                 for (int u = 0; u < LS_BATCH; ++u) {
                     const uint32_t i = i0 + u * BLK;
                     br[u] = make_uint4(0, 0, 0, 0);
-                    fpv[u] = 1;
+                    fp8[u] = 1;
+                    fp4[u] = 1;
                     if (i < qn) {
                         const uint2 kf = s_kf[i];
                         br[u] = a.brec[kf.x];
-                        fpv[u] = kf.y;
+                        fp8[u] = kf.y;
+                        // the gram itself (fingerprint of entries shorter than 8), from the tile
+                        const uint32_t ent = s_q[i];
+                        const int q = (int)(ent >> 17);
+                        const uint32_t c = (ent >> 14) & 7u;
+                        uint32_t w0 = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3));
+                        uint32_t w1 = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3) + 4);
+                        if (a.nocase) { w0 = fold4(w0); w1 = fold4(w1); }
+                        const uint32_t k0 = (q & 3) ? __builtin_amdgcn_alignbyte(w1, w0, q & 3) : w0;
+                        fp4[u] = (c >= 3) ? k0 : (k0 & ((1u << (8 * (c + 1))) - 1u));
                     }
                 }
+                // the bucket's first entry: its fingerprint kind by its pattern length
+                uint32_t fpv[LS_BATCH];
+#pragma unroll
+                for (int u = 0; u < LS_BATCH; ++u) fpv[u] = (br[u].z & 0xffffffu) >= 8u ? fp8[u] : fp4[u];
                 uint4 r0w[LS_BATCH], r1w[LS_BATCH];
 #pragma unroll
                 for (int u = 0; u < LS_BATCH; ++u) {
@@ -1013,8 +1088,8 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
                         // rare: more patterns share this bucket
                         const uint32_t k = s_kf[i].x;
                         for (uint32_t e = a.eoff[k] + 1; e < a.eoff[k + 1]; ++e) {
-                            if (a.efp[e] != fpv[u]) continue;
                             const uint4 inf = a.einfo[e];
+                            if (a.efp[e] != (inf.z >= 8u ? fp8[u] : fp4[u])) continue;
                             const uint4 w0 = a.pat16[inf.w];
                             const uint4 w1 = inf.z > 16 ? a.pat16[inf.w + 1] : make_uint4(0, 0, 0, 0);
                             if (lit_verify(a, s_tile, base, TILE, p, inf.y, inf.z, inf.w, c, w0, w1))
@@ -1291,6 +1366,8 @@ struct VerifyArgs {
     uint32_t n_singles, n_acc;  // automata count, total accept-table entries
 };
 
+constexpr int VF_PRE = 6;  // 16-B record chunks loaded before the walk (96 B: most banners)
+
 // Walk automaton (D, cls, acc with C classes, eol column, anchored start states mid) over
 // record [s, e): global tables, or the block's copy in LDS (the same code inlined with LDS
 // pointers, so the lookups are ds_reads).
@@ -1318,8 +1395,7 @@ __device__ __forceinline__ bool verify_walk(const uint8_t *__restrict__ buf, DT 
     }
     uint32_t st = 1;
     bool hit = acc[st] != 0;
-    for (uint32_t w = s & ~15u; w < e && !hit && st != 0; w += 16) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(buf + w);
+    auto walk16 = [&](uint32_t w, const uint4 &v) {
         const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (uint32_t b = 0; b < 16; ++b) {
@@ -1328,7 +1404,20 @@ __device__ __forceinline__ bool verify_walk(const uint8_t *__restrict__ buf, DT 
             st = D[st * C + cls[(xs[b >> 2] >> (8 * (b & 3))) & 0xffu]];
             hit = acc[st] != 0;
         }
-    }
+    };
+    // the record's first VF_PRE 16-B chunks are loaded together before the walk: one line
+    // fetch per record instead of a load per chunk spread over the walk, by which time the
+    // line has left L2 (round 2 PMC: 6x over-fetch, 6 % L2 hits); the rest as the walk goes
+    const uint32_t w0 = s & ~15u;
+    uint4 pre[VF_PRE];
+#pragma unroll
+    for (int j = 0; j < VF_PRE; ++j)
+        pre[j] = (w0 + 16u * j < e) ? *reinterpret_cast<const uint4 *>(buf + w0 + 16u * j) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < VF_PRE; ++j)
+        if (w0 + 16u * j < e && !hit && st != 0) walk16(w0 + 16u * j, pre[j]);
+    for (uint32_t w = w0 + 16u * VF_PRE; w < e && !hit && st != 0; w += 16)
+        walk16(w, *reinterpret_cast<const uint4 *>(buf + w));
     if (!hit && st != 0) hit = acc[D[st * C + eol]] != 0;
     return hit;
 }
@@ -1615,10 +1704,12 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     // prefilter candidates (regex plans): factor filter -> (record, pattern) pairs
     unsigned long long *cand = nullptr;
     uint32_t n_cand = 0;
+    // trial_tiles > 0: a timing run over the first tiles only, every output dropped (no spans,
+    // flags or hits: capacity 0)
     auto run_lit = [&](const char *name, const sg_matcher::Lit &Lt, unsigned long long *out, uint32_t *counter,
-                       uint32_t ocap, const uint32_t *fo, const uint32_t *fp) -> int {
+                       uint32_t ocap, const uint32_t *fo, const uint32_t *fp, uint32_t trial_tiles = 0) -> int {
         LitArgs a{};
-        a.buf = d_buf; a.n = n; a.tile_excl = L.tile_excl; a.n_tiles = L.n_tiles;
+        a.buf = d_buf; a.n = n; a.tile_excl = L.tile_excl; a.n_tiles = trial_tiles ? trial_tiles : L.n_tiles;
         a.bitmap = Lt.d_bitmap; a.rank = Lt.d_rank; a.eoff = Lt.d_eoff; a.efp = Lt.d_efp;
         a.brec = reinterpret_cast<const uint4 *>(Lt.d_brec);
         a.einfo = reinterpret_cast<const uint4 *>(Lt.d_einfo); a.pat16 = reinterpret_cast<const uint4 *>(Lt.d_pat16);
@@ -1628,12 +1719,12 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
             a.bits[k] = Lt.bits[k]; a.bm_off[k] = Lt.bm_off[k]; a.rank_base[k] = Lt.rank_base[k];
         }
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
-        a.spans_out = (fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
-        a.rec_flag = mf ? mf->flags : nullptr;
+        a.spans_out = (!trial_tiles && fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
+        a.rec_flag = (mf && !trial_tiles) ? mf->flags : nullptr;
         const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + 64;
         const uint32_t dyn = lit_lds_bytes(Lt);
         const uint32_t bpc = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
-        const uint32_t grid = std::min<uint32_t>(L.n_tiles, 256u * bpc);
+        const uint32_t grid = std::min<uint32_t>(a.n_tiles, 256u * bpc);
         // Block size: when the tables leave room for only <= 2 blocks per CU (large factor
         // sets: the regex prefilter), 512-thread blocks double the waves that hide the
         // candidate stage's L2 latency (C4 prefilter 2.71 -> 1.84 ms per 4M banners); with
@@ -1643,22 +1734,67 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         const double bytes = (double)n + 8.0 * R;
         auto launch = [&](auto kern, int blk) -> int {
             SG_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn));
-            SG_LAUNCH_B(c, name, bytes, kern, grid, blk, dyn, a);
+            if (trial_tiles) hipLaunchKernelGGL(kern, dim3(grid), dim3(blk), dyn, c->stream, a);
+            else SG_LAUNCH_B(c, name, bytes, kern, grid, blk, dyn, a);
+            SG_HIP(hipGetLastError());
             return SG_OK;
         };
         // (block, positions per thread) pairs of one parse tile; the template picks the
-        // length classes probed per position
-        auto by_tmpl = [&](auto k18, auto k1c, auto k1f, int blk) -> int {
-            if (Lt.tmpl == 0x18u) return launch(k18, blk);
-            if (Lt.tmpl == 0x1Cu) return launch(k1c, blk);
-            return launch(k1f, blk);
+        // class scheme and the length classes probed per position
+        auto by_tmpl = [&](auto k18, auto k1c, auto k1f, auto k20, auto k24, auto k27, int blk) -> int {
+            switch (Lt.tmpl) {
+                case 0x18u: return launch(k18, blk);
+                case 0x1Cu: return launch(k1c, blk);
+                case 0x1Fu: return launch(k1f, blk);
+                case 0x20u: return launch(k20, blk);
+                case 0x24u: return launch(k24, blk);
+                default: return launch(k27, blk);
+            }
         };
-        if (ls_block == 512 && bpt == 16) SG_TRY(by_tmpl(k_lit_scan<512, 16, 0x18u>, k_lit_scan<512, 16, 0x1Cu>, k_lit_scan<512, 16, 0x1Fu>, 512));
-        else if (ls_block == 512 && bpt == 32) SG_TRY(by_tmpl(k_lit_scan<512, 32, 0x18u>, k_lit_scan<512, 32, 0x1Cu>, k_lit_scan<512, 32, 0x1Fu>, 512));
-        else if (ls_block == 256 && bpt == 32) SG_TRY(by_tmpl(k_lit_scan<256, 32, 0x18u>, k_lit_scan<256, 32, 0x1Cu>, k_lit_scan<256, 32, 0x1Fu>, 256));
-        else if (ls_block == 256 && bpt == 64) SG_TRY(by_tmpl(k_lit_scan<256, 64, 0x18u>, k_lit_scan<256, 64, 0x1Cu>, k_lit_scan<256, 64, 0x1Fu>, 256));
+#define SG_LIT_KERNELS(B, P) k_lit_scan<B, P, 0x18u>, k_lit_scan<B, P, 0x1Cu>, k_lit_scan<B, P, 0x1Fu>, \
+                             k_lit_scan<B, P, 0x20u>, k_lit_scan<B, P, 0x24u>, k_lit_scan<B, P, 0x27u>
+        if (ls_block == 512 && bpt == 16) SG_TRY(by_tmpl(SG_LIT_KERNELS(512, 16), 512));
+        else if (ls_block == 512 && bpt == 32) SG_TRY(by_tmpl(SG_LIT_KERNELS(512, 32), 512));
+        else if (ls_block == 256 && bpt == 32) SG_TRY(by_tmpl(SG_LIT_KERNELS(256, 32), 256));
+        else if (ls_block == 256 && bpt == 64) SG_TRY(by_tmpl(SG_LIT_KERNELS(256, 64), 256));
         else { set_error("k_lit_scan: unsupported tile geometry"); return SG_E_INVAL; }
+#undef SG_LIT_KERNELS
         return SG_OK;
+    };
+    // The class scheme of a filter (two-class or joint, see build_lit): decided once per
+    // matcher, by timing both over the first tiles of the first input large enough to tell
+    // (until then the two-class scheme runs).
+    auto scheme = [&](const sg_matcher::Lit &two, const sg_matcher::Lit &joint, std::atomic<int> &mode,
+                      const uint32_t *fo, const uint32_t *fp) -> const sg_matcher::Lit & {
+        const int forced = sw_lit_scheme();
+        if (forced >= 0) return forced ? joint : two;
+        int m = mode.load();
+        constexpr uint32_t TRIAL_TILES = 2048, MIN_TILES = 1024;
+        if (m < 0 && L.n_tiles >= MIN_TILES) {
+            const uint32_t tt = std::min<uint32_t>(L.n_tiles, TRIAL_TILES);
+            hipEvent_t ev[3];
+            for (auto &e : ev) (void)hipEventCreate(&e);
+            float ms[2] = {0.f, 0.f};
+            bool ok = true;
+            for (int rep = 0; rep < 2 && ok; ++rep) {  // the first round warms caches
+                (void)hipEventRecord(ev[0], c->stream);
+                ok = run_lit("lit_trial", two, nullptr, cnt + 4, 0u, fo, fp, tt) == SG_OK;
+                (void)hipEventRecord(ev[1], c->stream);
+                ok = ok && run_lit("lit_trial", joint, nullptr, cnt + 4, 0u, fo, fp, tt) == SG_OK;
+                (void)hipEventRecord(ev[2], c->stream);
+                ok = ok && hipEventSynchronize(ev[2]) == hipSuccess;
+                if (ok && rep == 1) {
+                    (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
+                    (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
+                }
+            }
+            for (auto &e : ev) (void)hipEventDestroy(e);
+            if (ok) {
+                m = ms[1] < ms[0] ? 1 : 0;
+                mode.store(m);
+            }
+        }
+        return m == 1 ? joint : two;
     };
     if (h->has_pre && R) {
         uint64_t ccap = std::min<uint64_t>(std::max<uint64_t>(std::max<uint64_t>(1u << 20, (uint64_t)R), slot_elems<uint64_t>(c, S_PART)),
@@ -1666,7 +1802,8 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         for (int attempt = 0; attempt < 2; ++attempt) {
             SG_TRY(slot(c, S_PART, ccap, &cand));
             SG_HIP(hipMemsetAsync(cnt + 1, 0, 4, c->stream));
-            SG_TRY(run_lit("re_prefilter", h->prelit, cand, cnt + 1, (uint32_t)ccap, h->dplan.fac_off, h->dplan.fac_pids));
+            SG_TRY(run_lit("re_prefilter", scheme(h->prelit, h->prelit_j, h->prelit_mode, h->dplan.fac_off, h->dplan.fac_pids),
+                           cand, cnt + 1, (uint32_t)ccap, h->dplan.fac_off, h->dplan.fac_pids));
             SG_TRY(ctx_readback(c, &n_cand, cnt + 1, 4));
             if (n_cand <= ccap) break;
             ccap = std::min<uint64_t>((uint64_t)n_cand + (n_cand >> 3) + 1024, 0xfffff000ull);
@@ -1691,14 +1828,16 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     if (mf) {
         SG_TRY(slot(c, S_M_FLAG, (size_t)R + 16, &mf->flags));
         SG_HIP(hipMemsetAsync(mf->flags, 0, (size_t)R + 16, c->stream));
-        if (R) SG_TRY(run_lit("lit_match", h->lit, nullptr, cnt, 0u, nullptr, nullptr));
+        if (R) SG_TRY(run_lit("lit_match", scheme(h->lit, h->lit_j, h->lit_mode, nullptr, nullptr), nullptr, cnt, 0u, nullptr, nullptr));
         mf->L = L;
         return SG_OK;
     }
     for (int attempt = 0; attempt < 2; ++attempt) {
         SG_TRY(slot(c, S_M_HITS, cap, &hits));
         SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
-        if (R && h->lit.on) SG_TRY(run_lit("lit_match", h->lit, hits, cnt, (uint32_t)cap, nullptr, nullptr));
+        if (R && h->lit.on)
+            SG_TRY(run_lit("lit_match", scheme(h->lit, h->lit_j, h->lit_mode, nullptr, nullptr), hits, cnt, (uint32_t)cap, nullptr,
+                           nullptr));
         if (R) {
             const bool multi = sw_dfa_multi();
             if (multi) {
@@ -1853,7 +1992,8 @@ int sg_ac_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pats
     const auto &T = m->tables[0];
     if ((uint64_t)T.n_states * T.n_classes * 2 > AC_HOT_BYTES || sw_force_litfilter()) {
         // 128 bitmap bits per pattern: X1 candidates 37M -> 17M per 10M lines for 2 blocks/CU
-        rc = build_lit(pats, pat_offs, n_pats, flags, &m->lit, 1u);
+        rc = build_lit(pats, pat_offs, n_pats, flags, &m->lit, 1u, false);
+        if (rc == SG_OK) rc = build_lit(pats, pat_offs, n_pats, flags, &m->lit_j, 1u, true);
         if (rc == SG_E_UNSUPPORTED) {
             m->lit = sg_matcher::Lit{};  // too many patterns of one length class: keep the automaton
         } else if (rc != SG_OK) {
@@ -1884,7 +2024,9 @@ int sg_dfa_compile(const uint8_t *pats, const uint32_t *pat_offs, uint32_t n_pat
             blob.insert(blob.end(), f.begin(), f.end());
             offs.push_back((uint32_t)blob.size());
         }
-        rc = build_lit(blob.data(), offs.data(), (uint32_t)plan.factors.size(), SG_NOCASE, &m->prelit);
+        rc = build_lit(blob.data(), offs.data(), (uint32_t)plan.factors.size(), SG_NOCASE, &m->prelit, 0u, false);
+        if (rc == SG_OK)
+            rc = build_lit(blob.data(), offs.data(), (uint32_t)plan.factors.size(), SG_NOCASE, &m->prelit_j, 0u, true);
         if (rc != SG_OK) { delete m; return rc; }
         m->has_pre = true;
         m->fac_off = plan.fac_off;

@@ -24,6 +24,12 @@ inline bool sw_hit_radix() { return env_switch("SG_HIT_RADIX", false); }
 // SG_REGEX_ANCHORED=1: every prefiltered regex verified by its anchored DFA
 // (tests/test_gpu_match.py).
 inline bool sw_regex_anchored() { return env_switch("SG_REGEX_ANCHORED", false); }
+// SG_LIT_SCHEME=0|1: literal filters run the two-class (0) or the joint (1) class scheme
+// instead of timing both on the first large input (tests/test_gpu_match.py).
+inline int sw_lit_scheme() {
+    const char *v = getenv("SG_LIT_SCHEME");
+    return v ? (atoi(v) != 0 ? 1 : 0) : -1;
+}
 // SG_TM_SORT=1: nuclei templates evaluated through the sort path instead of the
 // record-wave evaluator (tests/test_gpu_templates.py).
 inline bool sw_tm_sort() { return env_switch("SG_TM_SORT", false); }

@@ -18,17 +18,20 @@ WORDS = [base64.b64decode(w) for w in SIG["words"]]
 REGEXES = [base64.b64decode(r["p"]) for r in SIG["regexes"]]
 
 
-@pytest.fixture(scope="module", params=["auto", "litfilter"])
+@pytest.fixture(scope="module", params=["auto", "litfilter", "joint"])
 def sg(request):
-    """Run every literal test with the engine the compiler picks and with the hashed
-    q-gram filter forced (SG_FORCE_LITFILTER is read at compile time)."""
+    """Run every literal test with the engine the compiler picks, with the hashed q-gram
+    filter forced (SG_FORCE_LITFILTER is read at compile time) in its two-class scheme, and
+    forced in its joint scheme (SG_LIT_SCHEME=1; large inputs pick one by timing both)."""
     import os
     import swarm_amd
     assert swarm_amd.device_count() > 0
-    if request.param == "litfilter":
+    if request.param in ("litfilter", "joint"):
         os.environ["SG_FORCE_LITFILTER"] = "1"
+        os.environ["SG_LIT_SCHEME"] = "0" if request.param == "litfilter" else "1"
     yield swarm_amd
     os.environ.pop("SG_FORCE_LITFILTER", None)
+    os.environ.pop("SG_LIT_SCHEME", None)
 
 
 @pytest.mark.parametrize("case", GR["literal"], ids=lambda c: c["name"])
