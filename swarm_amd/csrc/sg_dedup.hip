@@ -234,8 +234,8 @@ __device__ __forceinline__ int rec_cmp8(const uint8_t *buf, uint32_t sa, uint32_
 // refinement rounds (rare: wave-aggregated atomics, unordered — the refinement rounds place
 // each group's rows by their positions); otherwise brk is given (after refinement:
 // sub-segment heads) and read.
-// DUP: dup[i] = record i equals record i-1 inside its segment; segbad[i] = it differs (the
-// segment needs sorting; SegHeadPred lists its head).
+// DUP: dup[i] = record i equals record i-1 inside its segment; where it differs, the
+// segment's head is marked in segbad (the segment needs sorting; SegPred lists it).
 // cnt[2] = big groups (zeroed by the caller).
 // Bit j (0..15) = byte j of the 16-B word is nonzero.
 __device__ __forceinline__ uint32_t swar_nonzero16(uint4 w) {
@@ -304,43 +304,54 @@ __global__ __launch_bounds__(256) void k_adjacent2(const uint8_t *__restrict__ S
     }
     if constexpr (!DUP) return;
     bool d = false;
-    if (live && !head) d = ((ki & 0xffu) < bk_full(base)) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, bk_off(base));
-    if (live) {
-        dup[i] = d ? 1 : 0;
-        segbad[i] = (!head && !d) ? 1 : 0;  // i differs from i - 1 inside one segment
+    if (live && !head) {
+        d = ((ki & 0xffu) < bk_full(base)) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, bk_off(base));
+        if (!d) {
+            // i differs from i - 1 inside one segment: mark the segment's head (the last group
+            // start at or before i - 1) bad
+            uint32_t h = i - 1;
+            bool found = true;
+            if constexpr (KEYS) {
+                // the run of ki ending at i - 1 starts in [i - 64, i - 1] unless it is a big
+                // group (refinement rounds first, then this pass again): bisect the keys
+                uint32_t lo = i >= WAVE_GROUP ? i - WAVE_GROUP : 0u;
+                if (lo > 0 && K[lo] == ki) {
+                    found = false;
+                } else {
+                    while (lo < h) {
+                        const uint32_t mid = (lo + h) >> 1;
+                        if (K[mid] == ki) h = mid; else lo = mid + 1;
+                    }
+                }
+            } else {
+                for (;;) {  // 16 brk bytes per aligned load instead of a dependent byte walk
+                    const uint32_t a = h & ~15u;
+                    const uint32_t m = swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a)) & ((2u << (h - a)) - 1u);
+                    if (m) { h = a + 31u - (uint32_t)__clz(m); break; }
+                    if (a == 0) { h = 0; break; }
+                    h = a - 1;
+                }
+            }
+            if (found) segbad[h] = 1;
+        }
     }
+    if (live) dup[i] = d ? 1 : 0;
 }
 
-// Heads of the segments holding a bad pair (k_adjacent2's segbad[i]: record i differs from
-// record i - 1 in its segment): A = up to SEG_SMALL members, B = up to WAVE_GROUP. A head
-// looks at its segment's brk and segbad bytes 16 at a time (aligned loads, SWAR; the slots
-// have 16 B of tail room). Segments over WAVE_GROUP records are skipped: big groups, refined
-// first (and the adjacent pass run again).
-struct SegHeadPred {
+// Heads of bad segments (segbad, marked by k_adjacent2): A = up to SEG_SMALL members, B = more
+// (<= WAVE_GROUP). A bad head's segment is small iff a break (brk, or the end) lies in
+// (i, i + SEG_SMALL]: two aligned 16-B loads of brk (the slot has 32 B of tail room).
+struct SegPred {
     const uint8_t *brk, *segbad;
     uint32_t n;
-    __device__ uint32_t operator()(uint32_t j) const {
-        if (j != 0 && !brk[j]) return 0u;
-        if (j + 1 >= n || brk[j + 1]) return 0u;  // one member (most heads): never bad
-        // members j .. e-1: e = the next break after j (or n); bad iff a segbad byte in (j, e)
-        uint32_t a = (j + 1) & ~15u, sh = (j + 1) - a;
-        bool bad = false, ended = false;
-        uint32_t len = 1;
-        for (uint32_t step = 0; step < (WAVE_GROUP + 31) / 16 && !ended; ++step) {
-            uint32_t mb = swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a));
-            const uint32_t mg = swar_nonzero16(*reinterpret_cast<const uint4 *>(segbad + a));
-            if (n - a < 16u) mb |= ~0u << (n - a);  // positions >= n end the segment
-            mb = (mb >> sh) << sh;
-            const uint32_t stop = mb ? (uint32_t)__ffs((int)mb) - 1u : 16u;  // first break in this window
-            const uint32_t inside = ((stop >= 16u) ? 0xffffu : ((1u << stop) - 1u)) & ~((1u << sh) - 1u);
-            if (mg & inside) bad = true;
-            len += stop - sh;
-            if (stop < 16u) ended = true;
-            a += 16;
-            sh = 0;
-        }
-        if (!bad || !ended || len > WAVE_GROUP) return 0u;
-        return len <= SEG_SMALL ? 1u : 2u;
+    __device__ uint32_t operator()(uint32_t i) const {
+        static_assert(SEG_SMALL == 16, "window of two 16-B loads");
+        if (!segbad[i]) return 0u;
+        const uint32_t a = (i + 1) & ~15u, sh = (i + 1) - a;
+        uint32_t m = swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a)) |
+                     (swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a + 16)) << 16);
+        if (n - a < 32u) m |= ~0u << (n - a);  // positions >= n end the segment
+        return ((m >> sh) & 0xffffu) ? 1u : 2u;
     }
 };
 
@@ -1152,7 +1163,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // model: key0 + brk + span per record, both records' bytes where compared, dup out
     uint64_t *stot = nullptr;
     auto adjacent = [&](bool keys, bool with_dup, const uint8_t *Sb, const uint2 *SSp) -> int {
-        SG_HIP(hipMemsetAsync(acnt, 0, 16, c->stream));
+        SG_HIP(hipMemsetAsync(segbad, 0, cnt_off + 16, c->stream));  // head marks + list counters
         if (keys && with_dup)
             SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, (k_adjacent2<true, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
                         brk, R, dup, segbad, AL, base);
@@ -1162,7 +1173,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         else
             SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, (k_adjacent2<false, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
                         brk, R, dup, segbad, AL, base);
-        if (with_dup) SG_TRY(run_select2_nb(c, "seg_heads", SegHeadPred{brk, segbad, R}, R, hs, hb, S_COUNT2, &stot));
+        if (with_dup) SG_TRY(run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, &stot));
         return SG_OK;
     };
     uint32_t lerr_v = 0;
