@@ -46,7 +46,8 @@ KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_u
                  "bk_l1_count": "k_bp_count", "bk_l2_count": "k_bp_count", "bk_compact": "k_bk_compact",
                  "part_emit": "k_part_apply", "range_bytes": "k_range_bytes", "gather_spans": "k_gather_spans",
                  "gather_matched": "k_gather_matched", "seg_wave": "k_seg_wave", "seg_small": "k_seg_small",
-                 "rs_up": "k_rs_up", "lcp": "k_lcp", "rekey": "k_rekey"}
+                 "rs_up": "k_rs_up", "lcp": "k_lcp", "rekey": "k_rekey", "key_sample": "k_key_sample",
+                 "key_stats": "k_key_stats", "rs_dsum": "k_rs_dsum"}
 
 
 def pmc_traffic(workload, kernel):

@@ -688,43 +688,103 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
 // equality questions are then decided from byte L on, and key0 is taken there: for URL lists
 // (every record starts "https://") the first 7 bytes say nothing, and equal-key0 runs would
 // span the whole buffer (binary searches over them in the diff, refinement rounds in the sort).
+// Key statistics for the sort (sg_internal.hpp KeyStats, KeyStatD): OR and AND over every
+// key (their XOR: the bits that vary) and the tag byte's range (the narrowed tag
+// min(tag, kw + 1) varies iff its clamped ends differ). Each block writes its partial with
+// plain stores; k_key_sample's first block combines them (512 blocks' atomics on one line
+// serialised: +20 µs on C2's cur keys).
+struct KeyStatAcc {
+    uint64_t o = 0, a = ~0ull;
+    uint32_t tmin = 255u, tmax = 0u;
+    __device__ __forceinline__ void add(uint64_t k) {
+        o |= k;
+        a &= k;
+        const uint32_t t = (uint32_t)(k & 0xffu);
+        tmin = min(tmin, t);
+        tmax = max(tmax, t);
+    }
+};
+// Block-wide reduce (256 threads) into part[blockIdx.x]; s: 4 x KeyStatD of LDS.
+__device__ __forceinline__ void kstat_flush(KeyStatAcc acc, KeyStatD *s, KeyStatD *part) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        acc.o |= (uint64_t)__shfl_xor((long long)acc.o, off, 64);
+        acc.a &= (uint64_t)__shfl_xor((long long)acc.a, off, 64);
+        acc.tmin = min(acc.tmin, (uint32_t)__shfl_xor((int)acc.tmin, off, 64));
+        acc.tmax = max(acc.tmax, (uint32_t)__shfl_xor((int)acc.tmax, off, 64));
+    }
+    const int wid = threadIdx.x >> 6;
+    if (lane_id() == 0) s[wid] = KeyStatD{acc.o, acc.a, acc.tmin, acc.tmax};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) {
+            acc.o |= s[w].o;
+            acc.a &= s[w].a;
+            acc.tmin = min(acc.tmin, s[w].tmin);
+            acc.tmax = max(acc.tmax, s[w].tmax);
+        }
+        part[blockIdx.x] = KeyStatD{acc.o, acc.a, acc.tmin, acc.tmax};
+    }
+}
+
+// The common prefix of one record (key k, span xs) with the reference record.
+__device__ __forceinline__ uint32_t lcp_one(const uint8_t *buf, const uint2 *spans, uint32_t i, uint64_t k,
+                                            const uint8_t *rbuf, const uint2 *rspans, uint64_t kr, uint32_t best) {
+    // key0 = 7 bytes big-endian << 8 | min(len, 8): the first 7 bytes come from the keys
+    const uint64_t x = (k ^ kr) >> 8;
+    const uint32_t tk = (uint32_t)(k & 0xffu), tr = (uint32_t)(kr & 0xffu);
+    if (x) return min((uint32_t)__builtin_clzll(x << 8) >> 3, min(tk, tr));
+    if (tk < 8u || tr < 8u) return min(tk, tr);
+    // both share their first 7 bytes (URL schemes): 8 bytes per step from byte 7
+    const uint2 xs = spans[i], r = rspans[0];
+    const uint32_t m = min(min(xs.y - xs.x, r.y - r.x), best);
+    uint32_t l = 7;
+    while (l < m) {
+        const uint32_t t = (m - l) < 8u ? (m - l) : 8u;
+        const uint64_t d = load_le(buf, xs.x + l, t) ^ load_le(rbuf, r.x + l, t);
+        if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
+        l += t;
+    }
+    return min(l, m);
+}
+
+// st (optional): the keys' KeyStatD partial per block, gathered in the same read (the cur
+// keys, for the sort).
+constexpr int LCP_U = 4;
 __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                              const uint64_t *__restrict__ keys, uint32_t n,
                                              const uint8_t *__restrict__ rbuf, const uint2 *__restrict__ rspans,
-                                             const uint64_t *__restrict__ rkeys, uint32_t *__restrict__ out) {
+                                             const uint64_t *__restrict__ rkeys, uint32_t *__restrict__ out,
+                                             KeyStatD *__restrict__ st) {
     __shared__ uint32_t s_min[4];
+    __shared__ KeyStatD s_st[4];
     const uint64_t kr = rkeys[0];
-    const uint32_t tr = (uint32_t)(kr & 0xffu);
     uint32_t best = 255;
-    // grid-stride (at most 512 blocks): at most one memory-side atomic per block
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        // key0 = 7 bytes big-endian << 8 | min(len, 8): the first 7 bytes come from the keys
-        const uint64_t k = keys[i];
-        const uint64_t x = (k ^ kr) >> 8;
-        const uint32_t tk = (uint32_t)(k & 0xffu);
-        uint32_t l;
-        if (x) {
-            l = min((uint32_t)__builtin_clzll(x << 8) >> 3, min(tk, tr));
-        } else if (tk < 8u || tr < 8u) {
-            l = min(tk, tr);
-        } else {
-            // both share their first 7 bytes (URL schemes): 8 bytes per step from byte 7
-            const uint2 xs = spans[i], r = rspans[0];
-            const uint32_t m = min(min(xs.y - xs.x, r.y - r.x), best);
-            l = 7;
-            while (l < m) {
-                const uint32_t t = (m - l) < 8u ? (m - l) : 8u;
-                const uint64_t d = load_le(buf, xs.x + l, t) ^ load_le(rbuf, r.x + l, t);
-                if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
-                l += t;
-            }
-            l = min(l, m);
+    KeyStatAcc acc;
+    // grid-stride (at most 512 blocks): at most one memory-side atomic per block and word;
+    // LCP_U keys in flight per thread (one dependent load per trip left the loop latency-bound:
+    // 1.6 TB/s on C2's cur keys)
+    const uint32_t stride = gridDim.x * blockDim.x * LCP_U;
+    for (uint32_t i0 = blockIdx.x * blockDim.x * LCP_U + threadIdx.x; i0 < n; i0 += stride) {
+        uint64_t k[LCP_U];
+#pragma unroll
+        for (int u = 0; u < LCP_U; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            k[u] = i < n ? keys[i] : 0ull;
         }
-        best = min(best, l);
+#pragma unroll
+        for (int u = 0; u < LCP_U; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            if (i < n) {
+                best = min(best, lcp_one(buf, spans, i, k[u], rbuf, rspans, kr, best));
+                acc.add(k[u]);
+            }
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
     if (lane_id() == 0) s_min[threadIdx.x >> 6] = best;
+    if (st) kstat_flush(acc, s_st, st);
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
@@ -733,72 +793,22 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
     }
 }
 
-// k_lcp over cur fused with the 8 digit histograms of cur's keys (k_rs_hist's per-wave LDS
-// counting), so the keys are read once for both (C2: one 80 MB pass and a launch fewer).
-__global__ __launch_bounds__(256) void k_lcp_hist(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
-                                                  const uint64_t *__restrict__ keys, uint32_t n,
-                                                  const uint8_t *__restrict__ rbuf, const uint2 *__restrict__ rspans,
-                                                  const uint64_t *__restrict__ rkeys, uint32_t *__restrict__ out,
-                                                  uint32_t *__restrict__ hist) {
-    __shared__ uint32_t h[4][8][256];
-    __shared__ uint32_t s_min[4];
-    for (int x = threadIdx.x; x < 4 * 8 * 256; x += 256) (&h[0][0][0])[x] = 0;
-    __syncthreads();
-    const int wid = threadIdx.x >> 6;
-    const uint64_t kr = rkeys[0];
-    const uint32_t tr = (uint32_t)(kr & 0xffu);
-    uint32_t best = 255;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    const uint32_t n_up = ((n + stride - 1) / stride) * stride;  // every lane runs the same trips (ballots)
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
-        const bool valid = i < n;
-        const uint64_t k = valid ? keys[i] : 0ull;
-        if (valid) {
-            const uint64_t x = (k ^ kr) >> 8;
-            const uint32_t tk = (uint32_t)(k & 0xffu);
-            uint32_t l;
-            if (x) {
-                l = min((uint32_t)__builtin_clzll(x << 8) >> 3, min(tk, tr));
-            } else if (tk < 8u || tr < 8u) {
-                l = min(tk, tr);
-            } else {
-                const uint2 xs = spans[i], r = rspans[0];
-                const uint32_t m = min(min(xs.y - xs.x, r.y - r.x), best);
-                l = 7;
-                while (l < m) {
-                    const uint32_t t = (m - l) < 8u ? (m - l) : 8u;
-                    const uint64_t d = load_le(buf, xs.x + l, t) ^ load_le(rbuf, r.x + l, t);
-                    if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
-                    l += t;
-                }
-                l = min(l, m);
-            }
-            best = min(best, l);
-        }
-        const uint32_t cnt = (uint32_t)__popcll(__ballot(valid));
+// KeyStatD of keys already in place (the gathered cur records of the fused match step).
+__global__ __launch_bounds__(256) void k_key_stats(const uint64_t *__restrict__ keys, uint32_t n, KeyStatD *__restrict__ st) {
+    __shared__ KeyStatD s_st[4];
+    KeyStatAcc acc;
+    const uint32_t stride = gridDim.x * blockDim.x * LCP_U;
+    for (uint32_t i0 = blockIdx.x * blockDim.x * LCP_U + threadIdx.x; i0 < n; i0 += stride) {
+        uint64_t k[LCP_U];
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            const uint32_t d = (uint32_t)(k >> (8 * p)) & 255u;
-            const uint32_t d0 = (uint32_t)__shfl(d, 0, 64);
-            if (__all(!valid || d == d0)) {
-                if (lane_id() == 0 && cnt) h[wid][p][d0] += cnt;
-            } else if (valid) {
-                atomicAdd(&h[wid][p][d], 1u);
-            }
+        for (int u = 0; u < LCP_U; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            k[u] = i < n ? keys[i] : keys[i0];
         }
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
-    if (lane_id() == 0) s_min[wid] = best;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
-        if (b < 255u && b < __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(out, b);
+        for (int u = 0; u < LCP_U; ++u) acc.add(k[u]);
     }
-    for (int x = threadIdx.x; x < 8 * 256; x += 256) {
-        const uint32_t v = h[0][0][x] + h[1][0][x] + h[2][0][x] + h[3][0][x];
-        if (v) atomicAdd(&hist[x], v);
-    }
+    kstat_flush(acc, s_st, st);
 }
 
 // key0 (7 bytes + min(rem, 8)) -> the kw-byte key (kw bytes + min(rem, kw + 1)).
@@ -811,12 +821,18 @@ __global__ __launch_bounds__(256) void k_narrow_keys(uint64_t *__restrict__ keys
     }
 }
 
+// st (optional): the new keys' KeyStatD, gathered as they are written.
 __global__ __launch_bounds__(256) void k_rekey(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, uint32_t n,
-                                               uint32_t base, uint64_t *__restrict__ keys) {
+                                               uint32_t base, uint64_t *__restrict__ keys, KeyStatD *__restrict__ st) {
+    __shared__ KeyStatD s_st[4];
+    KeyStatAcc acc;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint2 x = spans[i];
-        keys[i] = chunk_key(buf, x.x, x.y, base);
+        const uint64_t k = chunk_key(buf, x.x, x.y, base);
+        keys[i] = k;
+        acc.add(k);
     }
+    if (st) kstat_flush(acc, s_st, st);
 }
 
 // ------------------------------------------------------------------ host pipeline
@@ -1071,7 +1087,7 @@ struct OutBuf {
 
 static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
                         UView *uv, const Lines *pre = nullptr, uint32_t base = make_bk(0u, 7u), const OutBuf *dst = nullptr,
-                        const uint32_t *host_hist = nullptr) {
+                        const KeyStats *ks = nullptr) {
     *uv = UView{};
     Lines L;
     if (pre) L = *pre;
@@ -1137,8 +1153,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // on the host the sort may finish its low digits per group in LDS (lerr: checked with
     // the group counts below, before anything trusts the order)
     uint32_t *lerr = nullptr;
-    SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V, "rs_pass", host_hist,
-                            (base >> 16) < 7u ? base >> 16 : 0u, host_hist ? &lerr : nullptr));
+    SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V, "rs_pass", ks,
+                            (base >> 16) < 7u ? base >> 16 : 0u, ks ? &lerr : nullptr));
     if (lerr) c->last_flags |= 1u;
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
@@ -1211,7 +1227,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         // plain LSD sort of the same pairs (keys already narrowed, histograms unchanged)
         uint64_t *Ka = (K == L.keys) ? k2 : L.keys;
         uint2 *Va = (V == L.spans) ? v2 : L.spans;
-        SG_TRY(radix_sort_spans(c, K, V, Ka, Va, R, 0, 64, &K, &V, "rs_pass", host_hist, 0u, nullptr));
+        SG_TRY(radix_sort_spans(c, K, V, Ka, Va, R, 0, 64, &K, &V, "rs_pass", ks, 0u, nullptr));
         lerr = nullptr;
         c->last_flags |= 2u;
     }
@@ -1297,10 +1313,18 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     // itself when strictly increasing), then the current scan's sort -u.
     Lines Lp, Lc;
     bool prior_sorted = true;
-    uint32_t *dflag;  // [0] prior not strictly increasing, [1] common prefix length
-    SG_TRY(slot(c, S_M_CNT, 4, &dflag));
-    const uint32_t init[2] = {0u, 255u};
-    SG_HIP(hipMemcpyAsync(dflag, init, 8, hipMemcpyHostToDevice, c->stream));
+    // dflag: [0] prior not strictly increasing, [1] common prefix length, then the cur keys'
+    // KeyStatD from byte 0 ([4..10)) and after a rekey at the common prefix ([12..18))
+    uint32_t *dflag;
+    SG_TRY(slot(c, S_M_CNT, 20, &dflag));
+    KeyStatD *st0 = reinterpret_cast<KeyStatD *>(dflag + 4), *st1 = reinterpret_cast<KeyStatD *>(dflag + 12);
+    {
+        uint32_t init[20] = {0u, 255u};
+        const KeyStatD z{0ull, ~0ull, 255u, 0u};
+        memcpy(init + 4, &z, sizeof z);
+        memcpy(init + 12, &z, sizeof z);
+        SG_HIP(hipMemcpyAsync(dflag, init, sizeof init, hipMemcpyHostToDevice, c->stream));
+    }
     if (cur_lcp) SG_HIP(hipMemcpyAsync(dflag + 1, cur_lcp, 4, hipMemcpyDeviceToDevice, c->stream));
     if (have_prior) {
         if (!cur_pre) SG_TRY(run_lines2(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp, d_cur, n_cur, CUR_VIEW.lines, &Lc));
@@ -1318,57 +1342,63 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint8_t *rbuf = ref_cur ? d_cur : d_prior;
     const uint2 *rsp = ref_cur ? Lc.spans : (have_prior ? Lp.spans : nullptr);
     const uint64_t *rkeys = ref_cur ? Lc.keys : (have_prior ? Lp.keys : nullptr);
+    // the sort's key statistics (KeyStats): exact varying bits, sampled digit histograms
     const bool want_hist = Lc.n_rec >= 4096;
-    const uint32_t *dhist = nullptr;
-    const bool fuse_hist = want_hist && rsp && Lc.n_rec && !cur_lcp;
-    if (fuse_hist) {
-        uint32_t *hist;
-        SG_TRY(slot(c, S_HIST, 8 * 256 * 2 + 8, &hist));
-        SG_HIP(hipMemsetAsync(hist, 0, 8 * 256 * 4, c->stream));
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp_hist, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 1024u), 256, 0, d_cur,
-                    Lc.spans, Lc.keys, Lc.n_rec, rbuf, rsp, rkeys, dflag + 1, hist);
-        dhist = hist;
-    } else if (rsp && Lc.n_rec && !cur_lcp) {
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 512u), 256, 0, d_cur,
-                    Lc.spans, Lc.keys, Lc.n_rec,
-                    rbuf, rsp, rkeys, dflag + 1);
+    uint32_t *shist = nullptr, hist_n = 0;
+    KeyStatD *parts = nullptr;  // per-block partials (k_lcp / k_key_stats / k_rekey blocks)
+    const uint32_t g_cur = std::min<uint32_t>(grid_for(Lc.n_rec, 256), 512u);
+    const uint32_t g_rekey = std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u);
+    if (want_hist) {
+        SG_TRY(slot(c, S_HIST, 8 * 256 + 2048 * sizeof(KeyStatD) / 4, &shist));
+        parts = reinterpret_cast<KeyStatD *>(shist + 8 * 256);
+        SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));
     }
+    if (rsp && Lc.n_rec && !cur_lcp)
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, g_cur, 256, 0, d_cur, Lc.spans, Lc.keys, Lc.n_rec, rbuf, rsp, rkeys,
+                    dflag + 1, parts);
+    else if (want_hist)
+        SG_LAUNCH_B(c, "key_stats", 8.0 * Lc.n_rec, k_key_stats, g_cur, 256, 0, Lc.keys, Lc.n_rec, parts);
     if (rsp && have_prior && Lp.n_rec)
         SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 512u), 256, 0, d_prior,
-                    Lp.spans, Lp.keys, Lp.n_rec,
-                    rbuf, rsp, rkeys, dflag + 1);
-    // the cur keys' digit histograms (for the key width below) are queued now and come back
-    // with the flags; they stay valid when the common prefix turns out to be empty
-    if (want_hist && !dhist) SG_TRY(key_hist8_async(c, Lc.keys, Lc.n_rec, &dhist));
-    uint32_t fl[2] = {0u, 0u};
-    {
+                    Lp.spans, Lp.keys, Lp.n_rec, rbuf, rsp, rkeys, dflag + 1, (KeyStatD *)nullptr);
+    // the sample histograms (and the combined partials) come back with the flags; they stay
+    // valid when the common prefix turns out to be empty
+    if (want_hist) SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, parts, g_cur, st0));
+    uint32_t *hh = c->hist_host;
+    uint32_t fl[20] = {0u};
+    auto read_stats = [&](uint32_t words) -> int {
         uint8_t *pin = (uint8_t *)c->pinned;
-        SG_HIP(hipMemcpyAsync(pin, dflag, 8, hipMemcpyDeviceToHost, c->stream));
-        if (dhist) SG_HIP(hipMemcpyAsync(pin + 64, dhist, 8 * 256 * 4, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipMemcpyAsync(pin, dflag, 4 * words, hipMemcpyDeviceToHost, c->stream));
+        if (shist) SG_HIP(hipMemcpyAsync(pin + 128, shist, 8 * 256 * 4, hipMemcpyDeviceToHost, c->stream));
         SG_HIP(hipStreamSynchronize(c->stream));
-        memcpy(fl, pin, 8);
-        if (dhist) memcpy(c->hist_host, pin + 64, 8 * 256 * 4);
-    }
+        memcpy(fl, pin, 4 * words);
+        if (shist) memcpy(hh, pin + 128, 8 * 256 * 4);
+        return SG_OK;
+    };
+    SG_TRY(read_stats(want_hist ? 12u : 2u));
     prior_sorted = fl[0] == 0;
     const uint32_t base = (rsp && (Lc.n_rec || (have_prior && Lp.n_rec))) ? fl[1] : 0u;
     if (base) {
-        SG_LAUNCH(c, "rekey", k_rekey, std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u), 256, 0, d_cur, Lc.spans, Lc.n_rec,
-                  base, Lc.keys);
+        if (want_hist) SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));
+        SG_LAUNCH(c, "rekey", k_rekey, g_rekey, 256, 0, d_cur, Lc.spans, Lc.n_rec, base, Lc.keys, parts);
         if (have_prior && Lp.n_rec)
             SG_LAUNCH(c, "rekey", k_rekey, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior, Lp.spans,
-                      Lp.n_rec, base, Lp.keys);
+                      Lp.n_rec, base, Lp.keys, (KeyStatD *)nullptr);
+        if (want_hist) {  // keys changed: their statistics again
+            SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, parts, g_rekey, st1));
+            SG_TRY(read_stats(20u));
+            memcpy(fl + 4, fl + 12, sizeof(KeyStatD));
+        }
     }
-    // Key width: the cur keys' digit histograms (one read, replacing the sort's own) give
-    // each byte position's entropy; when the first 6 (or 5) key bytes already carry well
-    // over as many bits as there are records (expected << 1 record per key value, so few tie
-    // segments), the keys are narrowed to those bytes and the sort runs 1 (or 2) fewer
-    // passes. IP-like text (few distinct bytes per position) keeps the 7-byte key.
+    // Key width: the cur keys' sampled digit histograms give each byte position's entropy;
+    // when the first 6 (or 5) key bytes already carry well over as many bits as there are
+    // records (expected << 1 record per key value, so few tie segments), the keys are
+    // narrowed to those bytes and the sort runs 1 (or 2) fewer passes. IP-like text (few
+    // distinct bytes per position) keeps the 7-byte key.
     uint32_t kw = 7;
-    uint32_t *hh = c->hist_host;
-    const uint32_t *cur_hist = nullptr;
+    KeyStats ks;
     if (want_hist) {
-        if (base) SG_TRY(key_hist8(c, Lc.keys, Lc.n_rec, hh));  // keys changed: histograms again
-        const double N = (double)Lc.n_rec;
+        const double N = (double)hist_n;
         double H[8] = {0};
         for (int p = 0; p < 8; ++p)
             for (int d = 0; d < 256; ++d)
@@ -1378,9 +1408,14 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
                 }
         // margins measured on C2/X1: a 5-byte key saved 2 radix passes but its tie segments
         // (distinct records sharing 5 bytes) cost the segment sort about as much again
-        const double lg = std::log2(N);
+        const double lg = std::log2((double)Lc.n_rec);
         const double h5 = H[7] + H[6] + H[5] + H[4] + H[3], h6 = h5 + H[2];
-        const bool live2 = H[2] > 0.0, live1 = H[1] > 0.0;  // the passes narrowing removes
+        KeyStatD k0;
+        memcpy(&k0, fl + 4, sizeof k0);
+        uint64_t vary = (uint64_t)(k0.o ^ k0.a);
+        // the passes narrowing removes must be live (a sampled zero entropy may miss a rare
+        // digit: the exact varying bits decide)
+        const bool live2 = (vary >> 16) & 0xffu, live1 = (vary >> 8) & 0xffu;
         if (h5 >= lg + 4.0 && (live2 || live1)) kw = 5;
         else if (h6 >= lg + 2.0 && live1) kw = 6;
         if (kw < 7) {
@@ -1389,19 +1424,23 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
             // the narrowed keys' histograms: bytes kw..6 are zero, the tag is clamped to kw + 1
             for (int p = 1; p <= 7 - (int)kw; ++p) {
                 for (int d = 0; d < 256; ++d) hh[p * 256 + d] = 0;
-                hh[p * 256] = Lc.n_rec;
+                hh[p * 256] = hist_n;
+                vary &= ~(0xffull << (8 * p));
             }
             uint32_t tg[256] = {0};
             for (int d = 0; d < 256; ++d) tg[d < (int)kw + 1 ? d : (int)kw + 1] += hh[d];
             for (int d = 0; d < 256; ++d) hh[d] = tg[d];
         }
-        cur_hist = hh;
+        const uint32_t cl = kw + 1;  // the (narrowed) tag varies iff its clamped range does
+        vary &= ~0xffull;
+        if (std::min(k0.tmin, cl) != std::min(k0.tmax, cl)) vary |= 0xffull;
+        ks = KeyStats{vary, hh, hist_n};
     }
     c->last_kw = kw;
     const uint32_t bk = make_bk(base, kw);
     if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, bk));
     UView cu;
-    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, cur_hist));
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, want_hist ? &ks : nullptr));
     res->in_records = cu.in_records;
     res->uniq = ou ? ou->p : const_cast<uint8_t *>(cu.buf);
     res->uniq_bytes = cu.bytes;

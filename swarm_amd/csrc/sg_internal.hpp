@@ -41,19 +41,35 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
 // LSD radix sort of (u64 key, u32 val) pairs on bits [begin_bit, end_bit), stable.
 // Ping-pongs between (keys, vals) and (keys_alt, vals_alt); returns the final arrays.
 // iota_vals: vals[i] = i is implied on input (vals need not be initialised).
+// What the caller already knows about the keys of a sort over bits [0, 64):
+//   vary   : OR ^ AND over every key — the bits that differ between two keys (exact; a digit
+//            position with no varying bit is a trivial pass, skipped);
+//   hist   : host copy of the 8 digit histograms of a SAMPLE of hist_n keys (key_sample_hist),
+//            used only to plan (never as offsets).
+struct KeyStats {
+    uint64_t vary = ~0ull;
+    const uint32_t *hist = nullptr;
+    uint32_t hist_n = 0;
+};
+// Device form of the keys' varying bits and tag range (per-block partials, then combined).
+struct KeyStatD {
+    unsigned long long o, a;  // OR, AND over the keys
+    uint32_t tmin, tmax;      // the tag byte's range
+};
 // Stable sort of (key, span) pairs: the spans themselves are the payload (no id gather after).
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out,
-                     const char *pass_name = "rs_pass", const uint32_t *host_hist = nullptr,
+                     const char *pass_name = "rs_pass", const KeyStats *ks = nullptr,
                      uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr);
-// lsort_err (with host_hist): allows the hybrid sort (global passes over the top digits, the
+// lsort_err (with ks->hist): allows the hybrid sort (global passes over the top digits, the
 // rest per group in LDS); *lsort_err is then the device word that turns nonzero when a group
 // did not fit the LDS — the pairs are a valid permutation but not sorted, and the caller must
 // sort them again with lsort_err = nullptr (null when the plain LSD sort ran).
-// The 8 digit histograms (bits [0, 64), 8 x 256 counts) of keys, read back to the host.
-int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist);
-// The same histograms queued only (device pointer, 8 x 256 u32), for a combined read-back.
-int key_hist8_async(sg_ctx *c, const uint64_t *keys, uint32_t n, const uint32_t **dev_hist);
+// Queue the digit histograms of a row sample of the keys into dev_hist (8 x 256 u32, zeroed
+// by the caller); *sample_n = the keys counted. With parts: the nparts per-block KeyStatD
+// partials of an earlier kernel are combined into *st in the same launch.
+int key_sample_hist(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *dev_hist, uint32_t *sample_n,
+                    const KeyStatD *parts = nullptr, uint32_t nparts = 0, KeyStatD *st = nullptr);
 int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt,
                uint32_t n, int begin_bit, int end_bit, bool iota_vals,
                uint64_t **keys_out, uint32_t **vals_out, const char *pass_name = "rs_pass");

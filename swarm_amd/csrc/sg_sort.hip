@@ -13,7 +13,10 @@ namespace sg {
 //
 //   k_rs_hist  : all 8 digit histograms in ONE read of the keys (per-wave LDS histograms,
 //                a wave whose lanes share a digit adds once) -> per-pass digit bases and
-//                "trivial" passes (one digit holds every key) that are skipped.
+//                "trivial" passes (one digit holds every key) that are skipped. A caller
+//                that knows the keys' varying bits (KeyStats: the dedup gathers them while
+//                it reads the keys anyway) skips this pass and its read-back: each pass's
+//                digit bases then come from its own tile counts (k_rs_dsum).
 //   per pass   : k_rs_up    per-tile digit counts (per-wave LDS histograms)
 //                k_rs_cscan per digit, exclusive over tiles + the digit base
 //                k_rs_down  rank in tile (wave64 8-ballot digit match, stable), keys then
@@ -91,6 +94,71 @@ __global__ __launch_bounds__(256) void k_rs_scan(const uint32_t *hist, uint32_t 
     if (threadIdx.x == 0) trivial[p] = all ? 1u : 0u;
 }
 
+// Digit histograms of a sample of the keys: the 64-key rows r with r % rstride == 0, one
+// wave per row (8 waves per block). Planning only (key width, hybrid split): the counts
+// are not the sort's offsets.
+__global__ __launch_bounds__(512) void k_key_sample(const uint64_t *__restrict__ keys, uint32_t n, uint32_t rstride,
+                                                    uint32_t *__restrict__ hist, const KeyStatD *__restrict__ parts,
+                                                    uint32_t nparts, KeyStatD *__restrict__ st) {
+    __shared__ uint32_t h[8][256];
+    if (parts && blockIdx.x == 0) {  // combine the KeyStatD partials (512 threads, 8 waves)
+        __shared__ KeyStatD s_p[8];
+        uint64_t o = 0, a = ~0ull;
+        uint32_t tmin = 255u, tmax = 0u;
+        for (uint32_t b = threadIdx.x; b < nparts; b += 512) {
+            const KeyStatD q = parts[b];
+            o |= q.o;
+            a &= q.a;
+            tmin = min(tmin, q.tmin);
+            tmax = max(tmax, q.tmax);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            o |= (uint64_t)__shfl_xor((long long)o, off, 64);
+            a &= (uint64_t)__shfl_xor((long long)a, off, 64);
+            tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, off, 64));
+            tmax = max(tmax, (uint32_t)__shfl_xor((int)tmax, off, 64));
+        }
+        if (lane_id() == 0) s_p[threadIdx.x >> 6] = KeyStatD{o, a, tmin, tmax};
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < 8; ++w) {
+                o |= s_p[w].o;
+                a &= s_p[w].a;
+                tmin = min(tmin, s_p[w].tmin);
+                tmax = max(tmax, s_p[w].tmax);
+            }
+            *st = KeyStatD{o, a, tmin, tmax};
+        }
+    }
+    for (int x = threadIdx.x; x < 8 * 256; x += 512) (&h[0][0])[x] = 0;
+    __syncthreads();
+    const uint32_t nrows = (n + 63) / 64;
+    constexpr int KS_U = 8;  // rows in flight per wave (the loads are independent)
+    const uint32_t jstep = gridDim.x * 8;
+    for (uint32_t j0 = blockIdx.x * 8 + (threadIdx.x >> 6); (uint64_t)j0 * rstride < nrows; j0 += jstep * KS_U) {
+        uint64_t k[KS_U];
+        bool ok[KS_U];
+#pragma unroll
+        for (int u = 0; u < KS_U; ++u) {
+            const uint64_t i = ((uint64_t)(j0 + u * jstep) * rstride) * 64 + lane_id();
+            ok[u] = i < n;
+            k[u] = ok[u] ? keys[i] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < KS_U; ++u)
+            if (ok[u]) {
+#pragma unroll
+                for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(uint32_t)(k[u] >> (8 * p)) & 255u], 1u);
+            }
+    }
+    __syncthreads();
+    for (int x = threadIdx.x; x < 8 * 256; x += 512) {
+        const uint32_t v = (&h[0][0])[x];
+        if (v) atomicAdd(&hist[x], v);
+    }
+}
+
 __global__ void k_iota(uint32_t *v, uint32_t n) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = i;
 }
@@ -150,13 +218,38 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__
     }
 }
 
-// One block per digit d: cnt[d][t] -> exclusive prefix over tiles + goffs[d].
-__global__ __launch_bounds__(256) void k_rs_cscan(uint32_t *__restrict__ cnt, uint32_t ntiles,
-                                                  const uint32_t *__restrict__ goffs) {
+// One block per digit d: the digit's total over the tiles (the pass's digit bases without a
+// key histogram: KeyStats sorts).
+__global__ __launch_bounds__(256) void k_rs_dsum(const uint32_t *__restrict__ cnt, uint32_t ntiles,
+                                                 uint32_t *__restrict__ dtot) {
     __shared__ uint32_t s_red[4];
+    const uint32_t *row = cnt + (size_t)blockIdx.x * ntiles;
+    uint32_t v = 0;
+    for (uint32_t i = threadIdx.x; i < ntiles; i += 256) v += row[i];
+    uint32_t tot;
+    block_excl_scan<256>(v, &tot, s_red);
+    if (threadIdx.x == 0) dtot[blockIdx.x] = tot;
+}
+
+// One block per digit d: cnt[d][t] -> exclusive prefix over tiles + the digit base (goffs[d],
+// or with dtot the sum of the digit totals below d).
+__global__ __launch_bounds__(256) void k_rs_cscan(uint32_t *__restrict__ cnt, uint32_t ntiles,
+                                                  const uint32_t *__restrict__ goffs,
+                                                  const uint32_t *__restrict__ dtot) {
+    __shared__ uint32_t s_red[4];
+    __shared__ uint32_t s_base;
     const uint32_t d = blockIdx.x;
     uint32_t *row = cnt + (size_t)d * ntiles;
-    uint32_t carry = goffs[d];
+    uint32_t carry;
+    if (dtot) {
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<256>(dtot[threadIdx.x], &tot, s_red);
+        if (threadIdx.x == d) s_base = ex;
+        __syncthreads();
+        carry = s_base;
+    } else {
+        carry = goffs[d];
+    }
     for (uint32_t b = 0; b < ntiles; b += 256 * 4) {
         const uint32_t i0 = b + threadIdx.x * 4;
         uint32_t v[4], sum = 0;
@@ -490,7 +583,7 @@ struct HybridPlan {
     uint64_t gmask = 0;
 };
 
-static HybridPlan plan_hybrid(const uint32_t *hh, uint32_t n, const int *live, int nlive) {
+static HybridPlan plan_hybrid(const uint32_t *hh, uint32_t hn, uint32_t n, const int *live, int nlive) {
     HybridPlan hp;
     if (n < (1u << 20) || nlive < 3) return hp;
     const double need = std::log2((double)n) - HY_SLACK_BITS;
@@ -502,7 +595,7 @@ static HybridPlan plan_hybrid(const uint32_t *hh, uint32_t n, const int *live, i
         double H = 0;
         for (int d = 0; d < 256; ++d)
             if (hh[p * 256 + d]) {
-                const double f = hh[p * 256 + d] / (double)n;
+                const double f = hh[p * 256 + d] / (double)hn;
                 H -= f * std::log2(f);
             }
         acc += H;
@@ -518,34 +611,31 @@ static HybridPlan plan_hybrid(const uint32_t *hh, uint32_t n, const int *live, i
     return hp;
 }
 
-int key_hist8_async(sg_ctx *c, const uint64_t *keys, uint32_t n, const uint32_t **dev_hist) {
-    uint32_t *hist;
-    SG_TRY(slot(c, S_HIST, RS_MAXPASS * 256 * 2 + RS_MAXPASS, &hist));
-    SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
-    uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
-    if (hgrid > 1024) hgrid = 1024;
-    if (n) SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, 0, RS_MAXPASS, hist, 0u);
-    *dev_hist = hist;
+int key_sample_hist(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *dev_hist, uint32_t *sample_n,
+                    const KeyStatD *parts, uint32_t nparts, KeyStatD *st) {
+    *sample_n = 0;
+    if (n == 0) return SG_OK;
+    const uint32_t nrows = (n + 63) / 64;
+    // about 2^16 sampled keys: the plug-in entropy estimate's bias is ~0.003 bit per digit
+    // (the LDS atomics of 2^18 sampled keys cost 12 µs on 64 CUs)
+    uint32_t rs = 1;
+    while (rs < 1024 && (uint64_t)(nrows / (rs * 2)) * 64 >= (1u << 16)) rs *= 2;
+    const uint32_t srows = (nrows + rs - 1) / rs;
+    const uint32_t grid = std::min<uint32_t>((srows + 7) / 8, 64u);
+    SG_LAUNCH_B(c, "key_sample", 8.0 * srows * 64, k_key_sample, grid, 512, 0, keys, n, rs, dev_hist, parts,
+                nparts, st);
+    const uint32_t last = (srows - 1) * rs;  // the last sampled row may be partial
+    *sample_n = (srows - 1) * 64 + std::min<uint32_t>(64u, n - last * 64);
     return SG_OK;
 }
 
-int key_hist8(sg_ctx *c, const uint64_t *keys, uint32_t n, uint32_t *host_hist) {
-    uint32_t *hist;
-    SG_TRY(slot(c, S_HIST, RS_MAXPASS * 256 * 2 + RS_MAXPASS, &hist));
-    SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
-    uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
-    if (hgrid > 1024) hgrid = 1024;
-    if (n) SG_LAUNCH_B(c, "rs_hist", 8.0 * n, k_rs_hist, hgrid, RS_HBLOCK, 0, keys, n, 0, RS_MAXPASS, hist, 0u);
-    return ctx_readback(c, host_hist, hist, RS_MAXPASS * 256 * 4);
-}
-
-// host_hist (optional): the 8 digit histograms of `keys` over bits [0, 64), already on the
-// host (key_hist8, possibly adjusted by the caller) — then the trivial passes are known
-// without a read-back.
+// ks (optional, bits [0, 64)): the keys' varying bits (exact: the trivial passes are known
+// without a histogram pass or a read-back; each pass's digit bases then come from its own
+// tile counts) and sampled digit histograms (the hybrid plan).
 template <typename VT>
 static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt, VT *vals_alt,
                         uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
-                        VT **vals_out, const char *pass_name, const uint32_t *host_hist = nullptr,
+                        VT **vals_out, const char *pass_name, const KeyStats *ks = nullptr,
                         uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr) {
     if (lsort_err) *lsort_err = nullptr;
     *keys_out = keys;
@@ -553,20 +643,16 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     if (n == 0) return SG_OK;
     const int npasses = (end_bit - begin_bit + 7) / 8;
     if (npasses <= 0 || npasses > RS_MAXPASS) { set_error("radix_sort: bad bit range"); return SG_E_INVAL; }
-    if (host_hist && (begin_bit != 0 || npasses != RS_MAXPASS)) { set_error("radix_sort: histograms cover 64 bits"); return SG_E_INVAL; }
+    if (ks && (begin_bit != 0 || npasses != RS_MAXPASS)) { set_error("radix_sort: key stats cover 64 bits"); return SG_E_INVAL; }
     uint32_t *hist;
     SG_TRY(slot(c, S_HIST, RS_MAXPASS * 256 * 2 + RS_MAXPASS, &hist));
     uint32_t *offs = hist + RS_MAXPASS * 256;
     uint32_t *triv = offs + RS_MAXPASS * 256;
+    uint32_t *dtot = nullptr;  // KeyStats sorts: per-pass digit totals (in the histogram area)
     uint32_t trivial[RS_MAXPASS];
-    if (host_hist) {
-        SG_HIP(hipMemcpyAsync(hist, host_hist, RS_MAXPASS * 256 * 4, hipMemcpyHostToDevice, c->stream));
-        SG_LAUNCH(c, "rs_scan", k_rs_scan, npasses, 256, 0, hist, offs, triv, n);
-        for (int p = 0; p < npasses; ++p) {
-            trivial[p] = 0;
-            for (int d = 0; d < 256; ++d)
-                if (host_hist[p * 256 + d] == n) trivial[p] = 1;
-        }
+    if (ks) {
+        dtot = hist;
+        for (int p = 0; p < npasses; ++p) trivial[p] = ((ks->vary >> (8 * p)) & 0xffu) == 0;
     } else {
         SG_HIP(hipMemsetAsync(hist, 0, RS_MAXPASS * 256 * 4, c->stream));
         uint32_t hgrid = (n + RS_HBLOCK * 16 - 1) / (RS_HBLOCK * 16);
@@ -595,7 +681,7 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     // global passes over the top digits only, the rest sorted per group in LDS
     HybridPlan hp;
     if constexpr (sizeof(VT) == 8) {
-        if (host_hist && lsort_err && begin_bit == 0) hp = plan_hybrid(host_hist, n, live, nlive);
+        if (ks && ks->hist && ks->hist_n && lsort_err) hp = plan_hybrid(ks->hist, ks->hist_n, n, live, nlive);
     }
     const int *passes = hp.on ? hp.top : live;
     const int npass = hp.on ? hp.ntop : nlive;
@@ -604,7 +690,8 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
         const int shift = begin_bit + 8 * p;
         const uint32_t kw = q == 0 ? narrow_kw : 0u;  // the first pass narrows as it reads
         SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, grid, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, kw, xcd);
-        SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, offs + p * 256);
+        if (dtot) SG_LAUNCH(c, "rs_dsum", k_rs_dsum, 256, 256, 0, tcnt, ntiles, dtot);
+        SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, offs + p * 256, dtot);
         if constexpr (sizeof(VT) == 4) {
             if (iota_pending)
                 SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
@@ -657,9 +744,9 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
 
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out, const char *pass_name,
-                     const uint32_t *host_hist, uint32_t narrow_kw, uint32_t **lsort_err) {
+                     const KeyStats *ks, uint32_t narrow_kw, uint32_t **lsort_err) {
     return radix_sort_t<uint2>(c, keys, spans, keys_alt, spans_alt, n, begin_bit, end_bit, false, keys_out, spans_out,
-                               pass_name, host_hist, narrow_kw, lsort_err);
+                               pass_name, ks, narrow_kw, lsort_err);
 }
 
 }  // namespace sg

@@ -472,3 +472,44 @@ def test_hybrid_sort_overflow_and_ties(sg, shape):
             assert flags & 1
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("shape", ["rare", "tags", "prefix_rare"])
+def test_key_stats_rare_digits(sg, shape):
+    """The sort skips a digit pass only on the keys' exact varying bits (OR ^ AND gathered
+    with the common-prefix scan, or with the re-key at the prefix), never on the sampled
+    histograms: a digit that one record in 300K carries must still be sorted. rare: key
+    bytes 1-3 constant but for single records; tags: lengths 1-12 (the length tag varies,
+    also after narrowing); prefix_rare: every record starts "https://" (re-keyed at the
+    prefix) with the rare bytes after it. Equal to the oracle."""
+    import torch
+    rng = np.random.default_rng({"rare": 11, "tags": 12, "prefix_rare": 13}[shape])
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", dtype=np.uint8)
+    n = 300_000
+    if shape == "tags":
+        lens = rng.integers(1, 13, size=n)
+        body = alpha[rng.integers(0, 36, size=(n, 12))]
+        recs = [bytes(body[i, : lens[i]]) for i in range(n)]
+    else:
+        body = alpha[rng.integers(0, 36, size=(n, 14))]
+        body[:, 1:4] = ord("q")
+        for j, i in enumerate(rng.choice(n, size=6, replace=False)):
+            body[i, 1 + j % 3] = ord("a") + j  # a rare digit at bytes 1..3
+        body[rng.integers(0, n), 0] = ord("~")  # byte 0 varies: no common prefix there
+        recs = [bytes(r) for r in body]
+        if shape == "prefix_rare":
+            recs = [b"https://" + r for r in recs]
+    recs += recs[: n // 5]  # duplicates
+    rng.shuffle(recs)
+    cur = b"\n".join(recs) + b"\n"
+    prior = S.dedup(b"\n".join(recs[::3]) + b"\n")
+    dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+    dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        r = ctx.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+        eu, ef = S.dedup_diff(cur, prior)
+        assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+        assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+    finally:
+        ctx.close()
