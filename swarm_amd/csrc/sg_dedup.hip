@@ -1152,9 +1152,17 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // the key narrowing to kw bytes happens in the sort's first pass; with the key histograms
     // on the host the sort may finish its low digits per group in LDS (lerr: checked with
     // the group counts below, before anything trusts the order)
+    // segbad (a flag per position), then the counters read back together: the three list
+    // counters (zeroed with the head marks), the segment-head select's total, the local
+    // sort's overflow word
+    const size_t cnt_off = ((size_t)R + 15) & ~(size_t)15;
+    uint8_t *segbad;
+    SG_TRY(slot(c, S_BAD, cnt_off + 32, &segbad));
+    uint32_t *acnt = reinterpret_cast<uint32_t *>(segbad + cnt_off);
+    uint64_t *stot_at = reinterpret_cast<uint64_t *>(acnt + 4);
     uint32_t *lerr = nullptr;
     SG_TRY(radix_sort_spans(c, L.keys, L.spans, k2, v2, R, 0, 64, &K, &V, "rs_pass", ks,
-                            (base >> 16) < 7u ? base >> 16 : 0u, ks ? &lerr : nullptr));
+                            (base >> 16) < 7u ? base >> 16 : 0u, ks ? &lerr : nullptr, acnt + 6));
     if (lerr) c->last_flags |= 1u;
 
     // key0 groups -> brk; groups of > 64 records sharing 7 bytes -> refinement rounds
@@ -1166,12 +1174,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint32_t B = 0;
     uint32_t ns = 0, nb = 0;
     uint32_t *hs, *hb;
-    uint8_t *dup, *segbad;
+    uint8_t *dup;
     SG_TRY(slot(c, S_DUP, R, &dup));
-    // segbad (a flag per position) with the three list counters after it
-    const size_t cnt_off = ((size_t)R + 15) & ~(size_t)15;
-    SG_TRY(slot(c, S_BAD, cnt_off + 16, &segbad));
-    uint32_t *acnt = reinterpret_cast<uint32_t *>(segbad + cnt_off);
     SG_TRY(slot(c, S_SEL, (size_t)R / 2 + 16, &hs));
     SG_TRY(slot(c, S_R_VAL, (size_t)R / 17 + 16, &hb));
     const AdjLists AL{hs, hb, GS, GE, acnt, R / 2 + 16, R / 17 + 16, R / 64 + 16};
@@ -1189,7 +1193,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         else
             SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, (k_adjacent2<false, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
                         brk, R, dup, segbad, AL, base);
-        if (with_dup) SG_TRY(run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, &stot));
+        if (with_dup) SG_TRY(run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, &stot, stot_at));
         return SG_OK;
     };
     uint32_t lerr_v = 0;
@@ -1197,9 +1201,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // word with one host sync
     auto read_counts = [&](bool with_heads) -> int {
         uint8_t *pin = (uint8_t *)c->pinned;
-        SG_HIP(hipMemcpyAsync(pin, acnt, 12, hipMemcpyDeviceToHost, c->stream));
-        if (with_heads) SG_HIP(hipMemcpyAsync(pin + 16, stot, 8, hipMemcpyDeviceToHost, c->stream));
-        if (lerr) SG_HIP(hipMemcpyAsync(pin + 24, lerr, 4, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipMemcpyAsync(pin, acnt, 28, hipMemcpyDeviceToHost, c->stream));  // acnt | stot | lerr
         SG_HIP(hipStreamSynchronize(c->stream));
         uint32_t v[3];
         memcpy(v, pin, 12);
@@ -1315,8 +1317,10 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     bool prior_sorted = true;
     // dflag: [0] prior not strictly increasing, [1] common prefix length, then the cur keys'
     // KeyStatD from byte 0 ([4..10)) and after a rekey at the common prefix ([12..18))
+    // (the front of one slot with the sample histograms and the stat partials after it: the
+    // flags, the stats and the histograms come back in one copy)
     uint32_t *dflag;
-    SG_TRY(slot(c, S_M_CNT, 20, &dflag));
+    SG_TRY(slot(c, S_HIST, 32 + 8 * 256 + 2048 * sizeof(KeyStatD) / 4, &dflag));
     KeyStatD *st0 = reinterpret_cast<KeyStatD *>(dflag + 4), *st1 = reinterpret_cast<KeyStatD *>(dflag + 12);
     {
         uint32_t init[20] = {0u, 255u};
@@ -1331,6 +1335,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         else SG_TRY(run_lines(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp));
         const uint32_t R = Lp.n_rec;
         // keys from byte 0 decide sortedness exactly like keys from the common prefix would
+        // (a separate launch: fused into the prior's common-prefix scan, whose grid is capped
+        // for its atomics, the byte compares of equal keys ran 40 µs longer on C2)
         if (R > 1 && R < (1u << 30))
             SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_prior, Lp.spans, Lp.keys,
                         R, dflag, make_bk(0u, 7u));
@@ -1349,7 +1355,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint32_t g_cur = std::min<uint32_t>(grid_for(Lc.n_rec, 256), 512u);
     const uint32_t g_rekey = std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u);
     if (want_hist) {
-        SG_TRY(slot(c, S_HIST, 8 * 256 + 2048 * sizeof(KeyStatD) / 4, &shist));
+        shist = dflag + 32;
         parts = reinterpret_cast<KeyStatD *>(shist + 8 * 256);
         SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));
     }
@@ -1368,8 +1374,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     uint32_t fl[20] = {0u};
     auto read_stats = [&](uint32_t words) -> int {
         uint8_t *pin = (uint8_t *)c->pinned;
-        SG_HIP(hipMemcpyAsync(pin, dflag, 4 * words, hipMemcpyDeviceToHost, c->stream));
-        if (shist) SG_HIP(hipMemcpyAsync(pin + 128, shist, 8 * 256 * 4, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipMemcpyAsync(pin, dflag, shist ? 128 + 8 * 256 * 4 : 4 * words, hipMemcpyDeviceToHost, c->stream));
         SG_HIP(hipStreamSynchronize(c->stream));
         memcpy(fl, pin, 4 * words);
         if (shist) memcpy(hh, pin + 128, 8 * 256 * 4);

@@ -289,14 +289,23 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_count(Item item, uint32_t n, 
     __shared__ uint64_t s_red[EM_BLOCK / 64];
     const uint32_t base = blockIdx.x * EM_TILE;
     uint64_t sum = 0;
+    // every round's item first, then the stores: a cache store between two item loads kept
+    // the next round's (possibly aliasing) loads behind it, one latency per round
+    uint32_t s[EM_ROUNDS], l[EM_ROUNDS];
+    bool f[EM_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        const uint32_t i = base + r * EM_BLOCK + threadIdx.x;
+        s[r] = 0;
+        l[r] = 0;
+        f[r] = (i < n) && item(i, &s[r], &l[r]);
+    }
 #pragma unroll
     for (int r = 0; r < EM_ROUNDS; ++r) {
         const uint32_t i = base + r * EM_BLOCK + threadIdx.x;
         if (i < n) {
-            uint32_t s = 0, l = 0;
-            const bool f = item(i, &s, &l);
-            cache[i] = make_uint2(s, f ? l : EM_DROP);
-            sum += f ? (EM_ONE | (uint64_t)(l + 1u)) : 0ull;
+            cache[i] = make_uint2(s[r], f[r] ? l[r] : EM_DROP);
+            sum += f[r] ? (EM_ONE | (uint64_t)(l[r] + 1u)) : 0ull;
         }
     }
     sum = wave_sum(sum);

@@ -60,11 +60,12 @@ struct KeyStatD {
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out,
                      const char *pass_name = "rs_pass", const KeyStats *ks = nullptr,
-                     uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr);
+                     uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr, uint32_t *err_at = nullptr);
 // lsort_err (with ks->hist): allows the hybrid sort (global passes over the top digits, the
 // rest per group in LDS); *lsort_err is then the device word that turns nonzero when a group
 // did not fit the LDS — the pairs are a valid permutation but not sorted, and the caller must
-// sort them again with lsort_err = nullptr (null when the plain LSD sort ran).
+// sort them again with lsort_err = nullptr (null when the plain LSD sort ran). err_at: the
+// device word to use for it (e.g. beside the caller's other counters: one read-back).
 // Queue the digit histograms of a row sample of the keys into dev_hist (8 x 256 u32, zeroed
 // by the caller); *sample_n = the keys counted. With parts: the nparts per-block KeyStatD
 // partials of an earlier kernel are combined into *st in the same launch.

@@ -26,11 +26,17 @@ __global__ __launch_bounds__(SEL_BLOCK) void k_sel_count(Pred pred, uint32_t n, 
     const int t = threadIdx.x, lane = lane_id(), wid = t >> 6;
     const uint32_t base = blockIdx.x * SEL_TILE;
     uint64_t cnt = 0;
+    // every row's predicate first, then the ballots and mask stores: a store between two
+    // rows kept the next row's (possibly aliasing) loads behind it (one latency per row)
+    uint32_t p[SEL_ROWS];
 #pragma unroll
     for (int j = 0; j < SEL_ROWS; ++j) {
         const uint32_t i = base + j * SEL_BLOCK + t;
-        const uint32_t p = (i < n) ? pred(i) : 0u;
-        const uint64_t ma = __ballot(p & 1u), mb = __ballot(p & 2u);
+        p[j] = (i < n) ? pred(i) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < SEL_ROWS; ++j) {
+        const uint64_t ma = __ballot(p[j] & 1u), mb = __ballot(p[j] & 2u);
         if (lane == 0) {
             mA[(uint64_t)blockIdx.x * SEL_MASKS + j * 4 + wid] = ma;
             mB[(uint64_t)blockIdx.x * SEL_MASKS + j * 4 + wid] = mb;

@@ -17,7 +17,7 @@ static int run_select2(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint3
     uint64_t *tp;  // tot | pre | total | maskA | maskB
     SG_TRY(slot(c, S_COUNT, 2 * (size_t)ntiles + 4 + 2 * (size_t)ntiles * SEL_MASKS, &tp));
     uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
-    uint64_t *mA = total + 4, *mB = mA + (size_t)ntiles * SEL_MASKS;
+    uint64_t *mA = tp + 2 * (size_t)ntiles + 4, *mB = mA + (size_t)ntiles * SEL_MASKS;
     SG_LAUNCH(c, name, k_sel_count<Pred>, ntiles, SEL_BLOCK, 0, pred, n, mA, mB, tot);
     SG_TRY(tile_scan(c, tot, ntiles, pre, total));
     SG_LAUNCH(c, "select.apply", k_sel_apply, ntiles, SEL_BLOCK, 0, n, mA, mB, pre, outA, outB);
@@ -34,17 +34,17 @@ static int run_select2(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint3
 // given status slot, for the caller to read back together with other counts.
 template <class Pred>
 static int run_select2_nb(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint32_t *outA, uint32_t *outB,
-                          int status_slot, uint64_t **total_out) {
+                          int status_slot, uint64_t **total_out, uint64_t *total_at = nullptr) {
     const uint32_t ntiles = (n + SEL_TILE - 1) / SEL_TILE;
     uint64_t *tp;  // tot | pre | total | maskA | maskB
     SG_TRY(slot(c, status_slot, 2 * (size_t)std::max<uint32_t>(ntiles, 1) + 4 + 2 * (size_t)ntiles * SEL_MASKS, &tp));
-    uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
+    uint64_t *tot = tp, *pre = tp + ntiles, *total = total_at ? total_at : tp + 2 * (size_t)ntiles;
     *total_out = total;
     if (n == 0) {
         SG_HIP(hipMemsetAsync(total, 0, 8, c->stream));
         return SG_OK;
     }
-    uint64_t *mA = total + 4, *mB = mA + (size_t)ntiles * SEL_MASKS;
+    uint64_t *mA = tp + 2 * (size_t)ntiles + 4, *mB = mA + (size_t)ntiles * SEL_MASKS;
     SG_LAUNCH(c, name, k_sel_count<Pred>, ntiles, SEL_BLOCK, 0, pred, n, mA, mB, tot);
     SG_TRY(tile_scan(c, tot, ntiles, pre, total));
     SG_LAUNCH(c, "select.apply", k_sel_apply, ntiles, SEL_BLOCK, 0, n, mA, mB, pre, outA, outB);

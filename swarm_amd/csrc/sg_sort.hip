@@ -636,7 +636,7 @@ template <typename VT>
 static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt, VT *vals_alt,
                         uint32_t n, int begin_bit, int end_bit, bool iota_vals, uint64_t **keys_out,
                         VT **vals_out, const char *pass_name, const KeyStats *ks = nullptr,
-                        uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr) {
+                        uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr, uint32_t *err_at = nullptr) {
     if (lsort_err) *lsort_err = nullptr;
     *keys_out = keys;
     *vals_out = vals;
@@ -708,8 +708,8 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     }
     if constexpr (sizeof(VT) == 8) {
         if (hp.on) {
-            uint32_t *err;
-            SG_TRY(slot(c, S_LS_ERR, 1, &err));
+            uint32_t *err = err_at;
+            if (!err) SG_TRY(slot(c, S_LS_ERR, 1, &err));
             SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
             const uint32_t g = (n + LS_T - 1) / LS_T;
             uint32_t *bounds;
@@ -744,9 +744,9 @@ int radix_sort(sg_ctx *c, uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, ui
 
 int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt, uint2 *spans_alt, uint32_t n,
                      int begin_bit, int end_bit, uint64_t **keys_out, uint2 **spans_out, const char *pass_name,
-                     const KeyStats *ks, uint32_t narrow_kw, uint32_t **lsort_err) {
+                     const KeyStats *ks, uint32_t narrow_kw, uint32_t **lsort_err, uint32_t *err_at) {
     return radix_sort_t<uint2>(c, keys, spans, keys_alt, spans_alt, n, begin_bit, end_bit, false, keys_out, spans_out,
-                               pass_name, ks, narrow_kw, lsort_err);
+                               pass_name, ks, narrow_kw, lsort_err, err_at);
 }
 
 }  // namespace sg
