@@ -344,14 +344,27 @@ __global__ __launch_bounds__(256) void k_adjacent2(const uint8_t *__restrict__ S
 struct SegPred {
     const uint8_t *brk, *segbad;
     uint32_t n;
+    // Wave-cooperative (k_sel_count calls it with the wave's 64 lanes on 64 consecutive
+    // positions): the row's brk bytes and the 16 after it as two ballots, each lane's window
+    // a funnel shift of them — no per-lane 32-B window loads and SWAR reductions (those,
+    // loaded for every position so the rows could issue together, were 100+ VALU ops per
+    // position; behind a per-row branch, a latency chain). Lanes past n (a partial tile's
+    // inactive lanes) lie past the end, which the boundary rule treats as a segment end.
     __device__ uint32_t operator()(uint32_t i) const {
-        static_assert(SEG_SMALL == 16, "window of two 16-B loads");
-        if (!segbad[i]) return 0u;
-        const uint32_t a = (i + 1) & ~15u, sh = (i + 1) - a;
-        uint32_t m = swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a)) |
-                     (swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a + 16)) << 16);
-        if (n - a < 32u) m |= ~0u << (n - a);  // positions >= n end the segment
-        return ((m >> sh) & 0xffffu) ? 1u : 2u;
+        static_assert(SEG_SMALL == 16, "window of 16 positions");
+        const uint32_t lane = lane_id(), r0 = i - lane;
+        const uint32_t bad = segbad[i];
+        const uint64_t lo = __ballot(brk[i] != 0);
+        // every lane loads (lanes 16..63 repeat 0..15's bytes; past n a valid in-row byte)
+        // so the load is unconditional and the row's loads issue together
+        const uint32_t q = r0 + 64u + (lane & 15u);
+        const uint32_t bq = brk[q < n ? q : i];
+        const uint64_t hi = __ballot((lane < 16u) & ((q >= n) | (bq != 0u)));
+        const uint32_t sft = lane + 1u;  // positions i+1 .. i+16
+        uint32_t win = (uint32_t)((sft < 64u ? (lo >> sft) | (hi << (64u - sft)) : hi) & 0xffffu);
+        const uint32_t rem = n - i - 1u;  // positions after i inside the input
+        if (rem < 16u) win |= 0xffffu << rem;
+        return bad ? (win ? 1u : 2u) : 0u;
     }
 };
 
@@ -1247,8 +1260,15 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         SG_TRY(adjacent(false, true, Sb, SS));
         SG_TRY(read_counts(true));
     }
+    // the run-sort error word beside the unique emit's total (that slot at its final size
+    // now, so run_emit finds it in place): one copy brings both back
     uint32_t *err;
-    SG_TRY(slot(c, S_ERR, 4, &err));
+    {
+        const uint32_t ent = (R + EM_TILE - 1) / EM_TILE;
+        uint64_t *etp;
+        SG_TRY(slot(c, S_EMIT2, 2 * (size_t)ent + 4, &etp));
+        err = reinterpret_cast<uint32_t *>(etp + 2 * (size_t)ent + 1);
+    }
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
     if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
     if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
@@ -1282,8 +1302,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
                     0.0, dst ? dst->shift() : 0u));
     // the output count and the run-sort error word come back with one host sync
     uint8_t *pin = (uint8_t *)c->pinned;
-    SG_HIP(hipMemcpyAsync(pin, uc, 8, hipMemcpyDeviceToHost, c->stream));
-    if (nb) SG_HIP(hipMemcpyAsync(pin + 8, err, 4, hipMemcpyDeviceToHost, c->stream));
+    if (nb && reinterpret_cast<uint32_t *>(uc + 1) != err) { set_error("emit: status slot moved"); return SG_E_HIP; }
+    SG_HIP(hipMemcpyAsync(pin, uc, nb ? 12 : 8, hipMemcpyDeviceToHost, c->stream));
     SG_HIP(hipStreamSynchronize(c->stream));
     uint64_t tt = 0;
     memcpy(&tt, pin, 8);

@@ -161,13 +161,14 @@ int run_lines2(sg_ctx *c, const uint8_t *a, uint64_t na, const SlotSet &sa, Line
         pres[k] = tp + ntiles;
         totals[k] = tp + 2 * (size_t)ntiles;
         nts[k] = ntiles;
+        // both totals side by side in the first buffer's slot (its spare words): one copy back
+        if (k == 1) totals[1] = totals[0] + 1;
         SG_LAUNCH(c, "lines.count", k_lines_count, ntiles, LN_BLOCK, 0, bufs[k], ns[k], tot);
         SG_TRY(tile_scan(c, tot, ntiles, pres[k], totals[k]));
         prof_bytes(c, "lines.count", (double)ns[k]);
     }
     uint8_t *pin = (uint8_t *)c->pinned;
-    SG_HIP(hipMemcpyAsync(pin, totals[0], 8, hipMemcpyDeviceToHost, c->stream));
-    SG_HIP(hipMemcpyAsync(pin + 8, totals[1], 8, hipMemcpyDeviceToHost, c->stream));
+    SG_HIP(hipMemcpyAsync(pin, totals[0], 16, hipMemcpyDeviceToHost, c->stream));
     SG_HIP(hipStreamSynchronize(c->stream));
     for (int k = 0; k < 2; ++k) {
         uint64_t tv;

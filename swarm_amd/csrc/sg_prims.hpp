@@ -28,11 +28,17 @@ __global__ __launch_bounds__(SEL_BLOCK) void k_sel_count(Pred pred, uint32_t n, 
     uint64_t cnt = 0;
     // every row's predicate first, then the ballots and mask stores: a store between two
     // rows kept the next row's (possibly aliasing) loads behind it (one latency per row)
+    // (full tiles without the per-row bounds branch, so the rows' loads can issue together)
     uint32_t p[SEL_ROWS];
+    if (base + SEL_TILE <= n) {
 #pragma unroll
-    for (int j = 0; j < SEL_ROWS; ++j) {
-        const uint32_t i = base + j * SEL_BLOCK + t;
-        p[j] = (i < n) ? pred(i) : 0u;
+        for (int j = 0; j < SEL_ROWS; ++j) p[j] = pred(base + j * SEL_BLOCK + t);
+    } else {
+#pragma unroll
+        for (int j = 0; j < SEL_ROWS; ++j) {
+            const uint32_t i = base + j * SEL_BLOCK + t;
+            p[j] = (i < n) ? pred(i) : 0u;
+        }
     }
 #pragma unroll
     for (int j = 0; j < SEL_ROWS; ++j) {

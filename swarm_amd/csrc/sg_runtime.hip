@@ -376,15 +376,19 @@ __global__ __launch_bounds__(SEL_BLOCK) void k_sel_apply(uint32_t n, const uint6
                                                          const uint64_t *__restrict__ pre, uint32_t *__restrict__ outA,
                                                          uint32_t *__restrict__ outB) {
     __shared__ uint32_t s_ca[SEL_MASKS], s_cb[SEL_MASKS];
+    __shared__ uint64_t s_ma[SEL_MASKS], s_mb[SEL_MASKS];  // the tile's masks, read once
     const int t = threadIdx.x, lane = lane_id(), wid = t >> 6;
     const uint32_t base = blockIdx.x * SEL_TILE;
     const uint64_t *ma = mA + (uint64_t)blockIdx.x * SEL_MASKS;
     const uint64_t *mb = mB + (uint64_t)blockIdx.x * SEL_MASKS;
     if (t < 64) {
-        const uint32_t a = (uint32_t)__popcll(ma[t]), b = (uint32_t)__popcll(mb[t]);
+        const uint64_t xa = ma[t], xb = mb[t];
+        const uint32_t a = (uint32_t)__popcll(xa), b = (uint32_t)__popcll(xb);
         const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
         s_ca[t] = ia - a;
         s_cb[t] = ib - b;
+        s_ma[t] = xa;
+        s_mb[t] = xb;
     }
     __syncthreads();
     const uint64_t p0 = pre[blockIdx.x];
@@ -393,10 +397,10 @@ __global__ __launch_bounds__(SEL_BLOCK) void k_sel_apply(uint32_t n, const uint6
 #pragma unroll
     for (int j = 0; j < SEL_ROWS; ++j) {
         const uint32_t i = base + j * SEL_BLOCK + t;
-        const uint64_t xa = ma[j * 4 + wid];
+        const uint64_t xa = s_ma[j * 4 + wid];
         if ((xa >> lane) & 1ull) outA[preA + s_ca[j * 4 + wid] + (uint32_t)__popcll(xa & lt)] = i;
         if (outB) {
-            const uint64_t xb = mb[j * 4 + wid];
+            const uint64_t xb = s_mb[j * 4 + wid];
             if ((xb >> lane) & 1ull) outB[preB + s_cb[j * 4 + wid] + (uint32_t)__popcll(xb & lt)] = i;
         }
     }
