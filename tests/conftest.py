@@ -28,3 +28,17 @@ def load_golden(name):
 def has_gpu():
     from swarm_amd import device_count
     return device_count() > 0
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _release_device_memory():
+    """After each test module: drop its tensors and return torch's cached device memory, so
+    one pytest process running every GPU module does not carry one module's buffers into the
+    next (no effect on CPU-only runs: CUDA is never initialised here)."""
+    yield
+    import gc
+    gc.collect()
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():  # never initialises HIP itself
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
