@@ -341,10 +341,18 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
     uint64_t loc[EM_ROUNDS];
     uint64_t run = 0;
     uint32_t fmask = 0;
+    // the rounds' cache entries loaded together (clamped index, no bounds branch: a branch
+    // per round kept each load behind the previous round's wait)
+    uint2 cvr[EM_ROUNDS];
 #pragma unroll
     for (int r = 0; r < EM_ROUNDS; ++r) {
         const uint32_t i = wbase + r * 64u + lane;
-        const uint2 cv = (i < n) ? cache[i] : make_uint2(0u, EM_DROP);
+        cvr[r] = cache[i < n ? i : n - 1u];
+    }
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        const uint32_t i = wbase + r * 64u + lane;
+        const uint2 cv = (i < n) ? cvr[r] : make_uint2(0u, EM_DROP);
         const bool f = cv.y != EM_DROP;
         st[r] = cv.x;
         ln[r] = f ? cv.y : 0u;
