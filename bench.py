@@ -448,6 +448,7 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
     bytes), the case key0 routing could not divide."""
     import numpy as np
     import torch
+    import torch.distributed as dist
 
     import swarm_amd
     from swarm_amd import corpus, sharded
@@ -488,18 +489,21 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
         def step():
             if prior_parts is not None:
                 return sharded.dedup_diff_large(ctx, cur, (), splitters=split, prior_parts=prior_parts)
+            # (pu's '\n' part padding reads as empty lines, which are not records: A7 drops them)
             return sharded.dedup_diff_large(ctx, cur, [pu], splitters=split)
     else:
-        # N > 1 (or --c5-path rounds at N = 1: the per-rank compute of the N-GPU step with no
-        # exchange, for the modelled multi-GPU step in DESIGN.md §5)
+        # N > 1 (or --c5-path rounds at N = 1: the per-rank compute of the N-GPU step; with a
+        # 1-rank process group (--dist-backend nccl) its size exchange and per-round RCCL
+        # all-to-alls are issued too, force_exchange)
+        force = world == 1 and dist.is_initialized()
         rounds = D.all_max_int(D.plan_rounds(max(cur_bytes, 1), world)) if world > 1 else \
             D.plan_rounds(max(cur_bytes, 1), 8)
         split = D.agree_splitters(ctx, prior_raw, world * rounds)
-        prior_parts, prior_store = D.build_prior_rounds(ctx, prior_raw, split, rounds)
+        prior_parts, prior_store = D.build_prior_rounds(ctx, prior_raw, split, rounds, force_exchange=force)
         del prior_raw
 
         def step():
-            return D.dedup_diff_rounds_step(ctx, cur, prior_parts, split, rounds)
+            return D.dedup_diff_rounds_step(ctx, cur, prior_parts, split, rounds, force_exchange=force)
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup
     prior_bytes = int(prior_store.numel())
@@ -532,6 +536,23 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
         gu, gf, _ = sharded.dedup_diff_large(ctx, [dev_bytes(c0, dev)], [dev_bytes(p0, dev)], part_bytes=16 << 20)
         cpu["gpu_bit_exact_on_sample"] = (gu.cpu().numpy().tobytes() == eu and gf.cpu().numpy().tobytes() == ef)
         del gu, gf
+        # the whole step at full size (untimed): its unique and new outputs against the
+        # expectation computed from the drawn combo ids (oracle/c5_check.py: counts, record
+        # checksum, strict byte order)
+        from oracle import c5_check
+        tc = time.perf_counter()
+        u_full, f_full, _ = step()
+        pool2 = (corpus.ip_pool_torch(n_hosts + n_hosts // 10 + 1, seed=5, device=dev) if args.c5_data == "ips"
+                 else corpus.host_pool_torch(n_hosts + n_hosts // 10 + 1, seed=5, device=dev))
+        chk = c5_check.check_step(pool2, K, K, corpus.hostport_ids(per, 0, U, 100 + rank, device=dev),
+                                  corpus.hostport_ids(per, U // 10, U + U // 10, 900 + rank, device=dev),
+                                  u_full, f_full)
+        chk["seconds"] = round(time.perf_counter() - tc, 1)
+        chk["method"] = ("the full step's outputs parsed back into records vs the drawn (host, port) ids: "
+                         "distinct counts, sum of 64-bit record fingerprints, strict byte order")
+        cpu["full_size"] = chk
+        cpu["full_size_bit_exact"] = chk["full_size_bit_exact"]
+        del u_full, f_full, pool2
     out = None
     if rank == 0:
         pb = st["part_bytes"]
@@ -549,11 +570,12 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
                        "part_balance_max_over_mean": round(max(pb) * len(pb) / max(1, sum(pb)), 3) if pb else None,
                        "rerouted_parts": st["rerouted_parts"],
                        "setup_s": round(t_setup, 1),
-                       "parallelism": ("byte-range sharding, %d exchange rounds of RCCL all-to-all x%d "
-                                       "(backend %s, world size %d)" % (rounds, world, args.dist_backend, world))
-                                      if world > 1 else ("single GPU" if args.c5_path == "local" else
-                                                         "single GPU, the N-rank step's local path (%d rounds, "
-                                                         "no exchange)" % rounds)},
+                       "parallelism": ("byte-range sharding, %d exchange rounds of all-to-all x%d "
+                                       "(backend %s, world size %d)" % (rounds, world, dist.get_backend(),
+                                                                        dist.get_world_size()))
+                                      if dist.is_initialized() else ("single GPU" if args.c5_path == "local" else
+                                                                     "single GPU, the N-rank step's local path (%d "
+                                                                     "rounds, no exchange)" % rounds)},
             "gbps": round(step_bytes * args.steps / el / 1e9, 2),
             "hbm_frac_step": round(step_bytes * args.steps / el / 1e9 / (HBM_PEAK_GBS * world), 4),
             "records": {"in_rank0": st["in_records"], "unique_rank0": st["uniq_records"],
@@ -1132,6 +1154,12 @@ def init_dist(args):
         world = dist.get_world_size()
     else:
         torch.cuda.set_device(0)
+        if args.workload == "c5" and args.c5_path == "rounds" and args.dist_backend:
+            # a 1-rank process group: the rounds step issues its collectives at world size 1
+            # (on nccl = RCCL, the device-tensor all-to-all path of the N-rank step)
+            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            dist.init_process_group(args.dist_backend, rank=0, world_size=1,
+                                    init_method="tcp://127.0.0.1:%d" % free_port())
     return world, rank, local, torch.device("cuda", local)
 
 
@@ -1207,7 +1235,7 @@ def main():
         if rank == 0:
             print(json.dumps(line), flush=True)
         ctx.close()
-        if world > 1:
+        if dist.is_initialized():
             dist.destroy_process_group()
         return 0
 

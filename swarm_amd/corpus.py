@@ -456,6 +456,24 @@ def ip_pool_torch(n_hosts: int, seed: int = 5, device="cuda", chunk: int = 1 << 
     return torch.cat(mats), torch.cat(lens)
 
 
+def hostport_ids(n: int, lo: int, hi: int, seed: int, per_piece: int = 50_000_000, device="cuda"):
+    """The combo ids hostport_pieces draws (uniform in [lo, hi), one torch.Generator seeded
+    with `seed`), yielded piece by piece: the same stream for the same arguments."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    for s in range(0, n, per_piece):
+        m = min(per_piece, n - s)
+        yield torch.randint(lo, hi, (m,), generator=g, device=device, dtype=torch.int64)
+
+
+def hostport_port(c, ports_per_host: int | None = None):
+    """Port index (into PORTS) of combo ids c: with k = ports_per_host slots per host, a hash
+    of the combo (a host keeps a few open ports); without it, c % len(PORTS)."""
+    P = len(PORTS)
+    return (c % P) if ports_per_host is None else ((_tmix(c * 0x2545F4914F6CDD1D) & 0x7FFFFFFF) % P)
+
+
 def hostport_pieces(pool, n: int, lo: int, hi: int, seed: int, per_piece: int = 50_000_000,
                     ports_per_host: int | None = None):
     """n 'host:port' records ('\\n'-terminated) for combo ids drawn uniformly from [lo, hi),
@@ -478,15 +496,12 @@ def hostport_pieces(pool, n: int, lo: int, hi: int, seed: int, per_piece: int = 
     W = mat.shape[1]
     if (hi - 1) // K >= mat.shape[0]:  # host ids index the pool on the GPU: check here
         raise ValueError("combo ids up to %d need %d hosts; the pool has %d" % (hi - 1, (hi - 1) // K + 1, mat.shape[0]))
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
     out = []
     cols = torch.arange(W + 8, device=dev)
-    for s in range(0, n, per_piece):
-        m = min(per_piece, n - s)
-        c = torch.randint(lo, hi, (m,), generator=g, device=dev, dtype=torch.int64)
+    for c in hostport_ids(n, lo, hi, seed, per_piece, dev):
+        m = c.numel()
         h = c // K
-        p = (c % P) if ports_per_host is None else ((_tmix(c * 0x2545F4914F6CDD1D) & 0x7FFFFFFF) % P)
+        p = hostport_port(c, ports_per_host)
         rows = torch.zeros((m, W + 8), dtype=torch.uint8, device=dev)
         rows[:, :W] = mat[h]
         hl = lens[h].to(torch.int64)

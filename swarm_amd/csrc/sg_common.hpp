@@ -73,6 +73,7 @@ enum Slot : int {
     S_PT_SP, S_PT_KEYS,             // piece partition: spans and parts kept from pass 1 for pass 2
     S_PT_RCNT, S_PT_RPRE, S_PT_SPOUT, S_PT_KOUT,  // piece partition: the parts' record spans/keys out
     S_LS_ERR, S_LS_BOUNDS,  // hybrid radix sort: overflow flag, local-sort tile bounds
+    S_LS_LIST, S_LF_OFF, S_LF_KEY, S_LF_KEY2, S_LF_VAL, S_LF_VAL2, S_LF_POS,  // its overflow fix-up
     S_NSLOTS
 };
 
@@ -98,6 +99,13 @@ struct sg_ctx {
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
     uint64_t pt_keep_recs = 0;  // piece partition: records the last call kept between its passes
+    // the last hybrid radix sort's local-sort plan (lsort_fixup redoes its flagged tiles)
+    struct LsLast {
+        bool on = false;
+        uint64_t gmask = 0;
+        uint32_t lpos = 0, nloc = 0, ntiles = 0;
+        uint32_t *bounds = nullptr;
+    } ls_last;
     // pinned staging for host-to-device uploads on the context stream (ctx_upload): grown on
     // demand; up_ev marks the last upload's copy so the buffer is not rewritten under it
     void *up_pin = nullptr;

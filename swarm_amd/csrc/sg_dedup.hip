@@ -1234,14 +1234,26 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // count comes back (one host sync for everything); when big groups exist (the 7-byte key
     // was kept: low-entropy text) the groups are marked first and compared after refinement.
     const bool speculate = (base >> 16) < 7u;
+    bool fix_tried = false;
     for (;;) {
         SG_TRY(adjacent(true, speculate, d_buf, V));
         SG_TRY(read_counts(speculate));
         if (!lerr_v) break;
-        // a group outgrew the local sort's LDS (the pairs are intact, unsorted there): the
-        // plain LSD sort of the same pairs (keys already narrowed, histograms unchanged)
         uint64_t *Ka = (K == L.keys) ? k2 : L.keys;
         uint2 *Va = (V == L.spans) ? v2 : L.spans;
+        if (!fix_tried) {
+            // a group outgrew the local sort's LDS (the pairs are intact, unsorted there): its
+            // tiles again from the local sort's input (Ka, Va still hold it), with the groups
+            // too large for one block sorted by one radix sort of their members only (a record
+            // repeated thousands of times), then the adjacent pass again
+            fix_tried = true;
+            SG_TRY(lsort_fixup(c, Ka, Va, K, V, R));
+            SG_HIP(hipMemsetAsync(lerr, 0, 4, c->stream));
+            c->last_flags |= 4u;
+            continue;
+        }
+        // (not reached unless the fix-up flags again) the plain LSD sort of the same pairs
+        // (keys already narrowed, histograms unchanged)
         SG_TRY(radix_sort_spans(c, K, V, Ka, Va, R, 0, 64, &K, &V, "rs_pass", ks, 0u, nullptr));
         lerr = nullptr;
         c->last_flags |= 2u;

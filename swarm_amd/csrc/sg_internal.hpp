@@ -66,6 +66,11 @@ int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt
 // did not fit the LDS — the pairs are a valid permutation but not sorted, and the caller must
 // sort them again with lsort_err = nullptr (null when the plain LSD sort ran). err_at: the
 // device word to use for it (e.g. beside the caller's other counters: one read-back).
+// The hybrid sort's flagged tiles (a group of equal top digits larger than one block's LDS),
+// redone from the local sort's input (Kin, Vin: the pairs after the global passes) into
+// (Ko, Vo): windows of whole groups in LDS again, the big groups' members by one stable
+// radix sort on (group, local digits). Uses the ctx's last hybrid plan (c->ls_last).
+int lsort_fixup(sg_ctx *c, const uint64_t *Kin, const uint2 *Vin, uint64_t *Ko, uint2 *Vo, uint32_t n);
 // Queue the digit histograms of a row sample of the keys into dev_hist (8 x 256 u32, zeroed
 // by the caller); *sample_n = the keys counted. With parts: the nparts per-block KeyStatD
 // partials of an earlier kernel are combined into *st in the same launch.

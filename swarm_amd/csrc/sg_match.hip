@@ -228,6 +228,8 @@ static int build_ac(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint3
 // a set bit is confirmed against the bucket's entry fingerprints (rank + CSR), then the
 // whole pattern is byte-compared.
 constexpr uint32_t LIT_CLASSES = 6;
+// Scheme choice (dev_match): one verified candidate costs about LIT_KAPPA LDS bitmap probes.
+constexpr double LIT_KAPPA = 24.0;
 constexpr uint32_t LIT_J = 5;  // the joint class
 __host__ __device__ constexpr uint32_t lit_len(uint32_t c) { return c < 3 ? c + 1 : (c == 3 ? 4 : (c == 4 ? 8 : 5)); }
 // class-set templates of k_lit_scan: two-class {4-7, 8+}, {3, 4-7, 8+}, all; joint {J},
@@ -814,8 +816,10 @@ __device__ __forceinline__ void lit_emit(const Args &a, Push &push, uint32_t rec
 // then compacted into an LDS queue and pass 2 spreads them over all lanes: confirm against
 // the bucket's entry fingerprints, then byte-compare the pattern (16-B rows from L2, text
 // from the LDS tile). Hits go through a per-block LDS buffer flushed with one atomic.
-template <int BLK, int BPT, uint32_t CM>
-__global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
+// COUNT (the scheme trial, k_lit_trial): pass 1 only; each tile adds its candidate count to
+// a.hit_count (deterministic, unlike a timing) and nothing else is written.
+template <int BLK, int BPT, uint32_t CM, bool COUNT>
+__device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
     constexpr int TILE = BLK * BPT;
     constexpr int NW = BPT / 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -990,6 +994,11 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
         for (uint32_t c = 0; c < LIT_CLASSES; ++c) ncand += (uint32_t)__popcll(cand[c]);
         uint32_t qtot;
         const uint32_t qex = block_excl_scan<BLK>(ncand, &qtot, s_red);
+        if constexpr (COUNT) {
+            if (t == 0 && qtot) atomicAdd(a.hit_count, qtot);
+            __syncthreads();  // the tile buffers are rewritten by the next tile
+            continue;
+        }
         const uint32_t lrec0 = excl;  // tile-local index of this thread's first record start
         for (uint32_t r0 = 0; r0 < qtot; r0 += LS_Q) {
             uint32_t qi = qex;
@@ -1106,6 +1115,18 @@ __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
         __syncthreads();
         flush(tile + gridDim.x >= a.n_tiles);
     }
+}
+
+template <int BLK, int BPT, uint32_t CM>
+__global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
+    lit_scan_body<BLK, BPT, CM, false>(a);
+}
+
+// The class-scheme trial (candidates counted over the first tiles): its own symbol, so kernel
+// statistics and PMC passes of k_lit_scan hold the real scans only.
+template <int BLK, int BPT, uint32_t CM>
+__global__ __launch_bounds__(BLK) void k_lit_trial(LitArgs a) {
+    lit_scan_body<BLK, BPT, CM, true>(a);
 }
 
 // LDS bytes of k_lit_scan's dynamic tables for a filter (entries in LDS when they fit).
@@ -1751,19 +1772,27 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
                 default: return launch(k27, blk);
             }
         };
-#define SG_LIT_KERNELS(B, P) k_lit_scan<B, P, 0x18u>, k_lit_scan<B, P, 0x1Cu>, k_lit_scan<B, P, 0x1Fu>, \
-                             k_lit_scan<B, P, 0x20u>, k_lit_scan<B, P, 0x24u>, k_lit_scan<B, P, 0x27u>
-        if (ls_block == 512 && bpt == 16) SG_TRY(by_tmpl(SG_LIT_KERNELS(512, 16), 512));
-        else if (ls_block == 512 && bpt == 32) SG_TRY(by_tmpl(SG_LIT_KERNELS(512, 32), 512));
-        else if (ls_block == 256 && bpt == 32) SG_TRY(by_tmpl(SG_LIT_KERNELS(256, 32), 256));
-        else if (ls_block == 256 && bpt == 64) SG_TRY(by_tmpl(SG_LIT_KERNELS(256, 64), 256));
+#define SG_LIT_KERNELS(K, B, P) K<B, P, 0x18u>, K<B, P, 0x1Cu>, K<B, P, 0x1Fu>, K<B, P, 0x20u>, K<B, P, 0x24u>, \
+                                K<B, P, 0x27u>
+#define SG_LIT_GEOMS(K)                                                                             \
+        if (ls_block == 512 && bpt == 16) SG_TRY(by_tmpl(SG_LIT_KERNELS(K, 512, 16), 512));         \
+        else if (ls_block == 512 && bpt == 32) SG_TRY(by_tmpl(SG_LIT_KERNELS(K, 512, 32), 512));    \
+        else if (ls_block == 256 && bpt == 32) SG_TRY(by_tmpl(SG_LIT_KERNELS(K, 256, 32), 256));    \
+        else if (ls_block == 256 && bpt == 64) SG_TRY(by_tmpl(SG_LIT_KERNELS(K, 256, 64), 256));    \
         else { set_error("k_lit_scan: unsupported tile geometry"); return SG_E_INVAL; }
+        if (trial_tiles) { SG_LIT_GEOMS(k_lit_trial) } else { SG_LIT_GEOMS(k_lit_scan) }
+#undef SG_LIT_GEOMS
 #undef SG_LIT_KERNELS
         return SG_OK;
     };
     // The class scheme of a filter (two-class or joint, see build_lit): decided once per
-    // matcher, by timing both over the first tiles of the first input large enough to tell
-    // (until then the two-class scheme runs).
+    // matcher, on the first input large enough to tell (until then the two-class scheme runs),
+    // by a cost model over DETERMINISTIC counts: both schemes' probe pass runs over the first
+    // tiles counting candidates only (k_lit_trial), and
+    //   cost = LDS probes per position x positions + LIT_KAPPA x candidates,
+    // a candidate (queue slot, bucket record, fingerprint, byte verify) costing about LIT_KAPPA
+    // probes (fitted on C3, X1, C4 and the fields JSON: DESIGN.md §4). The same input always
+    // picks the same scheme; SG_LIT_SCHEME=0/1 forces one.
     auto scheme = [&](const sg_matcher::Lit &two, const sg_matcher::Lit &joint, std::atomic<int> &mode,
                       const uint32_t *fo, const uint32_t *fp) -> const sg_matcher::Lit & {
         const int forced = sw_lit_scheme();
@@ -1772,26 +1801,21 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         constexpr uint32_t TRIAL_TILES = 2048, MIN_TILES = 1024;
         if (m < 0 && L.n_tiles >= MIN_TILES) {
             const uint32_t tt = std::min<uint32_t>(L.n_tiles, TRIAL_TILES);
-            hipEvent_t ev[3];
-            for (auto &e : ev) (void)hipEventCreate(&e);
-            float ms[2] = {0.f, 0.f};
-            bool ok = true;
-            for (int rep = 0; rep < 2 && ok; ++rep) {  // the first round warms caches
-                (void)hipEventRecord(ev[0], c->stream);
-                ok = run_lit("lit_trial", two, nullptr, cnt + 4, 0u, fo, fp, tt) == SG_OK;
-                (void)hipEventRecord(ev[1], c->stream);
-                ok = ok && run_lit("lit_trial", joint, nullptr, cnt + 4, 0u, fo, fp, tt) == SG_OK;
-                (void)hipEventRecord(ev[2], c->stream);
-                ok = ok && hipEventSynchronize(ev[2]) == hipSuccess;
-                if (ok && rep == 1) {
-                    (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
-                    (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
-                }
-            }
-            for (auto &e : ev) (void)hipEventDestroy(e);
+            bool ok = hipMemsetAsync(cnt + 4, 0, 8, c->stream) == hipSuccess;
+            ok = ok && run_lit("lit_trial", two, nullptr, cnt + 4, 0u, fo, fp, tt) == SG_OK;
+            ok = ok && run_lit("lit_trial", joint, nullptr, cnt + 5, 0u, fo, fp, tt) == SG_OK;
+            uint32_t cc[2] = {0u, 0u};
+            ok = ok && ctx_readback(c, cc, cnt + 4, 8) == SG_OK;
             if (ok) {
-                m = ms[1] < ms[0] ? 1 : 0;
+                const double P = std::min<double>((double)tt * L.tile_bytes, (double)n);
+                const double c2 = __builtin_popcount(two.tmpl) * P + LIT_KAPPA * cc[0];
+                const double cj = __builtin_popcount(joint.tmpl) * P + LIT_KAPPA * cc[1];
+                m = cj < c2 ? 1 : 0;
                 mode.store(m);
+                if (sw_lit_trial_log())
+                    fprintf(stderr, "sg lit scheme: positions %.0f cand two %u (%u probes) joint %u (%u probes) -> %s\n", P,
+                            cc[0], (unsigned)__builtin_popcount(two.tmpl), cc[1],
+                            (unsigned)__builtin_popcount(joint.tmpl), m ? "joint" : "two");
             }
         }
         return m == 1 ? joint : two;

@@ -2,6 +2,7 @@
 //
 // Design and measurements: the block comment at the top of namespace sg below.
 #include "sg_internal.hpp"
+#include "sg_prims_host.hpp"
 
 #include <stdlib.h>
 
@@ -426,31 +427,28 @@ __global__ __launch_bounds__(256) void k_rs_lbounds(const uint64_t *__restrict__
 }
 
 // lpos: the local key's digit positions (byte q of lpos = key byte of local digit q, LSD
-// order), nloc of them. A tile holds several groups: its pairs are sorted by the local key,
-// then (stable) by their group ordinal in the tile (1 or 2 more digits), which restores the
-// groups' order with each group sorted inside.
-__global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
-                                                       uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t n,
-                                                       uint64_t gmask, uint32_t lpos, uint32_t nloc,
-                                                       const uint32_t *__restrict__ bounds, uint32_t *__restrict__ err) {
-    __shared__ uint32_t s_key[LS_CAP];
-    __shared__ uint32_t s_ig[LS_CAP];  // tile offset | group ordinal << 16
-    __shared__ uint32_t s_wh[LS_BLOCK / 64][256];
-    __shared__ uint32_t s_dstart[256];
-    __shared__ uint32_t s_red[LS_BLOCK / 64];
-    __shared__ uint32_t s_bits[2][LS_BLOCK / 64];
+// order), nloc of them. A window holds several groups: its pairs are sorted by the local key,
+// then (stable) by their group ordinal in the window (1 or 2 more digits), which restores the
+// groups' order with each group sorted inside. Whole block, uniform call; [s, s + nt) holds
+// whole groups and nt <= LS_CAP.
+struct LsShared {
+    uint32_t key[LS_CAP];
+    uint32_t ig[LS_CAP];  // window offset | group ordinal << 16
+    uint32_t wh[LS_BLOCK / 64][256];
+    uint32_t dstart[256];
+    uint32_t red[LS_BLOCK / 64];
+    uint32_t bits[2][LS_BLOCK / 64];
+};
+
+__device__ __forceinline__ void ls_sort_window(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
+                                               uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t s,
+                                               uint32_t nt, uint64_t gmask, uint32_t lpos, uint32_t nloc,
+                                               LsShared &sh_) {
+    uint32_t *s_key = sh_.key, *s_ig = sh_.ig, *s_dstart = sh_.dstart, *s_red = sh_.red;
+    auto &s_wh = sh_.wh;
+    auto &s_bits = sh_.bits;
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
-    const uint32_t t = blockIdx.x;
-    const uint32_t b0 = bounds[t], b1 = bounds[t + 1];
-    const uint32_t s = b0 & 0x7fffffffu, e = max(b1 & 0x7fffffffu, s);
-    const uint32_t nt = e - s;
-    if (nt == 0) return;
-    if (nt > (uint32_t)LS_CAP || !(b0 >> 31) || !(b1 >> 31)) {
-        // a group larger than the LDS: keep the pairs (a valid permutation), flag the sort
-        for (uint32_t i = s + tid; i < e; i += LS_BLOCK) { Ko[i] = K[i]; Vo[i] = V[i]; }
-        if (tid == 0) atomicOr(err, 1u);
-        return;
-    }
+    __syncthreads();  // a previous window of this block may still read the shared arrays
     for (int x = tid; x < (LS_BLOCK / 64) * 256; x += LS_BLOCK) (&s_wh[0][0])[x] = 0;
     // touch the tile's spans now (one load per 128-B line): the sorted-order gather at the
     // end then hits L2 instead of waiting on HBM after the last pass
@@ -569,6 +567,147 @@ __global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restric
     }
     asm volatile("" ::"v"(touch));  // keeps the touch load (its result is not needed)
 }
+
+// Block-wide max of one value per thread (every thread gets the result).
+__device__ __forceinline__ uint32_t ls_blk_max(uint32_t v, uint32_t *s_agg) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    __syncthreads();
+    if (lane_id() == 0) s_agg[threadIdx.x >> 6] = v;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < LS_BLOCK / 64; ++w) v = max(v, s_agg[w]);
+    return v;
+}
+
+__global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
+                                                       uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t n,
+                                                       uint64_t gmask, uint32_t lpos, uint32_t nloc,
+                                                       const uint32_t *__restrict__ bounds, uint32_t *__restrict__ err) {
+    __shared__ LsShared sh_;
+    const uint32_t t = blockIdx.x;
+    const uint32_t b0 = bounds[t], b1 = bounds[t + 1];
+    const uint32_t s = b0 & 0x7fffffffu, e = max(b1 & 0x7fffffffu, s);
+    const uint32_t nt = e - s;
+    if (nt == 0) return;
+    if (nt > (uint32_t)LS_CAP || !(b0 >> 31) || !(b1 >> 31)) {
+        // a group larger than the LDS: keep the pairs (a valid permutation), flag the tile;
+        // the caller then runs k_rs_lsort_fix over the flagged tiles (lsort_fixup)
+        for (uint32_t i = s + threadIdx.x; i < e; i += LS_BLOCK) { Ko[i] = K[i]; Vo[i] = V[i]; }
+        if (threadIdx.x == 0) atomicOr(err, 1u);
+        return;
+    }
+    ls_sort_window(K, V, Ko, Vo, s, nt, gmask, lpos, nloc, sh_);
+}
+
+// The tiles k_rs_lsort could not sort (a group of equal top digits larger than the LDS lies
+// in them, or the tile edge cuts one), redone from the same input: windows of whole groups
+// (<= LS_CAP pairs) are sorted in LDS as usual; every group too large for a window ("big
+// group", e.g. one record repeated thousands of times) is copied and listed (gs, ge: its
+// position range, appended by the block that holds its first position; the blocks its tail
+// reaches skip it), and lsort_fixup sorts the listed groups' members by one global radix
+// sort on (group, local digits). Runs only after a flagged local sort (no cost otherwise).
+__global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort_fix(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
+                                                           uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t n,
+                                                           uint64_t gmask, uint32_t lpos, uint32_t nloc,
+                                                           const uint32_t *__restrict__ bounds, uint32_t *__restrict__ gs,
+                                                           uint32_t *__restrict__ ge, uint32_t cap, uint32_t *__restrict__ cnt) {
+    __shared__ LsShared sh_;
+    __shared__ uint32_t s_agg[LS_BLOCK / 64];
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    const uint32_t b0 = bounds[t], b1 = bounds[t + 1];
+    const uint32_t s = b0 & 0x7fffffffu, e = max(b1 & 0x7fffffffu, s);
+    if (e - s == 0 || !(e - s > (uint32_t)LS_CAP || !(b0 >> 31) || !(b1 >> 31))) return;  // sorted by k_rs_lsort
+    const bool e_real = (b1 >> 31) != 0;
+    auto is_head = [&](uint32_t i) -> bool { return i >= n || ((K[i] ^ K[i - 1]) & gmask) != 0; };
+    // the first group start in [from, lim) (lim when none); from >= 1
+    auto first_head = [&](uint32_t from, uint32_t lim) -> uint32_t {
+        for (uint32_t b = from; b < lim; b += LS_BLOCK) {
+            const uint32_t i = b + tid;
+            const uint32_t m = ~ls_blk_max((i < lim && is_head(i)) ? ~i : 0u, s_agg);
+            if (m != 0xffffffffu) return m;
+        }
+        return lim;
+    };
+    uint32_t p = s;
+    bool p_real = (b0 >> 31) != 0;
+    while (p < e) {
+        if (!p_real) {  // the tail of a big group listed by an earlier block
+            const uint32_t q = first_head(p + 1, e);
+            p = q;
+            p_real = q < e || e_real;
+            continue;
+        }
+        uint32_t h;
+        if (e - p <= (uint32_t)LS_CAP && e_real) {
+            h = e;
+        } else {
+            const uint32_t lim = min(p + (uint32_t)LS_CAP, e);  // window ends: group starts in (p, lim]
+            uint32_t best = 0;
+            for (uint32_t i = p + 1 + tid; i <= lim; i += LS_BLOCK)
+                if (i == e ? e_real : is_head(i)) best = max(best, i);
+            h = ls_blk_max(best, s_agg);
+        }
+        if (h > p) {
+            ls_sort_window(K, V, Ko, Vo, p, h - p, gmask, lpos, nloc, sh_);
+            p = h;
+            continue;
+        }
+        // a big group starts at p: its end may lie in a later tile
+        const uint32_t q = first_head(p + (uint32_t)LS_CAP + 1u, n);
+        for (uint32_t i = p + tid; i < q; i += LS_BLOCK) { Ko[i] = K[i]; Vo[i] = V[i]; }
+        if (tid == 0) {
+            const uint32_t k = atomicAdd(cnt, 1u);
+            if (k < cap) { gs[k] = p; ge[k] = q; }
+        }
+        p = q;  // >= e ends the tile
+    }
+}
+
+// Big groups -> member rows: row j -> its group g (goff: exclusive row offsets), position
+// gs[g] + (j - goff[g]), key = g << 32 | the position's local digits (as k_rs_lsort packs
+// them). One wave per 1024 consecutive rows (groups hold > LS_CAP rows).
+__global__ __launch_bounds__(256) void k_lfix_expand(const uint64_t *__restrict__ K, const uint32_t *__restrict__ gs,
+                                                     const uint64_t *__restrict__ goff, uint32_t B, uint32_t M,
+                                                     uint32_t lpos, uint32_t nloc, uint64_t *__restrict__ RK,
+                                                     uint32_t *__restrict__ RP) {
+    const uint32_t j0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 1024u;
+    if (j0 >= M) return;
+    uint32_t g = 0, hi = B;  // last g with goff[g] <= j0
+    while (hi - g > 1) {
+        const uint32_t mid = (g + hi) >> 1;
+        if (goff[mid] <= j0) g = mid; else hi = mid;
+    }
+    const uint32_t je = min(M, j0 + 1024u);
+    for (uint32_t j = j0 + lane_id(); j < je; j += 64) {
+        while (g + 1 < B && goff[g + 1] <= j) ++g;
+        const uint32_t pos = gs[g] + (j - (uint32_t)goff[g]);
+        const uint64_t k = K[pos];
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (q < (int)nloc) v |= (uint32_t)((k >> (8 * ((lpos >> (8 * q)) & 255u))) & 255u) << (8 * q);
+        RK[j] = ((uint64_t)g << 32) | v;
+        RP[j] = pos;
+    }
+}
+
+// Sorted rows -> the big groups' positions: row j's position takes the pair of the row that
+// sorted to j (rows are group-major, so row j's position lies in its sorted group).
+__global__ void k_lfix_apply(const uint64_t *__restrict__ K, const uint2 *__restrict__ V, const uint32_t *__restrict__ RP,
+                             const uint32_t *__restrict__ perm, uint32_t M, uint64_t *__restrict__ Ko,
+                             uint2 *__restrict__ Vo) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= M) return;
+    const uint32_t src = RP[perm[j]];
+    Ko[RP[j]] = K[src];
+    Vo[RP[j]] = V[src];
+}
+
+struct LfixSizeFn {
+    const uint32_t *gs, *ge;
+    __device__ uint64_t operator()(uint32_t g) const { return (uint64_t)(ge[g] - gs[g]); }
+};
 
 // Host plan: the top live digits (in descending significance) until their entropy leaves
 // groups of about 2^HY_SLACK_BITS pairs; hybrid only when 2..4 live digits remain below
@@ -718,6 +857,12 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
             // model: key read, key + span fetched in sorted order, both written
             SG_LAUNCH_B(c, "rs_lsort", 40.0 * n, k_rs_lsort, g, LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask, hp.lpos, hp.nloc,
                         bounds, err);
+            c->ls_last.on = true;
+            c->ls_last.gmask = hp.gmask;
+            c->ls_last.lpos = hp.lpos;
+            c->ls_last.nloc = hp.nloc;
+            c->ls_last.ntiles = g;
+            c->ls_last.bounds = bounds;
             uint64_t *tk = ck; ck = ak; ak = tk;
             VT *tv = cv; cv = av; av = tv;
             *lsort_err = err;
@@ -732,6 +877,41 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     }
     *keys_out = ck;
     *vals_out = cv;
+    return SG_OK;
+}
+
+int lsort_fixup(sg_ctx *c, const uint64_t *Kin, const uint2 *Vin, uint64_t *Ko, uint2 *Vo, uint32_t n) {
+    const auto &P = c->ls_last;
+    if (!P.on) { set_error("lsort_fixup: no hybrid sort to fix"); return SG_E_INVAL; }
+    const uint32_t g = P.ntiles, cap = g + 16;
+    uint32_t *lst;
+    SG_TRY(slot(c, S_LS_LIST, 2 * (size_t)cap + 16, &lst));
+    uint32_t *gs = lst, *ge = lst + cap, *cnt = lst + 2 * (size_t)cap;
+    SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
+    SG_LAUNCH(c, "rs_lfix", k_rs_lsort_fix, g, LS_BLOCK, 0, Kin, Vin, Ko, Vo, n, P.gmask, P.lpos, P.nloc, P.bounds, gs, ge,
+              cap, cnt);
+    uint32_t B = 0;
+    SG_TRY(ctx_readback(c, &B, cnt, 4));
+    if (B > cap) { set_error("lsort_fixup: %u big groups (list of %u)", B, cap); return SG_E_HIP; }
+    if (!B) return SG_OK;
+    // the big groups' members: one stable radix sort on (group, local digits)
+    uint64_t *goff;
+    SG_TRY(slot(c, S_LF_OFF, (size_t)B + 1, &goff));
+    uint64_t M64 = 0;
+    SG_TRY(run_scan64(c, "lfix_scan", LfixSizeFn{gs, ge}, B, goff, &M64));
+    const uint32_t M = (uint32_t)M64;
+    uint64_t *RK, *RK2, *SK;
+    uint32_t *RV, *RV2, *RP, *perm;
+    SG_TRY(slot(c, S_LF_KEY, M, &RK));
+    SG_TRY(slot(c, S_LF_KEY2, M, &RK2));
+    SG_TRY(slot(c, S_LF_VAL, M, &RV));
+    SG_TRY(slot(c, S_LF_VAL2, M, &RV2));
+    SG_TRY(slot(c, S_LF_POS, M, &RP));
+    SG_LAUNCH(c, "lfix_expand", k_lfix_expand, (M + 4095) / 4096, 256, 0, Kin, gs, goff, B, M, P.lpos, P.nloc, RK, RP);
+    int gbits = 1;
+    while (gbits < 31 && (1u << gbits) < B) ++gbits;
+    SG_TRY(radix_sort(c, RK, RV, RK2, RV2, M, 0, 32 + gbits, true, &SK, &perm, "rs_lfix_pass"));
+    SG_LAUNCH(c, "lfix_apply", k_lfix_apply, (M + 255) / 256, 256, 0, Kin, Vin, RP, perm, M, Ko, Vo);
     return SG_OK;
 }
 

@@ -30,6 +30,8 @@ inline int sw_lit_scheme() {
     const char *v = getenv("SG_LIT_SCHEME");
     return v ? (atoi(v) != 0 ? 1 : 0) : -1;
 }
+// SG_LIT_TRIAL_LOG=1: print the literal filter's scheme trial counts (calibration).
+inline bool sw_lit_trial_log() { return env_switch("SG_LIT_TRIAL_LOG", false); }
 // SG_TM_SORT=1: nuclei templates evaluated through the sort path instead of the
 // record-wave evaluator (tests/test_gpu_templates.py).
 inline bool sw_tm_sort() { return env_switch("SG_TM_SORT", false); }

@@ -98,6 +98,7 @@ def partition_exchange(ctx, buf: torch.Tensor, n: int, group=None) -> torch.Tens
     send = torch.empty(n + 1, dtype=torch.uint8, device=buf.device)
     ctx.fence_in()
     pbytes, _ = ctx.partition(buf.data_ptr(), n, world, send.data_ptr(), send.numel())
+    ctx.fence_out()  # the partition's copy pass is queued on the ctx stream; the collective reads send
     return exchange_records(send, pbytes, group)
 
 
@@ -156,6 +157,7 @@ def range_exchange(ctx, pieces: Sequence[torch.Tensor], gsplit, group=None, piec
         if n:
             ctx.fence_in()
             pb = sharded.route_piece(ctx, p, gsplit, send.data_ptr(), send.numel())
+            ctx.fence_out()  # the routing copy is queued on the ctx stream; the collective reads send
         else:
             pb = [0] * world
         recv = exchange_records(send, pb, group)
@@ -176,14 +178,18 @@ def plan_rounds(bytes_per_rank: int, world: int, part_bytes: int = 2 << 30, min_
     return int(max(1, min(r, 256 // max(world, 1))))
 
 
-def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int, group=None):
+def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int, group=None,
+                    force_exchange: bool = False):
     """Route this rank's pieces into world x rounds byte ranges with ONE partition call (the
     parts laid out round-major, sg_dev_partition_bytes_pieces_rounds), exchange every part's
     size with ONE all-to-all, then queue one all-to-all per round, all at once (async on RCCL's
     stream). Returns ([(work or None, receive tensor) per round], send buffer): the receive
     tensor of round p is this rank's local range p (every source's records of it, in source
     rank order), and work.wait() orders the caller's stream after its arrival. The send buffer
-    must stay referenced until every round has been waited for."""
+    must stay referenced until every round has been waited for.
+    force_exchange: issue the size exchange and the per-round all-to-alls even at world size 1
+    (a 1-rank RCCL group on one GPU runs the device-tensor collective path of the N-rank step;
+    without it a single rank skips the collectives)."""
     from .api import round_offsets
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     live = [p for p in pieces if p is not None and p.numel()]
@@ -197,9 +203,12 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
         ctx.fence_in()
         pb, _ = ctx.partition_bytes_pieces_rounds([(p.data_ptr(), p.numel()) for p in live], splitters, rounds,
                                                   send.data_ptr(), send.numel())
+        # the partition's copy pass is queued on the ctx stream and the call returns after the
+        # size read-back only: drain it before a collective (on another stream) reads send
+        ctx.fence_out()
     else:
         pb = [0] * nparts
-    if world == 1:
+    if world == 1 and not (force_exchange and dist.is_initialized()):
         offs = round_offsets(pb, rounds)
         return [(None, send[offs[p]:offs[p] + pb[p]]) for p in range(rounds)], send
     # rc[s * rounds + p]: bytes source s sends this rank in round p (peer g's slice of pb is
@@ -216,15 +225,17 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
     return out, send
 
 
-def dedup_diff_rounds_step(ctx, cur_pieces, prior_parts, splitters, rounds: int, group=None, align_parts=False):
+def dedup_diff_rounds_step(ctx, cur_pieces, prior_parts, splitters, rounds: int, group=None, align_parts=False,
+                           force_exchange: bool = False):
     """One multi-GPU dedup+diff step in exchange rounds: rank r ends with byte range r split
     into `rounds` local parts; each part is deduped and diffed against the rank's stored prior
     part as soon as its round has arrived, while the later rounds are still on the wire. The
     ranks' outputs concatenated in rank order are the global sort -u / comm -13 output.
     prior_parts: this rank's stored prior, one tensor (or None) per local part (None: no
-    prior). Returns (unique, new, stats) device tensors (new is unique without a prior)."""
+    prior). Returns (unique, new, stats) device tensors (new is unique without a prior).
+    force_exchange: run the collectives at world size 1 too (exchange_rounds)."""
     from . import sharded
-    recvd, send = exchange_rounds(ctx, cur_pieces, splitters, rounds, group)
+    recvd, send = exchange_rounds(ctx, cur_pieces, splitters, rounds, group, force_exchange)
     have_prior = prior_parts is not None and any(p is not None and p.numel() for p in prior_parts)
     if prior_parts is not None and len(prior_parts) != rounds:
         raise ValueError("prior_parts has %d entries for %d rounds" % (len(prior_parts), rounds))
@@ -241,13 +252,14 @@ def dedup_diff_rounds_step(ctx, cur_pieces, prior_parts, splitters, rounds: int,
     return u, (out.f[:out.fo] if have_prior else u), st
 
 
-def build_prior_rounds(ctx, prior_pieces, splitters, rounds: int, group=None):
+def build_prior_rounds(ctx, prior_pieces, splitters, rounds: int, group=None, force_exchange: bool = False):
     """Setup (untimed): route the rank's share of the prior scan's records to their owners
     with the same splitters and sort -u them there: returns the rank's stored prior, one
     16-byte aligned tensor per local part (read in place by every later step), and the
     stored bytes."""
     from . import sharded
-    u, _, st = dedup_diff_rounds_step(ctx, prior_pieces, None, splitters, rounds, group, align_parts=True)
+    u, _, st = dedup_diff_rounds_step(ctx, prior_pieces, None, splitters, rounds, group, align_parts=True,
+                                      force_exchange=force_exchange)
     return sharded.stored_parts(u, st), u
 
 

@@ -31,8 +31,13 @@ class _Res:
 
 
 class FakeCtx:
-    """The Context methods swarm_amd.distributed / sharded call for routing, on host memory."""
+    """The Context methods swarm_amd.distributed / sharded call for routing, on host memory.
+    `log` records the routing calls and the stream fences in call order (a test checks that
+    every partition's output is fenced before a collective may read it)."""
     device = 0
+
+    def __init__(self):
+        self.log = []
 
     @property
     def torch_device(self):
@@ -42,12 +47,16 @@ class FakeCtx:
     def fence_in(self):
         pass
 
+    def fence_out(self):
+        self.log.append("fence_out")
+
     def record_sample(self, ptr, n, m):
         return sample_heads(ctypes.string_at(ptr, n) if n else b"", m)
 
     def partition_bytes_pieces_rounds(self, pieces, splitters, rounds, out_ptr, cap):
         """include/swarmgpu.h sg_dev_partition_bytes_pieces_rounds restated: part q = g * rounds
         + p, laid out round-major, every round at a 16-byte aligned offset."""
+        self.log.append("partition")
         nparts = len(splitters) + 1
         parts = [b""] * nparts
         for ptr, n in pieces:
@@ -77,6 +86,7 @@ class FakeCtx:
         return _Res(len(u), len(f), len(S.parse_records(cur)), len(S.parse_records(u)), len(S.parse_records(f)))
 
     def partition_bytes(self, ptr, n, splitters, out_ptr, cap):
+        self.log.append("partition")
         parts = route_parts(ctypes.string_at(ptr, n) if n else b"", splitters)
         blob = b"".join(parts)
         assert len(blob) <= cap

@@ -167,6 +167,9 @@ def rounds_worker(rank, world, rounds, port, out_q):
     assert len(prior_parts) == rounds
     cur = rounds_shard(rank, world)
     u, f, st = D.dedup_diff_rounds_step(ctx, [t(c) for c in cur], prior_parts, split, rounds)
+    # every partition's copy is fenced before the collective that reads its output (ADVICE r3:
+    # a ctx off torch's stream must not hand a half-written send buffer to the all-to-all)
+    assert all(ctx.log[i + 1] == "fence_out" for i, x in enumerate(ctx.log) if x == "partition"), ctx.log
     out_q.put((rank, bytes(u.numpy().tobytes()), bytes(f.numpy().tobytes()), b"".join(cur), prior_raw,
                bytes(stored.numpy().tobytes()), st["parts"]))
     dist.barrier()
@@ -197,6 +200,39 @@ def test_rounds_step_global_order_gloo(world, rounds):
     # the stored prior: 16-byte aligned parts padded with empty lines = the prior's sort -u
     assert S.serialize(S.parse_records(b"".join(r[5] for r in res))) == S.dedup(prior_all)
     assert all(r[6] == rounds for r in res)
+
+
+def single_rank_worker(port, out_q):
+    """A 1-rank group with force_exchange: the size exchange and the per-round all-to-alls run
+    at world size 1 (the code path a 1-rank RCCL group exercises on one GPU)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    from route_oracle import FakeCtx
+    from swarm_amd import distributed as D
+    ctx = FakeCtx()
+    t = lambda b: torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8)[: len(b)]  # noqa: E731
+    prior_raw = b"".join(b"https://h%d.example.com/\n" % i for i in range(0, 2500, 3))
+    split = D.agree_splitters(ctx, [t(prior_raw)], 3, samples_per_piece=64)
+    prior_parts, _ = D.build_prior_rounds(ctx, [t(prior_raw)], split, 3, force_exchange=True)
+    cur = rounds_shard(0, 1)
+    recvd, send = D.exchange_rounds(ctx, [t(c) for c in cur], split, 3, force_exchange=True)
+    exchanged = [w for w, _ in recvd]
+    u, f, st = D.dedup_diff_rounds_step(ctx, [t(c) for c in cur], prior_parts, split, 3, force_exchange=True)
+    out_q.put((bytes(u.numpy().tobytes()), bytes(f.numpy().tobytes()), b"".join(cur), prior_raw, len(exchanged)))
+    dist.destroy_process_group()
+
+
+def test_rounds_step_force_exchange_single_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=single_rank_worker, args=(free_port(), q))
+    p.start()
+    u, f, cur, prior, nround = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    eu, ef = S.dedup_diff(cur, prior)
+    assert u == eu and f == ef
+    assert nround == 3
 
 
 def test_plan_rounds():

@@ -435,8 +435,8 @@ def test_hybrid_sort_subdomains(sg):
 @pytest.mark.parametrize("shape", ["overflow", "ties"])
 def test_hybrid_sort_overflow_and_ties(sg, shape):
     """overflow: half the records share their first 3 bytes, so the groups the global digits
-    leave are far larger than one block's LDS: the local sort flags it and the plain LSD sort
-    runs again (flags bits 0 and 1). ties: distinct records sharing all sorted key bytes,
+    leave are far larger than one block's LDS: the local sort flags them and the fix-up sorts
+    those groups' members by one radix sort (flags bits 0 and 2, no full re-sort: bit 1). ties: distinct records sharing all sorted key bytes,
     short records (live length tag), duplicates: the local sort keeps them in input order
     like the full sort. Both equal the oracle."""
     import torch
@@ -467,9 +467,38 @@ def test_hybrid_sort_overflow_and_ties(sg, shape):
         assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
         assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
         if shape == "overflow":
-            assert flags & 3 == 3
+            assert flags & 5 == 5 and not flags & 2  # fixed up, no full re-sort
         else:
             assert flags & 1
+    finally:
+        ctx.close()
+
+
+def test_hybrid_sort_repeated_record(sg):
+    """one record repeated ~10k times among ~1.2M distinct ones (40 of them sharing
+    its first 3 bytes) forms a group of equal top digits larger than one block's LDS: the
+    fix-up sorts only that group's members (flags bit 2), never the whole input again (bit 1
+    clear); output exact."""
+    import torch
+    rng = np.random.default_rng(8)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", dtype=np.uint8)
+    n = 1_200_000
+    body = alpha[rng.integers(0, 36, size=(n, 12))]
+    recs = [bytes(r) for r in body] + [b"rep" + bytes(r[3:]) for r in body[:40]]
+    recs += [b"repeated.target7.com"] * 10_000
+    rng.shuffle(recs)
+    cur = b"\n".join(recs) + b"\n"
+    prior = S.dedup(b"\n".join(recs[::4]) + b"\n")
+    dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+    dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        r = ctx.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+        flags = ctx.last_path()[1]
+        eu, ef = S.dedup_diff(cur, prior)
+        assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+        assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+        assert flags & 5 == 5 and not flags & 2
     finally:
         ctx.close()
 
