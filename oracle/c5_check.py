@@ -121,7 +121,9 @@ def parse_rows(buf, chunk: int = 1 << 23):
     n = buf.numel()
     if n == 0:
         return
-    ends = torch.nonzero(buf == 10).flatten()
+    # torch.nonzero counts in 32 bits on this build: find the newlines 1 GiB at a time
+    step = 1 << 30
+    ends = torch.cat([torch.nonzero(buf[o:o + step] == 10).flatten() + o for o in range(0, n, step)])
     starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=buf.device), ends[:-1] + 1])
     lens = ends - starts
     keep = lens > 0
