@@ -24,6 +24,7 @@
 #include "sg_internal.hpp"
 #include "sg_prims_host.hpp"
 #include "sg_emit.hpp"
+#include "sg_switches.hpp"
 
 #include <stdlib.h>
 #include <cmath>
@@ -64,6 +65,33 @@ static int run_emit(sg_ctx *c, EmitApplyFn kern, const char *name, const char *c
     SG_TRY(tile_scan(c, tot, ntiles, pre, total, dst_shift));
     SG_LAUNCH_B(c, name, bytes_model, kern, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin,
                 kout);
+    return SG_OK;
+}
+
+// run_emit with the sorted-staging apply kernel (k_emit_uniq_t: records from T, bs = the
+// common prefix's length).
+static int run_emit_t(sg_ctx *c, FlagItem item, uint32_t n, const uint8_t *src, uint8_t *dst, uint2 *out_spans,
+                      const uint64_t *kin, uint64_t *kout, const uint4 *T, uint32_t bs, uint64_t **total_out,
+                      uint32_t dst_shift) {
+    const uint32_t ntiles = (n + EM_TILE - 1) / EM_TILE;
+    uint64_t *tp;
+    SG_TRY(slot(c, S_EMIT2, 2 * (size_t)ntiles + 4, &tp));
+    uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
+    *total_out = total;
+    if (ntiles == 0) {
+        SG_HIP(hipMemsetAsync(total, 0, 8, c->stream));
+        return SG_OK;
+    }
+    uint2 *cache;
+    SG_TRY(slot(c, S_ECACHE, (size_t)n + 1, &cache));
+    SG_LAUNCH(c, "emit_uniq.count", k_emit_count<FlagItem>, ntiles, EM_BLOCK, 0, item, n, cache, tot);
+    SG_TRY(tile_scan(c, tot, ntiles, pre, total, dst_shift));
+    if (bs)
+        SG_LAUNCH_B(c, "emit_uniq", 0.0, k_emit_uniq_tp, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin, kout,
+                    T, bs);
+    else
+        SG_LAUNCH_B(c, "emit_uniq", 0.0, k_emit_uniq_t, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin, kout,
+                    T, bs);
     return SG_OK;
 }
 
@@ -338,6 +366,167 @@ __global__ __launch_bounds__(256) void k_adjacent2(const uint8_t *__restrict__ S
     if (live) dup[i] = d ? 1 : 0;
 }
 
+// ------------------------------------------------------------------ sorted staging (T)
+// Short-record inputs (C2 subdomains, host:port, URL lists) gather every record ONCE, in
+// sorted order, into a fixed-stride staging array T: slot i (32 B, two uint4) holds the
+// bytes [L, L + 31) of the i-th record in sort order (L = the common prefix), zero-padded,
+// and in byte 31 the count of bytes from L (255: more than 31, "long"; the rest is read from
+// the input through the span). Everything after the sort then reads T sequentially — the
+// adjacent compare (fused into the gather: a wave's 64 lanes hold 64 consecutive records and
+// take the predecessor's slot from the neighbouring lane), the segment sort and the unique
+// emit — instead of gathering the records from the input once per pass (round 3: three
+// random gathers of every kept record).
+constexpr uint32_t ST_DATA = 31;   // slot bytes of record data
+constexpr uint32_t ST_LONG = 255;  // length code of a record with more than ST_DATA bytes from L
+
+struct RecSlot {
+    uint32_t d[8];  // bytes 0..30: data (zero-padded), byte 31: length code
+};
+
+__device__ __forceinline__ uint32_t slot_code(const RecSlot &s) { return s.d[7] >> 24; }
+
+// Record (span x) of buf -> its slot (bytes from L = base & 0xffff).
+__device__ __forceinline__ RecSlot make_slot(const uint8_t *__restrict__ buf, uint2 x, uint32_t L) {
+    const uint32_t len = x.y - x.x;
+    const uint32_t rl = len > L ? len - L : 0u;
+    const uint32_t tk = rl < ST_DATA ? rl : ST_DATA;
+    uint4 c[4];
+    load_chunks(buf, x.x + L, tk, c);
+    uint32_t r[13];
+    normalize52(c, (x.x + L) & 15u, r);
+    RecSlot s;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+        const uint32_t b0 = 4u * q;
+        const uint32_t m = b0 + 4u <= tk ? ~0u : (b0 >= tk ? 0u : ((1u << (8u * (tk - b0))) - 1u));
+        s.d[q] = r[q] & m;
+    }
+    s.d[7] = (s.d[7] & 0x00ffffffu) | ((rl <= ST_DATA ? rl : ST_LONG) << 24);
+    return s;
+}
+
+__device__ __forceinline__ RecSlot load_slot(const uint4 *__restrict__ T, uint32_t i) {
+    const uint4 a = T[2 * (size_t)i], b = T[2 * (size_t)i + 1];
+    return RecSlot{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+}
+
+__device__ __forceinline__ void store_slot(uint4 *__restrict__ T, uint32_t i, const RecSlot &s) {
+    T[2 * (size_t)i] = make_uint4(s.d[0], s.d[1], s.d[2], s.d[3]);
+    T[2 * (size_t)i + 1] = make_uint4(s.d[4], s.d[5], s.d[6], s.d[7]);
+}
+
+__device__ __forceinline__ bool slot_eq(const RecSlot &a, const RecSlot &b) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x |= a.d[q] ^ b.d[q];
+    return x == 0;
+}
+
+// Order of two records by their slots (memcmp of the bytes from L, then length: the zero
+// padding and the length code in the last byte make the slots compare like the records), with
+// the bytes past the slot compared in the input when both are long.
+__device__ __forceinline__ int slot_cmp(const uint8_t *__restrict__ buf, const RecSlot &a, uint2 xa, const RecSlot &b, uint2 xb,
+                                        uint32_t L) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (a.d[q] != b.d[q]) {
+            const uint32_t x = a.d[q] ^ b.d[q];
+            const uint32_t sh = (uint32_t)__builtin_ctz(x) & ~7u;  // first differing byte (little-endian dword)
+            return ((a.d[q] >> sh) & 0xffu) < ((b.d[q] >> sh) & 0xffu) ? -1 : 1;
+        }
+    }
+    if (slot_code(a) != ST_LONG) return 0;
+    return rec_cmp_w(buf, xa.x, xa.y, buf, xb.x, xb.y, L + ST_DATA);
+}
+
+// The adjacent pass fused with the gather into T. One wave = 63 consecutive sorted positions
+// (lanes 1..63) plus their predecessor (lane 0), so every lane gathers one record and compares
+// it with lane - 1's. KEYS / DUP and the outputs as k_adjacent2 (without DUP only the groups
+// are marked and T is not written).
+template <bool KEYS>
+__global__ __launch_bounds__(256) void k_stage(const uint8_t *__restrict__ S, const uint2 *__restrict__ SS,
+                                               const uint64_t *__restrict__ K, uint8_t *__restrict__ brk, uint32_t n,
+                                               uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad, AdjLists L,
+                                               uint32_t base, uint4 *__restrict__ T) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const int64_t ig = (int64_t)w * 63 + (int64_t)lane - 1;  // lane 0: the predecessor
+    const bool live = lane > 0 && ig < (int64_t)n;
+    const uint32_t i = ig < 0 ? 0u : (ig >= (int64_t)n ? n - 1u : (uint32_t)ig);
+    const uint32_t Lp = base & 0xffffu;
+    const uint2 x = SS[i];
+    const uint64_t ki = K[i];
+    const RecSlot sl = make_slot(S, x, Lp);
+    RecSlot sp;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sp.d[q] = (uint32_t)__shfl_up((int)sl.d[q], 1, 64);
+    const uint64_t kp = (uint64_t)__shfl_up((long long)ki, 1, 64);
+    const uint2 xp = make_uint2((uint32_t)__shfl_up((int)x.x, 1, 64), (uint32_t)__shfl_up((int)x.y, 1, 64));
+    bool head;
+    if constexpr (KEYS) {
+        head = (i == 0) || kp != ki;
+        if (live) brk[i] = head ? 1 : 0;
+        const bool big = live && head && (ki & 0xffu) == bk_full(base) && i + WAVE_GROUP < n && K[i + WAVE_GROUP] == ki;
+        uint32_t last = 0;
+        if (big) {
+            uint32_t lo = i + WAVE_GROUP, step = WAVE_GROUP;  // K[lo] == ki
+            while (lo + step < n && K[lo + step] == ki) { lo += step; step <<= 1; }
+            uint32_t hi = min(n, lo + step);
+            while (hi - lo > 1) {
+                const uint32_t mid = lo + (hi - lo) / 2;
+                if (K[mid] == ki) lo = mid; else hi = mid;
+            }
+            last = lo;
+        }
+        const uint64_t m = __ballot(big);
+        if (m) {
+            const int lead = __ffsll((long long)m) - 1;
+            uint32_t b = 0;
+            if ((int)lane == lead) b = atomicAdd(&L.cnt[2], (uint32_t)__popcll(m));
+            b = (uint32_t)__shfl((int)b, lead, 64);
+            if (big) {
+                const uint32_t q = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (q < L.cap_g) { L.gs[q] = i; L.ge[q] = last; }
+            }
+        }
+    } else {
+        head = (i == 0) || brk[i];
+    }
+    if (live) store_slot(T, i, sl);
+    bool d = false;
+    if (live && !head) {
+        d = ((ki & 0xffu) < bk_full(base)) ||
+            (slot_eq(sl, sp) && (slot_code(sl) != ST_LONG || rec_equal_w(S, x.x, x.y, S, xp.x, xp.y, Lp + ST_DATA)));
+        if (!d) {
+            // i differs from i - 1 inside one segment: mark the segment's head (the last group
+            // start at or before i - 1) bad
+            uint32_t h = i - 1;
+            bool found = true;
+            if constexpr (KEYS) {
+                uint32_t lo = i >= WAVE_GROUP ? i - WAVE_GROUP : 0u;
+                if (lo > 0 && K[lo] == ki) {
+                    found = false;  // a big group: refinement rounds first, then this pass again
+                } else {
+                    while (lo < h) {
+                        const uint32_t mid = (lo + h) >> 1;
+                        if (K[mid] == ki) h = mid; else lo = mid + 1;
+                    }
+                }
+            } else {
+                for (;;) {
+                    const uint32_t a = h & ~15u;
+                    const uint32_t mm = swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a)) & ((2u << (h - a)) - 1u);
+                    if (mm) { h = a + 31u - (uint32_t)__clz(mm); break; }
+                    if (a == 0) { h = 0; break; }
+                    h = a - 1;
+                }
+            }
+            if (found) segbad[h] = 1;
+        }
+    }
+    if (live) dup[i] = d ? 1 : 0;
+}
+
 // Heads of bad segments (segbad, marked by k_adjacent2): A = up to SEG_SMALL members, B = more
 // (<= WAVE_GROUP). A bad head's segment is small iff a break (brk, or the end) lies in
 // (i, i + SEG_SMALL]: two aligned 16-B loads of brk (the slot has 32 B of tail room).
@@ -491,6 +680,87 @@ __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S,
     } else {
         seg_rank_group<64>(S, SS, dup, a[0], k[0], lane, 0u, true, base);
         if (k[1]) seg_rank_group<64>(S, SS, dup, a[1], k[1], lane, 0u, true, base);
+    }
+}
+
+// The segment sorts over T: members ranked by their slots (a long pair compared past the slot
+// in the input); spans, slots and dup flags permuted together.
+template <int G>
+__device__ __forceinline__ void seg_rank_group_t(const uint8_t *__restrict__ S, uint2 *__restrict__ SS, uint4 *__restrict__ T,
+                                                 uint8_t *__restrict__ dup, uint32_t a, uint32_t k, uint32_t gl,
+                                                 uint32_t gbase, bool live, uint32_t base) {
+    const bool act = live && gl < k;
+    const uint32_t Lp = base & 0xffffu;
+    const uint2 x = act ? SS[a + gl] : make_uint2(0u, 0u);
+    RecSlot ms;
+    if (act) ms = load_slot(T, a + gl);
+    else
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ms.d[q] = 0u;
+    uint32_t rank = 0;
+    bool d = false;
+    const uint32_t kk = live ? k : 0u;
+    uint32_t kmax = kk;
+#pragma unroll
+    for (int o = G; o < 64; o <<= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    for (uint32_t j = 0; j < kmax; ++j) {
+        const int src = (int)(gbase + (j < kk ? j : 0u));
+        RecSlot os;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) os.d[q] = (uint32_t)__shfl((int)ms.d[q], src, 64);
+        const uint2 y = make_uint2((uint32_t)__shfl((int)x.x, src, 64), (uint32_t)__shfl((int)x.y, src, 64));
+        if (act && j < kk && j != gl) {
+            const int c = slot_cmp(S, ms, x, os, y, Lp);
+            if (c > 0 || (c == 0 && j < gl)) ++rank;
+            if (c == 0 && j < gl) d = true;
+        }
+    }
+    if (act) {
+        SS[a + rank] = x;
+        store_slot(T, a + rank, ms);
+        dup[a + rank] = d ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_seg_small_t(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
+                                                     uint4 *__restrict__ T, const uint8_t *__restrict__ brk,
+                                                     uint8_t *__restrict__ dup, const uint32_t *__restrict__ heads,
+                                                     uint32_t nh, uint32_t n, uint32_t base) {
+    const uint32_t lane = lane_id(), gl = lane & 15u, gbase = lane & ~15u;
+    const uint32_t q = blockIdx.x * 16u + (threadIdx.x >> 4);
+    const bool live = q < nh;
+    const uint32_t a = live ? heads[q] : 0u;
+    const uint32_t pe = a + 1u + gl;
+    const bool eb = !live || pe >= n || gl == 15u || brk[pe];
+    const uint32_t me = (uint32_t)(__ballot(eb) >> gbase) & 0xffffu;
+    const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);
+    seg_rank_group_t<16>(S, SS, T, dup, a, k, gl, gbase, live, base);
+}
+
+__global__ __launch_bounds__(256) void k_seg_wave_t(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
+                                                    uint4 *__restrict__ T, const uint8_t *__restrict__ brk,
+                                                    uint8_t *__restrict__ dup, const uint32_t *__restrict__ heads,
+                                                    uint32_t nh, uint32_t n, uint32_t *err, uint32_t base) {
+    const uint32_t q0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2u;
+    const uint32_t lane = lane_id();
+    if (q0 >= nh) return;
+    uint32_t a[2], k[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const bool live = q0 + t < nh;
+        a[t] = live ? heads[q0 + t] : 0u;
+        const uint32_t pe = a[t] + 1u + lane;
+        const uint64_t me = __ballot(!live || pe >= n || brk[pe]);
+        if (!me) { if (lane == 0) atomicOr(err, 1u); return; }
+        k[t] = live ? 1u + (uint32_t)(__ffsll((long long)me) - 1) : 0u;
+    }
+    if (k[0] <= 32u && k[1] <= 32u) {
+        const uint32_t t = lane >> 5;
+        seg_rank_group_t<32>(S, SS, T, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u,
+                             (t ? k[1] : k[0]) > 0, base);
+    } else {
+        seg_rank_group_t<64>(S, SS, T, dup, a[0], k[0], lane, 0u, true, base);
+        if (k[1]) seg_rank_group_t<64>(S, SS, T, dup, a[1], k[1], lane, 0u, true, base);
     }
 }
 
@@ -1195,9 +1465,24 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // adjacent equality inside segments; segments holding two different records -> sort.
     // model: key0 + brk + span per record, both records' bytes where compared, dup out
     uint64_t *stot = nullptr;
+    // The sorted staging T (k_stage): short records (on average <= ~27 bytes past the common
+    // prefix, prefix <= 48 bytes) are gathered once into 32-B slots in sorted order; the adjacent
+    // compare, the segment sorts and the unique emit then read T instead of the input.
+    const uint32_t Lb = base & 0xffffu;
+    const bool staged = sw_stage() && R >= 4096 && Lb <= 48u && n <= (uint64_t)R * (28u + Lb);
+    uint4 *T = nullptr;
+    if (staged) SG_TRY(slot(c, S_STAGE, 2 * (size_t)R, &T));
     auto adjacent = [&](bool keys, bool with_dup, const uint8_t *Sb, const uint2 *SSp) -> int {
         SG_HIP(hipMemsetAsync(segbad, 0, cnt_off + 16, c->stream));  // head marks + list counters
-        if (keys && with_dup)
+        // model: key0 + span + brk + dup per record, the record's bytes gathered, its slot written
+        const uint32_t sgrid = (uint32_t)(((uint64_t)R + 62) / 63 + 3) / 4;
+        if (staged && with_dup && keys)
+            SG_LAUNCH_B(c, "stage", 18.0 * R + (double)n + 32.0 * R, (k_stage<true>), sgrid, 256, 0, Sb, SSp, K, brk, R, dup,
+                        segbad, AL, base, T);
+        else if (staged && with_dup)
+            SG_LAUNCH_B(c, "stage", 18.0 * R + (double)n + 32.0 * R, (k_stage<false>), sgrid, 256, 0, Sb, SSp, K, brk, R,
+                        dup, segbad, AL, base, T);
+        else if (keys && with_dup)
             SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, (k_adjacent2<true, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
                         brk, R, dup, segbad, AL, base);
         else if (keys)
@@ -1282,8 +1567,16 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         err = reinterpret_cast<uint32_t *>(etp + 2 * (size_t)ent + 1);
     }
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
-    if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
-    if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
+    if (staged) {
+        if (ns) SG_LAUNCH(c, "seg_small", k_seg_small_t, grid_for(ns, 16), 256, 0, Sb, SS, T, brk, dup, hs, ns, R, base);
+        if (nb)
+            SG_LAUNCH(c, "seg_wave", k_seg_wave_t, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, T, brk, dup, hb, nb, R, err,
+                      base);
+    } else {
+        if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
+        if (nb)
+            SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
+    }
     if (c->profile && c->prof_only.empty() && (ns || nb)) {  // full-profile steps only
         // byte model: per member its span read + written, ~4 chunk keys of record bytes, flag
         unsigned long long *mc;
@@ -1310,8 +1603,11 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint64_t *uc;
     // short records: the small-window emit (more blocks per CU for the random gather)
     const EmitApplyFn uk_kern = (n <= 40ull * R) ? k_emit_uniq_s : k_emit_uniq;
-    SG_TRY(run_emit(c, uk_kern, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
-                    0.0, dst ? dst->shift() : 0u));
+    if (staged)
+        SG_TRY(run_emit_t(c, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, T, Lb, &uc, dst ? dst->shift() : 0u));
+    else
+        SG_TRY(run_emit(c, uk_kern, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk,
+                        &uc, 0.0, dst ? dst->shift() : 0u));
     // the output count and the run-sort error word come back with one host sync
     uint8_t *pin = (uint8_t *)c->pinned;
     if (nb && reinterpret_cast<uint32_t *>(uc + 1) != err) { set_error("emit: status slot moved"); return SG_E_HIP; }

@@ -30,6 +30,9 @@ inline int sw_lit_scheme() {
     const char *v = getenv("SG_LIT_SCHEME");
     return v ? (atoi(v) != 0 ? 1 : 0) : -1;
 }
+// SG_STAGE=0: the dedup gathers records from the input in every pass after the sort instead
+// of staging them once in sorted order (sg_dedup.hip k_stage; A/B and the tests' second path).
+inline bool sw_stage() { return env_switch("SG_STAGE", true); }
 // SG_LIT_TRIAL_LOG=1: print the literal filter's scheme trial counts (calibration).
 inline bool sw_lit_trial_log() { return env_switch("SG_LIT_TRIAL_LOG", false); }
 // SG_TM_SORT=1: nuclei templates evaluated through the sort path instead of the

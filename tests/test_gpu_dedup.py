@@ -542,3 +542,50 @@ def test_key_stats_rare_digits(sg, shape):
         assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
     finally:
         ctx.close()
+
+
+# ------------------------------------------------------------------ sorted staging (T)
+@pytest.mark.parametrize("shape", ["mixed_long", "slot_edges", "url_prefix", "nul_cr"])
+@pytest.mark.parametrize("stage", ["1", "0"])
+def test_staged_dedup_shapes(sg, monkeypatch, shape, stage):
+    """The dedup with the sorted staging (k_stage: each record gathered once into a 32-B slot
+    of its bytes past the common prefix) and without it (SG_STAGE=0), against the oracle:
+    mixed_long: short records beside records too long for a slot (compared and emitted from
+    the input), many sharing their first 7+ bytes (segment sorts on slots, long pairs past the
+    slot); slot_edges: lengths 29..34 past the prefix around the 31-byte slot; url_prefix: a
+    common 'https://' prefix (slots start after it, the emit writes it back); nul_cr: NUL, CR
+    and 0xff bytes inside slots (zero padding must not tie a NUL byte with the record end)."""
+    import torch
+    monkeypatch.setenv("SG_STAGE", stage)
+    rng = np.random.default_rng({"mixed_long": 21, "slot_edges": 22, "url_prefix": 23, "nul_cr": 24}[shape])
+    n = 200_000
+    if shape == "mixed_long":
+        heads = [bytes(rng.choice(list(b"abc"), size=int(rng.integers(1, 12)))) for _ in range(3000)]
+        recs = []
+        for _ in range(n):
+            h = heads[int(rng.integers(0, len(heads)))]
+            tail = b"x" * int(rng.integers(25, 45)) + bytes(rng.choice(list(b"pq"), size=3)) if rng.random() < 0.25 else b""
+            recs.append(h + tail)
+    elif shape == "slot_edges":
+        base = bytes(rng.choice(list(b"mn"), size=28))
+        recs = [base + bytes(rng.choice(list(b"01"), size=int(rng.integers(1, 7)))) for _ in range(n // 4)]
+        recs += [bytes(rng.choice(list(b"abc"), size=int(rng.integers(3, 10)))) for _ in range(3 * n // 4)]
+    elif shape == "url_prefix":
+        recs = [b"https://h%d.t%d.example.com" % (int(rng.integers(0, 60_000)), int(rng.integers(0, 9))) for _ in range(n)]
+        recs += [b"https://" + b"y" * int(k) for k in rng.integers(20, 50, size=3000)]
+    else:
+        recs = [bytes(rng.choice([0, 13, 255, 97, 98], size=int(rng.integers(1, 9)))) for _ in range(n)]
+        recs += [r + b"\x00" for r in recs[:5000]]
+    rng.shuffle(recs)
+    cur = b"\n".join(recs) + b"\n"
+    prior = S.dedup(b"\n".join(recs[::3]) + b"\n")
+    dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+    dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        r = ctx.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+        eu, ef = S.dedup_diff(cur, prior)
+        assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+        assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+    finally:
+        ctx.close()
