@@ -32,7 +32,7 @@ inline int sw_lit_scheme() {
 }
 // SG_STAGE=0: the dedup gathers records from the input in every pass after the sort instead
 // of staging them once in sorted order (sg_dedup.hip k_stage; A/B and the tests' second path).
-inline bool sw_stage() { return env_switch("SG_STAGE", true); }
+inline bool sw_stage() { return env_switch("SG_STAGE", false); }
 // SG_LIT_TRIAL_LOG=1: print the literal filter's scheme trial counts (calibration).
 inline bool sw_lit_trial_log() { return env_switch("SG_LIT_TRIAL_LOG", false); }
 // SG_TM_SORT=1: nuclei templates evaluated through the sort path instead of the
