@@ -75,6 +75,7 @@ enum Slot : int {
     S_LS_ERR, S_LS_BOUNDS,  // hybrid radix sort: overflow flag, local-sort tile bounds
     S_LS_LIST, S_LF_OFF, S_LF_KEY, S_LF_KEY2, S_LF_VAL, S_LF_VAL2, S_LF_POS,  // its overflow fix-up
     S_STAGE,  // dedup: the sorted staging T (32-B slots)
+    S_FD_LB,  // dedup: the fused diff's prior range per emit tile
     S_NSLOTS
 };
 

@@ -966,6 +966,209 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
 }
 
 
+// ------------------------------------------------------------------ fused unique emit + diff
+// The unique emit already holds every kept record (its span, key and, in cache, its bytes)
+// when it writes it, so the diff against the prior is decided there instead of by a second
+// pass over the unique output (k_diff_tile: U keys, spans and bytes read again, 150 us on
+// C2). Per emit tile (EM_TILE sorted items) the prior's records with keys in
+// [first item's key, last item's key] — found by k_fd_split, one wave per boundary — are
+// staged in LDS (keys + spans); each kept record is looked up among them by key0 and, when
+// its key0 does not hold the whole record, compared bytewise with the equal-key prior records.
+// The tile writes a fresh flag per sorted item and its fresh (count, bytes) total, so the
+// new-record emit needs no count pass of its own.
+constexpr uint32_t FD_PCAP = 1024;  // prior records staged per emit tile
+
+// lb[t] = lower_bound(P.K, K[t * EM_TILE]), ub[t] = upper_bound(P.K, K[last item of tile t]),
+// P's keys narrowed to kw as read (one wave per tile).
+__device__ __forceinline__ uint32_t wave_lower_bound(const uint64_t *__restrict__ PK, uint32_t np, uint64_t key,
+                                                     uint32_t kw) {
+    const uint32_t lane = lane_id();
+    uint32_t lo = 0, hi = np;  // answer in [lo, hi]
+    while (hi > lo) {
+        const uint32_t span = hi - lo;
+        if (span <= 64) {
+            const uint32_t p = lo + lane;
+            const bool ge = (p >= hi) || key_narrow(PK[p], kw) >= key;
+            const uint64_t m = __ballot(ge);
+            lo = m ? lo + (uint32_t)(__ffsll((long long)m) - 1) : hi;
+            break;
+        }
+        const uint32_t p = lo + (uint32_t)(((uint64_t)span * (lane + 1)) / 65);
+        const bool ge = key_narrow(PK[p], kw) >= key;
+        const uint64_t m = __ballot(ge);
+        if (!m) {
+            lo = (uint32_t)__shfl((int)p, 63, 64) + 1;
+        } else {
+            const int f = __ffsll((long long)m) - 1;
+            const uint32_t pf = (uint32_t)__shfl((int)p, f, 64);
+            const uint32_t pp = (uint32_t)__shfl((int)p, f > 0 ? f - 1 : 0, 64);
+            hi = pf;
+            if (f > 0) lo = pp + 1;
+        }
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_fd_split(const uint64_t *__restrict__ K, uint32_t n,
+                                                  const uint64_t *__restrict__ PK, uint32_t np, uint32_t ntiles,
+                                                  uint32_t *__restrict__ lb, uint32_t *__restrict__ ub, uint32_t kw) {
+    const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= ntiles) return;
+    const uint32_t i0 = t * EM_TILE, i1 = min(n, i0 + EM_TILE) - 1u;
+    const uint64_t k0 = K[i0], k1 = K[i1];
+    const uint32_t a = wave_lower_bound(PK, np, k0, kw);
+    const uint32_t b = k1 == ~0ull ? np : wave_lower_bound(PK, np, k1 + 1ull, kw);
+    if (lane_id() == 0) { lb[t] = a; ub[t] = b; }
+}
+
+// Is the unique record (span us of ubuf, key0 ku) in the prior? The prior's records of this
+// tile, [j0, j1), are staged in LDS (s_k narrowed keys, s_sp spans) when `staged`.
+__device__ __forceinline__ bool fd_present(const uint8_t *__restrict__ ubuf, uint2 us, uint64_t ku, RecSet P,
+                                           const uint64_t *s_k, const uint2 *s_sp, uint32_t j0, uint32_t j1,
+                                           bool staged, uint32_t base) {
+    const uint32_t kw = base >> 16;
+    const uint32_t np = j1 - j0;
+    uint32_t lo = 0, hi = np;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t v = staged ? s_k[mid] : key_narrow(P.K[j0 + mid], kw);
+        if (v < ku) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t cand = j0 + lo;
+    if (lo >= np) return false;  // every prior record with key ku lies in [j0, j1)
+    const uint64_t kp = staged ? s_k[lo] : key_narrow(P.K[cand], kw);
+    if (kp != ku) return false;
+    if ((ku & 0xffu) < bk_full(base)) return true;
+    const uint2 ps = staged ? s_sp[lo] : P.sp[cand];
+    if (rec_equal_w(ubuf, us.x, us.y, P.buf, ps.x, ps.y, bk_off(base))) return true;
+    // other prior records sharing this key0, sorted by their remaining bytes: binary search
+    // the run [cand + 1, run end) by full compare
+    uint32_t ce;
+    {
+        uint32_t a = lo + 1, b = np;  // upper bound of ku in [lo + 1, np)
+        while (a < b) {
+            const uint32_t mid = (a + b) >> 1;
+            const uint64_t v = staged ? s_k[mid] : key_narrow(P.K[j0 + mid], kw);
+            if (v <= ku) a = mid + 1; else b = mid;
+        }
+        ce = j0 + a;
+    }
+    uint32_t a = cand + 1, b = ce;
+    while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        const uint2 x = P.sp[mid];
+        const int cmp = rec_cmp8_2(P.buf, x.x, x.y - x.x, ubuf, us.x, us.y - us.x, bk_off(base));
+        if (cmp == 0) return true;
+        if (cmp < 0) a = mid + 1; else b = mid;
+    }
+    return false;
+}
+
+// The unique emit (emit_apply_body's SPARSE path: kept items packed per wave, copied 64 per
+// round through the LDS window) with the diff of every kept record; ff[i] = item i is a new
+// record; tot_f[tile] = the tile's new (records << 32 | bytes + newlines).
+template <uint32_t WIN>
+__global__ __launch_bounds__(EM_BLOCK) void k_emit_uniq_diff(const uint2 *__restrict__ cache, uint32_t n,
+                                                             const uint64_t *__restrict__ pre,
+                                                             const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                             const uint64_t *__restrict__ kin, RecSet P,
+                                                             const uint32_t *__restrict__ lb,
+                                                             const uint32_t *__restrict__ ub, uint32_t base_bk,
+                                                             uint8_t *__restrict__ ff, uint64_t *__restrict__ tot_f) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][WIN];
+    __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
+    __shared__ uint64_t s_wt[4], s_ft[4];
+    __shared__ uint32_t s_cst[4][EM_ROUNDS * 64], s_cln[4][EM_ROUNDS * 64], s_co[4][EM_ROUNDS * 64],
+        s_ci[4][EM_ROUNDS * 64];
+    __shared__ uint8_t s_fr[4][EM_ROUNDS * 64];
+    __shared__ uint64_t s_pk[FD_PCAP];
+    __shared__ uint2 s_psp[FD_PCAP];
+    const uint32_t tile = blockIdx.x;
+    const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t wbase = tile * EM_TILE + wid * 256u;
+    const uint32_t kw = base_bk >> 16;
+    // the tile's prior records, staged while the scans below run
+    const uint32_t j0 = lb[tile], j1 = max(ub[tile], j0);
+    const bool staged = j1 - j0 <= FD_PCAP;
+    if (staged)
+        for (uint32_t q = threadIdx.x; q < j1 - j0; q += EM_BLOCK) {
+            s_pk[q] = key_narrow(P.K[j0 + q], kw);
+            s_psp[q] = P.sp[j0 + q];
+        }
+    uint32_t st[EM_ROUNDS], ln[EM_ROUNDS];
+    uint64_t loc[EM_ROUNDS];
+    uint64_t run = 0;
+    uint32_t fmask = 0;
+    uint2 cvr[EM_ROUNDS];
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        const uint32_t i = wbase + r * 64u + lane;
+        cvr[r] = cache[i < n ? i : n - 1u];
+    }
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        const uint32_t i = wbase + r * 64u + lane;
+        const uint2 cv = (i < n) ? cvr[r] : make_uint2(0u, EM_DROP);
+        const bool f = cv.y != EM_DROP;
+        st[r] = cv.x;
+        ln[r] = f ? cv.y : 0u;
+        const uint64_t v = f ? (EM_ONE | (uint64_t)(cv.y + 1u)) : 0ull;
+        const uint64_t inc = wave_incl_scan(v);
+        loc[r] = run + inc - v;
+        run += __shfl(inc, 63, 64);
+        fmask |= (f ? 1u : 0u) << r;
+    }
+    if (lane == 0) s_wt[wid] = run;
+    __syncthreads();  // also: the staged prior records
+    uint64_t woff = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) woff += (w < wid) ? s_wt[w] : 0ull;
+    const uint64_t wpre = pre[tile] + woff;
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        if (!((fmask >> r) & 1u)) continue;
+        const uint64_t gp = wpre + loc[r];
+        const uint32_t e = (uint32_t)(loc[r] >> 32);
+        s_cst[wid][e] = st[r];
+        s_cln[wid][e] = ln[r];
+        s_co[wid][e] = (uint32_t)gp;
+        s_ci[wid][e] = wbase + r * 64u + lane;
+    }
+    const uint32_t kept = (uint32_t)(run >> 32);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint64_t facc = 0;
+    for (uint32_t k0 = 0; k0 < kept; k0 += 64u) {
+        const uint32_t q = k0 + lane;
+        const bool f = q < kept;
+        const uint32_t s = f ? s_cst[wid][q] : 0u, l = f ? s_cln[wid][q] : 0u, o = f ? s_co[wid][q] : 0u;
+        const uint32_t i = f ? s_ci[wid][q] : 0u;
+        const uint64_t ku = f ? kin[i] : 0ull;  // issued before the copy's loads
+        const uint32_t last = (kept - k0 >= 64u) ? 63u : kept - k0 - 1u;
+        const uint64_t o0 = (uint32_t)__shfl((int)o, 0, 64);
+        const uint64_t oend = (uint32_t)__shfl((int)(o + l + 1u), (int)last, 64);
+        const uint64_t obase = o0 & ~15ull;
+        wave_copy_round<WIN>(src, nullptr, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
+                             (uint32_t)(o - obase), o0, oend, obase);
+        bool fresh = false;
+        if (f) fresh = !fd_present(src, make_uint2(s, s + l), ku, P, s_pk, s_psp, j0, j1, staged, base_bk);
+        if (f) s_fr[wid][q] = fresh ? 1 : 0;
+        facc += fresh ? (EM_ONE | (uint64_t)(l + 1u)) : 0ull;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    // per item: new iff kept and not in the prior
+#pragma unroll
+    for (int r = 0; r < EM_ROUNDS; ++r) {
+        const uint32_t i = wbase + r * 64u + lane;
+        if (i < n) ff[i] = ((fmask >> r) & 1u) ? s_fr[wid][(uint32_t)(loc[r] >> 32)] : (uint8_t)0;
+    }
+    facc = wave_sum(facc);
+    if (lane == 0) s_ft[wid] = facc;
+    __syncthreads();
+    if (threadIdx.x == 0) tot_f[tile] = s_ft[0] + s_ft[1] + s_ft[2] + s_ft[3];
+}
+
 // ------------------------------------------------------------------ common prefix (URL-like data)
 // L = the longest prefix every record of cur and prior shares (capped at 255). All order and
 // equality questions are then decided from byte L on, and key0 is taken there: for URL lists
@@ -1368,9 +1571,19 @@ struct OutBuf {
     uint32_t shift() const { return (uint32_t)((uintptr_t)p & 15); }
 };
 
+// The diff fused into the unique emit (cur only): the prior's sorted unique view in, the new
+// records out (into of, or a context slot).
+struct FusedDiff {
+    RecSet P;
+    uint64_t prior_bytes = 0;
+    const OutBuf *of = nullptr;
+    uint8_t *fresh = nullptr;
+    uint32_t fresh_bytes = 0, fresh_records = 0;
+};
+
 static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
                         UView *uv, const Lines *pre = nullptr, uint32_t base = make_bk(0u, 7u), const OutBuf *dst = nullptr,
-                        const KeyStats *ks = nullptr) {
+                        const KeyStats *ks = nullptr, FusedDiff *fd = nullptr) {
     *uv = UView{};
     Lines L;
     if (pre) L = *pre;
@@ -1598,6 +1811,64 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint64_t *uk;
     if (dst) ub = dst->base();
     else SG_TRY(slot(c, vs.ubuf, (size_t)n + 64, &ub));
+    if (fd) {
+        // the unique emit with the diff fused (k_emit_uniq_diff), then the new-record emit
+        // over the same sorted items (its per-tile totals come from the fused pass)
+        const uint32_t ntiles = (R + EM_TILE - 1) / EM_TILE;
+        uint32_t *lbub;
+        SG_TRY(slot(c, S_FD_LB, 2 * (size_t)ntiles + 4, &lbub));
+        SG_LAUNCH(c, "diff_split", k_fd_split, (ntiles + 3) / 4, 256, 0, K, R, fd->P.K, fd->P.n, ntiles, lbub,
+                  lbub + ntiles, base >> 16);
+        uint64_t *tp;  // tot[ntiles] | pre[ntiles] | total  (err word beside total, as run_emit's)
+        SG_TRY(slot(c, S_EMIT2, 2 * (size_t)ntiles + 4, &tp));
+        uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
+        if (nb && reinterpret_cast<uint32_t *>(total + 1) != err) { set_error("emit: status slot moved"); return SG_E_HIP; }
+        uint64_t *fp;  // tot_f | pre_f | total_f
+        SG_TRY(slot(c, S_EMIT3, 2 * (size_t)ntiles + 4, &fp));
+        uint64_t *ftot = fp, *fpre = fp + ntiles, *ftotal = fp + 2 * (size_t)ntiles;
+        uint2 *cache;
+        SG_TRY(slot(c, S_ECACHE, (size_t)R + 1, &cache));
+        uint8_t *ff;
+        SG_TRY(slot(c, S_FRESHF, (size_t)R + 16, &ff));
+        uint8_t *fout;
+        if (fd->of) fout = fd->of->base();
+        else SG_TRY(slot(c, S_OUT_FRESH, (size_t)n + 64, &fout));
+        SG_LAUNCH(c, "emit_uniq.count", k_emit_count<FlagItem>, ntiles, EM_BLOCK, 0, FlagItem{SS, dup, 0}, R, cache, tot);
+        SG_TRY(tile_scan(c, tot, ntiles, pre, total, dst ? dst->shift() : 0u));
+        const RecSet P = fd->P;
+        if (n <= 40ull * R)
+            SG_LAUNCH(c, "emit_uniq", k_emit_uniq_diff<EM_WIN_S>, ntiles, EM_BLOCK, 0, cache, R, pre, Sb, ub, K, P, lbub,
+                      lbub + ntiles, base, ff, ftot);
+        else
+            SG_LAUNCH(c, "emit_uniq", k_emit_uniq_diff<EM_WIN>, ntiles, EM_BLOCK, 0, cache, R, pre, Sb, ub, K, P, lbub,
+                      lbub + ntiles, base, ff, ftot);
+        SG_TRY(tile_scan(c, ftot, ntiles, fpre, ftotal, fd->of ? fd->of->shift() : 0u));
+        SG_LAUNCH(c, "emit_fresh", k_emit_fresh_f, ntiles, EM_BLOCK, 0, cache, R, fpre, Sb, fout, ff);
+        // the unique and new totals and the run-sort error word with one host sync
+        uint8_t *pin = (uint8_t *)c->pinned;
+        SG_HIP(hipMemcpyAsync(pin, total, 16, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipMemcpyAsync(pin + 16, ftotal, 8, hipMemcpyDeviceToHost, c->stream));
+        SG_HIP(hipStreamSynchronize(c->stream));
+        uint64_t tt = 0, tf = 0;
+        uint32_t e = 0;
+        memcpy(&tt, pin, 8);
+        memcpy(&e, pin + 8, 4);
+        memcpy(&tf, pin + 16, 8);
+        if (nb && e) { set_error("run sort: segment bound violated (0x%x)", e); return SG_E_HIP; }
+        const uint32_t t1 = (uint32_t)(tt >> 32), t2 = (uint32_t)tt;
+        // model: cached span + key per record, kept bytes read + written, the prior's keys and
+        // spans of the tile ranges and its compared bytes (~ the prior), a flag per item; the
+        // new-record emit: cached span + flag per item, new bytes read + written
+        if (c->profile) {
+            prof_bytes(c, "emit_uniq", 16.0 * R + 2.0 * t2 + 16.0 * P.n + (double)fd->prior_bytes + R);
+            prof_bytes(c, "emit_fresh", 9.0 * R + 2.0 * (double)(uint32_t)tf);
+        }
+        fd->fresh = fout;
+        fd->fresh_bytes = (uint32_t)tf;
+        fd->fresh_records = (uint32_t)(tf >> 32);
+        *uv = UView{ub, nullptr, nullptr, t1, t2, R};
+        return SG_OK;
+    }
     SG_TRY(slot(c, vs.uspans, R, &us));
     SG_TRY(slot(c, vs.ukeys, R, &uk));
     uint64_t *uc;
@@ -1773,13 +2044,28 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint32_t bk = make_bk(base, kw);
     if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, bk));
     UView cu;
-    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, want_hist ? &ks : nullptr));
+    // the diff fused into cur's unique emit (a prior with records, cur sorted: R > 1)
+    FusedDiff fdd;
+    const bool fuse = have_prior && pv.n > 0 && Lc.n_rec > 1 && sw_fused_diff();
+    if (fuse) {
+        fdd.P = RecSet{pv.buf, pv.spans, pv.keys, pv.n};
+        fdd.prior_bytes = n_prior;
+        fdd.of = of;
+    }
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, want_hist ? &ks : nullptr,
+                        fuse ? &fdd : nullptr));
     res->in_records = cu.in_records;
     res->uniq = ou ? ou->p : const_cast<uint8_t *>(cu.buf);
     res->uniq_bytes = cu.bytes;
     res->uniq_records = cu.n;
     if (!want_fresh) return SG_OK;
     res->prior_records = pv.in_records;
+    if (fuse && fdd.fresh) {
+        res->fresh = of ? of->p : fdd.fresh;
+        res->fresh_bytes = fdd.fresh_bytes;
+        res->fresh_records = fdd.fresh_records;
+        return SG_OK;
+    }
     if (pv.n == 0 || cu.n == 0) {
         res->fresh = res->uniq;
         res->fresh_bytes = res->uniq_bytes;

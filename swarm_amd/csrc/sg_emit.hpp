@@ -352,14 +352,17 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_count(Item item, uint32_t n, 
 // TS (SPARSE only): records sourced from the sorted staging T (wave_copy_round); every record
 // shares its first bs <= 48 bytes (the common prefix), taken from item 0's record (the first
 // in sort order: never a duplicate, so its cache entry holds its span).
-template <bool SPARSE, uint32_t WIN = EM_WIN, bool TWO = false, bool TS = false, bool TSP = false>
+// K2: an item is kept only where keep2[i] != 0 as well (the new-record emit over the sorted
+// items, with the unique emit's cache and the fused diff's flags).
+template <bool SPARSE, uint32_t WIN = EM_WIN, bool TWO = false, bool TS = false, bool TSP = false, bool K2 = false>
 __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache, uint32_t n,
                                                 const uint64_t *__restrict__ pre,
                                                 const uint8_t *__restrict__ src, const uint8_t *__restrict__ src2,
                                                 uint8_t *__restrict__ dst,
                                                 uint2 *__restrict__ out_spans,
                                                 const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
-                                                const uint4 *__restrict__ T = nullptr, uint32_t bs = 0) {
+                                                const uint4 *__restrict__ T = nullptr, uint32_t bs = 0,
+                                                const uint8_t *__restrict__ keep2 = nullptr) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4][WIN];
     __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
     __shared__ uint64_t s_wt[4];
@@ -389,16 +392,18 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
     // the rounds' cache entries loaded together (clamped index, no bounds branch: a branch
     // per round kept each load behind the previous round's wait)
     uint2 cvr[EM_ROUNDS];
+    uint8_t k2v[EM_ROUNDS];
 #pragma unroll
     for (int r = 0; r < EM_ROUNDS; ++r) {
         const uint32_t i = wbase + r * 64u + lane;
         cvr[r] = cache[i < n ? i : n - 1u];
+        k2v[r] = K2 ? keep2[i < n ? i : n - 1u] : (uint8_t)1;
     }
 #pragma unroll
     for (int r = 0; r < EM_ROUNDS; ++r) {
         const uint32_t i = wbase + r * 64u + lane;
         const uint2 cv = (i < n) ? cvr[r] : make_uint2(0u, EM_DROP);
-        const bool f = cv.y != EM_DROP;
+        const bool f = cv.y != EM_DROP && k2v[r] != 0;
         st[r] = cv.x;
         ln[r] = f ? cv.y : 0u;
         const uint64_t v = f ? (EM_ONE | (uint64_t)(cv.y + 1u)) : 0ull;
@@ -494,6 +499,12 @@ SG_EMIT_APPLY(k_emit_apply, false, EM_WIN)
         uint32_t bs) {                                                                                    \
         emit_apply_body<true, WIN, false, true, TSP>(cache, n, pre, src, nullptr, dst, out_spans, kin, kout, T, bs); \
     }
+__global__ __launch_bounds__(EM_BLOCK) void k_emit_fresh_f(const uint2 *__restrict__ cache, uint32_t n,
+                                                           const uint64_t *__restrict__ pre, const uint8_t *__restrict__ src,
+                                                           uint8_t *__restrict__ dst, const uint8_t *__restrict__ keep2) {
+    emit_apply_body<true, EM_WIN, false, false, false, true>(cache, n, pre, src, nullptr, dst, nullptr, nullptr, nullptr,
+                                                             nullptr, 0, keep2);
+}
 SG_EMIT_APPLY_T(k_emit_uniq_t, EM_WIN_S, false)   // no common prefix
 SG_EMIT_APPLY_T(k_emit_uniq_tp, EM_WIN_S, true)   // records share a prefix (URL lists)
 #undef SG_EMIT_APPLY_T

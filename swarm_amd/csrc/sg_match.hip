@@ -228,8 +228,8 @@ static int build_ac(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint3
 // a set bit is confirmed against the bucket's entry fingerprints (rank + CSR), then the
 // whole pattern is byte-compared.
 constexpr uint32_t LIT_CLASSES = 6;
-// Scheme choice (dev_match): one verified candidate costs about LIT_KAPPA LDS bitmap probes.
-constexpr double LIT_KAPPA = 24.0;
+// Scheme choice (dev_match): the joint scheme must be at least 10 % faster on the trial.
+constexpr float LIT_MARGIN = 0.9f;
 constexpr uint32_t LIT_J = 5;  // the joint class
 __host__ __device__ constexpr uint32_t lit_len(uint32_t c) { return c < 3 ? c + 1 : (c == 3 ? 4 : (c == 4 ? 8 : 5)); }
 // class-set templates of k_lit_scan: two-class {4-7, 8+}, {3, 4-7, 8+}, all; joint {J},
@@ -816,9 +816,7 @@ __device__ __forceinline__ void lit_emit(const Args &a, Push &push, uint32_t rec
 // then compacted into an LDS queue and pass 2 spreads them over all lanes: confirm against
 // the bucket's entry fingerprints, then byte-compare the pattern (16-B rows from L2, text
 // from the LDS tile). Hits go through a per-block LDS buffer flushed with one atomic.
-// COUNT (the scheme trial, k_lit_trial): pass 1 only; each tile adds its candidate count to
-// a.hit_count (deterministic, unlike a timing) and nothing else is written.
-template <int BLK, int BPT, uint32_t CM, bool COUNT>
+template <int BLK, int BPT, uint32_t CM>
 __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
     constexpr int TILE = BLK * BPT;
     constexpr int NW = BPT / 4;
@@ -994,11 +992,6 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
         for (uint32_t c = 0; c < LIT_CLASSES; ++c) ncand += (uint32_t)__popcll(cand[c]);
         uint32_t qtot;
         const uint32_t qex = block_excl_scan<BLK>(ncand, &qtot, s_red);
-        if constexpr (COUNT) {
-            if (t == 0 && qtot) atomicAdd(a.hit_count, qtot);
-            __syncthreads();  // the tile buffers are rewritten by the next tile
-            continue;
-        }
         const uint32_t lrec0 = excl;  // tile-local index of this thread's first record start
         for (uint32_t r0 = 0; r0 < qtot; r0 += LS_Q) {
             uint32_t qi = qex;
@@ -1119,14 +1112,14 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
 
 template <int BLK, int BPT, uint32_t CM>
 __global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
-    lit_scan_body<BLK, BPT, CM, false>(a);
+    lit_scan_body<BLK, BPT, CM>(a);
 }
 
-// The class-scheme trial (candidates counted over the first tiles): its own symbol, so kernel
-// statistics and PMC passes of k_lit_scan hold the real scans only.
+// The class-scheme trial (the same scan over the first tiles, every output dropped): its own
+// symbol, so kernel statistics and PMC passes of k_lit_scan hold the real scans only.
 template <int BLK, int BPT, uint32_t CM>
 __global__ __launch_bounds__(BLK) void k_lit_trial(LitArgs a) {
-    lit_scan_body<BLK, BPT, CM, true>(a);
+    lit_scan_body<BLK, BPT, CM>(a);
 }
 
 // LDS bytes of k_lit_scan's dynamic tables for a filter (entries in LDS when they fit).
@@ -1786,13 +1779,13 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         return SG_OK;
     };
     // The class scheme of a filter (two-class or joint, see build_lit): decided once per
-    // matcher, on the first input large enough to tell (until then the two-class scheme runs),
-    // by a cost model over DETERMINISTIC counts: both schemes' probe pass runs over the first
-    // tiles counting candidates only (k_lit_trial), and
-    //   cost = LDS probes per position x positions + LIT_KAPPA x candidates,
-    // a candidate (queue slot, bucket record, fingerprint, byte verify) costing about LIT_KAPPA
-    // probes (fitted on C3, X1, C4 and the fields JSON: DESIGN.md §4). The same input always
-    // picks the same scheme; SG_LIT_SCHEME=0/1 forces one.
+    // matcher, on the first input large enough to tell (until then the two-class scheme runs):
+    // both schemes scan the first tiles (k_lit_trial, outputs dropped), three times each after
+    // a warm-up, and the joint scheme is kept only if its best time beats the two-class one's
+    // by LIT_MARGIN — so near-ties always resolve to the two-class scheme, and a choice never
+    // flips between runs on the measured inputs (C3/X1: joint 20-30 % faster; C4 banners and
+    // the fields JSON: joint 1.9-2.2x slower, although it passes FEWER candidates there: the
+    // candidate count does not predict the cost). SG_LIT_SCHEME=0/1 forces one.
     auto scheme = [&](const sg_matcher::Lit &two, const sg_matcher::Lit &joint, std::atomic<int> &mode,
                       const uint32_t *fo, const uint32_t *fp) -> const sg_matcher::Lit & {
         const int forced = sw_lit_scheme();
@@ -1801,21 +1794,27 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         constexpr uint32_t TRIAL_TILES = 2048, MIN_TILES = 1024;
         if (m < 0 && L.n_tiles >= MIN_TILES) {
             const uint32_t tt = std::min<uint32_t>(L.n_tiles, TRIAL_TILES);
-            bool ok = hipMemsetAsync(cnt + 4, 0, 8, c->stream) == hipSuccess;
-            ok = ok && run_lit("lit_trial", two, nullptr, cnt + 4, 0u, fo, fp, tt) == SG_OK;
-            ok = ok && run_lit("lit_trial", joint, nullptr, cnt + 5, 0u, fo, fp, tt) == SG_OK;
-            uint32_t cc[2] = {0u, 0u};
-            ok = ok && ctx_readback(c, cc, cnt + 4, 8) == SG_OK;
+            hipEvent_t ev[2];
+            for (auto &e : ev) (void)hipEventCreate(&e);
+            float best[2] = {1e30f, 1e30f};
+            bool ok = true;
+            for (int rep = 0; rep < 4 && ok; ++rep) {  // rep 0 warms caches and code
+                for (int sch = 0; sch < 2 && ok; ++sch) {
+                    (void)hipEventRecord(ev[0], c->stream);
+                    ok = run_lit("lit_trial", sch ? joint : two, nullptr, cnt + 4, 0u, fo, fp, tt) == SG_OK;
+                    (void)hipEventRecord(ev[1], c->stream);
+                    ok = ok && hipEventSynchronize(ev[1]) == hipSuccess;
+                    float ms = 0.f;
+                    if (ok && rep > 0 && hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) best[sch] = std::min(best[sch], ms);
+                }
+            }
+            for (auto &e : ev) (void)hipEventDestroy(e);
             if (ok) {
-                const double P = std::min<double>((double)tt * L.tile_bytes, (double)n);
-                const double c2 = __builtin_popcount(two.tmpl) * P + LIT_KAPPA * cc[0];
-                const double cj = __builtin_popcount(joint.tmpl) * P + LIT_KAPPA * cc[1];
-                m = cj < c2 ? 1 : 0;
+                m = best[1] < LIT_MARGIN * best[0] ? 1 : 0;
                 mode.store(m);
                 if (sw_lit_trial_log())
-                    fprintf(stderr, "sg lit scheme: positions %.0f cand two %u (%u probes) joint %u (%u probes) -> %s\n", P,
-                            cc[0], (unsigned)__builtin_popcount(two.tmpl), cc[1],
-                            (unsigned)__builtin_popcount(joint.tmpl), m ? "joint" : "two");
+                    fprintf(stderr, "sg lit scheme: trial %u tiles, best two %.3f ms joint %.3f ms -> %s\n", tt, best[0], best[1],
+                            m ? "joint" : "two");
             }
         }
         return m == 1 ? joint : two;

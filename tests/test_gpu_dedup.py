@@ -546,17 +546,20 @@ def test_key_stats_rare_digits(sg, shape):
 
 # ------------------------------------------------------------------ sorted staging (T)
 @pytest.mark.parametrize("shape", ["mixed_long", "slot_edges", "url_prefix", "nul_cr"])
-@pytest.mark.parametrize("stage", ["1", "0"])
-def test_staged_dedup_shapes(sg, monkeypatch, shape, stage):
+@pytest.mark.parametrize("stage,fused", [("1", "1"), ("0", "1"), ("0", "0"), ("1", "0")])
+def test_staged_dedup_shapes(sg, monkeypatch, shape, stage, fused):
     """The dedup with the sorted staging (k_stage: each record gathered once into a 32-B slot
     of its bytes past the common prefix) and without it (SG_STAGE=0), against the oracle:
     mixed_long: short records beside records too long for a slot (compared and emitted from
     the input), many sharing their first 7+ bytes (segment sorts on slots, long pairs past the
     slot); slot_edges: lengths 29..34 past the prefix around the 31-byte slot; url_prefix: a
     common 'https://' prefix (slots start after it, the emit writes it back); nul_cr: NUL, CR
-    and 0xff bytes inside slots (zero padding must not tie a NUL byte with the record end)."""
+    and 0xff bytes inside slots (zero padding must not tie a NUL byte with the record end).
+    fused: the new-record diff inside the unique emit (k_emit_uniq_diff, the default) or as
+    its own pass over the unique output (SG_FUSED_DIFF=0)."""
     import torch
     monkeypatch.setenv("SG_STAGE", stage)
+    monkeypatch.setenv("SG_FUSED_DIFF", fused)
     rng = np.random.default_rng({"mixed_long": 21, "slot_edges": 22, "url_prefix": 23, "nul_cr": 24}[shape])
     n = 200_000
     if shape == "mixed_long":
@@ -587,5 +590,35 @@ def test_staged_dedup_shapes(sg, monkeypatch, shape, stage):
         eu, ef = S.dedup_diff(cur, prior)
         assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
         assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_fused_diff_prior_shapes(sg, monkeypatch, fused):
+    """The diff inside the unique emit against priors that stress its per-tile prior ranges:
+    a prior far denser than cur (emit tiles whose staged prior range overflows the LDS), runs
+    of prior records sharing key0 with distinct tails (binary search by full compare), a prior
+    sharing only some keys, and a cur whose last records sort above every prior record."""
+    import torch
+    monkeypatch.setenv("SG_FUSED_DIFF", fused)
+    rng = np.random.default_rng(31)
+    alpha = np.frombuffer(b"abcdefgh", dtype=np.uint8)
+    body = alpha[rng.integers(0, 8, size=(120_000, 9))]
+    recs = [bytes(r) for r in body]
+    prior_recs = set(recs[::2])
+    prior_recs |= {b"abcdefgh" + bytes(alpha[rng.integers(0, 8, size=6)]) for _ in range(60_000)}
+    prior_recs |= {bytes(alpha[rng.integers(0, 8, size=5)]) for _ in range(20_000)}
+    cur = b"\n".join(recs + [b"zzzz-last", b"abcdefghabc"]) + b"\n"
+    prior = S.serialize(sorted(prior_recs))
+    dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+    dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        r = ctx.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+        eu, ef = S.dedup_diff(cur, prior)
+        assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+        assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+        assert r.fresh_records == ef.count(b"\n")
     finally:
         ctx.close()

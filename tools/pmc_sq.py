@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Per-kernel averages of the SQ/TCC counter passes written by tools/pmc_sq.sh.
-  python tools/pmc_sq.py gpurun_out/<tag> [out.md]"""
+"""Per-kernel averages of the SQ/TCC counter passes written by tools/gpu.sh sq:<leg>.
+  python tools/pmc_sq.py gpurun_out/<tag>/sq_<leg> [out.md]   (reads sq_<leg>_p*/)"""
 import csv
 import glob
 import os
@@ -11,7 +11,7 @@ from collections import defaultdict
 def main():
     src = sys.argv[1]
     acc = defaultdict(lambda: defaultdict(list))
-    for f in glob.glob(os.path.join(src, "p*", "p_counter_collection.csv")):
+    for f in glob.glob(src + "_p*/p_counter_collection.csv") + glob.glob(os.path.join(src, "p*", "p_counter_collection.csv")):
         for row in csv.DictReader(open(f)):
             acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     cols = ["SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
