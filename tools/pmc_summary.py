@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Summarise one gpu_round.sh run: rocprofv3 kernel stats + the FETCH_SIZE / WRITE_SIZE passes.
+"""Summarise one tools/gpu.sh session's prof:<leg> and pmc:<leg> steps: rocprofv3 kernel
+stats + the FETCH_SIZE / WRITE_SIZE passes.
 
-  python tools/pmc_summary.py gpurun_out/<tag> profiles/r01/<name>  [c2|c3 ...]
+  python tools/pmc_summary.py gpurun_out/<tag> profiles/r04/<name>  [leg[:workload] ...]
+
+(leg: the gpu.sh leg, e.g. c3p; workload: the key bench.py looks the traffic up under, e.g. c3.)
 
 Writes <name>_<wl>_kernels.csv (rocprofv3 --stats, verbatim), <name>_<wl>_summary.md and
 updates profiles/pmc_traffic.json (per-kernel HBM bytes per launch, read by bench.py).
@@ -67,17 +70,18 @@ def main():
     tfile = os.path.join(os.path.dirname(dst), "..", "pmc_traffic.json")
     tfile = os.path.normpath(tfile)
     traffic = json.load(open(tfile)) if os.path.exists(tfile) else {}
-    for wl in wls:
+    for spec in wls:
+        wl, key = (spec.split(":") + [spec])[:2] if ":" in spec else (spec, spec)
         ks = os.path.join(src, "prof_" + wl, wl + "_kernel_stats.csv")
         if not os.path.exists(ks):
             continue
-        shutil.copy(ks, "%s_%s_kernels.csv" % (dst, wl))
+        shutil.copy(ks, "%s_%s_kernels.csv" % (dst, key))
         st = stats(ks)
         used = {}
         fe = per_kernel_counter(os.path.join(src, "pmc_%s_FETCH_SIZE" % wl, "p_counter_collection.csv"), "FETCH_SIZE",
                                 used)
         wr = per_kernel_counter(os.path.join(src, "pmc_%s_WRITE_SIZE" % wl, "p_counter_collection.csv"), "WRITE_SIZE")
-        lines = ["# %s — rocprofv3 kernel stats + HBM traffic (%s)" % (wl.upper(), os.path.basename(src)), "",
+        lines = ["# %s — rocprofv3 kernel stats + HBM traffic (%s, leg %s)" % (key.upper(), os.path.basename(src), wl), "",
                  "FETCH_SIZE doubled (gfx950 wide-read correction), WRITE_SIZE as reported; both KiB→bytes, "
                  "per launch, averaged over the PMC pass's dispatches (the matching engines: over their full-size "
                  "dispatches only, the largest grid and at least half the longest duration there; `pmc launches` = "
@@ -86,7 +90,7 @@ def main():
                  "| kernel | calls | avg µs | % time | fetch MB/launch | write MB/launch | traffic GB/s | pmc launches |",
                  "|---|---|---|---|---|---|---|---|"]
         if fe or wr:  # a fresh PMC pass replaces the workload's rows (no stale kernels survive)
-            traffic[wl] = {}
+            traffic[key] = {}
         for k, (calls, avg_us, pct) in sorted(st.items(), key=lambda kv: -kv[1][2]):
             f = fe.get(k)
             w = wr.get(k)
@@ -98,13 +102,13 @@ def main():
                 "%.2f" % (w / 1e6) if w is not None else "-",
                 "%.0f" % gbs if gbs is not None else "-",
                 "%d/%d" % used[k] if k in used else "-"))
-            if (f is not None or w is not None) and wl in traffic:
-                traffic[wl][k] = {"fetch_bytes": round(2.0 * f) if f is not None else None,
+            if (f is not None or w is not None) and key in traffic:
+                traffic[key][k] = {"fetch_bytes": round(2.0 * f) if f is not None else None,
                                   "write_bytes": round(w) if w is not None else None,
                                   "bytes": round(tb), "avg_us": round(avg_us, 2),
                                   "source": os.path.join(os.path.basename(os.path.dirname(dst)),
-                                                         os.path.basename(dst) + "_" + wl + "_summary.md")}
-        with open("%s_%s_summary.md" % (dst, wl), "w") as f:
+                                                         os.path.basename(dst) + "_" + key + "_summary.md")}
+        with open("%s_%s_summary.md" % (dst, key), "w") as f:
             f.write("\n".join(lines) + "\n")
         print("\n".join(lines[:16]))
     with open(tfile, "w") as f:
