@@ -874,16 +874,10 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
     const uint32_t j0 = jb[t], j1 = jb[t + 1];
     const uint32_t np = j1 - j0;
     const bool staged = np <= DF_PCAP;
-    // touch the records' first lines as their spans arrive (the tile's prior records while they
-    // are staged, each thread's unique record before its search): the byte compares after the
-    // LDS search then hit L2 instead of waiting on HBM
-    uint32_t touch = 0;
     if (staged)
         for (uint32_t q = threadIdx.x; q < np; q += 256) {
             s_k[q] = key_narrow(P.K[j0 + q], kw);
-            const uint2 ps = P.sp[j0 + q];
-            s_sp[q] = ps;
-            touch ^= *reinterpret_cast<const uint32_t *>(P.buf + (ps.x & ~3u));
+            s_sp[q] = P.sp[j0 + q];
         }
     uint32_t idx[DF_PER], cand[DF_PER];
     uint64_t ku[DF_PER];
@@ -894,7 +888,6 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
         idx[k] = i0 + threadIdx.x + 256u * k;
         ku[k] = idx[k] < U.n ? U.K[idx[k]] : 0ull;
         us[k] = idx[k] < U.n ? U.sp[idx[k]] : make_uint2(0u, 0u);
-        if (idx[k] < U.n) touch ^= *reinterpret_cast<const uint32_t *>(U.buf + (us[k].x & ~3u));
     }
     __syncthreads();
 #pragma unroll
@@ -965,7 +958,6 @@ __device__ __forceinline__ void diff_tile_body(RecSet U, RecSet P, const uint32_
 #pragma unroll
     for (int k = 0; k < DF_PER; ++k)
         if (idx[k] < U.n) fresh[idx[k]] = pres[k] ? 0 : 1;
-    asm volatile("" ::"v"(touch));  // keeps the touch loads
 }
 
 __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uint32_t *__restrict__ jb,

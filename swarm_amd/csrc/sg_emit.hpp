@@ -399,16 +399,6 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
         cvr[r] = cache[i < n ? i : n - 1u];
         k2v[r] = K2 ? keep2[i < n ? i : n - 1u] : (uint8_t)1;
     }
-    // touch every kept record's first line now (its address is in the cache entry): the four
-    // rounds' records are fetched together, and the copy rounds below, which take the records
-    // in kept order one 64-record round at a time, find them in L2 instead of each waiting on
-    // HBM (one memory latency per wave instead of one per copy round)
-    uint32_t touch = 0;
-    if constexpr (!TS && !TWO) {
-#pragma unroll
-        for (int r = 0; r < EM_ROUNDS; ++r)
-            if (cvr[r].y != EM_DROP && k2v[r]) touch ^= *reinterpret_cast<const uint32_t *>(src + (cvr[r].x & ~3u));
-    }
 #pragma unroll
     for (int r = 0; r < EM_ROUNDS; ++r) {
         const uint32_t i = wbase + r * 64u + lane;
@@ -460,7 +450,6 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
             __builtin_amdgcn_wave_barrier();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
-        asm volatile("" ::"v"(touch));  // keeps the touch loads (their results are not needed)
         return;
     }
 #pragma unroll
@@ -485,7 +474,6 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    asm volatile("" ::"v"(touch));
 }
 
 #ifndef SG_EMIT_DEVICE_ONLY  // (a translation unit that only needs the copy helpers)
