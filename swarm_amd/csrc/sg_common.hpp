@@ -97,8 +97,10 @@ struct sg_ctx {
     size_t slot_cap[sg::S_NSLOTS] = {};
     void *pinned = nullptr;   // host pinned staging for small readbacks (SG_PINNED_BYTES)
     int last_path = 0;        // dedup/diff pipeline of the last call: 0 = the radix pipeline (the only one)
-    uint32_t last_flags = 0;  // dedup sort of the last call: bit 0 hybrid (local LDS sort), bit 1 its overflow re-sort
+    uint32_t last_flags = 0;  // dedup of the last call: bit 0 hybrid sort (local LDS sort), bit 1 its overflow
+                              // re-sort, bit 2 its overflow fix-up, bit 3 all-segments mode
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
+    float last_uniq_frac = 1.0f;  // dedup: unique / input records of the last sort -u (all-segments mode)
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
     uint64_t pt_keep_recs = 0;  // piece partition: records the last call kept between its passes
     // the last hybrid radix sort's local-sort plan (lsort_fixup redoes its flagged tiles)

@@ -36,6 +36,8 @@ const SlotSet CUR_SLOTS = {S_STARTS, S_ENDS, S_KEYS, S_KEYS2, S_VALS, S_VALS2, S
 const SlotSet PRIOR_SLOTS = {S_P_STARTS, S_P_ENDS, S_P_KEYS, S_P_KEYS2, S_P_VALS, S_P_VALS2, S_P_UNIQ, S_P_FLAG};
 
 constexpr uint32_t WAVE_GROUP = 64;
+// all-segments mode when the context's last sort -u kept less than this fraction of records
+constexpr float SEG_ALL_UNIQ = 0.4f;
 
 // ------------------------------------------------------------------ launch helpers
 // Queue one emit (no host sync): count pass, tile scan, apply pass. *total_out: device u64,
@@ -282,7 +284,11 @@ struct AdjLists {
     uint32_t cap_s, cap_b, cap_g;
 };
 
-template <bool KEYS, bool DUP>
+// ZD (with !DUP, the all-segments mode): no byte compares at all. A segment whose key0 holds
+// its records whole (tag below full) is a run of one record repeated (dup = not its head);
+// every other segment of two or more records is marked bad at its head, so the segment sorts
+// rank all of its members and set their dup flags (singletons: dup = 0).
+template <bool KEYS, bool DUP, bool ZD = false>
 __global__ __launch_bounds__(256) void k_adjacent2(const uint8_t *__restrict__ S, const uint2 *__restrict__ SS,
                                                    const uint64_t *__restrict__ K, uint8_t *__restrict__ brk, uint32_t n,
                                                    uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad, AdjLists L,
@@ -330,7 +336,21 @@ __global__ __launch_bounds__(256) void k_adjacent2(const uint8_t *__restrict__ S
         if constexpr (DUP) { x = SS[ip]; y = SS[i]; }
         head = (i == 0) || bb;
     }
-    if constexpr (!DUP) return;
+    if constexpr (!DUP) {
+        if constexpr (ZD) {
+            if (live) {
+                const bool whole = (ki & 0xffu) < bk_full(base);
+                if (head) {
+                    bool multi;
+                    if constexpr (KEYS) multi = i + 1 < n && K[i + 1] == ki;
+                    else multi = i + 1 < n && !brk[i + 1];
+                    if (multi && !whole) segbad[i] = 1;
+                }
+                dup[i] = (!head && whole) ? 1 : 0;
+            }
+        }
+        return;
+    }
     bool d = false;
     if (live && !head) {
         d = ((ki & 0xffu) < bk_full(base)) || rec_equal_w(S, x.x, x.y, S, y.x, y.y, bk_off(base));
@@ -1685,8 +1705,27 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     const bool staged = sw_stage() && R >= 4096 && Lb <= 48u && n <= (uint64_t)R * (28u + Lb);
     uint4 *T = nullptr;
     if (staged) SG_TRY(slot(c, S_STAGE, 2 * (size_t)R, &T));
+    // All-segments mode: when the last call on this context kept few of its records (most
+    // records repeat, and their groups hold near-duplicates: host:port scans, where a host's
+    // ports share key0 — C5), the adjacent pass compares no bytes and every segment of two
+    // or more records goes to the segment sorts, which rank its members and mark their
+    // duplicates: each grouped record is gathered once (by its segment sort) instead of twice
+    // (the adjacent compare, then the sort). Results are the same either way.
+    const int sa = sw_seg_all();
+    const bool seg_all = sa == 2 || (sa == 1 && c->last_uniq_frac < SEG_ALL_UNIQ);
+    if (seg_all) c->last_flags |= 8u;
     auto adjacent = [&](bool keys, bool with_dup, const uint8_t *Sb, const uint2 *SSp) -> int {
         SG_HIP(hipMemsetAsync(segbad, 0, cnt_off + 16, c->stream));  // head marks + list counters
+        if (seg_all && with_dup) {
+            if (keys)
+                SG_LAUNCH_B(c, "mark_groups", 10.0 * R, (k_adjacent2<true, false, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
+                            brk, R, dup, segbad, AL, base);
+            else
+                SG_LAUNCH_B(c, "mark_groups", 2.0 * R, (k_adjacent2<false, false, true>), grid_for(R, 256), 256, 0, Sb, SSp,
+                            K, brk, R, dup, segbad, AL, base);
+            SG_TRY(run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, &stot, stot_at));
+            return SG_OK;
+        }
         // model: key0 + span + brk + dup per record, the record's bytes gathered, its slot written
         const uint32_t sgrid = (uint32_t)(((uint64_t)R + 62) / 63 + 3) / 4;
         if (staged && with_dup && keys)
@@ -1867,6 +1906,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         fd->fresh_bytes = (uint32_t)tf;
         fd->fresh_records = (uint32_t)(tf >> 32);
         *uv = UView{ub, nullptr, nullptr, t1, t2, R};
+        if (vs.ubuf == CUR_VIEW.ubuf) c->last_uniq_frac = R ? (float)t1 / (float)R : 1.0f;
         return SG_OK;
     }
     SG_TRY(slot(c, vs.uspans, R, &us));
@@ -1895,6 +1935,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         if (e) { set_error("run sort: segment bound violated (0x%x)", e); return SG_E_HIP; }
     }
     *uv = UView{ub, us, uk, t1, t2, R};
+    if (vs.ubuf == CUR_VIEW.ubuf) c->last_uniq_frac = R ? (float)t1 / (float)R : 1.0f;
     return SG_OK;
 }
 

@@ -37,6 +37,12 @@ inline bool sw_stage() { return env_switch("SG_STAGE", false); }
 // its own pass over the unique output (k_diff_tile). Off: measured 534 us for the fused emit
 // against 438 for emit + split + diff + new-record count on C2.
 inline bool sw_fused_diff() { return env_switch("SG_FUSED_DIFF", false); }
+// The dedup's all-segments mode (sg_dedup.hip SEG_ALL_UNIQ): SG_SEG_ALL=0 never, 1 (default)
+// by the context's last unique fraction, 2 always (tests).
+inline int sw_seg_all() {
+    const char *v = getenv("SG_SEG_ALL");
+    return v ? atoi(v) : 1;
+}
 // SG_LIT_TRIAL_LOG=1: print the literal filter's scheme trial counts (calibration).
 inline bool sw_lit_trial_log() { return env_switch("SG_LIT_TRIAL_LOG", false); }
 // SG_TM_SORT=1: nuclei templates evaluated through the sort path instead of the

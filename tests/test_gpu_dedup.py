@@ -546,8 +546,9 @@ def test_key_stats_rare_digits(sg, shape):
 
 # ------------------------------------------------------------------ sorted staging (T)
 @pytest.mark.parametrize("shape", ["mixed_long", "slot_edges", "url_prefix", "nul_cr"])
-@pytest.mark.parametrize("stage,fused", [("1", "1"), ("0", "1"), ("0", "0"), ("1", "0")])
-def test_staged_dedup_shapes(sg, monkeypatch, shape, stage, fused):
+@pytest.mark.parametrize("stage,fused,segall", [("1", "1", "1"), ("0", "1", "2"), ("0", "0", "1"), ("1", "0", "2"),
+                                                ("0", "0", "2")])
+def test_staged_dedup_shapes(sg, monkeypatch, shape, stage, fused, segall):
     """The dedup with the sorted staging (k_stage: each record gathered once into a 32-B slot
     of its bytes past the common prefix) and without it (SG_STAGE=0), against the oracle:
     mixed_long: short records beside records too long for a slot (compared and emitted from
@@ -555,11 +556,13 @@ def test_staged_dedup_shapes(sg, monkeypatch, shape, stage, fused):
     slot); slot_edges: lengths 29..34 past the prefix around the 31-byte slot; url_prefix: a
     common 'https://' prefix (slots start after it, the emit writes it back); nul_cr: NUL, CR
     and 0xff bytes inside slots (zero padding must not tie a NUL byte with the record end).
-    fused: the new-record diff inside the unique emit (k_emit_uniq_diff, the default) or as
-    its own pass over the unique output (SG_FUSED_DIFF=0)."""
+    fused: the new-record diff inside the unique emit (SG_FUSED_DIFF=1) or as its own pass
+    over the unique output (the default); segall=2: the all-segments mode (no byte compares in
+    the adjacent pass, every segment of 2+ records ranked by the segment sorts)."""
     import torch
     monkeypatch.setenv("SG_STAGE", stage)
     monkeypatch.setenv("SG_FUSED_DIFF", fused)
+    monkeypatch.setenv("SG_SEG_ALL", segall)
     rng = np.random.default_rng({"mixed_long": 21, "slot_edges": 22, "url_prefix": 23, "nul_cr": 24}[shape])
     n = 200_000
     if shape == "mixed_long":
@@ -620,5 +623,36 @@ def test_fused_diff_prior_shapes(sg, monkeypatch, fused):
         assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
         assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
         assert r.fresh_records == ef.count(b"\n")
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("segall", ["2", "0"])
+def test_seg_all_mode_hostports(sg, monkeypatch, segall):
+    """host:port records (a host's ports share key0: segments of near-duplicates, C5's shape)
+    with repeats, short records held whole by key0 repeated > 64 times, and a big group
+    sharing 7+ bytes (refinement rounds, then the mode's pass over the sub-segments): the
+    all-segments mode (2) and the compare mode (0) both equal the oracle."""
+    import torch
+    monkeypatch.setenv("SG_SEG_ALL", segall)
+    rng = np.random.default_rng(41)
+    hosts = [b"h%05d.t%d.example.com" % (int(rng.integers(0, 30_000)), int(rng.integers(0, 5))) for _ in range(8000)]
+    ports = [b"22", b"80", b"443", b"8080", b"3389", b"21"]
+    recs = [hosts[int(rng.integers(0, len(hosts)))] + b":" + ports[int(rng.integers(0, 6))] for _ in range(150_000)]
+    recs += [b"a:1"] * 200 + [b"b"] * 90
+    recs += [b"sharedprefix-" + b"%d" % int(k) for k in rng.integers(0, 500, size=3000)]
+    rng.shuffle(recs)
+    cur = b"\n".join(recs) + b"\n"
+    prior = S.dedup(b"\n".join(recs[::5]) + b"\n")
+    dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+    dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        for _ in range(2):  # the second call sees the first one's unique fraction (auto mode)
+            r = ctx.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+            eu, ef = S.dedup_diff(cur, prior)
+            assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+            assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+            assert bool(ctx.last_path()[1] & 8) == (segall == "2")
     finally:
         ctx.close()
