@@ -1733,13 +1733,11 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     if (seg_all) c->last_flags |= 8u;
     auto adjacent = [&](bool keys, bool with_dup, const uint8_t *Sb, const uint2 *SSp) -> int {
         SG_HIP(hipMemsetAsync(segbad, 0, cnt_off + 16, c->stream));  // head marks + list counters
-        if (seg_all && with_dup) {
-            if (keys)
-                SG_LAUNCH_B(c, "mark_groups", 10.0 * R, (k_adjacent2<true, false, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
-                            brk, R, dup, segbad, AL, base);
-            else
-                SG_LAUNCH_B(c, "mark_groups", 2.0 * R, (k_adjacent2<false, false, true>), grid_for(R, 256), 256, 0, Sb, SSp,
-                            K, brk, R, dup, segbad, AL, base);
+        // (keys only: after refinement rounds a segment of more than 64 identical records may
+        // remain — rounds stop where the records end — which only the byte compare marks)
+        if (seg_all && with_dup && keys) {
+            SG_LAUNCH_B(c, "mark_groups", 10.0 * R, (k_adjacent2<true, false, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
+                        brk, R, dup, segbad, AL, base);
             SG_TRY(run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, &stot, stot_at));
             return SG_OK;
         }
