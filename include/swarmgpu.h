@@ -78,9 +78,14 @@ int sg_ctx_memcpy(sg_ctx *ctx, void *dst, const void *src, size_t n);
  * pipeline — since round 3 the only one in the library (the bucket sample sort and the probe
  * path, both measured slower, live in tools/experiments/); *flags: bit 0 (SG_SORT_HYBRID) the
  * current scan's sort ran its top digits globally and finished each group in LDS, bit 1
- * (SG_SORT_RESORTED) a group did not fit and the plain LSD sort ran again. For tests/benchmarks. */
+ * (SG_SORT_RESORTED) the plain LSD sort ran again, bit 2 (SG_SORT_FIXUP) a group outgrew the
+ * local sort's LDS and its tiles were sorted again, bit 3 (SG_SEG_ALL) the all-segments mode
+ * (every segment of 2+ records ranked by the segment sorts, no adjacent byte compare). For
+ * tests/benchmarks. */
 #define SG_SORT_HYBRID 1u
 #define SG_SORT_RESORTED 2u
+#define SG_SORT_FIXUP 4u
+#define SG_SEG_ALL 8u
 #define SG_PATH_RADIX 0
 int sg_ctx_last_path(sg_ctx *ctx, int *path, uint32_t *flags);
 /* Sort-key width (bytes after the common prefix, 5..7) the last radix dedup chose from the

@@ -376,7 +376,8 @@ class Context:
     def last_path(self):
         """(pipeline, flags) of the last dedup_diff on this context: ("radix", flags) — the only
         pipeline in the library; flags bit 0: hybrid sort (top digits global, groups finished
-        in LDS), bit 1: a group overflowed the LDS and the plain LSD sort ran again
+        in LDS), bit 1: the plain LSD sort ran again, bit 2: a group overflowed the local sort's
+        LDS and its tiles were sorted again (k_rs_lsort_fix), bit 3: the all-segments mode
         (include/swarmgpu.h sg_ctx_last_path)."""
         p, f = C.c_int(), C.c_uint32()
         check(lib.sg_ctx_last_path(self._h, C.byref(p), C.byref(f)))

@@ -372,11 +372,9 @@ static int pack_byte_splitters(const uint8_t *splitters, const uint32_t *split_o
 // Pass 2 of the piece partition, one tile of PT_TILE records per block (the piece's records in
 // input order): each record's part (k_range_bytes' key), a stable rank by part inside the tile
 // (8 wave64 ballots per item, as the radix downsweep), the records' bytes scanned in part
-// order, and each record copied by its own lane to part base + tile offset + offset in the
-// part's run — consecutive lanes write consecutive bytes of one part, and the reads stay
-// inside the tile's ~100 KB of input; the copy goes part run by part run, 64 records per wave
-// task, through the wave's LDS window (whole 16-B stores). Replaces a radix sort of the record
-// ids by part and one gather-emit per part (random 27-B reads: C5's part_emit ran at ~1.6 TB/s).
+// order, and each record copied by its own lane, in input order, to part base + tile offset +
+// offset in the part's run. Replaces a radix sort of the record ids by part and one
+// gather-emit per part (random 27-B reads: C5's part_emit ran at ~1.6 TB/s).
 constexpr int PT_BLOCK = 256;
 constexpr int PT_ITEMS = 16;
 constexpr uint32_t PT_TILE = PT_BLOCK * PT_ITEMS;
@@ -435,8 +433,6 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     __shared__ uint32_t s_red[NW];
     __shared__ uint2 s_sp[PT_TILE];
     __shared__ uint32_t s_off[PT_TILE];
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[NW][EM_WIN_S];
-    __shared__ uint32_t s_csrc[NW][64], s_clen[NW][64], s_cdst[NW][64];
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
     for (int x = tid; x < NW * 256; x += PT_BLOCK) (&s_wh[0][0])[x] = 0;
     __syncthreads();
@@ -505,37 +501,29 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         }
     }
     __syncthreads();
-    // copy: part by part, 64 sorted positions of one part per wave task, each task one
-    // contiguous destination run assembled in the wave's LDS window and written with whole
-    // 16-B stores (emit's wave_copy_round). Lane stores of byte-aligned records straight to
-    // HBM (round 3) made L2 fetch every partially written destination line: PMC 6.1 GB read
-    // per 1.6 GB piece (2.5x), the reads of the tile and its spans being 2.4 GB.
-    uint32_t task = 0;
-    for (uint32_t p = 0; p < 256; ++p) {
-        const uint32_t a = s_dstart[p], b = (p == 255) ? n_t : min(s_dstart[p + 1], n_t);
-        if (a >= b) continue;
-        for (uint32_t c0 = a; c0 < b; c0 += 64, ++task) {
-            if (task % NW != (uint32_t)wid) continue;  // wave-uniform
-            const uint32_t q = c0 + (uint32_t)lane;
-            const bool f = q < b;
-            const uint32_t qq = f ? q : c0;
-            const uint2 x = s_sp[qq];
-            const uint32_t len = f ? x.y - x.x : 0u;
-            const uint64_t dst = s_dst[p] + s_off[qq];
-            const uint32_t last = (b - c0 >= 64u) ? 63u : b - c0 - 1u;
-            const uint64_t o0 = __shfl(dst, 0, 64);
-            const uint64_t oend = __shfl(dst + len + 1u, (int)last, 64);
-            const uint64_t base = o0 & ~15ull;
-            wave_copy_round<EM_WIN_S>(buf, nullptr, out, s_win[wid], s_csrc[wid], s_clen[wid], s_cdst[wid], f, x.x, len,
-                                      (uint32_t)(dst - base), o0, oend, base);
-            __builtin_amdgcn_wave_barrier();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (so.sp && f) {  // also the record's span inside its part and its key, at its index in the parts
-                const uint64_t g = s_g0[p] + q;
-                const uint32_t rel = (uint32_t)(dst - s_pst[p]);
-                so.sp[g] = make_uint2(rel, rel + len);
-                so.keys[g] = chunk_key(buf, x.x, x.y, 0u);
-            }
+    // copy in input order: lane-owned input record (a wave's 64 consecutive records: its loads
+    // read one contiguous run of the tile) to its sorted position's place in its part. Round
+    // 3 copied by sorted position (consecutive lanes, consecutive destination bytes), so each
+    // wave's loads scattered over the whole ~130 KB tile: with ~13 MB of tiles in flight per
+    // XCD (LDS-resident blocks), the 4 MB L2 re-fetched input lines (PMC: 6.1 GB read per
+    // 1.6 GB piece against 2.4 GB of tile and spans).
+#pragma unroll 2
+    for (int i = 0; i < PT_ITEMS; ++i) {
+        const uint32_t pos = wbase + i * 64 + lane;
+        if (pos >= R) break;  // positions grow with i
+        const uint32_t p = d[i];
+        const uint32_t q = s_dstart[p] + s_wh[wid][p] + r[i];
+        const uint2 x = s_sp[q];
+        const uint64_t dst = s_dst[p] + s_off[q];
+        if (so.sp) {  // also the record's span inside its part and its key, at its index in the parts
+            uint64_t k0;
+            put_medium<true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
+            const uint64_t g = s_g0[p] + q;
+            const uint32_t rel = (uint32_t)(dst - s_pst[p]);
+            so.sp[g] = make_uint2(rel, rel + (x.y - x.x));
+            so.keys[g] = k0;
+        } else {
+            put_medium(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
         }
     }
 }

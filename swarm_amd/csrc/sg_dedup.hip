@@ -1785,11 +1785,14 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // With narrowed keys (kw < 7: few big groups) the adjacent compare runs before the group
     // count comes back (one host sync for everything); when big groups exist (the 7-byte key
     // was kept: low-entropy text) the groups are marked first and compared after refinement.
+    // In the all-segments mode the keys pass compares no bytes either way, so it marks the
+    // segments at once; only when big groups come back does the byte pass follow refinement.
     const bool speculate = (base >> 16) < 7u;
+    const bool first_dup = speculate || seg_all;
     bool fix_tried = false;
     for (;;) {
-        SG_TRY(adjacent(true, speculate, d_buf, V));
-        SG_TRY(read_counts(speculate));
+        SG_TRY(adjacent(true, first_dup, d_buf, V));
+        SG_TRY(read_counts(first_dup));
         if (!lerr_v) break;
         uint64_t *Ka = (K == L.keys) ? k2 : L.keys;
         uint2 *Va = (V == L.spans) ? v2 : L.spans;
@@ -1820,7 +1823,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // each kept record once.
     uint8_t *Sb = const_cast<uint8_t *>(d_buf);
     uint2 *SS = V;  // the segment sorts permute it in place
-    if (!speculate || B) {
+    if (!first_dup || B) {
         SG_TRY(adjacent(false, true, Sb, SS));
         SG_TRY(read_counts(true));
     }

@@ -628,15 +628,22 @@ def test_fused_diff_prior_shapes(sg, monkeypatch, fused):
 
 
 @pytest.mark.parametrize("segall", ["2", "0"])
-def test_seg_all_mode_hostports(sg, monkeypatch, segall):
+@pytest.mark.parametrize("names", ["digits", "letters"])
+def test_seg_all_mode_hostports(sg, monkeypatch, segall, names):
     """host:port records (a host's ports share key0: segments of near-duplicates, C5's shape)
     with repeats, short records held whole by key0 repeated > 64 times, and a big group
     sharing 7+ bytes (refinement rounds, then the mode's pass over the sub-segments): the
-    all-segments mode (2) and the compare mode (0) both equal the oracle."""
+    all-segments mode (2) and the compare mode (0) both equal the oracle. digits: low-entropy
+    names keep the 7-byte key (marking pass first, as C5's range parts); letters: a narrowed
+    key (the adjacent pass runs before the big-group count comes back)."""
     import torch
     monkeypatch.setenv("SG_SEG_ALL", segall)
     rng = np.random.default_rng(41)
-    hosts = [b"h%05d.t%d.example.com" % (int(rng.integers(0, 30_000)), int(rng.integers(0, 5))) for _ in range(8000)]
+    if names == "digits":
+        hosts = [b"h%05d.t%d.example.com" % (int(rng.integers(0, 30_000)), int(rng.integers(0, 5))) for _ in range(8000)]
+    else:
+        alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", dtype=np.uint8)
+        hosts = [bytes(alpha[rng.integers(0, 26, size=int(rng.integers(6, 14)))]) + b".example.net" for _ in range(8000)]
     ports = [b"22", b"80", b"443", b"8080", b"3389", b"21"]
     recs = [hosts[int(rng.integers(0, len(hosts)))] + b":" + ports[int(rng.integers(0, 6))] for _ in range(150_000)]
     recs += [b"a:1"] * 200 + [b"b"] * 90
@@ -654,5 +661,6 @@ def test_seg_all_mode_hostports(sg, monkeypatch, segall):
             assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
             assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
             assert bool(ctx.last_path()[1] & 8) == (segall == "2")
+            assert (ctx.last_key_width() == 7) == (names == "digits")
     finally:
         ctx.close()
