@@ -372,8 +372,9 @@ static int pack_byte_splitters(const uint8_t *splitters, const uint32_t *split_o
 // Pass 2 of the piece partition, one tile of PT_TILE records per block (the piece's records in
 // input order): each record's part (k_range_bytes' key), a stable rank by part inside the tile
 // (8 wave64 ballots per item, as the radix downsweep), the records' bytes scanned in part
-// order, and each record copied by its own lane, in input order, to part base + tile offset +
-// offset in the part's run. Replaces a radix sort of the record ids by part and one
+// order, and each record copied by its own lane to part base + tile offset + offset in the
+// part's run — consecutive lanes write consecutive bytes of one part, and the reads stay
+// inside the tile's ~100 KB of input. Replaces a radix sort of the record ids by part and one
 // gather-emit per part (random 27-B reads: C5's part_emit ran at ~1.6 TB/s).
 constexpr int PT_BLOCK = 256;
 constexpr int PT_ITEMS = 16;
@@ -501,25 +502,23 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         }
     }
     __syncthreads();
-    // copy in input order: lane-owned input record (a wave's 64 consecutive records: its loads
-    // read one contiguous run of the tile) to its sorted position's place in its part. Round
-    // 3 copied by sorted position (consecutive lanes, consecutive destination bytes), so each
-    // wave's loads scattered over the whole ~130 KB tile: with ~13 MB of tiles in flight per
-    // XCD (LDS-resident blocks), the 4 MB L2 re-fetched input lines (PMC: 6.1 GB read per
-    // 1.6 GB piece against 2.4 GB of tile and spans).
-#pragma unroll 2
-    for (int i = 0; i < PT_ITEMS; ++i) {
-        const uint32_t pos = wbase + i * 64 + lane;
-        if (pos >= R) break;  // positions grow with i
-        const uint32_t p = d[i];
-        const uint32_t q = s_dstart[p] + s_wh[wid][p] + r[i];
+    // copy: sorted position q by lane q (consecutive lanes, consecutive bytes of one part)
+    for (uint32_t q = tid; q < n_t; q += PT_BLOCK) {
+        // the part of sorted position q: the last part whose run starts at or before q
+        uint32_t lo = 0, hi = 256;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_dstart[mid] <= q) lo = mid; else hi = mid;
+        }
+        // parts with empty runs share a start: take the last part starting at or before q
+        // whose run is non-empty (s_dstart is non-decreasing, so lo is that part)
         const uint2 x = s_sp[q];
-        const uint64_t dst = s_dst[p] + s_off[q];
+        const uint64_t dst = s_dst[lo] + s_off[q];
         if (so.sp) {  // also the record's span inside its part and its key, at its index in the parts
             uint64_t k0;
             put_medium<true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
-            const uint64_t g = s_g0[p] + q;
-            const uint32_t rel = (uint32_t)(dst - s_pst[p]);
+            const uint64_t g = s_g0[lo] + q;
+            const uint32_t rel = (uint32_t)(dst - s_pst[lo]);
             so.sp[g] = make_uint2(rel, rel + (x.y - x.x));
             so.keys[g] = k0;
         } else {

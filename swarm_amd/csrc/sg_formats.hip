@@ -350,31 +350,29 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
         // non-blank bytes (found after the walk). Escapes act inside strings only, as in a
         // byte walk: a backslash escapes the next byte, whatever it is.
         uint32_t esc_pos = JS_NONE;
-        // 128-byte steps on cache-line boundaries: a lane's eight 16-B loads of a step cover one
-        // whole line (requested once, not once per 64-B half: with 4M lines of ~660 B walked by
-        // independent lanes, a line was evicted between a lane's two halves and fetched again,
-        // PMC 4.5x the input), and the next step's eight are in flight while this one is walked
-        // in two 64-byte halves
+        // 64-byte steps: a lane's four 16-B loads of a step are issued together (a half cache
+        // line per request instead of 16 B, so a line evicted between a lane's steps is
+        // fetched 2x rather than 8x), and the next step's four are in flight while this one
+        // is walked
         const uint4 *gb = reinterpret_cast<const uint4 *>(a.buf);
-        const uint32_t w0 = sp.x & ~127u;
-        uint4 n[8];
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
-            n[k] = w0 + 16u * k + 16u > sp.x && w0 + 16u * k < sp.y ? gb[(w0 >> 4) + k] : make_uint4(0, 0, 0, 0);
-        for (uint32_t w2 = w0; w2 < sp.y && !bad; w2 += 128) {
-            uint4 v8[8];
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) v8[k] = n[k];
+        const uint32_t w0 = sp.x & ~63u;
+        uint4 n0, n1, n2, n3;
+        {
+            const uint32_t c = w0 >> 4;
+            n0 = w0 + 16u > sp.x && w0 < sp.y ? gb[c] : make_uint4(0, 0, 0, 0);
+            n1 = w0 + 32u > sp.x && w0 + 16u < sp.y ? gb[c + 1] : make_uint4(0, 0, 0, 0);
+            n2 = w0 + 48u > sp.x && w0 + 32u < sp.y ? gb[c + 2] : make_uint4(0, 0, 0, 0);
+            n3 = w0 + 64u > sp.x && w0 + 48u < sp.y ? gb[c + 3] : make_uint4(0, 0, 0, 0);
+        }
+        for (uint32_t w = w0; w < sp.y && !bad; w += 64) {
+            const uint4 v0 = n0, v1 = n1, v2 = n2, v3 = n3;
             {
-                const uint32_t wn = w2 + 128u;
-#pragma unroll
-                for (uint32_t k = 0; k < 8; ++k) n[k] = wn + 16u * k < sp.y ? gb[(wn >> 4) + k] : make_uint4(0, 0, 0, 0);
+                const uint32_t wn = w + 64u, c = wn >> 4;
+                n0 = wn < sp.y ? gb[c] : make_uint4(0, 0, 0, 0);
+                n1 = wn + 16u < sp.y ? gb[c + 1] : make_uint4(0, 0, 0, 0);
+                n2 = wn + 32u < sp.y ? gb[c + 2] : make_uint4(0, 0, 0, 0);
+                n3 = wn + 48u < sp.y ? gb[c + 3] : make_uint4(0, 0, 0, 0);
             }
-#pragma unroll
-          for (uint32_t h = 0; h < 2; ++h) {
-            const uint32_t w = w2 + 64u * h;
-            if (w >= sp.y || bad) break;
-            const uint4 v0 = v8[4 * h], v1 = v8[4 * h + 1], v2 = v8[4 * h + 2], v3 = v8[4 * h + 3];
             uint64_t ev = 0;
             const uint32_t wd[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
                                      v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
@@ -389,7 +387,7 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
                                    eqm(lx ^ 0x7d7d7d7du) | eqm(x ^ 0x3a3a3a3au) | eqm(x ^ 0x2c2c2c2cu);
                 ev |= (uint64_t)(((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * d);
             }
-            if (w < sp.x) ev &= sp.x - w >= 64u ? 0ull : ~0ull << (sp.x - w);
+            if (w < sp.x) ev &= ~0ull << (sp.x - w);
             if (sp.y - w < 64u) ev &= (1ull << (sp.y - w)) - 1ull;
             while (ev && !bad) {
                 const uint32_t j = (uint32_t)__builtin_ctzll(ev);
@@ -468,7 +466,6 @@ __global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
                     }
                 }
             }
-          }
         }
         // the line's first and last non-blank bytes (a JSON line starts with '{' and ends
         // with '}', so these loops stop at once)

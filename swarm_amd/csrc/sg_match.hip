@@ -1380,6 +1380,8 @@ struct VerifyArgs {
     uint32_t n_singles, n_acc;  // automata count, total accept-table entries
 };
 
+constexpr int VF_PRE = 6;  // 16-B record chunks loaded before the walk (96 B: most banners)
+
 // Walk automaton (D, cls, acc with C classes, eol column, anchored start states mid) over
 // record [s, e): global tables, or the block's copy in LDS (the same code inlined with LDS
 // pointers, so the lookups are ds_reads).
@@ -1417,28 +1419,19 @@ __device__ __forceinline__ bool verify_walk(const uint8_t *__restrict__ buf, DT 
             hit = acc[st] != 0;
         }
     };
-    // the record walked one 128-B cache line at a time: a line's eight 16-B chunks loaded
-    // together, the next line's in flight while this one is walked. (Round 3 loaded the first
-    // 96 B unaligned, then one 16-B chunk per step: every later chunk of a long banner was a
-    // fetch of its own, by then the line had left L2 — PMC 4.7x the credited bytes.)
-    const uint32_t w0 = s & ~127u;
-    uint4 cur[8];
+    // the record's first VF_PRE 16-B chunks are loaded together before the walk: one line
+    // fetch per record instead of a load per chunk spread over the walk, by which time the
+    // line has left L2 (round 2 PMC: 6x over-fetch, 6 % L2 hits); the rest as the walk goes
+    const uint32_t w0 = s & ~15u;
+    uint4 pre[VF_PRE];
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j)
-        cur[j] = (w0 + 16u * j + 16u > s && w0 + 16u * j < e) ? *reinterpret_cast<const uint4 *>(buf + w0 + 16u * j)
-                                                             : make_uint4(0, 0, 0, 0);
-    for (uint32_t w = w0; w < e && !hit && st != 0; w += 128) {
-        uint4 nxt[8];
+    for (int j = 0; j < VF_PRE; ++j)
+        pre[j] = (w0 + 16u * j < e) ? *reinterpret_cast<const uint4 *>(buf + w0 + 16u * j) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-            nxt[j] = (w + 128u + 16u * j < e) ? *reinterpret_cast<const uint4 *>(buf + w + 128u + 16u * j)
-                                             : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-            if (w + 16u * j < e && w + 16u * j + 16u > s && !hit && st != 0) walk16(w + 16u * j, cur[j]);
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) cur[j] = nxt[j];
-    }
+    for (int j = 0; j < VF_PRE; ++j)
+        if (w0 + 16u * j < e && !hit && st != 0) walk16(w0 + 16u * j, pre[j]);
+    for (uint32_t w = w0 + 16u * VF_PRE; w < e && !hit && st != 0; w += 16)
+        walk16(w, *reinterpret_cast<const uint4 *>(buf + w));
     if (!hit && st != 0) hit = acc[D[st * C + eol]] != 0;
     return hit;
 }

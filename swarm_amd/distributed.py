@@ -63,12 +63,55 @@ def exchange_counts(counts: Sequence[int], group=None) -> List[int]:
     return [int(x) for x in o.tolist()]
 
 
+# Largest per-peer message of one RCCL all-to-all. The RCCL in this image (2.26.6, torch's
+# wheel) returned wrong bytes for 1-rank all_to_all_single messages of 1800 MB where 512 MB
+# ones were exact (tools/rccl_probe.py), and a C5 rounds step with 1.65 GB
+# rounds faulted: larger exchanges go as several all-to-alls of at most this many bytes per
+# peer.
+A2A_CHUNK = 512 << 20
+
+
+def a2a_pieces(in_splits: Sequence[int], out_splits: Sequence[int], chunk: int):
+    """The chunked exchange plan: per piece c, ([(start, end)] send ranges per peer,
+    [(start, end)] receive ranges per peer), bytes [c * chunk, (c + 1) * chunk) of every
+    peer's message (empty ranges once a message is exhausted). Concatenated over pieces, each
+    peer's ranges cover its message once, in order."""
+    def offs(s):
+        o, a = [], 0
+        for x in s:
+            o.append(a)
+            a += x
+        return o
+    io, oo = offs(in_splits), offs(out_splits)
+    big = max(list(in_splits) + list(out_splits) + [0])
+    plan = []
+    for c0 in range(0, big, chunk):
+        sr = [(o + min(c0, s), o + min(c0 + chunk, s)) for o, s in zip(io, in_splits)]
+        rr = [(o + min(c0, s), o + min(c0 + chunk, s)) for o, s in zip(oo, out_splits)]
+        plan.append((sr, rr))
+    return plan
+
+
+class _Works:
+    """wait() of several async collectives (the pieces of one chunked exchange)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+
 def all_to_all_bytes(recv: torch.Tensor, send: torch.Tensor, out_splits: Sequence[int], in_splits: Sequence[int],
                      group=None, async_op: bool = False):
-    """One all_to_all_single of byte buffers with host split sizes (sum(in_splits) ==
-    send.numel(), sum(out_splits) == recv.numel()). RCCL: straight between the device
-    buffers, optionally async (the returned work's wait() orders the caller's stream after
-    it). gloo with device buffers: staged through host copies, synchronously (returns None)."""
+    """All-to-all of byte buffers with host split sizes (sum(in_splits) == send.numel(),
+    sum(out_splits) == recv.numel()). RCCL: straight between the device buffers, optionally
+    async (the returned work's wait() orders the caller's stream after it); one
+    all_to_all_single, or pieces of at most A2A_CHUNK bytes per peer (grouped send/recv
+    all-to-alls of buffer views) when a message is larger. gloo with device buffers: staged
+    through host copies, synchronously (returns None)."""
     out_splits, in_splits = [int(x) for x in out_splits], [int(x) for x in in_splits]
     if host_staged(group) and (send.is_cuda or recv.is_cuda):
         h = torch.empty(recv.numel(), dtype=torch.uint8)
@@ -76,8 +119,15 @@ def all_to_all_bytes(recv: torch.Tensor, send: torch.Tensor, out_splits: Sequenc
                                group=group)
         recv.copy_(h)
         return None
-    return dist.all_to_all_single(recv, send, output_split_sizes=out_splits, input_split_sizes=in_splits,
-                                  group=group, async_op=async_op)
+    if host_staged(group) or max(out_splits + in_splits + [0]) <= A2A_CHUNK:
+        return dist.all_to_all_single(recv, send, output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                      group=group, async_op=async_op)
+    works = []
+    for sr, rr in a2a_pieces(in_splits, out_splits, A2A_CHUNK):
+        w = dist.all_to_all([recv[a:b] for a, b in rr], [send[a:b] for a, b in sr], group=group, async_op=async_op)
+        if async_op:
+            works.append(w)
+    return _Works(works) if async_op else None
 
 
 def exchange_records(send: torch.Tensor, part_bytes: Sequence[int], group=None) -> torch.Tensor:

@@ -9,6 +9,7 @@ rank outputs concatenated in rank order must equal the global oracle output."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -233,6 +234,31 @@ def test_rounds_step_force_exchange_single_rank():
     eu, ef = S.dedup_diff(cur, prior)
     assert u == eu and f == ef
     assert nround == 3
+
+
+def test_a2a_pieces_cover_each_message_once():
+    """The chunked all-to-all plan (RCCL messages capped at A2A_CHUNK bytes per peer): over
+    the pieces, each peer's send and receive ranges tile its message in order."""
+    from swarm_amd.distributed import a2a_pieces
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        world = int(rng.integers(1, 6))
+        ins = [int(x) for x in rng.integers(0, 1000, size=world)]
+        outs = [int(x) for x in rng.integers(0, 1000, size=world)]
+        chunk = int(rng.integers(1, 400))
+        plan = a2a_pieces(ins, outs, chunk)
+        assert len(plan) == -(-max(ins + outs + [0]) // chunk)
+        for splits, side in ((ins, 0), (outs, 1)):
+            o = 0
+            for g, s in enumerate(splits):
+                pos = o
+                for piece in plan:
+                    a, b = piece[side][g]
+                    assert a == pos and b - a <= chunk
+                    pos = b
+                assert pos == o + s
+                o += s
+    assert a2a_pieces([0, 0], [0, 0], 16) == []
 
 
 def test_plan_rounds():

@@ -56,6 +56,14 @@ def rccl_worker(port, q):
             w.wait()
         torch.cuda.synchronize()
         out["a2a_equal"] = bool(torch.equal(recv, send))
+        # 1b. the same message in 256 KB pieces (grouped send/recv all-to-alls of views)
+        D.A2A_CHUNK = 1 << 18
+        recv2 = torch.empty(n, dtype=torch.uint8, device="cuda")
+        w2 = D.all_to_all_bytes(recv2, send, [n], [n], async_op=True)
+        out["chunked_pieces"] = len(w2.works) if hasattr(w2, "works") else 0
+        w2.wait()
+        torch.cuda.synchronize()
+        out["chunked_equal"] = bool(torch.equal(recv2, send))
         # 2. the small collectives on device tensors
         out["counts"] = D.exchange_counts([5, 6, 7])
         out["max_int"] = D.all_max_int(42)
@@ -67,6 +75,7 @@ def rccl_worker(port, q):
         prior_raw = corpus.hostport_pieces(pool, 150_000, U // 10, U, seed=900, per_piece=40_000)
         cur = corpus.hostport_pieces(pool, 200_000, 0, U, seed=100, per_piece=60_000)
         rounds = 3
+        D.A2A_CHUNK = 1 << 16  # the rounds' exchanges in pieces too
         split = D.agree_splitters(ctx, prior_raw, rounds)
         prior_parts, _ = D.build_prior_rounds(ctx, prior_raw, split, rounds, force_exchange=True)
         recvd, _send = D.exchange_rounds(ctx, cur, split, rounds, force_exchange=True)
@@ -102,6 +111,7 @@ def test_one_rank_rccl_collectives_and_rounds_step():
     assert p.exitcode == 0
     assert out["backend"] == "nccl" and out["world"] == 1 and out["host_staged"] is False
     assert out["work_is_async"] and out["a2a_equal"]
+    assert out["chunked_pieces"] == 5 and out["chunked_equal"]
     assert out["counts"] == [5, 6, 7]
     assert out["max_int"] == 42 and out["max_float"] == 1.5
     assert out["round_works"] == 3  # one async all-to-all per round, on RCCL

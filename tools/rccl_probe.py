@@ -1,8 +1,12 @@
 """RCCL probe (no swarm_amd code): a 1-rank "nccl" process group on cuda:0, async byte
-all_to_all_single calls of growing size between device buffers, each checked with
-torch.equal. Bisects a fault seen in the 1-rank forced-exchange C5 rounds step at 1B records
-(1.65 GB rounds): does RCCL itself handle GB-sized self messages?
-  python3 tools/rccl_probe.py [max_mb] [queued]"""
+all-to-alls between device buffers, each checked with torch.equal. Bisects the fault seen in
+the 1-rank forced-exchange C5 rounds step at 1B records (1.65 GB rounds).
+  python3 tools/rccl_probe.py sizes <MB> [<MB> ...]       one all_to_all_single per size
+  python3 tools/rccl_probe.py offsets <MB> <GB> [<GB> ...] one message of MB at each send offset
+  python3 tools/rccl_probe.py list <MB> [<MB> ...]        list all_to_all (grouped send/recv)
+  python3 tools/rccl_probe.py chunked <MB> <chunk MB>     swarm_amd's chunked all_to_all_bytes
+Exits 1 at the first mismatch.
+Round 4 result (5 queued messages): 64..512 MB equal, 1800 MB NOT equal."""
 import os
 import socket
 import sys
@@ -12,9 +16,15 @@ import torch
 import torch.distributed as dist
 
 
+def check(tag, recv, ref, t0):
+    torch.cuda.synchronize()
+    ok = torch.equal(recv, ref)
+    print("%s: equal %s, %.3f s" % (tag, ok, time.perf_counter() - t0), flush=True)
+    return ok
+
+
 def main():
-    max_mb = int(sys.argv[1]) if len(sys.argv) > 1 else 1800
-    queued = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    mode = sys.argv[1]
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -22,29 +32,47 @@ def main():
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, init_method="tcp://127.0.0.1:%d" % port)
-    mb = 64
-    while mb <= max_mb:
-        n = mb << 20
-        send = torch.randint(0, 256, (n * queued + 7,), dtype=torch.uint8, device="cuda")
-        recvs, works = [], []
-        t0 = time.perf_counter()
-        for q in range(queued):
-            r = torch.empty(n, dtype=torch.uint8, device="cuda")
-            w = dist.all_to_all_single(r, send[q * n:(q + 1) * n], output_split_sizes=[n], input_split_sizes=[n],
-                                       async_op=True)
-            recvs.append(r)
-            works.append(w)
-        for w in works:
+    if mode in ("sizes", "list"):
+        for mb in [int(x) for x in sys.argv[2:]]:
+            n = mb << 20
+            send = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+            recv = torch.empty(n, dtype=torch.uint8, device="cuda")
+            t0 = time.perf_counter()
+            if mode == "sizes":
+                w = dist.all_to_all_single(recv, send, output_split_sizes=[n], input_split_sizes=[n], async_op=True)
+            else:
+                w = dist.all_to_all([recv], [send], async_op=True)
             w.wait()
-        torch.cuda.synchronize()
-        ok = all(torch.equal(recvs[q], send[q * n:(q + 1) * n]) for q in range(queued))
-        print("size %d MB x %d queued: equal %s, %.3f s" % (mb, queued, ok, time.perf_counter() - t0), flush=True)
-        if not ok:
-            break
-        del send, recvs, works
-        mb *= 2 if mb < 1024 else 1
-        if mb >= 1024:
-            mb = max_mb if mb < max_mb else max_mb + 1
+            ok = check("%s %d MB" % (mode, mb), recv, send, t0)
+            del send, recv
+            if not ok:
+                sys.exit(1)
+    elif mode == "offsets":
+        mb = int(sys.argv[2])
+        n = mb << 20
+        offs = [int(float(x) * (1 << 30)) for x in sys.argv[3:]]
+        send = torch.randint(0, 256, (max(offs) + n,), dtype=torch.uint8, device="cuda")
+        for o in offs:
+            recv = torch.empty(n, dtype=torch.uint8, device="cuda")
+            t0 = time.perf_counter()
+            w = dist.all_to_all_single(recv, send[o:o + n], output_split_sizes=[n], input_split_sizes=[n],
+                                       async_op=True)
+            w.wait()
+            if not check("offset %.2f GB, %d MB" % (o / (1 << 30), mb), recv, send[o:o + n], t0):
+                sys.exit(1)
+    elif mode == "chunked":
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from swarm_amd import distributed as D
+        mb, cmb = int(sys.argv[2]), int(sys.argv[3])
+        D.A2A_CHUNK = cmb << 20
+        n = mb << 20
+        send = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+        recv = torch.empty(n, dtype=torch.uint8, device="cuda")
+        t0 = time.perf_counter()
+        w = D.all_to_all_bytes(recv, send, [n], [n], async_op=True)
+        w.wait()
+        if not check("chunked %d MB in %d MB pieces" % (mb, cmb), recv, send, t0):
+            sys.exit(1)
     dist.destroy_process_group()
 
 
