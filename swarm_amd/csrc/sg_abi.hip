@@ -4,6 +4,7 @@
 #include "sg_prims.hpp"
 #define SG_EMIT_DEVICE_ONLY
 #include "sg_emit.hpp"
+#include "sg_route.hpp"
 
 #include <string.h>
 
@@ -89,7 +90,7 @@ __device__ __forceinline__ void wave_count(unsigned long long *s_c, uint32_t str
 
 __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ buf,
                                                    const uint2 *__restrict__ spans, uint32_t R,
-                                                   uint32_t parts, uint64_t *keys,
+                                                   uint32_t parts, uint8_t *keys,
                                                    unsigned long long *cnt /* [2*parts] */) {
     __shared__ unsigned long long s_c[2 * 256];
     for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) s_c[i] = 0;
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ b
             const uint32_t s = spans[i].x, e = spans[i].y;
             const uint64_t h = hash_record(buf, s, e);
             q = part_of(h, parts);
-            keys[i] = q;
+            keys[i] = (uint8_t)q;
             bytes = e - s + 1;
         }
         wave_count(s_c, 256, i < R, q, bytes);
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void k_part_keys(const uint8_t *__restrict__ b
 // outputs concatenated in part order are the global sort -u output.
 __global__ __launch_bounds__(256) void k_range_keys(const uint64_t *__restrict__ key0, const uint2 *__restrict__ spans,
                                                     uint32_t R, const uint64_t *__restrict__ split, uint32_t ns,
-                                                    uint64_t *keys, unsigned long long *cnt /* [2*parts] */) {
+                                                    uint8_t *keys, unsigned long long *cnt /* [2*parts] */) {
     __shared__ unsigned long long s_c[2 * 256];
     __shared__ uint64_t s_split[256];
     for (int i = threadIdx.x; i < 2 * 256; i += blockDim.x) s_c[i] = 0;
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(256) void k_range_keys(const uint64_t *__restrict__
                 const uint32_t mid = (lo + hi) >> 1;
                 if (s_split[mid] <= k) lo = mid + 1; else hi = mid;
             }
-            keys[i] = lo;
+            keys[i] = (uint8_t)lo;
             bytes = spans[i].y - spans[i].x + 1;
         }
         wave_count(s_c, 256, i < R, lo, bytes);
@@ -149,40 +150,7 @@ __global__ __launch_bounds__(256) void k_range_keys(const uint64_t *__restrict__
     }
 }
 
-// Byte-string splitters (SG_SPLIT_BYTES = 64 bytes each at most): part(record) = number of
-// splitters <= record in bytewise order (shorter-is-smaller). Unlike a key0 splitter, a
-// byte splitter can fall inside a run of records sharing their first 7 bytes (https://...,
-// 10.0.x.y:port), so range parts stay balanced on URL and IP data. Both sides are compared
-// as 8 big-endian words of their first 64 bytes (zero past the end), then by length: words
-// differ => the first differing word decides; all equal => one is a prefix of the other
-// within 64 bytes (or they are equal there) and the longer one is larger, which is exact
-// because a splitter never has more than 64 bytes.
-constexpr uint32_t SPL_W = 64, SPL_WORDS = SPL_W / 8;
-
-__device__ __forceinline__ void head_words(const uint8_t *__restrict__ buf, uint32_t s, uint32_t e,
-                                           uint64_t (&w)[SPL_WORDS]) {
-    const uint32_t len = e - s;
-#pragma unroll
-    for (uint32_t k = 0; k < SPL_WORDS; ++k) {
-        const uint32_t o = 8u * k;
-        w[k] = o < len ? load_le(buf, s + o, min(len - o, 8u)) : 0ull;
-    }
-}
-
-// record < splitter (BE words in LDS)
-__device__ __forceinline__ bool head_less(const uint64_t (&w)[SPL_WORDS], uint32_t len, const uint64_t *sw,
-                                          uint32_t slen) {
-    int r = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < SPL_WORDS; ++k) {
-        if (r == 0) {
-            const uint64_t a = w[k], b = sw[k];
-            if (a != b) r = a < b ? -1 : 1;
-        }
-    }
-    return r ? r < 0 : len < slen;
-}
-
+// Byte-string splitters: sg_route.hpp.
 // Ordering by key0 first: record key0 vs splitter key0 (both the first 7 bytes + min(len, 8))
 // decides unless they are equal with tag 8; only then are the first 64 bytes loaded and
 // compared word by word (host:port records: one or two 8-B loads per record instead of
@@ -190,7 +158,7 @@ __device__ __forceinline__ bool head_less(const uint64_t (&w)[SPL_WORDS], uint32
 __global__ __launch_bounds__(256) void k_range_bytes(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                                      uint32_t R, const uint64_t *__restrict__ split_w,
                                                      const uint32_t *__restrict__ split_len, uint32_t ns,
-                                                     uint64_t *keys, unsigned long long *cnt /* [2*parts] */) {
+                                                     uint8_t *keys, unsigned long long *cnt /* [2*parts] */) {
     __shared__ unsigned long long s_c[2 * 256];
     __shared__ uint64_t s_w[255 * SPL_WORDS];
     __shared__ uint64_t s_k0[256];
@@ -208,30 +176,8 @@ __global__ __launch_bounds__(256) void k_range_bytes(const uint8_t *__restrict__
         uint32_t lo = 0, bytes = 0;
         if (i < R) {
             const uint2 x = spans[i];
-            const uint64_t rk = chunk_key(buf, x.x, x.y, 0);
-            uint64_t w[SPL_WORDS];
-            bool loaded = false;
-            uint32_t hi = ns;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                const uint64_t sk = s_k0[mid];
-                bool less;
-                if (rk != sk) {
-                    less = rk < sk;
-                } else if ((rk & 0xffu) < 8u) {
-                    less = false;  // the same record bytes: splitter <= record
-                } else {
-                    if (!loaded) {
-                        head_words(buf, x.x, x.y, w);
-#pragma unroll
-                        for (uint32_t k = 0; k < SPL_WORDS; ++k) w[k] = __builtin_bswap64(w[k]);
-                        loaded = true;
-                    }
-                    less = head_less(w, x.y - x.x, s_w + mid * SPL_WORDS, s_len[mid]);
-                }
-                if (!less) lo = mid + 1; else hi = mid;
-            }
-            keys[i] = lo;
+            lo = route_record(buf, ~0ull, x.x, x.y, chunk_key(buf, x.x, x.y, 0), s_k0, ns, s_w, s_len);
+            keys[i] = (uint8_t)lo;
             bytes = x.y - x.x + 1;
         }
         wave_count(s_c, 256, i < R, lo, bytes);
@@ -377,7 +323,7 @@ static int pack_byte_splitters(const uint8_t *splitters, const uint32_t *split_o
 // inside the tile's ~100 KB of input. Replaces a radix sort of the record ids by part and one
 // gather-emit per part (random 27-B reads: C5's part_emit ran at ~1.6 TB/s).
 constexpr int PT_BLOCK = 256;
-constexpr int PT_ITEMS = 16;
+constexpr int PT_ITEMS = 8;
 constexpr uint32_t PT_TILE = PT_BLOCK * PT_ITEMS;
 
 // bytes (record + '\n') per (part, tile), part-major: cnt[q * ntiles + t]
@@ -390,7 +336,7 @@ struct PartSpansOut {
     uint64_t *keys = nullptr;
 };
 
-__global__ __launch_bounds__(PT_BLOCK) void k_part_count(const uint2 *__restrict__ spans, const uint64_t *__restrict__ part,
+__global__ __launch_bounds__(PT_BLOCK) void k_part_count(const uint2 *__restrict__ spans, const uint8_t *__restrict__ part,
                                                           uint32_t R, uint32_t nparts, uint32_t ntiles,
                                                           uint32_t *__restrict__ cnt, uint32_t *__restrict__ rcnt) {
     __shared__ uint32_t s_b[256], s_r[256];
@@ -414,6 +360,18 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_count(const uint2 *__restrict
     }
 }
 
+// Per part q, this piece's record and byte totals from the per-(part, tile) counts and their
+// exclusive scans (part-major): cnt[q] = records, cnt[nparts + q] = bytes.
+__global__ __launch_bounds__(256) void k_part_totals(const uint32_t *__restrict__ pcnt, const uint64_t *__restrict__ ppre,
+                                                     const uint32_t *__restrict__ rcnt, const uint64_t *__restrict__ rpre,
+                                                     uint32_t nparts, uint32_t ntiles, unsigned long long *cnt) {
+    const uint32_t q = threadIdx.x;
+    if (q >= nparts) return;
+    const size_t a = (size_t)q * ntiles, z = a + ntiles - 1;
+    cnt[q] = rpre[z] + rcnt[z] - rpre[a];
+    cnt[nparts + q] = ppre[z] + pcnt[z] - ppre[a];
+}
+
 struct U32AsU64P {
     const uint32_t *v;
     __device__ uint64_t operator()(uint32_t i) const { return v[i]; }
@@ -422,7 +380,7 @@ struct U32AsU64P {
 // pre: exclusive prefix of cnt (flat, part-major); pbase[q]: where part q's bytes of this
 // piece start in the output (null: a single buffer, parts back to back from offset 0).
 __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
-                                                          const uint64_t *__restrict__ part, uint32_t R, uint32_t ntiles,
+                                                          const uint8_t *__restrict__ part, uint32_t R, uint32_t ntiles,
                                                           const uint64_t *__restrict__ pre,
                                                           const uint64_t *__restrict__ pbase, uint8_t *__restrict__ out,
                                                           const PartSpansOut so) {
@@ -503,27 +461,32 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     }
     __syncthreads();
     // copy: sorted position q by lane q (consecutive lanes, consecutive bytes of one part)
-    for (uint32_t q = tid; q < n_t; q += PT_BLOCK) {
-        // the part of sorted position q: the last part whose run starts at or before q
+    // the part of sorted position q: the last part whose run starts at or before q (parts
+    // with empty runs share a start; s_dstart is non-decreasing, so that is the non-empty one)
+    auto part_of = [&](uint32_t q) {
         uint32_t lo = 0, hi = 256;
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (s_dstart[mid] <= q) lo = mid; else hi = mid;
         }
-        // parts with empty runs share a start: take the last part starting at or before q
-        // whose run is non-empty (s_dstart is non-decreasing, so lo is that part)
-        const uint2 x = s_sp[q];
-        const uint64_t dst = s_dst[lo] + s_off[q];
+        return lo;
+    };
+    auto finish = [&](uint32_t q, uint32_t lo, uint2 x, uint64_t dst, uint64_t k0) {
         if (so.sp) {  // also the record's span inside its part and its key, at its index in the parts
-            uint64_t k0;
-            put_medium<true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
             const uint64_t g = s_g0[lo] + q;
             const uint32_t rel = (uint32_t)(dst - s_pst[lo]);
             so.sp[g] = make_uint2(rel, rel + (x.y - x.x));
             so.keys[g] = k0;
-        } else {
-            put_medium(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
         }
+    };
+    for (uint32_t q = tid; q < n_t; q += PT_BLOCK) {
+        const uint32_t lo = part_of(q);
+        const uint2 x = s_sp[q];
+        const uint64_t dst = s_dst[lo] + s_off[q];
+        uint64_t k0 = 0;
+        if (so.sp) put_medium<true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
+        else put_medium(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
+        finish(q, lo, x, dst, k0);
     }
 }
 
@@ -540,7 +503,7 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
     unsigned long long *cnt;
     SG_TRY(slot(c, S_M_CNT, 2 * 256, &cnt));
     SG_HIP(hipMemsetAsync(cnt, 0, 2 * 256 * 8, c->stream));
-    uint64_t *keys;
+    uint8_t *keys;  // part of each record
     SG_TRY(slot(c, S_KEYS2, R, &keys));
     if (R && bsplit) {
         uint64_t *d_w;
@@ -737,44 +700,92 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
     SG_TRY(slot(c, S_M_TMP2, sizeof(ByteSplit) / 8, &d_w));
     SG_HIP(hipMemcpyAsync(d_w, &bs, sizeof(ByteSplit), hipMemcpyHostToDevice, c->stream));
     const uint32_t *d_len = reinterpret_cast<const uint32_t *>(d_w + 255 * SPL_WORDS);
-    // pass 1: per-piece (records, bytes) of every part, one readback for all pieces
+    // pass 0: every piece's record count (count pass + tile scan per piece), one read-back
+    std::vector<const uint8_t *> pb_in(k, nullptr);
+    std::vector<uint32_t> lnt(k, 0);
+    std::vector<size_t> loff(k, 0);
+    size_t ltot = 0;
+    for (size_t j = 0; j < k; ++j) {
+        if (!lens[j]) continue;
+        lnt[j] = lines_tiles(lens[j]);
+        loff[j] = ltot;
+        ltot += 2 * (size_t)lnt[j] + 4;
+    }
+    uint64_t *ltp = nullptr;
+    if (ltot) SG_TRY(slot(c, S_PT_LTP, ltot, &ltp));
+    uint8_t *pin = (uint8_t *)c->pinned;
+    if (8 * k > SG_PINNED_BYTES) { set_error("partition: %zu pieces exceed the read-back staging", k); return SG_E_INVAL; }
+    // (a piece that is not 16-byte aligned is copied to the aligned staging slot before each
+    // of its three passes: the slot holds one piece at a time)
+    for (size_t j = 0; j < k; ++j) {
+        if (!lens[j]) continue;
+        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &pb_in[j]));
+        SG_TRY(lines_count_scan(c, pb_in[j], lens[j], ltp + loff[j]));
+        SG_HIP(hipMemcpyAsync(pin + 8 * j, ltp + loff[j] + 2 * (size_t)lnt[j], 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    SG_HIP(hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> Rj(k, 0);
+    std::vector<uint64_t> roff(k, 0);
+    uint64_t all_rec = 0;
+    for (size_t j = 0; j < k; ++j) {
+        if (!lens[j]) continue;
+        uint64_t tv;
+        memcpy(&tv, pin + 8 * j, 8);
+        Rj[j] = (uint32_t)(tv >> 31);
+        if (Rj[j] != (uint32_t)(tv & 0x7fffffffu)) { set_error("run_lines: start/end count mismatch"); return SG_E_HIP; }
+        roff[j] = all_rec;
+        all_rec += Rj[j];
+    }
+    // pass 1 per piece: parse + route (spans and a part byte per record, kept for pass 2),
+    // the per-(part, tile) byte and record counts and their scans (kept per piece), and the
+    // piece's per-part totals; one read-back of all pieces' totals
+    uint2 *keep_sp;
+    uint8_t *keep_k;
+    SG_TRY(slot(c, S_PT_SP, all_rec + 1, &keep_sp));
+    SG_TRY(slot(c, S_PT_KEYS, all_rec + 16, &keep_k));
+    std::vector<uint32_t> ptn(k, 0);
+    std::vector<size_t> poff(k, 0);
+    size_t ptot = 0;
+    for (size_t j = 0; j < k; ++j) {
+        if (!Rj[j]) continue;
+        ptn[j] = (Rj[j] + PT_TILE - 1) / PT_TILE;
+        poff[j] = ptot;
+        ptot += (size_t)n_parts * ptn[j];
+    }
+    uint32_t *pcnt_all = nullptr, *rcnt_all = nullptr;
+    uint64_t *ppre_all = nullptr, *rpre_all = nullptr;
+    if (ptot) {
+        SG_TRY(slot(c, S_PT_CNT, 2 * ptot, &pcnt_all));
+        SG_TRY(slot(c, S_PT_PRE, 2 * ptot, &ppre_all));
+        rcnt_all = pcnt_all + ptot;
+        rpre_all = ppre_all + ptot;
+    }
     unsigned long long *cnt;
     SG_TRY(slot(c, S_PART, (size_t)std::max<size_t>(k, 1) * 512, &cnt));
     SG_HIP(hipMemsetAsync(cnt, 0, std::max<size_t>(k, 1) * 512 * 8, c->stream));
-    // Pass 1's spans and parts are kept for pass 2 (no second parse or routing) while they
-    // fit the two keep slots, sized by the last call's record count (the first call of a
-    // size, or a larger one, parses the pieces that did not fit again).
-    uint2 *keep_sp = nullptr;
-    uint64_t *keep_k = nullptr, keep_cap = 0, kept = 0, all_rec = 0;
-    if (c->pt_keep_recs) {
-        SG_TRY(slot(c, S_PT_SP, c->pt_keep_recs, &keep_sp));
-        SG_TRY(slot(c, S_PT_KEYS, c->pt_keep_recs, &keep_k));
-        keep_cap = std::min(slot_elems<uint2>(c, S_PT_SP), slot_elems<uint64_t>(c, S_PT_KEYS));
-    }
-    std::vector<uint64_t> keep_off(k, ~0ull), keep_n(k, 0);
     for (size_t j = 0; j < k; ++j) {
-        if (!lens[j]) continue;
-        const uint8_t *b;
-        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &b));
-        Lines L;
-        SG_TRY(run_lines(c, b, lens[j], CUR_SLOTS, &L, false, true));
-        all_rec += L.n_rec;
-        if (!L.n_rec) continue;
-        uint64_t *keys;
-        if (kept + L.n_rec <= keep_cap) {
-            SG_HIP(hipMemcpyAsync(keep_sp + kept, L.spans, (size_t)L.n_rec * sizeof(uint2), hipMemcpyDeviceToDevice,
-                                  c->stream));
-            keys = keep_k + kept;
-            keep_off[j] = kept;
-            keep_n[j] = L.n_rec;
-            kept += L.n_rec;
-        } else {
-            SG_TRY(slot(c, S_KEYS2, L.n_rec, &keys));
+        if (!Rj[j]) continue;
+        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &pb_in[j]));
+        SG_TRY(lines_route_apply(c, pb_in[j], lens[j], ltp + loff[j], Rj[j], keep_sp + roff[j], d_w, d_len, ns,
+                                 keep_k + roff[j]));
+        const uint32_t ntiles = ptn[j];
+        const size_t nflat = (size_t)n_parts * ntiles;
+        uint32_t *pcnt = pcnt_all + poff[j], *rcnt = rcnt_all + poff[j];
+        uint64_t *ppre = ppre_all + poff[j], *rpre = rpre_all + poff[j];
+        SG_LAUNCH_B(c, "part_count", 9.0 * Rj[j], k_part_count, ntiles, PT_BLOCK, 0, keep_sp + roff[j], keep_k + roff[j],
+                    Rj[j], n_parts, ntiles, pcnt, rcnt);
+        const uint32_t nt = (uint32_t)((nflat + SCAN_TILE - 1) / SCAN_TILE);
+        uint64_t *tp;
+        SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
+        for (int pass = 0; pass < 2; ++pass) {
+            const U32AsU64P src{pass ? rcnt : pcnt};
+            SG_LAUNCH(c, "scan.count", k_scan64_count<U32AsU64P>, nt, SCAN_BLOCK, 0, src, (uint32_t)nflat, tp);
+            SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
+            SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64P>, nt, SCAN_BLOCK, 0, src, (uint32_t)nflat, tp + nt,
+                      pass ? rpre : ppre);
         }
-        SG_LAUNCH_B(c, "range_bytes", 24.0 * L.n_rec, k_range_bytes, std::min<uint32_t>((L.n_rec + 255) / 256, 2048u), 256, 0,
-                    b, L.spans, L.n_rec, d_w, d_len, ns, keys, cnt + 512 * j);
+        SG_LAUNCH(c, "part_totals", k_part_totals, 1, 256, 0, pcnt, ppre, rcnt, rpre, n_parts, ntiles, cnt + 512 * j);
     }
-    c->pt_keep_recs = std::max<uint64_t>(c->pt_keep_recs, all_rec);
     std::vector<uint64_t> h(std::max<size_t>(k, 1) * 512, 0);
     SG_TRY(ctx_readback(c, h.data(), cnt, h.size() * 8));
     // destinations: part p = pieces' part-p records in piece order
@@ -806,8 +817,8 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
         if (part_bytes) part_bytes[q] = pbytes[q];
         if (part_records) part_records[q] = prec[q];
     }
-    // pass 2: per piece, the multi-split: per-tile part byte counts, their scan, then every
-    // record copied straight to its part's place (k_part_apply)
+    // destinations of every (piece, part): part q's bytes of piece j follow those of pieces
+    // 0..j-1
     std::vector<uint64_t> acc(pbase);
     std::vector<uint64_t> pb_all((size_t)k * n_parts, 0);
     for (size_t j = 0; j < k; ++j) {
@@ -840,59 +851,16 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
     SG_TRY(slot(c, S_PT_BASE, pb_all.size(), &d_pb));
     SG_TRY(ctx_upload(c, d_pb, pb_all.data(), pb_all.size() * 8));
     const uint64_t *d_rb = d_pb + (size_t)k * n_parts, *d_pstart = d_pb + 2 * (size_t)k * n_parts;
+    // pass 2 per piece: the multi-split copy with pass 1's spans, parts and scans
     for (size_t j = 0; j < k; ++j) {
-        if (!lens[j]) continue;
-        const uint8_t *b;
-        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &b));
-        const uint2 *spans;
-        uint64_t *keys;
-        uint32_t R;
-        if (keep_off[j] != ~0ull) {
-            spans = keep_sp + keep_off[j];
-            keys = keep_k + keep_off[j];
-            R = (uint32_t)keep_n[j];
-        } else {
-            Lines L;
-            SG_TRY(run_lines(c, b, lens[j], CUR_SLOTS, &L, false, true));
-            R = L.n_rec;
-            if (!R) continue;
-            unsigned long long *scr;
-            SG_TRY(slot(c, S_M_CNT, 2 * 256, &scr));
-            SG_HIP(hipMemsetAsync(scr, 0, 2 * 256 * 8, c->stream));
-            SG_TRY(slot(c, S_KEYS2, R, &keys));
-            SG_LAUNCH_B(c, "range_bytes", 24.0 * R, k_range_bytes, std::min<uint32_t>((R + 255) / 256, 2048u), 256, 0, b,
-                        L.spans, R, d_w, d_len, ns, keys, scr);
-            spans = L.spans;
-        }
-        const uint32_t ntiles = (R + PT_TILE - 1) / PT_TILE;
-        const size_t nflat = (size_t)n_parts * ntiles;
-        uint32_t *pcnt;
-        uint64_t *ppre;
-        SG_TRY(slot(c, S_PT_CNT, nflat, &pcnt));
-        SG_TRY(slot(c, S_PT_PRE, nflat, &ppre));
-        uint32_t *rcnt = nullptr;
-        uint64_t *rpre = nullptr;
-        if (want_sp) {
-            SG_TRY(slot(c, S_PT_RCNT, nflat, &rcnt));
-            SG_TRY(slot(c, S_PT_RPRE, nflat, &rpre));
-        }
-        SG_LAUNCH_B(c, "part_count", 16.0 * R, k_part_count, ntiles, PT_BLOCK, 0, spans, keys, R, n_parts, ntiles, pcnt,
-                    rcnt);
-        const uint32_t nt = (uint32_t)((nflat + SCAN_TILE - 1) / SCAN_TILE);
-        uint64_t *tp;
-        SG_TRY(slot(c, S_TILES, 2 * (size_t)nt + 4, &tp));
-        for (int pass = 0; pass < (want_sp ? 2 : 1); ++pass) {
-            const U32AsU64P src{pass ? rcnt : pcnt};
-            SG_LAUNCH(c, "scan.count", k_scan64_count<U32AsU64P>, nt, SCAN_BLOCK, 0, src, (uint32_t)nflat, tp);
-            SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
-            SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64P>, nt, SCAN_BLOCK, 0, src, (uint32_t)nflat, tp + nt,
-                      pass ? rpre : ppre);
-        }
+        if (!Rj[j]) continue;
+        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &pb_in[j]));
         PartSpansOut so;
-        if (want_sp) so = PartSpansOut{rpre, d_rb + j * n_parts, d_pstart, d_sp, d_k};
+        if (want_sp) so = PartSpansOut{rpre_all + poff[j], d_rb + j * n_parts, d_pstart, d_sp, d_k};
         // model: span + part read, the record's bytes read and written (+ span and key out)
-        SG_LAUNCH_B(c, "part_emit", (want_sp ? 32.0 : 16.0) * R + 2.0 * (double)lens[j], k_part_apply, ntiles, PT_BLOCK,
-                    0, b, spans, keys, R, ntiles, ppre, d_pb + j * n_parts, d_out, so);
+        SG_LAUNCH_B(c, "part_emit", (want_sp ? 25.0 : 9.0) * Rj[j] + 2.0 * (double)lens[j], k_part_apply, ptn[j],
+                    PT_BLOCK, 0, pb_in[j], keep_sp + roff[j], keep_k + roff[j], Rj[j], ptn[j], ppre_all + poff[j],
+                    d_pb + j * n_parts, d_out, so);
     }
     return SG_OK;
 }

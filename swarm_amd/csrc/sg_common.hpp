@@ -71,6 +71,7 @@ enum Slot : int {
     S_TS2,  // two-level tile scan scratch
     S_PT_CNT, S_PT_PRE, S_PT_BASE,  // piece partition multi-split
     S_PT_SP, S_PT_KEYS,             // piece partition: spans and parts kept from pass 1 for pass 2
+    S_PT_LTP,                       // piece partition: every piece's parse tile counts and prefixes
     S_PT_RCNT, S_PT_RPRE, S_PT_SPOUT, S_PT_KOUT,  // piece partition: the parts' record spans/keys out
     S_LS_ERR, S_LS_BOUNDS,  // hybrid radix sort: overflow flag, local-sort tile bounds
     S_LS_LIST, S_LF_OFF, S_LF_KEY, S_LF_KEY2, S_LF_VAL, S_LF_VAL2, S_LF_POS,  // its overflow fix-up
@@ -102,7 +103,6 @@ struct sg_ctx {
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     float last_uniq_frac = 1.0f;  // dedup: unique / input records of the last sort -u (all-segments mode)
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
-    uint64_t pt_keep_recs = 0;  // piece partition: records the last call kept between its passes
     // the last hybrid radix sort's local-sort plan (lsort_fixup redoes its flagged tiles)
     struct LsLast {
         bool on = false;

@@ -158,6 +158,24 @@ __device__ __forceinline__ void put_win64(uint8_t *base, uint32_t d, const uint4
 // wave copy their records at once (the 16-lane group path copies one record per group at a
 // time: a load latency per record).
 constexpr uint32_t EM_MED = 1024;
+
+// The record's chunk_key(src, s, s + len, 0) from its first 64-byte window's loads c (record
+// start at byte sh <= 15 of the window).
+__device__ __forceinline__ uint64_t win_key0(const uint4 (&c)[4], uint32_t sh, uint32_t len) {
+    // bytes [sh, sh + 8) of the window: dwords sh / 4 .. sh / 4 + 2 (sh <= 15)
+    const uint32_t dw[6] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y};
+    const uint32_t a = sh >> 2, e = sh & 3u;
+    uint32_t w0 = dw[0], w1 = dw[1], w2 = dw[2];
+#pragma unroll
+    for (uint32_t t = 1; t < 4; ++t)
+        if (a == t) { w0 = dw[t]; w1 = dw[t + 1]; w2 = dw[t + 2]; }
+    const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, e), hi = __builtin_amdgcn_alignbyte(w2, w1, e);
+    uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+    const uint32_t take = len < 7u ? len : 7u;
+    v &= (1ull << (8u * take)) - 1ull;
+    return len ? ((__builtin_bswap64(v) & ~0xffull) | (uint64_t)(len < 8u ? len : 8u)) : 0ull;
+}
+
 // key0 (optional): the record's chunk_key(src, s, s + len, 0), taken from the first window's
 // loads instead of loading its first bytes again.
 template <bool KEY = false>
@@ -172,20 +190,7 @@ __device__ __forceinline__ void put_medium(const uint8_t *src, uint8_t *base, ui
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k)
             c[k] = (16u * k < ws + wl) ? *reinterpret_cast<const uint4 *>(src + q0 + wo + 16u * k) : make_uint4(0u, 0u, 0u, 0u);
-        if (KEY && wo == 0) {
-            // bytes [sh, sh + 8) of the window: dwords sh / 4 .. sh / 4 + 2 (sh <= 15)
-            const uint32_t dw[6] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y};
-            const uint32_t a = sh >> 2, e = sh & 3u;
-            uint32_t w0 = dw[0], w1 = dw[1], w2 = dw[2];
-#pragma unroll
-            for (uint32_t t = 1; t < 4; ++t)
-                if (a == t) { w0 = dw[t]; w1 = dw[t + 1]; w2 = dw[t + 2]; }
-            const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, e), hi = __builtin_amdgcn_alignbyte(w2, w1, e);
-            uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
-            const uint32_t take = len < 7u ? len : 7u;
-            v &= (1ull << (8u * take)) - 1ull;
-            *key0 = len ? ((__builtin_bswap64(v) & ~0xffull) | (uint64_t)(len < 8u ? len : 8u)) : 0ull;
-        }
+        if (KEY && wo == 0) *key0 = win_key0(c, sh, len);
         const bool nl = done + wl == len;
         put_win64(base, d + done, c, ws, wl, nl);
         done += wl;

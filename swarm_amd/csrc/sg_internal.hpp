@@ -37,6 +37,12 @@ int run_lines2(sg_ctx *c, const uint8_t *a, uint64_t na, const SlotSet &sa, Line
                const SlotSet &sb, Lines *lb);
 int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Lines *out, bool want_keys = true,
               bool apply = true);
+// The piece partition's parse with routing (sg_lines.hip): count + tile scan into tp (2 x
+// lines_tiles(n) + 4 words; packed record count at tp[2 x nt]), then spans + part bytes.
+uint32_t lines_tiles(uint64_t n);
+int lines_count_scan(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint64_t *tp);
+int lines_route_apply(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint64_t *tp, uint32_t R, uint2 *spans,
+                      const uint64_t *split_w, const uint32_t *split_len, uint32_t ns, uint8_t *parts);
 
 // LSD radix sort of (u64 key, u32 val) pairs on bits [begin_bit, end_bit), stable.
 // Ping-pongs between (keys, vals) and (keys_alt, vals_alt); returns the final arrays.

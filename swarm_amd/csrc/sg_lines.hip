@@ -13,6 +13,7 @@
 // into tile prefixes, k_lines re-reads the tile and writes the records. Algorithmic bytes:
 // 2 n read + 16 B written per record.
 #include "sg_internal.hpp"
+#include "sg_route.hpp"
 
 #include <stdlib.h>
 #include <string.h>
@@ -81,17 +82,32 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines_count(const uint8_t *__restr
     if (threadIdx.x == 0) tot[blockIdx.x] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
 }
 
-__global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ buf, uint64_t n,
-                                                    const uint64_t *__restrict__ pre, uint2 *__restrict__ spans,
-                                                    uint64_t *__restrict__ keys) {
+// ROUTE (the piece partition's pass 1, k_lines_route): each record's part (sg_route.hpp) from
+// its key0, taken from the staged tile bytes as the keys are, instead of a second pass that
+// reads every record's head again (k_range_bytes); the splitters' key0s in LDS.
+struct LinesRoute {
+    const uint64_t *split_w = nullptr;
+    const uint32_t *split_len = nullptr;
+    uint32_t ns = 0;
+    uint8_t *parts = nullptr;
+};
+
+template <bool ROUTE>
+__device__ __forceinline__ void lines_body(const uint8_t *__restrict__ buf, uint64_t n, const uint64_t *__restrict__ pre,
+                                           uint2 *__restrict__ spans, uint64_t *__restrict__ keys, const LinesRoute &rt) {
     __shared__ __attribute__((aligned(16))) uint8_t s_b[LN_TILE + 16];
     __shared__ uint64_t s_red[LN_BLOCK / 64];
+    __shared__ uint64_t s_k0[ROUTE ? 256 : 1];
     const uint32_t t = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * LN_TILE;
     const uint64_t my0 = base + (uint64_t)t * LN_BPT;
+    if constexpr (ROUTE) {
+        for (uint32_t q = t; q < rt.ns; q += LN_BLOCK) s_k0[q] = split_key0(rt.split_w, rt.split_len, q);
+    }
     uint32_t w[LN_NW], prev;
     load64(buf, n, base, my0, w, &prev);
-    if (keys) {
+    const bool stage = ROUTE || keys;
+    if (stage) {
 #pragma unroll
         for (int j = 0; j < LN_NW / 4; ++j)
             reinterpret_cast<uint4 *>(s_b)[(LN_NW / 4) * t + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
@@ -114,7 +130,7 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
         const int b = __ffsll((long long)bits) - 1;
         bits &= bits - 1;
         spans[si].x = (uint32_t)(my0 + b);
-        if (keys) {
+        if (stage) {
             // bytes [q, q+8) from three aligned dwords; tag = first '\n' in them (SWAR: the
             // lowest flagged byte is exact), key = the bytes before it (<= 7), big-endian
             const uint32_t q = t * LN_BPT + b;
@@ -127,7 +143,11 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
             const uint32_t rem = z ? (uint32_t)(__builtin_ctzll(z) >> 3) : 8u;
             const uint32_t take = rem < 7u ? rem : 7u;
             const uint64_t m = (1ull << (8u * take)) - 1ull;
-            keys[si] = (__builtin_bswap64(v & m) & ~0xffull) | rem;
+            const uint64_t k0 = (__builtin_bswap64(v & m) & ~0xffull) | rem;
+            if (keys) keys[si] = k0;
+            if constexpr (ROUTE)
+                rt.parts[si] = (uint8_t)route_record(buf, n, (uint32_t)(my0 + b), ~0u, k0, s_k0, rt.ns, rt.split_w,
+                                                     rt.split_len);
         }
         ++si;
     }
@@ -138,6 +158,18 @@ __global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ 
         spans[ei].y = (uint32_t)(my0 + b);
         ++ei;
     }
+}
+
+__global__ __launch_bounds__(LN_BLOCK) void k_lines(const uint8_t *__restrict__ buf, uint64_t n,
+                                                    const uint64_t *__restrict__ pre, uint2 *__restrict__ spans,
+                                                    uint64_t *__restrict__ keys) {
+    lines_body<false>(buf, n, pre, spans, keys, LinesRoute{});
+}
+
+__global__ __launch_bounds__(LN_BLOCK) void k_lines_route(const uint8_t *__restrict__ buf, uint64_t n,
+                                                          const uint64_t *__restrict__ pre, uint2 *__restrict__ spans,
+                                                          const LinesRoute rt) {
+    lines_body<true>(buf, n, pre, spans, nullptr, rt);
 }
 
 // Two buffers parsed with ONE host sync for both record counts (the dedup's prior and
@@ -215,4 +247,31 @@ int run_lines(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const SlotSet &ss, Li
     return SG_OK;
 }
 
+// The piece partition's parse in two halves: lines_count_scan queues the count pass and its
+// tile scan (tp: tot | pre | total, 2 * lines_tiles(n) + 4 words; the packed record count at
+// tp[2 * nt], read back by the caller with the other pieces'), lines_route_apply the
+// apply pass with routing (spans and one part byte per record).
+uint32_t lines_tiles(uint64_t n) { return (uint32_t)(n / LN_TILE + 1); }
+
+int lines_count_scan(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint64_t *tp) {
+    if (n > MAX_BYTES) { set_error("buffer of %llu bytes exceeds the 4 GiB per-call limit", (unsigned long long)n); return SG_E_TOO_LARGE; }
+    if (((uintptr_t)d_buf & 15) != 0) { set_error("run_lines: device buffer not 16-byte aligned"); return SG_E_INVAL; }
+    const uint32_t nt = lines_tiles(n);
+    SG_LAUNCH(c, "lines.count", k_lines_count, nt, LN_BLOCK, 0, d_buf, n, tp);
+    SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
+    prof_bytes(c, "lines.count", (double)n);
+    return SG_OK;
+}
+
+int lines_route_apply(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint64_t *tp, uint32_t R, uint2 *spans,
+                      const uint64_t *split_w, const uint32_t *split_len, uint32_t ns, uint8_t *parts) {
+    const uint32_t nt = lines_tiles(n);
+    const LinesRoute rt{split_w, split_len, ns, parts};
+    SG_LAUNCH(c, "lines", k_lines_route, nt, LN_BLOCK, 0, d_buf, n, tp + nt, spans, rt);
+    // text read once more + (start, end) and a part byte per record
+    prof_bytes(c, "lines", (double)n + 9.0 * R);
+    return SG_OK;
+}
+
 }  // namespace sg
+
