@@ -476,7 +476,7 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
     del pool
     cur_bytes = sum(p.numel() for p in cur)
     if world == 1 and args.c5_path == "local":
-        parts = sharded.plan_parts(prior_raw, [], 2 << 30)
+        parts = sharded.plan_parts(prior_raw, [], args.c5_part_bytes)
         split = sharded.choose_splitters(sharded.sample_records(ctx, prior_raw), parts)
         pu, _, pst = sharded.dedup_diff_large(ctx, prior_raw, (), splitters=split, align_parts=True)
         del prior_raw
@@ -1181,6 +1181,8 @@ def main():
     ap.add_argument("--no-x1", action="store_true", help="default run: skip the fused X1 and URL legs")
     ap.add_argument("--no-sub", action="store_true", help="default run: headline only (no c1/c3/c5/x1/urls legs)")
     ap.add_argument("--no-c2-weak", action="store_true", help="N > 1 c5 run: skip the C2 weak-scaling sub-object")
+    ap.add_argument("--c5-part-bytes", type=int, default=2 << 30,
+                    help="C5 local path: bytes per local part (one library call each; 1.25 x headroom)")
     ap.add_argument("--c5-hosts", type=int, default=64_000_000, help="C5 hosts (x 4 open-port slots = combos)")
     ap.add_argument("--c5-data", choices=["hosts", "ips"], default="hosts",
                     help="C5 records: host:port names, or 10.x.y.z:port (15M hosts x 16 port slots)")

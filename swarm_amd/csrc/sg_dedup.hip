@@ -625,6 +625,10 @@ __device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2
 // Rank the k members a.. of one segment with the G lanes gbase.. of the wave (lane gl of
 // the group = member gl): rank = members ordered before it (ties by index), dup = an
 // equal member with a smaller index exists. Writes the member's span at its rank.
+// Only two chunk keys per member travel between lanes: the group's first chunk where its
+// members differ (chunks before it are equal for all of them: a host's records share their
+// name), and the next; past those two the bytes are compared in the input (rare: the records
+// still tie there). Equivalent to seg_cmp: equal leading chunks with a full tag decide nothing.
 template <int G>
 __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                uint8_t *__restrict__ dup, uint32_t a, uint32_t k, uint32_t gl,
@@ -632,6 +636,23 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
     const bool act = live && gl < k;
     const uint2 x = act ? SS[a + gl] : make_uint2(0u, 0u);
     const SegKeys mk = act ? seg_keys(S, x, base) : SegKeys{{0, 0, 0, 0}};
+    // st: the first chunk that varies inside the group or ends its records (group-uniform)
+    const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << G) - 1ull) << gbase);
+    uint32_t st = SEG_CH;
+#pragma unroll
+    for (int c = SEG_CH - 1; c >= 0; --c) {
+        const uint64_t l = __shfl(mk.c[c], (int)gbase, 64);
+        const bool dif = act && mk.c[c] != l;
+        if ((__ballot(dif) & gmask) || (l & 0xffu) < 8u) st = (uint32_t)c;
+    }
+    auto pick = [&](uint32_t q) -> uint64_t {
+        uint64_t v = 0;
+#pragma unroll
+        for (int c = 0; c < SEG_CH; ++c) v = (q == (uint32_t)c) ? mk.c[c] : v;
+        return v;
+    };
+    const uint64_t m1 = pick(st), m2 = pick(st + 1);  // (past the last chunk: 0)
+    const uint32_t boff = bk_off(base) + 7u * (st + 2u < SEG_CH ? st + 2u : SEG_CH);
     uint32_t rank = 0;
     bool d = false;
     const uint32_t kk = live ? k : 0u;
@@ -641,12 +662,17 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
     for (int o = G; o < 64; o <<= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
     for (uint32_t j = 0; j < kmax; ++j) {
         const int src = (int)(gbase + (j < kk ? j : 0u));
-        SegKeys ok;
-#pragma unroll
-        for (int c = 0; c < SEG_CH; ++c) ok.c[c] = __shfl(mk.c[c], src, 64);
+        const uint64_t o1 = __shfl(m1, src, 64), o2 = __shfl(m2, src, 64);
         const uint2 y = make_uint2((uint32_t)__shfl(x.x, src, 64), (uint32_t)__shfl(x.y, src, 64));
         if (act && j < kk && j != gl) {
-            const int c = seg_cmp(S, mk, x, ok, y, base);
+            int c;
+            if (st >= SEG_CH) c = rec_cmp8(S, x.x, x.y - x.x, y.x, y.y - y.x, boff);
+            else if (m1 != o1) c = m1 < o1 ? -1 : 1;
+            else if ((m1 & 0xffu) < 8u) c = 0;
+            else if (st + 1u >= SEG_CH) c = rec_cmp8(S, x.x, x.y - x.x, y.x, y.y - y.x, boff);
+            else if (m2 != o2) c = m2 < o2 ? -1 : 1;
+            else if ((m2 & 0xffu) < 8u) c = 0;
+            else c = rec_cmp8(S, x.x, x.y - x.x, y.x, y.y - y.x, boff);
             if (c > 0 || (c == 0 && j < gl)) ++rank;
             if (c == 0 && j < gl) d = true;
         }

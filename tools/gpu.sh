@@ -31,6 +31,8 @@ args_of() {
     c4p) echo "--workload c4 --steps 2 --warmup 1 --no-cpu-baseline" ;;
     c5) echo "--workload c5 --steps 3 --warmup 1" ;;
     c5p) echo "--workload c5 --steps 1 --warmup 1 --no-cpu-baseline" ;;
+    c5pb1g) echo "--workload c5 --steps 3 --warmup 1 --no-cpu-baseline --c5-part-bytes 1073741824" ;;
+    c5pb512m) echo "--workload c5 --steps 3 --warmup 1 --no-cpu-baseline --c5-part-bytes 536870912" ;;
     c5r) echo "--workload c5 --c5-path rounds --c5-records 125000000 --steps 3 --warmup 1 --no-cpu-baseline" ;;
     c5rnccl) echo "--workload c5 --c5-path rounds --dist-backend nccl --steps 3 --warmup 1" ;;
     fields) echo "--workload fields --steps 3 --warmup 1" ;;
