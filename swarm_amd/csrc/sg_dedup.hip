@@ -844,29 +844,12 @@ __global__ void k_mark(const uint32_t *__restrict__ idx, uint32_t n, uint8_t *fl
     if (i < n) flag[idx[i]] = 1;
 }
 
-// Prior check: flag[0] = 1 if records are not strictly increasing. CS_U keys per thread,
-// their loads issued together: with one key pair per thread each wave did a single memory
-// round trip and the grid ran ~11 waves deep per slot (29 us for C2's 5.7M prior keys).
-constexpr int CS_U = 8;
-__global__ __launch_bounds__(256) void k_check_sorted(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
-                                                      const uint64_t *__restrict__ K, uint32_t n, uint32_t *flag,
-                                                      uint32_t base) {
-    const uint32_t i0 = (blockIdx.x * blockDim.x * CS_U) + threadIdx.x + 1;
-    uint64_t a[CS_U], b[CS_U];
-#pragma unroll
-    for (int u = 0; u < CS_U; ++u) {
-        const uint32_t i = i0 + u * blockDim.x;
-        const uint32_t j = i < n ? i : (n > 1 ? n - 1 : 0);
-        a[u] = K[j - (j ? 1 : 0)];
-        b[u] = K[j];
-    }
-    bool bad = false;
-#pragma unroll
-    for (int u = 0; u < CS_U; ++u) {
-        const uint32_t i = i0 + u * blockDim.x;
-        if (i < n && !bad) bad = key_cmp_full(buf, spans, a[u], i - 1, b[u], i, base) >= 0;
-    }
-    if (__ballot(bad) && lane_id() == 0) atomicOr(flag, 1u);
+// Prior check: flag[0] = 1 if records are not strictly increasing.
+__global__ void k_check_sorted(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans, const uint64_t *__restrict__ K,
+                               uint32_t n, uint32_t *flag, uint32_t base) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (i >= n) return;
+    if (key_cmp_full(buf, spans, K[i - 1], i - 1, K[i], i, base) >= 0) atomicOr(flag, 1u);
 }
 
 // ------------------------------------------------------------------ diff
@@ -1658,7 +1641,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         uint32_t *flag;
         SG_TRY(slot(c, S_M_CNT, 4, &flag));
         SG_HIP(hipMemsetAsync(flag, 0, 4, c->stream));
-        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256 * CS_U), 256, 0, d_buf, L.spans, L.keys, R, flag,
+        SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_buf, L.spans, L.keys, R, flag,
                     base);
         uint32_t f = 1;
         SG_TRY(ctx_readback(c, &f, flag, 4));
@@ -2022,7 +2005,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         // (a separate launch: fused into the prior's common-prefix scan, whose grid is capped
         // for its atomics, the byte compares of equal keys ran 40 µs longer on C2)
         if (R > 1 && R < (1u << 30))
-            SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256 * CS_U), 256, 0, d_prior, Lp.spans, Lp.keys,
+            SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_prior, Lp.spans, Lp.keys,
                         R, dflag, make_bk(0u, 7u));
     }
     if (cur_pre) Lc = *cur_pre;
