@@ -1293,10 +1293,16 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
     const uint64_t kr = rkeys[0];
     uint32_t best = 255;
     KeyStatAcc acc;
-    // grid-stride (at most 512 blocks): at most one memory-side atomic per block and word;
+    // grid-stride (at most 2048 blocks): at most one memory-side atomic per block and word;
     // LCP_U keys in flight per thread (one dependent load per trip left the loop latency-bound:
     // 1.6 TB/s on C2's cur keys)
+    // Records sharing the reference's first 7 bytes (URL lists: every record) continue in the
+    // bytes: their spans, then their bytes 7..14, are loaded for the LCP_U keys together (one
+    // record after another, each was two dependent loads: 228 us on 10M URLs); lcp_one takes
+    // the rare records that also tie there.
     const uint32_t stride = gridDim.x * blockDim.x * LCP_U;
+    const uint2 r = rspans[0];
+    const uint32_t rlen = r.y - r.x, tr = (uint32_t)(kr & 0xffu);
     for (uint32_t i0 = blockIdx.x * blockDim.x * LCP_U + threadIdx.x; i0 < n; i0 += stride) {
         uint64_t k[LCP_U];
 #pragma unroll
@@ -1304,13 +1310,36 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
             const uint32_t i = i0 + u * blockDim.x;
             k[u] = i < n ? keys[i] : 0ull;
         }
+        bool slow[LCP_U];
 #pragma unroll
         for (int u = 0; u < LCP_U; ++u) {
             const uint32_t i = i0 + u * blockDim.x;
+            const uint32_t tk = (uint32_t)(k[u] & 0xffu);
+            slow[u] = i < n && ((k[u] ^ kr) >> 8) == 0 && tk >= 8u && tr >= 8u && best > 7u;
             if (i < n) {
-                best = min(best, lcp_one(buf, spans, i, k[u], rbuf, rspans, kr, best));
                 acc.add(k[u]);
+                if (!slow[u]) best = min(best, lcp_one(buf, spans, i, k[u], rbuf, rspans, kr, best));
             }
+        }
+        uint2 xs[LCP_U];
+#pragma unroll
+        for (int u = 0; u < LCP_U; ++u) xs[u] = slow[u] ? spans[i0 + u * blockDim.x] : make_uint2(0u, 0u);
+        uint64_t d[LCP_U];
+        uint32_t m[LCP_U], tt[LCP_U];
+#pragma unroll
+        for (int u = 0; u < LCP_U; ++u) {
+            m[u] = min(min(xs[u].y - xs[u].x, rlen), best);
+            tt[u] = m[u] > 7u ? min(m[u] - 7u, 8u) : 0u;
+            d[u] = (slow[u] && tt[u]) ? (load_le(buf, xs[u].x + 7u, tt[u]) ^ load_le(rbuf, r.x + 7u, tt[u])) : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < LCP_U; ++u) {
+            if (!slow[u]) continue;
+            uint32_t l;
+            if (d[u]) l = 7u + ((uint32_t)__builtin_ctzll(d[u]) >> 3);
+            else if (7u + tt[u] >= m[u]) l = m[u];
+            else l = lcp_one(buf, spans, i0 + u * blockDim.x, k[u], rbuf, rspans, kr, best);
+            best = min(best, min(l, m[u]));
         }
     }
 #pragma unroll
@@ -2019,7 +2048,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const bool want_hist = Lc.n_rec >= 4096;
     uint32_t *shist = nullptr, hist_n = 0;
     KeyStatD *parts = nullptr;  // per-block partials (k_lcp / k_key_stats / k_rekey blocks)
-    const uint32_t g_cur = std::min<uint32_t>(grid_for(Lc.n_rec, 256), 512u);
+    // (2048 blocks: 512 left C2's 10M-key prefix scan at 2 waves per SIMD)
+    const uint32_t g_cur = std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u);
     const uint32_t g_rekey = std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u);
     if (want_hist) {
         shist = dflag + 32;
@@ -2032,7 +2062,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     else if (want_hist)
         SG_LAUNCH_B(c, "key_stats", 8.0 * Lc.n_rec, k_key_stats, g_cur, 256, 0, Lc.keys, Lc.n_rec, parts);
     if (rsp && have_prior && Lp.n_rec)
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 512u), 256, 0, d_prior,
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior,
                     Lp.spans, Lp.keys, Lp.n_rec, rbuf, rsp, rkeys, dflag + 1, (KeyStatD *)nullptr);
     // the sample histograms (and the combined partials) come back with the flags; they stay
     // valid when the common prefix turns out to be empty
