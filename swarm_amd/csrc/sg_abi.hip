@@ -323,7 +323,7 @@ static int pack_byte_splitters(const uint8_t *splitters, const uint32_t *split_o
 // inside the tile's ~100 KB of input. Replaces a radix sort of the record ids by part and one
 // gather-emit per part (random 27-B reads: C5's part_emit ran at ~1.6 TB/s).
 constexpr int PT_BLOCK = 256;
-constexpr int PT_ITEMS = 8;
+constexpr int PT_ITEMS = 2;
 constexpr uint32_t PT_TILE = PT_BLOCK * PT_ITEMS;
 
 // bytes (record + '\n') per (part, tile), part-major: cnt[q * ntiles + t]
@@ -484,8 +484,8 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         const uint2 x = s_sp[q];
         const uint64_t dst = s_dst[lo] + s_off[q];
         uint64_t k0 = 0;
-        if (so.sp) put_medium<true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
-        else put_medium(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
+        if (so.sp) put_medium<true, true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
+        else put_medium<false, true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
         finish(q, lo, x, dst, k0);
     }
 }

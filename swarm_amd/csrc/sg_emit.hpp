@@ -153,6 +153,92 @@ __device__ __forceinline__ void put_win64(uint8_t *base, uint32_t d, const uint4
     }
 }
 
+// put_win64 for a global destination with fewer store instructions: the record's whole
+// destination dwords leave as 16-, 8- and 4-byte stores (dword-aligned vectors), its partial
+// first and last dwords as byte + 16-bit + byte stores. A lane-per-record copy issues every
+// store instruction any lane of the wave needs: 18 dword and 8 byte stores per window before.
+typedef uint32_t sg_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t sg_u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ void put_edge(uint8_t *p, uint32_t v, uint32_t lo, uint32_t hi) {
+    // bytes [lo, hi) of the dword at p (0 <= lo < hi <= 4)
+    if (lo < hi && (lo & 1u)) { p[lo] = (uint8_t)(v >> (8u * lo)); ++lo; }
+    if (hi >= lo + 2u) { *reinterpret_cast<uint16_t *>(p + lo) = (uint16_t)(v >> (8u * lo)); lo += 2u; }
+    if (lo < hi) p[lo] = (uint8_t)(v >> (8u * lo));
+}
+
+__device__ __forceinline__ void put_win64_v(uint8_t *base, uint32_t d, const uint4 (&c)[4], uint32_t sh, uint32_t len,
+                                            bool nl) {
+    const uint32_t dw[20] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w,
+                             c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w, 0u, 0u, 0u, 0u};
+    const uint32_t t = sh >> 2, e = sh & 3u;
+    const uint32_t m2 = (t & 2u) ? ~0u : 0u, m1 = (t & 1u) ? ~0u : 0u;
+    uint32_t s1[18], s2[17], rec[17];
+#pragma unroll
+    for (int o = 0; o < 18; ++o) s1[o] = dw[o] ^ ((dw[o] ^ dw[o + 2]) & m2);
+#pragma unroll
+    for (int o = 0; o < 17; ++o) s2[o] = s1[o] ^ ((s1[o] ^ s1[o + 1]) & m1);
+#pragma unroll
+    for (int o = 0; o < 17; ++o) {
+        uint32_t x = (o < 16) ? __builtin_amdgcn_alignbyte(s2[o + 1], s2[o], e) : 0u;
+        const uint32_t b0 = 4u * o;
+        if (b0 + 4u > len) {
+            if (b0 <= len) {
+                const uint32_t k = len - b0;
+                x = (x & ((1u << (8u * k)) - 1u)) | (nl ? (0x0au << (8u * k)) : 0u);
+            } else {
+                x = 0u;
+            }
+        }
+        rec[o] = x;
+    }
+    const uint32_t f = d & 3u, D = d - f, end = f + len + (nl ? 1u : 0u);
+    const uint32_t mf = f ? ~0u : 0u;
+    // destination dword j (bytes [4j, 4j + 4) from D)
+    uint32_t v[18];
+#pragma unroll
+    for (int j = 0; j < 18; ++j) {
+        const uint32_t cur = (j < 17) ? rec[j] : 0u;
+        const uint32_t lo = (j > 0) ? rec[j - 1] : 0u;
+        const uint32_t sh_v = __builtin_amdgcn_alignbyte(cur, lo, (4u - f) & 3u);
+        v[j] = (cur & ~mf) | (sh_v & mf);
+    }
+    if (end == 0u) return;
+    uint8_t *B = base + D;
+    const uint32_t je = end >> 2;           // dwords [0, je) end inside the record
+    const uint32_t jf = f ? 1u : 0u;       // the first whole dword
+    // partial edges: dword 0 when f > 0, dword je when end is not a multiple of 4
+    if (f) put_edge(B, v[0], f, je == 0u ? end : 4u);
+    if ((end & 3u) && je >= jf) {
+        uint32_t vt = 0;
+#pragma unroll
+        for (int j = 1; j < 18; ++j) vt = (je == (uint32_t)j) ? v[j] : vt;
+        if (je == 0u) vt = v[0];
+        if (!(f && je == 0u)) put_edge(B + 4u * je, vt, 0u, end & 3u);
+    }
+    // whole dwords [jf, je): u[k] = v[jf + k]
+    const uint32_t ni = je > jf ? je - jf : 0u;
+    uint32_t u[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) u[k] = f ? v[k + 1] : v[k];
+    uint8_t *A = B + 4u * jf;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+        if (4u * g + 4u <= ni)
+            *reinterpret_cast<sg_u32x4_a4 *>(A + 16u * g) = sg_u32x4_a4{u[4 * g], u[4 * g + 1], u[4 * g + 2], u[4 * g + 3]};
+    const uint32_t r0 = ni & ~3u, rem = ni & 3u;
+    auto sel = [&](uint32_t i) -> uint32_t {  // u[i], i in {0, 1, 2, 4, 5, 6, ..., 16}
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 17; ++k) x = (i == (uint32_t)k) ? u[k] : x;
+        return x;
+    };
+    if (rem >= 2u) *reinterpret_cast<sg_u32x2_a4 *>(A + 4u * r0) = sg_u32x2_a4{sel(r0), sel(r0 + 1u)};
+    if (rem & 1u) {
+        const uint32_t i = r0 + (rem & 2u);
+        *reinterpret_cast<uint32_t *>(A + 4u * i) = sel(i);
+    }
+}
+
 // A medium record (longer than the short path, <= EM_MED bytes) copied by its own lane in
 // 64-byte windows: each window's four 16-B loads are issued together, and all lanes of the
 // wave copy their records at once (the 16-lane group path copies one record per group at a
@@ -178,7 +264,7 @@ __device__ __forceinline__ uint64_t win_key0(const uint4 (&c)[4], uint32_t sh, u
 
 // key0 (optional): the record's chunk_key(src, s, s + len, 0), taken from the first window's
 // loads instead of loading its first bytes again.
-template <bool KEY = false>
+template <bool KEY = false, bool VEC = false>
 __device__ __forceinline__ void put_medium(const uint8_t *src, uint8_t *base, uint32_t d, uint32_t s, uint32_t len,
                                            uint64_t *key0 = nullptr) {
     const uint32_t q0 = s & ~15u, sh = s - q0;
@@ -192,7 +278,8 @@ __device__ __forceinline__ void put_medium(const uint8_t *src, uint8_t *base, ui
             c[k] = (16u * k < ws + wl) ? *reinterpret_cast<const uint4 *>(src + q0 + wo + 16u * k) : make_uint4(0u, 0u, 0u, 0u);
         if (KEY && wo == 0) *key0 = win_key0(c, sh, len);
         const bool nl = done + wl == len;
-        put_win64(base, d + done, c, ws, wl, nl);
+        if (VEC) put_win64_v(base, d + done, c, ws, wl, nl);
+        else put_win64(base, d + done, c, ws, wl, nl);
         done += wl;
         if (nl) break;
     }
