@@ -263,6 +263,15 @@ __device__ __forceinline__ uint64_t chunk_key(const uint8_t *buf, uint32_t s, ui
     return (__builtin_bswap64(v) & ~0xffull) | tag;
 }
 
+// Bytes [lo, hi) of the little-endian dword v stored at p (p 4-byte aligned, 0 <= lo <= hi
+// <= 4): at most a byte, a 16-bit and a byte store (a partial dword shared with a
+// neighbouring lane's bytes).
+__device__ __forceinline__ void put_edge(uint8_t *p, uint32_t v, uint32_t lo, uint32_t hi) {
+    if (lo < hi && (lo & 1u)) { p[lo] = (uint8_t)(v >> (8u * lo)); ++lo; }
+    if (hi >= lo + 2u) { *reinterpret_cast<uint16_t *>(p + lo) = (uint16_t)(v >> (8u * lo)); lo += 2u; }
+    if (lo < hi) p[lo] = (uint8_t)(v >> (8u * lo));
+}
+
 // Bytes [p, p+t) (t <= 8) little-endian in a u64, zero above; buf 8-byte aligned.
 __device__ __forceinline__ uint64_t load_le(const uint8_t *buf, uint32_t p, uint32_t t) {
     const uint32_t a = p & ~7u;

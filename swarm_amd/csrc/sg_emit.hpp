@@ -159,12 +159,6 @@ __device__ __forceinline__ void put_win64(uint8_t *base, uint32_t d, const uint4
 // store instruction any lane of the wave needs: 18 dword and 8 byte stores per window before.
 typedef uint32_t sg_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t sg_u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
-__device__ __forceinline__ void put_edge(uint8_t *p, uint32_t v, uint32_t lo, uint32_t hi) {
-    // bytes [lo, hi) of the dword at p (0 <= lo < hi <= 4)
-    if (lo < hi && (lo & 1u)) { p[lo] = (uint8_t)(v >> (8u * lo)); ++lo; }
-    if (hi >= lo + 2u) { *reinterpret_cast<uint16_t *>(p + lo) = (uint16_t)(v >> (8u * lo)); lo += 2u; }
-    if (lo < hi) p[lo] = (uint8_t)(v >> (8u * lo));
-}
 
 __device__ __forceinline__ void put_win64_v(uint8_t *base, uint32_t d, const uint4 (&c)[4], uint32_t sh, uint32_t len,
                                             bool nl) {
@@ -350,7 +344,10 @@ __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src0
             put_win64(bp, d + bs, cs, 0u, len - bs, true);
         }
     }
-    if (medr) put_medium(src, in_lds ? win : out + base, d, s, len);
+    if (medr) {
+        if (in_lds) put_medium(src, win, d, s, len);
+        else put_medium<false, true>(src, out + base, d, s, len);
+    }
     if (ml) {
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
