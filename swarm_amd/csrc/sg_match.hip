@@ -730,6 +730,7 @@ struct LitArgs {
     const uint32_t *fac_off, *fac_pids;  // regex prefilter expansion (else null)
     uint2 *spans_out;                    // non-null: also write the parse's record spans (fused A3)
     uint8_t *rec_flag;                   // non-null: mark matched records here instead of listing hits
+    uint32_t rank_lds;                   // the bitmap words' ranks staged in LDS too (else read from L2)
 };
 
 constexpr uint32_t LS_HB = 256;    // per-block LDS hit buffer (entries)
@@ -828,8 +829,14 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
     __shared__ uint32_t s_red[BLK / 64];
     __shared__ uint32_t s_hn, s_g, s_base, s_ebase;
     uint32_t *s_bm = s_dyn;
+    // The bitmap words' ranks (a candidate's bucket lookup) are staged after the bitmaps unless
+    // leaving them in L2 gives the CU another block (their LDS is half the bitmaps': the fields
+    // matcher's tables 68 -> 45 KB, 1 -> 2 blocks per CU, lit_match 8.2 -> 5.7 ms).
     uint16_t *s_rank = reinterpret_cast<uint16_t *>(s_dyn + a.bm_words);
-    for (uint32_t q = threadIdx.x; q < a.bm_words; q += BLK) { s_bm[q] = a.bitmap[q]; s_rank[q] = a.rank[q]; }
+    for (uint32_t q = threadIdx.x; q < a.bm_words; q += BLK) {
+        s_bm[q] = a.bitmap[q];
+        if (a.rank_lds) s_rank[q] = a.rank[q];
+    }
     if (threadIdx.x == 0) s_hn = 0;
     __syncthreads();
     const uint32_t t = threadIdx.x;
@@ -1029,7 +1036,8 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                 const uint32_t key = (c >= 3) ? k0 : (k0 & ((1u << (8 * (c + 1))) - 1u));
                 const uint32_t h = lit_h(key, k1, c, a.bits[c]);
                 const uint32_t wi = a.bm_off[c] + (h >> 5);
-                const uint32_t k = a.rank_base[c] + s_rank[wi] + (uint32_t)__popc(s_bm[wi] & ((1u << (h & 31)) - 1u));
+                const uint32_t rk = a.rank_lds ? (uint32_t)s_rank[wi] : (uint32_t)a.rank[wi];
+                const uint32_t k = a.rank_base[c] + rk + (uint32_t)__popc(s_bm[wi] & ((1u << (h & 31)) - 1u));
                 // fingerprints: the gram itself (entries shorter than 8) and the 8-gram's
                 s_kf[i] = make_uint2(k, lit_fp8(k0, k1));
             }
@@ -1122,10 +1130,10 @@ __global__ __launch_bounds__(BLK) void k_lit_trial(LitArgs a) {
     lit_scan_body<BLK, BPT, CM>(a);
 }
 
-// LDS bytes of k_lit_scan's dynamic tables for a filter (entries in LDS when they fit).
-static uint32_t lit_lds_bytes(const sg_matcher::Lit &T) {
+// LDS bytes of k_lit_scan's dynamic tables for a filter: the bitmaps (u32), + their ranks (u16).
+static uint32_t lit_lds_bytes(const sg_matcher::Lit &T, bool ranks = true) {
     const uint32_t bmw = (uint32_t)T.bitmap.size();
-    return 4u * (bmw + (bmw + 1) / 2);  // bitmaps (u32) + ranks (u16)
+    return 4u * bmw + (ranks ? 4u * ((bmw + 1) / 2) : 0u);
 }
 
 // ------------------------------------------------------------------ device: regex DFAs
@@ -1736,8 +1744,13 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         a.spans_out = (!trial_tiles && fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
         a.rec_flag = (mf && !trial_tiles) ? mf->flags : nullptr;
         const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + 64;
-        const uint32_t dyn = lit_lds_bytes(Lt);
-        const uint32_t bpc = std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
+        auto blocks_per_cu = [&](uint32_t dyn) {
+            return std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
+        };
+        const uint32_t dyn_r = lit_lds_bytes(Lt, true), dyn_n = lit_lds_bytes(Lt, false);
+        a.rank_lds = blocks_per_cu(dyn_r) == blocks_per_cu(dyn_n) ? 1u : 0u;
+        const uint32_t dyn = a.rank_lds ? dyn_r : dyn_n;
+        const uint32_t bpc = blocks_per_cu(dyn);
         const uint32_t grid = std::min<uint32_t>(a.n_tiles, 256u * bpc);
         // Block size: when the tables leave room for only <= 2 blocks per CU (large factor
         // sets: the regex prefilter), 512-thread blocks double the waves that hide the
@@ -1813,8 +1826,8 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
                 m = best[1] < LIT_MARGIN * best[0] ? 1 : 0;
                 mode.store(m);
                 if (sw_lit_trial_log())
-                    fprintf(stderr, "sg lit scheme: trial %u tiles, best two %.3f ms joint %.3f ms -> %s\n", tt, best[0], best[1],
-                            m ? "joint" : "two");
+                    fprintf(stderr, "sg lit scheme: trial %u tiles, best two %.3f ms joint %.3f ms -> %s (tables: two %u B, joint %u B of LDS)\n",
+                            tt, best[0], best[1], m ? "joint" : "two", lit_lds_bytes(two), lit_lds_bytes(joint));
             }
         }
         return m == 1 ? joint : two;
