@@ -77,6 +77,8 @@ enum Slot : int {
     S_LS_LIST, S_LF_OFF, S_LF_KEY, S_LF_KEY2, S_LF_VAL, S_LF_VAL2, S_LF_POS,  // its overflow fix-up
     S_STAGE,  // dedup: the sorted staging T (32-B slots)
     S_FD_LB,  // dedup: the fused diff's prior range per emit tile
+    S_KEYSL, S_KEYSL2,  // dedup: cur / prior keys at the last call's common prefix (speculative)
+    S_SPEC_PARTS,       // X1: the speculative keys' KeyStatD partials
     S_NSLOTS
 };
 
@@ -102,6 +104,7 @@ struct sg_ctx {
                               // re-sort, bit 2 its overflow fix-up, bit 3 all-segments mode
     uint32_t last_kw = 7;     // dedup: key width (bytes) the last radix sort used
     float last_uniq_frac = 1.0f;  // dedup: unique / input records of the last sort -u (all-segments mode)
+    uint32_t last_base = 0;       // dedup: the last call's common prefix (keys taken there speculatively)
     uint32_t hist_host[8 * 256] = {};  // dedup: digit histograms of the current keys (host copy)
     // the last hybrid radix sort's local-sort plan (lsort_fixup redoes its flagged tiles)
     struct LsLast {

@@ -22,6 +22,7 @@
 // The result is exact for any input (NULs, CR, 0xff, long shared prefixes, duplicates of
 // any multiplicity): ordering is decided by bytes, never by a hash.
 #include "sg_internal.hpp"
+#include "sg_keystat.hpp"
 #include "sg_prims_host.hpp"
 #include "sg_emit.hpp"
 #include "sg_switches.hpp"
@@ -1225,39 +1226,6 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_uniq_diff(const uint2 *__rest
 // min(tag, kw + 1) varies iff its clamped ends differ). Each block writes its partial with
 // plain stores; k_key_sample's first block combines them (512 blocks' atomics on one line
 // serialised: +20 µs on C2's cur keys).
-struct KeyStatAcc {
-    uint64_t o = 0, a = ~0ull;
-    uint32_t tmin = 255u, tmax = 0u;
-    __device__ __forceinline__ void add(uint64_t k) {
-        o |= k;
-        a &= k;
-        const uint32_t t = (uint32_t)(k & 0xffu);
-        tmin = min(tmin, t);
-        tmax = max(tmax, t);
-    }
-};
-// Block-wide reduce (256 threads) into part[blockIdx.x]; s: 4 x KeyStatD of LDS.
-__device__ __forceinline__ void kstat_flush(KeyStatAcc acc, KeyStatD *s, KeyStatD *part) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        acc.o |= (uint64_t)__shfl_xor((long long)acc.o, off, 64);
-        acc.a &= (uint64_t)__shfl_xor((long long)acc.a, off, 64);
-        acc.tmin = min(acc.tmin, (uint32_t)__shfl_xor((int)acc.tmin, off, 64));
-        acc.tmax = max(acc.tmax, (uint32_t)__shfl_xor((int)acc.tmax, off, 64));
-    }
-    const int wid = threadIdx.x >> 6;
-    if (lane_id() == 0) s[wid] = KeyStatD{acc.o, acc.a, acc.tmin, acc.tmax};
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; ++w) {
-            acc.o |= s[w].o;
-            acc.a &= s[w].a;
-            acc.tmin = min(acc.tmin, s[w].tmin);
-            acc.tmax = max(acc.tmax, s[w].tmax);
-        }
-        part[blockIdx.x] = KeyStatD{acc.o, acc.a, acc.tmin, acc.tmax};
-    }
-}
 
 // The common prefix of one record (key k, span xs) with the reference record.
 __device__ __forceinline__ uint32_t lcp_one(const uint8_t *buf, const uint2 *spans, uint32_t i, uint64_t k,
@@ -1287,12 +1255,13 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
                                              const uint64_t *__restrict__ keys, uint32_t n,
                                              const uint8_t *__restrict__ rbuf, const uint2 *__restrict__ rspans,
                                              const uint64_t *__restrict__ rkeys, uint32_t *__restrict__ out,
-                                             KeyStatD *__restrict__ st) {
+                                             KeyStatD *__restrict__ st, uint64_t *__restrict__ keysL = nullptr,
+                                             uint32_t Ls = 0, KeyStatD *__restrict__ stL = nullptr) {
     __shared__ uint32_t s_min[4];
     __shared__ KeyStatD s_st[4];
     const uint64_t kr = rkeys[0];
     uint32_t best = 255;
-    KeyStatAcc acc;
+    KeyStatAcc acc, accL;
     // grid-stride (at most 2048 blocks): at most one memory-side atomic per block and word;
     // LCP_U keys in flight per thread (one dependent load per trip left the loop latency-bound:
     // 1.6 TB/s on C2's cur keys)
@@ -1324,13 +1293,14 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
         uint2 xs[LCP_U];
 #pragma unroll
         for (int u = 0; u < LCP_U; ++u) xs[u] = slow[u] ? spans[i0 + u * blockDim.x] : make_uint2(0u, 0u);
-        uint64_t d[LCP_U];
+        uint64_t d[LCP_U], raw[LCP_U];
         uint32_t m[LCP_U], tt[LCP_U];
 #pragma unroll
         for (int u = 0; u < LCP_U; ++u) {
             m[u] = min(min(xs[u].y - xs[u].x, rlen), best);
             tt[u] = m[u] > 7u ? min(m[u] - 7u, 8u) : 0u;
-            d[u] = (slow[u] && tt[u]) ? (load_le(buf, xs[u].x + 7u, tt[u]) ^ load_le(rbuf, r.x + 7u, tt[u])) : 0ull;
+            raw[u] = (slow[u] && tt[u]) ? load_le(buf, xs[u].x + 7u, tt[u]) : 0ull;
+            d[u] = (slow[u] && tt[u]) ? (raw[u] ^ load_le(rbuf, r.x + 7u, tt[u])) : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < LCP_U; ++u) {
@@ -1341,11 +1311,37 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
             else l = lcp_one(buf, spans, i0 + u * blockDim.x, k[u], rbuf, rspans, kr, best);
             best = min(best, min(l, m[u]));
         }
+        // keysL (Ls >= 8, the last call's common prefix): the keys at Ls of the records that
+        // tie the reference on key0 (their bytes are in cache). Every record is one of them
+        // when the common prefix comes out at Ls again; otherwise the keys are rebuilt.
+        if (keysL) {
+#pragma unroll
+            for (int u = 0; u < LCP_U; ++u) {
+                if (!slow[u]) continue;
+                // at Ls = 8 the key's bytes 8..14 are in hand (bytes 7..14 were just loaded)
+                const uint32_t len = xs[u].y - xs[u].x, rem = len > Ls ? len - Ls : 0u;
+                uint64_t kl;
+                if (Ls == 8u && tt[u] == 8u) {
+                    const uint32_t take = rem < 7u ? rem : 7u;
+                    kl = rem ? ((__builtin_bswap64((raw[u] >> 8) & ((1ull << (8u * take)) - 1ull)) & ~0xffull) |
+                                (uint64_t)(rem < 8u ? rem : 8u))
+                             : 0ull;
+                } else {
+                    kl = chunk_key(buf, xs[u].x, xs[u].y, Ls);
+                }
+                keysL[i0 + u * blockDim.x] = kl;
+                accL.add(kl);
+            }
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
     if (lane_id() == 0) s_min[threadIdx.x >> 6] = best;
     if (st) kstat_flush(acc, s_st, st);
+    if (stL) {
+        __syncthreads();  // s_st reused
+        kstat_flush(accL, s_st, stL);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
@@ -2016,7 +2012,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     // (the front of one slot with the sample histograms and the stat partials after it: the
     // flags, the stats and the histograms come back in one copy)
     uint32_t *dflag;
-    SG_TRY(slot(c, S_HIST, 32 + 8 * 256 + 2048 * sizeof(KeyStatD) / 4, &dflag));
+    SG_TRY(slot(c, S_HIST, 32 + 8 * 256 + 2 * 2048 * sizeof(KeyStatD) / 4, &dflag));
     KeyStatD *st0 = reinterpret_cast<KeyStatD *>(dflag + 4), *st1 = reinterpret_cast<KeyStatD *>(dflag + 12);
     {
         uint32_t init[20] = {0u, 255u};
@@ -2056,14 +2052,36 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         parts = reinterpret_cast<KeyStatD *>(shist + 8 * 256);
         SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));
     }
+    // Speculation: when the last call's records shared a prefix of >= 8 bytes (URL lists),
+    // the prefix scans also write the keys at that offset, so a common prefix that comes out
+    // the same needs no re-key pass (and its second key-statistics pass reads these keys).
+    // (cur gathered elsewhere, cur_lcp: its gatherer wrote the speculative keys, Lines::spec_*)
+    const bool cur_spec = !cur_lcp || (Lc.spec_keys && Lc.spec_off == c->last_base);
+    const uint32_t Ls = (c->last_base >= 8u && rsp && want_hist && cur_spec) ? c->last_base : 0u;
+    uint64_t *kLc = nullptr, *kLp = nullptr;
+    KeyStatD *partsL = nullptr;
+    uint32_t npartsL = 0;
+    if (Ls) {
+        if (cur_lcp) {
+            kLc = Lc.spec_keys;
+            partsL = const_cast<KeyStatD *>(Lc.spec_parts);
+            npartsL = Lc.spec_nparts;
+        } else {
+            SG_TRY(slot(c, S_KEYSL, (size_t)Lc.n_rec + 1, &kLc));
+            partsL = parts + 2048;
+            npartsL = g_cur;
+        }
+        if (have_prior && Lp.n_rec) SG_TRY(slot(c, S_KEYSL2, (size_t)Lp.n_rec + 1, &kLp));
+    }
     if (rsp && Lc.n_rec && !cur_lcp)
         SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, g_cur, 256, 0, d_cur, Lc.spans, Lc.keys, Lc.n_rec, rbuf, rsp, rkeys,
-                    dflag + 1, parts);
+                    dflag + 1, parts, kLc, Ls, partsL);  // (not reached with cur_lcp)
     else if (want_hist)
         SG_LAUNCH_B(c, "key_stats", 8.0 * Lc.n_rec, k_key_stats, g_cur, 256, 0, Lc.keys, Lc.n_rec, parts);
     if (rsp && have_prior && Lp.n_rec)
         SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior,
-                    Lp.spans, Lp.keys, Lp.n_rec, rbuf, rsp, rkeys, dflag + 1, (KeyStatD *)nullptr);
+                    Lp.spans, Lp.keys, Lp.n_rec, rbuf, rsp, rkeys, dflag + 1, (KeyStatD *)nullptr, kLp, Ls,
+                    (KeyStatD *)nullptr);
     // the sample histograms (and the combined partials) come back with the flags; they stay
     // valid when the common prefix turns out to be empty
     if (want_hist) SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, parts, g_cur, st0));
@@ -2082,16 +2100,24 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint32_t base = (rsp && (Lc.n_rec || (have_prior && Lp.n_rec))) ? fl[1] : 0u;
     if (base) {
         if (want_hist) SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));
-        SG_LAUNCH(c, "rekey", k_rekey, g_rekey, 256, 0, d_cur, Lc.spans, Lc.n_rec, base, Lc.keys, parts);
-        if (have_prior && Lp.n_rec)
-            SG_LAUNCH(c, "rekey", k_rekey, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior, Lp.spans,
-                      Lp.n_rec, base, Lp.keys, (KeyStatD *)nullptr);
+        const bool spec = Ls && base == Ls;
+        if (spec) {  // the speculative keys are every record's keys at the common prefix
+            Lc.keys = kLc;
+            if (kLp) Lp.keys = kLp;
+        } else {
+            SG_LAUNCH(c, "rekey", k_rekey, g_rekey, 256, 0, d_cur, Lc.spans, Lc.n_rec, base, Lc.keys, parts);
+            if (have_prior && Lp.n_rec)
+                SG_LAUNCH(c, "rekey", k_rekey, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior,
+                          Lp.spans, Lp.n_rec, base, Lp.keys, (KeyStatD *)nullptr);
+        }
         if (want_hist) {  // keys changed: their statistics again
-            SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, parts, g_rekey, st1));
+            SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, spec ? partsL : parts, spec ? npartsL : g_rekey,
+                                   st1));
             SG_TRY(read_stats(20u));
             memcpy(fl + 4, fl + 12, sizeof(KeyStatD));
         }
     }
+    c->last_base = base;
     // Key width: the cur keys' sampled digit histograms give each byte position's entropy;
     // when the first 6 (or 5) key bytes already carry well over as many bits as there are
     // records (expected << 1 record per key value, so few tie segments), the keys are

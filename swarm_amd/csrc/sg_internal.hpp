@@ -29,6 +29,12 @@ struct Lines {
     // tile_bytes bytes): the tile prefixes of the parse's reduce-then-scan.
     const uint64_t *tile_excl = nullptr;
     uint32_t tile_bytes = 0, n_tiles = 0;
+    // Keys at offset spec_off (the context's last common prefix, >= 8) written by whoever
+    // gathered the records (X1's matched records), with their per-block KeyStatD partials:
+    // used when the common prefix comes out at spec_off again (sg_dedup.hip).
+    uint64_t *spec_keys = nullptr;
+    const struct KeyStatD *spec_parts = nullptr;
+    uint32_t spec_off = 0, spec_nparts = 0;
 };
 // Split d_buf (16-byte aligned device pointer, n bytes) into non-empty records.
 // apply = false: count and allocate only; the spans are then written by a consumer that

@@ -14,6 +14,7 @@
 // radix-sorted and de-duplicated, so hits come out sorted by (record, signature) and the
 // matched lines in input order (grep's output).
 #include "sg_internal.hpp"
+#include "sg_keystat.hpp"
 #include "sg_switches.hpp"
 #include "sg_prims_host.hpp"
 
@@ -1639,10 +1640,16 @@ __global__ void k_split_hits(const unsigned long long *K, const uint32_t *idx, u
 // Matched records (input order) -> their spans and key0 from byte 0, and (block minimum, a
 // guarded atomic per block) their common prefix with the first matched record — the dedup's
 // common-prefix scan of these records, done while their first bytes are being read anyway.
+// keysL (Ls >= 8, the context's last common prefix): also the keys at Ls and their KeyStatD
+// partial per block (stL), for the records tying the first one on key0 (all of them when the
+// common prefix comes out at Ls again).
 __global__ __launch_bounds__(256) void k_gather_matched(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                                         const uint32_t *__restrict__ mrec, uint32_t m, uint2 *__restrict__ sp,
-                                                        uint64_t *__restrict__ keys, uint32_t *__restrict__ lcp_out) {
+                                                        uint64_t *__restrict__ keys, uint32_t *__restrict__ lcp_out,
+                                                        uint64_t *__restrict__ keysL, uint32_t Ls, KeyStatD *__restrict__ stL) {
     __shared__ uint32_t s_min[4];
+    __shared__ KeyStatD s_st[4];
+    KeyStatAcc accL;
     const uint2 r = spans[mrec[0]];
     const uint64_t kr = chunk_key(buf, r.x, r.y, 0);
     const uint32_t tr = (uint32_t)(kr & 0xffu);
@@ -1669,9 +1676,15 @@ __global__ __launch_bounds__(256) void k_gather_matched(const uint8_t *__restric
                 l += t;
             }
             l = min(l, mm);
+            if (keysL) {
+                const uint64_t kl = chunk_key(buf, x.x, x.y, Ls);
+                keysL[i] = kl;
+                accL.add(kl);
+            }
         }
         best = min(best, l);
     }
+    if (stL) kstat_flush(accL, s_st, stL);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
     if (lane_id() == 0) s_min[threadIdx.x >> 6] = best;
@@ -2170,8 +2183,19 @@ int sg_dev_match_dedup_diff(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, size
         SG_TRY(slot(c, S_M_TMP, 4, &lcp));
         const uint32_t init = 255u;
         SG_HIP(hipMemcpyAsync(lcp, &init, 4, hipMemcpyHostToDevice, c->stream));
-        if (M) SG_LAUNCH_B(c, "gather_matched", 24.0 * M, k_gather_matched, std::min<uint32_t>((M + 255) / 256, 2048u), 256, 0,
-                           b, mf.L.spans, mrec, M, Lm.spans, Lm.keys, lcp);
+        const uint32_t gg = std::min<uint32_t>((M + 255) / 256, 2048u);
+        // keys at the last call's common prefix too (see sg_dedup.hip: a re-key pass saved
+        // when the matched records share that prefix again)
+        KeyStatD *gparts = nullptr;
+        if (M >= 4096 && c->last_base >= 8u) {
+            SG_TRY(slot(c, S_KEYSL, (size_t)M + 1, &Lm.spec_keys));
+            SG_TRY(slot(c, S_SPEC_PARTS, (size_t)gg * sizeof(KeyStatD) / 8 + 1, &gparts));
+            Lm.spec_off = c->last_base;
+            Lm.spec_parts = gparts;
+            Lm.spec_nparts = gg;
+        }
+        if (M) SG_LAUNCH_B(c, "gather_matched", 24.0 * M, k_gather_matched, gg, 256, 0, b, mf.L.spans, mrec, M, Lm.spans,
+                           Lm.keys, lcp, Lm.spec_keys, Lm.spec_off, gparts);
         if (matched_records) *matched_records = M;
         SG_TRY(dev_dedup_diff_lines(c, b, n, Lm, n_prior ? p : nullptr, n_prior, res, M ? lcp : nullptr));
         res->in_records = R;

@@ -664,3 +664,39 @@ def test_seg_all_mode_hostports(sg, monkeypatch, segall, names):
             assert (ctx.last_key_width() == 7) == (names == "digits")
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_prefix_key_speculation_sequence(sg):
+    """Keys taken speculatively at the last call's common prefix (>= 8 bytes): a sequence of
+    calls on one context whose prefix stays, grows, shrinks and vanishes, each output against
+    the oracle (a wrong speculation falls back to re-keying)."""
+    import torch
+    rng = np.random.default_rng(57)
+
+    def urls(prefix, n, extra=b""):
+        return [prefix + bytes(rng.choice(list(b"abcdefgh./"), size=int(rng.integers(1, 20)))) + extra
+                for _ in range(n)]
+
+    seq = [
+        urls(b"https://", 60_000),                      # base 8 (speculation armed)
+        urls(b"https://", 60_000),                      # base 8 again: speculative keys used
+        urls(b"https://www.", 60_000),                  # base 12 != 8: re-keyed
+        urls(b"https://www.", 50_000) + [b"https://x"],  # prefix drops back to 8
+        urls(b"http://", 60_000),                       # base 7: no speculation next
+        urls(b"", 60_000),                              # no common prefix
+        urls(b"https://", 60_000),
+    ]
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        for recs in seq:
+            cur = b"\n".join(recs) + b"\n"
+            prior = S.dedup(b"\n".join(recs[::4]) + b"\n")
+            dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+            dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+            r = ctx.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+            eu, ef = S.dedup_diff(cur, prior)
+            assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+            assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+    finally:
+        ctx.close()

@@ -126,3 +126,29 @@ def test_fused_flag_path_edge_records(ctx, seed, monkeypatch):
     none = swarm_amd.Matcher([b"never-there"], "literal")
     u, f, r, nh, nm = fused(ctx, none, data, prior, count_hits=False)
     assert (u, f, nm) == (b"", b"", 0)
+
+
+def test_fused_prefix_key_speculation(sigs):
+    """Repeated fused steps on one context: the matched records' keys are also taken at the
+    last call's common prefix (>= 8 bytes: httpx lines start with https://), used when the
+    prefix comes out the same, re-keyed otherwise; every output against the oracle."""
+    import torch
+    import swarm_amd
+    c = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        m = swarm_amd.Matcher(sigs, "literal")
+        tails = corpus.httpx_tails(sigs, n_tails=512, seed=7)
+        for step, (n, seed, swap) in enumerate([(30000, 7, None), (30000, 8, None), (30000, 9, (b"https://", b"http://x")),
+                                                 (30000, 10, None)]):
+            buf, ids = corpus.httpx_hosts(n, tails, seed=seed, universe=n // 2)
+            data = buf.tobytes()
+            if swap:
+                data = data.replace(swap[0], swap[1])
+            prior_all = corpus.httpx_rows(corpus.prior_ids(ids), tails).tobytes()
+            prior = S.dedup(S.matched_lines(prior_all, S.literal_hits(prior_all, sigs)))
+            for count_hits in (False, True):
+                u, f, r, nh, nm = fused(c, m, data, prior, count_hits)
+                eu, ef, hits, matched = oracle(data, sigs, prior)
+                assert u == eu and f == ef, (step, count_hits)
+    finally:
+        c.close()
