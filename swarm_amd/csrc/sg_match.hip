@@ -1669,15 +1669,25 @@ __global__ __launch_bounds__(256) void k_gather_matched(const uint8_t *__restric
         } else {
             const uint32_t mm = min(min(x.y - x.x, r.y - r.x), best);
             l = 7;
+            uint64_t raw7 = 0;  // bytes 7..14 when the first step loaded all 8
+            bool have7 = false;
             while (l < mm) {
                 const uint32_t t = (mm - l) < 8u ? (mm - l) : 8u;
-                const uint64_t d = load_le(buf, x.x + l, t) ^ load_le(buf, r.x + l, t);
+                const uint64_t xb = load_le(buf, x.x + l, t);
+                if (l == 7u && t == 8u) { raw7 = xb; have7 = true; }
+                const uint64_t d = xb ^ load_le(buf, r.x + l, t);
                 if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
                 l += t;
             }
             l = min(l, mm);
             if (keysL) {
-                const uint64_t kl = chunk_key(buf, x.x, x.y, Ls);
+                // at Ls = 8 the key's bytes 8..14 are the first step's load
+                const uint32_t len = x.y - x.x, rem = len > Ls ? len - Ls : 0u, take = rem < 7u ? rem : 7u;
+                const uint64_t kl = (Ls == 8u && have7)
+                                        ? (rem ? ((__builtin_bswap64((raw7 >> 8) & ((1ull << (8u * take)) - 1ull)) & ~0xffull) |
+                                                  (uint64_t)(rem < 8u ? rem : 8u))
+                                               : 0ull)
+                                        : chunk_key(buf, x.x, x.y, Ls);
                 keysL[i] = kl;
                 accL.add(kl);
             }
