@@ -876,12 +876,17 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
         }
     };
 
-    for (uint32_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-        const uint64_t base = (uint64_t)tile * TILE;
-        const uint64_t my0 = base + (uint64_t)t * BPT;
-        uint32_t w[NW];
-        if (base + TILE + LS_HALO <= n) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(a.buf + my0);
+    // A tile's text (its BPT bytes per thread, the halo words, its parse counts) is loaded
+    // into registers one tile ahead: the next tile's loads are issued after pass 1 and land
+    // while pass 2 runs (LDS bounds these blocks' occupancy, so the registers are free).
+    uint32_t w[NW];
+    uint32_t hx = 0;
+    uint64_t tex = 0;
+    auto load_text = [&](uint32_t tl) {
+        const uint64_t b0 = (uint64_t)tl * TILE;
+        const uint64_t m0 = b0 + (uint64_t)t * BPT;
+        if (b0 + TILE + LS_HALO <= n) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(a.buf + m0);
 #pragma unroll
             for (int j = 0; j < NW / 4; ++j) {
                 const uint4 v = p[j];
@@ -893,7 +898,7 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                 uint32_t x = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const uint64_t pos = my0 + 4 * j + k;
+                    const uint64_t pos = m0 + 4 * j + k;
                     x |= (uint32_t)((pos < n) ? a.buf[pos] : 0x0au) << (8 * k);
                 }
                 w[j] = x;
@@ -902,7 +907,7 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
         // halos: 16 lanes x 4 B on each side ('\n' outside the buffer)
         if (t < 2 * LS_HALO / 4) {
             const bool right = t >= LS_HALO / 4;
-            const int64_t pos0 = right ? (int64_t)(base + TILE) + 4 * (t - LS_HALO / 4) : (int64_t)base - LS_HALO + 4 * t;
+            const int64_t pos0 = right ? (int64_t)(b0 + TILE) + 4 * (t - LS_HALO / 4) : (int64_t)b0 - LS_HALO + 4 * t;
             uint32_t x = 0;
             if (pos0 >= 0 && (uint64_t)pos0 + 4 <= n) {
                 x = *reinterpret_cast<const uint32_t *>(a.buf + pos0);
@@ -913,15 +918,25 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                     x |= (uint32_t)((pos >= 0 && (uint64_t)pos < n) ? a.buf[pos] : 0x0au) << (8 * k);
                 }
             }
-            *reinterpret_cast<uint32_t *>(right ? s_tile + TILE + 4 * (t - LS_HALO / 4) : s_t + 4 * t) = x;
+            hx = x;
+        }
+        if (t == 0) tex = a.tile_excl[tl];
+    };
+    if (blockIdx.x < a.n_tiles) load_text(blockIdx.x);
+
+    for (uint32_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+        const uint64_t base = (uint64_t)tile * TILE;
+        const uint64_t my0 = base + (uint64_t)t * BPT;
+        if (t < 2 * LS_HALO / 4) {
+            const bool right = t >= LS_HALO / 4;
+            *reinterpret_cast<uint32_t *>(right ? s_tile + TILE + 4 * (t - LS_HALO / 4) : s_t + 4 * t) = hx;
         }
 #pragma unroll
         for (int j = 0; j < NW / 4; ++j)
             reinterpret_cast<uint4 *>(s_tile)[(NW / 4) * t + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
         if (t == 0) {
-            const uint64_t te = a.tile_excl[tile];
-            s_base = (uint32_t)(te >> 31);
-            s_ebase = (uint32_t)(te & 0x7fffffffu);
+            s_base = (uint32_t)(tex >> 31);
+            s_ebase = (uint32_t)(tex & 0x7fffffffu);
         }
         uint64_t m = 0;
 #pragma unroll
@@ -1000,6 +1015,7 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
         for (uint32_t c = 0; c < LIT_CLASSES; ++c) ncand += (uint32_t)__popcll(cand[c]);
         uint32_t qtot;
         const uint32_t qex = block_excl_scan<BLK>(ncand, &qtot, s_red);
+        if (tile + gridDim.x < a.n_tiles) load_text(tile + gridDim.x);
         const uint32_t lrec0 = excl;  // tile-local index of this thread's first record start
         for (uint32_t r0 = 0; r0 < qtot; r0 += LS_Q) {
             uint32_t qi = qex;
@@ -1120,14 +1136,14 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
 }
 
 template <int BLK, int BPT, uint32_t CM>
-__global__ __launch_bounds__(BLK) void k_lit_scan(LitArgs a) {
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4))) void k_lit_scan(LitArgs a) {
     lit_scan_body<BLK, BPT, CM>(a);
 }
 
 // The class-scheme trial (the same scan over the first tiles, every output dropped): its own
 // symbol, so kernel statistics and PMC passes of k_lit_scan hold the real scans only.
 template <int BLK, int BPT, uint32_t CM>
-__global__ __launch_bounds__(BLK) void k_lit_trial(LitArgs a) {
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(4))) void k_lit_trial(LitArgs a) {
     lit_scan_body<BLK, BPT, CM>(a);
 }
 
