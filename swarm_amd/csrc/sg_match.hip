@@ -668,6 +668,10 @@ __device__ __forceinline__ void emit_hit(const ACArgs &a, const HitSink &sink, u
     sink.push(((unsigned long long)rec << 32) | sig);
 }
 
+// WIDE (mean record >= 128 B: JSON lines): 64-byte steps, four 16-B loads issued together,
+// so a lane's cache line is requested twice rather than 32 times (4-byte steps); short
+// records (banners) keep 4-byte steps that end at the record.
+template <bool WIDE>
 __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint8_t *s_cls = lds;
@@ -693,19 +697,40 @@ __global__ __launch_bounds__(512) void k_ac_match(ACArgs a) {
         uint32_t st = 0;
         uint32_t seen[4];
         uint32_t nseen = 0;
-        for (uint32_t w = s & ~3u; w < e; w += 4) {
-            const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
+        auto step = [&](uint32_t p, uint32_t byte) {
+            if (p < s || p >= e) return;
+            const uint32_t c = s_cls[byte];
+            st = (st < a.H) ? (uint32_t)s_hot[st * a.C + c] : a.delta[(size_t)st * a.C + c];
+            if ((bits[st >> 5] >> (st & 31)) & 1u) {
+                for (uint32_t t = st; t != NONE; t = a.dict[t])
+                    for (uint32_t q = a.own_off[t]; q < a.own_off[t + 1]; ++q)
+                        emit_hit(a, sink, r, a.own_ids[q], seen, nseen);
+            }
+        };
+        if constexpr (WIDE) {
+            for (uint32_t w = s & ~63u; w < e; w += 64) {
+                uint4 q[4];
 #pragma unroll
-            for (uint32_t b = 0; b < 4; ++b) {
-                const uint32_t p = w + b;
-                if (p < s || p >= e) continue;
-                const uint32_t c = s_cls[(x >> (8 * b)) & 0xffu];
-                st = (st < a.H) ? (uint32_t)s_hot[st * a.C + c] : a.delta[(size_t)st * a.C + c];
-                if ((bits[st >> 5] >> (st & 31)) & 1u) {
-                    for (uint32_t t = st; t != NONE; t = a.dict[t])
-                        for (uint32_t q = a.own_off[t]; q < a.own_off[t + 1]; ++q)
-                            emit_hit(a, sink, r, a.own_ids[q], seen, nseen);
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const uint32_t wk = w + 16u * k;
+                    q[k] = (wk < e && wk + 16u > s) ? *reinterpret_cast<const uint4 *>(a.buf + wk) : make_uint4(0u, 0u, 0u, 0u);
                 }
+#pragma unroll 1
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const uint32_t wk = w + 16u * k;
+                    const uint4 v = q[0];  // (rotated down one register per pass, as in k_dfa_multi)
+                    q[0] = q[1]; q[1] = q[2]; q[2] = q[3];
+                    if (wk >= e || wk + 16u <= s) continue;
+                    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (uint32_t b = 0; b < 16; ++b) step(wk + b, (xs[b >> 2] >> (8 * (b & 3))) & 0xffu);
+                }
+            }
+        } else {
+            for (uint32_t w = s & ~3u; w < e; w += 4) {
+                const uint32_t x = *reinterpret_cast<const uint32_t *>(a.buf + w);
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) step(w + b, (x >> (8 * b)) & 0xffu);
             }
         }
     }
@@ -1340,7 +1365,11 @@ __global__ __launch_bounds__(DFM_BLOCK) void k_dfa_multi(DFAMultiArgs a) {
 #pragma unroll 1
             for (uint32_t k = 0; k < NQ; ++k) {
                 const uint32_t wk = w + 16u * k;
-                const uint4 v = NQ == 1 ? vq[0] : (k == 0 ? vq[0] : (k == 1 ? vq[NQ > 1 ? 1 : 0] : (k == 2 ? vq[NQ > 2 ? 2 : 0] : vq[NQ - 1])));
+                // chunk k is vq[0]: the chunks rotate down one register per pass (a select on k
+                // would index them through scratch)
+                const uint4 v = vq[0];
+#pragma unroll
+                for (int j = 0; j + 1 < NQ; ++j) vq[j] = vq[j + 1];
                 const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
                 const uint32_t lo = s > wk ? min(s - wk, 16u) : 0u, hi = e > wk ? min(e - wk, 16u) : 0u;
                 if (lo >= hi) continue;
@@ -1471,8 +1500,16 @@ __device__ __forceinline__ bool verify_walk(const uint8_t *__restrict__ buf, DT 
 #pragma unroll
     for (int j = 0; j < VF_PRE; ++j)
         if (w0 + 16u * j < e && !hit && st != 0) walk16(w0 + 16u * j, pre[j]);
-    for (uint32_t w = w0 + 16u * VF_PRE; w < e && !hit && st != 0; w += 16)
-        walk16(w, *reinterpret_cast<const uint4 *>(buf + w));
+    // past them, four chunks' loads issued together per step (long records: JSON lines)
+    for (uint32_t w = w0 + 16u * VF_PRE; w < e && !hit && st != 0; w += 64) {
+        uint4 q[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            q[k] = (w + 16u * k < e) ? *reinterpret_cast<const uint4 *>(buf + w + 16u * k) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (w + 16u * k < e && !hit && st != 0) walk16(w + 16u * k, q[k]);
+    }
     if (!hit && st != 0) hit = acc[D[st * C + eol]] != 0;
     return hit;
 }
@@ -1972,7 +2009,8 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
                     ACArgs a{d_buf, L.spans, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                              D.outbits, D.own_off, D.own_ids, D.dict, hits, cnt, (uint32_t)cap, bits_in_lds,
                              nullptr, nullptr};
-                    SG_LAUNCH_B(c, "ac_match", (double)n + 8.0 * R, k_ac_match, grid, 512, lds, a);
+                    if (n >= 128ull * R) SG_LAUNCH_B(c, "ac_match", (double)n + 8.0 * R, k_ac_match<true>, grid, 512, lds, a);
+                    else SG_LAUNCH_B(c, "ac_match", (double)n + 8.0 * R, k_ac_match<false>, grid, 512, lds, a);
                 } else {
                     DFAArgs a{d_buf, L.spans, R, D.cls, D.delta, D.hot, T.n_classes, D.H, T.n_states,
                               T.anchored_eol, D.outbits, reinterpret_cast<const unsigned long long *>(D.omask), D.gpids,
