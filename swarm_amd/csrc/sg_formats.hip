@@ -316,7 +316,7 @@ struct JsCount {
 // framing). Per-thread key spans live in LDS. Requested keys are pre-filtered by length
 // and first byte before a byte compare.
 constexpr int JT_BLOCK = 128;
-__global__ __launch_bounds__(JT_BLOCK) void k_json_scan_t(JsonArgs a) {
+__global__ __launch_bounds__(JT_BLOCK) __attribute__((amdgpu_waves_per_eu(6))) void k_json_scan_t(JsonArgs a) {
     extern __shared__ uint2 s_span[];  // JT_BLOCK * nkeys
     __shared__ uint8_t s_keys[JS_KEYBYTES];
     __shared__ uint32_t s_koff[JS_MAXKEYS + 1];
@@ -530,7 +530,7 @@ struct JsWrite {
     }
 };
 
-__global__ __launch_bounds__(256) void k_json_emit(const uint8_t *__restrict__ buf, const uint4 *__restrict__ desc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_json_emit(const uint8_t *__restrict__ buf, const uint4 *__restrict__ desc,
                                                    const uint64_t *__restrict__ offs, uint32_t nitems, uint32_t nkeys,
                                                    uint8_t *__restrict__ out, uint32_t *__restrict__ row_rec,
                                                    uint32_t *__restrict__ row_key) {
