@@ -250,11 +250,12 @@ def bench_c3(args, ctx=None, emit=True):
     return out
 
 
-def bench_c4(args):
+def bench_c4(args, ctx=None, emit=True):
     """BASELINE.json configs[3] (C4): nmap-service-probes-style port banners x ~10k regex
     signatures (the 1,176 DFA-compilable nuclei template regexes + 8,800 synthetic
     nmap-style `match` families), regex-DFA with literal-factor prefilter. Per GPU: the
-    8-GPU config's share, 12.5M banners; weak scaling with --gpus."""
+    8-GPU config's share, 12.5M banners; weak scaling with --gpus. ctx given: a sub-leg of
+    the default line (1 GPU, the caller's context; returns the leg's dict)."""
     import base64
 
     import numpy as np
@@ -266,20 +267,25 @@ def bench_c4(args):
     import torch.distributed as dist
     from swarm_amd import distributed as D
 
-    world, rank, local = dist_setup(args)
-    if world > 1:
-        local = local % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(local)
-        dist.init_process_group(args.dist_backend)
+    own = ctx is None
+    if own:
+        world, rank, local = dist_setup(args)
+        if world > 1:
+            local = local % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(local)
+            dist.init_process_group(args.dist_backend)
+        else:
+            torch.cuda.set_device(0)
     else:
-        torch.cuda.set_device(0)
+        world, rank, local = 1, 0, 0
     sig = json.load(open(os.path.join(ROOT, "tests", "golden", "signatures.json")))
     pats, n_generic = corpus.c4_signatures([base64.b64decode(r["p"]) for r in sig["regexes"]])
     n_lines = args.c4_lines
     pool = corpus.banner_pool()
     buf = corpus.lines_from_pool(pool, n_lines, seed=3 + rank)  # rank r's contiguous input shard
     d = torch.from_numpy(buf).cuda()
-    ctx = swarm_amd.Context(local, torch.cuda.current_stream().cuda_stream)
+    if own:
+        ctx = swarm_amd.Context(local, torch.cuda.current_stream().cuda_stream)
     tc0 = time.perf_counter()
     m = swarm_amd.Matcher(pats, "regex")  # replicated automata
     compile_s = time.perf_counter() - tc0
@@ -323,8 +329,9 @@ def bench_c4(args):
                                "sample": "%d C4 banners x the %d-signature grep-agreeing subset" % (g_lines, len(sub)),
                                "command": "LC_ALL=C grep -a -E -f subset (x%d line-aligned splits)" % cores,
                                "bit_exact_vs_gpu_same_subset": ctx.to_bytes(rg.lines, rg.lines_bytes) == gm}
-    if rank == 0:
-        print(json.dumps({
+            msub.close()
+            del dg, rg
+    out = {
         "metric": METRIC, "value": round(g_rec * args.steps / el, 1), "unit": "records/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
@@ -344,10 +351,17 @@ def bench_c4(args):
         "kernels": kernel_table(full),
         "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
                         "HIP events only around the dominant kernel",
-        }), flush=True)
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    }
+    out["kernels_top"] = dict(list(out["kernels"].items())[:8])
+    if rank == 0 and emit:
+        print(json.dumps(out), flush=True)
+    m.close()
+    del d, buf, r
+    if own:
+        ctx.close()
+        if world > 1:
+            dist.destroy_process_group()
+    return out
 
 
 def field_templates():
@@ -369,22 +383,26 @@ def field_templates():
     return T
 
 
-def bench_fields(args):
+def bench_fields(args, ctx=None, emit=True):
     """SURVEY.md §8(f) rows 1+3: httpx -json result lines -> field rows (url, title,
     webserver, tech) and nuclei matcher logic (the 1,006 word/regex templates of the
     reference corpus on the record + 31 field templates) per GPU. One step = field
-    extraction + template evaluation over the whole batch."""
+    extraction + template evaluation over the whole batch. ctx given: a sub-leg of the
+    default line (returns the leg's dict)."""
     import numpy as np
     import torch
 
     import swarm_amd
     from swarm_amd import corpus
 
-    torch.cuda.set_device(0)
+    own = ctx is None
+    if own:
+        torch.cuda.set_device(0)
     n_lines = args.fields_lines
     buf = corpus.lines_from_pool(corpus.httpx_json_pool(1 << 14, seed=5), n_lines, seed=6)
     d = torch.from_numpy(buf).cuda()
-    ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
+    if own:
+        ctx = swarm_amd.Context(0, torch.cuda.current_stream().cuda_stream)
     keys = [b"url", b"title", b"webserver", b"tech"]
     T = field_templates()
     tm = swarm_amd.Templates(T, keys)
@@ -411,7 +429,7 @@ def bench_fields(args):
                "host_cpus": os.cpu_count()}
         cpu["gpu_bit_exact_on_sample"] = (tm.match(sample) == want and
                                           swarm_amd.json_fields(sample, keys)[0] == rows[0])
-    print(json.dumps({
+    out = {
         "metric": METRIC, "value": round(R * args.steps / el, 1), "unit": "records/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
@@ -425,8 +443,15 @@ def bench_fields(args):
         "kernels": kernel_table(full),
         "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "
                         "HIP events only around the dominant kernel",
-    }), flush=True)
-    ctx.close()
+    }
+    out["kernels_top"] = dict(list(out["kernels"].items())[:8])
+    if emit:
+        print(json.dumps(out), flush=True)
+    tm.close()
+    del d, buf, r, holder
+    if own:
+        ctx.close()
+    return out
 
 
 def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
@@ -1179,7 +1204,7 @@ def main():
     ap.add_argument("--fields-lines", type=int, default=4_000_000, help="fields leg httpx -json lines")
     ap.add_argument("--gnu-lines", type=int, default=2_000_000, help="lines of the GNU-tool CPU baseline sample")
     ap.add_argument("--no-x1", action="store_true", help="default run: skip the fused X1 and URL legs")
-    ap.add_argument("--no-sub", action="store_true", help="default run: headline only (no c1/c3/c5/x1/urls legs)")
+    ap.add_argument("--no-sub", action="store_true", help="default run: headline only (no c1/c3/c4/c5/fields/x1/urls legs)")
     ap.add_argument("--no-c2-weak", action="store_true", help="N > 1 c5 run: skip the C2 weak-scaling sub-object")
     ap.add_argument("--c5-part-bytes", type=int, default=2 << 30,
                     help="C5 local path: bytes per local part (one library call each; 1.25 x headroom)")
@@ -1208,9 +1233,11 @@ def main():
         bench_c3(args)
         return 0
     if args.workload == "c4":
-        return bench_c4(args)
+        bench_c4(args)
+        return 0
     if args.workload == "fields":
-        return bench_fields(args)
+        bench_fields(args)
+        return 0
     if args.workload == "x1":
         bench_x1(args)
         return 0
@@ -1259,6 +1286,9 @@ def main():
         line["c1"] = sub_leg("c1", lambda: bench_c1(args, ctx))
         line["c3"] = sub_leg("c3", lambda: bench_c3(args, ctx=ctx, emit=False), SUB_KEYS + ("error",))
         line["c5"] = sub_leg("c5", lambda: bench_c5(args, 1, 0, dev, ctx, emit=False), SUB_KEYS + ("error",))
+        line["c4"] = sub_leg("c4", lambda: bench_c4(args, ctx=ctx, emit=False), SUB_KEYS + ("records", "error"))
+        line["fields"] = sub_leg("fields", lambda: bench_fields(args, ctx=ctx, emit=False),
+                                 SUB_KEYS + ("records", "error"))
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

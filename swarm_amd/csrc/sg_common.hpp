@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/swarmgpu.h"
+#include "sg_switches.hpp"
 
 #define SG_PINNED_BYTES 16384
 
@@ -75,8 +76,6 @@ enum Slot : int {
     S_PT_RCNT, S_PT_RPRE, S_PT_SPOUT, S_PT_KOUT,  // piece partition: the parts' record spans/keys out
     S_LS_ERR, S_LS_BOUNDS,  // hybrid radix sort: overflow flag, local-sort tile bounds
     S_LS_LIST, S_LF_OFF, S_LF_KEY, S_LF_KEY2, S_LF_VAL, S_LF_VAL2, S_LF_POS,  // its overflow fix-up
-    S_STAGE,  // dedup: the sorted staging T (32-B slots)
-    S_FD_LB,  // dedup: the fused diff's prior range per emit tile
     S_KEYSL, S_KEYSL2,  // dedup: cur / prior keys at the last call's common prefix (speculative)
     S_SPEC_PARTS,       // X1: the speculative keys' KeyStatD partials
     S_NSLOTS
@@ -170,6 +169,13 @@ void prof_bytes(sg_ctx *c, const char *name, double bytes);
             return SG_E_HIP;                                                          \
         }                                                                             \
         if (st_ >= 0) ::sg::prof_end((ctx), st_, ea_);                                \
+        if (::sg::sw_sync_check()) {                                                  \
+            hipError_t se_ = hipStreamSynchronize((ctx)->stream);                     \
+            if (se_ != hipSuccess) {                                                  \
+                ::sg::set_error("kernel %s: %s", (name), hipGetErrorString(se_));     \
+                return SG_E_HIP;                                                      \
+            }                                                                         \
+        }                                                                             \
     } while (0)
 
 // Same, crediting `bytes` algorithmic bytes to the kernel's roofline accounting.

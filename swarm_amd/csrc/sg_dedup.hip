@@ -71,33 +71,6 @@ static int run_emit(sg_ctx *c, EmitApplyFn kern, const char *name, const char *c
     return SG_OK;
 }
 
-// run_emit with the sorted-staging apply kernel (k_emit_uniq_t: records from T, bs = the
-// common prefix's length).
-static int run_emit_t(sg_ctx *c, FlagItem item, uint32_t n, const uint8_t *src, uint8_t *dst, uint2 *out_spans,
-                      const uint64_t *kin, uint64_t *kout, const uint4 *T, uint32_t bs, uint64_t **total_out,
-                      uint32_t dst_shift) {
-    const uint32_t ntiles = (n + EM_TILE - 1) / EM_TILE;
-    uint64_t *tp;
-    SG_TRY(slot(c, S_EMIT2, 2 * (size_t)ntiles + 4, &tp));
-    uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
-    *total_out = total;
-    if (ntiles == 0) {
-        SG_HIP(hipMemsetAsync(total, 0, 8, c->stream));
-        return SG_OK;
-    }
-    uint2 *cache;
-    SG_TRY(slot(c, S_ECACHE, (size_t)n + 1, &cache));
-    SG_LAUNCH(c, "emit_uniq.count", k_emit_count<FlagItem>, ntiles, EM_BLOCK, 0, item, n, cache, tot);
-    SG_TRY(tile_scan(c, tot, ntiles, pre, total, dst_shift));
-    if (bs)
-        SG_LAUNCH_B(c, "emit_uniq", 0.0, k_emit_uniq_tp, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin, kout,
-                    T, bs);
-    else
-        SG_LAUNCH_B(c, "emit_uniq", 0.0, k_emit_uniq_t, ntiles, EM_BLOCK, 0, cache, n, pre, src, dst, out_spans, kin, kout,
-                    T, bs);
-    return SG_OK;
-}
-
 static inline uint32_t grid_for(uint64_t n, uint32_t block, uint32_t cap = 0x7fffffffu) {
     uint64_t g = (n + block - 1) / block;
     if (g == 0) g = 1;
@@ -387,167 +360,6 @@ __global__ __launch_bounds__(256) void k_adjacent2(const uint8_t *__restrict__ S
     if (live) dup[i] = d ? 1 : 0;
 }
 
-// ------------------------------------------------------------------ sorted staging (T)
-// Short-record inputs (C2 subdomains, host:port, URL lists) gather every record ONCE, in
-// sorted order, into a fixed-stride staging array T: slot i (32 B, two uint4) holds the
-// bytes [L, L + 31) of the i-th record in sort order (L = the common prefix), zero-padded,
-// and in byte 31 the count of bytes from L (255: more than 31, "long"; the rest is read from
-// the input through the span). Everything after the sort then reads T sequentially — the
-// adjacent compare (fused into the gather: a wave's 64 lanes hold 64 consecutive records and
-// take the predecessor's slot from the neighbouring lane), the segment sort and the unique
-// emit — instead of gathering the records from the input once per pass (round 3: three
-// random gathers of every kept record).
-constexpr uint32_t ST_DATA = 31;   // slot bytes of record data
-constexpr uint32_t ST_LONG = 255;  // length code of a record with more than ST_DATA bytes from L
-
-struct RecSlot {
-    uint32_t d[8];  // bytes 0..30: data (zero-padded), byte 31: length code
-};
-
-__device__ __forceinline__ uint32_t slot_code(const RecSlot &s) { return s.d[7] >> 24; }
-
-// Record (span x) of buf -> its slot (bytes from L = base & 0xffff).
-__device__ __forceinline__ RecSlot make_slot(const uint8_t *__restrict__ buf, uint2 x, uint32_t L) {
-    const uint32_t len = x.y - x.x;
-    const uint32_t rl = len > L ? len - L : 0u;
-    const uint32_t tk = rl < ST_DATA ? rl : ST_DATA;
-    uint4 c[4];
-    load_chunks(buf, x.x + L, tk, c);
-    uint32_t r[13];
-    normalize52(c, (x.x + L) & 15u, r);
-    RecSlot s;
-#pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) {
-        const uint32_t b0 = 4u * q;
-        const uint32_t m = b0 + 4u <= tk ? ~0u : (b0 >= tk ? 0u : ((1u << (8u * (tk - b0))) - 1u));
-        s.d[q] = r[q] & m;
-    }
-    s.d[7] = (s.d[7] & 0x00ffffffu) | ((rl <= ST_DATA ? rl : ST_LONG) << 24);
-    return s;
-}
-
-__device__ __forceinline__ RecSlot load_slot(const uint4 *__restrict__ T, uint32_t i) {
-    const uint4 a = T[2 * (size_t)i], b = T[2 * (size_t)i + 1];
-    return RecSlot{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
-}
-
-__device__ __forceinline__ void store_slot(uint4 *__restrict__ T, uint32_t i, const RecSlot &s) {
-    T[2 * (size_t)i] = make_uint4(s.d[0], s.d[1], s.d[2], s.d[3]);
-    T[2 * (size_t)i + 1] = make_uint4(s.d[4], s.d[5], s.d[6], s.d[7]);
-}
-
-__device__ __forceinline__ bool slot_eq(const RecSlot &a, const RecSlot &b) {
-    uint32_t x = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) x |= a.d[q] ^ b.d[q];
-    return x == 0;
-}
-
-// Order of two records by their slots (memcmp of the bytes from L, then length: the zero
-// padding and the length code in the last byte make the slots compare like the records), with
-// the bytes past the slot compared in the input when both are long.
-__device__ __forceinline__ int slot_cmp(const uint8_t *__restrict__ buf, const RecSlot &a, uint2 xa, const RecSlot &b, uint2 xb,
-                                        uint32_t L) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        if (a.d[q] != b.d[q]) {
-            const uint32_t x = a.d[q] ^ b.d[q];
-            const uint32_t sh = (uint32_t)__builtin_ctz(x) & ~7u;  // first differing byte (little-endian dword)
-            return ((a.d[q] >> sh) & 0xffu) < ((b.d[q] >> sh) & 0xffu) ? -1 : 1;
-        }
-    }
-    if (slot_code(a) != ST_LONG) return 0;
-    return rec_cmp_w(buf, xa.x, xa.y, buf, xb.x, xb.y, L + ST_DATA);
-}
-
-// The adjacent pass fused with the gather into T. One wave = 63 consecutive sorted positions
-// (lanes 1..63) plus their predecessor (lane 0), so every lane gathers one record and compares
-// it with lane - 1's. KEYS / DUP and the outputs as k_adjacent2 (without DUP only the groups
-// are marked and T is not written).
-template <bool KEYS>
-__global__ __launch_bounds__(256) void k_stage(const uint8_t *__restrict__ S, const uint2 *__restrict__ SS,
-                                               const uint64_t *__restrict__ K, uint8_t *__restrict__ brk, uint32_t n,
-                                               uint8_t *__restrict__ dup, uint8_t *__restrict__ segbad, AdjLists L,
-                                               uint32_t base, uint4 *__restrict__ T) {
-    const uint32_t lane = lane_id();
-    const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const int64_t ig = (int64_t)w * 63 + (int64_t)lane - 1;  // lane 0: the predecessor
-    const bool live = lane > 0 && ig < (int64_t)n;
-    const uint32_t i = ig < 0 ? 0u : (ig >= (int64_t)n ? n - 1u : (uint32_t)ig);
-    const uint32_t Lp = base & 0xffffu;
-    const uint2 x = SS[i];
-    const uint64_t ki = K[i];
-    const RecSlot sl = make_slot(S, x, Lp);
-    RecSlot sp;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) sp.d[q] = (uint32_t)__shfl_up((int)sl.d[q], 1, 64);
-    const uint64_t kp = (uint64_t)__shfl_up((long long)ki, 1, 64);
-    const uint2 xp = make_uint2((uint32_t)__shfl_up((int)x.x, 1, 64), (uint32_t)__shfl_up((int)x.y, 1, 64));
-    bool head;
-    if constexpr (KEYS) {
-        head = (i == 0) || kp != ki;
-        if (live) brk[i] = head ? 1 : 0;
-        const bool big = live && head && (ki & 0xffu) == bk_full(base) && i + WAVE_GROUP < n && K[i + WAVE_GROUP] == ki;
-        uint32_t last = 0;
-        if (big) {
-            uint32_t lo = i + WAVE_GROUP, step = WAVE_GROUP;  // K[lo] == ki
-            while (lo + step < n && K[lo + step] == ki) { lo += step; step <<= 1; }
-            uint32_t hi = min(n, lo + step);
-            while (hi - lo > 1) {
-                const uint32_t mid = lo + (hi - lo) / 2;
-                if (K[mid] == ki) lo = mid; else hi = mid;
-            }
-            last = lo;
-        }
-        const uint64_t m = __ballot(big);
-        if (m) {
-            const int lead = __ffsll((long long)m) - 1;
-            uint32_t b = 0;
-            if ((int)lane == lead) b = atomicAdd(&L.cnt[2], (uint32_t)__popcll(m));
-            b = (uint32_t)__shfl((int)b, lead, 64);
-            if (big) {
-                const uint32_t q = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                if (q < L.cap_g) { L.gs[q] = i; L.ge[q] = last; }
-            }
-        }
-    } else {
-        head = (i == 0) || brk[i];
-    }
-    if (live) store_slot(T, i, sl);
-    bool d = false;
-    if (live && !head) {
-        d = ((ki & 0xffu) < bk_full(base)) ||
-            (slot_eq(sl, sp) && (slot_code(sl) != ST_LONG || rec_equal_w(S, x.x, x.y, S, xp.x, xp.y, Lp + ST_DATA)));
-        if (!d) {
-            // i differs from i - 1 inside one segment: mark the segment's head (the last group
-            // start at or before i - 1) bad
-            uint32_t h = i - 1;
-            bool found = true;
-            if constexpr (KEYS) {
-                uint32_t lo = i >= WAVE_GROUP ? i - WAVE_GROUP : 0u;
-                if (lo > 0 && K[lo] == ki) {
-                    found = false;  // a big group: refinement rounds first, then this pass again
-                } else {
-                    while (lo < h) {
-                        const uint32_t mid = (lo + h) >> 1;
-                        if (K[mid] == ki) h = mid; else lo = mid + 1;
-                    }
-                }
-            } else {
-                for (;;) {
-                    const uint32_t a = h & ~15u;
-                    const uint32_t mm = swar_nonzero16(*reinterpret_cast<const uint4 *>(brk + a)) & ((2u << (h - a)) - 1u);
-                    if (mm) { h = a + 31u - (uint32_t)__clz(mm); break; }
-                    if (a == 0) { h = 0; break; }
-                    h = a - 1;
-                }
-            }
-            if (found) segbad[h] = 1;
-        }
-    }
-    if (live) dup[i] = d ? 1 : 0;
-}
-
 // Heads of bad segments (segbad, marked by k_adjacent2): A = up to SEG_SMALL members, B = more
 // (<= WAVE_GROUP). A bad head's segment is small iff a break (brk, or the end) lies in
 // (i, i + SEG_SMALL]: two aligned 16-B loads of brk (the slot has 32 B of tail room).
@@ -727,88 +539,6 @@ __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S,
     } else {
         seg_rank_group<64>(S, SS, dup, a[0], k[0], lane, 0u, true, base);
         if (k[1]) seg_rank_group<64>(S, SS, dup, a[1], k[1], lane, 0u, true, base);
-    }
-}
-
-// The segment sorts over T: members ranked by their slots (a long pair compared past the slot
-// in the input); spans, slots and dup flags permuted together.
-template <int G>
-__device__ __forceinline__ void seg_rank_group_t(const uint8_t *__restrict__ S, uint2 *__restrict__ SS, uint4 *__restrict__ T,
-                                                 uint8_t *__restrict__ dup, uint32_t a, uint32_t k, uint32_t gl,
-                                                 uint32_t gbase, bool live, uint32_t base) {
-    const bool act = live && gl < k;
-    const uint32_t Lp = base & 0xffffu;
-    const uint2 x = act ? SS[a + gl] : make_uint2(0u, 0u);
-    RecSlot ms;
-    if (act) ms = load_slot(T, a + gl);
-    else
-#pragma unroll
-        for (int q = 0; q < 8; ++q) ms.d[q] = 0u;
-    uint32_t rank = 0;
-    bool d = false;
-    const uint32_t kk = live ? k : 0u;
-    uint32_t kmax = kk;
-#pragma unroll
-    for (int o = G; o < 64; o <<= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
-    for (uint32_t j = 0; j < kmax; ++j) {
-        const int src = (int)(gbase + (j < kk ? j : 0u));
-        RecSlot os;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) os.d[q] = (uint32_t)__shfl((int)ms.d[q], src, 64);
-        const uint2 y = make_uint2((uint32_t)__shfl((int)x.x, src, 64), (uint32_t)__shfl((int)x.y, src, 64));
-        if (act && j < kk && j != gl) {
-            const int c = slot_cmp(S, ms, x, os, y, Lp);
-            if (c > 0 || (c == 0 && j < gl)) ++rank;
-            if (c == 0 && j < gl) d = true;
-        }
-    }
-    if (act) {
-        SS[a + rank] = x;
-        store_slot(T, a + rank, ms);
-        dup[a + rank] = d ? 1 : 0;
-    }
-}
-
-// (held to 8 waves per SIMD: 65 -> 64 VGPRs, 12 B of spill; X1 seg_small 0.140 -> 0.133 ms)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_seg_small_t(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
-                                                     uint4 *__restrict__ T, const uint8_t *__restrict__ brk,
-                                                     uint8_t *__restrict__ dup, const uint32_t *__restrict__ heads,
-                                                     uint32_t nh, uint32_t n, uint32_t base) {
-    const uint32_t lane = lane_id(), gl = lane & 15u, gbase = lane & ~15u;
-    const uint32_t q = blockIdx.x * 16u + (threadIdx.x >> 4);
-    const bool live = q < nh;
-    const uint32_t a = live ? heads[q] : 0u;
-    const uint32_t pe = a + 1u + gl;
-    const bool eb = !live || pe >= n || gl == 15u || brk[pe];
-    const uint32_t me = (uint32_t)(__ballot(eb) >> gbase) & 0xffffu;
-    const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);
-    seg_rank_group_t<16>(S, SS, T, dup, a, k, gl, gbase, live, base);
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_seg_wave_t(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
-                                                    uint4 *__restrict__ T, const uint8_t *__restrict__ brk,
-                                                    uint8_t *__restrict__ dup, const uint32_t *__restrict__ heads,
-                                                    uint32_t nh, uint32_t n, uint32_t *err, uint32_t base) {
-    const uint32_t q0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2u;
-    const uint32_t lane = lane_id();
-    if (q0 >= nh) return;
-    uint32_t a[2], k[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const bool live = q0 + t < nh;
-        a[t] = live ? heads[q0 + t] : 0u;
-        const uint32_t pe = a[t] + 1u + lane;
-        const uint64_t me = __ballot(!live || pe >= n || brk[pe]);
-        if (!me) { if (lane == 0) atomicOr(err, 1u); return; }
-        k[t] = live ? 1u + (uint32_t)(__ffsll((long long)me) - 1) : 0u;
-    }
-    if (k[0] <= 32u && k[1] <= 32u) {
-        const uint32_t t = lane >> 5;
-        seg_rank_group_t<32>(S, SS, T, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u,
-                             (t ? k[1] : k[0]) > 0, base);
-    } else {
-        seg_rank_group_t<64>(S, SS, T, dup, a[0], k[0], lane, 0u, true, base);
-        if (k[1]) seg_rank_group_t<64>(S, SS, T, dup, a[1], k[1], lane, 0u, true, base);
     }
 }
 
@@ -1013,209 +743,6 @@ __global__ __launch_bounds__(256) void k_diff_tile(RecSet U, RecSet P, const uin
     diff_tile_body(U, P, jb, fresh, base);
 }
 
-
-// ------------------------------------------------------------------ fused unique emit + diff
-// The unique emit already holds every kept record (its span, key and, in cache, its bytes)
-// when it writes it, so the diff against the prior is decided there instead of by a second
-// pass over the unique output (k_diff_tile: U keys, spans and bytes read again, 150 us on
-// C2). Per emit tile (EM_TILE sorted items) the prior's records with keys in
-// [first item's key, last item's key] — found by k_fd_split, one wave per boundary — are
-// staged in LDS (keys + spans); each kept record is looked up among them by key0 and, when
-// its key0 does not hold the whole record, compared bytewise with the equal-key prior records.
-// The tile writes a fresh flag per sorted item and its fresh (count, bytes) total, so the
-// new-record emit needs no count pass of its own.
-constexpr uint32_t FD_PCAP = 1024;  // prior records staged per emit tile
-
-// lb[t] = lower_bound(P.K, K[t * EM_TILE]), ub[t] = upper_bound(P.K, K[last item of tile t]),
-// P's keys narrowed to kw as read (one wave per tile).
-__device__ __forceinline__ uint32_t wave_lower_bound(const uint64_t *__restrict__ PK, uint32_t np, uint64_t key,
-                                                     uint32_t kw) {
-    const uint32_t lane = lane_id();
-    uint32_t lo = 0, hi = np;  // answer in [lo, hi]
-    while (hi > lo) {
-        const uint32_t span = hi - lo;
-        if (span <= 64) {
-            const uint32_t p = lo + lane;
-            const bool ge = (p >= hi) || key_narrow(PK[p], kw) >= key;
-            const uint64_t m = __ballot(ge);
-            lo = m ? lo + (uint32_t)(__ffsll((long long)m) - 1) : hi;
-            break;
-        }
-        const uint32_t p = lo + (uint32_t)(((uint64_t)span * (lane + 1)) / 65);
-        const bool ge = key_narrow(PK[p], kw) >= key;
-        const uint64_t m = __ballot(ge);
-        if (!m) {
-            lo = (uint32_t)__shfl((int)p, 63, 64) + 1;
-        } else {
-            const int f = __ffsll((long long)m) - 1;
-            const uint32_t pf = (uint32_t)__shfl((int)p, f, 64);
-            const uint32_t pp = (uint32_t)__shfl((int)p, f > 0 ? f - 1 : 0, 64);
-            hi = pf;
-            if (f > 0) lo = pp + 1;
-        }
-    }
-    return lo;
-}
-
-__global__ __launch_bounds__(256) void k_fd_split(const uint64_t *__restrict__ K, uint32_t n,
-                                                  const uint64_t *__restrict__ PK, uint32_t np, uint32_t ntiles,
-                                                  uint32_t *__restrict__ lb, uint32_t *__restrict__ ub, uint32_t kw) {
-    const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= ntiles) return;
-    const uint32_t i0 = t * EM_TILE, i1 = min(n, i0 + EM_TILE) - 1u;
-    const uint64_t k0 = K[i0], k1 = K[i1];
-    const uint32_t a = wave_lower_bound(PK, np, k0, kw);
-    const uint32_t b = k1 == ~0ull ? np : wave_lower_bound(PK, np, k1 + 1ull, kw);
-    if (lane_id() == 0) { lb[t] = a; ub[t] = b; }
-}
-
-// Is the unique record (span us of ubuf, key0 ku) in the prior? The prior's records of this
-// tile, [j0, j1), are staged in LDS (s_k narrowed keys, s_sp spans) when `staged`.
-__device__ __forceinline__ bool fd_present(const uint8_t *__restrict__ ubuf, uint2 us, uint64_t ku, RecSet P,
-                                           const uint64_t *s_k, const uint2 *s_sp, uint32_t j0, uint32_t j1,
-                                           bool staged, uint32_t base) {
-    const uint32_t kw = base >> 16;
-    const uint32_t np = j1 - j0;
-    uint32_t lo = 0, hi = np;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const uint64_t v = staged ? s_k[mid] : key_narrow(P.K[j0 + mid], kw);
-        if (v < ku) lo = mid + 1; else hi = mid;
-    }
-    const uint32_t cand = j0 + lo;
-    if (lo >= np) return false;  // every prior record with key ku lies in [j0, j1)
-    const uint64_t kp = staged ? s_k[lo] : key_narrow(P.K[cand], kw);
-    if (kp != ku) return false;
-    if ((ku & 0xffu) < bk_full(base)) return true;
-    const uint2 ps = staged ? s_sp[lo] : P.sp[cand];
-    if (rec_equal_w(ubuf, us.x, us.y, P.buf, ps.x, ps.y, bk_off(base))) return true;
-    // other prior records sharing this key0, sorted by their remaining bytes: binary search
-    // the run [cand + 1, run end) by full compare
-    uint32_t ce;
-    {
-        uint32_t a = lo + 1, b = np;  // upper bound of ku in [lo + 1, np)
-        while (a < b) {
-            const uint32_t mid = (a + b) >> 1;
-            const uint64_t v = staged ? s_k[mid] : key_narrow(P.K[j0 + mid], kw);
-            if (v <= ku) a = mid + 1; else b = mid;
-        }
-        ce = j0 + a;
-    }
-    uint32_t a = cand + 1, b = ce;
-    while (a < b) {
-        const uint32_t mid = (a + b) >> 1;
-        const uint2 x = P.sp[mid];
-        const int cmp = rec_cmp8_2(P.buf, x.x, x.y - x.x, ubuf, us.x, us.y - us.x, bk_off(base));
-        if (cmp == 0) return true;
-        if (cmp < 0) a = mid + 1; else b = mid;
-    }
-    return false;
-}
-
-// The unique emit (emit_apply_body's SPARSE path: kept items packed per wave, copied 64 per
-// round through the LDS window) with the diff of every kept record; ff[i] = item i is a new
-// record; tot_f[tile] = the tile's new (records << 32 | bytes + newlines).
-template <uint32_t WIN>
-__global__ __launch_bounds__(EM_BLOCK) void k_emit_uniq_diff(const uint2 *__restrict__ cache, uint32_t n,
-                                                             const uint64_t *__restrict__ pre,
-                                                             const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
-                                                             const uint64_t *__restrict__ kin, RecSet P,
-                                                             const uint32_t *__restrict__ lb,
-                                                             const uint32_t *__restrict__ ub, uint32_t base_bk,
-                                                             uint8_t *__restrict__ ff, uint64_t *__restrict__ tot_f) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][WIN];
-    __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
-    __shared__ uint64_t s_wt[4], s_ft[4];
-    __shared__ uint32_t s_cst[4][EM_ROUNDS * 64], s_cln[4][EM_ROUNDS * 64], s_co[4][EM_ROUNDS * 64],
-        s_ci[4][EM_ROUNDS * 64];
-    __shared__ uint8_t s_fr[4][EM_ROUNDS * 64];
-    __shared__ uint64_t s_pk[FD_PCAP];
-    __shared__ uint2 s_psp[FD_PCAP];
-    const uint32_t tile = blockIdx.x;
-    const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t wbase = tile * EM_TILE + wid * 256u;
-    const uint32_t kw = base_bk >> 16;
-    // the tile's prior records, staged while the scans below run
-    const uint32_t j0 = lb[tile], j1 = max(ub[tile], j0);
-    const bool staged = j1 - j0 <= FD_PCAP;
-    if (staged)
-        for (uint32_t q = threadIdx.x; q < j1 - j0; q += EM_BLOCK) {
-            s_pk[q] = key_narrow(P.K[j0 + q], kw);
-            s_psp[q] = P.sp[j0 + q];
-        }
-    uint32_t st[EM_ROUNDS], ln[EM_ROUNDS];
-    uint64_t loc[EM_ROUNDS];
-    uint64_t run = 0;
-    uint32_t fmask = 0;
-    uint2 cvr[EM_ROUNDS];
-#pragma unroll
-    for (int r = 0; r < EM_ROUNDS; ++r) {
-        const uint32_t i = wbase + r * 64u + lane;
-        cvr[r] = cache[i < n ? i : n - 1u];
-    }
-#pragma unroll
-    for (int r = 0; r < EM_ROUNDS; ++r) {
-        const uint32_t i = wbase + r * 64u + lane;
-        const uint2 cv = (i < n) ? cvr[r] : make_uint2(0u, EM_DROP);
-        const bool f = cv.y != EM_DROP;
-        st[r] = cv.x;
-        ln[r] = f ? cv.y : 0u;
-        const uint64_t v = f ? (EM_ONE | (uint64_t)(cv.y + 1u)) : 0ull;
-        const uint64_t inc = wave_incl_scan(v);
-        loc[r] = run + inc - v;
-        run += __shfl(inc, 63, 64);
-        fmask |= (f ? 1u : 0u) << r;
-    }
-    if (lane == 0) s_wt[wid] = run;
-    __syncthreads();  // also: the staged prior records
-    uint64_t woff = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < 4; ++w) woff += (w < wid) ? s_wt[w] : 0ull;
-    const uint64_t wpre = pre[tile] + woff;
-#pragma unroll
-    for (int r = 0; r < EM_ROUNDS; ++r) {
-        if (!((fmask >> r) & 1u)) continue;
-        const uint64_t gp = wpre + loc[r];
-        const uint32_t e = (uint32_t)(loc[r] >> 32);
-        s_cst[wid][e] = st[r];
-        s_cln[wid][e] = ln[r];
-        s_co[wid][e] = (uint32_t)gp;
-        s_ci[wid][e] = wbase + r * 64u + lane;
-    }
-    const uint32_t kept = (uint32_t)(run >> 32);
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint64_t facc = 0;
-    for (uint32_t k0 = 0; k0 < kept; k0 += 64u) {
-        const uint32_t q = k0 + lane;
-        const bool f = q < kept;
-        const uint32_t s = f ? s_cst[wid][q] : 0u, l = f ? s_cln[wid][q] : 0u, o = f ? s_co[wid][q] : 0u;
-        const uint32_t i = f ? s_ci[wid][q] : 0u;
-        const uint64_t ku = f ? kin[i] : 0ull;  // issued before the copy's loads
-        const uint32_t last = (kept - k0 >= 64u) ? 63u : kept - k0 - 1u;
-        const uint64_t o0 = (uint32_t)__shfl((int)o, 0, 64);
-        const uint64_t oend = (uint32_t)__shfl((int)(o + l + 1u), (int)last, 64);
-        const uint64_t obase = o0 & ~15ull;
-        wave_copy_round<WIN>(src, nullptr, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
-                             (uint32_t)(o - obase), o0, oend, obase);
-        bool fresh = false;
-        if (f) fresh = !fd_present(src, make_uint2(s, s + l), ku, P, s_pk, s_psp, j0, j1, staged, base_bk);
-        if (f) s_fr[wid][q] = fresh ? 1 : 0;
-        facc += fresh ? (EM_ONE | (uint64_t)(l + 1u)) : 0ull;
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    // per item: new iff kept and not in the prior
-#pragma unroll
-    for (int r = 0; r < EM_ROUNDS; ++r) {
-        const uint32_t i = wbase + r * 64u + lane;
-        if (i < n) ff[i] = ((fmask >> r) & 1u) ? s_fr[wid][(uint32_t)(loc[r] >> 32)] : (uint8_t)0;
-    }
-    facc = wave_sum(facc);
-    if (lane == 0) s_ft[wid] = facc;
-    __syncthreads();
-    if (threadIdx.x == 0) tot_f[tile] = s_ft[0] + s_ft[1] + s_ft[2] + s_ft[3];
-}
 
 // ------------------------------------------------------------------ common prefix (URL-like data)
 // L = the longest prefix every record of cur and prior shares (capped at 255). All order and
@@ -1643,19 +1170,9 @@ struct OutBuf {
     uint32_t shift() const { return (uint32_t)((uintptr_t)p & 15); }
 };
 
-// The diff fused into the unique emit (cur only): the prior's sorted unique view in, the new
-// records out (into of, or a context slot).
-struct FusedDiff {
-    RecSet P;
-    uint64_t prior_bytes = 0;
-    const OutBuf *of = nullptr;
-    uint8_t *fresh = nullptr;
-    uint32_t fresh_bytes = 0, fresh_records = 0;
-};
-
 static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewSlots &vs, bool trust_sorted,
                         UView *uv, const Lines *pre = nullptr, uint32_t base = make_bk(0u, 7u), const OutBuf *dst = nullptr,
-                        const KeyStats *ks = nullptr, FusedDiff *fd = nullptr) {
+                        const KeyStats *ks = nullptr) {
     *uv = UView{};
     Lines L;
     if (pre) L = *pre;
@@ -1750,13 +1267,6 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // adjacent equality inside segments; segments holding two different records -> sort.
     // model: key0 + brk + span per record, both records' bytes where compared, dup out
     uint64_t *stot = nullptr;
-    // The sorted staging T (k_stage): short records (on average <= ~27 bytes past the common
-    // prefix, prefix <= 48 bytes) are gathered once into 32-B slots in sorted order; the adjacent
-    // compare, the segment sorts and the unique emit then read T instead of the input.
-    const uint32_t Lb = base & 0xffffu;
-    const bool staged = sw_stage() && R >= 4096 && Lb <= 48u && n <= (uint64_t)R * (28u + Lb);
-    uint4 *T = nullptr;
-    if (staged) SG_TRY(slot(c, S_STAGE, 2 * (size_t)R, &T));
     // All-segments mode: when the last call on this context kept few of its records (most
     // records repeat, and their groups hold near-duplicates: host:port scans, where a host's
     // ports share key0 — C5), the adjacent pass compares no bytes and every segment of two
@@ -1776,15 +1286,7 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
             SG_TRY(run_select2_nb(c, "seg_heads", SegPred{brk, segbad, R}, R, hs, hb, S_COUNT2, &stot, stot_at));
             return SG_OK;
         }
-        // model: key0 + span + brk + dup per record, the record's bytes gathered, its slot written
-        const uint32_t sgrid = (uint32_t)(((uint64_t)R + 62) / 63 + 3) / 4;
-        if (staged && with_dup && keys)
-            SG_LAUNCH_B(c, "stage", 18.0 * R + (double)n + 32.0 * R, (k_stage<true>), sgrid, 256, 0, Sb, SSp, K, brk, R, dup,
-                        segbad, AL, base, T);
-        else if (staged && with_dup)
-            SG_LAUNCH_B(c, "stage", 18.0 * R + (double)n + 32.0 * R, (k_stage<false>), sgrid, 256, 0, Sb, SSp, K, brk, R,
-                        dup, segbad, AL, base, T);
-        else if (keys && with_dup)
+        if (keys && with_dup)
             SG_LAUNCH_B(c, "adjacent", 19.0 * R + (double)n, (k_adjacent2<true, true>), grid_for(R, 256), 256, 0, Sb, SSp, K,
                         brk, R, dup, segbad, AL, base);
         else if (keys)
@@ -1872,16 +1374,8 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         err = reinterpret_cast<uint32_t *>(etp + 2 * (size_t)ent + 1);
     }
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
-    if (staged) {
-        if (ns) SG_LAUNCH(c, "seg_small", k_seg_small_t, grid_for(ns, 16), 256, 0, Sb, SS, T, brk, dup, hs, ns, R, base);
-        if (nb)
-            SG_LAUNCH(c, "seg_wave", k_seg_wave_t, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, T, brk, dup, hb, nb, R, err,
-                      base);
-    } else {
-        if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
-        if (nb)
-            SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
-    }
+    if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
+    if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
     if (c->profile && c->prof_only.empty() && (ns || nb)) {  // full-profile steps only
         // byte model: per member its span read + written, ~4 chunk keys of record bytes, flag
         unsigned long long *mc;
@@ -1903,75 +1397,13 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     uint64_t *uk;
     if (dst) ub = dst->base();
     else SG_TRY(slot(c, vs.ubuf, (size_t)n + 64, &ub));
-    if (fd) {
-        // the unique emit with the diff fused (k_emit_uniq_diff), then the new-record emit
-        // over the same sorted items (its per-tile totals come from the fused pass)
-        const uint32_t ntiles = (R + EM_TILE - 1) / EM_TILE;
-        uint32_t *lbub;
-        SG_TRY(slot(c, S_FD_LB, 2 * (size_t)ntiles + 4, &lbub));
-        SG_LAUNCH(c, "diff_split", k_fd_split, (ntiles + 3) / 4, 256, 0, K, R, fd->P.K, fd->P.n, ntiles, lbub,
-                  lbub + ntiles, base >> 16);
-        uint64_t *tp;  // tot[ntiles] | pre[ntiles] | total  (err word beside total, as run_emit's)
-        SG_TRY(slot(c, S_EMIT2, 2 * (size_t)ntiles + 4, &tp));
-        uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles;
-        if (nb && reinterpret_cast<uint32_t *>(total + 1) != err) { set_error("emit: status slot moved"); return SG_E_HIP; }
-        uint64_t *fp;  // tot_f | pre_f | total_f
-        SG_TRY(slot(c, S_EMIT3, 2 * (size_t)ntiles + 4, &fp));
-        uint64_t *ftot = fp, *fpre = fp + ntiles, *ftotal = fp + 2 * (size_t)ntiles;
-        uint2 *cache;
-        SG_TRY(slot(c, S_ECACHE, (size_t)R + 1, &cache));
-        uint8_t *ff;
-        SG_TRY(slot(c, S_FRESHF, (size_t)R + 16, &ff));
-        uint8_t *fout;
-        if (fd->of) fout = fd->of->base();
-        else SG_TRY(slot(c, S_OUT_FRESH, (size_t)n + 64, &fout));
-        SG_LAUNCH(c, "emit_uniq.count", k_emit_count<FlagItem>, ntiles, EM_BLOCK, 0, FlagItem{SS, dup, 0}, R, cache, tot);
-        SG_TRY(tile_scan(c, tot, ntiles, pre, total, dst ? dst->shift() : 0u));
-        const RecSet P = fd->P;
-        if (n <= 40ull * R)
-            SG_LAUNCH(c, "emit_uniq", k_emit_uniq_diff<EM_WIN_S>, ntiles, EM_BLOCK, 0, cache, R, pre, Sb, ub, K, P, lbub,
-                      lbub + ntiles, base, ff, ftot);
-        else
-            SG_LAUNCH(c, "emit_uniq", k_emit_uniq_diff<EM_WIN>, ntiles, EM_BLOCK, 0, cache, R, pre, Sb, ub, K, P, lbub,
-                      lbub + ntiles, base, ff, ftot);
-        SG_TRY(tile_scan(c, ftot, ntiles, fpre, ftotal, fd->of ? fd->of->shift() : 0u));
-        SG_LAUNCH(c, "emit_fresh", k_emit_fresh_f, ntiles, EM_BLOCK, 0, cache, R, fpre, Sb, fout, ff);
-        // the unique and new totals and the run-sort error word with one host sync
-        uint8_t *pin = (uint8_t *)c->pinned;
-        SG_HIP(hipMemcpyAsync(pin, total, 16, hipMemcpyDeviceToHost, c->stream));
-        SG_HIP(hipMemcpyAsync(pin + 16, ftotal, 8, hipMemcpyDeviceToHost, c->stream));
-        SG_HIP(hipStreamSynchronize(c->stream));
-        uint64_t tt = 0, tf = 0;
-        uint32_t e = 0;
-        memcpy(&tt, pin, 8);
-        memcpy(&e, pin + 8, 4);
-        memcpy(&tf, pin + 16, 8);
-        if (nb && e) { set_error("run sort: segment bound violated (0x%x)", e); return SG_E_HIP; }
-        const uint32_t t1 = (uint32_t)(tt >> 32), t2 = (uint32_t)tt;
-        // model: cached span + key per record, kept bytes read + written, the prior's keys and
-        // spans of the tile ranges and its compared bytes (~ the prior), a flag per item; the
-        // new-record emit: cached span + flag per item, new bytes read + written
-        if (c->profile) {
-            prof_bytes(c, "emit_uniq", 16.0 * R + 2.0 * t2 + 16.0 * P.n + (double)fd->prior_bytes + R);
-            prof_bytes(c, "emit_fresh", 9.0 * R + 2.0 * (double)(uint32_t)tf);
-        }
-        fd->fresh = fout;
-        fd->fresh_bytes = (uint32_t)tf;
-        fd->fresh_records = (uint32_t)(tf >> 32);
-        *uv = UView{ub, nullptr, nullptr, t1, t2, R};
-        if (vs.ubuf == CUR_VIEW.ubuf) c->last_uniq_frac = R ? (float)t1 / (float)R : 1.0f;
-        return SG_OK;
-    }
     SG_TRY(slot(c, vs.uspans, R, &us));
     SG_TRY(slot(c, vs.ukeys, R, &uk));
     uint64_t *uc;
     // short records: the small-window emit (more blocks per CU for the random gather)
     const EmitApplyFn uk_kern = (n <= 40ull * R) ? k_emit_uniq_s : k_emit_uniq;
-    if (staged)
-        SG_TRY(run_emit_t(c, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, T, Lb, &uc, dst ? dst->shift() : 0u));
-    else
-        SG_TRY(run_emit(c, uk_kern, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk,
-                        &uc, 0.0, dst ? dst->shift() : 0u));
+    SG_TRY(run_emit(c, uk_kern, "emit_uniq", "emit_uniq.count", S_EMIT2, FlagItem{SS, dup, 0}, R, Sb, ub, us, K, uk, &uc,
+                    0.0, dst ? dst->shift() : 0u));
     // the output count and the run-sort error word come back with one host sync
     uint8_t *pin = (uint8_t *)c->pinned;
     if (nb && reinterpret_cast<uint32_t *>(uc + 1) != err) { set_error("emit: status slot moved"); return SG_E_HIP; }
@@ -2169,28 +1601,13 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint32_t bk = make_bk(base, kw);
     if (have_prior) SG_TRY(build_unique(c, d_prior, n_prior, PRIOR_VIEW, prior_sorted, &pv, &Lp, bk));
     UView cu;
-    // the diff fused into cur's unique emit (a prior with records, cur sorted: R > 1)
-    FusedDiff fdd;
-    const bool fuse = have_prior && pv.n > 0 && Lc.n_rec > 1 && sw_fused_diff();
-    if (fuse) {
-        fdd.P = RecSet{pv.buf, pv.spans, pv.keys, pv.n};
-        fdd.prior_bytes = n_prior;
-        fdd.of = of;
-    }
-    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, want_hist ? &ks : nullptr,
-                        fuse ? &fdd : nullptr));
+    SG_TRY(build_unique(c, d_cur, n_cur, CUR_VIEW, false, &cu, &Lc, bk, ou, want_hist ? &ks : nullptr));
     res->in_records = cu.in_records;
     res->uniq = ou ? ou->p : const_cast<uint8_t *>(cu.buf);
     res->uniq_bytes = cu.bytes;
     res->uniq_records = cu.n;
     if (!want_fresh) return SG_OK;
     res->prior_records = pv.in_records;
-    if (fuse && fdd.fresh) {
-        res->fresh = of ? of->p : fdd.fresh;
-        res->fresh_bytes = fdd.fresh_bytes;
-        res->fresh_records = fdd.fresh_records;
-        return SG_OK;
-    }
     if (pv.n == 0 || cu.n == 0) {
         res->fresh = res->uniq;
         res->fresh_bytes = res->uniq_bytes;

@@ -285,30 +285,15 @@ __device__ __forceinline__ void put_medium(const uint8_t *src, uint8_t *base, ui
 // compacted into s_src/s_len/s_dst and copied by 16-lane groups with coalesced word loads.
 // Assembled in the wave's LDS window when the span fits, then written with 16-byte stores.
 // TWO: records come from two sources, src (start bit 31 clear) and src2 (bit 31 set).
-// TS (the sorted staging T, sg_dedup.hip): a record whose bytes from the common prefix bs fit
-// its 32-B slot (slot ti of T) is written as the prefix (pw: the prefix bytes, bs <= 48) + the
-// slot, with no gather from src; longer records take the input path below.
-template <uint32_t WIN = EM_WIN, bool TWO = false, bool TS = false, bool TSP = false>
+template <uint32_t WIN = EM_WIN, bool TWO = false>
 __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src0, const uint8_t *__restrict__ src2,
                                                 uint8_t *__restrict__ out,
                                                 uint8_t *win, uint32_t *s_src, uint32_t *s_len, uint32_t *s_dst,
-                                                bool f_in, uint32_t s_in, uint32_t len, uint32_t d, uint64_t o0,
-                                                uint64_t oend, uint64_t base, const uint4 *__restrict__ T = nullptr,
-                                                uint32_t ti = 0, uint32_t bs = 0, const uint32_t *pw = nullptr) {
+                                                bool f, uint32_t s_in, uint32_t len, uint32_t d, uint64_t o0,
+                                                uint64_t oend, uint64_t base) {
     const uint32_t lane = lane_id();
     const uint64_t span = oend - base;
     const bool in_lds = span <= WIN;
-    bool tsrc = false;
-    uint4 ct[2] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
-    if constexpr (TS) {
-        tsrc = f_in && len - bs <= 31u;
-        if (tsrc) {
-            ct[0] = T[2 * (size_t)ti];
-            ct[1] = T[2 * (size_t)ti + 1];
-            ct[1].w &= 0x00ffffffu;  // the length code
-        }
-    }
-    const bool f = f_in && !tsrc;
     const uint8_t *src = (TWO && (s_in >> 31)) ? src2 : src0;
     const uint32_t s = TWO ? (s_in & 0x7fffffffu) : s_in;
     const uint32_t q0 = s & ~15u, sh = s - q0;
@@ -331,18 +316,6 @@ __device__ __forceinline__ void wave_copy_round(const uint8_t *__restrict__ src0
     if (shortr) {
         if (in_lds) put_short_win(win, d, c, sh, len);
         else put_short(out + base + d, c, sh, len);
-    }
-    if constexpr (TS) {
-        if (tsrc) {
-            uint8_t *bp = in_lds ? win : out + base;
-            if (TSP && bs) {
-                const uint4 cp[4] = {make_uint4(pw[0], pw[1], pw[2], pw[3]), make_uint4(pw[4], pw[5], pw[6], pw[7]),
-                                     make_uint4(pw[8], pw[9], pw[10], pw[11]), make_uint4(0u, 0u, 0u, 0u)};
-                put_win64(bp, d, cp, 0u, bs, false);
-            }
-            const uint4 cs[4] = {ct[0], ct[1], make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u)};
-            put_win64(bp, d + bs, cs, 0u, len - bs, true);
-        }
     }
     if (medr) {
         if (in_lds) put_medium(src, win, d, s, len);
@@ -442,39 +415,18 @@ __global__ __launch_bounds__(EM_BLOCK) void k_emit_count(Item item, uint32_t n, 
 // SPARSE (selections that drop items: unique compaction, new records): the wave's kept
 // items are first packed in LDS in output order, then copied 64 per round, so a round is
 // not spent on a 64-item slice that keeps only a few records.
-// TS (SPARSE only): records sourced from the sorted staging T (wave_copy_round); every record
-// shares its first bs <= 48 bytes (the common prefix), taken from item 0's record (the first
-// in sort order: never a duplicate, so its cache entry holds its span).
-// K2: an item is kept only where keep2[i] != 0 as well (the new-record emit over the sorted
-// items, with the unique emit's cache and the fused diff's flags).
-template <bool SPARSE, uint32_t WIN = EM_WIN, bool TWO = false, bool TS = false, bool TSP = false, bool K2 = false>
+template <bool SPARSE, uint32_t WIN = EM_WIN, bool TWO = false>
 __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache, uint32_t n,
                                                 const uint64_t *__restrict__ pre,
                                                 const uint8_t *__restrict__ src, const uint8_t *__restrict__ src2,
                                                 uint8_t *__restrict__ dst,
                                                 uint2 *__restrict__ out_spans,
-                                                const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
-                                                const uint4 *__restrict__ T = nullptr, uint32_t bs = 0,
-                                                const uint8_t *__restrict__ keep2 = nullptr) {
+                                                const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout) {
     __shared__ __attribute__((aligned(16))) uint8_t s_win[4][WIN];
     __shared__ uint32_t s_src[4][64], s_len[4][64], s_dst[4][64];
     __shared__ uint64_t s_wt[4];
     constexpr int CK = SPARSE ? EM_ROUNDS * 64 : 1;
-    constexpr int CT = TS ? EM_ROUNDS * 64 : 1;
-    __shared__ uint32_t s_cst[4][CK], s_cln[4][CK], s_co[4][CK], s_cti[4][CT];
-    // the common prefix (TS, bs <= 48): its 12 dwords, every lane the same (broadcast loads)
-    uint32_t pw[12] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if constexpr (TSP) {
-        if (bs) {
-            const uint32_t tpos = cache[0].x;
-            uint4 c[4];
-            load_chunks(src, tpos, bs, c);
-            uint32_t r[13];
-            normalize52(c, tpos & 15u, r);
-#pragma unroll
-            for (int q = 0; q < 12; ++q) pw[q] = r[q];
-        }
-    }
+    __shared__ uint32_t s_cst[4][CK], s_cln[4][CK], s_co[4][CK];
     const uint32_t tile = blockIdx.x;
     const uint32_t wid = threadIdx.x >> 6, lane = lane_id();
     const uint32_t wbase = tile * EM_TILE + wid * 256u;
@@ -485,18 +437,16 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
     // the rounds' cache entries loaded together (clamped index, no bounds branch: a branch
     // per round kept each load behind the previous round's wait)
     uint2 cvr[EM_ROUNDS];
-    uint8_t k2v[EM_ROUNDS];
 #pragma unroll
     for (int r = 0; r < EM_ROUNDS; ++r) {
         const uint32_t i = wbase + r * 64u + lane;
         cvr[r] = cache[i < n ? i : n - 1u];
-        k2v[r] = K2 ? keep2[i < n ? i : n - 1u] : (uint8_t)1;
     }
 #pragma unroll
     for (int r = 0; r < EM_ROUNDS; ++r) {
         const uint32_t i = wbase + r * 64u + lane;
         const uint2 cv = (i < n) ? cvr[r] : make_uint2(0u, EM_DROP);
-        const bool f = cv.y != EM_DROP && k2v[r] != 0;
+        const bool f = cv.y != EM_DROP;
         st[r] = cv.x;
         ln[r] = f ? cv.y : 0u;
         const uint64_t v = f ? (EM_ONE | (uint64_t)(cv.y + 1u)) : 0ull;
@@ -524,7 +474,6 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
             s_cst[wid][e] = st[r];
             s_cln[wid][e] = ln[r];
             s_co[wid][e] = o;
-            if constexpr (TS) s_cti[wid][e] = wbase + r * 64u + lane;
         }
         const uint32_t kept = (uint32_t)(run >> 32);
         __builtin_amdgcn_wave_barrier();
@@ -533,13 +482,12 @@ __device__ __forceinline__ void emit_apply_body(const uint2 *__restrict__ cache,
             const uint32_t q = k0 + lane;
             const bool f = q < kept;
             const uint32_t s = f ? s_cst[wid][q] : 0u, l = f ? s_cln[wid][q] : 0u, o = f ? s_co[wid][q] : 0u;
-            const uint32_t ti = (TS && f) ? s_cti[wid][q] : 0u;
             const uint32_t last = (kept - k0 >= 64u) ? 63u : kept - k0 - 1u;
             const uint64_t o0 = (uint32_t)__shfl((int)o, 0, 64);
             const uint64_t oend = (uint32_t)__shfl((int)(o + l + 1u), (int)last, 64);
             const uint64_t base = o0 & ~15ull;
-            wave_copy_round<WIN, TWO, TS, TSP>(src, src2, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
-                                          (uint32_t)(o - base), o0, oend, base, T, ti, bs, pw);
+            wave_copy_round<WIN, TWO>(src, src2, dst, s_win[wid], s_src[wid], s_len[wid], s_dst[wid], f, s, l,
+                                      (uint32_t)(o - base), o0, oend, base);
             __builtin_amdgcn_wave_barrier();
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
@@ -583,24 +531,6 @@ SG_EMIT_APPLY(k_emit_uniq_s, true, EM_WIN_S)
 SG_EMIT_APPLY(k_emit_fresh, true, EM_WIN)
 SG_EMIT_APPLY(k_emit_apply, false, EM_WIN)
 #undef SG_EMIT_APPLY
-// The unique emit from the sorted staging T (sg_dedup.hip): short and long-record windows.
-#define SG_EMIT_APPLY_T(NAME, WIN, TSP)                                                                   \
-    __global__ __launch_bounds__(EM_BLOCK) void NAME(                                                     \
-        const uint2 *__restrict__ cache, uint32_t n, const uint64_t *__restrict__ pre,                    \
-        const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, uint2 *__restrict__ out_spans,        \
-        const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout, const uint4 *__restrict__ T,       \
-        uint32_t bs) {                                                                                    \
-        emit_apply_body<true, WIN, false, true, TSP>(cache, n, pre, src, nullptr, dst, out_spans, kin, kout, T, bs); \
-    }
-__global__ __launch_bounds__(EM_BLOCK) void k_emit_fresh_f(const uint2 *__restrict__ cache, uint32_t n,
-                                                           const uint64_t *__restrict__ pre, const uint8_t *__restrict__ src,
-                                                           uint8_t *__restrict__ dst, const uint8_t *__restrict__ keep2) {
-    emit_apply_body<true, EM_WIN, false, false, false, true>(cache, n, pre, src, nullptr, dst, nullptr, nullptr, nullptr,
-                                                             nullptr, 0, keep2);
-}
-SG_EMIT_APPLY_T(k_emit_uniq_t, EM_WIN_S, false)   // no common prefix
-SG_EMIT_APPLY_T(k_emit_uniq_tp, EM_WIN_S, true)   // records share a prefix (URL lists)
-#undef SG_EMIT_APPLY_T
 #endif
 
 // ------------------------------------------------------------------ common items

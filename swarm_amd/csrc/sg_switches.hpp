@@ -30,13 +30,6 @@ inline int sw_lit_scheme() {
     const char *v = getenv("SG_LIT_SCHEME");
     return v ? (atoi(v) != 0 ? 1 : 0) : -1;
 }
-// SG_STAGE=0: the dedup gathers records from the input in every pass after the sort instead
-// of staging them once in sorted order (sg_dedup.hip k_stage; A/B and the tests' second path).
-inline bool sw_stage() { return env_switch("SG_STAGE", false); }
-// SG_FUSED_DIFF=1: the new-record diff inside the unique emit (k_emit_uniq_diff) instead of
-// its own pass over the unique output (k_diff_tile). Off: measured 534 us for the fused emit
-// against 438 for emit + split + diff + new-record count on C2.
-inline bool sw_fused_diff() { return env_switch("SG_FUSED_DIFF", false); }
 // The dedup's all-segments mode (sg_dedup.hip SEG_ALL_UNIQ): SG_SEG_ALL=0 never, 1 (default)
 // by the context's last unique fraction, 2 always (tests).
 inline int sw_seg_all() {
@@ -48,5 +41,12 @@ inline bool sw_lit_trial_log() { return env_switch("SG_LIT_TRIAL_LOG", false); }
 // SG_TM_SORT=1: nuclei templates evaluated through the sort path instead of the
 // record-wave evaluator (tests/test_gpu_templates.py).
 inline bool sw_tm_sort() { return env_switch("SG_TM_SORT", false); }
+
+// SG_SYNC_CHECK=1 (diagnosis only): every kernel launch is followed by a stream sync, so an
+// asynchronous fault is reported with the name of the kernel that raised it.
+inline bool sw_sync_check() {
+    static const bool on = env_switch("SG_SYNC_CHECK", false);
+    return on;
+}
 
 }  // namespace sg

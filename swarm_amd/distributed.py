@@ -64,36 +64,28 @@ def exchange_counts(counts: Sequence[int], group=None) -> List[int]:
 
 
 # Largest per-peer message of one RCCL all-to-all. The RCCL in this image (2.26.6, torch's
-# wheel) returned wrong bytes for 1-rank all_to_all_single messages of 1800 MB where 512 MB
-# ones were exact (tools/rccl_probe.py), and a C5 rounds step with 1.65 GB
-# rounds faulted: larger exchanges go as several all-to-alls of at most this many bytes per
-# peer.
+# wheel) returns wrong bytes for 1-rank all_to_all_single messages of 1,536 MB where 1,024 MB
+# ones are exact (tools/rccl_probe.py): larger exchanges go as point-to-point
+# pieces of at most this many bytes.
 A2A_CHUNK = 512 << 20
 
 
-def a2a_pieces(in_splits: Sequence[int], out_splits: Sequence[int], chunk: int):
-    """The chunked exchange plan: per piece c, ([(start, end)] send ranges per peer,
-    [(start, end)] receive ranges per peer), bytes [c * chunk, (c + 1) * chunk) of every
-    peer's message (empty ranges once a message is exhausted). Concatenated over pieces, each
-    peer's ranges cover its message once, in order."""
-    def offs(s):
-        o, a = [], 0
-        for x in s:
-            o.append(a)
-            a += x
-        return o
-    io, oo = offs(in_splits), offs(out_splits)
-    big = max(list(in_splits) + list(out_splits) + [0])
-    plan = []
-    for c0 in range(0, big, chunk):
-        sr = [(o + min(c0, s), o + min(c0 + chunk, s)) for o, s in zip(io, in_splits)]
-        rr = [(o + min(c0, s), o + min(c0 + chunk, s)) for o, s in zip(oo, out_splits)]
-        plan.append((sr, rr))
-    return plan
+def a2a_pieces(size: int, chunk: int) -> List[Tuple[int, int]]:
+    """(start, end) pieces of one message of `size` bytes, each at most `chunk` long. Both
+    ends of a message know its size, so sender and receiver cut it the same way."""
+    return [(a, min(a + chunk, size)) for a in range(0, size, chunk)]
+
+
+def _offsets(splits: Sequence[int]) -> List[int]:
+    o, a = [], 0
+    for x in splits:
+        o.append(a)
+        a += x
+    return o
 
 
 class _Works:
-    """wait() of several async collectives (the pieces of one chunked exchange)."""
+    """wait() of several async operations (the pieces of one chunked exchange)."""
 
     def __init__(self, works):
         self.works = works
@@ -105,13 +97,18 @@ class _Works:
 
 
 def all_to_all_bytes(recv: torch.Tensor, send: torch.Tensor, out_splits: Sequence[int], in_splits: Sequence[int],
-                     group=None, async_op: bool = False):
+                     group=None, async_op: bool = False, global_max: int = None):
     """All-to-all of byte buffers with host split sizes (sum(in_splits) == send.numel(),
     sum(out_splits) == recv.numel()). RCCL: straight between the device buffers, optionally
-    async (the returned work's wait() orders the caller's stream after it); one
-    all_to_all_single, or pieces of at most A2A_CHUNK bytes per peer (grouped send/recv
-    all-to-alls of buffer views) when a message is larger. gloo with device buffers: staged
-    through host copies, synchronously (returns None)."""
+    async (the returned work's wait() orders the caller's stream after it). gloo with device
+    buffers: staged through host copies, synchronously (returns None).
+
+    Every rank takes the same path: one all_to_all_single when the largest message of the
+    whole exchange (global_max, the max over ranks of their largest split; agreed here by one
+    max all-reduce when the caller has not) is at most A2A_CHUNK, else every message goes
+    as point-to-point pieces of at most A2A_CHUNK bytes (one batched isend/irecv list; a
+    rank's message to itself is a local copy). So no rank issues a collective its peers do
+    not."""
     out_splits, in_splits = [int(x) for x in out_splits], [int(x) for x in in_splits]
     if host_staged(group) and (send.is_cuda or recv.is_cuda):
         h = torch.empty(recv.numel(), dtype=torch.uint8)
@@ -119,15 +116,31 @@ def all_to_all_bytes(recv: torch.Tensor, send: torch.Tensor, out_splits: Sequenc
                                group=group)
         recv.copy_(h)
         return None
-    if host_staged(group) or max(out_splits + in_splits + [0]) <= A2A_CHUNK:
+    if global_max is None:
+        global_max = all_max_int(max(out_splits + in_splits + [0]), group)
+    if global_max <= A2A_CHUNK:
         return dist.all_to_all_single(recv, send, output_split_sizes=out_splits, input_split_sizes=in_splits,
                                       group=group, async_op=async_op)
-    works = []
-    for sr, rr in a2a_pieces(in_splits, out_splits, A2A_CHUNK):
-        w = dist.all_to_all([recv[a:b] for a, b in rr], [send[a:b] for a, b in sr], group=group, async_op=async_op)
-        if async_op:
-            works.append(w)
-    return _Works(works) if async_op else None
+    me = dist.get_rank(group) if group is not None else dist.get_rank()
+    io, oo = _offsets(in_splits), _offsets(out_splits)
+    ops = []
+    for g in range(len(in_splits)):
+        peer = dist.get_global_rank(group, g) if group is not None else g
+        if g == me:
+            if in_splits[g] != out_splits[g]:
+                raise ValueError("self message: %d bytes sent, %d expected" % (in_splits[g], out_splits[g]))
+            recv[oo[g]:oo[g] + out_splits[g]].copy_(send[io[g]:io[g] + in_splits[g]])
+            continue
+        for a, b in a2a_pieces(in_splits[g], A2A_CHUNK):
+            ops.append(dist.P2POp(dist.isend, send[io[g] + a:io[g] + b], peer, group))
+        for a, b in a2a_pieces(out_splits[g], A2A_CHUNK):
+            ops.append(dist.P2POp(dist.irecv, recv[oo[g] + a:oo[g] + b], peer, group))
+    works = dist.batch_isend_irecv(ops) if ops else []
+    if async_op:
+        return _Works(works)
+    for w in works:
+        w.wait()
+    return None
 
 
 def exchange_records(send: torch.Tensor, part_bytes: Sequence[int], group=None) -> torch.Tensor:
@@ -232,11 +245,12 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
                     force_exchange: bool = False):
     """Route this rank's pieces into world x rounds byte ranges with ONE partition call (the
     parts laid out round-major, sg_dev_partition_bytes_pieces_rounds), exchange every part's
-    size with ONE all-to-all, then queue one all-to-all per round, all at once (async on RCCL's
-    stream). Returns ([(work or None, receive tensor) per round], send buffer): the receive
-    tensor of round p is this rank's local range p (every source's records of it, in source
-    rank order), and work.wait() orders the caller's stream after its arrival. The send buffer
-    must stay referenced until every round has been waited for.
+    size and record count with ONE all-to-all, then queue one all-to-all per round, all at once
+    (async on RCCL's stream). Returns ([(work or None, receive tensor, records the sources
+    routed into it) per round], send buffer): the receive tensor of round p is this rank's
+    local range p (every source's records of it, in source rank order), and work.wait()
+    orders the caller's stream after its arrival. The send buffer must stay referenced until
+    every round has been waited for.
     force_exchange: issue the size exchange and the per-round all-to-alls even at world size 1
     (a 1-rank RCCL group on one GPU runs the device-tensor collective path of the N-rank step;
     without it a single rank skips the collectives)."""
@@ -251,27 +265,37 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
     send = torch.empty(total + len(live) + 16 * (rounds + 1), dtype=torch.uint8, device=dev)
     if live:
         ctx.fence_in()
-        pb, _ = ctx.partition_bytes_pieces_rounds([(p.data_ptr(), p.numel()) for p in live], splitters, rounds,
-                                                  send.data_ptr(), send.numel())
+        pb, pr = ctx.partition_bytes_pieces_rounds([(p.data_ptr(), p.numel()) for p in live], splitters, rounds,
+                                                   send.data_ptr(), send.numel())
         # the partition's copy pass is queued on the ctx stream and the call returns after the
         # size read-back only: drain it before a collective (on another stream) reads send
         ctx.fence_out()
     else:
-        pb = [0] * nparts
+        pb, pr = [0] * nparts, [0] * nparts
     if world == 1 and not (force_exchange and dist.is_initialized()):
         offs = round_offsets(pb, rounds)
-        return [(None, send[offs[p]:offs[p] + pb[p]]) for p in range(rounds)], send
-    # rc[s * rounds + p]: bytes source s sends this rank in round p (peer g's slice of pb is
-    # its rounds parts g * rounds .. + rounds - 1, contiguous)
-    rc = exchange_counts(pb, group)
+        return [(None, send[offs[p]:offs[p] + pb[p]], int(pr[p])) for p in range(rounds)], send
+    # per peer g: the bytes, then the records, of its rounds parts g * rounds .. + rounds - 1
+    # (contiguous in pb / pr); back: rc2[s * 2R + p] bytes and rc2[s * 2R + R + p] records that
+    # source s sends this rank in round p
+    R = rounds
+    cnt = []
+    for g in range(world):
+        cnt += [int(x) for x in pb[g * R:(g + 1) * R]] + [int(x) for x in pr[g * R:(g + 1) * R]]
+    rc2 = exchange_counts(cnt, group)
+    rc = [rc2[s * 2 * R + p] for s in range(world) for p in range(R)]
+    rrec = [sum(rc2[s * 2 * R + R + p] for s in range(world)) for p in range(R)]
     offs = round_offsets(pb, rounds)
+    # the largest message of any round on any rank: every rank picks the same transport
+    gmax = all_max_int(max(list(pb) + list(rc) + [0]), group)
     out = []
     for p in range(rounds):
         ins = [pb[g * rounds + p] for g in range(world)]
         outs = [rc[s * rounds + p] for s in range(world)]
         recv = torch.empty(sum(outs), dtype=torch.uint8, device=dev)
-        w = all_to_all_bytes(recv, send[offs[p]:offs[p] + sum(ins)], outs, ins, group, async_op=True)
-        out.append((w, recv))
+        w = all_to_all_bytes(recv, send[offs[p]:offs[p] + sum(ins)], outs, ins, group, async_op=True,
+                             global_max=gmax)
+        out.append((w, recv, rrec[p]))
     return out, send
 
 
@@ -291,12 +315,19 @@ def dedup_diff_rounds_step(ctx, cur_pieces, prior_parts, splitters, rounds: int,
         raise ValueError("prior_parts has %d entries for %d rounds" % (len(prior_parts), rounds))
     dev = recvd[0][1].device
     st = sharded.new_stats(rounds)
-    st["recv_bytes"] = [int(r.numel()) for _, r in recvd]
+    st["recv_bytes"] = [int(r.numel()) for _, r, _ in recvd]
     out = sharded._Results(sum(st["recv_bytes"]) + 4096, dev, have_prior, align16=align_parts)
-    for p, (w, recv) in enumerate(recvd):
+    for p, (w, recv, want) in enumerate(recvd):
         if w is not None:
             w.wait()
+        before = st["in_records"]
         sharded.dedup_part(ctx, recv if recv.numel() else None, prior_parts[p] if have_prior else None, out, st)
+        # the senders' routed record counts travel with the sizes: a transfer that delivered
+        # other bytes (round 4: this image's RCCL left half of a 1.5 GB message unwritten)
+        # fails loudly here instead of deduping whatever the buffer held
+        if st["in_records"] - before != want:
+            raise RuntimeError("exchange round %d: %d records arrived, the senders routed %d (%d bytes): the "
+                               "transfer is corrupt" % (p, st["in_records"] - before, want, recv.numel()))
     del send, recvd
     u = out.u[:out.uo]
     return u, (out.f[:out.fo] if have_prior else u), st

@@ -153,11 +153,13 @@ def rounds_shard(rank, world):
     return [cur]
 
 
-def rounds_worker(rank, world, rounds, port, out_q):
+def rounds_worker(rank, world, rounds, port, out_q, chunk=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from route_oracle import FakeCtx
     from swarm_amd import distributed as D
+    if chunk:
+        D.A2A_CHUNK = chunk  # every exchange in point-to-point pieces of at most this many bytes
     ctx = FakeCtx()
     t = lambda b: torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8)[: len(b)]  # noqa: E731
     prior_raw = [b"https://h%d.example.com/\n" % i for i in range(rank, 2500, 2 * world)]
@@ -177,16 +179,17 @@ def rounds_worker(rank, world, rounds, port, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rounds", [(2, 3), (3, 2), (2, 1)])
-def test_rounds_step_global_order_gloo(world, rounds):
+@pytest.mark.parametrize("world,rounds,chunk", [(2, 3, None), (3, 2, None), (2, 1, None), (2, 3, 37), (3, 2, 1000)])
+def test_rounds_step_global_order_gloo(world, rounds, chunk):
     """dedup_diff_rounds_step (the C5 multi-GPU step: one partition into world x rounds ranges,
     one size exchange, one all-to-all per round, each part deduped as its round arrives): the
     ranks' outputs concatenated in rank order equal the global oracle output, with unequal
-    piece counts, an empty piece and a rank holding nothing."""
+    piece counts, an empty piece and a rank holding nothing. chunk: messages capped at that
+    many bytes (the point-to-point pieces path, ranks with uneven message sizes)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=rounds_worker, args=(r, world, rounds, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=rounds_worker, args=(r, world, rounds, port, q, chunk)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in range(world))
@@ -217,7 +220,7 @@ def single_rank_worker(port, out_q):
     prior_parts, _ = D.build_prior_rounds(ctx, [t(prior_raw)], split, 3, force_exchange=True)
     cur = rounds_shard(0, 1)
     recvd, send = D.exchange_rounds(ctx, [t(c) for c in cur], split, 3, force_exchange=True)
-    exchanged = [w for w, _ in recvd]
+    exchanged = [w for w, _, _ in recvd]
     u, f, st = D.dedup_diff_rounds_step(ctx, [t(c) for c in cur], prior_parts, split, 3, force_exchange=True)
     out_q.put((bytes(u.numpy().tobytes()), bytes(f.numpy().tobytes()), b"".join(cur), prior_raw, len(exchanged)))
     dist.destroy_process_group()
@@ -237,28 +240,58 @@ def test_rounds_step_force_exchange_single_rank():
 
 
 def test_a2a_pieces_cover_each_message_once():
-    """The chunked all-to-all plan (RCCL messages capped at A2A_CHUNK bytes per peer): over
-    the pieces, each peer's send and receive ranges tile its message in order."""
+    """A message of `size` bytes in pieces of at most `chunk`: in order, covering it once
+    (sender and receiver cut a message the same way, both knowing its size)."""
     from swarm_amd.distributed import a2a_pieces
     rng = np.random.default_rng(5)
-    for _ in range(50):
-        world = int(rng.integers(1, 6))
-        ins = [int(x) for x in rng.integers(0, 1000, size=world)]
-        outs = [int(x) for x in rng.integers(0, 1000, size=world)]
-        chunk = int(rng.integers(1, 400))
-        plan = a2a_pieces(ins, outs, chunk)
-        assert len(plan) == -(-max(ins + outs + [0]) // chunk)
-        for splits, side in ((ins, 0), (outs, 1)):
-            o = 0
-            for g, s in enumerate(splits):
-                pos = o
-                for piece in plan:
-                    a, b = piece[side][g]
-                    assert a == pos and b - a <= chunk
-                    pos = b
-                assert pos == o + s
-                o += s
-    assert a2a_pieces([0, 0], [0, 0], 16) == []
+    for _ in range(200):
+        size, chunk = int(rng.integers(0, 5000)), int(rng.integers(1, 700))
+        pcs = a2a_pieces(size, chunk)
+        assert len(pcs) == -(-size // chunk)
+        pos = 0
+        for a, b in pcs:
+            assert a == pos and 0 < b - a <= chunk
+            pos = b
+        assert pos == size
+    assert a2a_pieces(0, 16) == []
+
+
+def a2a_worker(rank, world, port, chunk, out_q):
+    """all_to_all_bytes with uneven splits: rank 0's messages all fit one piece, the others'
+    do not. Every rank must take the same transport and deliver exact bytes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from swarm_amd import distributed as D
+    D.A2A_CHUNK = chunk
+    rng = np.random.default_rng(100 + rank)
+    ins = [int(rng.integers(0, chunk + 1)) if rank == 0 else int(rng.integers(0, 4 * chunk)) for _ in range(world)]
+    ins[(rank + 1) % world] = 0  # an empty message
+    outs = D.exchange_counts(ins)
+    send = torch.cat([torch.full((n,), 16 * rank + g, dtype=torch.uint8) for g, n in enumerate(ins)])
+    recv = torch.empty(sum(outs), dtype=torch.uint8)
+    w = D.all_to_all_bytes(recv, send, outs, ins, async_op=True)
+    if w is not None:
+        w.wait()
+    exp = torch.cat([torch.full((n,), 16 * s + rank, dtype=torch.uint8) for s, n in enumerate(outs)])
+    out_q.put((rank, bool(torch.equal(recv, exp)), max(ins + outs)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_to_all_bytes_pieces_uneven_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=a2a_worker, args=(r, world, port, 64, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res)
+    assert max(m for _, _, m in res) > 64  # the pieces path ran
 
 
 def test_plan_rounds():
@@ -327,3 +360,43 @@ def test_match_step_gloo(world):
     for _, tot, lines, _ in res:
         assert tot == want
         assert lines == S.matched_lines(data, hits)
+
+
+def corrupt_worker(port, out_q):
+    """A transfer that leaves the upper half of a round's receive buffer unwritten (what this
+    image's RCCL does with a 1.5 GB message, tools/rccl_probe.py detail): the rounds step must
+    raise, not dedup the stale bytes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    from route_oracle import FakeCtx
+    from swarm_amd import distributed as D
+    ctx = FakeCtx()
+    t = lambda b: torch.frombuffer(bytearray(b + b"\0"), dtype=torch.uint8)[: len(b)]  # noqa: E731
+    prior_raw = b"".join(b"https://h%d.example.com/\n" % i for i in range(0, 2500, 3))
+    split = D.agree_splitters(ctx, [t(prior_raw)], 2, samples_per_piece=64)
+    real = D.all_to_all_bytes
+
+    def half(recv, send, outs, ins, group=None, async_op=False, global_max=None):
+        w = real(recv, send, outs, ins, group, async_op, global_max)
+        if w is not None:
+            w.wait()
+        recv[recv.numel() // 2:] = 0
+        return None
+
+    D.all_to_all_bytes = half
+    try:
+        D.dedup_diff_rounds_step(ctx, [t(c) for c in rounds_shard(0, 1)], None, split, 2, force_exchange=True)
+        out_q.put("no error")
+    except RuntimeError as e:
+        out_q.put(str(e))
+    dist.destroy_process_group()
+
+
+def test_rounds_step_detects_corrupt_transfer():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=corrupt_worker, args=(free_port(), q))
+    p.start()
+    msg = q.get(timeout=120)
+    p.join(timeout=60)
+    assert "transfer is corrupt" in msg, msg

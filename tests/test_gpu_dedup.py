@@ -544,24 +544,18 @@ def test_key_stats_rare_digits(sg, shape):
         ctx.close()
 
 
-# ------------------------------------------------------------------ sorted staging (T)
+# ------------------------------------------------------------------ record shapes x segment modes
 @pytest.mark.parametrize("shape", ["mixed_long", "slot_edges", "url_prefix", "nul_cr"])
-@pytest.mark.parametrize("stage,fused,segall", [("1", "1", "1"), ("0", "1", "2"), ("0", "0", "1"), ("1", "0", "2"),
-                                                ("0", "0", "2")])
-def test_staged_dedup_shapes(sg, monkeypatch, shape, stage, fused, segall):
-    """The dedup with the sorted staging (k_stage: each record gathered once into a 32-B slot
-    of its bytes past the common prefix) and without it (SG_STAGE=0), against the oracle:
-    mixed_long: short records beside records too long for a slot (compared and emitted from
-    the input), many sharing their first 7+ bytes (segment sorts on slots, long pairs past the
-    slot); slot_edges: lengths 29..34 past the prefix around the 31-byte slot; url_prefix: a
-    common 'https://' prefix (slots start after it, the emit writes it back); nul_cr: NUL, CR
-    and 0xff bytes inside slots (zero padding must not tie a NUL byte with the record end).
-    fused: the new-record diff inside the unique emit (SG_FUSED_DIFF=1) or as its own pass
-    over the unique output (the default); segall=2: the all-segments mode (no byte compares in
-    the adjacent pass, every segment of 2+ records ranked by the segment sorts)."""
+@pytest.mark.parametrize("segall", ["0", "1", "2"])
+def test_dedup_shapes_seg_modes(sg, monkeypatch, shape, segall):
+    """Record shapes against the oracle in every segment mode: mixed_long: short records
+    beside long ones, many sharing their first 7+ bytes (segment sorts, byte compares past the
+    chunk keys); slot_edges: lengths 29..34 past a shared 28-byte head; url_prefix: a common
+    'https://' prefix (keys taken past it); nul_cr: NUL, CR and 0xff bytes (a NUL byte must not
+    tie with the record end). segall=2: the all-segments mode (no byte compares in the
+    adjacent pass, every segment of 2+ records ranked by the segment sorts); 0: compare mode;
+    1: chosen by the context's last unique fraction."""
     import torch
-    monkeypatch.setenv("SG_STAGE", stage)
-    monkeypatch.setenv("SG_FUSED_DIFF", fused)
     monkeypatch.setenv("SG_SEG_ALL", segall)
     rng = np.random.default_rng({"mixed_long": 21, "slot_edges": 22, "url_prefix": 23, "nul_cr": 24}[shape])
     n = 200_000
@@ -597,14 +591,12 @@ def test_staged_dedup_shapes(sg, monkeypatch, shape, stage, fused, segall):
         ctx.close()
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_fused_diff_prior_shapes(sg, monkeypatch, fused):
-    """The diff inside the unique emit against priors that stress its per-tile prior ranges:
-    a prior far denser than cur (emit tiles whose staged prior range overflows the LDS), runs
-    of prior records sharing key0 with distinct tails (binary search by full compare), a prior
-    sharing only some keys, and a cur whose last records sort above every prior record."""
+def test_diff_prior_shapes(sg):
+    """The diff against priors that stress its per-tile prior ranges: a prior far denser than
+    cur (tiles whose staged prior range overflows the LDS), runs of prior records sharing key0
+    with distinct tails (binary search by full compare), a prior sharing only some keys, and a
+    cur whose last records sort above every prior record."""
     import torch
-    monkeypatch.setenv("SG_FUSED_DIFF", fused)
     rng = np.random.default_rng(31)
     alpha = np.frombuffer(b"abcdefgh", dtype=np.uint8)
     body = alpha[rng.integers(0, 8, size=(120_000, 9))]

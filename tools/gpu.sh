@@ -8,6 +8,7 @@
 #   pmc:<leg>                 FETCH_SIZE and WRITE_SIZE passes (one counter per pass) -> pmc_<leg>_*/
 #   sq:<leg>[@label]          two SQ/TCC counter passes over the leg -> sq_<leg>[@label]_p{1,2}/
 #   py:<script>[,args]        python3 <script> args -> py_<name>.log
+#   bin:<exe>[,args]          a built program (tools/bin) -> bin_<name>.log
 #   VAR=value                 exported for the following steps (e.g. SG_LIT_SCHEME=1)
 # Every GPU step runs under its own timeout and the session stops at the first failure.
 set -o pipefail
@@ -91,6 +92,12 @@ for s in "$@"; do
       step "python3 $scr ${rest//,/ }"
       timeout -k 10 600 python3 -u "$scr" ${rest//,/ } > "$OUT/py_$name.log" 2>&1 || { tail -30 "$OUT/py_$name.log"; exit 1; }
       tail -40 "$OUT/py_$name.log" ;;
+    bin)
+      exe=${arg%%,*}; rest=""; [ "$exe" != "$arg" ] && rest=${arg#*,}
+      name=$(basename "$exe")
+      step "$exe ${rest//,/ }"
+      timeout -k 10 300 "$exe" ${rest//,/ } > "$OUT/bin_$name.log" 2>&1 || { tail -30 "$OUT/bin_$name.log"; exit 1; }
+      tail -20 "$OUT/bin_$name.log" ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
 done
