@@ -216,6 +216,27 @@ int sg_dev_partition_bytes_pieces_rounds(sg_ctx *ctx, const uint8_t *const *d_pi
                                          const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
                                          uint32_t rounds, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
                                          uint64_t *part_records);
+/* Pass 0 of a piece partition on its own: *n_records = the pieces' total record count, so a
+ * caller can size the span buffers of sg_dev_partition_bytes_pieces_rounds_spans; the counts
+ * are kept in ctx and reused by the next partition call on the same pieces. */
+int sg_dev_partition_pieces_count(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                  uint64_t *n_records);
+/* sg_dev_partition_bytes_pieces_rounds that also hands over every record's parse, for the
+ * receivers of the exchange (no second parse of the received parts): d_spans (2 x uint32 per
+ * record: start, end before its '\n', relative to its part's start) and d_keys (first-chunk
+ * sort key), records in the round-major part order of the bytes; capacity rec_cap records. */
+int sg_dev_partition_bytes_pieces_rounds_spans(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens,
+                                               size_t k, const uint8_t *splitters, const uint32_t *split_offs,
+                                               uint32_t n_parts, uint32_t rounds, uint8_t *d_out, size_t out_cap,
+                                               uint64_t *part_bytes, uint64_t *part_records, uint32_t *d_spans,
+                                               uint64_t *d_keys, size_t rec_cap);
+/* Received spans of nseg (<= SG_REBASE_SEGS) sources made relative to the receive buffer
+ * d_buf: records [seg_first[s], seg_first[s + 1]) get + seg_off[s] (host arrays). *bad = how
+ * many of each source's first and last 256 records do not end right before a '\n' of d_buf
+ * afterwards (0 for an intact transfer; a short or stale message is caught at its tail). */
+#define SG_REBASE_SEGS 64
+int sg_dev_rebase_spans(sg_ctx *ctx, const uint8_t *d_buf, size_t n, uint32_t *d_spans, size_t n_rec,
+                        const uint64_t *seg_first, const uint64_t *seg_off, uint32_t nseg, uint64_t *bad);
 /* m evenly spaced records' first SG_SPLIT_BYTES bytes (heads: m x SG_SPLIT_BYTES host bytes,
  * zero-filled) and min(len, SG_SPLIT_BYTES) (lens), for choosing byte splitters; nothing is
  * written when the buffer has no records; *n_rec = the buffer's record count. */

@@ -169,8 +169,18 @@ for _name, (_res, _args) in {
 EXPORTS += ["sg_dev_partition_range", "sg_dev_key_sample", "sg_dev_partition_bytes", "sg_dev_record_sample",
             "sg_dev_partition_bytes_pieces", "sg_dev_partition_bytes_pieces_a16", "sg_dev_dedup_diff_into",
             "sg_dev_partition_bytes_pieces_spans", "sg_dev_dedup_diff_spans_into",
-            "sg_dev_partition_bytes_pieces_rounds"]
+            "sg_dev_partition_bytes_pieces_rounds", "sg_dev_partition_pieces_count",
+            "sg_dev_partition_bytes_pieces_rounds_spans", "sg_dev_rebase_spans"]
 for _name, (_res, _args) in {
+    "sg_dev_partition_pieces_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                                C.POINTER(C.c_uint64)]),
+    "sg_dev_partition_bytes_pieces_rounds_spans": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p),
+                                                             C.POINTER(C.c_size_t), C.c_size_t, C.c_void_p,
+                                                             C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32, C.c_void_p,
+                                                             C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                                             C.c_void_p, C.c_void_p, C.c_size_t]),
+    "sg_dev_rebase_spans": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64)]),
     "sg_dev_partition_bytes_pieces": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t,
                                                 C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p, C.c_size_t,
                                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

@@ -467,6 +467,48 @@ class Context:
                                                        C.c_void_p(d_out) if d_out else None, out_cap, pb, pr))
         return list(pb), list(pr)
 
+    def partition_pieces_count(self, pieces: Sequence[Tuple[int, int]]) -> int:
+        """The pieces' total record count (pass 0 of the piece partition, kept for the next
+        partition call on the same pieces: include/swarmgpu.h sg_dev_partition_pieces_count)."""
+        k = len(pieces)
+        ptrs = (C.c_void_p * max(1, k))(*[C.c_void_p(p) for p, _ in pieces])
+        lens = (C.c_size_t * max(1, k))(*[n for _, n in pieces])
+        nr = C.c_uint64(0)
+        check(lib.sg_dev_partition_pieces_count(self._h, ptrs, lens, k, C.byref(nr)))
+        return int(nr.value)
+
+    def partition_bytes_pieces_rounds_spans(self, pieces: Sequence[Tuple[int, int]], splitters: Sequence[bytes],
+                                            rounds: int, d_out: int, out_cap: int, d_spans: int, d_keys: int,
+                                            rec_cap: int):
+        """partition_bytes_pieces_rounds that also writes every record's span (relative to its
+        part's start) and first-chunk key into the caller's buffers (8 bytes each per record,
+        round-major part order). Returns (bytes per part, records per part)."""
+        blob, offs = _keys_blob(list(splitters))
+        parts = len(splitters) + 1
+        k = len(pieces)
+        ptrs = (C.c_void_p * max(1, k))(*[C.c_void_p(p) for p, _ in pieces])
+        lens = (C.c_size_t * max(1, k))(*[n for _, n in pieces])
+        pb = (C.c_uint64 * parts)()
+        pr = (C.c_uint64 * parts)()
+        check(lib.sg_dev_partition_bytes_pieces_rounds_spans(
+            self._h, ptrs, lens, k, blob.ctypes.data, offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts, rounds,
+            C.c_void_p(d_out) if d_out else None, out_cap, pb, pr, C.c_void_p(d_spans) if d_spans else None,
+            C.c_void_p(d_keys) if d_keys else None, rec_cap))
+        return list(pb), list(pr)
+
+    def rebase_spans(self, d_buf: int, n: int, d_spans: int, n_rec: int, seg_first: Sequence[int],
+                     seg_off: Sequence[int]) -> int:
+        """Received spans made relative to the receive buffer (segment s: records from
+        seg_first[s] on get + seg_off[s]); returns how many records do not end before a '\n'
+        of the buffer afterwards (0 for an intact transfer)."""
+        ns = len(seg_first)
+        sf = (C.c_uint64 * max(1, ns))(*[int(x) for x in seg_first])
+        so = (C.c_uint64 * max(1, ns))(*[int(x) for x in seg_off])
+        bad = C.c_uint64(0)
+        check(lib.sg_dev_rebase_spans(self._h, C.c_void_p(d_buf) if d_buf else None, n,
+                                      C.c_void_p(d_spans) if d_spans else None, n_rec, sf, so, ns, C.byref(bad)))
+        return int(bad.value)
+
     def partition_bytes_pieces_spans(self, pieces: Sequence[Tuple[int, int]], splitters: Sequence[bytes], d_out: int,
                                      out_cap: int):
         """partition_bytes_pieces(align16=True) that also returns the parts' parse: (bytes per

@@ -490,6 +490,62 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     }
 }
 
+// Spans received from several sources (a multi-GPU exchange round: each source's spans are
+// relative to the start of its own bytes) rebased to the receive buffer: records
+// [first[s], first[s + 1]) get + off[s]. The transfer is checked on the first and last
+// SG_REBASE_CHECK records of every source: each must end right before a '\n' of the buffer
+// (the routing wrote every record '\n'-terminated), so a message that arrived short or
+// stale (this image's RCCL left the upper half of a 1.5 GB message unwritten) is reported in
+// *bad instead of deduped — without reading every record's bytes (a per-record check touched
+// the whole buffer: 8.7 ms per 1B records).
+constexpr uint32_t SG_REBASE_CHECK = 256;
+struct RebaseSegs {
+    uint32_t first[SG_REBASE_SEGS + 1];
+    uint32_t off[SG_REBASE_SEGS];
+    uint32_t nseg;
+};
+
+__device__ __forceinline__ bool span_ends_at_nl(uint2 x, const uint8_t *__restrict__ buf, uint32_t n) {
+    return x.x <= x.y && x.y < n && buf[x.y] == 0x0a;
+}
+
+// every record rebased; the sampled ones checked
+__global__ __launch_bounds__(256) void k_rebase_spans(uint2 *__restrict__ sp, uint32_t n_rec, const uint8_t *__restrict__ buf,
+                                                      uint32_t n, const RebaseSegs sg_, unsigned long long *__restrict__ bad) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    bool ok = true;
+    if (i < n_rec) {
+        uint32_t lo = 0, hi = sg_.nseg;  // last segment whose first record <= i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sg_.first[mid] <= i) lo = mid; else hi = mid;
+        }
+        uint2 x = sp[i];
+        const uint32_t o = sg_.off[lo];
+        x.x += o;
+        x.y += o;
+        sp[i] = x;
+        if (i - sg_.first[lo] < SG_REBASE_CHECK || sg_.first[lo + 1] - i <= SG_REBASE_CHECK) ok = span_ends_at_nl(x, buf, n);
+    }
+    const uint64_t m = __ballot(!ok);
+    if (m && lane_id() == 0) atomicAdd(bad, (unsigned long long)__popcll(m));
+}
+
+// spans already relative to the buffer (one source at offset 0): the sampled records only
+__global__ __launch_bounds__(256) void k_check_spans(const uint2 *__restrict__ sp, const uint8_t *__restrict__ buf, uint32_t n,
+                                                     const RebaseSegs sg_, unsigned long long *__restrict__ bad) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t s = t / (2 * SG_REBASE_CHECK), j = t % (2 * SG_REBASE_CHECK);
+    bool ok = true;
+    if (s < sg_.nseg) {
+        const uint32_t a = sg_.first[s], e = sg_.first[s + 1];
+        const uint32_t i = j < SG_REBASE_CHECK ? a + j : e - (2 * SG_REBASE_CHECK - j);
+        if (i >= a && i < e && (j < SG_REBASE_CHECK || e - a > SG_REBASE_CHECK)) ok = span_ends_at_nl(sp[i], buf, n);
+    }
+    const uint64_t m = __ballot(!ok);
+    if (m && lane_id() == 0) atomicAdd(bad, (unsigned long long)__popcll(m));
+}
+
 int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, uint8_t *d_out,
                   size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, const uint64_t *split = nullptr,
                   const ByteSplit *bsplit = nullptr) {
@@ -672,10 +728,62 @@ int sg_dev_partition_bytes(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint
 // range p of rank g, and the parts are laid out round-major: round p's parts (0, p), (1, p),
 // ..., (G - 1, p) back to back (one contiguous all-to-all send buffer per round), each round
 // starting at a 16-byte aligned offset.
+// Pass 0 of the piece partition: every piece's record count (count pass + tile scan per
+// piece into slot S_PT_LTP, one read-back). Kept in c->pt_prep for the next partition call on
+// the same pieces (sg_dev_partition_pieces_count: the caller sizes its span buffers first).
+static int pieces_pass0(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                        std::vector<uint32_t> &lnt, std::vector<size_t> &loff, uint64_t **ltp_out,
+                        std::vector<uint32_t> &Rj) {
+    lnt.assign(k, 0);
+    loff.assign(k, 0);
+    Rj.assign(k, 0);
+    size_t ltot = 0;
+    for (size_t j = 0; j < k; ++j) {
+        if (!lens[j]) continue;
+        lnt[j] = lines_tiles(lens[j]);
+        loff[j] = ltot;
+        ltot += 2 * (size_t)lnt[j] + 4;
+    }
+    uint64_t *ltp = nullptr;
+    if (ltot) SG_TRY(slot(c, S_PT_LTP, ltot, &ltp));
+    *ltp_out = ltp;
+    auto &P = c->pt_prep;
+    if (P.on && P.ptrs.size() == k && std::equal(P.lens.begin(), P.lens.end(), lens) &&
+        std::equal(P.ptrs.begin(), P.ptrs.end(), d_pieces)) {
+        Rj = P.Rj;  // the counts and tile scans of sg_dev_partition_pieces_count
+        P.on = false;
+        return SG_OK;
+    }
+    P.on = false;
+    uint8_t *pin = (uint8_t *)c->pinned;
+    if (8 * k > SG_PINNED_BYTES) { set_error("partition: %zu pieces exceed the read-back staging", k); return SG_E_INVAL; }
+    // (a piece that is not 16-byte aligned is copied to the aligned staging slot before each
+    // of its passes: the slot holds one piece at a time)
+    for (size_t j = 0; j < k; ++j) {
+        if (!lens[j]) continue;
+        const uint8_t *pb = nullptr;
+        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &pb));
+        SG_TRY(lines_count_scan(c, pb, lens[j], ltp + loff[j]));
+        SG_HIP(hipMemcpyAsync(pin + 8 * j, ltp + loff[j] + 2 * (size_t)lnt[j], 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    SG_HIP(hipStreamSynchronize(c->stream));
+    for (size_t j = 0; j < k; ++j) {
+        if (!lens[j]) continue;
+        uint64_t tv;
+        memcpy(&tv, pin + 8 * j, 8);
+        Rj[j] = (uint32_t)(tv >> 31);
+        if (Rj[j] != (uint32_t)(tv & 0x7fffffffu)) { set_error("run_lines: start/end count mismatch"); return SG_E_HIP; }
+    }
+    return SG_OK;
+}
+
+// user_sp / user_k (rec_cap records): the span and key outputs in caller buffers (any
+// rounds), records in the same part order as the bytes (round-major with rounds > 1).
 static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
                             const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out,
                             size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, bool a16,
-                            const uint2 **sp_out = nullptr, const uint64_t **k_out = nullptr, uint32_t rounds = 1) {
+                            const uint2 **sp_out = nullptr, const uint64_t **k_out = nullptr, uint32_t rounds = 1,
+                            uint2 *user_sp = nullptr, uint64_t *user_k = nullptr, size_t rec_cap = 0) {
     if (!c || (k && (!d_pieces || !lens)) || ((!splitters || !split_offs) && n_parts > 1)) {
         set_error("sg_dev_partition_bytes_pieces: bad arguments");
         return SG_E_INVAL;
@@ -685,6 +793,7 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
         set_error("n_parts (%u) must be a multiple of rounds (%u)", n_parts, rounds);
         return SG_E_INVAL;
     }
+    if ((user_sp != nullptr) != (user_k != nullptr)) { set_error("partition: span and key buffers go together"); return SG_E_INVAL; }
     uint64_t total_in = 0;
     for (size_t j = 0; j < k; ++j) {
         if (!d_pieces[j] && lens[j]) { set_error("piece %zu is NULL", j); return SG_E_INVAL; }
@@ -702,37 +811,13 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
     const uint32_t *d_len = reinterpret_cast<const uint32_t *>(d_w + 255 * SPL_WORDS);
     // pass 0: every piece's record count (count pass + tile scan per piece), one read-back
     std::vector<const uint8_t *> pb_in(k, nullptr);
-    std::vector<uint32_t> lnt(k, 0);
-    std::vector<size_t> loff(k, 0);
-    size_t ltot = 0;
-    for (size_t j = 0; j < k; ++j) {
-        if (!lens[j]) continue;
-        lnt[j] = lines_tiles(lens[j]);
-        loff[j] = ltot;
-        ltot += 2 * (size_t)lnt[j] + 4;
-    }
+    std::vector<uint32_t> lnt, Rj;
+    std::vector<size_t> loff;
     uint64_t *ltp = nullptr;
-    if (ltot) SG_TRY(slot(c, S_PT_LTP, ltot, &ltp));
-    uint8_t *pin = (uint8_t *)c->pinned;
-    if (8 * k > SG_PINNED_BYTES) { set_error("partition: %zu pieces exceed the read-back staging", k); return SG_E_INVAL; }
-    // (a piece that is not 16-byte aligned is copied to the aligned staging slot before each
-    // of its three passes: the slot holds one piece at a time)
-    for (size_t j = 0; j < k; ++j) {
-        if (!lens[j]) continue;
-        SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &pb_in[j]));
-        SG_TRY(lines_count_scan(c, pb_in[j], lens[j], ltp + loff[j]));
-        SG_HIP(hipMemcpyAsync(pin + 8 * j, ltp + loff[j] + 2 * (size_t)lnt[j], 8, hipMemcpyDeviceToHost, c->stream));
-    }
-    SG_HIP(hipStreamSynchronize(c->stream));
-    std::vector<uint32_t> Rj(k, 0);
+    SG_TRY(pieces_pass0(c, d_pieces, lens, k, lnt, loff, &ltp, Rj));
     std::vector<uint64_t> roff(k, 0);
     uint64_t all_rec = 0;
     for (size_t j = 0; j < k; ++j) {
-        if (!lens[j]) continue;
-        uint64_t tv;
-        memcpy(&tv, pin + 8 * j, 8);
-        Rj[j] = (uint32_t)(tv >> 31);
-        if (Rj[j] != (uint32_t)(tv & 0x7fffffffu)) { set_error("run_lines: start/end count mismatch"); return SG_E_HIP; }
         roff[j] = all_rec;
         all_rec += Rj[j];
     }
@@ -829,23 +914,40 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
     }
     // span output: part q's records at [rstart[q], rstart[q + 1]) of the parts' records;
     // piece j's part-q records from rb_all[j][q] on
-    const bool want_sp = sp_out != nullptr;
+    const bool want_sp = sp_out != nullptr || user_sp != nullptr;
     uint2 *d_sp = nullptr;
     uint64_t *d_k = nullptr;
     if (want_sp) {
+        // part q's records start at racc[q] of the span output, parts in the order of the
+        // byte layout (round-major with rounds > 1)
         uint64_t rtot = 0;
         std::vector<uint64_t> racc(n_parts);
-        for (uint32_t q = 0; q < n_parts; ++q) { racc[q] = rtot; rtot += prec[q]; }
+        if (rounds > 1) {
+            const uint32_t G = n_parts / rounds;
+            for (uint32_t p = 0; p < rounds; ++p)
+                for (uint32_t g = 0; g < G; ++g) { racc[g * rounds + p] = rtot; rtot += prec[g * rounds + p]; }
+        } else {
+            for (uint32_t q = 0; q < n_parts; ++q) { racc[q] = rtot; rtot += prec[q]; }
+        }
         for (size_t j = 0; j < k; ++j)
             for (uint32_t q = 0; q < n_parts; ++q) {
                 pb_all.push_back(racc[q]);
                 racc[q] += h[512 * j + q];
             }
         for (uint32_t q = 0; q < n_parts; ++q) pb_all.push_back(pbase[q]);
-        SG_TRY(slot(c, S_PT_SPOUT, rtot + 1, &d_sp));
-        SG_TRY(slot(c, S_PT_KOUT, rtot + 1, &d_k));
-        *sp_out = d_sp;
-        *k_out = d_k;
+        if (user_sp) {
+            if (rtot > rec_cap) {
+                set_error("span capacity %zu < %llu records", rec_cap, (unsigned long long)rtot);
+                return SG_E_CAP;
+            }
+            d_sp = user_sp;
+            d_k = user_k;
+        } else {
+            SG_TRY(slot(c, S_PT_SPOUT, rtot + 1, &d_sp));
+            SG_TRY(slot(c, S_PT_KOUT, rtot + 1, &d_k));
+            *sp_out = d_sp;
+            *k_out = d_k;
+        }
     }
     uint64_t *d_pb;
     SG_TRY(slot(c, S_PT_BASE, pb_all.size(), &d_pb));
@@ -901,6 +1003,78 @@ int sg_dev_partition_bytes_pieces_rounds(sg_ctx *c, const uint8_t *const *d_piec
                                          uint64_t *part_records) {
     return partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
                             part_records, false, nullptr, nullptr, rounds);
+}
+
+int sg_dev_partition_pieces_count(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                  uint64_t *n_records) {
+    if (!c || !n_records || (k && (!d_pieces || !lens))) { set_error("sg_dev_partition_pieces_count: bad arguments"); return SG_E_INVAL; }
+    *n_records = 0;
+    for (size_t j = 0; j < k; ++j) {
+        if (!d_pieces[j] && lens[j]) { set_error("piece %zu is NULL", j); return SG_E_INVAL; }
+        if (lens[j] > MAX_BYTES) { set_error("piece %zu exceeds 4 GiB", j); return SG_E_TOO_LARGE; }
+    }
+    SG_HIP(hipSetDevice(c->device));
+    std::vector<uint32_t> lnt, Rj;
+    std::vector<size_t> loff;
+    uint64_t *ltp = nullptr;
+    SG_TRY(pieces_pass0(c, d_pieces, lens, k, lnt, loff, &ltp, Rj));
+    uint64_t tot = 0;
+    for (uint32_t r : Rj) tot += r;
+    *n_records = tot;
+    auto &P = c->pt_prep;
+    P.ptrs.assign(d_pieces, d_pieces + k);
+    P.lens.assign(lens, lens + k);
+    P.Rj = Rj;
+    P.on = true;
+    return SG_OK;
+}
+
+int sg_dev_partition_bytes_pieces_rounds_spans(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
+                                               const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
+                                               uint32_t rounds, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
+                                               uint64_t *part_records, uint32_t *d_spans, uint64_t *d_keys,
+                                               size_t rec_cap) {
+    if (!d_spans || !d_keys) { set_error("sg_dev_partition_bytes_pieces_rounds_spans: bad arguments"); return SG_E_INVAL; }
+    return partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
+                            part_records, false, nullptr, nullptr, rounds, reinterpret_cast<uint2 *>(d_spans), d_keys,
+                            rec_cap);
+}
+
+int sg_dev_rebase_spans(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t *d_spans, size_t n_rec,
+                        const uint64_t *seg_first, const uint64_t *seg_off, uint32_t nseg, uint64_t *bad) {
+    if (!c || !bad || (n_rec && (!d_spans || !d_buf)) || nseg > SG_REBASE_SEGS || (nseg && (!seg_first || !seg_off))) {
+        set_error("sg_dev_rebase_spans: bad arguments");
+        return SG_E_INVAL;
+    }
+    *bad = 0;
+    if (!n_rec) return SG_OK;
+    if (n > MAX_BYTES || n_rec >= (1ull << 32)) { set_error("sg_dev_rebase_spans: input exceeds 4 GiB"); return SG_E_TOO_LARGE; }
+    SG_HIP(hipSetDevice(c->device));
+    RebaseSegs sg_{};
+    const uint32_t ns = nseg ? nseg : 1u;
+    sg_.nseg = ns;
+    bool shift = false;
+    for (uint32_t s = 0; s < ns; ++s) {
+        const uint64_t f = nseg ? seg_first[s] : 0, o = nseg ? seg_off[s] : 0;
+        if (o > n || f > n_rec || (s && f < sg_.first[s - 1])) { set_error("sg_dev_rebase_spans: bad segments"); return SG_E_INVAL; }
+        sg_.first[s] = (uint32_t)f;
+        sg_.off[s] = (uint32_t)o;
+        shift |= o != 0;
+    }
+    sg_.first[ns] = (uint32_t)n_rec;
+    unsigned long long *d_bad;
+    SG_TRY(slot(c, S_M_CNT, 4, &d_bad));
+    SG_HIP(hipMemsetAsync(d_bad, 0, 8, c->stream));
+    if (shift)
+        SG_LAUNCH_B(c, "rebase_spans", 16.0 * (double)n_rec, k_rebase_spans, (uint32_t)((n_rec + 255) / 256), 256, 0,
+                    reinterpret_cast<uint2 *>(d_spans), (uint32_t)n_rec, d_buf, (uint32_t)n, sg_, d_bad);
+    else
+        SG_LAUNCH(c, "check_spans", k_check_spans, (ns * 2 * SG_REBASE_CHECK + 255) / 256, 256, 0,
+                  reinterpret_cast<const uint2 *>(d_spans), d_buf, (uint32_t)n, sg_, d_bad);
+    unsigned long long b = 0;
+    SG_TRY(ctx_readback(c, &b, d_bad, 8));
+    *bad = b;
+    return SG_OK;
 }
 
 int sg_dev_dedup_diff_spans_into(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, const uint32_t *d_spans,

@@ -112,6 +112,14 @@ struct sg_ctx {
         uint32_t lpos = 0, nloc = 0, ntiles = 0;
         uint32_t *bounds = nullptr;
     } ls_last;
+    // the piece partition's pass 0 (record counts per piece) kept from sg_dev_partition_pieces_count
+    // for the next partition call on the same pieces (its tile scans stay in slot S_PT_LTP)
+    struct PtPrep {
+        bool on = false;
+        std::vector<const uint8_t *> ptrs;
+        std::vector<size_t> lens;
+        std::vector<uint32_t> Rj;
+    } pt_prep;
     // pinned staging for host-to-device uploads on the context stream (ctx_upload): grown on
     // demand; up_ev marks the last upload's copy so the buffer is not rewritten under it
     void *up_pin = nullptr;

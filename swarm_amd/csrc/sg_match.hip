@@ -757,6 +757,7 @@ struct LitArgs {
     uint2 *spans_out;                    // non-null: also write the parse's record spans (fused A3)
     uint8_t *rec_flag;                   // non-null: mark matched records here instead of listing hits
     uint32_t rank_lds;                   // the bitmap words' ranks staged in LDS too (else read from L2)
+    unsigned long long *diag;            // calibration (SG_LIT_TRIAL_LOG): queued, fingerprint-confirmed, verified
 };
 
 constexpr uint32_t LS_HB = 256;    // per-block LDS hit buffer (entries)
@@ -1040,6 +1041,7 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
         for (uint32_t c = 0; c < LIT_CLASSES; ++c) ncand += (uint32_t)__popcll(cand[c]);
         uint32_t qtot;
         const uint32_t qex = block_excl_scan<BLK>(ncand, &qtot, s_red);
+        if (a.diag && t == 0) atomicAdd(&a.diag[0], (unsigned long long)qtot);
         if (tile + gridDim.x < a.n_tiles) load_text(tile + gridDim.x);
         const uint32_t lrec0 = excl;  // tile-local index of this thread's first record start
         for (uint32_t r0 = 0; r0 < qtot; r0 += LS_Q) {
@@ -1132,9 +1134,13 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                     const uint32_t rec = s_base + (ent & 0x3fffu) - 1;
                     const uint64_t p = base + q;
                     if (br[u].x == fpv[u]) {
-                        if (lit_verify(a, s_tile, base, TILE, p, br[u].z >> 24, br[u].z & 0xffffffu, br[u].w & 0x7fffffffu,
-                                       c, r0w[u], r1w[u]))
-                            lit_emit(a, push, rec, br[u].y);
+                        const bool ok = lit_verify(a, s_tile, base, TILE, p, br[u].z >> 24, br[u].z & 0xffffffu,
+                                                   br[u].w & 0x7fffffffu, c, r0w[u], r1w[u]);
+                        if (ok) lit_emit(a, push, rec, br[u].y);
+                        if (a.diag) {
+                            atomicAdd(&a.diag[1], 1ull);
+                            if (ok) atomicAdd(&a.diag[2], 1ull);
+                        }
                     }
                     if (br[u].w >> 31) {
                         // rare: more patterns share this bucket
@@ -1841,6 +1847,13 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         };
         const uint32_t dyn_r = lit_lds_bytes(Lt, true), dyn_n = lit_lds_bytes(Lt, false);
         a.rank_lds = blocks_per_cu(dyn_r) == blocks_per_cu(dyn_n) ? 1u : 0u;
+        a.diag = nullptr;
+        unsigned long long *diag = nullptr;
+        if (sw_lit_trial_log() && !trial_tiles) {
+            SG_TRY(slot(c, S_M_TMP2, 4, &diag));
+            SG_HIP(hipMemsetAsync(diag, 0, 32, c->stream));
+            a.diag = diag;
+        }
         const uint32_t dyn = a.rank_lds ? dyn_r : dyn_n;
         const uint32_t bpc = blocks_per_cu(dyn);
         const uint32_t grid = std::min<uint32_t>(a.n_tiles, 256u * bpc);
@@ -1881,6 +1894,13 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         if (trial_tiles) { SG_LIT_GEOMS(k_lit_trial) } else { SG_LIT_GEOMS(k_lit_scan) }
 #undef SG_LIT_GEOMS
 #undef SG_LIT_KERNELS
+        if (diag) {
+            unsigned long long dv[4] = {0, 0, 0, 0};
+            SG_TRY(ctx_readback(c, dv, diag, 32));
+            fprintf(stderr, "sg %s: %u records, %llu bitmap candidates, %llu fingerprint-confirmed, %llu verified "
+                            "(first bucket entries; tmpl 0x%x, %s scheme)\n",
+                    name, R, dv[0], dv[1], dv[2], Lt.tmpl, Lt.joint ? "joint" : "two");
+        }
         return SG_OK;
     };
     // The class scheme of a filter (two-class or joint, see build_lit): decided once per
@@ -1952,6 +1972,37 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         SG_TRY(slot(c, S_R_VAL2, (size_t)n_cand + 1, &w2));
         SG_TRY(radix_sort(c, reinterpret_cast<uint64_t *>(cand), w1, alt, w2, n_cand, 0, pbits, true, &KC, &WV, "rs_cand"));
         vcand = reinterpret_cast<const unsigned long long *>(KC);
+        if (sw_lit_trial_log()) {
+            // calibration: the verify's shape (candidates per record and per automaton, blocks
+            // that can stage their automaton in LDS)
+            std::vector<unsigned long long> hc(n_cand);
+            SG_HIP(hipMemcpyAsync(hc.data(), vcand, 8ull * n_cand, hipMemcpyDeviceToHost, c->stream));
+            SG_HIP(hipStreamSynchronize(c->stream));
+            std::vector<uint32_t> per_rec(R, 0);
+            for (auto x : hc) ++per_rec[(uint32_t)(x >> 32)];
+            uint32_t recs_with = 0, maxc = 0;
+            for (uint32_t v : per_rec) { recs_with += v ? 1u : 0u; maxc = std::max(maxc, v); }
+            uint32_t blocks = 0, single = 0, stageable = 0, autos = 0, big_autos = 0;
+            for (uint32_t k = 0; k < h->n_singles; ++k) {
+                const uint32_t nst = (k + 1u < h->n_singles ? h->s_acc_off[k + 1u] : (uint32_t)h->s_acc.size()) - h->s_acc_off[k];
+                ++autos;
+                if (nst * h->s_C[k] > 12288u || nst > 4096u) ++big_autos;
+            }
+            for (uint32_t i0 = 0; i0 < n_cand; i0 += 256) {
+                const uint32_t il = std::min(i0 + 256u, n_cand) - 1u;
+                const uint32_t k0 = h->single_of_pid[(uint32_t)hc[i0]], kl = h->single_of_pid[(uint32_t)hc[il]];
+                ++blocks;
+                if (k0 == kl) {
+                    ++single;
+                    const uint32_t nst = (k0 + 1u < h->n_singles ? h->s_acc_off[k0 + 1u] : (uint32_t)h->s_acc.size()) -
+                                         h->s_acc_off[k0];
+                    if (nst * h->s_C[k0] <= 12288u && nst <= 4096u) ++stageable;
+                }
+            }
+            fprintf(stderr, "sg verify: %u candidates over %u records (%u with any, max %u per record); %u verify "
+                            "automata (%u too big for LDS); %u blocks, %u on one automaton, %u staged\n",
+                    n_cand, R, recs_with, maxc, autos, big_autos, blocks, single, stageable);
+        }
     }
     if (mf) {
         SG_TRY(slot(c, S_M_FLAG, (size_t)R + 16, &mf->flags));

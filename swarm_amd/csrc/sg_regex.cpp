@@ -811,12 +811,21 @@ struct Sum {
     std::vector<std::string> exact;
     bool fac_ok = false;
     std::vector<std::string> fac;
-    // every factor set of a concatenation's parts (score >= 3), so the plan can prefer
+    // every factor set of a concatenation's parts (score >= FAC_MIN), so the plan can prefer
     // a set that few other signatures share over the merely longest one
     std::vector<std::vector<std::string>> alts;
 };
 constexpr size_t FAC_MAXALTS = 24;
 constexpr size_t FAC_MAXSET = 64, FAC_MAXLEN = 48;
+// Shortest factor string a filtered pattern may have. Round 5 measured 4 on C4 (the 25
+// three-byte factors of the C4 set: ':99', 'are', 'asp', ... go, with their 27 patterns, to
+// the factor-less DFA groups, tools/factor_stats.cpp): the prefilter's third length class
+// disappears (re_prefilter 3.54 -> 3.19 ms) but the DFA groups grow from 4 to 7 and
+// dfa_match doubles (1.02 -> 2.17 ms): C4 6.88 -> 7.51 ms, fields 54.1 -> 55.9 ms.
+#ifndef SG_FAC_MIN
+#define SG_FAC_MIN 3
+#endif
+constexpr int FAC_MIN = SG_FAC_MIN;
 
 static int fac_score(const std::vector<std::string> &f) {
     if (f.empty()) return 0;
@@ -868,7 +877,7 @@ static Sum summarize(const Node *n) {
             bool all_exact = true;
             auto consider = [&](const std::vector<std::string> &f) {
                 if (!f.empty() && fac_score(f) > 0 && (best.empty() || better(f, best))) best = f;
-                if (fac_score(f) >= 3 && r.alts.size() < FAC_MAXALTS) r.alts.push_back(f);
+                if (fac_score(f) >= FAC_MIN && r.alts.size() < FAC_MAXALTS) r.alts.push_back(f);
             };
             for (auto &k : n->kids) {
                 Sum cs = summarize(k.get());
@@ -974,7 +983,7 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         std::vector<std::string> f = eff[p.id];
         uint64_t best_cost = ~0ull;
         for (auto &c : cands[p.id]) {
-            if (fac_score(c) < 3) continue;
+            if (fac_score(c) < FAC_MIN) continue;
             uint32_t worst = 0;
             for (auto &x : c) worst = std::max(worst, share[x]);
             const uint64_t cost = ((uint64_t)worst << 32) | (uint32_t)(0x7fffffff - fac_score(c));
@@ -984,7 +993,7 @@ int regex_build_plan(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         // a factor holding '\n' can never occur inside a record: drop it
         f.erase(std::remove_if(f.begin(), f.end(), [](const std::string &s) { return s.find('\n') != std::string::npos; }),
                 f.end());
-        bool filtered = fac_score(f) >= 3 || (had && f.empty());
+        bool filtered = fac_score(f) >= FAC_MIN || (had && f.empty());
         if (filtered) {
             RegexDFA d;
             bool fits = false;

@@ -96,6 +96,27 @@ class _Works:
         return True
 
 
+_SIDE = {}
+
+
+def _side_stream(device) -> "torch.cuda.Stream":
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+class _EventWork:
+    """wait() of a copy queued on a side stream: the caller's stream waits for its event."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
+
+
 def all_to_all_bytes(recv: torch.Tensor, send: torch.Tensor, out_splits: Sequence[int], in_splits: Sequence[int],
                      group=None, async_op: bool = False, global_max: int = None):
     """All-to-all of byte buffers with host split sizes (sum(in_splits) == send.numel(),
@@ -124,18 +145,35 @@ def all_to_all_bytes(recv: torch.Tensor, send: torch.Tensor, out_splits: Sequenc
     me = dist.get_rank(group) if group is not None else dist.get_rank()
     io, oo = _offsets(in_splits), _offsets(out_splits)
     ops = []
+    self_work = None
     for g in range(len(in_splits)):
         peer = dist.get_global_rank(group, g) if group is not None else g
         if g == me:
             if in_splits[g] != out_splits[g]:
                 raise ValueError("self message: %d bytes sent, %d expected" % (in_splits[g], out_splits[g]))
-            recv[oo[g]:oo[g] + out_splits[g]].copy_(send[io[g]:io[g] + in_splits[g]])
+            dst, src = recv[oo[g]:oo[g] + out_splits[g]], send[io[g]:io[g] + in_splits[g]]
+            if async_op and recv.is_cuda and out_splits[g]:
+                # on a side stream, as RCCL's own copies run: it overlaps the caller's work on
+                # the earlier rounds instead of queueing ahead of it
+                side = _side_stream(recv.device)
+                side.wait_stream(torch.cuda.current_stream(recv.device))
+                with torch.cuda.stream(side):
+                    dst.copy_(src)
+                recv.record_stream(side)
+                send.record_stream(side)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                self_work = _EventWork(ev)
+            else:
+                dst.copy_(src)
             continue
         for a, b in a2a_pieces(in_splits[g], A2A_CHUNK):
             ops.append(dist.P2POp(dist.isend, send[io[g] + a:io[g] + b], peer, group))
         for a, b in a2a_pieces(out_splits[g], A2A_CHUNK):
             ops.append(dist.P2POp(dist.irecv, recv[oo[g] + a:oo[g] + b], peer, group))
     works = dist.batch_isend_irecv(ops) if ops else []
+    if self_work is not None:
+        works = list(works) + [self_work]
     if async_op:
         return _Works(works)
     for w in works:
@@ -242,7 +280,7 @@ def plan_rounds(bytes_per_rank: int, world: int, part_bytes: int = 2 << 30, min_
 
 
 def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int, group=None,
-                    force_exchange: bool = False):
+                    force_exchange: bool = False, spans: bool = True):
     """Route this rank's pieces into world x rounds byte ranges with ONE partition call (the
     parts laid out round-major, sg_dev_partition_bytes_pieces_rounds), exchange every part's
     size and record count with ONE all-to-all, then queue one all-to-all per round, all at once
@@ -251,6 +289,10 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
     local range p (every source's records of it, in source rank order), and work.wait()
     orders the caller's stream after its arrival. The send buffer must stay referenced until
     every round has been waited for.
+    spans: every record's parse travels with its bytes (its span, relative to its source's
+    bytes, and its first-chunk key: 16 B per record, written by the routing pass itself), so
+    the receiver dedups the round without parsing it again; the 4th element of a round is
+    then (spans, keys, [first record, byte offset] per source) for rebase_spans, else None.
     force_exchange: issue the size exchange and the per-round all-to-alls even at world size 1
     (a 1-rank RCCL group on one GPU runs the device-tensor collective path of the N-rank step;
     without it a single rank skips the collectives)."""
@@ -263,18 +305,42 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
         raise ValueError("%d splitters for %d ranks x %d rounds" % (len(splitters), world, rounds))
     total = sum(int(p.numel()) for p in live)
     send = torch.empty(total + len(live) + 16 * (rounds + 1), dtype=torch.uint8, device=dev)
+    ssp = skey = None
     if live:
         ctx.fence_in()
-        pb, pr = ctx.partition_bytes_pieces_rounds([(p.data_ptr(), p.numel()) for p in live], splitters, rounds,
-                                                   send.data_ptr(), send.numel())
+        plist = [(p.data_ptr(), p.numel()) for p in live]
+        if spans:
+            nrec = ctx.partition_pieces_count(plist)
+            ssp = torch.empty(2 * max(nrec, 1), dtype=torch.int32, device=dev)
+            skey = torch.empty(max(nrec, 1), dtype=torch.int64, device=dev)
+            pb, pr = ctx.partition_bytes_pieces_rounds_spans(plist, splitters, rounds, send.data_ptr(), send.numel(),
+                                                             ssp.data_ptr(), skey.data_ptr(), nrec)
+        else:
+            pb, pr = ctx.partition_bytes_pieces_rounds(plist, splitters, rounds, send.data_ptr(), send.numel())
         # the partition's copy pass is queued on the ctx stream and the call returns after the
         # size read-back only: drain it before a collective (on another stream) reads send
         ctx.fence_out()
     else:
         pb, pr = [0] * nparts, [0] * nparts
+        if spans:
+            ssp = torch.empty(2, dtype=torch.int32, device=dev)
+            skey = torch.empty(1, dtype=torch.int64, device=dev)
+    R = rounds
+    # records of round p start at rround[p] in the span outputs (round-major, like the bytes)
+    rround, acc = [], 0
+    for p in range(R):
+        rround.append(acc)
+        acc += sum(int(pr[g * R + p]) for g in range(world))
     if world == 1 and not (force_exchange and dist.is_initialized()):
         offs = round_offsets(pb, rounds)
-        return [(None, send[offs[p]:offs[p] + pb[p]], int(pr[p])) for p in range(rounds)], send
+        out = []
+        for p in range(rounds):
+            par = None
+            if spans:
+                r0, nr = rround[p], int(pr[p])
+                par = (ssp[2 * r0:2 * (r0 + nr)], skey[r0:r0 + nr], [[0, 0]])
+            out.append((None, send[offs[p]:offs[p] + pb[p]], int(pr[p]), par))
+        return out, (send, ssp, skey)
     # per peer g: the bytes, then the records, of its rounds parts g * rounds .. + rounds - 1
     # (contiguous in pb / pr); back: rc2[s * 2R + p] bytes and rc2[s * 2R + R + p] records that
     # source s sends this rank in round p
@@ -284,10 +350,12 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
         cnt += [int(x) for x in pb[g * R:(g + 1) * R]] + [int(x) for x in pr[g * R:(g + 1) * R]]
     rc2 = exchange_counts(cnt, group)
     rc = [rc2[s * 2 * R + p] for s in range(world) for p in range(R)]
-    rrec = [sum(rc2[s * 2 * R + R + p] for s in range(world)) for p in range(R)]
+    rcr = [rc2[s * 2 * R + R + p] for s in range(world) for p in range(R)]
+    rrec = [sum(rcr[s * R + p] for s in range(world)) for p in range(R)]
     offs = round_offsets(pb, rounds)
-    # the largest message of any round on any rank: every rank picks the same transport
-    gmax = all_max_int(max(list(pb) + list(rc) + [0]), group)
+    # the largest message of any round on any rank (bytes, and 8 B per record for the spans
+    # and keys): every rank picks the same transport
+    gmax = all_max_int(max(list(pb) + list(rc) + [8 * int(x) for x in list(pr) + rcr] + [0]), group)
     out = []
     for p in range(rounds):
         ins = [pb[g * rounds + p] for g in range(world)]
@@ -295,8 +363,26 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
         recv = torch.empty(sum(outs), dtype=torch.uint8, device=dev)
         w = all_to_all_bytes(recv, send[offs[p]:offs[p] + sum(ins)], outs, ins, group, async_op=True,
                              global_max=gmax)
-        out.append((w, recv, rrec[p]))
-    return out, send
+        par = None
+        if spans:
+            ins_r = [int(pr[g * rounds + p]) for g in range(world)]
+            outs_r = [rcr[s * rounds + p] for s in range(world)]
+            r0, nin, nout = rround[p], sum(ins_r), sum(outs_r)
+            rsp = torch.empty(2 * max(nout, 1), dtype=torch.int32, device=dev)
+            rk = torch.empty(max(nout, 1), dtype=torch.int64, device=dev)
+            ws = [w]
+            for src, dst in ((ssp[2 * r0:2 * (r0 + nin)], rsp[:2 * nout]), (skey[r0:r0 + nin], rk[:nout])):
+                ws.append(all_to_all_bytes(dst.view(torch.uint8), src.view(torch.uint8), [8 * x for x in outs_r],
+                                           [8 * x for x in ins_r], group, async_op=True, global_max=gmax))
+            w = _Works([x for x in ws if x is not None])
+            segs, fr, fo = [], 0, 0
+            for s_ in range(world):
+                segs.append([fr, fo])
+                fr += outs_r[s_]
+                fo += outs[s_]
+            par = (rsp[:2 * nout], rk[:nout], segs)
+        out.append((w, recv, rrec[p], par))
+    return out, (send, ssp, skey)
 
 
 def dedup_diff_rounds_step(ctx, cur_pieces, prior_parts, splitters, rounds: int, group=None, align_parts=False,
@@ -315,13 +401,27 @@ def dedup_diff_rounds_step(ctx, cur_pieces, prior_parts, splitters, rounds: int,
         raise ValueError("prior_parts has %d entries for %d rounds" % (len(prior_parts), rounds))
     dev = recvd[0][1].device
     st = sharded.new_stats(rounds)
-    st["recv_bytes"] = [int(r.numel()) for _, r, _ in recvd]
+    st["recv_bytes"] = [int(r.numel()) for _, r, _, _ in recvd]
     out = sharded._Results(sum(st["recv_bytes"]) + 4096, dev, have_prior, align16=align_parts)
-    for p, (w, recv, want) in enumerate(recvd):
+    for p, (w, recv, want, par) in enumerate(recvd):
         if w is not None:
             w.wait()
         before = st["in_records"]
-        sharded.dedup_part(ctx, recv if recv.numel() else None, prior_parts[p] if have_prior else None, out, st)
+        parse = None
+        if par is not None and want:
+            rsp, rk, segs = par
+            # the spans arrive relative to each source's bytes: rebased to this buffer, and
+            # every record checked to end before a '\n' (the routing '\n'-terminated them)
+            if w is not None or len(segs) > 1 or segs[0][1]:
+                ctx.fence_in()
+                bad = ctx.rebase_spans(recv.data_ptr(), recv.numel(), rsp.data_ptr(), want, [x[0] for x in segs],
+                                       [x[1] for x in segs])
+                if bad:
+                    raise RuntimeError("exchange round %d: %d of %d records do not end at a newline of the %d "
+                                       "received bytes: the transfer is corrupt" % (p, bad, want, recv.numel()))
+            parse = (rsp.data_ptr(), rk.data_ptr(), want)
+        sharded.dedup_part(ctx, recv if recv.numel() else None, prior_parts[p] if have_prior else None, out, st,
+                           parse=parse)
         # the senders' routed record counts travel with the sizes: a transfer that delivered
         # other bytes (round 4: this image's RCCL left half of a 1.5 GB message unwritten)
         # fails loudly here instead of deduping whatever the buffer held

@@ -92,3 +92,77 @@ class FakeCtx:
         assert len(blob) <= cap
         ctypes.memmove(out_ptr, blob, len(blob))
         return [len(p) for p in parts], [len(S.parse_records(p)) for p in parts]
+
+
+def key0(rec: bytes) -> int:
+    """include/swarmgpu.h's first-chunk sort key restated: bytes [0, 7) big-endian in bits
+    63..8 (zero past the end), tag = min(len, 8) in bits 7..0."""
+    head = rec[:7] + b"\0" * (7 - min(len(rec), 7))
+    return (int.from_bytes(head, "big") << 8) | min(len(rec), 8)
+
+
+def _i64(v: int) -> int:
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def _fake_pieces_count(self, pieces):
+    return sum(len(S.parse_records(ctypes.string_at(p, n) if n else b"")) for p, n in pieces)
+
+
+def _fake_rounds_spans(self, pieces, splitters, rounds, out_ptr, cap, sp_ptr, k_ptr, rec_cap):
+    """sg_dev_partition_bytes_pieces_rounds_spans restated: the round-major byte layout of
+    partition_bytes_pieces_rounds, plus every record's span (relative to its part's start) and
+    key0, records in the same round-major part order."""
+    pb, pr = self.partition_bytes_pieces_rounds(pieces, splitters, rounds, out_ptr, cap)
+    nparts = len(pb)
+    G = nparts // rounds
+    # the parts' bytes as written (round-major), read back
+    off, r = 0, 0
+    sp = (ctypes.c_uint32 * (2 * max(rec_cap, 1))).from_address(sp_ptr)
+    kk = (ctypes.c_int64 * max(rec_cap, 1)).from_address(k_ptr)
+    for p in range(rounds):
+        off = (off + 15) & ~15
+        for g in range(G):
+            q = g * rounds + p
+            b = ctypes.string_at(out_ptr + off, pb[q]) if pb[q] else b""
+            for a, e in S.record_spans(b):
+                assert r < rec_cap
+                sp[2 * r], sp[2 * r + 1] = a, e
+                kk[r] = _i64(key0(b[a:e]))
+                r += 1
+            off += pb[q]
+    return pb, pr
+
+
+def _fake_rebase(self, buf_ptr, n, sp_ptr, n_rec, seg_first, seg_off):
+    sp = (ctypes.c_uint32 * (2 * max(n_rec, 1))).from_address(sp_ptr)
+    buf = ctypes.string_at(buf_ptr, n) if n else b""
+    bad = 0
+    for i in range(n_rec):
+        s = max(j for j in range(len(seg_first)) if seg_first[j] <= i) if seg_first else 0
+        o = seg_off[s] if seg_off else 0
+        sp[2 * i] += o
+        sp[2 * i + 1] += o
+        a, e = sp[2 * i], sp[2 * i + 1]
+        bad += 0 if (a <= e < n and buf[e] == 0x0A) else 1
+    return bad
+
+
+def _fake_spans_into(self, cur_ptr, n, sp_ptr, k_ptr, n_rec, prior_ptr, pn, u_ptr, ucap, f_ptr, fcap):
+    """sg_dev_dedup_diff_spans_into restated: the handed-over parse must be the buffer's own
+    (spans and keys checked against the oracle's parse), then dedup_diff_into."""
+    cur = ctypes.string_at(cur_ptr, n) if n else b""
+    sp = (ctypes.c_uint32 * (2 * max(n_rec, 1))).from_address(sp_ptr)
+    kk = (ctypes.c_int64 * max(n_rec, 1)).from_address(k_ptr)
+    want = S.record_spans(cur)
+    got = [(sp[2 * i], sp[2 * i + 1]) for i in range(n_rec)]
+    assert got == want, "handed-over spans differ from the parse"
+    assert all(kk[i] == _i64(key0(cur[a:e])) for i, (a, e) in enumerate(got)), "handed-over keys differ"
+    self.log.append("spans_into")
+    return self.dedup_diff_into(cur_ptr, n, prior_ptr, pn, u_ptr, ucap, f_ptr, fcap)
+
+
+FakeCtx.partition_pieces_count = _fake_pieces_count
+FakeCtx.partition_bytes_pieces_rounds_spans = _fake_rounds_spans
+FakeCtx.rebase_spans = _fake_rebase
+FakeCtx.dedup_diff_spans_into = _fake_spans_into

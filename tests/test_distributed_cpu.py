@@ -173,6 +173,8 @@ def rounds_worker(rank, world, rounds, port, out_q, chunk=None):
     # every partition's copy is fenced before the collective that reads its output (ADVICE r3:
     # a ctx off torch's stream must not hand a half-written send buffer to the all-to-all)
     assert all(ctx.log[i + 1] == "fence_out" for i, x in enumerate(ctx.log) if x == "partition"), ctx.log
+    # the received rounds are deduped with the parse the routing handed over (no second parse)
+    assert "spans_into" in ctx.log, ctx.log
     out_q.put((rank, bytes(u.numpy().tobytes()), bytes(f.numpy().tobytes()), b"".join(cur), prior_raw,
                bytes(stored.numpy().tobytes()), st["parts"]))
     dist.barrier()
@@ -220,7 +222,7 @@ def single_rank_worker(port, out_q):
     prior_parts, _ = D.build_prior_rounds(ctx, [t(prior_raw)], split, 3, force_exchange=True)
     cur = rounds_shard(0, 1)
     recvd, send = D.exchange_rounds(ctx, [t(c) for c in cur], split, 3, force_exchange=True)
-    exchanged = [w for w, _, _ in recvd]
+    exchanged = [w for w, _, _, _ in recvd]
     u, f, st = D.dedup_diff_rounds_step(ctx, [t(c) for c in cur], prior_parts, split, 3, force_exchange=True)
     out_q.put((bytes(u.numpy().tobytes()), bytes(f.numpy().tobytes()), b"".join(cur), prior_raw, len(exchanged)))
     dist.destroy_process_group()

@@ -79,8 +79,8 @@ def rccl_worker(port, q):
         split = D.agree_splitters(ctx, prior_raw, rounds)
         prior_parts, _ = D.build_prior_rounds(ctx, prior_raw, split, rounds, force_exchange=True)
         recvd, _send = D.exchange_rounds(ctx, cur, split, rounds, force_exchange=True)
-        out["round_works"] = sum(1 for wk, _, _ in recvd if wk is not None)
-        for wk, _, _ in recvd:
+        out["round_works"] = sum(1 for wk, _, _, _ in recvd if wk is not None)
+        for wk, _, _, _ in recvd:
             if wk is not None:
                 wk.wait()
         del recvd, _send
@@ -111,7 +111,7 @@ def test_one_rank_rccl_collectives_and_rounds_step():
     assert p.exitcode == 0
     assert out["backend"] == "nccl" and out["world"] == 1 and out["host_staged"] is False
     assert out["work_is_async"] and out["a2a_equal"]
-    assert out["chunked_pieces"] == 0 and out["chunked_equal"]
+    assert out["chunked_pieces"] == 1 and out["chunked_equal"]  # the self message: one side-stream copy
     assert out["counts"] == [5, 6, 7]
     assert out["max_int"] == 42 and out["max_float"] == 1.5
     assert out["round_works"] == 3  # one async all-to-all per round, on RCCL

@@ -391,6 +391,68 @@ def test_partition_pieces_rounds_layout(ctx, world, rounds):
     del host
 
 
+@pytest.mark.parametrize("world,rounds", [(2, 3), (3, 1), (1, 4)])
+def test_partition_pieces_rounds_spans(ctx, world, rounds):
+    """sg_dev_partition_bytes_pieces_rounds_spans (after sg_dev_partition_pieces_count): the
+    round-major bytes of the plain call, plus every record's span (relative to its part) and
+    key0 in the same round-major order, equal to the host restatement; then a round received
+    from the parts of several sources (concatenated) is rebased to its own buffer with every
+    record checked to end at a '\n', and a damaged copy of it is reported."""
+    import torch
+    from swarm_amd.api import round_offsets
+    from route_oracle import FakeCtx
+    recs = shared_prefix_records(20_000, 41 + world)
+    data = b"\n".join(recs) + b"\n"
+    cuts = [0, len(data) // 3, len(data) // 3, len(data)]  # an empty piece in the middle
+    cuts = [c if c in (0, len(data)) else data.index(b"\n", c) + 1 for c in cuts]
+    d = dev(b"#" + data)
+    pieces = [d[1 + a:1 + b] for a, b in zip(cuts, cuts[1:])]
+    plist = [(p.data_ptr(), p.numel()) for p in pieces]
+    sp = sorted(random.Random(42).sample(recs, world * rounds - 1))
+    cap = len(data) + len(pieces) + 16 * (rounds + 1)
+    nrec = ctx.partition_pieces_count(plist)
+    assert nrec == len(recs)
+    out = torch.full((cap + 64,), 0x55, dtype=torch.uint8, device=d.device)
+    dsp = torch.zeros(2 * nrec, dtype=torch.int32, device=d.device)
+    dk = torch.zeros(nrec, dtype=torch.int64, device=d.device)
+    pb, pr = ctx.partition_bytes_pieces_rounds_spans(plist, sp, rounds, out.data_ptr(), cap, dsp.data_ptr(),
+                                                     dk.data_ptr(), nrec)
+    hp = [np.frombuffer(bytearray(data[a:b] or b"\0"), dtype=np.uint8) for a, b in zip(cuts, cuts[1:])]
+    wb = np.full(cap + 64, 0x55, dtype=np.uint8)
+    wsp = np.zeros(2 * nrec, dtype=np.uint32)
+    wk = np.zeros(nrec, dtype=np.int64)
+    wpb, wpr = FakeCtx().partition_bytes_pieces_rounds_spans([(h.ctypes.data, b - a) for h, (a, b) in
+                                                              zip(hp, zip(cuts, cuts[1:]))], sp, rounds, wb.ctypes.data,
+                                                             cap, wsp.ctypes.data, wk.ctypes.data, nrec)
+    assert (pb, pr) == (wpb, wpr)
+    assert out.cpu().numpy().tobytes() == wb.tobytes()
+    assert np.array_equal(dsp.cpu().numpy().view(np.uint32), wsp)
+    assert np.array_equal(dk.cpu().numpy(), wk)
+    # a receiver's round p: the sources' parts (g, p) concatenated, spans relative to each
+    offs = round_offsets(pb, rounds)
+    G = world
+    for p in range(rounds):
+        o, r0 = offs[p], sum(pr[g * rounds + q] for q in range(p) for g in range(G))
+        n, nr = sum(pb[g * rounds + p] for g in range(G)), sum(pr[g * rounds + p] for g in range(G))
+        if not nr:
+            continue
+        recv = out[o:o + n].clone()
+        rsp = dsp[2 * r0:2 * (r0 + nr)].clone()
+        seg_first, seg_off, fr, fo = [], [], 0, 0
+        for g in range(G):
+            seg_first.append(fr)
+            seg_off.append(fo)
+            fr += pr[g * rounds + p]
+            fo += pb[g * rounds + p]
+        assert ctx.rebase_spans(recv.data_ptr(), n, rsp.data_ptr(), nr, seg_first, seg_off) == 0
+        part = recv.cpu().numpy().tobytes()
+        assert [tuple(x) for x in rsp.cpu().numpy().view(np.uint32).reshape(-1, 2).tolist()] == S.record_spans(part)
+        bad = out[o:o + n].clone()
+        bad[n // 2:] = 0xAB  # the upper half never delivered
+        rsp2 = dsp[2 * r0:2 * (r0 + nr)].clone()
+        assert ctx.rebase_spans(bad.data_ptr(), n, rsp2.data_ptr(), nr, seg_first, seg_off) > 0
+
+
 def test_stored_prior_aligned_parts(ctx):
     """dedup_diff_large(align_parts=True): every part's unique output starts 16-byte aligned
     ('\\n' padding: the buffer's records are still the sort -u records) and those parts,
