@@ -392,6 +392,7 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     __shared__ uint32_t s_red[NW];
     __shared__ uint2 s_sp[PT_TILE];
     __shared__ uint32_t s_off[PT_TILE];
+    __shared__ uint8_t s_pq[PT_TILE];  // part of each sorted position
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
     for (int x = tid; x < NW * 256; x += PT_BLOCK) (&s_wh[0][0])[x] = 0;
     __syncthreads();
@@ -430,7 +431,11 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
 #pragma unroll
     for (int i = 0; i < PT_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane;
-        if (pos < R) s_sp[s_dstart[d[i]] + s_wh[wid][d[i]] + r[i]] = spans[pos];
+        if (pos < R) {
+            const uint32_t q = s_dstart[d[i]] + s_wh[wid][d[i]] + r[i];
+            s_sp[q] = spans[pos];
+            s_pq[q] = (uint8_t)d[i];
+        }
     }
     __syncthreads();
     // bytes in part order: thread tid scans sorted positions tid*PT_ITEMS .. + PT_ITEMS - 1
@@ -460,17 +465,9 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         }
     }
     __syncthreads();
-    // copy: sorted position q by lane q (consecutive lanes, consecutive bytes of one part)
-    // the part of sorted position q: the last part whose run starts at or before q (parts
-    // with empty runs share a start; s_dstart is non-decreasing, so that is the non-empty one)
-    auto part_of = [&](uint32_t q) {
-        uint32_t lo = 0, hi = 256;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_dstart[mid] <= q) lo = mid; else hi = mid;
-        }
-        return lo;
-    };
+    // copy: sorted position q by lane q (consecutive lanes, consecutive bytes of one part);
+    // the part of sorted position q recorded when it was ranked (round 5: a binary search over
+    // the 256 part starts, 8 dependent LDS reads per record)
     auto finish = [&](uint32_t q, uint32_t lo, uint2 x, uint64_t dst, uint64_t k0) {
         if (so.sp) {  // also the record's span inside its part and its key, at its index in the parts
             const uint64_t g = s_g0[lo] + q;
@@ -480,7 +477,7 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         }
     };
     for (uint32_t q = tid; q < n_t; q += PT_BLOCK) {
-        const uint32_t lo = part_of(q);
+        const uint32_t lo = s_pq[q];
         const uint2 x = s_sp[q];
         const uint64_t dst = s_dst[lo] + s_off[q];
         uint64_t k0 = 0;
