@@ -391,7 +391,10 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
             const uint32_t hi = (c == 4) ? word_at(i, o + 4, 4) : (c == LIT_J ? (uint32_t)T->pat[T->pat_off[i] + o + 4] : 0u);
             const uint32_t h = lit_h(lo, hi, c, T->bits[c]);
             constexpr uint32_t w_share = 64u;  // cost of one more pattern sharing the gram
-            const uint64_t cost = (uint64_t)(std::max(shared_by(i, o, L), 1u) - 1) * w_share + (uint64_t)load[c][h] * 16 +
+#ifndef SG_LIT_LOADW
+#define SG_LIT_LOADW 16
+#endif
+            const uint64_t cost = (uint64_t)(std::max(shared_by(i, o, L), 1u) - 1) * w_share + (uint64_t)load[c][h] * SG_LIT_LOADW +
                                   gram_commonness(&T->pat[T->pat_off[i] + o], L);
             if (cost < best) { best = cost; bo = o; bh = h; }
         }
@@ -764,6 +767,7 @@ constexpr uint32_t LS_HB = 256;    // per-block LDS hit buffer (entries)
 constexpr uint32_t LS_HALO = 64;   // text bytes staged on each side of the tile
 constexpr uint32_t LS_Q = 512;     // per-block candidate queue (entries: pos:14 | class:3 | record:14)
 constexpr int LS_BATCH = 4;        // candidates per lane whose global loads are issued together
+constexpr uint32_t LS_MW = 512;    // per-block queue of (candidate, further entry) pairs of shared buckets
 
 __device__ __forceinline__ uint32_t fold4(uint32_t w) {
     // ASCII 'A'..'Z' -> 'a'..'z' in each byte (SWAR)
@@ -853,6 +857,8 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
     __shared__ unsigned long long s_hits[LS_HB];
     __shared__ uint32_t s_q[LS_Q];
     __shared__ uint2 s_kf[LS_Q];  // per queued candidate: (bucket, 8-gram fingerprint)
+    __shared__ uint2 s_mw[LS_MW];  // (candidate, entry) pairs of shared buckets
+    __shared__ uint32_t s_mn;
     __shared__ uint32_t s_red[BLK / 64];
     __shared__ uint32_t s_hn, s_g, s_base, s_ebase;
     uint32_t *s_bm = s_dyn;
@@ -864,7 +870,7 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
         s_bm[q] = a.bitmap[q];
         if (a.rank_lds) s_rank[q] = a.rank[q];
     }
-    if (threadIdx.x == 0) s_hn = 0;
+    if (threadIdx.x == 0) { s_hn = 0; s_mn = 0; }
     __syncthreads();
     const uint32_t t = threadIdx.x;
     const uint64_t n = a.n;
@@ -1085,6 +1091,17 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                 // fingerprints: the gram itself (entries shorter than 8) and the 8-gram's
                 s_kf[i] = make_uint2(k, lit_fp8(k0, k1));
             }
+            // one further entry e of a shared bucket against the candidate at p (fp8/fp4: its
+            // 8-gram fingerprint and its gram)
+            auto check_entry = [&](uint32_t e, uint32_t fp8v, uint32_t fp4v, uint32_t c, uint64_t p, uint32_t rec) {
+                const uint4 inf = a.einfo[e];
+                if (a.diag) atomicAdd(&a.diag[4], 1ull);
+                if (a.efp[e] != (inf.z >= 8u ? fp8v : fp4v)) return;
+                if (a.diag) atomicAdd(&a.diag[5], 1ull);
+                const uint4 w0 = a.pat16[inf.w];
+                const uint4 w1 = inf.z > 16 ? a.pat16[inf.w + 1] : make_uint4(0, 0, 0, 0);
+                if (lit_verify(a, s_tile, base, TILE, p, inf.y, inf.z, inf.w, c, w0, w1)) lit_emit(a, push, rec, inf.x);
+            };
             // stage 2: LS_BATCH candidates per lane, their bucket records and first pattern
             // rows loaded together, then verified against the LDS text
             for (uint32_t i0 = t; i0 < qn; i0 += LS_BATCH * BLK) {
@@ -1143,20 +1160,37 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                         }
                     }
                     if (br[u].w >> 31) {
-                        // rare: more patterns share this bucket
+                        // more patterns share this bucket: its further entries are queued as
+                        // (candidate, entry) pairs that the whole block checks below, one pair
+                        // per thread, instead of this lane walking them one dependent load
+                        // chain after another while its wave waits (C4: 3.6 % of candidates,
+                        // half of the scan's time walked in line)
                         const uint32_t k = s_kf[i].x;
-                        for (uint32_t e = a.eoff[k] + 1; e < a.eoff[k + 1]; ++e) {
-                            const uint4 inf = a.einfo[e];
-                            if (a.efp[e] != (inf.z >= 8u ? fp8[u] : fp4[u])) continue;
-                            const uint4 w0 = a.pat16[inf.w];
-                            const uint4 w1 = inf.z > 16 ? a.pat16[inf.w + 1] : make_uint4(0, 0, 0, 0);
-                            if (lit_verify(a, s_tile, base, TILE, p, inf.y, inf.z, inf.w, c, w0, w1))
-                                lit_emit(a, push, rec, inf.x);
+                        const uint32_t e0 = a.eoff[k] + 1, e1 = a.eoff[k + 1];
+                        if (a.diag) atomicAdd(&a.diag[3], 1ull);
+                        const uint32_t slot = atomicAdd(&s_mn, e1 - e0);
+                        for (uint32_t e = e0; e < e1; ++e) {
+                            if (slot + (e - e0) < LS_MW) s_mw[slot + (e - e0)] = make_uint2(i, e);
+                            else check_entry(e, fp8[u], fp4[u], c, p, rec);  // queue full: in line
                         }
                     }
                 }
             }
             __syncthreads();
+            for (uint32_t j = t; j < min(s_mn, LS_MW); j += BLK) {
+                const uint2 we = s_mw[j];
+                const uint32_t ent = s_q[we.x];
+                const uint32_t q = ent >> 17;
+                const uint32_t c = (ent >> 14) & 7u;
+                uint32_t w0 = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3u));
+                uint32_t w1 = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3u) + 4);
+                if (a.nocase) { w0 = fold4(w0); w1 = fold4(w1); }
+                const uint32_t k0 = (q & 3) ? __builtin_amdgcn_alignbyte(w1, w0, q & 3) : w0;
+                check_entry(we.y, s_kf[we.x].y, (c >= 3) ? k0 : (k0 & ((1u << (8 * (c + 1))) - 1u)), c, base + q,
+                            s_base + (ent & 0x3fffu) - 1);
+            }
+            __syncthreads();
+            if (t == 0) s_mn = 0;
             // hit-dense inputs (regex prefilter fan-out): drain between queue batches, so the
             // buffer rarely overflows into per-wave global atomics
             flush(false);
@@ -1841,7 +1875,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
         a.spans_out = (!trial_tiles && fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
         a.rec_flag = (mf && !trial_tiles) ? mf->flags : nullptr;
-        const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + 64;
+        const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + LS_MW * 8 + 64;
         auto blocks_per_cu = [&](uint32_t dyn) {
             return std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
         };
@@ -1850,8 +1884,8 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         a.diag = nullptr;
         unsigned long long *diag = nullptr;
         if (sw_lit_trial_log() && !trial_tiles) {
-            SG_TRY(slot(c, S_M_TMP2, 4, &diag));
-            SG_HIP(hipMemsetAsync(diag, 0, 32, c->stream));
+            SG_TRY(slot(c, S_M_TMP2, 8, &diag));
+            SG_HIP(hipMemsetAsync(diag, 0, 64, c->stream));
             a.diag = diag;
         }
         const uint32_t dyn = a.rank_lds ? dyn_r : dyn_n;
@@ -1895,11 +1929,19 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
 #undef SG_LIT_GEOMS
 #undef SG_LIT_KERNELS
         if (diag) {
-            unsigned long long dv[4] = {0, 0, 0, 0};
-            SG_TRY(ctx_readback(c, dv, diag, 32));
+            unsigned long long dv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            SG_TRY(ctx_readback(c, dv, diag, 64));
             fprintf(stderr, "sg %s: %u records, %llu bitmap candidates, %llu fingerprint-confirmed, %llu verified "
-                            "(first bucket entries; tmpl 0x%x, %s scheme)\n",
-                    name, R, dv[0], dv[1], dv[2], Lt.tmpl, Lt.joint ? "joint" : "two");
+                            "(first bucket entries; tmpl 0x%x, %s scheme); %llu candidates in shared buckets, "
+                            "%llu further entries walked, %llu fingerprint-equal\n",
+                    name, R, dv[0], dv[1], dv[2], Lt.tmpl, Lt.joint ? "joint" : "two", dv[3], dv[4], dv[5]);
+            uint32_t nb = (uint32_t)Lt.eoff.size() - 1, multi = 0, mx = 0, in_multi = 0;
+            for (uint32_t k = 0; k < nb; ++k) {
+                const uint32_t e = Lt.eoff[k + 1] - Lt.eoff[k];
+                if (e > 1) { ++multi; in_multi += e; }
+                mx = std::max(mx, e);
+            }
+            fprintf(stderr, "sg %s: %u buckets, %u shared (%u entries), largest %u entries\n", name, nb, multi, in_multi, mx);
         }
         return SG_OK;
     };
