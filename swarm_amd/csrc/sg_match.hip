@@ -391,10 +391,8 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
             const uint32_t hi = (c == 4) ? word_at(i, o + 4, 4) : (c == LIT_J ? (uint32_t)T->pat[T->pat_off[i] + o + 4] : 0u);
             const uint32_t h = lit_h(lo, hi, c, T->bits[c]);
             constexpr uint32_t w_share = 64u;  // cost of one more pattern sharing the gram
-#ifndef SG_LIT_LOADW
-#define SG_LIT_LOADW 16
-#endif
-            const uint64_t cost = (uint64_t)(std::max(shared_by(i, o, L), 1u) - 1) * w_share + (uint64_t)load[c][h] * SG_LIT_LOADW +
+            // (a load weight of 256 instead of 16, fewer hash-shared buckets: C4 5.78 -> 5.87 ms)
+            const uint64_t cost = (uint64_t)(std::max(shared_by(i, o, L), 1u) - 1) * w_share + (uint64_t)load[c][h] * 16 +
                                   gram_commonness(&T->pat[T->pat_off[i] + o], L);
             if (cost < best) { best = cost; bo = o; bh = h; }
         }
@@ -767,7 +765,7 @@ constexpr uint32_t LS_HB = 256;    // per-block LDS hit buffer (entries)
 constexpr uint32_t LS_HALO = 64;   // text bytes staged on each side of the tile
 constexpr uint32_t LS_Q = 512;     // per-block candidate queue (entries: pos:14 | class:3 | record:14)
 constexpr int LS_BATCH = 4;        // candidates per lane whose global loads are issued together
-constexpr uint32_t LS_MW = 512;    // per-block queue of (candidate, further entry) pairs of shared buckets
+constexpr uint32_t LS_MW = 256;    // per-block queue of (further entry, candidate) pairs of shared buckets
 
 __device__ __forceinline__ uint32_t fold4(uint32_t w) {
     // ASCII 'A'..'Z' -> 'a'..'z' in each byte (SWAR)
@@ -857,7 +855,7 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
     __shared__ unsigned long long s_hits[LS_HB];
     __shared__ uint32_t s_q[LS_Q];
     __shared__ uint2 s_kf[LS_Q];  // per queued candidate: (bucket, 8-gram fingerprint)
-    __shared__ uint2 s_mw[LS_MW];  // (candidate, entry) pairs of shared buckets
+    __shared__ uint4 s_mw[LS_MW];  // {entry, 8-gram fingerprint, gram, queue word} of shared buckets
     __shared__ uint32_t s_mn;
     __shared__ uint32_t s_red[BLK / 64];
     __shared__ uint32_t s_hn, s_g, s_base, s_ebase;
@@ -1050,6 +1048,28 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
         if (a.diag && t == 0) atomicAdd(&a.diag[0], (unsigned long long)qtot);
         if (tile + gridDim.x < a.n_tiles) load_text(tile + gridDim.x);
         const uint32_t lrec0 = excl;  // tile-local index of this thread's first record start
+        // one further entry e of a shared bucket against the candidate at p (fp8/fp4: its
+        // 8-gram fingerprint and its gram)
+        auto check_entry = [&](uint32_t e, uint32_t fp8v, uint32_t fp4v, uint32_t c, uint64_t p, uint32_t rec) {
+            const uint4 inf = a.einfo[e];
+            if (a.diag) atomicAdd(&a.diag[4], 1ull);
+            if (a.efp[e] != (inf.z >= 8u ? fp8v : fp4v)) return;
+            if (a.diag) atomicAdd(&a.diag[5], 1ull);
+            const uint4 w0 = a.pat16[inf.w];
+            const uint4 w1 = inf.z > 16 ? a.pat16[inf.w + 1] : make_uint4(0, 0, 0, 0);
+            if (lit_verify(a, s_tile, base, TILE, p, inf.y, inf.z, inf.w, c, w0, w1)) lit_emit(a, push, rec, inf.x);
+        };
+        // the queued pairs, one per thread (block-uniform call sites; the tile's text must
+        // still be in LDS)
+        auto run_pairs = [&]() {
+            const uint32_t mn = min(s_mn, LS_MW);
+            for (uint32_t j = t; j < mn; j += BLK) {
+                const uint4 pr = s_mw[j];
+                check_entry(pr.x, pr.y, pr.z, (pr.w >> 14) & 7u, base + (pr.w >> 17), s_base + (pr.w & 0x3fffu) - 1);
+            }
+            __syncthreads();
+            if (t == 0) s_mn = 0;
+        };
         for (uint32_t r0 = 0; r0 < qtot; r0 += LS_Q) {
             uint32_t qi = qex;
             if (qi < r0 + LS_Q && qi + ncand > r0) {
@@ -1091,17 +1111,6 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                 // fingerprints: the gram itself (entries shorter than 8) and the 8-gram's
                 s_kf[i] = make_uint2(k, lit_fp8(k0, k1));
             }
-            // one further entry e of a shared bucket against the candidate at p (fp8/fp4: its
-            // 8-gram fingerprint and its gram)
-            auto check_entry = [&](uint32_t e, uint32_t fp8v, uint32_t fp4v, uint32_t c, uint64_t p, uint32_t rec) {
-                const uint4 inf = a.einfo[e];
-                if (a.diag) atomicAdd(&a.diag[4], 1ull);
-                if (a.efp[e] != (inf.z >= 8u ? fp8v : fp4v)) return;
-                if (a.diag) atomicAdd(&a.diag[5], 1ull);
-                const uint4 w0 = a.pat16[inf.w];
-                const uint4 w1 = inf.z > 16 ? a.pat16[inf.w + 1] : make_uint4(0, 0, 0, 0);
-                if (lit_verify(a, s_tile, base, TILE, p, inf.y, inf.z, inf.w, c, w0, w1)) lit_emit(a, push, rec, inf.x);
-            };
             // stage 2: LS_BATCH candidates per lane, their bucket records and first pattern
             // rows loaded together, then verified against the LDS text
             for (uint32_t i0 = t; i0 < qn; i0 += LS_BATCH * BLK) {
@@ -1161,41 +1170,29 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                     }
                     if (br[u].w >> 31) {
                         // more patterns share this bucket: its further entries are queued as
-                        // (candidate, entry) pairs that the whole block checks below, one pair
-                        // per thread, instead of this lane walking them one dependent load
-                        // chain after another while its wave waits (C4: 3.6 % of candidates,
-                        // half of the scan's time walked in line)
+                        // (entry, candidate) pairs that the whole block checks once the queue is
+                        // half full or the tile ends, one pair per thread, instead of this lane
+                        // walking them one dependent load chain after another while its wave
+                        // waits (C4: 3.7 % of candidates, half of the scan's time in line)
                         const uint32_t k = s_kf[i].x;
                         const uint32_t e0 = a.eoff[k] + 1, e1 = a.eoff[k + 1];
                         if (a.diag) atomicAdd(&a.diag[3], 1ull);
                         const uint32_t slot = atomicAdd(&s_mn, e1 - e0);
                         for (uint32_t e = e0; e < e1; ++e) {
-                            if (slot + (e - e0) < LS_MW) s_mw[slot + (e - e0)] = make_uint2(i, e);
+                            if (slot + (e - e0) < LS_MW) s_mw[slot + (e - e0)] = make_uint4(e, fp8[u], fp4[u], ent);
                             else check_entry(e, fp8[u], fp4[u], c, p, rec);  // queue full: in line
                         }
                     }
                 }
             }
             __syncthreads();
-            for (uint32_t j = t; j < min(s_mn, LS_MW); j += BLK) {
-                const uint2 we = s_mw[j];
-                const uint32_t ent = s_q[we.x];
-                const uint32_t q = ent >> 17;
-                const uint32_t c = (ent >> 14) & 7u;
-                uint32_t w0 = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3u));
-                uint32_t w1 = *reinterpret_cast<const uint32_t *>(s_tile + (q & ~3u) + 4);
-                if (a.nocase) { w0 = fold4(w0); w1 = fold4(w1); }
-                const uint32_t k0 = (q & 3) ? __builtin_amdgcn_alignbyte(w1, w0, q & 3) : w0;
-                check_entry(we.y, s_kf[we.x].y, (c >= 3) ? k0 : (k0 & ((1u << (8 * (c + 1))) - 1u)), c, base + q,
-                            s_base + (ent & 0x3fffu) - 1);
-            }
-            __syncthreads();
-            if (t == 0) s_mn = 0;
+            if (s_mn >= LS_MW / 2) run_pairs();
             // hit-dense inputs (regex prefilter fan-out): drain between queue batches, so the
             // buffer rarely overflows into per-wave global atomics
             flush(false);
         }
         __syncthreads();
+        if (s_mn) run_pairs();
         flush(tile + gridDim.x >= a.n_tiles);
     }
 }
@@ -1875,7 +1872,7 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
         a.spans_out = (!trial_tiles && fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
         a.rec_flag = (mf && !trial_tiles) ? mf->flags : nullptr;
-        const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + LS_MW * 8 + 64;
+        const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + LS_MW * 16 + 64;
         auto blocks_per_cu = [&](uint32_t dyn) {
             return std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
         };
