@@ -99,6 +99,7 @@ struct sg_matcher {
         std::vector<uint32_t> efp;           // per entry: gram fingerprint (the gram itself for L <= 4)
         std::vector<uint32_t> einfo;         // per entry: {pid, anchor, len, 16-B pattern row}
         std::vector<uint32_t> brec;          // per bucket: {fp, pid, len | anchor << 24, row | more << 31}
+        uint32_t n_shared = 0;               // buckets holding more than one entry
         std::vector<uint32_t> pat_off;       // per pattern (n + 1), into pat
         std::vector<uint8_t> pat;            // folded pattern bytes
         std::vector<uint8_t> pat16;          // folded pattern bytes, each padded to 16 B rows
@@ -442,6 +443,8 @@ static int build_lit(const uint8_t *pats, const uint32_t *offs, uint32_t n, uint
         T->einfo.insert(T->einfo.end(), {e.pid, e.anc, len_of(e.pid), row[e.pid]});
     }
     if (ne) T->eoff.push_back(ne);
+    T->n_shared = 0;
+    for (size_t k = 0; k + 1 < T->eoff.size(); ++k) T->n_shared += (T->eoff[k + 1] - T->eoff[k] > 1) ? 1u : 0u;
     if (T->eoff.size() != (size_t)acc + 1) { set_error("build_lit: bucket bookkeeping mismatch"); return SG_E_INVAL; }
     // one 16-B record per bucket: its first entry, plus a flag when more entries follow
     T->brec.assign((size_t)acc * 4, 0);
@@ -758,6 +761,7 @@ struct LitArgs {
     uint2 *spans_out;                    // non-null: also write the parse's record spans (fused A3)
     uint8_t *rec_flag;                   // non-null: mark matched records here instead of listing hits
     uint32_t rank_lds;                   // the bitmap words' ranks staged in LDS too (else read from L2)
+    uint32_t mw_cap;                     // shared-bucket pair queue entries in dynamic LDS (0: walked in line)
     unsigned long long *diag;            // calibration (SG_LIT_TRIAL_LOG): queued, fingerprint-confirmed, verified
 };
 
@@ -765,7 +769,7 @@ constexpr uint32_t LS_HB = 256;    // per-block LDS hit buffer (entries)
 constexpr uint32_t LS_HALO = 64;   // text bytes staged on each side of the tile
 constexpr uint32_t LS_Q = 512;     // per-block candidate queue (entries: pos:14 | class:3 | record:14)
 constexpr int LS_BATCH = 4;        // candidates per lane whose global loads are issued together
-constexpr uint32_t LS_MW = 256;    // per-block queue of (further entry, candidate) pairs of shared buckets
+constexpr uint32_t LS_MW = 256;    // per-block queue of (further entry, candidate) pairs of shared buckets (when it fits)
 
 __device__ __forceinline__ uint32_t fold4(uint32_t w) {
     // ASCII 'A'..'Z' -> 'a'..'z' in each byte (SWAR)
@@ -855,7 +859,6 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
     __shared__ unsigned long long s_hits[LS_HB];
     __shared__ uint32_t s_q[LS_Q];
     __shared__ uint2 s_kf[LS_Q];  // per queued candidate: (bucket, 8-gram fingerprint)
-    __shared__ uint4 s_mw[LS_MW];  // {entry, 8-gram fingerprint, gram, queue word} of shared buckets
     __shared__ uint32_t s_mn;
     __shared__ uint32_t s_red[BLK / 64];
     __shared__ uint32_t s_hn, s_g, s_base, s_ebase;
@@ -864,6 +867,11 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
     // leaving them in L2 gives the CU another block (their LDS is half the bitmaps': the fields
     // matcher's tables 68 -> 45 KB, 1 -> 2 blocks per CU, lit_match 8.2 -> 5.7 ms).
     uint16_t *s_rank = reinterpret_cast<uint16_t *>(s_dyn + a.bm_words);
+    // {entry, 8-gram fingerprint, gram, queue word} of shared buckets: after the bitmaps (and
+    // their ranks), 16-B aligned; a.mw_cap entries (0 when the filter has no shared bucket or
+    // the queue would cost the CU a block)
+    uint4 *s_mw = reinterpret_cast<uint4 *>(s_dyn + ((a.bm_words + (a.rank_lds ? (a.bm_words + 1) / 2 : 0) + 3) & ~3u));
+    const uint32_t mwcap = a.mw_cap;
     for (uint32_t q = threadIdx.x; q < a.bm_words; q += BLK) {
         s_bm[q] = a.bitmap[q];
         if (a.rank_lds) s_rank[q] = a.rank[q];
@@ -1062,7 +1070,7 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
         // the queued pairs, one per thread (block-uniform call sites; the tile's text must
         // still be in LDS)
         auto run_pairs = [&]() {
-            const uint32_t mn = min(s_mn, LS_MW);
+            const uint32_t mn = min(s_mn, mwcap);
             for (uint32_t j = t; j < mn; j += BLK) {
                 const uint4 pr = s_mw[j];
                 check_entry(pr.x, pr.y, pr.z, (pr.w >> 14) & 7u, base + (pr.w >> 17), s_base + (pr.w & 0x3fffu) - 1);
@@ -1179,20 +1187,20 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
                         if (a.diag) atomicAdd(&a.diag[3], 1ull);
                         const uint32_t slot = atomicAdd(&s_mn, e1 - e0);
                         for (uint32_t e = e0; e < e1; ++e) {
-                            if (slot + (e - e0) < LS_MW) s_mw[slot + (e - e0)] = make_uint4(e, fp8[u], fp4[u], ent);
+                            if (slot + (e - e0) < mwcap) s_mw[slot + (e - e0)] = make_uint4(e, fp8[u], fp4[u], ent);
                             else check_entry(e, fp8[u], fp4[u], c, p, rec);  // queue full: in line
                         }
                     }
                 }
             }
             __syncthreads();
-            if (s_mn >= LS_MW / 2) run_pairs();
+            if (mwcap && s_mn >= mwcap / 2) run_pairs();
             // hit-dense inputs (regex prefilter fan-out): drain between queue batches, so the
             // buffer rarely overflows into per-wave global atomics
             flush(false);
         }
         __syncthreads();
-        if (s_mn) run_pairs();
+        if (mwcap && s_mn) run_pairs();
         flush(tile + gridDim.x >= a.n_tiles);
     }
 }
@@ -1872,12 +1880,18 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
         a.spans_out = (!trial_tiles && fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
         a.rec_flag = (mf && !trial_tiles) ? mf->flags : nullptr;
-        const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + LS_MW * 16 + 64;
+        const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + 64;
         auto blocks_per_cu = [&](uint32_t dyn) {
             return std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
         };
-        const uint32_t dyn_r = lit_lds_bytes(Lt, true), dyn_n = lit_lds_bytes(Lt, false);
+        // the shared-bucket pair queue (LS_MW entries of 16 B after the tables) when the filter
+        // has shared buckets: it decides with the tables whether the ranks fit too (a static
+        // queue in every filter's scan took X1's lit_match from 1.02 to 1.28-1.31 ms; C4's
+        // prefilter, 847 shared buckets, runs 3.67 -> 2.57 ms with it)
+        const uint32_t qb = Lt.n_shared ? LS_MW * 16u + 16u : 0u;
+        const uint32_t dyn_r = lit_lds_bytes(Lt, true) + qb, dyn_n = lit_lds_bytes(Lt, false) + qb;
         a.rank_lds = blocks_per_cu(dyn_r) == blocks_per_cu(dyn_n) ? 1u : 0u;
+        a.mw_cap = Lt.n_shared ? LS_MW : 0u;
         a.diag = nullptr;
         unsigned long long *diag = nullptr;
         if (sw_lit_trial_log() && !trial_tiles) {
@@ -1893,6 +1907,9 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         // candidate stage's L2 latency (C4 prefilter 2.71 -> 1.84 ms per 4M banners); with
         // room for 3+ blocks, 256 threads x 64 positions probe faster (C3 1.35 vs 1.54 ms).
         const int ls_block = bpc <= 2 ? 512 : 256;
+        if (sw_lit_trial_log() && !trial_tiles)
+            fprintf(stderr, "sg %s: %u shared buckets, pair queue %u, ranks in LDS %u, %u B LDS + %u static, %u blocks/CU of %d\n",
+                    name, Lt.n_shared, a.mw_cap, a.rank_lds, dyn, stat, bpc, ls_block);
         const int bpt = (int)(L.tile_bytes / ls_block);
         const double bytes = (double)n + 8.0 * R;
         auto launch = [&](auto kern, int blk) -> int {
