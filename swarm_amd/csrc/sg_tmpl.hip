@@ -335,18 +335,42 @@ __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
         for (uint32_t x = lane; x < cw; x += 64) cnt[x] = 0;
         for (uint32_t x = lane; x < ntw; x += 64) { tch[x] = 0; res[x] = 0; }
         for (uint32_t x = lane; x < naw; x += 64) seen[x] = 0;
+        // every segment's [start, end) of this record at once (lanes 2g, 2g + 1), not one
+        // dependent pair of offset loads per segment (loading them one record ahead gained nothing)
+        uint32_t myo = 0;
+        if (nseg <= 32 && lane < 2 * nseg) myo = roff[(size_t)(lane >> 1) * (R + 1) + r + (lane & 1)];
         tm_wave_sync();
-        for (uint32_t sg = 0; sg < nseg; ++sg) {
-            const uint32_t *ro = roff + (size_t)sg * (R + 1);
-            const uint32_t a = ro[r], e = ro[r + 1];
-            for (uint32_t i = a + lane; i < e; i += 64) {
-                const uint32_t at = (uint32_t)K[i], bit = 1u << (at & 31);
-                if (at == TM_NO_ATOM || (atomicOr(&seen[at >> 5], bit) & bit)) continue;  // counted once
-                for (uint32_t q = s_occ[at], qe = s_occ[at + 1]; q < qe; ++q) {
-                    const uint32_t mt = s_mt[q], m = mt & 0xffffu, t = mt >> 16;
-                    atomicAdd(&cnt[m >> 2], 1u << (8 * (m & 3)));
-                    atomicOr(&tch[t >> 5], 1u << (t & 31));
+        // one atom: counted once per record, its (matcher, template) occurrences
+        auto count_atom = [&](uint32_t at) {
+            const uint32_t bit = 1u << (at & 31);
+            if (at == TM_NO_ATOM || (atomicOr(&seen[at >> 5], bit) & bit)) return;
+            for (uint32_t q = s_occ[at], qe = s_occ[at + 1]; q < qe; ++q) {
+                const uint32_t mt = s_mt[q], m = mt & 0xffffu, t = mt >> 16;
+                atomicAdd(&cnt[m >> 2], 1u << (8 * (m & 3)));
+                atomicOr(&tch[t >> 5], 1u << (t & 31));
+            }
+        };
+        if (nseg <= 32) {
+            // the record's hits of all segments as one list: lane j loads hit j, so the
+            // segments' loads are issued together instead of one round trip per segment
+            uint32_t tot = 0;
+            for (uint32_t sg = 0; sg < nseg; ++sg)
+                tot += (uint32_t)__shfl((int)myo, (int)(2 * sg + 1), 64) - (uint32_t)__shfl((int)myo, (int)(2 * sg), 64);
+            for (uint32_t j0 = 0; j0 < tot; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                uint32_t idx = 0xffffffffu, base = 0;
+                for (uint32_t sg = 0; sg < nseg; ++sg) {
+                    const uint32_t sa = (uint32_t)__shfl((int)myo, (int)(2 * sg), 64);
+                    const uint32_t c = (uint32_t)__shfl((int)myo, (int)(2 * sg + 1), 64) - sa;
+                    if (j >= base && j < base + c) idx = sa + (j - base);
+                    base += c;
                 }
+                if (idx != 0xffffffffu) count_atom((uint32_t)K[idx]);
+            }
+        } else {
+            for (uint32_t sg = 0; sg < nseg; ++sg) {
+                const uint32_t *ro = roff + (size_t)sg * (R + 1);
+                for (uint32_t i = ro[r] + lane; i < ro[r + 1]; i += 64) count_atom((uint32_t)K[i]);
             }
         }
         tm_wave_sync();
@@ -463,6 +487,9 @@ static int tm_rec_wave(sg_ctx *c, const sg_templates *h, const sg_templates::Dev
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((R + TMW_WAVES - 1) / TMW_WAVES, 8192);
     if (lds > 65536)
         SG_HIP(hipFuncSetAttribute((const void *)k_tm_rec_eval, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if (sw_lit_trial_log())
+        fprintf(stderr, "sg tm_rec_eval: %u records, %u hit segments, %u matchers, %u atoms, %u templates, %zu B LDS per block\n",
+                Ru, nseg, h->n_match, h->n_atoms, h->n_tmpl, lds);
     SG_LAUNCH(c, "tm_rec_eval", k_tm_rec_eval, blocks, 64 * TMW_WAVES, lds, K, roff, nseg, Ru, D.occ16, D.occ_mt, D.tinfo,
               D.minfo, D.vacm, h->n_atoms, n_occ, h->n_match, h->n_tmpl, G, rcnt);
     uint64_t nout = 0;
