@@ -421,27 +421,50 @@ struct TmRecCnt {
     __device__ uint64_t operator()(uint32_t i) const { return rcnt[i]; }
 };
 
+// Each record's (record, template) pairs go through a per-wave LDS buffer: the lanes (one per
+// bitmap word) scatter their template ids there, then the wave writes the record's run with
+// consecutive lanes on consecutive slots (the direct version had every lane store its own run
+// one pair at a time: 64 runs per store instruction). Runs longer than the buffer are written
+// directly.
+constexpr uint32_t TE_CAP = 1024;
 __global__ __launch_bounds__(256) void k_tm_rec_emit(const uint32_t *__restrict__ G, const uint64_t *__restrict__ off,
-                                                     uint32_t R, uint32_t ntw, uint32_t *__restrict__ rec,
-                                                     uint32_t *__restrict__ tid) {
-    const uint32_t lane = threadIdx.x & 63;
+                                                     const uint32_t *__restrict__ rcnt, uint32_t R, uint32_t ntw,
+                                                     uint32_t *__restrict__ rec, uint32_t *__restrict__ tid) {
+    __shared__ uint32_t s_t[4][TE_CAP];
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t *buf = s_t[wid];
     const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < R; r += nw) {
-        uint64_t base = off[r];
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + wid; r < R; r += nw) {
+        const uint64_t base = off[r];
+        const uint32_t n = rcnt[r];
+        const bool staged = n <= TE_CAP;
+        uint32_t lp = 0;  // pairs of the words before this lane's, within the record
         for (uint32_t w0 = 0; w0 < ntw; w0 += 64) {
             const uint32_t w = w0 + lane;
             uint32_t bits = w < ntw ? G[(size_t)r * ntw + w] : 0u;
             const uint32_t c = (uint32_t)__popc(bits);
             const uint32_t inc = wave_incl_scan(c);
-            uint64_t p = base + inc - c;
+            uint32_t p = lp + inc - c;
             while (bits) {
-                const uint32_t b = (uint32_t)__builtin_ctz(bits);
+                const uint32_t t = 32 * w + (uint32_t)__builtin_ctz(bits);
                 bits &= bits - 1;
-                rec[p] = r;
-                tid[p] = 32 * w + b;
+                if (staged) buf[p] = t;
+                else { rec[base + p] = r; tid[base + p] = t; }
                 ++p;
             }
-            base += __shfl(inc, 63, 64);
+            lp += (uint32_t)__shfl((int)inc, 63, 64);
+        }
+        if (staged) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            for (uint32_t j = lane; j < n; j += 64) {
+                rec[base + j] = r;
+                tid[base + j] = buf[j];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
     }
 }
@@ -500,7 +523,7 @@ static int tm_rec_wave(sg_ctx *c, const sg_templates *h, const sg_templates::Dev
     SG_TRY(slot(c, S_T_REC, nout + 1, &rec));
     SG_TRY(slot(c, S_T_TID, nout + 1, &tid));
     const uint32_t eblocks = (uint32_t)std::min<uint64_t>((R + 3) / 4, 16384);
-    SG_LAUNCH_B(c, "tm_rec_emit", 8.0 * nout + 4.0 * R * ntw, k_tm_rec_emit, eblocks, 256, 0, G, off, Ru, ntw, rec,
+    SG_LAUNCH_B(c, "tm_rec_emit", 8.0 * nout + 4.0 * R * ntw, k_tm_rec_emit, eblocks, 256, 0, G, off, rcnt, Ru, ntw, rec,
                 tid);
     res->rec_idx = rec;
     res->tmpl_id = tid;
