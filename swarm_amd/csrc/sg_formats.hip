@@ -515,15 +515,20 @@ struct JsonLen {
     }
 };
 
-struct JsWrite {
-    uint8_t *out;
+// A wave's 64 items write one contiguous output range (items in order, offsets from one
+// scan): the rows are decoded into a per-wave LDS window at their offsets inside that range,
+// then the wave stores the range with consecutive lanes on consecutive bytes — the direct
+// version had each lane store its own rows one byte at a time (64 scattered bytes per store
+// instruction). A wave whose range exceeds the window writes directly.
+constexpr uint32_t JE_CAP = 4096;
+struct JsWriteLds {
+    uint8_t *win;  // the wave's window (or the output at the wave's range start); o relative to it
     uint32_t *row_rec, *row_key;
-    uint64_t o;
-    uint32_t row, rec, key;
+    uint32_t o, row, rec, key;
     __device__ void begin() {}
-    __device__ void operator()(uint8_t ch) { out[o++] = ch; }
+    __device__ void operator()(uint8_t ch) { win[o++] = ch; }
     __device__ void end() {
-        out[o++] = '\n';
+        win[o++] = '\n';
         row_rec[row] = rec;
         row_key[row] = key;
         ++row;
@@ -532,15 +537,33 @@ struct JsWrite {
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_json_emit(const uint8_t *__restrict__ buf, const uint4 *__restrict__ desc,
                                                    const uint64_t *__restrict__ offs, uint32_t nitems, uint32_t nkeys,
-                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ row_rec,
-                                                   uint32_t *__restrict__ row_key) {
+                                                   uint64_t total_bytes, uint8_t *__restrict__ out,
+                                                   uint32_t *__restrict__ row_rec, uint32_t *__restrict__ row_key) {
+    __shared__ uint8_t s_win[4][JE_CAP];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nitems) return;
-    const uint4 d = desc[i];
-    if (d.z == 0) return;
-    const uint64_t off = offs[i];
-    JsWrite w{out, row_rec, row_key, off >> 32, (uint32_t)off, i / nkeys, i % nkeys};
-    js_value(buf, d.x, d.y, w);
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t iw0 = i - lane;
+    if (iw0 >= nitems) return;  // whole wave
+    const uint64_t wb = offs[iw0] >> 32;
+    const uint64_t we = iw0 + 64 < nitems ? offs[iw0 + 64] >> 32 : total_bytes;
+    const bool staged = we - wb <= JE_CAP;
+    if (i < nitems) {
+        const uint4 d = desc[i];
+        if (d.z != 0) {
+            const uint64_t off = offs[i];
+            // one writer for both cases (two instantiations of the walk cost registers): the
+            // window, or the output at the wave's range start
+            JsWriteLds w{staged ? s_win[wid] : out + wb, row_rec, row_key, (uint32_t)((off >> 32) - wb), (uint32_t)off,
+                         i / nkeys, i % nkeys};
+            js_value(buf, d.x, d.y, w);
+        }
+    }
+    if (!staged) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t len = (uint32_t)(we - wb);
+    for (uint32_t k = lane; k < len; k += 64) out[wb + k] = s_win[wid][k];
 }
 
 int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *keys, const uint32_t *key_offs,
@@ -580,7 +603,7 @@ int dev_json_fields(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const uint8_t *
     SG_TRY(slot(c, S_F_REC, rows + 1, &rrec));
     SG_TRY(slot(c, S_F_KEY, rows + 1, &rkey));
     SG_LAUNCH_B(c, "json_emit", 2.0 * bytes + 8.0 * rows, k_json_emit, (uint32_t)((items + 255) / 256), 256, 0, d_buf,
-                desc, offs, (uint32_t)items, nkeys, out, rrec, rkey);
+                desc, offs, (uint32_t)items, nkeys, bytes, out, rrec, rkey);
     res->data = out;
     res->bytes = bytes;
     res->rows = rows;
