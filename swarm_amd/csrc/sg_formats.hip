@@ -291,6 +291,93 @@ __device__ __forceinline__ void js_value(const Buf &buf, uint32_t vs, uint32_t v
     }
 }
 
+// js_value's (rows, bytes) for an array value [vs, ve) holding no backslash (its strings
+// decode to themselves), 16 bytes per step: SWAR masks of the bytes js_value reacts to
+// ('"', '[', '{', ']', '}', ',') and of the non-blank bytes, and only those events walked
+// through js_value's state machine (same depth arithmetic, same item ends), each item's first
+// and last non-blank bytes taken from the masks between events. The byte walk cost the JSON
+// scan ~2.7 ms of its 10.5 per fields step (measured by walking every such value twice).
+__device__ __forceinline__ uint32_t js_swar_eq(uint32_t x, uint32_t pat) {
+    const uint32_t y = x ^ pat;
+    const uint32_t z = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
+    return (((z >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+}
+__device__ __forceinline__ void js_count_array_plain(const uint8_t *buf, uint32_t vs, uint32_t ve, uint32_t *rows,
+                                                     uint32_t *bytes) {
+    const uint4 *gb = reinterpret_cast<const uint4 *>(buf);
+    uint32_t depth = 0, nrow = 0, nb = 0;
+    bool in_str = false;
+    uint32_t fnw = 0xffffffffu, lnw = 0;  // the current item's first / last non-blank byte
+    bool fq = false, lq = false;          // ... are quotes
+    auto item_end = [&]() {
+        if (fnw != 0xffffffffu) {
+            uint32_t len = lnw - fnw + 1u;
+            if (fq && lq && len >= 2u) len = len == 2u ? 0u : len - 2u;
+            if (len) { ++nrow; nb += len + 1u; }
+        }
+        fnw = 0xffffffffu;
+    };
+    auto content = [&](uint32_t pos, bool q) {  // a non-blank byte of the current item
+        if (fnw == 0xffffffffu) { fnw = pos; fq = q; }
+        lnw = pos;
+        lq = q;
+    };
+    for (uint32_t b0 = vs & ~15u; b0 < ve; b0 += 16u) {
+        const uint4 v = gb[b0 >> 4];
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+        uint32_t qm = 0, om = 0, cm = 0, km = 0, wm = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t x = wd[d], lx = x | 0x20202020u;
+            qm |= js_swar_eq(x, 0x22222222u) << (4 * d);
+            om |= js_swar_eq(lx, 0x7b7b7b7bu) << (4 * d);
+            cm |= js_swar_eq(lx, 0x7d7d7d7du) << (4 * d);
+            km |= js_swar_eq(x, 0x2c2c2c2cu) << (4 * d);
+            wm |= (js_swar_eq(x, 0x20202020u) | js_swar_eq(x, 0x09090909u) | js_swar_eq(x, 0x0d0d0d0du) |
+                   js_swar_eq(x, 0x0a0a0a0au)) << (4 * d);
+        }
+        const uint32_t lo = vs > b0 ? vs - b0 : 0u, hi = ve - b0 < 16u ? ve - b0 : 16u;
+        const uint32_t rng = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+        const uint32_t nw = ~wm & rng;
+        uint32_t ev = (qm | om | cm | km) & rng, from = lo;
+        while (ev) {
+            const uint32_t j = (uint32_t)__builtin_ctz(ev);
+            ev &= ev - 1u;
+            const uint32_t seg = nw & ((1u << j) - 1u) & ~((1u << from) - 1u);  // plain bytes before it
+            if (seg) {
+                content(b0 + (uint32_t)__builtin_ctz(seg), false);
+                lnw = b0 + 31u - (uint32_t)__builtin_clz(seg);
+                lq = false;
+            }
+            from = j + 1u;
+            const uint32_t bit = 1u << j, pos = b0 + j;
+            if (in_str) {  // only the closing quote ends it; the rest is the item's text
+                if (qm & bit) in_str = false;
+                content(pos, (qm & bit) != 0u);
+                continue;
+            }
+            if (qm & bit) { in_str = true; content(pos, true); continue; }
+            if (om & bit) { ++depth; if (pos != vs) content(pos, false); continue; }  // all but the array's own
+            if (cm & bit) {
+                if (depth == 1u) item_end();
+                else content(pos, false);
+                --depth;
+                continue;
+            }
+            if (depth == 1u) item_end();  // ','
+            else content(pos, false);
+        }
+        const uint32_t seg = nw & ~((1u << from) - 1u);
+        if (seg) {
+            content(b0 + (uint32_t)__builtin_ctz(seg), false);
+            lnw = b0 + 31u - (uint32_t)__builtin_clz(seg);
+            lq = false;
+        }
+    }
+    *rows = nrow;
+    *bytes = nb;
+}
+
 // Compares a decoded key stream with one requested key.
 struct JsKeyEq {
     const uint8_t *k;
@@ -493,6 +580,10 @@ __global__ __launch_bounds__(JT_BLOCK) __attribute__((amdgpu_waves_per_eu(6))) v
                 } else if (c0 != '[' && !((escm >> k) & 1u)) {
                     const uint32_t len = strv ? ve - vs - 2 : ve - vs;
                     d = make_uint4(vs, ve, len ? 1u : 0u, len ? len + 1u : 0u);
+                } else if (c0 == '[' && !((escm >> k) & 1u)) {
+                    uint32_t nr, nbt;
+                    js_count_array_plain(a.buf, vs, ve, &nr, &nbt);
+                    d = make_uint4(vs, ve, nr, nbt);
                 } else {
                     JsCount cnt;
                     js_value(a.buf, vs, ve, cnt);

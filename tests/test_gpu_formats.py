@@ -124,6 +124,23 @@ def test_json_duplicates_malformed_and_whitespace(sg):
     check(sg, b"\n".join(lines) + b"\n", [b"title", b"tech", b"url"])
 
 
+def test_json_plain_arrays(sg):
+    """Array values without backslashes take the scan's 16-byte SWAR counter (rows and bytes
+    must equal the byte walk's): nesting, blanks around and inside items, empty strings,
+    separators and brackets inside strings, empty items, text after the closing bracket, a
+    second array in the same value, at every alignment of the value inside 16-byte blocks."""
+    vals = [b'[]', b'[ ]', b'[,]', b'[1,,2]', b'["a" , "" ,"b"]', b'[ "x,y]" , "[z" ]', b'[[1,2],{"k":[3]},4]',
+            b'[ "" ]', b'[""]', b'["\t"]', b'[  1  2 , 3 ]', b'[1] x', b'[1] [2]',
+            b'["' + b"q" * 40 + b'", "' + b"r" * 17 + b'"]', b'[{"a":"]"},"}",["[",","]]', b'[ true , null , -1.5e3 ]',
+            b'[1,[2,[3,[4]]],5]', b'["a"\t,\r"b" ]', b'[ "a" "b" ]', b'["]"]']
+    lines = []
+    for pad in range(0, 17):
+        for v in vals:
+            lines.append(b'{"' + b"p" * pad + b'":1,"tech":' + v + b',"title":"t"}')
+            lines.append(b'{"tech" :  ' + v + b'  }')
+    check(sg, b"\n".join(lines) + b"\n", [b"tech", b"title"])
+
+
 def test_json_device_rows_match_and_feed_matcher(sg):
     """Rows are a line buffer: the A4 matcher runs on them directly (part-scoped match)."""
     import torch
