@@ -302,19 +302,17 @@ __device__ __forceinline__ uint32_t js_swar_eq(uint32_t x, uint32_t pat) {
     const uint32_t z = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
     return (((z >> 7) & 0x01010101u) * 0x01020408u) >> 24;
 }
-__device__ __forceinline__ void js_count_array_plain(const uint8_t *buf, uint32_t vs, uint32_t ve, uint32_t *rows,
-                                                     uint32_t *bytes) {
+// on_item(a, b, q): each item's trimmed text [a, b) (non-empty), as js_value's emit_item sees
+// it; q: it starts and ends with a quote (2+ bytes)
+template <class OnItem>
+__device__ __forceinline__ void js_array_plain_items(const uint8_t *buf, uint32_t vs, uint32_t ve, OnItem on_item) {
     const uint4 *gb = reinterpret_cast<const uint4 *>(buf);
-    uint32_t depth = 0, nrow = 0, nb = 0;
+    uint32_t depth = 0;
     bool in_str = false;
     uint32_t fnw = 0xffffffffu, lnw = 0;  // the current item's first / last non-blank byte
     bool fq = false, lq = false;          // ... are quotes
     auto item_end = [&]() {
-        if (fnw != 0xffffffffu) {
-            uint32_t len = lnw - fnw + 1u;
-            if (fq && lq && len >= 2u) len = len == 2u ? 0u : len - 2u;
-            if (len) { ++nrow; nb += len + 1u; }
-        }
+        if (fnw != 0xffffffffu) on_item(fnw, lnw + 1u, fq && lq && lnw > fnw);
         fnw = 0xffffffffu;
     };
     auto content = [&](uint32_t pos, bool q) {  // a non-blank byte of the current item
@@ -347,7 +345,6 @@ __device__ __forceinline__ void js_count_array_plain(const uint8_t *buf, uint32_
             if (seg) {
                 content(b0 + (uint32_t)__builtin_ctz(seg), false);
                 lnw = b0 + 31u - (uint32_t)__builtin_clz(seg);
-                lq = false;
             }
             from = j + 1u;
             const uint32_t bit = 1u << j, pos = b0 + j;
@@ -371,11 +368,34 @@ __device__ __forceinline__ void js_count_array_plain(const uint8_t *buf, uint32_
         if (seg) {
             content(b0 + (uint32_t)__builtin_ctz(seg), false);
             lnw = b0 + 31u - (uint32_t)__builtin_clz(seg);
-            lq = false;
         }
     }
+}
+
+// js_value's (rows, bytes) for such an array: an item "..." of 2+ bytes gives its text
+// between the quotes (none when empty), any other item its raw text
+__device__ __forceinline__ void js_count_array_plain(const uint8_t *buf, uint32_t vs, uint32_t ve, uint32_t *rows,
+                                                     uint32_t *bytes) {
+    uint32_t nrow = 0, nb = 0;
+    js_array_plain_items(buf, vs, ve, [&](uint32_t a, uint32_t b, bool q) {
+        const uint32_t len = q ? b - a - 2u : b - a;
+        if (len) { ++nrow; nb += len + 1u; }
+    });
     *rows = nrow;
     *bytes = nb;
+}
+
+// no backslash in [vs, ve) (16-byte steps)
+__device__ __forceinline__ bool js_no_backslash(const uint8_t *buf, uint32_t vs, uint32_t ve) {
+    const uint4 *gb = reinterpret_cast<const uint4 *>(buf);
+    for (uint32_t b0 = vs & ~15u; b0 < ve; b0 += 16u) {
+        const uint4 v = gb[b0 >> 4];
+        const uint32_t m = js_swar_eq(v.x, 0x5c5c5c5cu) | (js_swar_eq(v.y, 0x5c5c5c5cu) << 4) |
+                           (js_swar_eq(v.z, 0x5c5c5c5cu) << 8) | (js_swar_eq(v.w, 0x5c5c5c5cu) << 12);
+        const uint32_t lo = vs > b0 ? vs - b0 : 0u, hi = ve - b0 < 16u ? ve - b0 : 16u;
+        if (m & ((1u << hi) - 1u) & ~((1u << lo) - 1u)) return false;
+    }
+    return true;
 }
 
 // Compares a decoded key stream with one requested key.
@@ -646,7 +666,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
             // window, or the output at the wave's range start
             JsWriteLds w{staged ? s_win[wid] : out + wb, row_rec, row_key, (uint32_t)((off >> 32) - wb), (uint32_t)off,
                          i / nkeys, i % nkeys};
-            js_value(buf, d.x, d.y, w);
+            if (buf[d.x] == '[' && js_no_backslash(buf, d.x, d.y)) {
+                // an array whose strings decode to themselves: items from the 16-byte walk
+                js_array_plain_items(buf, d.x, d.y, [&](uint32_t a, uint32_t b, bool q) {
+                    if (q) {
+                        if (b - a == 2u) return;
+                        ++a;
+                        --b;
+                    }
+                    for (uint32_t q = a; q < b; ++q) w(buf[q]);
+                    w.end();
+                });
+            } else {
+                js_value(buf, d.x, d.y, w);
+            }
         }
     }
     if (!staged) return;
