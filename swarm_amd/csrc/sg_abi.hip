@@ -323,8 +323,15 @@ static int pack_byte_splitters(const uint8_t *splitters, const uint32_t *split_o
 // inside the tile's ~100 KB of input. Replaces a radix sort of the record ids by part and one
 // gather-emit per part (random 27-B reads: C5's part_emit ran at ~1.6 TB/s).
 constexpr int PT_BLOCK = 256;
-constexpr int PT_ITEMS = 2;
+#ifndef SG_PT_ITEMS
+#define SG_PT_ITEMS 2
+#endif
+#ifndef SG_PT_IMG
+#define SG_PT_IMG 20480
+#endif
+constexpr int PT_ITEMS = SG_PT_ITEMS;
 constexpr uint32_t PT_TILE = PT_BLOCK * PT_ITEMS;
+constexpr uint32_t PT_IMG = SG_PT_IMG;  // LDS image of a tile's output (records of <= ~38 B on average)
 
 // bytes (record + '\n') per (part, tile), part-major: cnt[q * ntiles + t]
 // Optional span output of k_part_apply (sp null: none): rpre = exclusive prefix of the
@@ -381,30 +388,51 @@ struct U32AsU64P {
 // piece start in the output (null: a single buffer, parts back to back from offset 0).
 __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                                           const uint8_t *__restrict__ part, uint32_t R, uint32_t ntiles,
-                                                          const uint64_t *__restrict__ pre,
+                                                          uint32_t nparts, const uint64_t *__restrict__ pre,
                                                           const uint64_t *__restrict__ pbase, uint8_t *__restrict__ out,
                                                           const PartSpansOut so) {
     constexpr int NW = PT_BLOCK / 64;
-    __shared__ uint32_t s_wh[NW][256];
     __shared__ uint32_t s_dstart[256];
     __shared__ uint64_t s_dst[256];
-    __shared__ uint64_t s_g0[256], s_pst[256];
+    __shared__ uint64_t s_g0[256];
+    __shared__ uint32_t s_rel0[256];  // span of sorted position q inside its part: s_rel0[part] + s_off[q]
     __shared__ uint32_t s_red[NW];
     __shared__ uint2 s_sp[PT_TILE];
     __shared__ uint32_t s_off[PT_TILE];
     __shared__ uint8_t s_pq[PT_TILE];  // part of each sorted position
+    // the tile's output, part runs aligned as in `out`; before it is written, the ranking's
+    // per-wave part counters (LDS per block decides the resident tiles per CU)
+    __shared__ __attribute__((aligned(16))) uint8_t s_img[PT_IMG > NW * 1024 ? PT_IMG : NW * 1024];
+    uint32_t(*s_wh)[256] = reinterpret_cast<uint32_t(*)[256]>(s_img);
+    __shared__ uint32_t s_lp[256], s_le[256];  // image offset - tile offset of part p's run; its image end
+    __shared__ uint32_t s_red2[NW];
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
     for (int x = tid; x < NW * 256; x += PT_BLOCK) (&s_wh[0][0])[x] = 0;
-    __syncthreads();
     const uint32_t tile = blockIdx.x, tbase = tile * PT_TILE;
     const uint32_t wbase = tbase + wid * (PT_ITEMS * 64);
     const uint64_t lt = (1ull << lane) - 1ull;
+    // The tile's loads that need no ranking are issued here, before it: the per-part offsets
+    // (thread p: part p) and each item's span (round 5 before: each behind a block phase).
+    uint64_t p_pre = 0, p_pre0 = 0, p_pb = 0, p_r = 0, p_r0 = 0, p_rb = 0, p_ps = 0;
+    if ((uint32_t)tid < nparts) {
+        p_pre = pre[(size_t)tid * ntiles + tile];
+        if (pbase) { p_pre0 = pre[(size_t)tid * ntiles]; p_pb = pbase[tid]; }
+        if (so.sp) {
+            p_r = so.rpre[(size_t)tid * ntiles + tile];
+            p_r0 = so.rpre[(size_t)tid * ntiles];
+            p_rb = so.rbase[tid];
+            p_ps = so.pstart[tid];
+        }
+    }
     uint32_t d[PT_ITEMS], r[PT_ITEMS];
+    uint2 sp[PT_ITEMS];
 #pragma unroll
     for (int i = 0; i < PT_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane;
         d[i] = pos < R ? (uint32_t)part[pos] : 0u;
+        sp[i] = pos < R ? spans[pos] : make_uint2(0u, 0u);
     }
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < PT_ITEMS; ++i) {
         const bool valid = (wbase + i * 64 + lane) < R;
@@ -428,13 +456,14 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     s_dstart[tid] = dstart;
     s_dst[tid] = 0;
     __syncthreads();
+    uint32_t qi[PT_ITEMS];
 #pragma unroll
     for (int i = 0; i < PT_ITEMS; ++i) {
         const uint32_t pos = wbase + i * 64 + lane;
+        qi[i] = s_dstart[d[i]] + s_wh[wid][d[i]] + r[i];
         if (pos < R) {
-            const uint32_t q = s_dstart[d[i]] + s_wh[wid][d[i]] + r[i];
-            s_sp[q] = spans[pos];
-            s_pq[q] = (uint8_t)d[i];
+            s_sp[qi[i]] = sp[i];
+            s_pq[qi[i]] = (uint8_t)d[i];
         }
     }
     __syncthreads();
@@ -454,36 +483,83 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     __syncthreads();
     // destination of each part's run: its piece base + this tile's prefix inside the part,
     // minus the tile-local byte offset where the part's run starts
-    if (tid < 256 && s_dstart[tid] < n_t && (tid == 255 || s_dstart[tid + 1] > s_dstart[tid])) {
+    const bool present = (uint32_t)tid < nparts && s_dstart[tid] < n_t && (tid == 255 || s_dstart[tid + 1] > s_dstart[tid]);
+    uint32_t npresent;
+    const uint32_t prank = block_excl_scan<PT_BLOCK>(present ? 1u : 0u, &npresent, s_red2);
+    // the tile's output assembled in LDS when it fits: part p's run at image offset l_p with
+    // l_p = its global address mod 16 (runs in part order, at most 15 bytes apart)
+    const bool use_img = btot + 16u * npresent <= PT_IMG;  // block-uniform
+    if (present) {
         // pbase null: one buffer, parts in part order (pre is already the global offset)
-        const uint64_t pt = pre[(size_t)tid * ntiles + tile] - (pbase ? pre[(size_t)tid * ntiles] : 0ull);
-        s_dst[tid] = (pbase ? pbase[tid] : 0ull) + pt - s_off[s_dstart[tid]];
+        const uint32_t o_s = s_off[s_dstart[tid]];
+        const uint32_t e = tid == 255 ? n_t : s_dstart[tid + 1];
+        const uint32_t o_e = e < n_t ? s_off[e] : btot;
+        const uint64_t g = p_pb + (p_pre - p_pre0);  // the run's first byte in out
+        s_dst[tid] = g - o_s;
+        const uint32_t S = o_s + 16u * prank;
+        const uint32_t l = S + (((uint32_t)((uintptr_t)out + g) - S) & 15u);
+        s_lp[tid] = l - o_s;
+        s_le[tid] = l + (o_e - o_s);
         if (so.sp) {  // record index of sorted position q = s_g0[part] + q; span base = part start
-            s_g0[tid] = so.rbase[tid] + (so.rpre[(size_t)tid * ntiles + tile] - so.rpre[(size_t)tid * ntiles]) -
-                        s_dstart[tid];
-            s_pst[tid] = so.pstart[tid];
+            s_g0[tid] = p_rb + (p_r - p_r0) - s_dstart[tid];
+            s_rel0[tid] = (uint32_t)(s_dst[tid] - p_ps);
         }
     }
     __syncthreads();
-    // copy: sorted position q by lane q (consecutive lanes, consecutive bytes of one part);
-    // the part of sorted position q recorded when it was ranked (round 5: a binary search over
-    // the 256 part starts, 8 dependent LDS reads per record)
-    auto finish = [&](uint32_t q, uint32_t lo, uint2 x, uint64_t dst, uint64_t k0) {
+    auto finish = [&](uint32_t q, uint32_t lo, uint2 x, uint64_t k0) {
         if (so.sp) {  // also the record's span inside its part and its key, at its index in the parts
             const uint64_t g = s_g0[lo] + q;
-            const uint32_t rel = (uint32_t)(dst - s_pst[lo]);
+            const uint32_t rel = s_rel0[lo] + s_off[q];
             so.sp[g] = make_uint2(rel, rel + (x.y - x.x));
             so.keys[g] = k0;
         }
     };
+    if (!use_img) {  // long records: each lane stores its own record
+        for (uint32_t q = tid; q < n_t; q += PT_BLOCK) {
+            const uint32_t lo = s_pq[q];
+            const uint2 x = s_sp[q];
+            const uint64_t dst = s_dst[lo] + s_off[q];
+            uint64_t k0 = 0;
+            if (so.sp) put_medium<true, true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
+            else put_medium<false, true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
+            finish(q, lo, x, k0);
+        }
+        return;
+    }
+    // Each lane places its own records in the image (LDS stores),
+    // then every 16-B chunk of a part run leaves as one aligned 16-B store, by the lane whose
+    // sorted position holds the chunk's first byte: consecutive lanes store consecutive chunks
+    // (a lane-per-record global copy issued 16/8/4-byte, 16-bit and byte stores at every
+    // record's own alignment).
+#pragma unroll
+    for (int i = 0; i < PT_ITEMS; ++i) {
+        if (wbase + i * 64 + lane >= R) continue;
+        const uint32_t q = qi[i], lo = d[i];
+        const uint2 x = sp[i];
+        const uint32_t li = s_lp[lo] + s_off[q];
+        uint64_t k0 = 0;
+        if (so.sp) put_medium<true, false>(buf, s_img, li, x.x, x.y - x.x, &k0);
+        else put_medium<false, false>(buf, s_img, li, x.x, x.y - x.x);
+        finish(q, lo, x, k0);
+    }
+    __syncthreads();
     for (uint32_t q = tid; q < n_t; q += PT_BLOCK) {
         const uint32_t lo = s_pq[q];
         const uint2 x = s_sp[q];
-        const uint64_t dst = s_dst[lo] + s_off[q];
-        uint64_t k0 = 0;
-        if (so.sp) put_medium<true, true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
-        else put_medium<false, true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
-        finish(q, lo, x, dst, k0);
+        const uint32_t li = s_lp[lo] + s_off[q], le = li + (x.y - x.x) + 1u;  // the record's image bytes
+        const uint32_t pe = s_le[lo];                                          // its run's image end
+        uint8_t *g = out + (s_dst[lo] - s_lp[lo]);                             // image offset b -> g + b
+        if (q == s_dstart[lo] && (li & 15u)) {  // the run's unaligned head
+            const uint32_t he = min((li + 15u) & ~15u, pe);
+            for (uint32_t b = li; b < he; ++b) g[b] = s_img[b];
+        }
+        for (uint32_t b = (li + 15u) & ~15u; b < le; b += 16u) {
+            if (b + 16u <= pe) {
+                *reinterpret_cast<uint4 *>(g + b) = *reinterpret_cast<const uint4 *>(s_img + b);
+            } else {  // the run's tail (its chunk is shared with the next tile's run)
+                for (uint32_t k = b; k < pe; ++k) g[k] = s_img[k];
+            }
+        }
     }
 }
 
@@ -593,7 +669,7 @@ int dev_partition(sg_ctx *c, const uint8_t *d_buf, uint64_t n, uint32_t parts, u
         SG_TRY(tile_scan(c, tp, nt, tp + nt, tp + 2 * (size_t)nt));
         SG_LAUNCH(c, "scan.apply", k_scan64_apply<U32AsU64P>, nt, SCAN_BLOCK, 0, U32AsU64P{pcnt}, (uint32_t)nflat, tp + nt, ppre);
         SG_LAUNCH_B(c, "part_emit", 16.0 * R + 2.0 * (double)n, k_part_apply, ntiles, PT_BLOCK, 0, d_buf, L.spans, keys, R,
-                    ntiles, ppre, (const uint64_t *)nullptr, d_out, PartSpansOut{});
+                    ntiles, parts, ppre, (const uint64_t *)nullptr, d_out, PartSpansOut{});
     }
     uint64_t h[2 * 256];
     SG_TRY(ctx_readback(c, h, cnt, 2 * parts * 8));
@@ -958,7 +1034,7 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
         if (want_sp) so = PartSpansOut{rpre_all + poff[j], d_rb + j * n_parts, d_pstart, d_sp, d_k};
         // model: span + part read, the record's bytes read and written (+ span and key out)
         SG_LAUNCH_B(c, "part_emit", (want_sp ? 25.0 : 9.0) * Rj[j] + 2.0 * (double)lens[j], k_part_apply, ptn[j],
-                    PT_BLOCK, 0, pb_in[j], keep_sp + roff[j], keep_k + roff[j], Rj[j], ptn[j], ppre_all + poff[j],
+                    PT_BLOCK, 0, pb_in[j], keep_sp + roff[j], keep_k + roff[j], Rj[j], ptn[j], n_parts, ppre_all + poff[j],
                     d_pb + j * n_parts, d_out, so);
     }
     return SG_OK;
