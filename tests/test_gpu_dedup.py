@@ -692,3 +692,37 @@ def test_prefix_key_speculation_sequence(sg):
             assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("segall", ["2", "0"])
+def test_segment_ranks_every_group_size(sg, monkeypatch, segall):
+    """Segments of every size 1..64 (the 16-lane, the paired 32-lane and the whole-wave
+    rankers), their members differing in chunk 0, 1, 2, 3 or past the fourth chunk (byte
+    compares), some records ending inside a chunk, with duplicates, against the oracle."""
+    import torch
+    monkeypatch.setenv("SG_SEG_ALL", segall)
+    rng = np.random.default_rng(53)
+    alpha = np.frombuffer(b"0123456789abcdefghij:.-", dtype=np.uint8)
+    recs = []
+    for g in range(1, 65):
+        for rep in range(3):
+            head = b"g%02dr%d-" % (g, rep)  # 7 bytes: the segment's key0
+            mid = bytes(alpha[rng.integers(0, len(alpha), size=int(rng.choice([0, 5, 12, 19, 26, 33])))])
+            distinct = max(1, g // int(rng.choice([1, 2, 4])))
+            tails = [bytes(alpha[rng.integers(0, len(alpha), size=int(rng.integers(0, 9)))]) for _ in range(distinct)]
+            members = [head + mid + tails[int(rng.integers(0, distinct))] for _ in range(g)]
+            recs += members
+    rng.shuffle(recs)
+    cur = b"\n".join(recs) + b"\n"
+    prior = S.dedup(b"\n".join(recs[::7]) + b"\n")
+    dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+    dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+    ctx = sg.Context(0, torch.cuda.current_stream().cuda_stream)
+    try:
+        for _ in range(2):
+            r = ctx.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+            eu, ef = S.dedup_diff(cur, prior)
+            assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
+            assert ctx.to_bytes(r.fresh, r.fresh_bytes) == ef
+    finally:
+        ctx.close()
