@@ -327,7 +327,7 @@ constexpr int PT_BLOCK = 256;
 #define SG_PT_ITEMS 2
 #endif
 #ifndef SG_PT_IMG
-#define SG_PT_IMG 20480
+#define SG_PT_IMG 19456
 #endif
 constexpr int PT_ITEMS = SG_PT_ITEMS;
 constexpr uint32_t PT_TILE = PT_BLOCK * PT_ITEMS;
@@ -384,6 +384,19 @@ struct U32AsU64P {
     __device__ uint64_t operator()(uint32_t i) const { return v[i]; }
 };
 
+// Bytes [lo, hi) of the 16-B aligned chunk at p, from v: whole dwords as dword stores, the
+// partial ones as byte + 16-bit stores (a byte loop issued up to 15 byte stores).
+__device__ __forceinline__ void put_chunk_part(uint8_t *p, const uint4 &v, uint32_t lo, uint32_t hi) {
+    const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t a = max(lo, 4u * k), e = min(hi, 4u * k + 4u);
+        if (a >= e) continue;
+        if (a == 4u * k && e == 4u * k + 4u) *reinterpret_cast<uint32_t *>(p + 4u * k) = dw[k];
+        else put_edge(p + 4u * k, dw[k], a - 4u * k, e - 4u * k);
+    }
+}
+
 // pre: exclusive prefix of cnt (flat, part-major); pbase[q]: where part q's bytes of this
 // piece start in the output (null: a single buffer, parts back to back from offset 0).
 __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
@@ -406,6 +419,7 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     uint32_t(*s_wh)[256] = reinterpret_cast<uint32_t(*)[256]>(s_img);
     __shared__ uint32_t s_lp[256], s_le[256];  // image offset - tile offset of part p's run; its image end
     __shared__ uint32_t s_red2[NW];
+    __shared__ uint64_t s_k0[PT_TILE];  // key0 of each sorted position (written out in sorted order)
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
     for (int x = tid; x < NW * 256; x += PT_BLOCK) (&s_wh[0][0])[x] = 0;
     const uint32_t tile = blockIdx.x, tbase = tile * PT_TILE;
@@ -526,11 +540,11 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         }
         return;
     }
-    // Each lane places its own records in the image (LDS stores),
-    // then every 16-B chunk of a part run leaves as one aligned 16-B store, by the lane whose
-    // sorted position holds the chunk's first byte: consecutive lanes store consecutive chunks
-    // (a lane-per-record global copy issued 16/8/4-byte, 16-bit and byte stores at every
-    // record's own alignment).
+    // Each lane places its own records in the image (LDS stores), then every 16-B chunk of a
+    // part run leaves as one aligned 16-B store, by the lane whose sorted position holds the
+    // chunk's first byte: consecutive lanes store consecutive chunks (a lane-per-record global
+    // copy issued 16/8/4-byte, 16-bit and byte stores at every record's own alignment). The
+    // spans and keys leave in sorted order too (consecutive lanes, consecutive slots).
 #pragma unroll
     for (int i = 0; i < PT_ITEMS; ++i) {
         if (wbase + i * 64 + lane >= R) continue;
@@ -540,7 +554,7 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         uint64_t k0 = 0;
         if (so.sp) put_medium<true, false>(buf, s_img, li, x.x, x.y - x.x, &k0);
         else put_medium<false, false>(buf, s_img, li, x.x, x.y - x.x);
-        finish(q, lo, x, k0);
+        if (so.sp) s_k0[q] = k0;
     }
     __syncthreads();
     for (uint32_t q = tid; q < n_t; q += PT_BLOCK) {
@@ -549,16 +563,20 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         const uint32_t li = s_lp[lo] + s_off[q], le = li + (x.y - x.x) + 1u;  // the record's image bytes
         const uint32_t pe = s_le[lo];                                          // its run's image end
         uint8_t *g = out + (s_dst[lo] - s_lp[lo]);                             // image offset b -> g + b
+        if (so.sp) {  // the record's span inside its part and its key, at its index in the parts
+            const uint64_t gi = s_g0[lo] + q;
+            const uint32_t rel = s_rel0[lo] + s_off[q];
+            so.sp[gi] = make_uint2(rel, rel + (x.y - x.x));
+            so.keys[gi] = s_k0[q];
+        }
         if (q == s_dstart[lo] && (li & 15u)) {  // the run's unaligned head
-            const uint32_t he = min((li + 15u) & ~15u, pe);
-            for (uint32_t b = li; b < he; ++b) g[b] = s_img[b];
+            const uint32_t hb = li & ~15u;
+            put_chunk_part(g + hb, *reinterpret_cast<const uint4 *>(s_img + hb), li - hb, min(16u, pe - hb));
         }
         for (uint32_t b = (li + 15u) & ~15u; b < le; b += 16u) {
-            if (b + 16u <= pe) {
-                *reinterpret_cast<uint4 *>(g + b) = *reinterpret_cast<const uint4 *>(s_img + b);
-            } else {  // the run's tail (its chunk is shared with the next tile's run)
-                for (uint32_t k = b; k < pe; ++k) g[k] = s_img[k];
-            }
+            const uint4 v = *reinterpret_cast<const uint4 *>(s_img + b);
+            if (b + 16u <= pe) *reinterpret_cast<uint4 *>(g + b) = v;
+            else put_chunk_part(g + b, v, 0u, pe - b);  // the run's tail (the next tile's run shares the chunk)
         }
     }
 }
