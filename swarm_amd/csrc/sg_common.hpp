@@ -200,13 +200,42 @@ constexpr uint64_t MAX_BYTES = 0xFFFF0000ull;  // 32-bit record offsets with hea
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 template <class T>
-__device__ __forceinline__ T wave_incl_scan(T v) {
+__device__ __forceinline__ T wave_incl_scan_shfl(T v) {
     const int lane = lane_id();
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         T t = __shfl_up(v, o, 64);
         if (lane >= o) v += t;
     }
+    return v;
+}
+
+// DPP move of a 32- or 64-bit value (lanes without a source, and rows outside RM, read 0).
+template <int CTRL, int RM, class T>
+__device__ __forceinline__ T dpp_mov0(T v) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit");
+    if constexpr (sizeof(T) == 4) {
+        return (T)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, RM, 0xf, true);
+    } else {
+        const uint64_t u = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, RM, 0xf, true);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, RM, 0xf, true);
+        return (T)((uint64_t)lo | ((uint64_t)hi << 32));
+    }
+}
+
+// Inclusive wave64 scan by DPP: row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast:15
+// (rows 1, 3 add the previous row's last lane) and row_bcast:31 (rows 2, 3 add lane 31): no
+// LDS round trips (the __shfl_up form costs a ds_bpermute round trip per step). Every lane
+// of the wave must be active (block-uniform call sites); wave_incl_scan_shfl otherwise.
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+    v += dpp_mov0<0x111, 0xf>(v);
+    v += dpp_mov0<0x112, 0xf>(v);
+    v += dpp_mov0<0x114, 0xf>(v);
+    v += dpp_mov0<0x118, 0xf>(v);
+    v += dpp_mov0<0x142, 0xa>(v);
+    v += dpp_mov0<0x143, 0xc>(v);
     return v;
 }
 

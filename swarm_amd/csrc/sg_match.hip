@@ -1462,7 +1462,7 @@ __global__ __launch_bounds__(DFM_BLOCK) void k_dfa_multi(DFAMultiArgs a) {
             for (int g = 0; g < G; ++g) cnt += (uint32_t)__popcll(acc[g]);
         }
         if (__ballot(cnt != 0)) {
-            const uint32_t inc = wave_incl_scan(cnt);
+            const uint32_t inc = wave_incl_scan_shfl(cnt);
             const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(a.hit_count, tot);

@@ -381,7 +381,7 @@ __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
             const uint32_t w = w0 + lane;
             uint32_t bits = w < ntw ? tch[w] : 0u;
             if (w < ntw) res[w] = s_vac[w] & ~bits;
-            const uint32_t c = (uint32_t)__popc(bits), inc = wave_incl_scan(c);
+            const uint32_t c = (uint32_t)__popc(bits), inc = wave_incl_scan_shfl(c);
             uint32_t p = nl + inc - c;
             while (bits) {
                 list[p++] = (uint16_t)(32 * w + (uint32_t)__builtin_ctz(bits));
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256) void k_tm_rec_emit(const uint32_t *__restrict_
             const uint32_t w = w0 + lane;
             uint32_t bits = w < ntw ? G[(size_t)r * ntw + w] : 0u;
             const uint32_t c = (uint32_t)__popc(bits);
-            const uint32_t inc = wave_incl_scan(c);
+            const uint32_t inc = wave_incl_scan_shfl(c);
             uint32_t p = lp + inc - c;
             while (bits) {
                 const uint32_t t = 32 * w + (uint32_t)__builtin_ctz(bits);
