@@ -239,8 +239,28 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
     return v;
 }
 
+// Lane `lane`'s value in every lane (v_readlane: `lane` must be wave-uniform).
+template <class T>
+__device__ __forceinline__ T wave_bcast(T v, int lane) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit");
+    if constexpr (sizeof(T) == 4) {
+        return (T)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    } else {
+        const uint64_t u = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+        return (T)((uint64_t)lo | ((uint64_t)hi << 32));
+    }
+}
+
+// Wave sum in every lane: the DPP scan's last lane (every lane active; wave_sum_shfl otherwise).
 template <class T>
 __device__ __forceinline__ T wave_sum(T v) {
+    return wave_bcast(wave_incl_scan(v), 63);
+}
+
+template <class T>
+__device__ __forceinline__ T wave_sum_shfl(T v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;

@@ -64,7 +64,7 @@ __global__ __launch_bounds__(RS_HBLOCK) void k_rs_hist(const uint64_t *__restric
             for (int p = 0; p < RS_MAXPASS; ++p) {
                 if (p >= npasses) break;
                 const uint32_t d = (uint32_t)(kk >> (8 * p)) & 255u;
-                const uint32_t d0 = (uint32_t)__shfl(d, 0, 64);
+                const uint32_t d0 = wave_bcast(d, 0);
                 if (__all(!valid || d == d0)) {
                     if (lane_id() == 0 && cnt) h[wid][p][d0] += cnt;
                 } else if (valid) {
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__
 #pragma unroll
     for (int i = 0; i < RD_ITEMS; ++i) {
         const uint32_t d = dd[i];
-        const uint32_t d0 = (uint32_t)__shfl(d, 0, 64);
+        const uint32_t d0 = wave_bcast(d, 0);
         if (__all(d == d0 || d == 256u)) {
             const uint32_t cnt = (uint32_t)__popcll(__ballot(d < 256u));
             if (lane_id() == 0 && d0 < 256u) h[wid][d0] += cnt;

@@ -410,7 +410,7 @@ __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
             G[(size_t)r * ntw + w] = tr;
             tot += (uint32_t)__popc(tr);
         }
-        tot = wave_sum(tot);
+        tot = wave_sum_shfl(tot);
         if (lane == 0) rcnt[r] = tot;
         tm_wave_sync();
     }
