@@ -391,23 +391,28 @@ struct SegPred {
 };
 
 // Ranking inside a segment. Members share their first 7 bytes, so they are ordered by the
-// 7-byte chunk keys at offsets 7, 14, 21, 28 (chunk_key: big-endian bytes + tag, tag < 8
-// ends the record) held in registers, and by a byte compare from offset 35 only when all
-// four chunks tie with tag 8. dup = an equal member with a smaller index exists.
-constexpr int SEG_CH = 4;
+// 7-byte chunk keys at offsets 7, 14, 21, 28, 35 (chunk_key: big-endian bytes + tag, tag < 8
+// ends the record) held in registers, and by a byte compare from offset 42 only when all
+// five chunks tie with tag 8 (round 5: four chunks left C5's longer host:port records, 36-42
+// bytes, to byte compares inside the rank loop for every duplicate pair: segment sorts
+// 46.9 -> 39.6 ms per step with five; six were no better). dup = an equal member with a smaller index exists.
+#ifndef SG_SEG_CH
+#define SG_SEG_CH 5
+#endif
+constexpr int SEG_CH = SG_SEG_CH;
 
 struct SegKeys {
     uint64_t c[SEG_CH];
 };
 
-// The four chunk keys from one set of wide loads: the suffix's first 28 bytes in at most
-// three aligned 16-B loads (normalised), instead of up to eight scattered 8-B loads.
+// The SEG_CH chunk keys from one set of wide loads: the suffix's first 7 * SEG_CH bytes in at
+// most four aligned 16-B loads (normalised), instead of scattered 8-B loads.
 __device__ __forceinline__ SegKeys seg_keys(const uint8_t *S, uint2 x, uint32_t base) {
     SegKeys k;
     const uint32_t off = bk_off(base), len = x.y - x.x;
     const uint32_t rem = len > off ? len - off : 0u;
     uint4 c[4];
-    load_chunks(S, x.x + off, rem < 28u ? rem : 28u, c);
+    load_chunks(S, x.x + off, rem < 7u * SEG_CH ? rem : 7u * SEG_CH, c);
     uint32_t r[13];
     normalize52(c, (x.x + off) & 15u, r);
 #pragma unroll
