@@ -24,6 +24,7 @@ constexpr int LN_BLOCK = 256;
 constexpr int LN_BPT = 64;
 constexpr int LN_TILE = LN_BLOCK * LN_BPT;
 constexpr int LN_NW = LN_BPT / 4;
+constexpr uint32_t LN_CAP = 768;  // records per tile assembled in LDS (~21 B or more per record on average)
 
 __device__ __forceinline__ uint32_t nl_mask4(uint32_t x) {
     uint32_t y = x ^ 0x0a0a0a0au;
@@ -95,8 +96,9 @@ struct LinesRoute {
 template <bool ROUTE>
 __device__ __forceinline__ void lines_body(const uint8_t *__restrict__ buf, uint64_t n, const uint64_t *__restrict__ pre,
                                            uint2 *__restrict__ spans, uint64_t *__restrict__ keys, const LinesRoute &rt) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_b[LN_TILE + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t s_b[LN_TILE + 16];  // then the tile's span ends
     __shared__ uint64_t s_red[LN_BLOCK / 64];
+    __shared__ uint32_t s_x[ROUTE ? 1 : LN_CAP];  // the tile's span starts
     __shared__ uint64_t s_k0[ROUTE ? 256 : 1];
     const uint32_t t = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * LN_TILE;
@@ -121,15 +123,26 @@ __device__ __forceinline__ void lines_body(const uint8_t *__restrict__ buf, uint
     const uint64_t packed = ((uint64_t)__popcll(sm) << 31) | (uint64_t)__popcll(em);
     uint64_t total;
     const uint64_t excl = block_excl_scan<LN_BLOCK>(packed, &total, s_red);  // includes barriers
-    const uint64_t p0 = pre[blockIdx.x] + excl;
+    const uint64_t tpre = pre[blockIdx.x];
+    const uint64_t p0 = tpre + excl;
     uint32_t si = (uint32_t)(p0 >> 31);
     uint32_t ei = (uint32_t)(p0 & 0x7fffffffu);
+    // The tile's spans are assembled in LDS and leave as whole 8-B stores in record order
+    // (each record's start and end used to be two 4-B stores from two lane loops, its end
+    // often from the next lane or block). S0/E0: the tile's first start and end index; a
+    // record started in the previous tile (E0 < S0) has its end written directly.
+    const uint32_t S0 = (uint32_t)(tpre >> 31), E0 = (uint32_t)(tpre & 0x7fffffffu);
+    const uint32_t ns = (uint32_t)(total >> 31), ne = (uint32_t)(total & 0x7fffffffu);
+    // block-uniform; dense tiles and the routing parse (its LDS is one block per CU short,
+    // and its part bytes dominate its stores) store directly
+    const bool staged = !ROUTE && ns <= LN_CAP;
 
     uint64_t bits = sm;
     while (bits) {
         const int b = __ffsll((long long)bits) - 1;
         bits &= bits - 1;
-        spans[si].x = (uint32_t)(my0 + b);
+        if (staged) s_x[si - S0] = (uint32_t)(my0 + b);
+        else spans[si].x = (uint32_t)(my0 + b);
         if (stage) {
             // bytes [q, q+8) from three aligned dwords; tag = first '\n' in them (SWAR: the
             // lowest flagged byte is exact), key = the bytes before it (<= 7), big-endian
@@ -151,12 +164,31 @@ __device__ __forceinline__ void lines_body(const uint8_t *__restrict__ buf, uint
         }
         ++si;
     }
+    if (!staged) {
+        bits = em;
+        while (bits) {
+            const int b = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            spans[ei].y = (uint32_t)(my0 + b);
+            ++ei;
+        }
+        return;
+    }
+    __syncthreads();  // s_b (the tile's bytes) is read by the start loop's keys: free after this
+    uint32_t *s_y = reinterpret_cast<uint32_t *>(s_b);
     bits = em;
     while (bits) {
         const int b = __ffsll((long long)bits) - 1;
         bits &= bits - 1;
-        spans[ei].y = (uint32_t)(my0 + b);
+        if (ei >= S0) s_y[ei - S0] = (uint32_t)(my0 + b);
+        else spans[ei].y = (uint32_t)(my0 + b);  // the record the previous tile started
         ++ei;
+    }
+    __syncthreads();
+    const uint32_t ended = E0 + ne - S0;  // records [0, ended) of this tile's starts end in it
+    for (uint32_t i = t; i < ns; i += LN_BLOCK) {
+        if (i < ended) spans[S0 + i] = make_uint2(s_x[i], s_y[i]);
+        else spans[S0 + i].x = s_x[i];  // ends in the next tile (which writes .y)
     }
 }
 
