@@ -99,6 +99,7 @@ __device__ __forceinline__ void lines_body(const uint8_t *__restrict__ buf, uint
     __shared__ __attribute__((aligned(16))) uint8_t s_b[LN_TILE + 16];  // then the tile's span ends
     __shared__ uint64_t s_red[LN_BLOCK / 64];
     __shared__ uint32_t s_x[ROUTE ? 1 : LN_CAP];  // the tile's span starts
+    __shared__ uint64_t s_kk[ROUTE ? 1 : LN_CAP];  // and their keys
     __shared__ uint64_t s_k0[ROUTE ? 256 : 1];
     const uint32_t t = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * LN_TILE;
@@ -127,7 +128,7 @@ __device__ __forceinline__ void lines_body(const uint8_t *__restrict__ buf, uint
     const uint64_t p0 = tpre + excl;
     uint32_t si = (uint32_t)(p0 >> 31);
     uint32_t ei = (uint32_t)(p0 & 0x7fffffffu);
-    // The tile's spans are assembled in LDS and leave as whole 8-B stores in record order
+    // The tile's spans and keys are assembled in LDS and leave as whole 8-B stores in record order
     // (each record's start and end used to be two 4-B stores from two lane loops, its end
     // often from the next lane or block). S0/E0: the tile's first start and end index; a
     // record started in the previous tile (E0 < S0) has its end written directly.
@@ -157,7 +158,8 @@ __device__ __forceinline__ void lines_body(const uint8_t *__restrict__ buf, uint
             const uint32_t take = rem < 7u ? rem : 7u;
             const uint64_t m = (1ull << (8u * take)) - 1ull;
             const uint64_t k0 = (__builtin_bswap64(v & m) & ~0xffull) | rem;
-            if (keys) keys[si] = k0;
+            if (keys && staged) s_kk[si - S0] = k0;
+            else if (keys) keys[si] = k0;
             if constexpr (ROUTE)
                 rt.parts[si] = (uint8_t)route_record(buf, n, (uint32_t)(my0 + b), ~0u, k0, s_k0, rt.ns, rt.split_w,
                                                      rt.split_len);
@@ -189,6 +191,7 @@ __device__ __forceinline__ void lines_body(const uint8_t *__restrict__ buf, uint
     for (uint32_t i = t; i < ns; i += LN_BLOCK) {
         if (i < ended) spans[S0 + i] = make_uint2(s_x[i], s_y[i]);
         else spans[S0 + i].x = s_x[i];  // ends in the next tile (which writes .y)
+        if (keys) keys[S0 + i] = s_kk[i];
     }
 }
 
