@@ -447,7 +447,14 @@ __device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2
 // members differ (chunks before it are equal for all of them: a host's records share their
 // name), and the next; past those two the bytes are compared in the input (rare: the records
 // still tie there). Equivalent to seg_cmp: equal leading chunks with a full tag decide nothing.
-template <int G>
+// The rank loop's byte compare past the chunk keys (members tying there: long records, X1's
+// httpx lines): wide loads, 48 bytes per round trip (8-B steps before: X1 seg_small 0.128 ->
+// 0.098 ms).
+// WIDE only for long records: its code in the loop costs the short-record launches occupancy
+// (C5 seg_wave 23.9 -> 27.9 ms with it).
+#define SEG_BYTES_CMP(S_, x_, y_, o_)                                                              \
+    (WIDE ? rec_cmp_w(S_, x_.x, x_.y, S_, y_.x, y_.y, o_) : rec_cmp8(S_, x_.x, x_.y - x_.x, y_.x, y_.y - y_.x, o_))
+template <int G, bool WIDE>
 __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                uint8_t *__restrict__ dup, uint32_t a, uint32_t k, uint32_t gl,
                                                uint32_t gbase, bool live, uint32_t base) {
@@ -484,13 +491,13 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
         const uint2 y = make_uint2((uint32_t)__shfl(x.x, src, 64), (uint32_t)__shfl(x.y, src, 64));
         if (act && j < kk && j != gl) {
             int c;
-            if (st >= SEG_CH) c = rec_cmp8(S, x.x, x.y - x.x, y.x, y.y - y.x, boff);
+            if (st >= SEG_CH) c = SEG_BYTES_CMP(S, x, y, boff);
             else if (m1 != o1) c = m1 < o1 ? -1 : 1;
             else if ((m1 & 0xffu) < 8u) c = 0;
-            else if (st + 1u >= SEG_CH) c = rec_cmp8(S, x.x, x.y - x.x, y.x, y.y - y.x, boff);
+            else if (st + 1u >= SEG_CH) c = SEG_BYTES_CMP(S, x, y, boff);
             else if (m2 != o2) c = m2 < o2 ? -1 : 1;
             else if ((m2 & 0xffu) < 8u) c = 0;
-            else c = rec_cmp8(S, x.x, x.y - x.x, y.x, y.y - y.x, boff);
+            else c = SEG_BYTES_CMP(S, x, y, boff);
             if (c > 0 || (c == 0 && j < gl)) ++rank;
             if (c == 0 && j < gl) d = true;
         }
@@ -502,6 +509,7 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
 }
 
 // 16 lanes per small segment (<= SEG_SMALL members).
+template <bool WIDE>
 __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                    const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
                                                    const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n,
@@ -514,12 +522,13 @@ __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S
     const bool eb = !live || pe >= n || gl == 15u || brk[pe];
     const uint32_t me = (uint32_t)(__ballot(eb) >> gbase) & 0xffffu;
     const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);  // members: a .. a+k-1
-    seg_rank_group<16>(S, SS, dup, a, k, gl, gbase, live, base);
+    seg_rank_group<16, WIDE>(S, SS, dup, a, k, gl, gbase, live, base);
 }
 
 // Larger segments (17..64 members), two heads per wave: two half-waves when both segments
 // hold <= 32 members (the common case: a host's few ports x a few copies), else one
 // segment after the other on the whole wave.
+template <bool WIDE>
 __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                   const uint8_t *__restrict__ brk, uint8_t *__restrict__ dup,
                                                   const uint32_t *__restrict__ heads, uint32_t nh, uint32_t n,
@@ -539,11 +548,11 @@ __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S,
     }
     if (k[0] <= 32u && k[1] <= 32u) {
         const uint32_t t = lane >> 5;
-        seg_rank_group<32>(S, SS, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u, (t ? k[1] : k[0]) > 0,
+        seg_rank_group<32, WIDE>(S, SS, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u, (t ? k[1] : k[0]) > 0,
                            base);
     } else {
-        seg_rank_group<64>(S, SS, dup, a[0], k[0], lane, 0u, true, base);
-        if (k[1]) seg_rank_group<64>(S, SS, dup, a[1], k[1], lane, 0u, true, base);
+        seg_rank_group<64, WIDE>(S, SS, dup, a[0], k[0], lane, 0u, true, base);
+        if (k[1]) seg_rank_group<64, WIDE>(S, SS, dup, a[1], k[1], lane, 0u, true, base);
     }
 }
 
@@ -1379,8 +1388,18 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         err = reinterpret_cast<uint32_t *>(etp + 2 * (size_t)ent + 1);
     }
     if (nb) SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
-    if (ns) SG_LAUNCH(c, "seg_small", k_seg_small, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
-    if (nb) SG_LAUNCH(c, "seg_wave", k_seg_wave, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
+    // long records (mean >= 48 B: httpx lines) compare their tails with wide loads
+    const bool wide_cmp = n >= 48ull * R;
+    if (ns) {
+        if (wide_cmp) SG_LAUNCH(c, "seg_small", k_seg_small<true>, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
+        else SG_LAUNCH(c, "seg_small", k_seg_small<false>, grid_for(ns, 16), 256, 0, Sb, SS, brk, dup, hs, ns, R, base);
+    }
+    if (nb) {
+        if (wide_cmp)
+            SG_LAUNCH(c, "seg_wave", k_seg_wave<true>, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
+        else
+            SG_LAUNCH(c, "seg_wave", k_seg_wave<false>, grid_for((nb + 1) / 2, 4), 256, 0, Sb, SS, brk, dup, hb, nb, R, err, base);
+    }
     if (c->profile && c->prof_only.empty() && (ns || nb)) {  // full-profile steps only
         // byte model: per member its span read + written, ~4 chunk keys of record bytes, flag
         unsigned long long *mc;

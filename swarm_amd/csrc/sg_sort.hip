@@ -417,8 +417,10 @@ __device__ __forceinline__ uint32_t ls_head(const uint64_t *__restrict__ K, uint
 // bounds[t] = head(t * LS_T) | real << 31, t = 0 .. ntiles (one wave per boundary): the group
 // search runs as its own launch, many waves in flight, instead of at the head of every
 // local-sort block.
+// (err: the local sort's overflow word, zeroed here instead of by a memset launch)
 __global__ __launch_bounds__(256) void k_rs_lbounds(const uint64_t *__restrict__ K, uint32_t n, uint64_t gmask,
-                                                    uint32_t nb, uint32_t *__restrict__ bounds) {
+                                                    uint32_t nb, uint32_t *__restrict__ bounds, uint32_t *__restrict__ err) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *err = 0u;
     const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= nb) return;
     uint32_t real;
@@ -849,11 +851,10 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
         if (hp.on) {
             uint32_t *err = err_at;
             if (!err) SG_TRY(slot(c, S_LS_ERR, 1, &err));
-            SG_HIP(hipMemsetAsync(err, 0, 4, c->stream));
             const uint32_t g = (n + LS_T - 1) / LS_T;
             uint32_t *bounds;
             SG_TRY(slot(c, S_LS_BOUNDS, (size_t)g + 1, &bounds));
-            SG_LAUNCH(c, "rs_lbounds", k_rs_lbounds, (g + 1 + 3) / 4, 256, 0, ck, n, hp.gmask, g + 1, bounds);
+            SG_LAUNCH(c, "rs_lbounds", k_rs_lbounds, (g + 1 + 3) / 4, 256, 0, ck, n, hp.gmask, g + 1, bounds, err);
             // model: key read, key + span fetched in sorted order, both written
             SG_LAUNCH_B(c, "rs_lsort", 40.0 * n, k_rs_lsort, g, LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask, hp.lpos, hp.nloc,
                         bounds, err);
