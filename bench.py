@@ -40,7 +40,7 @@ KERNEL_SYMBOL = {"rs_pass": "k_rs_down", "emit_sorted": "k_emit_sorted", "emit_u
                  "emit_fresh": "k_emit_fresh", "diff_tile": "k_diff_tile", "adjacent": ("k_adjacent2", "k_adjacent"),
                  "rs_lsort": "k_rs_lsort", "rs_lbounds": "k_rs_lbounds", "seg_heads": "k_sel_count",
                  "lines": "k_lines", "lit_match": "k_lit_scan", "dfa_match": "k_dfa_match", "ac_match": "k_ac_match",
-                 "re_prefilter": "k_lit_scan", "re_verify": "k_verify", "json_scan": "k_json_scan",
+                 "re_prefilter": "k_lit_scan", "re_verify": "k_verify", "json_scan": ("k_json_scan_t", "k_json_scan"),
                  "json_emit": "k_json_emit", "tm_eval": "k_tm_eval", "tm_collect": "k_tm_collect",
                  "bk_sort": "k_bk_sort", "bk_l1_apply": "k_bp_apply", "bk_l2_apply": "k_bp_apply",
                  "bk_l1_count": "k_bp_count", "bk_l2_count": "k_bp_count", "bk_compact": "k_bk_compact",
@@ -92,6 +92,36 @@ def roofline_of(stats, kernel=None, workload=None, full=None):
     if t:
         out["traffic"] = t["bytes"]
         out["traffic_source"] = "profiles/" + t["source"] + " (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, per launch)"
+    return out
+
+
+def _exact_flags(d, out, depth=0):
+    """Every bit-exactness flag of a cpu_baseline object (and its nested GNU legs)."""
+    for k, v in (d or {}).items():
+        if isinstance(v, bool) and "exact" in k:
+            out.append(v)
+        elif isinstance(v, dict) and depth < 2:
+            _exact_flags(v, out, depth + 1)
+    return out
+
+
+def legs_summary(line):
+    """A compact per-leg digest for the end of the JSON line (the driver keeps only the line's
+    tail): ms per step, records/s, the dominant kernel's roofline fraction, its measured HBM
+    traffic over its algorithmic bytes, and whether every bit-exactness check of the leg held."""
+    out = {}
+    for name, leg in [("c2", line)] + [(k, line[k]) for k in ("fused_x1", "urls", "c1", "c3", "c4", "c5", "fields")
+                                       if isinstance(line.get(k), dict)]:
+        if "error" in leg:
+            out[name] = {"error": str(leg["error"])[:120]}
+            continue
+        rf = leg.get("roofline") or {}
+        flags = _exact_flags(leg.get("cpu_baseline"), [])
+        d = {"ms": leg.get("ms_per_step"), "value": leg.get("value"), "kernel": rf.get("kernel"),
+             "frac": rf.get("frac"), "traffic_x": None, "bit_exact": (all(flags) if flags else None)}
+        if rf.get("traffic") and rf.get("bytes_per_launch"):
+            d["traffic_x"] = round(rf["traffic"] / rf["bytes_per_launch"], 2)
+        out[name] = d
     return out
 
 
@@ -1289,6 +1319,7 @@ def main():
         line["c4"] = sub_leg("c4", lambda: bench_c4(args, ctx=ctx, emit=False), SUB_KEYS + ("records", "error"))
         line["fields"] = sub_leg("fields", lambda: bench_fields(args, ctx=ctx, emit=False),
                                  SUB_KEYS + ("records", "error"))
+        line["legs"] = legs_summary(line)  # last: survives a truncated tail of the line
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -44,6 +44,7 @@ extern "C" {
 #define SG_E_UNSUPPORTED 6  /* regex construct outside the supported subset */
 #define SG_E_STATES 7       /* automaton exceeds its state budget */
 #define SG_E_NODEV 8        /* no HIP device */
+#define SG_E_CORRUPT 9      /* a handed-over parse does not match its bytes (sg_dev_dedup_diff_spans_into) */
 
 /* matcher flags */
 #define SG_NOCASE 1u        /* ASCII case-insensitive (nuclei `case-insensitive: true`, grep -i) */
@@ -142,11 +143,30 @@ int sg_dev_dedup_diff_into(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur, cons
                            size_t n_prior, uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh,
                            size_t fresh_cap, sg_dev_result *res);
 /* sg_dev_dedup_diff_into for a 16-byte aligned d_cur already parsed by
- * sg_dev_partition_bytes_pieces_spans (its part's n_rec spans and keys): no second parse. */
-int sg_dev_dedup_diff_spans_into(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur, const uint32_t *d_spans,
-                                 const uint64_t *d_keys, size_t n_rec, const uint8_t *d_prior, size_t n_prior,
-                                 uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap,
+ * sg_dev_partition_bytes_pieces_spans / _rounds_spans (a part's, or an exchange round's,
+ * n_rec spans and keys): no second parse. The handed-over parse is checked before any kernel
+ * reads a byte through it, in the pass that already reads every key (the common-prefix
+ * scan), and a mismatch returns SG_E_CORRUPT with nothing written:
+ *   - the records tile d_cur in order: record 0 starts at 0, record i + 1 starts right after
+ *     record i's '\n' (end + 1), every record is non-empty, the last '\n' is byte n_cur - 1
+ *     (so every span lies inside the buffer whatever arrived);
+ *   - sg_span_sum(spans, keys) == span_sum, the producer's checksum (part_sums of the
+ *     partition calls, summed over the sources of an exchange round): a changed key or length
+ *     is caught;
+ *   - every 256th record ends at a '\n' of d_cur and its key equals its own bytes' key.
+ * n_rec == 0 requires n_cur == 0 and span_sum == 0. d_spans and d_keys are consumed: the
+ * sort works in them (their contents are unspecified afterwards). */
+int sg_dev_dedup_diff_spans_into(sg_ctx *ctx, const uint8_t *d_cur, size_t n_cur, uint32_t *d_spans,
+                                 uint64_t *d_keys, size_t n_rec, uint64_t span_sum, const uint8_t *d_prior,
+                                 size_t n_prior, uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap,
                                  sg_dev_result *res);
+/* The handover checksum of n_rec records (host arrays: spans as 2 x uint32 start, end;
+ * first-chunk keys): the sum mod 2^64 over records of mix(end - start, key), with
+ *   h = (k + l * 0x9E3779B97F4A7C15) * 0xBF58476D1CE4E5B9 (mod 2^64); mix = h ^ h >> 31.
+ * Order-free, so producers sum it per tile and receivers per call. It detects transport
+ * damage (any one changed key or length; stale, truncated or shifted runs), not a deliberate
+ * exchange of two equal-length records' keys. */
+uint64_t sg_span_sum(const uint32_t *spans, const uint64_t *keys, size_t n_rec);
 
 /* Multi-GPU: route every record of d_buf to partition
  * part(hash64(record), n_parts), n_parts <= 256. Writes '\n'-terminated records grouped by
@@ -197,11 +217,15 @@ int sg_dev_partition_bytes_pieces_a16(sg_ctx *ctx, const uint8_t *const *d_piece
 /* The _a16 routing that also hands over every part's parse: *d_spans (context-owned, valid
  * until the next _spans call on ctx) holds 2 x uint32 (start, end of the record before its
  * '\n', relative to its part's start) per record and *d_keys its first-chunk sort key,
- * part p's records at [sum of part_records[< p], + part_records[p]), in part order. */
+ * part p's records at [sum of part_records[< p], + part_records[p]), in part order.
+ * part_sums (host array of n_parts, may be NULL): part p's handover checksum (sg_span_sum of
+ * its records' spans and keys), for sg_dev_dedup_diff_spans_into; computed in the copy pass,
+ * so with part_sums the call returns after that pass instead of queueing it. */
 int sg_dev_partition_bytes_pieces_spans(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens,
                                         size_t k, const uint8_t *splitters, const uint32_t *split_offs,
                                         uint32_t n_parts, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
-                                        uint64_t *part_records, const uint32_t **d_spans, const uint64_t **d_keys);
+                                        uint64_t *part_records, const uint32_t **d_spans, const uint64_t **d_keys,
+                                        uint64_t *part_sums);
 /* Range routing for a multi-GPU exchange in rounds (swarm_amd.distributed.dedup_diff_rounds_step):
  * n_parts = G x rounds byte-range parts, part q = g * rounds + p being local range p of rank g
  * (so rank g owns parts g * rounds .. g * rounds + rounds - 1, in byte order). The parts are
@@ -224,16 +248,21 @@ int sg_dev_partition_pieces_count(sg_ctx *ctx, const uint8_t *const *d_pieces, c
 /* sg_dev_partition_bytes_pieces_rounds that also hands over every record's parse, for the
  * receivers of the exchange (no second parse of the received parts): d_spans (2 x uint32 per
  * record: start, end before its '\n', relative to its part's start) and d_keys (first-chunk
- * sort key), records in the round-major part order of the bytes; capacity rec_cap records. */
+ * sort key), records in the round-major part order of the bytes; capacity rec_cap records.
+ * part_sums (host, n_parts, may be NULL): each part's handover checksum, as in
+ * sg_dev_partition_bytes_pieces_spans; it travels with the part's size and record count, and
+ * a receiver passes the sum over its sources to sg_dev_dedup_diff_spans_into. */
 int sg_dev_partition_bytes_pieces_rounds_spans(sg_ctx *ctx, const uint8_t *const *d_pieces, const size_t *lens,
                                                size_t k, const uint8_t *splitters, const uint32_t *split_offs,
                                                uint32_t n_parts, uint32_t rounds, uint8_t *d_out, size_t out_cap,
                                                uint64_t *part_bytes, uint64_t *part_records, uint32_t *d_spans,
-                                               uint64_t *d_keys, size_t rec_cap);
-/* Received spans of nseg (<= SG_REBASE_SEGS) sources made relative to the receive buffer
- * d_buf: records [seg_first[s], seg_first[s + 1]) get + seg_off[s] (host arrays). *bad = how
- * many of each source's first and last 256 records do not end right before a '\n' of d_buf
- * afterwards (0 for an intact transfer; a short or stale message is caught at its tail). */
+                                               uint64_t *d_keys, size_t rec_cap, uint64_t *part_sums);
+/* Received spans of nseg sources made relative to the receive buffer d_buf: records
+ * [seg_first[s], seg_first[s + 1]) get + seg_off[s] (host arrays, seg_first[0] == 0; one
+ * launch per SG_REBASE_SEGS sources). *bad = how many of each source's first and last 256
+ * records do not end right before a '\n' of d_buf afterwards (0 for an intact transfer; a
+ * short or stale message is caught at its tail; sg_dev_dedup_diff_spans_into then checks
+ * every record). */
 #define SG_REBASE_SEGS 64
 int sg_dev_rebase_spans(sg_ctx *ctx, const uint8_t *d_buf, size_t n, uint32_t *d_spans, size_t n_rec,
                         const uint64_t *seg_first, const uint64_t *seg_off, uint32_t nseg, uint64_t *bad);

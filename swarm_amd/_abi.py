@@ -17,10 +17,11 @@ SG_E_TOO_LARGE = 5
 SG_E_UNSUPPORTED = 6
 SG_E_STATES = 7
 SG_E_NODEV = 8
+SG_E_CORRUPT = 9
 SG_NOCASE = 1
 
 ERRNAMES = {1: "SG_E_INVAL", 2: "SG_E_CAP", 3: "SG_E_HIP", 4: "SG_E_NOMEM", 5: "SG_E_TOO_LARGE",
-            6: "SG_E_UNSUPPORTED", 7: "SG_E_STATES", 8: "SG_E_NODEV"}
+            6: "SG_E_UNSUPPORTED", 7: "SG_E_STATES", 8: "SG_E_NODEV", 9: "SG_E_CORRUPT"}
 
 EXPORTS = [
     "sg_last_error", "sg_version", "sg_device_count", "sg_ctx_create", "sg_ctx_destroy",
@@ -170,7 +171,7 @@ EXPORTS += ["sg_dev_partition_range", "sg_dev_key_sample", "sg_dev_partition_byt
             "sg_dev_partition_bytes_pieces", "sg_dev_partition_bytes_pieces_a16", "sg_dev_dedup_diff_into",
             "sg_dev_partition_bytes_pieces_spans", "sg_dev_dedup_diff_spans_into",
             "sg_dev_partition_bytes_pieces_rounds", "sg_dev_partition_pieces_count",
-            "sg_dev_partition_bytes_pieces_rounds_spans", "sg_dev_rebase_spans"]
+            "sg_dev_partition_bytes_pieces_rounds_spans", "sg_dev_rebase_spans", "sg_span_sum"]
 for _name, (_res, _args) in {
     "sg_dev_partition_pieces_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t,
                                                 C.POINTER(C.c_uint64)]),
@@ -178,7 +179,8 @@ for _name, (_res, _args) in {
                                                              C.POINTER(C.c_size_t), C.c_size_t, C.c_void_p,
                                                              C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32, C.c_void_p,
                                                              C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
-                                                             C.c_void_p, C.c_void_p, C.c_size_t]),
+                                                             C.c_void_p, C.c_void_p, C.c_size_t,
+                                                             C.POINTER(C.c_uint64)]),
     "sg_dev_rebase_spans": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32, C.POINTER(C.c_uint64)]),
     "sg_dev_partition_bytes_pieces": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t,
@@ -198,10 +200,11 @@ for _name, (_res, _args) in {
                                                       C.c_size_t, C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32,
                                                       C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64),
                                                       C.POINTER(C.c_uint64), C.POINTER(C.c_void_p),
-                                                      C.POINTER(C.c_void_p)]),
+                                                      C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     "sg_dev_dedup_diff_spans_into": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p,
-                                               C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
-                                               C.c_void_p, C.c_size_t, C.POINTER(DevResult)]),
+                                               C.c_size_t, C.c_uint64, C.c_void_p, C.c_size_t, C.c_void_p,
+                                               C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(DevResult)]),
+    "sg_span_sum": (C.c_uint64, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "sg_dev_partition_bytes": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(C.c_uint32),
                                          C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint64),
                                          C.POINTER(C.c_uint64)]),

@@ -263,6 +263,16 @@ def hash64(rec: bytes) -> int:
     return int(lib.sg_hash64(_ptr(a), a.size))
 
 
+def span_sum(spans: np.ndarray, keys: np.ndarray) -> int:
+    """The handover checksum (include/swarmgpu.h sg_span_sum) of host spans (n x 2 uint32:
+    start, end) and first-chunk keys (n uint64)."""
+    sp = np.ascontiguousarray(spans, dtype=np.uint32).reshape(-1)
+    k = np.ascontiguousarray(keys).view(np.uint64).reshape(-1)
+    if sp.size != 2 * k.size:
+        raise ValueError("%d span words for %d keys" % (sp.size, k.size))
+    return int(lib.sg_span_sum(sp.ctypes.data, k.ctypes.data, k.size))
+
+
 def device_count() -> int:
     n = C.c_int(0)
     check(lib.sg_device_count(C.byref(n)))
@@ -482,7 +492,8 @@ class Context:
                                             rec_cap: int):
         """partition_bytes_pieces_rounds that also writes every record's span (relative to its
         part's start) and first-chunk key into the caller's buffers (8 bytes each per record,
-        round-major part order). Returns (bytes per part, records per part)."""
+        round-major part order). Returns (bytes per part, records per part, handover checksum per
+        part: include/swarmgpu.h sg_span_sum)."""
         blob, offs = _keys_blob(list(splitters))
         parts = len(splitters) + 1
         k = len(pieces)
@@ -490,11 +501,12 @@ class Context:
         lens = (C.c_size_t * max(1, k))(*[n for _, n in pieces])
         pb = (C.c_uint64 * parts)()
         pr = (C.c_uint64 * parts)()
+        ps = (C.c_uint64 * parts)()
         check(lib.sg_dev_partition_bytes_pieces_rounds_spans(
             self._h, ptrs, lens, k, blob.ctypes.data, offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts, rounds,
             C.c_void_p(d_out) if d_out else None, out_cap, pb, pr, C.c_void_p(d_spans) if d_spans else None,
-            C.c_void_p(d_keys) if d_keys else None, rec_cap))
-        return list(pb), list(pr)
+            C.c_void_p(d_keys) if d_keys else None, rec_cap, ps))
+        return list(pb), list(pr), list(ps)
 
     def rebase_spans(self, d_buf: int, n: int, d_spans: int, n_rec: int, seg_first: Sequence[int],
                      seg_off: Sequence[int]) -> int:
@@ -512,7 +524,8 @@ class Context:
     def partition_bytes_pieces_spans(self, pieces: Sequence[Tuple[int, int]], splitters: Sequence[bytes], d_out: int,
                                      out_cap: int):
         """partition_bytes_pieces(align16=True) that also returns the parts' parse: (bytes per
-        part, records per part, device spans pointer, device keys pointer); part p's records
+        part, records per part, device spans pointer, device keys pointer, handover checksum per
+        part for dedup_diff_spans_into); part p's records
         start at index sum(records[:p]) (8 bytes per record in each array; context-owned until
         the next call of this kind)."""
         blob, offs = _keys_blob(list(splitters))
@@ -522,21 +535,27 @@ class Context:
         lens = (C.c_size_t * max(1, k))(*[n for _, n in pieces])
         pb = (C.c_uint64 * parts)()
         pr = (C.c_uint64 * parts)()
+        ps = (C.c_uint64 * parts)()
         sp, kp = C.c_void_p(), C.c_void_p()
         check(lib.sg_dev_partition_bytes_pieces_spans(self._h, ptrs, lens, k, blob.ctypes.data,
                                                       offs.ctypes.data_as(C.POINTER(C.c_uint32)), parts,
                                                       C.c_void_p(d_out) if d_out else None, out_cap, pb, pr,
-                                                      C.byref(sp), C.byref(kp)))
-        return list(pb), list(pr), sp.value or 0, kp.value or 0
+                                                      C.byref(sp), C.byref(kp), ps))
+        return list(pb), list(pr), sp.value or 0, kp.value or 0, list(ps)
 
-    def dedup_diff_spans_into(self, d_cur: int, n_cur: int, d_spans: int, d_keys: int, n_rec: int, d_prior: int,
-                              n_prior: int, d_uniq: int, uniq_cap: int, d_fresh: int, fresh_cap: int) -> _abi.DevResult:
+    def dedup_diff_spans_into(self, d_cur: int, n_cur: int, d_spans: int, d_keys: int, n_rec: int, span_sum: int,
+                              d_prior: int, n_prior: int, d_uniq: int, uniq_cap: int, d_fresh: int,
+                              fresh_cap: int) -> _abi.DevResult:
         """dedup_diff_into for an aligned part whose records partition_bytes_pieces_spans
-        already parsed (its n_rec spans and keys)."""
+        already parsed (its n_rec spans and keys, and their handover checksum span_sum). The
+        parse is checked against the bytes first (records tile the buffer, the checksum, sampled
+        newlines and keys): SGError with rc SG_E_CORRUPT when it does not match. The spans and
+        keys are consumed (the sort works in them)."""
         r = _abi.DevResult()
         check(lib.sg_dev_dedup_diff_spans_into(self._h, C.c_void_p(d_cur) if d_cur else None, n_cur,
                                                C.c_void_p(d_spans) if d_spans else None,
                                                C.c_void_p(d_keys) if d_keys else None, n_rec,
+                                               int(span_sum) & 0xFFFFFFFFFFFFFFFF,
                                                C.c_void_p(d_prior) if d_prior else None, n_prior, C.c_void_p(d_uniq),
                                                uniq_cap, C.c_void_p(d_fresh) if d_fresh else None, fresh_cap,
                                                C.byref(r)))

@@ -337,10 +337,13 @@ constexpr uint32_t PT_IMG = SG_PT_IMG;  // LDS image of a tile's output (records
 // Optional span output of k_part_apply (sp null: none): rpre = exclusive prefix of the
 // per-(part, tile) record counts (part-major), rbase[p] = index of part p's first record of
 // this piece among all parts' records, pstart[p] = part p's start in the output.
+// sums (optional, with sp): per (part, tile), part-major, the sum of the tile's span_mix terms
+// of that part's records (the handover checksum, sg_span_sum), reduced per part by k_part_sums.
 struct PartSpansOut {
     const uint64_t *rpre = nullptr, *rbase = nullptr, *pstart = nullptr;
     uint2 *sp = nullptr;
     uint64_t *keys = nullptr;
+    uint64_t *sums = nullptr;
 };
 
 __global__ __launch_bounds__(PT_BLOCK) void k_part_count(const uint2 *__restrict__ spans, const uint8_t *__restrict__ part,
@@ -377,6 +380,23 @@ __global__ __launch_bounds__(256) void k_part_totals(const uint32_t *__restrict_
     const size_t a = (size_t)q * ntiles, z = a + ntiles - 1;
     cnt[q] = rpre[z] + rcnt[z] - rpre[a];
     cnt[nparts + q] = ppre[z] + pcnt[z] - ppre[a];
+}
+
+// Part q's handover checksum over this piece's tiles (per-(part, tile) sums, part-major),
+// added into tot[q]: block (x, q) sums tiles [x * PS_CHUNK, + PS_CHUNK) of part q's row.
+constexpr uint32_t PS_CHUNK = 4096;
+__global__ __launch_bounds__(256) void k_part_sums(const uint64_t *__restrict__ sums, uint32_t ntiles,
+                                                   unsigned long long *__restrict__ tot) {
+    __shared__ uint64_t s[4];
+    const uint64_t *row = sums + (size_t)blockIdx.y * ntiles;
+    const uint32_t t0 = blockIdx.x * PS_CHUNK, t1 = min(ntiles, t0 + PS_CHUNK);
+    uint64_t v = 0;
+    for (uint32_t t = t0 + threadIdx.x; t < t1; t += 256u) v += row[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((long long)v, o, 64);
+    if (lane_id() == 0) s[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&tot[blockIdx.y], (unsigned long long)(s[0] + s[1] + s[2] + s[3]));
 }
 
 struct U32AsU64P {
@@ -420,7 +440,9 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
     __shared__ uint32_t s_lp[256], s_le[256];  // image offset - tile offset of part p's run; its image end
     __shared__ uint32_t s_red2[NW];
     __shared__ uint64_t s_k0[PT_TILE];  // key0 of each sorted position (written out in sorted order)
+    __shared__ uint64_t s_sum[256];     // per part: the tile's handover checksum terms
     const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
+    if (so.sums) s_sum[tid] = 0;
     for (int x = tid; x < NW * 256; x += PT_BLOCK) (&s_wh[0][0])[x] = 0;
     const uint32_t tile = blockIdx.x, tbase = tile * PT_TILE;
     const uint32_t wbase = tbase + wid * (PT_ITEMS * 64);
@@ -537,6 +559,11 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
             if (so.sp) put_medium<true, true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x, &k0);
             else put_medium<false, true>(buf, out + (dst & ~3ull), (uint32_t)(dst & 3u), x.x, x.y - x.x);
             finish(q, lo, x, k0);
+            if (so.sums) atomicAdd((unsigned long long *)&s_sum[lo], (unsigned long long)span_mix(x.y - x.x, k0));
+        }
+        if (so.sums) {
+            __syncthreads();
+            if ((uint32_t)tid < nparts) so.sums[(size_t)tid * ntiles + tile] = s_sum[tid];
         }
         return;
     }
@@ -555,8 +582,10 @@ __global__ __launch_bounds__(PT_BLOCK) void k_part_apply(const uint8_t *__restri
         if (so.sp) put_medium<true, false>(buf, s_img, li, x.x, x.y - x.x, &k0);
         else put_medium<false, false>(buf, s_img, li, x.x, x.y - x.x);
         if (so.sp) s_k0[q] = k0;
+        if (so.sums) atomicAdd((unsigned long long *)&s_sum[lo], (unsigned long long)span_mix(x.y - x.x, k0));
     }
     __syncthreads();
+    if (so.sums && (uint32_t)tid < nparts) so.sums[(size_t)tid * ntiles + tile] = s_sum[tid];
     for (uint32_t q = tid; q < n_t; q += PT_BLOCK) {
         const uint32_t lo = s_pq[q];
         const uint2 x = s_sp[q];
@@ -600,12 +629,13 @@ __device__ __forceinline__ bool span_ends_at_nl(uint2 x, const uint8_t *__restri
     return x.x <= x.y && x.y < n && buf[x.y] == 0x0a;
 }
 
-// every record rebased; the sampled ones checked
-__global__ __launch_bounds__(256) void k_rebase_spans(uint2 *__restrict__ sp, uint32_t n_rec, const uint8_t *__restrict__ buf,
+// every record of one batch of sources (records [sg_.first[0], sg_.first[nseg])) rebased; the
+// sampled ones checked
+__global__ __launch_bounds__(256) void k_rebase_spans(uint2 *__restrict__ sp, const uint8_t *__restrict__ buf,
                                                       uint32_t n, const RebaseSegs sg_, unsigned long long *__restrict__ bad) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t i = sg_.first[0] + blockIdx.x * 256u + threadIdx.x;
     bool ok = true;
-    if (i < n_rec) {
+    if (i < sg_.first[sg_.nseg]) {
         uint32_t lo = 0, hi = sg_.nseg;  // last segment whose first record <= i
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -706,6 +736,12 @@ extern "C" {
 
 uint64_t sg_hash64(const uint8_t *rec, size_t len) {
     return hash_words([&](uint32_t j) { return rec[j]; }, (uint32_t)len);
+}
+
+uint64_t sg_span_sum(const uint32_t *spans, const uint64_t *keys, size_t n_rec) {
+    uint64_t s = 0;
+    for (size_t i = 0; i < n_rec; ++i) s += span_mix(spans[2 * i + 1] - spans[2 * i], keys[i]);
+    return s;
 }
 
 int sg_lines(const uint8_t *buf, size_t n, uint64_t *spans, size_t cap, size_t *n_rec) {
@@ -822,9 +858,11 @@ int sg_dev_partition_bytes(sg_ctx *c, const uint8_t *d_buf, size_t n, const uint
 // Pass 0 of the piece partition: every piece's record count (count pass + tile scan per
 // piece into slot S_PT_LTP, one read-back). Kept in c->pt_prep for the next partition call on
 // the same pieces (sg_dev_partition_pieces_count: the caller sizes its span buffers first).
+// prep: the context's kept pass 0 may be used (taken, and cleared, by the caller on entry, so
+// a call that fails before reaching here never leaves it for a later one).
 static int pieces_pass0(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
                         std::vector<uint32_t> &lnt, std::vector<size_t> &loff, uint64_t **ltp_out,
-                        std::vector<uint32_t> &Rj) {
+                        std::vector<uint32_t> &Rj, bool prep) {
     lnt.assign(k, 0);
     loff.assign(k, 0);
     Rj.assign(k, 0);
@@ -839,13 +877,11 @@ static int pieces_pass0(sg_ctx *c, const uint8_t *const *d_pieces, const size_t 
     if (ltot) SG_TRY(slot(c, S_PT_LTP, ltot, &ltp));
     *ltp_out = ltp;
     auto &P = c->pt_prep;
-    if (P.on && P.ptrs.size() == k && std::equal(P.lens.begin(), P.lens.end(), lens) &&
+    if (prep && P.ptrs.size() == k && std::equal(P.lens.begin(), P.lens.end(), lens) &&
         std::equal(P.ptrs.begin(), P.ptrs.end(), d_pieces)) {
         Rj = P.Rj;  // the counts and tile scans of sg_dev_partition_pieces_count
-        P.on = false;
         return SG_OK;
     }
-    P.on = false;
     uint8_t *pin = (uint8_t *)c->pinned;
     if (8 * k > SG_PINNED_BYTES) { set_error("partition: %zu pieces exceed the read-back staging", k); return SG_E_INVAL; }
     // (a piece that is not 16-byte aligned is copied to the aligned staging slot before each
@@ -874,7 +910,11 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
                             const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts, uint8_t *d_out,
                             size_t out_cap, uint64_t *part_bytes, uint64_t *part_records, bool a16,
                             const uint2 **sp_out = nullptr, const uint64_t **k_out = nullptr, uint32_t rounds = 1,
-                            uint2 *user_sp = nullptr, uint64_t *user_k = nullptr, size_t rec_cap = 0) {
+                            uint2 *user_sp = nullptr, uint64_t *user_k = nullptr, size_t rec_cap = 0,
+                            uint64_t *part_sums = nullptr) {
+    // the kept pass 0 of sg_dev_partition_pieces_count serves this call only, whatever happens
+    const bool prep = c && c->pt_prep.on;
+    if (c) c->pt_prep.on = false;
     if (!c || (k && (!d_pieces || !lens)) || ((!splitters || !split_offs) && n_parts > 1)) {
         set_error("sg_dev_partition_bytes_pieces: bad arguments");
         return SG_E_INVAL;
@@ -905,7 +945,7 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
     std::vector<uint32_t> lnt, Rj;
     std::vector<size_t> loff;
     uint64_t *ltp = nullptr;
-    SG_TRY(pieces_pass0(c, d_pieces, lens, k, lnt, loff, &ltp, Rj));
+    SG_TRY(pieces_pass0(c, d_pieces, lens, k, lnt, loff, &ltp, Rj, prep));
     std::vector<uint64_t> roff(k, 0);
     uint64_t all_rec = 0;
     for (size_t j = 0; j < k; ++j) {
@@ -1044,16 +1084,36 @@ static int partition_pieces(sg_ctx *c, const uint8_t *const *d_pieces, const siz
     SG_TRY(slot(c, S_PT_BASE, pb_all.size(), &d_pb));
     SG_TRY(ctx_upload(c, d_pb, pb_all.data(), pb_all.size() * 8));
     const uint64_t *d_rb = d_pb + (size_t)k * n_parts, *d_pstart = d_pb + 2 * (size_t)k * n_parts;
+    // the handover checksum per part (sg_span_sum of its records' spans and keys): per-(part,
+    // tile) partials from the copy pass, then per part over every piece's tiles
+    const bool want_sums = want_sp && part_sums;
+    uint64_t *d_sums = nullptr;
+    unsigned long long *d_stot = nullptr;
+    if (want_sums) {
+        SG_TRY(slot(c, S_PT_SUMS, ptot + n_parts + 1, &d_sums));
+        d_stot = reinterpret_cast<unsigned long long *>(d_sums + ptot);
+        SG_HIP(hipMemsetAsync(d_stot, 0, 8ull * n_parts, c->stream));
+    }
     // pass 2 per piece: the multi-split copy with pass 1's spans, parts and scans
     for (size_t j = 0; j < k; ++j) {
         if (!Rj[j]) continue;
         SG_TRY(aligned_in(c, S_IN, d_pieces[j], lens[j], &pb_in[j]));
         PartSpansOut so;
-        if (want_sp) so = PartSpansOut{rpre_all + poff[j], d_rb + j * n_parts, d_pstart, d_sp, d_k};
+        if (want_sp)
+            so = PartSpansOut{rpre_all + poff[j], d_rb + j * n_parts, d_pstart, d_sp, d_k,
+                              want_sums ? d_sums + poff[j] : nullptr};
         // model: span + part read, the record's bytes read and written (+ span and key out)
         SG_LAUNCH_B(c, "part_emit", (want_sp ? 25.0 : 9.0) * Rj[j] + 2.0 * (double)lens[j], k_part_apply, ptn[j],
                     PT_BLOCK, 0, pb_in[j], keep_sp + roff[j], keep_k + roff[j], Rj[j], ptn[j], n_parts, ppre_all + poff[j],
                     d_pb + j * n_parts, d_out, so);
+        if (want_sums)
+            SG_LAUNCH(c, "part_sums", k_part_sums, dim3((ptn[j] + PS_CHUNK - 1) / PS_CHUNK, n_parts), 256, 0,
+                      d_sums + poff[j], ptn[j], d_stot);
+    }
+    if (want_sums) {  // (the host waits for the copy pass here: the sums travel with the sizes)
+        std::vector<uint64_t> hs(n_parts, 0);
+        SG_TRY(ctx_readback(c, hs.data(), d_stot, 8ull * n_parts));
+        for (uint32_t q = 0; q < n_parts; ++q) part_sums[q] = hs[q];
     }
     return SG_OK;
 }
@@ -1077,13 +1137,17 @@ int sg_dev_partition_bytes_pieces_a16(sg_ctx *c, const uint8_t *const *d_pieces,
 int sg_dev_partition_bytes_pieces_spans(sg_ctx *c, const uint8_t *const *d_pieces, const size_t *lens, size_t k,
                                         const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
                                         uint8_t *d_out, size_t out_cap, uint64_t *part_bytes, uint64_t *part_records,
-                                        const uint32_t **d_spans, const uint64_t **d_keys) {
-    if (!d_spans || !d_keys) { set_error("sg_dev_partition_bytes_pieces_spans: bad arguments"); return SG_E_INVAL; }
+                                        const uint32_t **d_spans, const uint64_t **d_keys, uint64_t *part_sums) {
+    if (!d_spans || !d_keys) {
+        if (c) c->pt_prep.on = false;
+        set_error("sg_dev_partition_bytes_pieces_spans: bad arguments");
+        return SG_E_INVAL;
+    }
     *d_spans = nullptr;
     *d_keys = nullptr;
     const uint2 *sp = nullptr;
     SG_TRY(partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
-                            part_records, true, &sp, d_keys));
+                            part_records, true, &sp, d_keys, 1, nullptr, nullptr, 0, part_sums));
     *d_spans = reinterpret_cast<const uint32_t *>(sp);
     return SG_OK;
 }
@@ -1108,7 +1172,8 @@ int sg_dev_partition_pieces_count(sg_ctx *c, const uint8_t *const *d_pieces, con
     std::vector<uint32_t> lnt, Rj;
     std::vector<size_t> loff;
     uint64_t *ltp = nullptr;
-    SG_TRY(pieces_pass0(c, d_pieces, lens, k, lnt, loff, &ltp, Rj));
+    c->pt_prep.on = false;
+    SG_TRY(pieces_pass0(c, d_pieces, lens, k, lnt, loff, &ltp, Rj, false));
     uint64_t tot = 0;
     for (uint32_t r : Rj) tot += r;
     *n_records = tot;
@@ -1124,16 +1189,20 @@ int sg_dev_partition_bytes_pieces_rounds_spans(sg_ctx *c, const uint8_t *const *
                                                const uint8_t *splitters, const uint32_t *split_offs, uint32_t n_parts,
                                                uint32_t rounds, uint8_t *d_out, size_t out_cap, uint64_t *part_bytes,
                                                uint64_t *part_records, uint32_t *d_spans, uint64_t *d_keys,
-                                               size_t rec_cap) {
-    if (!d_spans || !d_keys) { set_error("sg_dev_partition_bytes_pieces_rounds_spans: bad arguments"); return SG_E_INVAL; }
+                                               size_t rec_cap, uint64_t *part_sums) {
+    if (!d_spans || !d_keys) {
+        if (c) c->pt_prep.on = false;
+        set_error("sg_dev_partition_bytes_pieces_rounds_spans: bad arguments");
+        return SG_E_INVAL;
+    }
     return partition_pieces(c, d_pieces, lens, k, splitters, split_offs, n_parts, d_out, out_cap, part_bytes,
                             part_records, false, nullptr, nullptr, rounds, reinterpret_cast<uint2 *>(d_spans), d_keys,
-                            rec_cap);
+                            rec_cap, part_sums);
 }
 
 int sg_dev_rebase_spans(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t *d_spans, size_t n_rec,
                         const uint64_t *seg_first, const uint64_t *seg_off, uint32_t nseg, uint64_t *bad) {
-    if (!c || !bad || (n_rec && (!d_spans || !d_buf)) || nseg > SG_REBASE_SEGS || (nseg && (!seg_first || !seg_off))) {
+    if (!c || !bad || (n_rec && (!d_spans || !d_buf)) || (nseg && (!seg_first || !seg_off))) {
         set_error("sg_dev_rebase_spans: bad arguments");
         return SG_E_INVAL;
     }
@@ -1141,36 +1210,46 @@ int sg_dev_rebase_spans(sg_ctx *c, const uint8_t *d_buf, size_t n, uint32_t *d_s
     if (!n_rec) return SG_OK;
     if (n > MAX_BYTES || n_rec >= (1ull << 32)) { set_error("sg_dev_rebase_spans: input exceeds 4 GiB"); return SG_E_TOO_LARGE; }
     SG_HIP(hipSetDevice(c->device));
-    RebaseSegs sg_{};
     const uint32_t ns = nseg ? nseg : 1u;
-    sg_.nseg = ns;
+    std::vector<uint32_t> F(ns + 1), O(ns);
     bool shift = false;
     for (uint32_t s = 0; s < ns; ++s) {
         const uint64_t f = nseg ? seg_first[s] : 0, o = nseg ? seg_off[s] : 0;
-        if (o > n || f > n_rec || (s && f < sg_.first[s - 1])) { set_error("sg_dev_rebase_spans: bad segments"); return SG_E_INVAL; }
-        sg_.first[s] = (uint32_t)f;
-        sg_.off[s] = (uint32_t)o;
+        if (o > n || f > n_rec || (s && f < F[s - 1]) || (!s && f)) {
+            set_error("sg_dev_rebase_spans: bad segments");
+            return SG_E_INVAL;
+        }
+        F[s] = (uint32_t)f;
+        O[s] = (uint32_t)o;
         shift |= o != 0;
     }
-    sg_.first[ns] = (uint32_t)n_rec;
+    F[ns] = (uint32_t)n_rec;
     unsigned long long *d_bad;
     SG_TRY(slot(c, S_M_CNT, 4, &d_bad));
     SG_HIP(hipMemsetAsync(d_bad, 0, 8, c->stream));
-    if (shift)
-        SG_LAUNCH_B(c, "rebase_spans", 16.0 * (double)n_rec, k_rebase_spans, (uint32_t)((n_rec + 255) / 256), 256, 0,
-                    reinterpret_cast<uint2 *>(d_spans), (uint32_t)n_rec, d_buf, (uint32_t)n, sg_, d_bad);
-    else
-        SG_LAUNCH(c, "check_spans", k_check_spans, (ns * 2 * SG_REBASE_CHECK + 255) / 256, 256, 0,
-                  reinterpret_cast<const uint2 *>(d_spans), d_buf, (uint32_t)n, sg_, d_bad);
+    // one launch per batch of SG_REBASE_SEGS sources (a kernel argument holds one batch's table)
+    for (uint32_t s0 = 0; s0 < ns; s0 += SG_REBASE_SEGS) {
+        RebaseSegs sg_{};
+        sg_.nseg = std::min<uint32_t>(SG_REBASE_SEGS, ns - s0);
+        for (uint32_t s = 0; s < sg_.nseg; ++s) { sg_.first[s] = F[s0 + s]; sg_.off[s] = O[s0 + s]; }
+        sg_.first[sg_.nseg] = F[s0 + sg_.nseg];
+        const uint32_t nr = sg_.first[sg_.nseg] - sg_.first[0];
+        if (shift && nr)
+            SG_LAUNCH_B(c, "rebase_spans", 16.0 * (double)nr, k_rebase_spans, (nr + 255) / 256, 256, 0,
+                        reinterpret_cast<uint2 *>(d_spans), d_buf, (uint32_t)n, sg_, d_bad);
+        else if (!shift)
+            SG_LAUNCH(c, "check_spans", k_check_spans, (sg_.nseg * 2 * SG_REBASE_CHECK + 255) / 256, 256, 0,
+                      reinterpret_cast<const uint2 *>(d_spans), d_buf, (uint32_t)n, sg_, d_bad);
+    }
     unsigned long long b = 0;
     SG_TRY(ctx_readback(c, &b, d_bad, 8));
     *bad = b;
     return SG_OK;
 }
 
-int sg_dev_dedup_diff_spans_into(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, const uint32_t *d_spans,
-                                 const uint64_t *d_keys, size_t n_rec, const uint8_t *d_prior, size_t n_prior,
-                                 uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap,
+int sg_dev_dedup_diff_spans_into(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, uint32_t *d_spans,
+                                 uint64_t *d_keys, size_t n_rec, uint64_t span_sum, const uint8_t *d_prior,
+                                 size_t n_prior, uint8_t *d_uniq, size_t uniq_cap, uint8_t *d_fresh, size_t fresh_cap,
                                  sg_dev_result *res) {
     if (!c || !res || (!d_cur && n_cur) || (!d_prior && n_prior) || !d_uniq || (n_rec && (!d_spans || !d_keys))) {
         set_error("sg_dev_dedup_diff_spans_into: bad arguments");
@@ -1181,13 +1260,20 @@ int sg_dev_dedup_diff_spans_into(sg_ctx *c, const uint8_t *d_cur, size_t n_cur, 
         set_error("input exceeds 4 GiB per call");
         return SG_E_TOO_LARGE;
     }
+    if (!n_rec && (n_cur || span_sum)) {  // records tile the buffer: no records, no bytes
+        set_error("handed-over parse does not match the buffer: 0 records for %zu bytes, checksum %016llx", n_cur,
+                  (unsigned long long)span_sum);
+        return SG_E_CORRUPT;
+    }
     SG_HIP(hipSetDevice(c->device));
     const uint8_t *prior = nullptr;
     if (n_prior) SG_TRY(aligned_in(c, S_IN2, d_prior, n_prior, &prior));
     Lines L;
-    L.spans = const_cast<uint2 *>(reinterpret_cast<const uint2 *>(d_spans));
-    L.keys = const_cast<uint64_t *>(d_keys);
+    L.spans = reinterpret_cast<uint2 *>(d_spans);  // consumed: the sort works in place
+    L.keys = d_keys;
     L.n_rec = (uint32_t)n_rec;
+    L.chk = true;  // checked by the dedup's prefix scan before any byte is read through a span
+    L.chk_sum = span_sum;
     return dev_dedup_diff_into_lines(c, d_cur, n_cur, L, prior, n_prior, d_uniq, uniq_cap, d_fresh, fresh_cap, res);
 }
 

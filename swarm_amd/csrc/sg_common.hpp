@@ -74,6 +74,7 @@ enum Slot : int {
     S_PT_SP, S_PT_KEYS,             // piece partition: spans and parts kept from pass 1 for pass 2
     S_PT_LTP,                       // piece partition: every piece's parse tile counts and prefixes
     S_PT_RCNT, S_PT_RPRE, S_PT_SPOUT, S_PT_KOUT,  // piece partition: the parts' record spans/keys out
+    S_PT_SUMS,                      // piece partition: per-(part, tile) handover checksums, per-part totals
     S_LS_ERR, S_LS_BOUNDS,  // hybrid radix sort: overflow flag, local-sort tile bounds
     S_LS_LIST, S_LF_OFF, S_LF_KEY, S_LF_KEY2, S_LF_VAL, S_LF_VAL2, S_LF_POS,  // its overflow fix-up
     S_KEYSL, S_KEYSL2,  // dedup: cur / prior keys at the last call's common prefix (speculative)
@@ -109,8 +110,9 @@ struct sg_ctx {
     struct LsLast {
         bool on = false;
         uint64_t gmask = 0;
-        uint32_t lpos = 0, nloc = 0, ntiles = 0;
+        uint32_t lpos = 0, nloc = 0, ntiles = 0, cap = 0;
         uint32_t *bounds = nullptr;
+        uint32_t *gs = nullptr, *ge = nullptr;  // the big groups the fix-up pass listed
     } ls_last;
     // the piece partition's pass 0 (record counts per piece) kept from sg_dev_partition_pieces_count
     // for the next partition call on the same pieces (its tile scans stay in slot S_PT_LTP)
@@ -327,6 +329,15 @@ __device__ __forceinline__ uint64_t chunk_key(const uint8_t *buf, uint32_t s, ui
     if (p + take > a + 8u) v |= *reinterpret_cast<const uint64_t *>(buf + a + 8) << (64u - sh);
     v &= (1ull << (8u * take)) - 1ull;  // take <= 7
     return (__builtin_bswap64(v) & ~0xffull) | tag;
+}
+
+// One record's term of the handover checksum (include/swarmgpu.h sg_span_sum): its length
+// (end - start) and its first-chunk key, mixed by one odd multiply and an xor-shift (both
+// bijective: a change of one record's key or length always changes the sum). The checksum is
+// the sum of the terms mod 2^64, so producers add them in any order (per tile, per part).
+__host__ __device__ __forceinline__ uint64_t span_mix(uint32_t len, uint64_t key) {
+    const uint64_t h = (key + (uint64_t)len * 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 31);
 }
 
 // Bytes [lo, hi) of the little-endian dword v stored at p (p 4-byte aligned, 0 <= lo <= hi

@@ -793,17 +793,37 @@ __device__ __forceinline__ uint32_t lcp_one(const uint8_t *buf, const uint2 *spa
 // st (optional): the keys' KeyStatD partial per block, gathered in the same read (the cur
 // keys, for the sort).
 constexpr int LCP_U = 4;
+// CHK (sg_dev_dedup_diff_spans_into): the scan also checks the handed-over parse of `buf` (nb
+// bytes) before anything else indexes the bytes with it: records must tile the buffer in
+// order (record 0 starts at 0, each starts right after its predecessor's '\n', is non-empty,
+// and the last '\n' is the buffer's last byte), and the span_mix terms are summed (per-block
+// partials in chk) for comparison with the producer's checksum; k_chk_sample checks the
+// sampled records' bytes. The spans are read beside the keys (each lane also loads its
+// predecessor's span: the same lines, from cache). rnb (any mode): bytes of the reference
+// record's buffer when its span is not trusted (0: trusted); an out-of-place reference span
+// turns every byte compare off (the call fails on the check anyway). Records out of place are
+// counted into *cbad_out (one atomic per wave that saw one: none when the parse is intact).
+constexpr uint32_t CHK_SAMPLE = 256;
+struct SpanChkPart {
+    uint64_t sum;
+    uint32_t bad, pad;
+};
+template <bool CHK>
 __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                              const uint64_t *__restrict__ keys, uint32_t n,
                                              const uint8_t *__restrict__ rbuf, const uint2 *__restrict__ rspans,
                                              const uint64_t *__restrict__ rkeys, uint32_t *__restrict__ out,
-                                             KeyStatD *__restrict__ st, uint64_t *__restrict__ keysL = nullptr,
-                                             uint32_t Ls = 0, KeyStatD *__restrict__ stL = nullptr) {
+                                             KeyStatD *__restrict__ st, uint64_t *__restrict__ keysL, uint32_t Ls,
+                                             KeyStatD *__restrict__ stL, uint32_t rnb, SpanChkPart *__restrict__ chk,
+                                             uint32_t nb, uint32_t *__restrict__ cbad_out) {
     __shared__ uint32_t s_min[4];
     __shared__ KeyStatD s_st[4];
+    __shared__ SpanChkPart s_chk[4];
     const uint64_t kr = rkeys[0];
     uint32_t best = 255;
     KeyStatAcc acc, accL;
+    uint64_t csum = 0;
+    uint32_t cbad = 0;
     // grid-stride (at most 2048 blocks): at most one memory-side atomic per block and word;
     // LCP_U keys in flight per thread (one dependent load per trip left the loop latency-bound:
     // 1.6 TB/s on C2's cur keys)
@@ -813,23 +833,46 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
     // the rare records that also tie there.
     const uint32_t stride = gridDim.x * blockDim.x * LCP_U;
     const uint2 r = rspans[0];
+    const bool rok = rnb == 0u || (r.y > r.x && r.y < rnb);
     const uint32_t rlen = r.y - r.x, tr = (uint32_t)(kr & 0xffu);
     for (uint32_t i0 = blockIdx.x * blockDim.x * LCP_U + threadIdx.x; i0 < n; i0 += stride) {
         uint64_t k[LCP_U];
+        uint2 cs[LCP_U];
+        uint32_t py[LCP_U];
+        bool okl[LCP_U];
 #pragma unroll
         for (int u = 0; u < LCP_U; ++u) {
             const uint32_t i = i0 + u * blockDim.x;
             k[u] = i < n ? keys[i] : 0ull;
+            if (CHK) {
+                cs[u] = i < n ? spans[i] : make_uint2(0u, 0u);
+                py[u] = (i < n && i > 0u) ? spans[i - 1u].y : 0xffffffffu;  // record 0 must start at 0
+            }
+        }
+        if (CHK) {
+#pragma unroll
+            for (int u = 0; u < LCP_U; ++u) {
+                const uint32_t i = i0 + u * blockDim.x;
+                okl[u] = i < n && cs[u].y > cs[u].x && cs[u].y < nb;
+                const bool tiled = cs[u].x == py[u] + 1u;
+                const bool last = i + 1u != n || cs[u].y + 1u == nb;
+                if (i < n) {
+                    cbad += (okl[u] && tiled && last) ? 0u : 1u;
+                    csum += span_mix(cs[u].y - cs[u].x, k[u]);
+                }
+            }
         }
         bool slow[LCP_U];
 #pragma unroll
         for (int u = 0; u < LCP_U; ++u) {
             const uint32_t i = i0 + u * blockDim.x;
             const uint32_t tk = (uint32_t)(k[u] & 0xffu);
-            slow[u] = i < n && ((k[u] ^ kr) >> 8) == 0 && tk >= 8u && tr >= 8u && best > 7u;
+            // bytes are read through a span only when it (and the reference's) is in place
+            const bool bytes_ok = rok && (!CHK || okl[u]);
+            slow[u] = i < n && ((k[u] ^ kr) >> 8) == 0 && tk >= 8u && tr >= 8u && best > 7u && bytes_ok;
             if (i < n) {
                 acc.add(k[u]);
-                if (!slow[u]) best = min(best, lcp_one(buf, spans, i, k[u], rbuf, rspans, kr, best));
+                if (!slow[u] && bytes_ok) best = min(best, lcp_one(buf, spans, i, k[u], rbuf, rspans, kr, best));
             }
         }
         uint2 xs[LCP_U];
@@ -884,11 +927,61 @@ __global__ __launch_bounds__(256) void k_lcp(const uint8_t *__restrict__ buf, co
         __syncthreads();  // s_st reused
         kstat_flush(accL, s_st, stL);
     }
+    if (CHK) {
+        if (__ballot(cbad != 0u)) {  // (rare: a damaged parse) one atomic per such wave
+            const uint32_t wb = wave_sum(cbad);
+            if (lane_id() == 0) atomicAdd(cbad_out, wb);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) csum += (uint64_t)__shfl_xor((long long)csum, o, 64);
+        if (lane_id() == 0) s_chk[threadIdx.x >> 6] = SpanChkPart{csum, 0u, 0u};
+    }
     __syncthreads();
+    if (CHK && threadIdx.x == 0)
+        chk[blockIdx.x] = SpanChkPart{s_chk[0].sum + s_chk[1].sum + s_chk[2].sum + s_chk[3].sum, 0u, 0u};
     if (threadIdx.x == 0) {
         const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
         // skip the memory-side atomic when an earlier block already published as small a prefix
         if (b < 255u && b < __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(out, b);
+    }
+}
+
+// The handover check's per-block checksum partials summed into out[0..1], read back with the
+// prefix scan's flags (out[2], the records out of place, is counted by the checking kernels).
+__global__ __launch_bounds__(256) void k_chk_combine(const SpanChkPart *__restrict__ part, uint32_t np,
+                                                     uint32_t *__restrict__ out) {
+    __shared__ uint64_t s[4];
+    uint64_t sum = 0;
+    for (uint32_t b = threadIdx.x; b < np; b += 256u) sum += part[b].sum;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += (uint64_t)__shfl_xor((long long)sum, o, 64);
+    if (lane_id() == 0) s[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t t = s[0] + s[1] + s[2] + s[3];
+        out[0] = (uint32_t)t;
+        out[1] = (uint32_t)(t >> 32);
+    }
+}
+
+// The handover check's byte samples: every CHK_SAMPLE-th record, when its span lies inside the
+// buffer, must end at a '\n' and carry the key of its own bytes (a delivery that left a region
+// of the bytes stale or shifted while the parse arrived intact); out-of-place ones counted
+// into *bad (one atomic per wave that saw one).
+__global__ __launch_bounds__(256) void k_chk_sample(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
+                                                    const uint64_t *__restrict__ keys, uint32_t n, uint32_t nb,
+                                                    uint32_t *__restrict__ bad) {
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x, i = j * CHK_SAMPLE;
+    uint32_t b = 0;
+    if (i < n) {
+        const uint2 x = spans[i];
+        const uint64_t k = keys[i];
+        if (x.y > x.x && x.y < nb) b = (buf[x.y] == 0x0a && chunk_key(buf, x.x, x.y, 0u) == k) ? 0u : 1u;
+        else b = 1u;
+    }
+    if (__ballot(b != 0u)) {
+        const uint32_t wb = wave_sum(b);
+        if (lane_id() == 0) atomicAdd(bad, wb);
     }
 }
 
@@ -1317,12 +1410,17 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
     // word with one host sync
     auto read_counts = [&](bool with_heads) -> int {
         uint8_t *pin = (uint8_t *)c->pinned;
-        SG_HIP(hipMemcpyAsync(pin, acnt, 28, hipMemcpyDeviceToHost, c->stream));  // acnt | stot | lerr
+        SG_HIP(hipMemcpyAsync(pin, acnt, 32, hipMemcpyDeviceToHost, c->stream));  // acnt | stot | lerr[2]
         SG_HIP(hipStreamSynchronize(c->stream));
         uint32_t v[3];
         memcpy(v, pin, 12);
         lerr_v = 0;
-        if (lerr) memcpy(&lerr_v, pin + 24, 4);
+        if (lerr) {
+            uint32_t fixed = 0;
+            memcpy(&lerr_v, pin + 24, 4);  // big groups listed by the local sort's fix-up pass
+            memcpy(&fixed, pin + 28, 4);   // tiles that pass redid
+            if (fixed) c->last_flags |= 4u;
+        }
         B = v[2];
         if (with_heads) {
             uint64_t t = 0;
@@ -1348,12 +1446,12 @@ static int build_unique(sg_ctx *c, const uint8_t *d_buf, uint64_t n, const ViewS
         uint64_t *Ka = (K == L.keys) ? k2 : L.keys;
         uint2 *Va = (V == L.spans) ? v2 : L.spans;
         if (!fix_tried) {
-            // a group outgrew the local sort's LDS (the pairs are intact, unsorted there): its
-            // tiles again from the local sort's input (Ka, Va still hold it), with the groups
-            // too large for one block sorted by one radix sort of their members only (a record
-            // repeated thousands of times), then the adjacent pass again
+            // a group larger than any LDS window (its pairs are intact, unsorted; the tiles
+            // around it were already redone in the sort's own stream): the big groups' members
+            // sorted by one radix sort from the local sort's input (Ka, Va still hold it; a
+            // record repeated thousands of times), then the adjacent pass again
             fix_tried = true;
-            SG_TRY(lsort_fixup(c, Ka, Va, K, V, R));
+            SG_TRY(lsort_fixup_big(c, Ka, Va, K, V, R, lerr_v));
             SG_HIP(hipMemsetAsync(lerr, 0, 4, c->stream));
             c->last_flags |= 4u;
             continue;
@@ -1469,7 +1567,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     // (the front of one slot with the sample histograms and the stat partials after it: the
     // flags, the stats and the histograms come back in one copy)
     uint32_t *dflag;
-    SG_TRY(slot(c, S_HIST, 32 + 8 * 256 + 2 * 2048 * sizeof(KeyStatD) / 4, &dflag));
+    constexpr size_t DF_CHK = 32 + 8 * 256 + 2 * 2048 * sizeof(KeyStatD) / 4;  // handover check partials
+    SG_TRY(slot(c, S_HIST, DF_CHK + 2048 * sizeof(SpanChkPart) / 4, &dflag));
     KeyStatD *st0 = reinterpret_cast<KeyStatD *>(dflag + 4), *st1 = reinterpret_cast<KeyStatD *>(dflag + 12);
     {
         uint32_t init[20] = {0u, 255u};
@@ -1530,20 +1629,37 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         }
         if (have_prior && Lp.n_rec) SG_TRY(slot(c, S_KEYSL2, (size_t)Lp.n_rec + 1, &kLp));
     }
-    if (rsp && Lc.n_rec && !cur_lcp)
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp, g_cur, 256, 0, d_cur, Lc.spans, Lc.keys, Lc.n_rec, rbuf, rsp, rkeys,
-                    dflag + 1, parts, kLc, Ls, partsL);  // (not reached with cur_lcp)
-    else if (want_hist)
+    // a handed-over parse (Lc.chk) is checked by the cur scan, and nothing reads bytes through
+    // an unchecked reference span (rnb) before the check's result comes back with the flags
+    const bool chk = Lc.chk && Lc.n_rec;
+    const uint32_t rnb = chk && ref_cur ? (uint32_t)n_cur : 0u;
+    SpanChkPart *chk_parts = reinterpret_cast<SpanChkPart *>(dflag + DF_CHK);
+    if (rsp && Lc.n_rec && !cur_lcp) {
+        if (chk) {
+            // model: key + span per record (the sampled byte checks are not credited)
+            SG_HIP(hipMemsetAsync(dflag + 22, 0, 4, c->stream));
+            SG_LAUNCH_B(c, "lcp", 16.0 * Lc.n_rec, k_lcp<true>, g_cur, 256, 0, d_cur, Lc.spans, Lc.keys, Lc.n_rec, rbuf,
+                        rsp, rkeys, dflag + 1, parts, kLc, Ls, partsL, rnb, chk_parts, (uint32_t)n_cur, dflag + 22);
+            SG_LAUNCH(c, "chk_combine", k_chk_combine, 1, 256, 0, chk_parts, g_cur, dflag + 20);
+            const uint32_t ns = (Lc.n_rec + CHK_SAMPLE - 1) / CHK_SAMPLE;
+            SG_LAUNCH(c, "chk_sample", k_chk_sample, (ns + 255) / 256, 256, 0, d_cur, Lc.spans, Lc.keys, Lc.n_rec,
+                      (uint32_t)n_cur, dflag + 22);
+        } else {
+            SG_LAUNCH_B(c, "lcp", 8.0 * Lc.n_rec, k_lcp<false>, g_cur, 256, 0, d_cur, Lc.spans, Lc.keys, Lc.n_rec, rbuf,
+                        rsp, rkeys, dflag + 1, parts, kLc, Ls, partsL, 0u, (SpanChkPart *)nullptr, 0u, (uint32_t *)nullptr);
+        }
+    } else if (want_hist) {  // (not reached with a handed-over parse: it always has cur_lcp null)
         SG_LAUNCH_B(c, "key_stats", 8.0 * Lc.n_rec, k_key_stats, g_cur, 256, 0, Lc.keys, Lc.n_rec, parts);
+    }
     if (rsp && have_prior && Lp.n_rec)
-        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior,
-                    Lp.spans, Lp.keys, Lp.n_rec, rbuf, rsp, rkeys, dflag + 1, (KeyStatD *)nullptr, kLp, Ls,
-                    (KeyStatD *)nullptr);
+        SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp<false>, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0,
+                    d_prior, Lp.spans, Lp.keys, Lp.n_rec, rbuf, rsp, rkeys, dflag + 1, (KeyStatD *)nullptr, kLp, Ls,
+                    (KeyStatD *)nullptr, rnb, (SpanChkPart *)nullptr, 0u, (uint32_t *)nullptr);
     // the sample histograms (and the combined partials) come back with the flags; they stay
     // valid when the common prefix turns out to be empty
     if (want_hist) SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, parts, g_cur, st0));
     uint32_t *hh = c->hist_host;
-    uint32_t fl[20] = {0u};
+    uint32_t fl[32] = {0u};
     auto read_stats = [&](uint32_t words) -> int {
         uint8_t *pin = (uint8_t *)c->pinned;
         SG_HIP(hipMemcpyAsync(pin, dflag, shist ? 128 + 8 * 256 * 4 : 4 * words, hipMemcpyDeviceToHost, c->stream));
@@ -1552,7 +1668,16 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         if (shist) memcpy(hh, pin + 128, 8 * 256 * 4);
         return SG_OK;
     };
-    SG_TRY(read_stats(want_hist ? 12u : 2u));
+    SG_TRY(read_stats(chk ? 24u : (want_hist ? 12u : 2u)));
+    if (chk) {  // before any kernel indexes the bytes through the handed-over spans
+        uint64_t sum = 0;
+        memcpy(&sum, fl + 20, 8);
+        if (fl[22] || sum != Lc.chk_sum) {
+            set_error("handed-over parse does not match the buffer: %u of %u records out of place, checksum %016llx "
+                      "(expected %016llx)", fl[22], Lc.n_rec, (unsigned long long)sum, (unsigned long long)Lc.chk_sum);
+            return SG_E_CORRUPT;
+        }
+    }
     prior_sorted = fl[0] == 0;
     const uint32_t base = (rsp && (Lc.n_rec || (have_prior && Lp.n_rec))) ? fl[1] : 0u;
     if (base) {

@@ -35,6 +35,11 @@ struct Lines {
     uint64_t *spec_keys = nullptr;
     const struct KeyStatD *spec_parts = nullptr;
     uint32_t spec_off = 0, spec_nparts = 0;
+    // A parse handed over by another call (sg_dev_dedup_diff_spans_into): checked by the
+    // dedup's prefix scan before anything indexes the bytes with it (records tile the buffer,
+    // sum of span_mix terms == chk_sum, sampled records end at a '\n' and match their keys).
+    bool chk = false;
+    uint64_t chk_sum = 0;
 };
 // Split d_buf (16-byte aligned device pointer, n bytes) into non-empty records.
 // apply = false: count and allocate only; the spans are then written by a consumer that
@@ -74,15 +79,16 @@ int radix_sort_spans(sg_ctx *c, uint64_t *keys, uint2 *spans, uint64_t *keys_alt
                      const char *pass_name = "rs_pass", const KeyStats *ks = nullptr,
                      uint32_t narrow_kw = 0, uint32_t **lsort_err = nullptr, uint32_t *err_at = nullptr);
 // lsort_err (with ks->hist): allows the hybrid sort (global passes over the top digits, the
-// rest per group in LDS); *lsort_err is then the device word that turns nonzero when a group
-// did not fit the LDS — the pairs are a valid permutation but not sorted, and the caller must
-// sort them again with lsort_err = nullptr (null when the plain LSD sort ran). err_at: the
-// device word to use for it (e.g. beside the caller's other counters: one read-back).
-// The hybrid sort's flagged tiles (a group of equal top digits larger than one block's LDS),
-// redone from the local sort's input (Kin, Vin: the pairs after the global passes) into
-// (Ko, Vo): windows of whole groups in LDS again, the big groups' members by one stable
-// radix sort on (group, local digits). Uses the ctx's last hybrid plan (c->ls_last).
-int lsort_fixup(sg_ctx *c, const uint64_t *Kin, const uint2 *Vin, uint64_t *Ko, uint2 *Vo, uint32_t n);
+// rest per group in one block's LDS). The tiles one window cannot hold are redone right behind
+// the local sort, in the same stream (k_rs_lsort_fix over the listed tiles); *lsort_err is then
+// the device word counting the groups too large for any window ("big groups": the pairs there
+// are a valid permutation but not sorted), and the caller that reads it nonzero must run
+// lsort_fixup_big (null when the plain LSD sort ran). err_at: the device words to use (2: the
+// big-group count, then the count of tiles redone), e.g. beside the caller's other counters.
+// The hybrid sort's big groups (listed by its fix-up pass) sorted from the local sort's input
+// (Kin, Vin: the pairs after the global passes) into (Ko, Vo) by one stable radix sort of
+// their members on (group, local digits). Uses the ctx's last hybrid plan (c->ls_last).
+int lsort_fixup_big(sg_ctx *c, const uint64_t *Kin, const uint2 *Vin, uint64_t *Ko, uint2 *Vo, uint32_t n, uint32_t B);
 // Queue the digit histograms of a row sample of the keys into dev_hist (8 x 256 u32, zeroed
 // by the caller); *sample_n = the keys counted. With parts: the nparts per-block KeyStatD
 // partials of an earlier kernel are combined into *st in the same launch.

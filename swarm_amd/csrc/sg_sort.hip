@@ -219,6 +219,40 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_up(const uint64_t *__restrict__
     }
 }
 
+// k_rs_up from the digit bytes the previous pass's downsweep wrote beside the keys (dig[i] =
+// the digit of the pair now at position i): 1 B read per pair instead of the 8-B key. Eight
+// consecutive digits per thread (one 8-B load), per-wave LDS histograms.
+__global__ __launch_bounds__(RD_BLOCK) void k_rs_up8(const uint8_t *__restrict__ dig, uint32_t n, uint32_t ntiles,
+                                                     uint32_t *__restrict__ cnt, bool xcd) {
+    static_assert(RD_ITEMS == 8, "eight digits per thread");
+    __shared__ uint32_t h[RD_WAVES][256];
+    const int wid = threadIdx.x >> 6;
+    const uint32_t tile = xcd ? rs_tile_of(blockIdx.x, ntiles) : blockIdx.x;
+    if (tile >= ntiles) return;
+    for (int x = threadIdx.x; x < RD_WAVES * 256; x += RD_BLOCK) (&h[0][0])[x] = 0;
+    __syncthreads();
+    const uint32_t base = tile * RD_TILE + threadIdx.x * 8u;
+    uint64_t w = 0;
+    uint32_t m = 0;
+    if (base + 8u <= n) {
+        w = *reinterpret_cast<const uint64_t *>(dig + base);
+        m = 8u;
+    } else if (base < n) {
+        m = n - base;
+        for (uint32_t j = 0; j < m; ++j) w |= (uint64_t)dig[base + j] << (8u * j);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j)
+        if (j < m) atomicAdd(&h[wid][(uint32_t)(w >> (8u * j)) & 255u], 1u);
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int ww = 0; ww < RD_WAVES; ++ww) v += h[ww][threadIdx.x];
+        cnt[(size_t)threadIdx.x * ntiles + tile] = v;
+    }
+}
+
 // One block per digit d: the digit's total over the tiles (the pass's digit bases without a
 // key histogram: KeyStats sorts).
 __global__ __launch_bounds__(256) void k_rs_dsum(const uint32_t *__restrict__ cnt, uint32_t ntiles,
@@ -267,12 +301,15 @@ __global__ __launch_bounds__(256) void k_rs_cscan(uint32_t *__restrict__ cnt, ui
 
 // VT: u32 record ids (IOTA: generated on the first pass) or uint2 spans carried along, so
 // the sorted spans need no gather afterwards (sg_dedup.hip build_unique).
+// dnext (optional): each pair's digit for the next pass (at shift_next), written beside its
+// key at its output position, so the next pass's tile counts read 1 B per pair (k_rs_up8).
 template <bool IOTA, typename VT = uint32_t>
 __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict__ kin,
                                                       const VT *__restrict__ vin,
                                                       uint64_t *__restrict__ kout, VT *__restrict__ vout,
                                                       uint32_t n, int shift, uint32_t ntiles,
-                                                      const uint32_t *__restrict__ toffs, uint32_t kw, bool xcd) {
+                                                      const uint32_t *__restrict__ toffs, uint32_t kw, bool xcd,
+                                                      uint8_t *__restrict__ dnext, int shift_next) {
     static_assert(sizeof(VT) <= sizeof(uint64_t), "values staged in the key buffer");
     __shared__ uint64_t s_k[RD_TILE];  // keys, then (aliased) values
     VT *s_v = reinterpret_cast<VT *>(s_k);
@@ -346,6 +383,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
             const uint32_t d = (uint32_t)(kk >> shift) & 255u;
             dg[j >> 2] |= d << (8 * (j & 3));
             kout[s_gbase[d] + p] = kk;
+            if (dnext) dnext[s_gbase[d] + p] = (uint8_t)(kk >> shift_next);
         }
     }
     VT v[RD_ITEMS];
@@ -389,7 +427,7 @@ __global__ __launch_bounds__(RD_BLOCK) void k_rs_down(const uint64_t *__restrict
 constexpr int LS_BLOCK = SG_LS_BLOCK;  // 256 or 512 (digit owners: the first 256 threads)
 constexpr int LS_CAP = 4096;           // pairs sorted in one block's LDS
 #ifndef SG_LS_T
-#define SG_LS_T 3584
+#define SG_LS_T 3072
 #endif
 constexpr int LS_T = SG_LS_T;          // base tile (LS_CAP - LS_T: room for the last group)
 constexpr int LS_ITEMS = LS_CAP / LS_BLOCK;
@@ -417,10 +455,11 @@ __device__ __forceinline__ uint32_t ls_head(const uint64_t *__restrict__ K, uint
 // bounds[t] = head(t * LS_T) | real << 31, t = 0 .. ntiles (one wave per boundary): the group
 // search runs as its own launch, many waves in flight, instead of at the head of every
 // local-sort block.
-// (err: the local sort's overflow word, zeroed here instead of by a memset launch)
+// (err[0]: the big-group count of the local sort's fix-up, err[1]: its flagged-tile count;
+// zeroed here instead of by a memset launch)
 __global__ __launch_bounds__(256) void k_rs_lbounds(const uint64_t *__restrict__ K, uint32_t n, uint64_t gmask,
                                                     uint32_t nb, uint32_t *__restrict__ bounds, uint32_t *__restrict__ err) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *err = 0u;
+    if (blockIdx.x == 0 && threadIdx.x < 2) err[threadIdx.x] = 0u;
     const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= nb) return;
     uint32_t real;
@@ -582,10 +621,14 @@ __device__ __forceinline__ uint32_t ls_blk_max(uint32_t v, uint32_t *s_agg) {
     return v;
 }
 
+// flist / fcnt: the tiles this sort could not do in one window (over LS_CAP pairs: a group
+// straddles the tile's end boundary far enough, or is larger than the LDS), listed for
+// k_rs_lsort_fix, which the host launches right behind this kernel (no read-back between).
 __global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
                                                        uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t n,
                                                        uint64_t gmask, uint32_t lpos, uint32_t nloc,
-                                                       const uint32_t *__restrict__ bounds, uint32_t *__restrict__ err) {
+                                                       const uint32_t *__restrict__ bounds, uint32_t *__restrict__ flist,
+                                                       uint32_t *__restrict__ fcnt) {
     __shared__ LsShared sh_;
     const uint32_t t = blockIdx.x;
     const uint32_t b0 = bounds[t], b1 = bounds[t + 1];
@@ -593,33 +636,27 @@ __global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort(const uint64_t *__restric
     const uint32_t nt = e - s;
     if (nt == 0) return;
     if (nt > (uint32_t)LS_CAP || !(b0 >> 31) || !(b1 >> 31)) {
-        // a group larger than the LDS: keep the pairs (a valid permutation), flag the tile;
-        // the caller then runs k_rs_lsort_fix over the flagged tiles (lsort_fixup)
-        for (uint32_t i = s + threadIdx.x; i < e; i += LS_BLOCK) { Ko[i] = K[i]; Vo[i] = V[i]; }
-        if (threadIdx.x == 0) atomicOr(err, 1u);
+        if (threadIdx.x == 0) flist[atomicAdd(fcnt, 1u)] = t;
         return;
     }
     ls_sort_window(K, V, Ko, Vo, s, nt, gmask, lpos, nloc, sh_);
 }
 
-// The tiles k_rs_lsort could not sort (a group of equal top digits larger than the LDS lies
-// in them, or the tile edge cuts one), redone from the same input: windows of whole groups
-// (<= LS_CAP pairs) are sorted in LDS as usual; every group too large for a window ("big
-// group", e.g. one record repeated thousands of times) is copied and listed (gs, ge: its
-// position range, appended by the block that holds its first position; the blocks its tail
-// reaches skip it), and lsort_fixup sorts the listed groups' members by one global radix
-// sort on (group, local digits). Runs only after a flagged local sort (no cost otherwise).
-__global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort_fix(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
-                                                           uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t n,
-                                                           uint64_t gmask, uint32_t lpos, uint32_t nloc,
-                                                           const uint32_t *__restrict__ bounds, uint32_t *__restrict__ gs,
-                                                           uint32_t *__restrict__ ge, uint32_t cap, uint32_t *__restrict__ cnt) {
-    __shared__ LsShared sh_;
-    __shared__ uint32_t s_agg[LS_BLOCK / 64];
-    const uint32_t t = blockIdx.x, tid = threadIdx.x;
-    const uint32_t b0 = bounds[t], b1 = bounds[t + 1];
+// The tiles k_rs_lsort listed (a group of equal top digits larger than the LDS lies in them,
+// or the tile edge cuts one far enough), redone from the same input right behind it, a few
+// blocks walking the list (cost proportional to the listed tiles, no host round trip):
+// windows of whole groups (<= LS_CAP pairs) are sorted in LDS as usual; every group too large
+// for a window ("big group", e.g. one record repeated thousands of times) is copied and listed
+// (gs, ge: its position range, appended by the block that holds its first position; the
+// blocks its tail reaches skip it; cnt: how many), and lsort_fixup_big sorts the listed
+// groups' members by one global radix sort on (group, local digits) — the only case the host
+// sees (cnt comes back with the dedup's counts).
+__device__ void ls_fix_tile(const uint64_t *__restrict__ K, const uint2 *__restrict__ V, uint64_t *__restrict__ Ko,
+                            uint2 *__restrict__ Vo, uint32_t n, uint64_t gmask, uint32_t lpos, uint32_t nloc, uint32_t b0,
+                            uint32_t b1, uint32_t *__restrict__ gs, uint32_t *__restrict__ ge, uint32_t cap,
+                            uint32_t *__restrict__ cnt, LsShared &sh_, uint32_t *s_agg) {
+    const uint32_t tid = threadIdx.x;
     const uint32_t s = b0 & 0x7fffffffu, e = max(b1 & 0x7fffffffu, s);
-    if (e - s == 0 || !(e - s > (uint32_t)LS_CAP || !(b0 >> 31) || !(b1 >> 31))) return;  // sorted by k_rs_lsort
     const bool e_real = (b1 >> 31) != 0;
     auto is_head = [&](uint32_t i) -> bool { return i >= n || ((K[i] ^ K[i - 1]) & gmask) != 0; };
     // the first group start in [from, lim) (lim when none); from >= 1
@@ -663,6 +700,22 @@ __global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort_fix(const uint64_t *__res
             if (k < cap) { gs[k] = p; ge[k] = q; }
         }
         p = q;  // >= e ends the tile
+    }
+}
+
+__global__ __launch_bounds__(LS_BLOCK) void k_rs_lsort_fix(const uint64_t *__restrict__ K, const uint2 *__restrict__ V,
+                                                           uint64_t *__restrict__ Ko, uint2 *__restrict__ Vo, uint32_t n,
+                                                           uint64_t gmask, uint32_t lpos, uint32_t nloc,
+                                                           const uint32_t *__restrict__ bounds,
+                                                           const uint32_t *__restrict__ flist,
+                                                           const uint32_t *__restrict__ fcnt, uint32_t *__restrict__ gs,
+                                                           uint32_t *__restrict__ ge, uint32_t cap, uint32_t *__restrict__ cnt) {
+    __shared__ LsShared sh_;
+    __shared__ uint32_t s_agg[LS_BLOCK / 64];
+    const uint32_t nf = *fcnt;  // final: k_rs_lsort completed before this launch
+    for (uint32_t j = blockIdx.x; j < nf; j += gridDim.x) {
+        const uint32_t t = flist[j];
+        ls_fix_tile(K, V, Ko, Vo, n, gmask, lpos, nloc, bounds[t], bounds[t + 1], gs, ge, cap, cnt, sh_, s_agg);
     }
 }
 
@@ -715,7 +768,14 @@ struct LfixSizeFn {
 // groups of about 2^HY_SLACK_BITS pairs; hybrid only when 2..4 live digits remain below
 // them (each one a global pass saved). top[]: the global passes (LSD order), lpos/nloc: the
 // local key's digit positions.
-constexpr double HY_SLACK_BITS = 8.0;
+// 10 bits (round 6; 8 before): C5's 52M-record parts take 4 global passes instead of 5 and
+// finish groups of ~600 pairs in LDS (one more local pass, ~2.7 ms per step, against ~6 ms per
+// global pass); with 3,072-pair base tiles no C5 tile outgrows a window (3,584: ~2 % did, and
+// the fix-up pass then cost 1.7 ms). C5 179.9 -> 173.9 ms, C2 unchanged (1.596 / 1.592).
+#ifndef SG_HY_SLACK
+#define SG_HY_SLACK 10.0
+#endif
+constexpr double HY_SLACK_BITS = SG_HY_SLACK;
 struct HybridPlan {
     bool on = false;
     int top[RS_MAXPASS];
@@ -826,44 +886,67 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     }
     const int *passes = hp.on ? hp.top : live;
     const int npass = hp.on ? hp.ntop : nlive;
+    // every pass after the first counts its tiles from the digit bytes its predecessor wrote
+    uint8_t *dig = nullptr;
+    if (npass > 1) SG_TRY(slot(c, S_RS_DIGITS, (size_t)n + 16, &dig));
     for (int q = 0; q < npass; ++q) {
         const int p = passes[q];
         const int shift = begin_bit + 8 * p;
         const uint32_t kw = q == 0 ? narrow_kw : 0u;  // the first pass narrows as it reads
-        SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, grid, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, kw, xcd);
+        if (q == 0 || !dig) SG_LAUNCH_B(c, "rs_up", 8.0 * n, k_rs_up, grid, RD_BLOCK, 0, ck, n, shift, ntiles, tcnt, kw, xcd);
+        else SG_LAUNCH_B(c, "rs_up", 1.0 * n, k_rs_up8, grid, RD_BLOCK, 0, dig, n, ntiles, tcnt, xcd);
         if (dtot) SG_LAUNCH(c, "rs_dsum", k_rs_dsum, 256, 256, 0, tcnt, ntiles, dtot);
         SG_LAUNCH(c, "rs_cscan", k_rs_cscan, 256, 256, 0, tcnt, ntiles, offs + p * 256, dtot);
+        uint8_t *dn = q + 1 < npass ? dig : nullptr;
+        const int shn = q + 1 < npass ? begin_bit + 8 * passes[q + 1] : 0;
         if constexpr (sizeof(VT) == 4) {
             if (iota_pending)
-                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
+                SG_LAUNCH(c, pass_name, (k_rs_down<true, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd,
+                          dn, shn);
             else
-                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
+                SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw,
+                          xcd, dn, shn);
         } else {
-            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd);
+            SG_LAUNCH(c, pass_name, (k_rs_down<false, VT>), grid, RD_BLOCK, 0, ck, cv, ak, av, n, shift, ntiles, tcnt, kw, xcd,
+                      dn, shn);
         }
-        // 8 B key + the value read (implied for iota ids) and both written, per pair
-        prof_bytes(c, pass_name, (iota_pending ? 16.0 + VB : 16.0 + 2.0 * VB) * n);
+        // 8 B key + the value read (implied for iota ids) and both written, per pair (+ the
+        // next pass's digit byte)
+        prof_bytes(c, pass_name, (iota_pending ? 16.0 + VB : 16.0 + 2.0 * VB) * n + (dn ? 1.0 * n : 0.0));
         iota_pending = false;
         uint64_t *tk = ck; ck = ak; ak = tk;
         VT *tv = cv; cv = av; av = tv;
     }
     if constexpr (sizeof(VT) == 8) {
         if (hp.on) {
+            // err[0]: big groups the fix-up listed (the caller reads it back), err[1]: tiles
+            // it redid
             uint32_t *err = err_at;
-            if (!err) SG_TRY(slot(c, S_LS_ERR, 1, &err));
+            if (!err) SG_TRY(slot(c, S_LS_ERR, 2, &err));
             const uint32_t g = (n + LS_T - 1) / LS_T;
             uint32_t *bounds;
             SG_TRY(slot(c, S_LS_BOUNDS, (size_t)g + 1, &bounds));
+            // the fix-up's lists: flagged tiles (g), big groups' ranges (cap each)
+            const uint32_t cap = g + 16;
+            uint32_t *lst;
+            SG_TRY(slot(c, S_LS_LIST, (size_t)g + 2 * (size_t)cap + 16, &lst));
+            uint32_t *flist = lst, *gs = lst + g, *ge = gs + cap;
             SG_LAUNCH(c, "rs_lbounds", k_rs_lbounds, (g + 1 + 3) / 4, 256, 0, ck, n, hp.gmask, g + 1, bounds, err);
             // model: key read, key + span fetched in sorted order, both written
             SG_LAUNCH_B(c, "rs_lsort", 40.0 * n, k_rs_lsort, g, LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask, hp.lpos, hp.nloc,
-                        bounds, err);
+                        bounds, flist, err + 1);
+            // the listed tiles redone from the same input by a few blocks walking the list
+            SG_LAUNCH(c, "rs_lfix", k_rs_lsort_fix, std::min<uint32_t>(g, 256u), LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask,
+                      hp.lpos, hp.nloc, bounds, flist, err + 1, gs, ge, cap, err);
             c->ls_last.on = true;
             c->ls_last.gmask = hp.gmask;
             c->ls_last.lpos = hp.lpos;
             c->ls_last.nloc = hp.nloc;
             c->ls_last.ntiles = g;
             c->ls_last.bounds = bounds;
+            c->ls_last.gs = gs;
+            c->ls_last.ge = ge;
+            c->ls_last.cap = cap;
             uint64_t *tk = ck; ck = ak; ak = tk;
             VT *tv = cv; cv = av; av = tv;
             *lsort_err = err;
@@ -881,20 +964,12 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
     return SG_OK;
 }
 
-int lsort_fixup(sg_ctx *c, const uint64_t *Kin, const uint2 *Vin, uint64_t *Ko, uint2 *Vo, uint32_t n) {
+int lsort_fixup_big(sg_ctx *c, const uint64_t *Kin, const uint2 *Vin, uint64_t *Ko, uint2 *Vo, uint32_t n, uint32_t B) {
     const auto &P = c->ls_last;
     if (!P.on) { set_error("lsort_fixup: no hybrid sort to fix"); return SG_E_INVAL; }
-    const uint32_t g = P.ntiles, cap = g + 16;
-    uint32_t *lst;
-    SG_TRY(slot(c, S_LS_LIST, 2 * (size_t)cap + 16, &lst));
-    uint32_t *gs = lst, *ge = lst + cap, *cnt = lst + 2 * (size_t)cap;
-    SG_HIP(hipMemsetAsync(cnt, 0, 4, c->stream));
-    SG_LAUNCH(c, "rs_lfix", k_rs_lsort_fix, g, LS_BLOCK, 0, Kin, Vin, Ko, Vo, n, P.gmask, P.lpos, P.nloc, P.bounds, gs, ge,
-              cap, cnt);
-    uint32_t B = 0;
-    SG_TRY(ctx_readback(c, &B, cnt, 4));
-    if (B > cap) { set_error("lsort_fixup: %u big groups (list of %u)", B, cap); return SG_E_HIP; }
+    if (B > P.cap) { set_error("lsort_fixup: %u big groups (list of %u)", B, P.cap); return SG_E_HIP; }
     if (!B) return SG_OK;
+    const uint32_t *gs = P.gs, *ge = P.ge;
     // the big groups' members: one stable radix sort on (group, local digits)
     uint64_t *goff;
     SG_TRY(slot(c, S_LF_OFF, (size_t)B + 1, &goff));

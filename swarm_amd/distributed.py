@@ -30,6 +30,16 @@ from typing import List, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from . import _abi
+
+_U64 = (1 << 64) - 1
+
+
+def _i64(v: int) -> int:
+    """A uint64 (a handover checksum) as the int64 with the same bits, for an int64 tensor."""
+    v = int(v) & _U64
+    return v - (1 << 64) if v >> 63 else v
+
 
 def host_staged(group=None) -> bool:
     """gloo rehearsals (several ranks sharing one GPU, or CPU tests): the collectives take host
@@ -292,7 +302,9 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
     spans: every record's parse travels with its bytes (its span, relative to its source's
     bytes, and its first-chunk key: 16 B per record, written by the routing pass itself), so
     the receiver dedups the round without parsing it again; the 4th element of a round is
-    then (spans, keys, [first record, byte offset] per source) for rebase_spans, else None.
+    then (spans, keys, [first record, byte offset] per source, handover checksum) — the
+    segments for rebase_spans, the checksum (the sources' part sums, which travel with the
+    sizes) for dedup_diff_spans_into, which checks the parse against it — else None.
     force_exchange: issue the size exchange and the per-round all-to-alls even at world size 1
     (a 1-rank RCCL group on one GPU runs the device-tensor collective path of the N-rank step;
     without it a single rank skips the collectives)."""
@@ -313,15 +325,16 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
             nrec = ctx.partition_pieces_count(plist)
             ssp = torch.empty(2 * max(nrec, 1), dtype=torch.int32, device=dev)
             skey = torch.empty(max(nrec, 1), dtype=torch.int64, device=dev)
-            pb, pr = ctx.partition_bytes_pieces_rounds_spans(plist, splitters, rounds, send.data_ptr(), send.numel(),
-                                                             ssp.data_ptr(), skey.data_ptr(), nrec)
+            pb, pr, ps = ctx.partition_bytes_pieces_rounds_spans(plist, splitters, rounds, send.data_ptr(),
+                                                                 send.numel(), ssp.data_ptr(), skey.data_ptr(), nrec)
         else:
             pb, pr = ctx.partition_bytes_pieces_rounds(plist, splitters, rounds, send.data_ptr(), send.numel())
+            ps = [0] * nparts
         # the partition's copy pass is queued on the ctx stream and the call returns after the
         # size read-back only: drain it before a collective (on another stream) reads send
         ctx.fence_out()
     else:
-        pb, pr = [0] * nparts, [0] * nparts
+        pb, pr, ps = [0] * nparts, [0] * nparts, [0] * nparts
         if spans:
             ssp = torch.empty(2, dtype=torch.int32, device=dev)
             skey = torch.empty(1, dtype=torch.int64, device=dev)
@@ -338,19 +351,22 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
             par = None
             if spans:
                 r0, nr = rround[p], int(pr[p])
-                par = (ssp[2 * r0:2 * (r0 + nr)], skey[r0:r0 + nr], [[0, 0]])
+                par = (ssp[2 * r0:2 * (r0 + nr)], skey[r0:r0 + nr], [[0, 0]], int(ps[p]))
             out.append((None, send[offs[p]:offs[p] + pb[p]], int(pr[p]), par))
         return out, (send, ssp, skey)
-    # per peer g: the bytes, then the records, of its rounds parts g * rounds .. + rounds - 1
-    # (contiguous in pb / pr); back: rc2[s * 2R + p] bytes and rc2[s * 2R + R + p] records that
-    # source s sends this rank in round p
+    # per peer g: the bytes, the records and the handover checksums of its rounds parts
+    # g * rounds .. + rounds - 1 (contiguous in pb / pr / ps); back: rc2[s * 3R + p] bytes,
+    # rc2[s * 3R + R + p] records and rc2[s * 3R + 2R + p] the checksum that source s sends this
+    # rank in round p (checksums as int64 two's complement)
     R = rounds
     cnt = []
     for g in range(world):
         cnt += [int(x) for x in pb[g * R:(g + 1) * R]] + [int(x) for x in pr[g * R:(g + 1) * R]]
+        cnt += [_i64(x) for x in ps[g * R:(g + 1) * R]]
     rc2 = exchange_counts(cnt, group)
-    rc = [rc2[s * 2 * R + p] for s in range(world) for p in range(R)]
-    rcr = [rc2[s * 2 * R + R + p] for s in range(world) for p in range(R)]
+    rc = [rc2[s * 3 * R + p] for s in range(world) for p in range(R)]
+    rcr = [rc2[s * 3 * R + R + p] for s in range(world) for p in range(R)]
+    rcs = [rc2[s * 3 * R + 2 * R + p] & _U64 for s in range(world) for p in range(R)]
     rrec = [sum(rcr[s * R + p] for s in range(world)) for p in range(R)]
     offs = round_offsets(pb, rounds)
     # the largest message of any round on any rank (bytes, and 8 B per record for the spans
@@ -380,7 +396,7 @@ def exchange_rounds(ctx, pieces: Sequence[torch.Tensor], splitters, rounds: int,
                 segs.append([fr, fo])
                 fr += outs_r[s_]
                 fo += outs[s_]
-            par = (rsp[:2 * nout], rk[:nout], segs)
+            par = (rsp[:2 * nout], rk[:nout], segs, sum(rcs[s_ * rounds + p] for s_ in range(world)) & _U64)
         out.append((w, recv, rrec[p], par))
     return out, (send, ssp, skey)
 
@@ -408,24 +424,34 @@ def dedup_diff_rounds_step(ctx, cur_pieces, prior_parts, splitters, rounds: int,
             w.wait()
         before = st["in_records"]
         parse = None
-        if par is not None and want:
-            rsp, rk, segs = par
-            # the spans arrive relative to each source's bytes: rebased to this buffer, and
-            # every record checked to end before a '\n' (the routing '\n'-terminated them)
-            if w is not None or len(segs) > 1 or segs[0][1]:
+        if par is not None and (want or recv.numel()):
+            rsp, rk, segs, ssum = par
+            # the spans arrive relative to each source's bytes: rebased to this buffer, and each
+            # source's first and last records checked to end before a '\n' (a short or stale
+            # message is reported here, at its tail)
+            if want and (w is not None or len(segs) > 1 or segs[0][1]):
                 ctx.fence_in()
                 bad = ctx.rebase_spans(recv.data_ptr(), recv.numel(), rsp.data_ptr(), want, [x[0] for x in segs],
                                        [x[1] for x in segs])
                 if bad:
                     raise RuntimeError("exchange round %d: %d of %d records do not end at a newline of the %d "
                                        "received bytes: the transfer is corrupt" % (p, bad, want, recv.numel()))
-            parse = (rsp.data_ptr(), rk.data_ptr(), want)
-        sharded.dedup_part(ctx, recv if recv.numel() else None, prior_parts[p] if have_prior else None, out, st,
-                           parse=parse)
-        # the senders' routed record counts travel with the sizes: a transfer that delivered
-        # other bytes (round 4: this image's RCCL left half of a 1.5 GB message unwritten)
-        # fails loudly here instead of deduping whatever the buffer held
-        if st["in_records"] - before != want:
+            # every record's span and key is then checked by the dedup itself before any kernel
+            # reads a byte through them (records tile the buffer, the senders' checksum, sampled
+            # newlines and keys; include/swarmgpu.h sg_dev_dedup_diff_spans_into)
+            parse = (rsp.data_ptr(), rk.data_ptr(), want, ssum)
+        try:
+            sharded.dedup_part(ctx, recv if recv.numel() else None, prior_parts[p] if have_prior else None, out, st,
+                               parse=parse)
+        except _abi.SGError as e:
+            if e.rc != _abi.SG_E_CORRUPT:
+                raise
+            raise RuntimeError("exchange round %d: the parse handed over with %d records / %d bytes does not match "
+                               "them: the transfer is corrupt (%s)" % (p, want, recv.numel(), e)) from e
+        # without the parse handed over, the dedup parsed the bytes itself: its record count
+        # must be the one the senders routed (round 4: this image's RCCL left half of a 1.5 GB
+        # message unwritten; a transfer that delivered other bytes fails here)
+        if parse is None and st["in_records"] - before != want:
             raise RuntimeError("exchange round %d: %d records arrived, the senders routed %d (%d bytes): the "
                                "transfer is corrupt" % (p, st["in_records"] - before, want, recv.numel()))
     del send, recvd

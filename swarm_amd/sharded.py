@@ -143,8 +143,9 @@ def route(ctx, pieces: Sequence, splitters) -> List:
 
 def route_spans(ctx, pieces: Sequence, splitters):
     """route() with byte splitters that also returns every part's parse from the routing
-    pass: (parts, [(device spans, device keys, records) or None per part]). The parse lives
-    in context buffers until the next route_spans call on ctx."""
+    pass: (parts, [(device spans, device keys, records, handover checksum) or None per part]).
+    The parse lives in context buffers until the next route_spans call on ctx; the dedup checks
+    it against the part's bytes and the checksum before using it."""
     import torch
     parts = n_splitters(splitters) + 1
     live = [p for p in pieces if p is not None and p.numel()]
@@ -153,12 +154,12 @@ def route_spans(ctx, pieces: Sequence, splitters):
     total = sum(p.numel() for p in live)
     out = torch.empty(total + len(live) + 16 * (parts + 1), dtype=torch.uint8, device=live[0].device)
     ctx.fence_in()
-    pb, pr, sp, kp = ctx.partition_bytes_pieces_spans([(p.data_ptr(), p.numel()) for p in live], splitters,
-                                                      out.data_ptr(), out.numel())
+    pb, pr, sp, kp, ps = ctx.partition_bytes_pieces_spans([(p.data_ptr(), p.numel()) for p in live], splitters,
+                                                          out.data_ptr(), out.numel())
     res, parse, r0 = [], [], 0
-    for o, n, nr in zip(part_offsets(pb, align16=True), pb, pr):
+    for o, n, nr, s in zip(part_offsets(pb, align16=True), pb, pr, ps):
         res.append(out[o:o + n] if n else None)
-        parse.append((sp + 8 * r0, kp + 8 * r0, nr) if n else None)
+        parse.append((sp + 8 * r0, kp + 8 * r0, nr, s) if n else None)
         r0 += nr
     return res, parse
 
@@ -284,8 +285,9 @@ def dedup_part(ctx, c, p, out, st, samples_per_piece: int = 1 << 12, depth: int 
                 (out.f.data_ptr() + out.fo) if out.f is not None else 0,
                 (out.f.numel() - out.fo) if out.f is not None else 0)
         if parse is not None:
-            sp, kp, nr = parse
-            r = ctx.dedup_diff_spans_into(c.data_ptr(), c.numel(), sp, kp, nr, p.data_ptr() if pn else 0, pn, *outs)
+            sp, kp, nr, ssum = parse
+            r = ctx.dedup_diff_spans_into(c.data_ptr(), c.numel(), sp, kp, nr, ssum, p.data_ptr() if pn else 0, pn,
+                                          *outs)
         else:
             r = ctx.dedup_diff_into(c.data_ptr(), c.numel(), p.data_ptr() if pn else 0, pn, *outs)
     except Exception as e:

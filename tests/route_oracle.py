@@ -105,6 +105,45 @@ def _i64(v: int) -> int:
     return v - (1 << 64) if v >= 1 << 63 else v
 
 
+M64 = (1 << 64) - 1
+
+
+def span_mix(length: int, key: int) -> int:
+    """include/swarmgpu.h sg_span_sum's per-record term restated: h = (key + length *
+    0x9E3779B97F4A7C15) * 0xBF58476D1CE4E5B9 (mod 2^64), then h ^ h >> 31."""
+    h = ((key + length * 0x9E3779B97F4A7C15) * 0xBF58476D1CE4E5B9) & M64
+    return h ^ (h >> 31)
+
+
+def span_sum(spans, keys) -> int:
+    """sg_span_sum restated: sum mod 2^64 of span_mix(end - start, key) over the records."""
+    return sum(span_mix(e - a, k & M64) for (a, e), k in zip(spans, keys)) & M64
+
+
+CHK_SAMPLE = 256
+
+
+def check_handover(buf: bytes, spans, keys, expect_sum: int) -> str:
+    """sg_dev_dedup_diff_spans_into's check of a handed-over parse restated: '' when it holds,
+    else why not (records tile the buffer, the checksum, every CHK_SAMPLE-th record's '\n'
+    and key)."""
+    n = len(buf)
+    if not spans:
+        return "" if n == 0 and (expect_sum & M64) == 0 else "no records for %d bytes" % n
+    prev = -1
+    for i, (a, e) in enumerate(spans):
+        if not (a == prev + 1 and e > a and e < n):
+            return "record %d (%d, %d) out of place" % (i, a, e)
+        prev = e
+        if i % CHK_SAMPLE == 0 and (buf[e] != 0x0A or key0(buf[a:e]) != keys[i] & M64):
+            return "record %d does not match its bytes" % i
+    if prev != n - 1:
+        return "records end at %d of %d bytes" % (prev + 1, n)
+    if span_sum(spans, keys) != expect_sum & M64:
+        return "checksum mismatch"
+    return ""
+
+
 def _fake_pieces_count(self, pieces):
     return sum(len(S.parse_records(ctypes.string_at(p, n) if n else b"")) for p, n in pieces)
 
@@ -116,6 +155,7 @@ def _fake_rounds_spans(self, pieces, splitters, rounds, out_ptr, cap, sp_ptr, k_
     pb, pr = self.partition_bytes_pieces_rounds(pieces, splitters, rounds, out_ptr, cap)
     nparts = len(pb)
     G = nparts // rounds
+    ps = [0] * nparts
     # the parts' bytes as written (round-major), read back
     off, r = 0, 0
     sp = (ctypes.c_uint32 * (2 * max(rec_cap, 1))).from_address(sp_ptr)
@@ -129,35 +169,45 @@ def _fake_rounds_spans(self, pieces, splitters, rounds, out_ptr, cap, sp_ptr, k_
                 assert r < rec_cap
                 sp[2 * r], sp[2 * r + 1] = a, e
                 kk[r] = _i64(key0(b[a:e]))
+                ps[q] = (ps[q] + span_mix(e - a, key0(b[a:e]))) & M64
                 r += 1
             off += pb[q]
-    return pb, pr
+    return pb, pr, ps
+
+
+REBASE_CHECK = 256
 
 
 def _fake_rebase(self, buf_ptr, n, sp_ptr, n_rec, seg_first, seg_off):
+    """sg_dev_rebase_spans restated: every span shifted by its source's offset, each source's
+    first and last REBASE_CHECK records checked to end at a '\n' of the buffer."""
     sp = (ctypes.c_uint32 * (2 * max(n_rec, 1))).from_address(sp_ptr)
     buf = ctypes.string_at(buf_ptr, n) if n else b""
+    first = list(seg_first) if seg_first else [0]
     bad = 0
-    for i in range(n_rec):
-        s = max(j for j in range(len(seg_first)) if seg_first[j] <= i) if seg_first else 0
+    for s, f in enumerate(first):
+        e_ = first[s + 1] if s + 1 < len(first) else n_rec
         o = seg_off[s] if seg_off else 0
-        sp[2 * i] += o
-        sp[2 * i + 1] += o
-        a, e = sp[2 * i], sp[2 * i + 1]
-        bad += 0 if (a <= e < n and buf[e] == 0x0A) else 1
+        for i in range(f, e_):
+            sp[2 * i] += o
+            sp[2 * i + 1] += o
+            if i - f < REBASE_CHECK or e_ - i <= REBASE_CHECK:
+                a, e = sp[2 * i], sp[2 * i + 1]
+                bad += 0 if (a <= e < n and buf[e] == 0x0A) else 1
     return bad
 
 
-def _fake_spans_into(self, cur_ptr, n, sp_ptr, k_ptr, n_rec, prior_ptr, pn, u_ptr, ucap, f_ptr, fcap):
-    """sg_dev_dedup_diff_spans_into restated: the handed-over parse must be the buffer's own
-    (spans and keys checked against the oracle's parse), then dedup_diff_into."""
+def _fake_spans_into(self, cur_ptr, n, sp_ptr, k_ptr, n_rec, ssum, prior_ptr, pn, u_ptr, ucap, f_ptr, fcap):
+    """sg_dev_dedup_diff_spans_into restated: the library's check of the handed-over parse
+    (check_handover: SG_E_CORRUPT when it fails), then dedup_diff_into."""
+    from swarm_amd import _abi
     cur = ctypes.string_at(cur_ptr, n) if n else b""
     sp = (ctypes.c_uint32 * (2 * max(n_rec, 1))).from_address(sp_ptr)
     kk = (ctypes.c_int64 * max(n_rec, 1)).from_address(k_ptr)
-    want = S.record_spans(cur)
     got = [(sp[2 * i], sp[2 * i + 1]) for i in range(n_rec)]
-    assert got == want, "handed-over spans differ from the parse"
-    assert all(kk[i] == _i64(key0(cur[a:e])) for i, (a, e) in enumerate(got)), "handed-over keys differ"
+    why = check_handover(cur, got, [kk[i] & M64 for i in range(n_rec)], ssum)
+    if why:
+        raise _abi.SGError(_abi.SG_E_CORRUPT, "handed-over parse does not match the buffer: " + why)
     self.log.append("spans_into")
     return self.dedup_diff_into(cur_ptr, n, prior_ptr, pn, u_ptr, ucap, f_ptr, fcap)
 

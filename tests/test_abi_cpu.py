@@ -40,6 +40,33 @@ def test_hash64_host_matches_restatement(rec):
     assert hash64(rec) == py_hash64(rec)
 
 
+def test_span_sum_host_matches_restatement():
+    """sg_span_sum (the handover checksum the partition returns and the dedup checks) equals
+    its restatement in route_oracle, keys with the top bit set included; order-free."""
+    import random
+    import numpy as np
+    from route_oracle import key0, span_sum as py_span_sum
+    from swarm_amd.api import span_sum
+    rng = random.Random(3)
+    recs = [bytes(rng.randrange(256) for _ in range(rng.randrange(1, 40))) for _ in range(500)]
+    recs = [r.replace(b"\n", b"x") for r in recs] + [b"\xff" * 9, b"a"]
+    spans, keys, off = [], [], 0
+    for r in recs:
+        spans.append((off, off + len(r)))
+        keys.append(key0(r))
+        off += len(r) + 1
+    sp = np.array(spans, dtype=np.uint32)
+    k = np.array(keys, dtype=np.uint64)
+    want = py_span_sum(spans, keys)
+    assert span_sum(sp, k) == want
+    perm = np.random.default_rng(4).permutation(len(recs))
+    assert span_sum(sp[perm], k[perm]) == want
+    assert span_sum(np.zeros((0, 2), np.uint32), np.zeros(0, np.uint64)) == 0
+    k2 = k.copy()
+    k2[7] ^= np.uint64(1)
+    assert span_sum(sp, k2) != want
+
+
 def test_no_gpu_fails_loudly_not_silently():
     """Without a device the product path raises instead of computing on the CPU."""
     from swarm_amd import device_count, dedup

@@ -364,10 +364,12 @@ def test_match_step_gloo(world):
         assert lines == S.matched_lines(data, hits)
 
 
-def corrupt_worker(port, out_q):
-    """A transfer that leaves the upper half of a round's receive buffer unwritten (what this
-    image's RCCL does with a 1.5 GB message, tools/rccl_probe.py detail): the rounds step must
-    raise, not dedup the stale bytes."""
+def corrupt_worker(port, out_q, mode="half"):
+    """A transfer that arrives damaged: "half" leaves the upper half of a round's receive
+    buffer unwritten (what this image's RCCL does with a 1.5 GB message, tools/rccl_probe.py
+    detail); "key" changes one record's key and "span" one record's end in the middle of a
+    round (outside the records the rebase samples); "tail" drops the last record's span. The
+    rounds step must raise, not dedup what arrived."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=0, world_size=1)
     from route_oracle import FakeCtx
@@ -377,15 +379,28 @@ def corrupt_worker(port, out_q):
     prior_raw = b"".join(b"https://h%d.example.com/\n" % i for i in range(0, 2500, 3))
     split = D.agree_splitters(ctx, [t(prior_raw)], 2, samples_per_piece=64)
     real = D.all_to_all_bytes
+    calls = [0]
 
-    def half(recv, send, outs, ins, group=None, async_op=False, global_max=None):
+    def damaged(recv, send, outs, ins, group=None, async_op=False, global_max=None):
         w = real(recv, send, outs, ins, group, async_op, global_max)
         if w is not None:
             w.wait()
-        recv[recv.numel() // 2:] = 0
+        k = calls[0]  # per round: the bytes, then the spans, then the keys
+        calls[0] += 1
+        if mode == "half" and k % 3 == 0:
+            recv[recv.numel() // 2:] = 0
+        elif mode == "key" and k == 2:
+            kk = recv.view(torch.int64)
+            kk[kk.numel() // 2] ^= 1 << 20
+        elif mode == "span" and k == 1:
+            sp = recv.view(torch.int32)
+            sp[2 * (sp.numel() // 4) + 1] += 1
+        elif mode == "tail" and k == 1:
+            sp = recv.view(torch.int32)
+            sp[-1] -= 1
         return None
 
-    D.all_to_all_bytes = half
+    D.all_to_all_bytes = damaged
     try:
         D.dedup_diff_rounds_step(ctx, [t(c) for c in rounds_shard(0, 1)], None, split, 2, force_exchange=True)
         out_q.put("no error")
@@ -394,10 +409,11 @@ def corrupt_worker(port, out_q):
     dist.destroy_process_group()
 
 
-def test_rounds_step_detects_corrupt_transfer():
+@pytest.mark.parametrize("mode", ["half", "key", "span", "tail"])
+def test_rounds_step_detects_corrupt_transfer(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=corrupt_worker, args=(free_port(), q))
+    p = ctx.Process(target=corrupt_worker, args=(free_port(), q, mode))
     p.start()
     msg = q.get(timeout=120)
     p.join(timeout=60)

@@ -322,7 +322,8 @@ def test_partition_spans_handover(ctx):
     fed that parse (dedup_diff_spans_into) equals the oracle's sort -u / comm -13 per part."""
     import swarm_amd
     import torch
-    from swarm_amd.api import part_offsets
+    from swarm_amd.api import part_offsets, span_sum
+    from route_oracle import key0, span_sum as py_span_sum
     recs = shared_prefix_records(25_000, 17) + [b"", b"x", b"x" * 300]
     random.Random(18).shuffle(recs)
     data = b"\n".join(recs) + b"\n"
@@ -332,23 +333,27 @@ def test_partition_spans_handover(ctx):
     pieces = [d[1 + a:1 + b] for a, b in zip(cuts, cuts[1:])]
     sp = sorted(random.Random(19).sample([r for r in recs if r], 9))
     out = torch.full((len(data) + 16 * 11 + 64,), 0x55, dtype=torch.uint8, device=d.device)
-    pb, pr, dsp, dkp = ctx.partition_bytes_pieces_spans([(p.data_ptr(), p.numel()) for p in pieces], sp,
-                                                        out.data_ptr(), out.numel())
+    pb, pr, dsp, dkp, ps = ctx.partition_bytes_pieces_spans([(p.data_ptr(), p.numel()) for p in pieces], sp,
+                                                            out.data_ptr(), out.numel())
     nrec = sum(pr)
     spans = np.frombuffer(ctx.to_bytes(dsp, 8 * nrec), dtype=np.uint32).reshape(-1, 2)
+    keys = np.frombuffer(ctx.to_bytes(dkp, 8 * nrec), dtype=np.uint64)
     got = out.cpu().numpy().tobytes()
     prior_recs = sorted(set(random.Random(20).sample([r for r in recs if r], 5000)))
     r0 = 0
-    for o, n, nr in zip(part_offsets(pb, align16=True), pb, pr):
+    for o, n, nr, ssum in zip(part_offsets(pb, align16=True), pb, pr, ps):
         part = got[o:o + n]
         assert np.array_equal(spans[r0:r0 + nr].astype(np.uint64), swarm_amd.lines(part))
+        # the part's handover checksum, as the restatement computes it from the part's bytes
+        assert ssum == py_span_sum(S.record_spans(part), [key0(part[a:e]) for a, e in S.record_spans(part)])
+        assert ssum == span_sum(spans[r0:r0 + nr], keys[r0:r0 + nr])
         if n:
             lo, hi = S.parse_records(part)[0], S.parse_records(part)[-1]
             prior = b"".join(r + b"\n" for r in prior_recs if lo <= r <= hi)
             dp = dev(prior)
             ub = torch.empty(n + 64, dtype=torch.uint8, device=d.device)
             fb = torch.empty(n + 64, dtype=torch.uint8, device=d.device)
-            r = ctx.dedup_diff_spans_into(out.data_ptr() + o, n, dsp + 8 * r0, dkp + 8 * r0, nr, dp.data_ptr(),
+            r = ctx.dedup_diff_spans_into(out.data_ptr() + o, n, dsp + 8 * r0, dkp + 8 * r0, nr, ssum, dp.data_ptr(),
                                           len(prior), ub.data_ptr() + 3, n + 1, fb.data_ptr() + 5, n + 1)
             eu, ef = S.dedup_diff(part, prior)
             assert ctx.to_bytes(r.uniq, r.uniq_bytes) == eu
@@ -415,16 +420,17 @@ def test_partition_pieces_rounds_spans(ctx, world, rounds):
     out = torch.full((cap + 64,), 0x55, dtype=torch.uint8, device=d.device)
     dsp = torch.zeros(2 * nrec, dtype=torch.int32, device=d.device)
     dk = torch.zeros(nrec, dtype=torch.int64, device=d.device)
-    pb, pr = ctx.partition_bytes_pieces_rounds_spans(plist, sp, rounds, out.data_ptr(), cap, dsp.data_ptr(),
-                                                     dk.data_ptr(), nrec)
+    pb, pr, ps = ctx.partition_bytes_pieces_rounds_spans(plist, sp, rounds, out.data_ptr(), cap, dsp.data_ptr(),
+                                                         dk.data_ptr(), nrec)
     hp = [np.frombuffer(bytearray(data[a:b] or b"\0"), dtype=np.uint8) for a, b in zip(cuts, cuts[1:])]
     wb = np.full(cap + 64, 0x55, dtype=np.uint8)
     wsp = np.zeros(2 * nrec, dtype=np.uint32)
     wk = np.zeros(nrec, dtype=np.int64)
-    wpb, wpr = FakeCtx().partition_bytes_pieces_rounds_spans([(h.ctypes.data, b - a) for h, (a, b) in
-                                                              zip(hp, zip(cuts, cuts[1:]))], sp, rounds, wb.ctypes.data,
-                                                             cap, wsp.ctypes.data, wk.ctypes.data, nrec)
-    assert (pb, pr) == (wpb, wpr)
+    wpb, wpr, wps = FakeCtx().partition_bytes_pieces_rounds_spans([(h.ctypes.data, b - a) for h, (a, b) in
+                                                                   zip(hp, zip(cuts, cuts[1:]))], sp, rounds,
+                                                                  wb.ctypes.data, cap, wsp.ctypes.data, wk.ctypes.data,
+                                                                  nrec)
+    assert (pb, pr, ps) == (wpb, wpr, wps)
     assert out.cpu().numpy().tobytes() == wb.tobytes()
     assert np.array_equal(dsp.cpu().numpy().view(np.uint32), wsp)
     assert np.array_equal(dk.cpu().numpy(), wk)
