@@ -635,7 +635,8 @@ def bench_c5(args, world=1, rank=0, dev=None, ctx=None, emit=True):
             "hbm_frac_step": round(step_bytes * args.steps / el / 1e9 / (HBM_PEAK_GBS * world), 4),
             "records": {"in_rank0": st["in_records"], "unique_rank0": st["uniq_records"],
                         "new_rank0": st["fresh_records"], "max_part_bytes": st["max_part_bytes"]},
-            "roofline": roofline_of(stats, dominant, "c5", full),
+            # the rounds path's traffic from its own PMC passes (profiles/pmc_traffic.json "c5r")
+            "roofline": roofline_of(stats, dominant, "c5" if world == 1 and args.c5_path == "local" else "c5r", full),
             "cpu_baseline": cpu,
             "kernels": kernel_table(full),
             "kernels_note": "per-kernel table from one fully profiled untimed step; the timed steps record "

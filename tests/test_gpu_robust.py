@@ -174,6 +174,49 @@ def test_uniform_random_bytes(env, seed):
     check(torch, ctx, cur, prior=S.dedup(cur[: 8 * MB]))
 
 
+@pytest.mark.parametrize("seg_all", ["1", "2"])
+def test_large_part_with_stale_record_tail(env, monkeypatch, seg_all):
+    """Round 4's faulting shape with NON-zero stale bytes: 1.65 GB = 1.05 GB of
+    host:port records + 0.6 GB of another host:port buffer's bytes, starting mid-record and
+    cut mid-record (what a caching allocator's reused block holds), plus a prior. The dedup
+    must not fault, and its result must equal the sort -u / comm -13 of the union of the two
+    halves' records, computed by deduping each half on its own and then their outputs
+    together (and the diff against the prior the same way)."""
+    torch, ctx = env
+    monkeypatch.setenv("SG_SEG_ALL", seg_all)
+    from swarm_amd import corpus
+    pool = corpus.host_pool_torch(8_000_000, seed=71)
+    (head,) = corpus.hostport_pieces(pool, 33_500_000, 0, 32_000_000, seed=72, per_piece=33_500_000, ports_per_host=4)
+    (old,) = corpus.hostport_pieces(pool, 20_000_000, 0, 32_000_000, seed=73, per_piece=20_000_000, ports_per_host=4)
+    (pri,) = corpus.hostport_pieces(pool, 4_000_000, 0, 32_000_000, seed=74, per_piece=4_000_000, ports_per_host=4)
+    del pool
+    a = 17
+    tail = old[a:a + min(600 * MB, old.numel() - a - 5)]  # starts and ends inside records
+    assert int(tail[0]) != 0x0A and int(tail[-1]) != 0x0A
+    d = torch.cat([head, tail])
+    n = d.numel()
+
+    def run(buf, prior):
+        ou = torch.empty(buf.numel() + 64, dtype=torch.uint8, device="cuda")
+        of = torch.empty(buf.numel() + 64, dtype=torch.uint8, device="cuda")
+        r = ctx.dedup_diff_into(buf.data_ptr(), buf.numel(), prior.data_ptr(), prior.numel(), ou.data_ptr(), ou.numel(),
+                                of.data_ptr(), of.numel())
+        torch.cuda.synchronize()
+        return r, ou[:r.uniq_bytes], of[:r.fresh_bytes]
+
+    r, u, f = run(d, pri)
+    rh, uh, fh = run(head, pri)
+    rt, ut, ft = run(tail.clone(), pri)
+    assert r.in_records == rh.in_records + rt.in_records
+    _, u2, _ = run(torch.cat([uh, ut]), pri[:0])
+    _, f2, _ = run(torch.cat([fh, ft]), pri[:0])
+    assert torch.equal(u, u2)
+    assert torch.equal(f, f2)
+    assert int(u[-1]) == 10 and r.uniq_records < r.in_records
+    del d, u, f, u2, f2, head, tail, old
+    torch.cuda.empty_cache()
+
+
 def test_large_part_with_zero_tail(env):
     """The shape of round 4's faulting part: 1.65 GB = 1.05 GB of records (a 105 MB subdomain
     buffer repeated 10 times) + 0.6 GB that stayed zero. Expected: the NUL-only record first

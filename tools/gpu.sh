@@ -36,6 +36,7 @@ args_of() {
     c5pb512m) echo "--workload c5 --steps 3 --warmup 1 --no-cpu-baseline --c5-part-bytes 536870912" ;;
     c5r) echo "--workload c5 --c5-path rounds --c5-records 125000000 --steps 3 --warmup 1 --no-cpu-baseline" ;;
     c5rnccl) echo "--workload c5 --c5-path rounds --dist-backend nccl --steps 3 --warmup 1" ;;
+    c5rp) echo "--workload c5 --c5-path rounds --dist-backend nccl --steps 1 --warmup 1 --no-cpu-baseline" ;;
     fields) echo "--workload fields --steps 3 --warmup 1" ;;
     fieldsp) echo "--workload fields --steps 2 --warmup 1 --no-cpu-baseline" ;;
     n2gloo) echo "--gpus 2 --dist-backend gloo --c5-records 200000000 --steps 3 --warmup 1" ;;
