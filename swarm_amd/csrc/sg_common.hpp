@@ -79,6 +79,7 @@ enum Slot : int {
     S_LS_LIST, S_LF_OFF, S_LF_KEY, S_LF_KEY2, S_LF_VAL, S_LF_VAL2, S_LF_POS,  // its overflow fix-up
     S_KEYSL, S_KEYSL2,  // dedup: cur / prior keys at the last call's common prefix (speculative)
     S_SPEC_PARTS,       // X1: the speculative keys' KeyStatD partials
+    S_M_K0, S_M_R7,     // X1: every record's key0 and bytes 7..14, written by the literal scan
     S_NSLOTS
 };
 

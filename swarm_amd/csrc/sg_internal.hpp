@@ -125,6 +125,7 @@ int dev_dedup_diff(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur, const uint8_
 struct MatchFlags {
     Lines L;
     uint8_t *flags = nullptr;
+    uint64_t *key0 = nullptr, *raw7 = nullptr;  // every record's key0 and bytes 7..14 (from the scan)
 };
 int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res, bool want_lines,
               MatchFlags *mf = nullptr);

@@ -760,6 +760,8 @@ struct LitArgs {
     const uint32_t *fac_off, *fac_pids;  // regex prefilter expansion (else null)
     uint2 *spans_out;                    // non-null: also write the parse's record spans (fused A3)
     uint8_t *rec_flag;                   // non-null: mark matched records here instead of listing hits
+    uint64_t *keys_out, *raw7_out;       // non-null (with spans_out): every record's key0 and its bytes
+                                         // 7..14 (little-endian), taken from the staged tile (X1)
     uint32_t rank_lds;                   // the bitmap words' ranks staged in LDS too (else read from L2)
     uint32_t mw_cap;                     // shared-bucket pair queue entries in dynamic LDS (0: walked in line)
     unsigned long long *diag;            // calibration (SG_LIT_TRIAL_LOG): queued, fingerprint-confirmed, verified
@@ -995,7 +997,34 @@ __device__ __forceinline__ void lit_scan_body(const LitArgs &a) {
             uint32_t etot;
             const uint32_t eexcl = block_excl_scan<BLK>((uint32_t)__popcll(em), &etot, s_red);
             uint32_t si = s_base + excl, ei = s_ebase + eexcl;
-            for (uint64_t bits = sm; bits; bits &= bits - 1) a.spans_out[si++].x = (uint32_t)(my0 + __ffsll((long long)bits) - 1);
+            if (a.keys_out) {
+                // X1: each record's key0 (chunk_key at 0) and its bytes 7..14, read from the
+                // staged tile at the record's start (the right halo holds 64 bytes past the
+                // tile, '\n' past the buffer): the matched records' gather then reads 16 B per
+                // record instead of each record's first line again
+                for (uint64_t bits = sm; bits; bits &= bits - 1) {
+                    const uint32_t o = t * BPT + (uint32_t)__ffsll((long long)bits) - 1u;  // tile offset
+                    const uint32_t *dw = reinterpret_cast<const uint32_t *>(s_tile + (o & ~3u));
+                    const uint32_t sh = o & 3u;
+                    const uint32_t d0 = dw[0], d1 = dw[1], d2 = dw[2], d3 = dw[3], d4 = dw[4];
+                    const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, sh), b1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                    const uint32_t b2 = __builtin_amdgcn_alignbyte(d3, d2, sh), b3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+                    const uint64_t v = (uint64_t)b0 | ((uint64_t)b1 << 32);  // bytes 0..7
+                    // the record's length within its first 8 bytes: the first '\n' there
+                    const uint64_t y = v ^ 0x0a0a0a0a0a0a0a0aull;
+                    const uint64_t z = ~(((y & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | y | 0x7f7f7f7f7f7f7f7full);
+                    const uint32_t len8 = z ? (uint32_t)__builtin_ctzll(z) >> 3 : 8u;
+                    const uint32_t take = len8 < 7u ? len8 : 7u;
+                    const uint64_t kv = v & ((1ull << (8u * take)) - 1ull);
+                    a.keys_out[si] = len8 ? ((__builtin_bswap64(kv) & ~0xffull) | len8) : 0ull;
+                    // bytes 7..14: byte 3 of b1 on, then b2, then b3's first 3
+                    a.raw7_out[si] = (uint64_t)__builtin_amdgcn_alignbyte(b2, b1, 3u) |
+                                     ((uint64_t)__builtin_amdgcn_alignbyte(b3, b2, 3u) << 32);
+                    a.spans_out[si++].x = (uint32_t)(my0 + __ffsll((long long)bits) - 1);
+                }
+            } else {
+                for (uint64_t bits = sm; bits; bits &= bits - 1) a.spans_out[si++].x = (uint32_t)(my0 + __ffsll((long long)bits) - 1);
+            }
             for (uint64_t bits = em; bits; bits &= bits - 1) a.spans_out[ei++].y = (uint32_t)(my0 + __ffsll((long long)bits) - 1);
         }
         uint32_t wn0 = *reinterpret_cast<const uint32_t *>(s_tile + (t + 1) * BPT);
@@ -1757,21 +1786,30 @@ __global__ void k_split_hits(const unsigned long long *K, const uint32_t *idx, u
 // keysL (Ls >= 8, the context's last common prefix): also the keys at Ls and their KeyStatD
 // partial per block (stL), for the records tying the first one on key0 (all of them when the
 // common prefix comes out at Ls again).
+// K0 / R7 (optional): every record's key0 and bytes 7..14 as the literal scan took them from
+// its staged tiles: the matched records' keys and first prefix step come from them (16 B per
+// record, in record order) instead of each record's first line (X1 gather 204 µs, 1.27 GB
+// fetched for 10M httpx lines).
 __global__ __launch_bounds__(256) void k_gather_matched(const uint8_t *__restrict__ buf, const uint2 *__restrict__ spans,
                                                         const uint32_t *__restrict__ mrec, uint32_t m, uint2 *__restrict__ sp,
                                                         uint64_t *__restrict__ keys, uint32_t *__restrict__ lcp_out,
-                                                        uint64_t *__restrict__ keysL, uint32_t Ls, KeyStatD *__restrict__ stL) {
+                                                        uint64_t *__restrict__ keysL, uint32_t Ls, KeyStatD *__restrict__ stL,
+                                                        const uint64_t *__restrict__ K0, const uint64_t *__restrict__ R7) {
     __shared__ uint32_t s_min[4];
     __shared__ KeyStatD s_st[4];
     KeyStatAcc accL;
-    const uint2 r = spans[mrec[0]];
-    const uint64_t kr = chunk_key(buf, r.x, r.y, 0);
+    const uint32_t r0 = mrec[0];
+    const uint2 r = spans[r0];
+    const uint64_t kr = K0 ? K0[r0] : chunk_key(buf, r.x, r.y, 0);
+    const uint64_t rr7 = R7 ? R7[r0] : 0ull;
     const uint32_t tr = (uint32_t)(kr & 0xffu);
     uint32_t best = 255;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        const uint2 x = spans[mrec[i]];
+        const uint32_t ri = mrec[i];
+        const uint2 x = spans[ri];
         sp[i] = x;
-        const uint64_t k = chunk_key(buf, x.x, x.y, 0);
+        const uint64_t k = K0 ? K0[ri] : chunk_key(buf, x.x, x.y, 0);
+        const uint64_t x7 = R7 ? R7[ri] : 0ull;
         keys[i] = k;
         const uint64_t d0 = (k ^ kr) >> 8;
         const uint32_t tk = (uint32_t)(k & 0xffu);
@@ -1787,9 +1825,11 @@ __global__ __launch_bounds__(256) void k_gather_matched(const uint8_t *__restric
             bool have7 = false;
             while (l < mm) {
                 const uint32_t t = (mm - l) < 8u ? (mm - l) : 8u;
-                const uint64_t xb = load_le(buf, x.x + l, t);
+                const uint64_t tm = t == 8u ? ~0ull : ((1ull << (8u * t)) - 1ull);
+                const bool from7 = R7 && l == 7u;  // the first step from the scan's bytes 7..14
+                const uint64_t xb = from7 ? (x7 & tm) : load_le(buf, x.x + l, t);
                 if (l == 7u && t == 8u) { raw7 = xb; have7 = true; }
-                const uint64_t d = xb ^ load_le(buf, r.x + l, t);
+                const uint64_t d = xb ^ (from7 ? (rr7 & tm) : load_le(buf, r.x + l, t));
                 if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
                 l += t;
             }
@@ -1814,6 +1854,117 @@ __global__ __launch_bounds__(256) void k_gather_matched(const uint8_t *__restric
     if (lane_id() == 0) s_min[threadIdx.x >> 6] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
+        const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
+        if (b < 255u && b < __hip_atomic_load(lcp_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(lcp_out, b);
+    }
+}
+
+// The matched records' compaction and gather in one pass (X1): over the flag select's tiles
+// (k_sel_count's ballots and the tile scan), each flagged record's span, key0 (K0) and bytes
+// 7..14 (R7, both written by the literal scan) are read in record order and written at its
+// position in the matched list, with the common-prefix scan of k_gather_matched: per block
+// against the tile's first matched record (the set's common prefix is the minimum, over the
+// set, of the prefix any one member shares with the others, so every block may use its own).
+// Replaces select.apply + k_gather_matched (two dependent gathers through the record list).
+struct MFlagPred {
+    const uint8_t *f;
+    __device__ uint32_t operator()(uint32_t i) const { return f[i] ? 1u : 0u; }
+};
+__global__ __launch_bounds__(SEL_BLOCK) void k_gather_flagged(uint32_t n, const uint64_t *__restrict__ mA,
+                                                              const uint64_t *__restrict__ pre, const uint8_t *__restrict__ buf,
+                                                              const uint2 *__restrict__ spans, const uint64_t *__restrict__ K0,
+                                                              const uint64_t *__restrict__ R7, uint2 *__restrict__ sp,
+                                                              uint64_t *__restrict__ keys, uint32_t *__restrict__ lcp_out,
+                                                              uint64_t *__restrict__ keysL, uint32_t Ls,
+                                                              KeyStatD *__restrict__ stL) {
+    __shared__ uint32_t s_ca[SEL_MASKS];
+    __shared__ uint64_t s_ma[SEL_MASKS];
+    __shared__ uint32_t s_first;
+    __shared__ uint32_t s_min[SEL_BLOCK / 64];
+    __shared__ KeyStatD s_st[SEL_BLOCK / 64];
+    const int t = threadIdx.x, lane = lane_id(), wid = t >> 6;
+    const uint32_t base = blockIdx.x * SEL_TILE;
+    const uint64_t *ma = mA + (uint64_t)blockIdx.x * SEL_MASKS;
+    if (t < 64) {
+        const uint64_t xa = ma[t];
+        const uint32_t a = (uint32_t)__popcll(xa);
+        s_ca[t] = wave_incl_scan(a) - a;
+        s_ma[t] = xa;
+        // the tile's first flagged item: mask t covers row t / 4, wave t % 4 (items base +
+        // (t / 4) * 256 + (t % 4) * 64 + lane)
+        const uint32_t f = xa ? (t >> 2) * SEL_BLOCK + (t & 3) * 64 + (uint32_t)(__ffsll((long long)xa) - 1) : 0xffffffffu;
+        uint32_t m = f;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        if (t == 0) s_first = m;
+    }
+    __syncthreads();
+    KeyStatAcc accL;
+    uint32_t best = 255;
+    if (s_first != 0xffffffffu) {
+        const uint32_t ri = base + s_first;
+        const uint2 r = spans[ri];
+        const uint64_t kr = K0[ri], rr7 = R7[ri];
+        const uint32_t tr = (uint32_t)(kr & 0xffu);
+        const uint32_t preA = (uint32_t)(pre[blockIdx.x] >> 31);
+        const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll 4
+        for (int j = 0; j < SEL_ROWS; ++j) {
+            const uint32_t i = base + j * SEL_BLOCK + t;
+            const uint64_t xa = s_ma[j * 4 + wid];
+            if (!((xa >> lane) & 1ull)) continue;
+            const uint32_t pos = preA + s_ca[j * 4 + wid] + (uint32_t)__popcll(xa & lt);
+            const uint2 x = spans[i];
+            const uint64_t k = K0[i], x7 = R7[i];
+            sp[pos] = x;
+            keys[pos] = k;
+            const uint64_t d0 = (k ^ kr) >> 8;
+            const uint32_t tk = (uint32_t)(k & 0xffu);
+            uint32_t l;
+            if (d0) {
+                l = min((uint32_t)__builtin_clzll(d0 << 8) >> 3, min(tk, tr));
+            } else if (tk < 8u || tr < 8u) {
+                l = min(tk, tr);
+            } else {
+                const uint32_t mm = min(min(x.y - x.x, r.y - r.x), best);
+                l = 7;
+                uint64_t raw7 = 0;
+                bool have7 = false;
+                while (l < mm) {
+                    const uint32_t tt = (mm - l) < 8u ? (mm - l) : 8u;
+                    const uint64_t tm = tt == 8u ? ~0ull : ((1ull << (8u * tt)) - 1ull);
+                    const bool from7 = l == 7u;
+                    const uint64_t xb = from7 ? (x7 & tm) : load_le(buf, x.x + l, tt);
+                    if (from7 && tt == 8u) { raw7 = xb; have7 = true; }
+                    const uint64_t d = xb ^ (from7 ? (rr7 & tm) : load_le(buf, r.x + l, tt));
+                    if (d) { l += (uint32_t)__builtin_ctzll(d) >> 3; break; }
+                    l += tt;
+                }
+                l = min(l, mm);
+                if (keysL) {
+                    const uint32_t len = x.y - x.x, rem = len > Ls ? len - Ls : 0u, take = rem < 7u ? rem : 7u;
+                    uint64_t kl;
+                    if (Ls == 8u && (have7 || len >= 15u)) {
+                        const uint64_t b8 = have7 ? raw7 : x7;  // bytes 7..14: the key's are 8..14
+                        kl = rem ? ((__builtin_bswap64((b8 >> 8) & ((1ull << (8u * take)) - 1ull)) & ~0xffull) |
+                                    (uint64_t)(rem < 8u ? rem : 8u))
+                                 : 0ull;
+                    } else {
+                        kl = chunk_key(buf, x.x, x.y, Ls);
+                    }
+                    keysL[pos] = kl;
+                    accL.add(kl);
+                }
+            }
+            best = min(best, l);
+        }
+    }
+    if (stL) kstat_flush(accL, s_st, stL);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    if (lane == 0) s_min[wid] = best;
+    __syncthreads();
+    if (t == 0) {
         const uint32_t b = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
         if (b < 255u && b < __hip_atomic_load(lcp_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(lcp_out, b);
     }
@@ -1880,6 +2031,8 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
         a.hits = out; a.hit_count = counter; a.cap = ocap; a.fac_off = fo; a.fac_pids = fp;
         a.spans_out = (!trial_tiles && fuse_spans && strcmp(name, span_writer) == 0) ? L.spans : nullptr;
         a.rec_flag = (mf && !trial_tiles) ? mf->flags : nullptr;
+        a.keys_out = (a.rec_flag && a.spans_out) ? mf->key0 : nullptr;
+        a.raw7_out = a.keys_out ? mf->raw7 : nullptr;
         const uint32_t stat = L.tile_bytes + 2 * LS_HALO + LS_HB * 8 + LS_Q * 12 + 64;
         auto blocks_per_cu = [&](uint32_t dyn) {
             return std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / (dyn + stat)));
@@ -2063,6 +2216,10 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     if (mf) {
         SG_TRY(slot(c, S_M_FLAG, (size_t)R + 16, &mf->flags));
         SG_HIP(hipMemsetAsync(mf->flags, 0, (size_t)R + 16, c->stream));
+        if (fuse_spans) {  // (the scan writes the spans, so it also takes the keys there)
+            SG_TRY(slot(c, S_M_K0, (size_t)R + 1, &mf->key0));
+            SG_TRY(slot(c, S_M_R7, (size_t)R + 1, &mf->raw7));
+        }
         if (R) SG_TRY(run_lit("lit_match", scheme(h->lit, h->lit_j, h->lit_mode, nullptr, nullptr), nullptr, cnt, 0u, nullptr, nullptr));
         mf->L = L;
         return SG_OK;
@@ -2368,31 +2525,63 @@ int sg_dev_match_dedup_diff(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, size
         MatchFlags mf;
         SG_TRY(dev_match(c, h, b, n, &hits, false, &mf));
         const uint32_t R = mf.L.n_rec;
-        uint32_t *mrec;
-        SG_TRY(slot(c, S_R_POS, (size_t)R + 1, &mrec));
         uint32_t M = 0;
-        if (R) SG_TRY(select_flags(c, mf.flags, R, mrec, &M));
         Lines Lm;
-        SG_TRY(slot(c, S_M_SP2, (size_t)M + 1, &Lm.spans));
-        SG_TRY(slot(c, S_M_K2, (size_t)M + 1, &Lm.keys));
-        Lm.n_rec = M;
         uint32_t *lcp;
         SG_TRY(slot(c, S_M_TMP, 4, &lcp));
         const uint32_t init = 255u;
         SG_HIP(hipMemcpyAsync(lcp, &init, 4, hipMemcpyHostToDevice, c->stream));
-        const uint32_t gg = std::min<uint32_t>((M + 255) / 256, 2048u);
-        // keys at the last call's common prefix too (see sg_dedup.hip: a re-key pass saved
-        // when the matched records share that prefix again)
-        KeyStatD *gparts = nullptr;
-        if (M >= 4096 && c->last_base >= 8u) {
-            SG_TRY(slot(c, S_KEYSL, (size_t)M + 1, &Lm.spec_keys));
-            SG_TRY(slot(c, S_SPEC_PARTS, (size_t)gg * sizeof(KeyStatD) / 8 + 1, &gparts));
-            Lm.spec_off = c->last_base;
-            Lm.spec_parts = gparts;
-            Lm.spec_nparts = gg;
+        if (R && mf.key0) {
+            // the scan took every record's key0 and bytes 7..14: select and gather in one pass
+            // (output slots sized for every record: the matched count is known after it)
+            const uint32_t ntiles = (R + SEL_TILE - 1) / SEL_TILE;
+            uint64_t *tp;  // tot | pre | total | masks A | masks B (unused: one predicate)
+            SG_TRY(slot(c, S_COUNT, 2 * (size_t)ntiles + 4 + 2 * (size_t)ntiles * SEL_MASKS, &tp));
+            uint64_t *tot = tp, *pre = tp + ntiles, *total = tp + 2 * (size_t)ntiles, *mA = total + 4;
+            uint64_t *mB = mA + (size_t)ntiles * SEL_MASKS;
+            SG_TRY(slot(c, S_M_SP2, (size_t)R + 1, &Lm.spans));
+            SG_TRY(slot(c, S_M_K2, (size_t)R + 1, &Lm.keys));
+            KeyStatD *gparts = nullptr;
+            if (R >= 4096 && c->last_base >= 8u) {
+                SG_TRY(slot(c, S_KEYSL, (size_t)R + 1, &Lm.spec_keys));
+                SG_TRY(slot(c, S_SPEC_PARTS, (size_t)ntiles * sizeof(KeyStatD) / 8 + 1, &gparts));
+                Lm.spec_off = c->last_base;
+                Lm.spec_parts = gparts;
+                Lm.spec_nparts = ntiles;
+            }
+            SG_LAUNCH(c, "select", k_sel_count<MFlagPred>, ntiles, SEL_BLOCK, 0, MFlagPred{mf.flags}, R, mA, mB, tot);
+            SG_TRY(tile_scan(c, tot, ntiles, pre, total));
+            // model: flag masks, then span + key0 + bytes 7..14 read and span + keys written per
+            // matched record (the prefix scan's rare byte compares not credited)
+            SG_LAUNCH(c, "gather_matched", k_gather_flagged, ntiles, SEL_BLOCK, 0, R, mA, pre, b, mf.L.spans,
+                      (const uint64_t *)mf.key0, (const uint64_t *)mf.raw7, Lm.spans, Lm.keys, lcp, Lm.spec_keys,
+                      Lm.spec_off, gparts);
+            uint64_t tv = 0;
+            SG_TRY(ctx_readback(c, &tv, total, 8));
+            M = (uint32_t)(tv >> 31);
+            if (c->profile) prof_bytes(c, "gather_matched", R / 8.0 + (Lm.spec_keys ? 48.0 : 40.0) * M);
+        } else {
+            uint32_t *mrec;
+            SG_TRY(slot(c, S_R_POS, (size_t)R + 1, &mrec));
+            if (R) SG_TRY(select_flags(c, mf.flags, R, mrec, &M));
+            SG_TRY(slot(c, S_M_SP2, (size_t)M + 1, &Lm.spans));
+            SG_TRY(slot(c, S_M_K2, (size_t)M + 1, &Lm.keys));
+            const uint32_t gg = std::min<uint32_t>((M + 255) / 256, 2048u);
+            // keys at the last call's common prefix too (see sg_dedup.hip: a re-key pass saved
+            // when the matched records share that prefix again)
+            KeyStatD *gparts = nullptr;
+            if (M >= 4096 && c->last_base >= 8u) {
+                SG_TRY(slot(c, S_KEYSL, (size_t)M + 1, &Lm.spec_keys));
+                SG_TRY(slot(c, S_SPEC_PARTS, (size_t)gg * sizeof(KeyStatD) / 8 + 1, &gparts));
+                Lm.spec_off = c->last_base;
+                Lm.spec_parts = gparts;
+                Lm.spec_nparts = gg;
+            }
+            if (M) SG_LAUNCH_B(c, "gather_matched", 24.0 * M, k_gather_matched, gg, 256, 0, b, mf.L.spans, mrec, M, Lm.spans,
+                               Lm.keys, lcp, Lm.spec_keys, Lm.spec_off, gparts, (const uint64_t *)nullptr,
+                               (const uint64_t *)nullptr);
         }
-        if (M) SG_LAUNCH_B(c, "gather_matched", 24.0 * M, k_gather_matched, gg, 256, 0, b, mf.L.spans, mrec, M, Lm.spans,
-                           Lm.keys, lcp, Lm.spec_keys, Lm.spec_off, gparts);
+        Lm.n_rec = M;
         if (matched_records) *matched_records = M;
         SG_TRY(dev_dedup_diff_lines(c, b, n, Lm, n_prior ? p : nullptr, n_prior, res, M ? lcp : nullptr));
         res->in_records = R;
