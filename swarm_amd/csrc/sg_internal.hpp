@@ -128,7 +128,7 @@ struct MatchFlags {
     uint64_t *key0 = nullptr, *raw7 = nullptr;  // every record's key0 and bytes 7..14 (from the scan)
 };
 int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res, bool want_lines,
-              MatchFlags *mf = nullptr);
+              MatchFlags *mf = nullptr, Lines *reuse = nullptr);
 // dev_dedup_diff (radix pipeline) for a current scan given as already parsed records of
 // d_cur (spans + key0 from byte 0), e.g. the matched subset of a larger buffer.
 // dev_dedup_diff_into with cur's records already parsed (spans + byte-0 keys).

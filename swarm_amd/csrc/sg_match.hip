@@ -1981,7 +1981,7 @@ static int select_one(sg_ctx *c, const char *name, Pred pred, uint32_t n, uint32
 }
 
 int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev_hits *res, bool want_lines,
-              MatchFlags *mf) {
+              MatchFlags *mf, Lines *reuse) {
     if (mf && !(h->lit.on && h->tables.empty() && !h->has_pre)) {
         set_error("dev_match: record flags need a literal-filter matcher");
         return SG_E_INVAL;
@@ -1989,11 +1989,17 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     *res = sg_dev_hits{};
     SG_TRY(ensure_device(h, c->device));
     Lines L;
+    // reuse: the parse of this same buffer by an earlier call (several engines over one input:
+    // the template evaluation), its spans and tile prefixes still in the context's CUR slots;
+    // filled with this call's parse otherwise
+    const bool reused = reuse && reuse->spans && reuse->tile_excl;
     // When a literal scan runs first (literal filter or regex prefilter), it writes the
     // record spans itself from the same tiles, so the parse's second pass is skipped.
-    const bool fuse_spans = h->has_pre || h->lit.on;
+    const bool fuse_spans = !reused && (h->has_pre || h->lit.on);
     const char *span_writer = h->has_pre ? "re_prefilter" : "lit_match";
-    SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L, false, !fuse_spans));
+    if (reused) L = *reuse;
+    else SG_TRY(run_lines(c, d_buf, n, CUR_SLOTS, &L, false, !fuse_spans));
+    if (reuse && !reused) *reuse = L;  // (the spans are complete once this call's kernels have run)
     const uint32_t R = L.n_rec;
     res->in_records = R;
     uint32_t *cnt;

@@ -543,12 +543,14 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
     std::vector<std::pair<uint32_t, uint32_t>> segs;  // each collect launch's hits in acc
     uint64_t R = 0;
     bool have_R = false;
-    // stream 0: the records themselves
+    // stream 0: the records themselves (one parse shared by every engine's run: the parse
+    // of a 2.4 GB JSON body was redone per engine)
+    Lines parse0;
     for (size_t ri = 0; ri < h->runs.size(); ++ri) {
         auto &run = h->runs[ri];
         if (run.stream != 0) continue;
         sg_dev_hits r;
-        SG_TRY(dev_match(c, run.m, d_buf, n, &r, false));
+        SG_TRY(dev_match(c, run.m, d_buf, n, &r, false, nullptr, &parse0));
         R = r.in_records;
         have_R = true;
         if (!r.n_hits) continue;
@@ -569,11 +571,12 @@ static int dev_tmpl_eval(sg_ctx *c, sg_templates *h, const uint8_t *d_buf, uint6
                                     &rows));
         R = rows.in_records;
         have_R = true;
+        Lines parse1;  // the rows' parse, shared the same way
         for (size_t ri = 0; ri < h->runs.size(); ++ri) {
             auto &run = h->runs[ri];
             if (run.stream != 1 || rows.bytes == 0) continue;
             sg_dev_hits r;
-            SG_TRY(dev_match(c, run.m, rows.data, rows.bytes, &r, false));
+            SG_TRY(dev_match(c, run.m, rows.data, rows.bytes, &r, false, nullptr, &parse1));
             if (!r.n_hits) continue;
             SG_TRY(tm_grow(c, &acc, acc.n + r.n_hits));
             SG_LAUNCH(c, "tm_collect", k_tm_collect, (uint32_t)((r.n_hits + 255) / 256), 256, 0, r.rec_idx, r.sig_id,
