@@ -1682,6 +1682,7 @@ constexpr uint32_t HB_RBMAX = 12;     // log2 records per bucket, at most (LDS c
 constexpr uint32_t HB_CAP = 6144;     // hits per bucket sorted in LDS
 constexpr uint32_t HB_T = 1024;       // count/scatter/sort block
 constexpr uint32_t HB_NBLK = 256;     // count/scatter blocks
+constexpr uint32_t HB_NBMAX = 32768;  // buckets at most (their counters in one block's LDS)
 
 __global__ __launch_bounds__(HB_T) void k_hb_count(const unsigned long long *__restrict__ hits, uint32_t n,
                                                     uint32_t nb, uint32_t rb, uint32_t *__restrict__ cnt) {
@@ -1749,18 +1750,21 @@ __global__ __launch_bounds__(HB_T) void k_hb_sort(unsigned long long *__restrict
         s_k[atomicAdd(&s_c[(uint32_t)(k >> 32) & (NR - 1u)], 1u)] = k;
     }
     __syncthreads();
-    // s_c[r] = end of record r's run = start of r + 1
-    for (uint32_t r = t; r < NR; r += HB_T) {
+    // s_c[r] = end of record r's run = start of r + 1. Each hit's place inside its record's
+    // run is its rank there (hits ordered before it, ties by position), one thread per hit:
+    // every thread works, where an insertion sort per record kept 2^rb of them busy (dense
+    // hits, ~18 per record: the fields step's 73M-hit engine spent 1.6 ms here)
+    for (uint32_t q = t; q < m; q += HB_T) {
+        const unsigned long long k = s_k[q];
+        const uint32_t r = (uint32_t)(k >> 32) & (NR - 1u);
         const uint32_t a = r ? s_c[r - 1] : 0u, e = s_c[r];
-        for (uint32_t i = a + 1; i < e; ++i) {
-            const unsigned long long x = s_k[i];
-            uint32_t j = i;
-            while (j > a && s_k[j - 1] > x) { s_k[j] = s_k[j - 1]; --j; }
-            s_k[j] = x;
+        uint32_t rank = a;
+        for (uint32_t j = a; j < e; ++j) {
+            const unsigned long long x = s_k[j];
+            rank += (x < k || (x == k && j < q)) ? 1u : 0u;
         }
+        keys[e0 + rank] = k;
     }
-    __syncthreads();
-    for (uint32_t q = t; q < m; q += HB_T) keys[e0 + q] = s_k[q];
 }
 
 // Sorted hits: bit 0 = first of its (record, signature), bit 1 = first of its record.
@@ -2308,8 +2312,15 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
     uint32_t rb = HB_RBMAX;
     while (rb > 4 && (double)total * (1u << rb) / std::max<uint32_t>(R, 1u) > HB_CAP / 2) --rb;
     const uint32_t nb = (uint32_t)(((uint64_t)R + (1u << rb) - 1) >> rb);
-    if (total > 1 && !sw_hit_radix() && nb <= 12288) {
+    // (up to 32,768 buckets: the count and scatter blocks' LDS counters then take up to 128 KB,
+    // one block per CU; the fields step's dense engine, 73M hits over 4M records, needs 31,250
+    // buckets and went through a 5-pass radix sort of its hits: 2.9 ms)
+    if (total > 1 && !sw_hit_radix() && nb <= HB_NBMAX) {
         const uint32_t nblk = std::max<uint32_t>(1u, std::min<uint32_t>(HB_NBLK, (total + 4095) / 4096));
+        if (nb * 4u > 65536u) {
+            SG_HIP(hipFuncSetAttribute((const void *)k_hb_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(nb * 4u)));
+            SG_HIP(hipFuncSetAttribute((const void *)k_hb_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(nb * 4u)));
+        }
         const size_t nc = (size_t)nb * nblk;
         uint32_t *hcnt, *herr;
         uint64_t *hoff;
@@ -2337,6 +2348,9 @@ int dev_match(sg_ctx *c, sg_matcher *h, const uint8_t *d_buf, uint64_t n, sg_dev
             sorted = true;
         }
     }
+    if (sw_lit_trial_log())
+        fprintf(stderr, "sg hit sort: %u hits over %u records, rb %u, %u buckets: %s\n", total, R, rb, nb,
+                sorted ? "bucket sort" : "radix sort");
     if (!sorted) {
         uint64_t *k2;
         uint32_t *v1, *v2;

@@ -935,8 +935,10 @@ static int radix_sort_t(sg_ctx *c, uint64_t *keys, VT *vals, uint64_t *keys_alt,
             // model: key read, key + span fetched in sorted order, both written
             SG_LAUNCH_B(c, "rs_lsort", 40.0 * n, k_rs_lsort, g, LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask, hp.lpos, hp.nloc,
                         bounds, flist, err + 1);
-            // the listed tiles redone from the same input by a few blocks walking the list
-            SG_LAUNCH(c, "rs_lfix", k_rs_lsort_fix, std::min<uint32_t>(g, 256u), LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask,
+            // the listed tiles redone from the same input by a few blocks walking the list (64:
+            // the launch costs ~7 us at 256 blocks when, as usual, no tile is listed; folding it
+            // into k_rs_lsort as a call took that kernel to 184 VGPRs)
+            SG_LAUNCH(c, "rs_lfix", k_rs_lsort_fix, std::min<uint32_t>(g, 64u), LS_BLOCK, 0, ck, cv, ak, av, n, hp.gmask,
                       hp.lpos, hp.nloc, bounds, flist, err + 1, gs, ge, cap, err);
             c->ls_last.on = true;
             c->ls_last.gmask = hp.gmask;
