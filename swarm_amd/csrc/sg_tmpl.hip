@@ -48,8 +48,11 @@ constexpr int TM_MAX_DEV = 64;
 constexpr uint32_t TMW_WAVES = 12;          // waves per block
 constexpr uint32_t TMW_WORDS_MAX = 20480;   // 80 KB per block (two blocks per CU)
 constexpr uint32_t TMW_NEED_AND = 1u << 16, TMW_NEED_NEG = 1u << 17;
+// per wave: the matcher counters, touched + result template bitmaps, the seen-atom bitmap,
+// and the touched-template list (its words also serve as the occurrence scratch: 128 words)
 constexpr uint32_t tm_wave_words(uint32_t n_match, uint32_t n_tmpl, uint32_t n_atoms) {
-    return (n_match + 3) / 4 + 2 * ((n_tmpl + 31) / 32) + (n_atoms + 31) / 32 + (n_tmpl + 1) / 2;
+    return (n_match + 3) / 4 + 2 * ((n_tmpl + 31) / 32) + (n_atoms + 31) / 32 +
+           ((n_tmpl + 1) / 2 > 128u ? (n_tmpl + 1) / 2 : 128u);
 }
 constexpr uint64_t tm_block_words(uint32_t n_atoms, uint32_t n_occ, uint32_t n_match, uint32_t n_tmpl) {
     return (uint64_t)(n_atoms + 2) / 2 + n_occ + n_tmpl + n_match + (n_tmpl + 31) / 32 +
@@ -340,15 +343,39 @@ __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
         uint32_t myo = 0;
         if (nseg <= 32 && lane < 2 * nseg) myo = roff[(size_t)(lane >> 1) * (R + 1) + r + (lane & 1)];
         tm_wave_sync();
-        // one atom: counted once per record, its (matcher, template) occurrences
-        auto count_atom = [&](uint32_t at) {
-            const uint32_t bit = 1u << (at & 31);
-            if (at == TM_NO_ATOM || (atomicOr(&seen[at >> 5], bit) & bit)) return;
-            for (uint32_t q = s_occ[at], qe = s_occ[at + 1]; q < qe; ++q) {
+        // one atom per lane (TM_NO_ATOM: none; wave-uniform call): each atom counted once per
+        // record, and the (matcher, template) occurrences of the wave's new atoms spread over
+        // all 64 lanes (lane k's run at its prefix in scratch), instead of each lane walking
+        // its own atom's list while the wave waits for the longest (an atom can sit in dozens
+        // of matchers)
+        uint32_t *sc_inc = reinterpret_cast<uint32_t *>(list), *sc_q0 = sc_inc + 64;
+        auto count_atoms = [&](uint32_t at) {
+            uint32_t q0 = 0, c = 0;
+            if (at != TM_NO_ATOM) {
+                const uint32_t bit = 1u << (at & 31);
+                if (!(atomicOr(&seen[at >> 5], bit) & bit)) {
+                    q0 = s_occ[at];
+                    c = (uint32_t)s_occ[at + 1] - q0;
+                }
+            }
+            const uint32_t inc = wave_incl_scan_shfl(c);
+            const uint32_t T = (uint32_t)__shfl((int)inc, 63, 64);
+            if (T == 0u) return;
+            sc_inc[lane] = inc;
+            sc_q0[lane] = q0;
+            tm_wave_sync();
+            for (uint32_t o = lane; o < T; o += 64) {
+                uint32_t lo = 0, hi = 63;  // the first lane whose inclusive prefix exceeds o
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (sc_inc[mid] > o) hi = mid; else lo = mid + 1;
+                }
+                const uint32_t q = sc_q0[lo] + o - (lo ? sc_inc[lo - 1] : 0u);
                 const uint32_t mt = s_mt[q], m = mt & 0xffffu, t = mt >> 16;
                 atomicAdd(&cnt[m >> 2], 1u << (8 * (m & 3)));
                 atomicOr(&tch[t >> 5], 1u << (t & 31));
             }
+            tm_wave_sync();  // scratch reused by the next batch
         };
         if (nseg <= 32) {
             // the record's hits of all segments as one list: lane j loads hit j, so the
@@ -365,12 +392,14 @@ __global__ __launch_bounds__(64 * TMW_WAVES) void k_tm_rec_eval(
                     if (j >= base && j < base + c) idx = sa + (j - base);
                     base += c;
                 }
-                if (idx != 0xffffffffu) count_atom((uint32_t)K[idx]);
+                count_atoms(idx != 0xffffffffu ? (uint32_t)K[idx] : TM_NO_ATOM);
             }
         } else {
             for (uint32_t sg = 0; sg < nseg; ++sg) {
                 const uint32_t *ro = roff + (size_t)sg * (R + 1);
-                for (uint32_t i = ro[r] + lane; i < ro[r + 1]; i += 64) count_atom((uint32_t)K[i]);
+                const uint32_t a0 = ro[r], a1 = ro[r + 1];  // (wave-uniform: one record per wave)
+                for (uint32_t i0 = a0; i0 < a1; i0 += 64)
+                    count_atoms(i0 + lane < a1 ? (uint32_t)K[i0 + lane] : TM_NO_ATOM);
             }
         }
         tm_wave_sync();
