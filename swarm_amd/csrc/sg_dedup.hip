@@ -454,10 +454,19 @@ __device__ __forceinline__ int seg_cmp(const uint8_t *S, const SegKeys &a, uint2
 // (C5 seg_wave 23.9 -> 27.9 ms with it).
 #define SEG_BYTES_CMP(S_, x_, y_, o_)                                                              \
     (WIDE ? rec_cmp_w(S_, x_.x, x_.y, S_, y_.x, y_.y, o_) : rec_cmp8(S_, x_.x, x_.y - x_.x, y_.x, y_.y - y_.x, o_))
+// The two chunk keys travel through LDS (s_w: this wave's SEG_WS entries): each rank step is
+// one broadcast 16-B read instead of four 32-bit lane shuffles, and the other member's span,
+// needed only for the rare byte compare, is read from SS then (two more shuffles per step
+// before: C5 seg_wave + seg_small 39.4 ms per step).
+constexpr uint32_t SEG_WS = 68;  // 64 members + a 16-B pad per 16-lane group (no bank conflicts)
+__device__ __forceinline__ void seg_wave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
 template <int G, bool WIDE>
 __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, uint2 *__restrict__ SS,
                                                uint8_t *__restrict__ dup, uint32_t a, uint32_t k, uint32_t gl,
-                                               uint32_t gbase, bool live, uint32_t base) {
+                                               uint32_t gbase, bool live, uint32_t base, uint4 *s_w) {
     const bool act = live && gl < k;
     const uint2 x = act ? SS[a + gl] : make_uint2(0u, 0u);
     const SegKeys mk = act ? seg_keys(S, x, base) : SegKeys{{0, 0, 0, 0}};
@@ -485,19 +494,30 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
     uint32_t kmax = kk;
 #pragma unroll
     for (int o = G; o < 64; o <<= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    uint4 *gw = s_w + gbase + (gbase >> 4);
+    seg_wave_sync();  // the previous group's reads of s_w are done
+    gw[gl] = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), (uint32_t)m2, (uint32_t)(m2 >> 32));
+    seg_wave_sync();
     for (uint32_t j = 0; j < kmax; ++j) {
-        const int src = (int)(gbase + (j < kk ? j : 0u));
-        const uint64_t o1 = __shfl(m1, src, 64), o2 = __shfl(m2, src, 64);
-        const uint2 y = make_uint2((uint32_t)__shfl(x.x, src, 64), (uint32_t)__shfl(x.y, src, 64));
+        const uint4 ov = gw[j];  // (j >= kk: a stale entry, never used)
+        const uint64_t o1 = (uint64_t)ov.x | ((uint64_t)ov.y << 32), o2 = (uint64_t)ov.z | ((uint64_t)ov.w << 32);
+        // long records (WIDE) tie past the chunk keys often: their spans still travel by shuffle
+        uint2 yw = make_uint2(0u, 0u);
+        if constexpr (WIDE) {
+            const int src = (int)(gbase + (j < kk ? j : 0u));
+            yw = make_uint2((uint32_t)__shfl(x.x, src, 64), (uint32_t)__shfl(x.y, src, 64));
+        }
+#define SEG_Y (WIDE ? yw : SS[a + j])
         if (act && j < kk && j != gl) {
             int c;
-            if (st >= SEG_CH) c = SEG_BYTES_CMP(S, x, y, boff);
+            if (st >= SEG_CH) c = SEG_BYTES_CMP(S, x, SEG_Y, boff);
             else if (m1 != o1) c = m1 < o1 ? -1 : 1;
             else if ((m1 & 0xffu) < 8u) c = 0;
-            else if (st + 1u >= SEG_CH) c = SEG_BYTES_CMP(S, x, y, boff);
+            else if (st + 1u >= SEG_CH) c = SEG_BYTES_CMP(S, x, SEG_Y, boff);
             else if (m2 != o2) c = m2 < o2 ? -1 : 1;
             else if ((m2 & 0xffu) < 8u) c = 0;
-            else c = SEG_BYTES_CMP(S, x, y, boff);
+            else c = SEG_BYTES_CMP(S, x, SEG_Y, boff);
+#undef SEG_Y
             if (c > 0 || (c == 0 && j < gl)) ++rank;
             if (c == 0 && j < gl) d = true;
         }
@@ -522,7 +542,8 @@ __global__ __launch_bounds__(256) void k_seg_small(const uint8_t *__restrict__ S
     const bool eb = !live || pe >= n || gl == 15u || brk[pe];
     const uint32_t me = (uint32_t)(__ballot(eb) >> gbase) & 0xffffu;
     const uint32_t k = 1u + (uint32_t)(__ffs((int)me) - 1);  // members: a .. a+k-1
-    seg_rank_group<16, WIDE>(S, SS, dup, a, k, gl, gbase, live, base);
+    __shared__ uint4 s_w[4][SEG_WS];
+    seg_rank_group<16, WIDE>(S, SS, dup, a, k, gl, gbase, live, base, s_w[threadIdx.x >> 6]);
 }
 
 // Larger segments (17..64 members), two heads per wave: two half-waves when both segments
@@ -546,13 +567,15 @@ __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S,
         if (!me) { if (lane == 0) atomicOr(err, 1u); return; }
         k[t] = live ? 1u + (uint32_t)(__ffsll((long long)me) - 1) : 0u;
     }
+    __shared__ uint4 s_w[4][SEG_WS];
+    uint4 *w = s_w[threadIdx.x >> 6];
     if (k[0] <= 32u && k[1] <= 32u) {
         const uint32_t t = lane >> 5;
         seg_rank_group<32, WIDE>(S, SS, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u, (t ? k[1] : k[0]) > 0,
-                           base);
+                                 base, w);
     } else {
-        seg_rank_group<64, WIDE>(S, SS, dup, a[0], k[0], lane, 0u, true, base);
-        if (k[1]) seg_rank_group<64, WIDE>(S, SS, dup, a[1], k[1], lane, 0u, true, base);
+        seg_rank_group<64, WIDE>(S, SS, dup, a[0], k[0], lane, 0u, true, base, w);
+        if (k[1]) seg_rank_group<64, WIDE>(S, SS, dup, a[1], k[1], lane, 0u, true, base, w);
     }
 }
 
