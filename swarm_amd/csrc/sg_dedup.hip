@@ -485,7 +485,13 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
         for (int c = 0; c < SEG_CH; ++c) v = (q == (uint32_t)c) ? mk.c[c] : v;
         return v;
     };
-    const uint64_t m1 = pick(st), m2 = pick(st + 1);  // (past the last chunk: 0)
+    const uint64_t m1 = pick(st), m2r = pick(st + 1);  // (past the last chunk: 0)
+    // Branch-free order on (m1, m2): m2 counts only while m1 holds a full 7 bytes (a tag < 8
+    // ends the record, so equal m1 then means equal records); `full`: equal keys leave the
+    // order to the bytes past them (group-uniform given equal m1 and m2)
+    const bool m1full = (m1 & 0xffu) >= 8u;
+    const uint64_t m2 = m1full ? m2r : 0ull;
+    const bool full = st >= SEG_CH || (m1full && (st + 1u >= SEG_CH || (m2 & 0xffu) >= 8u));
     const uint32_t boff = bk_off(base) + 7u * (st + 2u < SEG_CH ? st + 2u : SEG_CH);
     uint32_t rank = 0;
     bool d = false;
@@ -508,19 +514,18 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
             yw = make_uint2((uint32_t)__shfl(x.x, src, 64), (uint32_t)__shfl(x.y, src, 64));
         }
 #define SEG_Y (WIDE ? yw : SS[a + j])
-        if (act && j < kk && j != gl) {
-            int c;
-            if (st >= SEG_CH) c = SEG_BYTES_CMP(S, x, SEG_Y, boff);
-            else if (m1 != o1) c = m1 < o1 ? -1 : 1;
-            else if ((m1 & 0xffu) < 8u) c = 0;
-            else if (st + 1u >= SEG_CH) c = SEG_BYTES_CMP(S, x, SEG_Y, boff);
-            else if (m2 != o2) c = m2 < o2 ? -1 : 1;
-            else if ((m2 & 0xffu) < 8u) c = 0;
-            else c = SEG_BYTES_CMP(S, x, SEG_Y, boff);
-#undef SEG_Y
-            if (c > 0 || (c == 0 && j < gl)) ++rank;
-            if (c == 0 && j < gl) d = true;
+        const bool valid = act && j < kk && j != gl;
+        bool gt = (o1 < m1) || (o1 == m1 && o2 < m2);  // the other member orders first
+        bool eq = o1 == m1 && o2 == m2;
+        if (valid && eq && full) {  // rare on short records: the bytes decide
+            const int c = SEG_BYTES_CMP(S, x, SEG_Y, boff);
+            gt = c > 0;
+            eq = c == 0;
         }
+#undef SEG_Y
+        const bool before = j < gl;
+        rank += (valid && (gt || (eq && before))) ? 1u : 0u;
+        d = d || (valid && eq && before);
     }
     if (act) {
         SS[a + rank] = x;
