@@ -20,7 +20,7 @@
 #include "../../include/swarmgpu.h"
 #include "sg_switches.hpp"
 
-#define SG_PINNED_BYTES 16384
+#define SG_PINNED_BYTES 32768
 
 namespace sg {
 

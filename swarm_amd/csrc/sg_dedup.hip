@@ -1599,7 +1599,9 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     // (the front of one slot with the sample histograms and the stat partials after it: the
     // flags, the stats and the histograms come back in one copy)
     uint32_t *dflag;
-    constexpr size_t DF_CHK = 32 + 8 * 256 + 2 * 2048 * sizeof(KeyStatD) / 4;  // handover check partials
+    // [32, 32 + 2048): the sample histograms of the keys from byte 0, then those of the
+    // speculative keys at the last common prefix, then the key-stat partials
+    constexpr size_t DF_CHK = 32 + 2 * 8 * 256 + 2 * 2048 * sizeof(KeyStatD) / 4;  // handover check partials
     SG_TRY(slot(c, S_HIST, DF_CHK + 2048 * sizeof(SpanChkPart) / 4, &dflag));
     KeyStatD *st0 = reinterpret_cast<KeyStatD *>(dflag + 4), *st1 = reinterpret_cast<KeyStatD *>(dflag + 12);
     {
@@ -1637,8 +1639,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     const uint32_t g_rekey = std::min<uint32_t>(grid_for(Lc.n_rec, 256), 2048u);
     if (want_hist) {
         shist = dflag + 32;
-        parts = reinterpret_cast<KeyStatD *>(shist + 8 * 256);
-        SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));
+        parts = reinterpret_cast<KeyStatD *>(shist + 2 * 8 * 256);
+        SG_HIP(hipMemsetAsync(shist, 0, 2 * 8 * 256 * 4, c->stream));
     }
     // Speculation: when the last call's records shared a prefix of >= 8 bytes (URL lists),
     // the prefix scans also write the keys at that offset, so a common prefix that comes out
@@ -1690,17 +1692,23 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     // the sample histograms (and the combined partials) come back with the flags; they stay
     // valid when the common prefix turns out to be empty
     if (want_hist) SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, parts, g_cur, st0));
+    // with speculative keys, their sample histograms and combined statistics too: when the
+    // common prefix comes out where they were taken (the usual case for URL-like lists), the
+    // sort's plan needs no second round trip (X1, URLs: one host sync fewer per call)
+    const bool spec_hist = want_hist && Ls;
+    uint32_t hist_n2 = 0;
+    if (spec_hist) SG_TRY(key_sample_hist(c, kLc, Lc.n_rec, shist + 8 * 256, &hist_n2, partsL, npartsL, st1));
     uint32_t *hh = c->hist_host;
     uint32_t fl[32] = {0u};
-    auto read_stats = [&](uint32_t words) -> int {
-        uint8_t *pin = (uint8_t *)c->pinned;
-        SG_HIP(hipMemcpyAsync(pin, dflag, shist ? 128 + 8 * 256 * 4 : 4 * words, hipMemcpyDeviceToHost, c->stream));
+    uint8_t *pin = (uint8_t *)c->pinned;
+    auto read_stats = [&](uint32_t words, uint32_t nhist) -> int {
+        SG_HIP(hipMemcpyAsync(pin, dflag, nhist ? 128 + nhist * 8 * 256 * 4 : 4 * words, hipMemcpyDeviceToHost, c->stream));
         SG_HIP(hipStreamSynchronize(c->stream));
         memcpy(fl, pin, 4 * words);
-        if (shist) memcpy(hh, pin + 128, 8 * 256 * 4);
+        if (nhist) memcpy(hh, pin + 128, 8 * 256 * 4);
         return SG_OK;
     };
-    SG_TRY(read_stats(chk ? 24u : (want_hist ? 12u : 2u)));
+    SG_TRY(read_stats(chk ? 24u : (spec_hist ? 20u : (want_hist ? 12u : 2u)), spec_hist ? 2u : (shist ? 1u : 0u)));
     if (chk) {  // before any kernel indexes the bytes through the handed-over spans
         uint64_t sum = 0;
         memcpy(&sum, fl + 20, 8);
@@ -1713,8 +1721,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     prior_sorted = fl[0] == 0;
     const uint32_t base = (rsp && (Lc.n_rec || (have_prior && Lp.n_rec))) ? fl[1] : 0u;
     if (base) {
-        if (want_hist) SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));
         const bool spec = Ls && base == Ls;
+        if (want_hist && !spec) SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));
         if (spec) {  // the speculative keys are every record's keys at the common prefix
             Lc.keys = kLc;
             if (kLp) Lp.keys = kLp;
@@ -1724,10 +1732,13 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
                 SG_LAUNCH(c, "rekey", k_rekey, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0, d_prior,
                           Lp.spans, Lp.n_rec, base, Lp.keys, (KeyStatD *)nullptr);
         }
-        if (want_hist) {  // keys changed: their statistics again
-            SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, spec ? partsL : parts, spec ? npartsL : g_rekey,
-                                   st1));
-            SG_TRY(read_stats(20u));
+        if (want_hist && spec) {  // keys changed: their statistics, already read back
+            memcpy(hh, pin + 128 + 8 * 256 * 4, 8 * 256 * 4);
+            hist_n = hist_n2;
+            memcpy(fl + 4, fl + 12, sizeof(KeyStatD));
+        } else if (want_hist) {
+            SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, parts, g_rekey, st1));
+            SG_TRY(read_stats(20u, 1u));
             memcpy(fl + 4, fl + 12, sizeof(KeyStatD));
         }
     }
