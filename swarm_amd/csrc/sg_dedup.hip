@@ -504,12 +504,8 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
     seg_wave_sync();  // the previous group's reads of s_w are done
     gw[gl] = make_uint4((uint32_t)m1, (uint32_t)(m1 >> 32), (uint32_t)m2, (uint32_t)(m2 >> 32));
     seg_wave_sync();
-    uint4 nv = gw[0];
-    for (uint32_t j = 0; j < kmax; ++j) {
-        // the next member's keys read one step ahead (gw[j + 1] stays inside this wave's
-        // SEG_WS entries; j >= kk: a stale entry, never used)
-        const uint4 ov = nv;
-        nv = gw[j + 1];
+    // one member's comparison (j: its index in the group, ov: its keys from LDS)
+    auto step = [&](uint32_t j, const uint4 ov) {
         const uint64_t o1 = (uint64_t)ov.x | ((uint64_t)ov.y << 32), o2 = (uint64_t)ov.z | ((uint64_t)ov.w << 32);
         // long records (WIDE) tie past the chunk keys often: their spans still travel by shuffle
         uint2 yw = make_uint2(0u, 0u);
@@ -530,6 +526,14 @@ __device__ __forceinline__ void seg_rank_group(const uint8_t *__restrict__ S, ui
         const bool before = j < gl;
         rank += (valid && (gt || (eq && before))) ? 1u : 0u;
         d = d || (valid && eq && before);
+    };
+    uint4 nv = gw[0];
+    for (uint32_t j = 0; j < kmax; ++j) {
+        // the next member's keys read one step ahead (gw[j + 1] stays inside this wave's
+        // SEG_WS entries; j >= kk: a stale entry, never used)
+        const uint4 ov = nv;
+        nv = gw[j + 1];
+        step(j, ov);
     }
     if (act) {
         SS[a + rank] = x;
