@@ -584,8 +584,8 @@ __global__ __launch_bounds__(256) void k_seg_wave(const uint8_t *__restrict__ S,
     uint4 *w = s_w[threadIdx.x >> 6];
     if (k[0] <= 32u && k[1] <= 32u) {
         const uint32_t t = lane >> 5;
-        seg_rank_group<32, WIDE>(S, SS, dup, t ? a[1] : a[0], t ? k[1] : k[0], lane & 31u, lane & 32u, (t ? k[1] : k[0]) > 0,
-                                 base, w);
+        const uint32_t kt = t ? k[1] : k[0];
+        seg_rank_group<32, WIDE>(S, SS, dup, t ? a[1] : a[0], kt, lane & 31u, lane & 32u, kt > 0, base, w);
     } else {
         seg_rank_group<64, WIDE>(S, SS, dup, a[0], k[0], lane, 0u, true, base, w);
         if (k[1]) seg_rank_group<64, WIDE>(S, SS, dup, a[1], k[1], lane, 0u, true, base, w);
@@ -1619,14 +1619,21 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
     if (have_prior) {
         if (!cur_pre) SG_TRY(run_lines2(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp, d_cur, n_cur, CUR_VIEW.lines, &Lc));
         else SG_TRY(run_lines(c, d_prior, n_prior, PRIOR_VIEW.lines, &Lp));
-        const uint32_t R = Lp.n_rec;
-        // keys from byte 0 decide sortedness exactly like keys from the common prefix would
-        // (a separate launch: fused into the prior's common-prefix scan, whose grid is capped
-        // for its atomics, the byte compares of equal keys ran 40 µs longer on C2)
-        if (R > 1 && R < (1u << 30))
-            SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_prior, Lp.spans, Lp.keys,
-                        R, dflag, make_bk(0u, 7u));
     }
+    // The prior's sortedness (dflag[0]): keys from byte 0 decide it exactly like keys from the
+    // common prefix would (a separate launch: fused into the prior's common-prefix scan, whose
+    // grid is capped for its atomics, the byte compares of equal keys ran 40 µs longer on C2).
+    // With speculative keys (below) the check runs on the prior's keys at the last common
+    // prefix instead, after the prior's prefix scan wrote them: URL-like priors share their
+    // first bytes, so keys from byte 0 all tie and every pair would be compared bytewise.
+    // Those keys decide it only if the prefix comes out the same (checked after the read-back).
+    auto check_prior = [&](const uint64_t *keys, uint32_t bk) -> int {
+        const uint32_t R = Lp.n_rec;
+        if (R > 1 && R < (1u << 30))
+            SG_LAUNCH_B(c, "check_sorted", 8.0 * R, k_check_sorted, grid_for(R - 1, 256), 256, 0, d_prior, Lp.spans, keys,
+                        R, dflag, bk);
+        return SG_OK;
+    };
     if (cur_pre) Lc = *cur_pre;
     else if (!have_prior) SG_TRY(run_lines(c, d_cur, n_cur, CUR_VIEW.lines, &Lc));
     // common prefix of every record (reference: the first record of cur, else of prior)
@@ -1667,6 +1674,8 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         }
         if (have_prior && Lp.n_rec) SG_TRY(slot(c, S_KEYSL2, (size_t)Lp.n_rec + 1, &kLp));
     }
+    const bool spec_chk = have_prior && kLp && rsp;  // the prior's check on its keys at Ls
+    if (have_prior && !spec_chk) SG_TRY(check_prior(Lp.keys, make_bk(0u, 7u)));
     // a handed-over parse (Lc.chk) is checked by the cur scan, and nothing reads bytes through
     // an unchecked reference span (rnb) before the check's result comes back with the flags
     const bool chk = Lc.chk && Lc.n_rec;
@@ -1693,6 +1702,7 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
         SG_LAUNCH_B(c, "lcp", 8.0 * Lp.n_rec, k_lcp<false>, std::min<uint32_t>(grid_for(Lp.n_rec, 256), 2048u), 256, 0,
                     d_prior, Lp.spans, Lp.keys, Lp.n_rec, rbuf, rsp, rkeys, dflag + 1, (KeyStatD *)nullptr, kLp, Ls,
                     (KeyStatD *)nullptr, rnb, (SpanChkPart *)nullptr, 0u, (uint32_t *)nullptr);
+    if (spec_chk) SG_TRY(check_prior(kLp, make_bk(Ls, 7u)));
     // the sample histograms (and the combined partials) come back with the flags; they stay
     // valid when the common prefix turns out to be empty
     if (want_hist) SG_TRY(key_sample_hist(c, Lc.keys, Lc.n_rec, shist, &hist_n, parts, g_cur, st0));
@@ -1722,8 +1732,13 @@ static int dev_dedup_diff_radix(sg_ctx *c, const uint8_t *d_cur, uint64_t n_cur,
             return SG_E_CORRUPT;
         }
     }
-    prior_sorted = fl[0] == 0;
     const uint32_t base = (rsp && (Lc.n_rec || (have_prior && Lp.n_rec))) ? fl[1] : 0u;
+    if (spec_chk && base != Ls) {  // the prefix moved: the check again on keys from byte 0
+        SG_HIP(hipMemsetAsync(dflag, 0, 4, c->stream));
+        SG_TRY(check_prior(Lp.keys, make_bk(0u, 7u)));
+        SG_TRY(ctx_readback(c, fl, dflag, 4));
+    }
+    prior_sorted = fl[0] == 0;
     if (base) {
         const bool spec = Ls && base == Ls;
         if (want_hist && !spec) SG_HIP(hipMemsetAsync(shist, 0, 8 * 256 * 4, c->stream));

@@ -334,6 +334,46 @@ def test_common_prefix_edges(sg, case):
     assert sg.dedup(cur) == S.dedup(cur)
 
 
+@pytest.mark.parametrize("prior_ok", [True, False], ids=["sorted_prior", "swapped_prior"])
+@pytest.mark.parametrize("second", ["same_prefix", "longer_prefix", "shorter_prefix", "no_prefix"])
+def test_prior_check_on_speculative_keys(prior_ok, second):
+    """The prior's sortedness is checked on its keys at the last call's common prefix (URL
+    lists: keys from byte 0 all tie); when the prefix comes out elsewhere the check runs again
+    on keys from byte 0. One swapped pair past the prefix is caught either way, and a sorted
+    prior is trusted either way (both give the oracle's output)."""
+    import numpy as np
+    import torch
+    rng = random.Random(7)
+    c = _kw_ctx()
+
+    def run(recs, prior_recs, swap):
+        pr = sorted(set(prior_recs))
+        if swap:
+            i = len(pr) // 2
+            pr[i], pr[i + 1] = pr[i + 1], pr[i]
+        cur, prior = b"\n".join(recs) + b"\n", b"".join(r + b"\n" for r in pr)
+        dc = torch.from_numpy(np.frombuffer(cur, dtype=np.uint8).copy()).cuda()
+        dp = torch.from_numpy(np.frombuffer(prior, dtype=np.uint8).copy()).cuda()
+        r = c.dedup_diff(dc.data_ptr(), len(cur), dp.data_ptr(), len(prior))
+        eu, ef = S.dedup_diff(cur, prior)
+        assert c.to_bytes(r.uniq, r.uniq_bytes) == eu and c.to_bytes(r.fresh, r.fresh_bytes) == ef
+
+    try:
+        first = _url_recs(rng, 6000)  # common prefix 'https://www.h' (13 bytes): kept by the context
+        run(first, first[::3], False)
+        if second == "same_prefix":
+            recs = _url_recs(rng, 6000)
+        elif second == "longer_prefix":
+            recs = [b"https://www.h7" + r[14:] for r in _url_recs(rng, 6000)]
+        elif second == "shorter_prefix":
+            recs = [r if i % 2 else b"https://a" + r[13:] for i, r in enumerate(_url_recs(rng, 6000))]
+        else:
+            recs = [bytes(rng.choice(b"abcdefgh/.:") for _ in range(rng.randint(1, 30))) for _ in range(6000)]
+        run(recs, recs[::2] + [recs[0] + b"-old"], not prior_ok)
+    finally:
+        c.close()
+
+
 def _kw_ctx():
     import torch
     import swarm_amd
