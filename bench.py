@@ -1317,7 +1317,7 @@ def main():
         line["c1"] = sub_leg("c1", lambda: bench_c1(args, ctx))
         line["c3"] = sub_leg("c3", lambda: bench_c3(args, ctx=ctx, emit=False), SUB_KEYS + ("error",))
         # C5 on a context of its own (its slots sized by its own parts, not grown from the
-        # legs before it: in the shared context the leg ran 3-5 ms per step slower than alone)
+        # legs before it)
         line["c5"] = sub_leg("c5", lambda: bench_c5(args, 1, 0, dev, None, emit=False), SUB_KEYS + ("error",))
         line["c4"] = sub_leg("c4", lambda: bench_c4(args, ctx=ctx, emit=False), SUB_KEYS + ("records", "error"))
         line["fields"] = sub_leg("fields", lambda: bench_fields(args, ctx=ctx, emit=False),
