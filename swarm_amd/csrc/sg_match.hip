@@ -1603,27 +1603,37 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 constexpr uint32_t VF_D = 12288;   // u16 transition entries staged per block
 constexpr uint32_t VF_ACC = 4096;  // accept flags staged per block
 
+// A block whose candidates span two automata (its first and last candidate's: 18 % of C4's
+// blocks, at the boundary between two patterns' runs) stages both when they fit together, so
+// its threads do not walk an automaton from L2 one dependent transition after another.
 __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
     __shared__ uint16_t s_D[VF_D];
-    __shared__ uint8_t s_cls[256];
+    __shared__ uint8_t s_cls[512];
     __shared__ uint8_t s_acc[VF_ACC];
     const uint32_t i0 = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
     const uint32_t i = i0 + threadIdx.x;
     const uint32_t il = min(i0 + blockDim.x, a.n_cand) - 1u;
     const uint32_t k0 = a.single_of_pid[(uint32_t)a.cand[i0]];
     const uint32_t kl = a.single_of_pid[(uint32_t)a.cand[il]];
-    uint32_t nst = 0, nd = 0;
-    if (k0 == kl) {
-        nst = (k0 + 1u < a.n_singles ? a.s_acc_off[k0 + 1u] : a.n_acc) - a.s_acc_off[k0];
-        nd = nst * a.s_C[k0];
-    }
-    const bool staged = k0 == kl && nd <= VF_D && nst <= VF_ACC;  // block-uniform
+    auto n_states = [&](uint32_t k) { return (k + 1u < a.n_singles ? a.s_acc_off[k + 1u] : a.n_acc) - a.s_acc_off[k]; };
+    const uint32_t nst = n_states(k0), nd = nst * a.s_C[k0];
+    const uint32_t nst2 = k0 != kl ? n_states(kl) : 0u, nd2 = k0 != kl ? nst2 * a.s_C[kl] : 0u;
+    // block-uniform: the first automaton, and the last one too when both fit
+    const bool staged = nd <= VF_D && nst <= VF_ACC;
+    const bool staged2 = staged && k0 != kl && nd + nd2 <= VF_D && nst + nst2 <= VF_ACC;
     if (staged) {
         const uint16_t *D = a.s_delta + a.s_off[k0];
         for (uint32_t q = threadIdx.x; q < nd; q += blockDim.x) s_D[q] = D[q];
         const uint8_t *acc = a.s_acc + a.s_acc_off[k0];
         for (uint32_t q = threadIdx.x; q < nst; q += blockDim.x) s_acc[q] = acc[q];
         s_cls[threadIdx.x] = a.s_cls[256u * k0 + threadIdx.x];
+        if (staged2) {
+            const uint16_t *D2 = a.s_delta + a.s_off[kl];
+            for (uint32_t q = threadIdx.x; q < nd2; q += blockDim.x) s_D[nd + q] = D2[q];
+            const uint8_t *acc2 = a.s_acc + a.s_acc_off[kl];
+            for (uint32_t q = threadIdx.x; q < nst2; q += blockDim.x) s_acc[nst + q] = acc2[q];
+            s_cls[256u + threadIdx.x] = a.s_cls[256u * kl + threadIdx.x];
+        }
         __syncthreads();
     }
     bool hit = false;
@@ -1635,6 +1645,8 @@ __global__ __launch_bounds__(256) void k_verify(VerifyArgs a) {
         const uint2 sp = a.spans[r];
         if (staged && k == k0) {  // pids of one automaton need not be contiguous
             hit = verify_walk(a.buf, s_D, s_cls, s_acc, a.s_C[k], a.s_eol[k], a.s_mid[k], sp.x, sp.y);
+        } else if (staged2 && k == kl) {
+            hit = verify_walk(a.buf, s_D + nd, s_cls + 256, s_acc + nst, a.s_C[k], a.s_eol[k], a.s_mid[k], sp.x, sp.y);
         } else {
             hit = verify_walk(a.buf, a.s_delta + a.s_off[k], a.s_cls + 256u * k, a.s_acc + a.s_acc_off[k], a.s_C[k],
                               a.s_eol[k], a.s_mid[k], sp.x, sp.y);
