@@ -1600,7 +1600,14 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
 // Candidates are sorted by pattern, so almost every block verifies one automaton: when the
 // first and last candidate share it and it fits, the block copies that automaton (rows, byte classes, accept flags) into LDS once and
 // every lane walks it there — the per-byte transitions were dependent L1/L2 loads.
-constexpr uint32_t VF_D = 12288;   // u16 transition entries staged per block
+// u16 transition entries staged per block. Round 6: 12,288 -> 6,144 (a block's LDS 28.7 ->
+// 16.4 KB, 5 -> 8 blocks per CU, the wave limit): the walks are latency-bound and the waves
+// hide more than the automata pushed to L2 walks cost (C4 re_verify 1.35 -> 1.22 ms, fields
+// 3.63 -> 2.71 ms; 4,096 / 3,072 / 2,048 flat, 16,384 slower: profiles/r06/ab/ab10*, ab11*)
+#ifndef SG_VF_D
+#define SG_VF_D 6144
+#endif
+constexpr uint32_t VF_D = SG_VF_D;
 constexpr uint32_t VF_ACC = 4096;  // accept flags staged per block
 
 // A block whose candidates span two automata (its first and last candidate's: 18 % of C4's
