@@ -232,6 +232,23 @@ def test_regex_c4_banners_full_signature_set(sg):
     assert len(exp) > 50
 
 
+def test_regex_verify_blocks_over_two_automata(sg):
+    """Enough prefilter candidates (> 4096) that the verify sorts them by pattern and its
+    256-candidate blocks straddle the boundary between two patterns' runs: such a block
+    stages both automata (or the first) in LDS; every hit equals re.search."""
+    import random
+    from swarm_amd import corpus
+    pats = corpus.nmap_signatures(n_products=60)
+    rows = corpus.banner_pool(n_products=60, pool=1500, match_frac=0.6, seed=33)
+    rng = random.Random(33)
+    data = b"".join(rng.choice(rows) + b"\n" for _ in range(9000))
+    m = sg.Matcher(pats, "regex")
+    got = m.match(data)
+    exp = S.regex_hits(data, pats)
+    assert got == exp
+    assert len(exp) > 4096
+
+
 @pytest.mark.parametrize("multi", ["1", "0"])
 def test_regex_factorless_groups_packed_and_single(sg, multi, monkeypatch):
     """Factor-less patterns whose DFAs split into several groups: walked together by the
